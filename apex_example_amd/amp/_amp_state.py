@@ -1,0 +1,56 @@
+"""Global amp state (apex@f3a960f8 apex/amp/_amp_state.py).
+
+Holds the active opt-level Properties, the loss scalers and the O1 handle.
+"""
+import os
+
+import torch
+
+
+class AmpState(object):
+    def __init__(self):
+        self.hard_override = False
+        self.allow_incoming_model_not_fp32 = False
+        self.verbosity = 1
+
+
+_amp_state = AmpState()
+
+
+def warn_or_err(msg):
+    if _amp_state.hard_override:
+        print("Warning:  " + msg)
+    else:
+        raise RuntimeError(msg)
+
+
+def _rank0():
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank() == 0
+    except Exception:  # pragma: no cover
+        pass
+    return int(os.environ.get("RANK", "0")) == 0
+
+
+def maybe_print(msg, rank0=False):
+    if _amp_state.verbosity > 0:
+        if rank0:
+            if _rank0():
+                print(msg)
+        else:
+            print(msg)
+
+
+def master_params(optimizer):
+    """Generator over the parameters the optimizer updates (fp32 masters under
+    O2), as ``apex.amp.master_params``."""
+    for group in optimizer.param_groups:
+        for p in group["params"]:
+            yield p
+
+
+def is_half_dtype(dt):
+    return dt in (torch.float16, torch.bfloat16)

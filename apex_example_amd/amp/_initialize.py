@@ -1,0 +1,256 @@
+"""amp ``_initialize`` (apex@f3a960f8 apex/amp/_initialize.py).
+
+Casts models per the opt level (BatchNorm kept fp32 under O2), patches
+``forward`` to cast inputs / outputs, processes optimizers (master weights) and
+creates one LossScaler per loss.
+"""
+from __future__ import annotations
+
+import functools
+import warnings
+
+import torch
+
+from ..fp16_utils import convert_network
+from ._amp_state import _amp_state, maybe_print, warn_or_err
+from ._process_optimizer import _process_optimizer
+from .scaler import LossScaler
+
+
+def to_type(dtype, t):
+    if isinstance(t, torch.Tensor):
+        if not t.is_cuda and torch.cuda.is_available() and _amp_state.opt_properties.cast_model_type not in (None, torch.float32):
+            # Apex warns about cpu inputs with GPU models
+            warnings.warn("An input tensor was not cuda.")
+        if t.is_floating_point():
+            return t.to(dtype)
+        return t
+    else:
+        return t.to(dtype)
+
+
+def applier(value, fn):
+    if isinstance(value, torch.Tensor):
+        return fn(value)
+    elif isinstance(value, str):
+        return value
+    elif hasattr(value, "_fields") and isinstance(value, tuple):  # namedtuple
+        return type(value)(*(applier(v, fn) for v in value))
+    elif isinstance(value, dict):
+        return {k: applier(v, fn) for k, v in value.items()}
+    elif isinstance(value, (list, tuple)):
+        return type(value)(applier(v, fn) for v in value)
+    elif hasattr(value, "to") and callable(getattr(value, "to")):
+        try:
+            return fn(value)
+        except Exception:
+            return value
+    return value
+
+
+def check_models(models):
+    from ..parallel.distributed import DistributedDataParallel as AmdDDP
+
+    for model in models:
+        parallel_type = None
+        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+            parallel_type = "torch.nn.parallel.DistributedDataParallel"
+        if isinstance(model, AmdDDP):
+            parallel_type = "apex_example_amd.parallel.DistributedDataParallel"
+        if isinstance(model, torch.nn.parallel.DataParallel):
+            parallel_type = "torch.nn.parallel.DataParallel"
+        if parallel_type is not None:
+            raise RuntimeError("Incoming model is an instance of {}. ".format(parallel_type) +
+                               "Parallel wrappers should only be applied to the model(s) AFTER \n"
+                               "the model(s) have been returned from amp.initialize.")
+
+
+def check_params_fp32(models):
+    for model in models:
+        for name, param in model.named_parameters():
+            if param.is_floating_point():
+                if param.dtype != torch.float32:
+                    warn_or_err("Found param {} with type {}, expected torch.float32.\n"
+                                "When using amp.initialize, you do not need to call .half() on "
+                                "your model\nbefore passing it, no matter what optimization "
+                                "level you choose.".format(name, param.dtype))
+        for name, buf in model.named_buffers():
+            if buf.is_floating_point():
+                if buf.dtype != torch.float32:
+                    warn_or_err("Found buffer {} with type {}, expected torch.float32.\n"
+                                "When using amp.initialize, you do not need to call .half() on "
+                                "your model\nbefore passing it, no matter what optimization "
+                                "level you choose.".format(name, buf.dtype))
+
+
+def check_optimizers(optimizers):
+    from ..fp16_utils.fp16_optimizer import FP16_Optimizer
+
+    for optim in optimizers:
+        bad_optim_type = None
+        if isinstance(optim, FP16_Optimizer):
+            bad_optim_type = "apex_example_amd.fp16_utils.FP16_Optimizer"
+        if bad_optim_type is not None:
+            raise RuntimeError("An incoming optimizer is an instance of {}. ".format(bad_optim_type) +
+                               "The optimizer(s) passed to amp.initialize() must be bare \n"
+                               "instances of either ordinary Pytorch optimizers, or Apex fused \n"
+                               "optimizers.\n")
+
+
+class O2StateDictHook(object):
+    """Return fp32 copies of half params in state_dict (apex O2 behaviour is to keep
+    the model's own dtype; this hook is installed only for cast_model_outputs)."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self, module, state_dict, prefix, local_metadata):
+        for key in state_dict:
+            param = state_dict[key]
+            if "Half" in param.type():
+                param = param.to(torch.float32)
+                state_dict[key] = param
+
+
+def _patch_forward(model, input_caster, output_caster):
+    old_fwd = model.forward
+
+    @functools.wraps(old_fwd)
+    def new_fwd(*args, **kwargs):
+        output = old_fwd(*applier(args, input_caster), **applier(kwargs, input_caster))
+        return applier(output, output_caster)
+
+    model.forward = new_fwd
+    model._amp_old_forward = old_fwd
+
+
+def _all_fused(optimizers):
+    from ..optimizers import _FUSED_TYPES
+
+    return len(optimizers) > 0 and all(isinstance(o, _FUSED_TYPES) for o in optimizers)
+
+
+def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs=None,
+                sync_free=None):
+    from ..parallel.LARC import LARC
+
+    optimizers_was_list = False
+    if isinstance(optimizers, torch.optim.Optimizer) or isinstance(optimizers, LARC):
+        optimizers = [optimizers]
+    elif optimizers is None:
+        optimizers = []
+    elif isinstance(optimizers, list):
+        optimizers_was_list = True
+        check_optimizers(optimizers)
+    else:
+        check_optimizers([optimizers])
+        raise TypeError("optimizers must be either a single optimizer or a list of optimizers.")
+
+    if isinstance(models, torch.nn.Module):
+        models_was_list = False
+        models = [models]
+    elif isinstance(models, list):
+        models_was_list = True
+    else:
+        raise TypeError("models must be either a single model or a list of models.")
+
+    check_models(models)
+
+    if not _amp_state.allow_incoming_model_not_fp32:
+        check_params_fp32(models)
+
+    # In the future, when FP16_Optimizer can be deprecated and master weights can
+    # become an attribute, remember to stash master weights before casting the model.
+
+    if properties.cast_model_type:
+        if properties.keep_batchnorm_fp32:
+            for model in models:
+                convert_network(model, properties.cast_model_type)
+        else:
+            for model in models:
+                model.to(properties.cast_model_type)
+
+        input_caster = functools.partial(to_type, properties.cast_model_type)
+        if cast_model_outputs is not None:
+            output_caster = functools.partial(to_type, cast_model_outputs)
+        else:
+            output_caster = functools.partial(to_type, torch.float32)
+
+        for model in models:
+            _patch_forward(model, input_caster, output_caster)
+
+        for optimizer in optimizers:
+            optimizer.load_state_dict(optimizer.state_dict())
+
+    elif cast_model_outputs is not None:
+        output_caster = functools.partial(to_type, cast_model_outputs)
+        for model in models:
+            _patch_forward(model, lambda x: x, output_caster)
+
+    # device of the loss scaler state: the models' device
+    device = None
+    for model in models:
+        for p in model.parameters():
+            device = p.device
+            break
+        if device is not None:
+            break
+    if device is None:
+        device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+    if sync_free is None:
+        sync_free = (device.type == "cuda" and _all_fused(optimizers)
+                     and properties.loss_scale == "dynamic")
+    for i, optimizer in enumerate(optimizers):
+        optimizers[i] = _process_optimizer(optimizer, properties)
+
+    _amp_state.loss_scalers = []
+    for _ in range(num_losses):
+        _amp_state.loss_scalers.append(LossScaler(properties.loss_scale,
+                                                  min_loss_scale=_amp_state.min_loss_scale,
+                                                  max_loss_scale=_amp_state.max_loss_scale,
+                                                  device=device, sync_free=bool(sync_free)))
+    for optimizer in optimizers:
+        optimizer._amp_stash.sync_free = bool(sync_free)
+
+    if properties.patch_torch_functions:
+        from .amp import init as amp_init
+
+        # handle is unused for the new API, but the O1 casting policy lives in it
+        handle = amp_init(loss_scale=properties.loss_scale, verbose=(_amp_state.verbosity == 2),
+                          dtype=properties.half_dtype,
+                          device_type="cuda" if device.type == "cuda" else "cpu")
+        for optimizer in optimizers:
+            # Disable Amp casting for the optimizer step, because it should only be
+            # applied to FP32 master params anyway.
+            def patch_step(old_step):
+                def new_step(self, *args, **kwargs):
+                    with handle._disable_casts():
+                        output = old_step(*args, **kwargs)
+                    return output
+                return new_step
+
+            import types
+
+            optimizer.step = types.MethodType(patch_step(optimizer.step), optimizer)
+
+    maybe_print("Amp: initialized {} model(s), {} optimizer(s), {} loss scaler(s) "
+                "[sync_free={}]".format(len(models), len(optimizers), num_losses,
+                                       bool(sync_free)), True)
+
+    if optimizers_was_list:
+        if models_was_list:
+            return models, optimizers
+        else:
+            return models[0], optimizers
+    else:
+        if models_was_list:
+            if len(optimizers) == 0:
+                return models
+            else:
+                return models, optimizers[0]
+        else:
+            if len(optimizers) == 0:
+                return models[0]
+            else:
+                return models[0], optimizers[0]

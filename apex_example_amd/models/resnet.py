@@ -1,0 +1,160 @@
+"""ResNet family (He et al. 2015, v1.5: stride on the 3x3 conv), defined in-repo
+(torchvision is not available).  ResNet-50 = 25,557,032 parameters in 161 tensors.
+
+``fused_bn=True`` replaces each BatchNorm(+ReLU)(+residual add) with the fused
+gfx950 op ``BatchNorm2dReLU`` (one stats pass + one elementwise pass forward,
+one reduction + one elementwise pass backward, ReLU and the residual add folded
+in).  With ``channels_last`` activations the NHWC kernels run, which is the
+layout MIOpen's bf16 convolutions prefer on MI355X.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops.batch_norm import BatchNorm2dReLU
+
+
+def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
+    return nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation,
+                     groups=groups, bias=False, dilation=dilation)
+
+
+def conv1x1(in_planes, out_planes, stride=1):
+    return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
+
+
+class _BNAct(nn.Module):
+    """BN (+ residual) (+ ReLU): plain torch modules or the fused op."""
+
+    def __init__(self, planes, relu, fused, zero_init=False):
+        super().__init__()
+        self.fused = fused
+        self.relu_after = relu
+        if fused:
+            self.bn = BatchNorm2dReLU(planes, fuse_relu=relu)
+        else:
+            self.bn = nn.BatchNorm2d(planes)
+        if zero_init:
+            nn.init.zeros_(self.bn.weight)
+
+    def forward(self, x, z=None):
+        if self.fused:
+            return self.bn(x, z)
+        y = self.bn(x)
+        if z is not None:
+            y = y + z
+        return torch.relu(y) if self.relu_after else y
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, fused_bn=False,
+                 zero_init_residual=False):
+        super().__init__()
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bn1 = _BNAct(planes, True, fused_bn)
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = _BNAct(planes, True, fused_bn, zero_init_residual)
+        self.downsample = downsample
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), identity)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, fused_bn=False,
+                 zero_init_residual=False):
+        super().__init__()
+        width = planes
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = _BNAct(width, True, fused_bn)
+        self.conv2 = conv3x3(width, width, stride)
+        self.bn2 = _BNAct(width, True, fused_bn)
+        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.bn3 = _BNAct(planes * self.expansion, True, fused_bn, zero_init_residual)
+        self.downsample = downsample
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), identity)
+
+
+class _Downsample(nn.Module):
+    def __init__(self, inplanes, outplanes, stride, fused_bn):
+        super().__init__()
+        self.conv = conv1x1(inplanes, outplanes, stride)
+        self.bn = _BNAct(outplanes, False, fused_bn)
+
+    def forward(self, x):
+        return self.bn(self.conv(x))
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, layers, num_classes=1000, fused_bn=False, zero_init_residual=False):
+        super().__init__()
+        self.fused_bn = fused_bn
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = _BNAct(self.inplanes, True, fused_bn)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0], 1, zero_init_residual)
+        self.layer2 = self._make_layer(block, 128, layers[1], 2, zero_init_residual)
+        self.layer3 = self._make_layer(block, 256, layers[2], 2, zero_init_residual)
+        self.layer4 = self._make_layer(block, 512, layers[3], 2, zero_init_residual)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def _make_layer(self, block, planes, blocks, stride, zero_init_residual):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = _Downsample(self.inplanes, planes * block.expansion, stride,
+                                     self.fused_bn)
+        layers = [block(self.inplanes, planes, stride, downsample, self.fused_bn,
+                        zero_init_residual)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes, fused_bn=self.fused_bn,
+                                zero_init_residual=zero_init_residual))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.bn1(self.conv1(x))
+        x = self.maxpool(x)
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        x = self.layer4(x)
+        x = self.avgpool(x)
+        x = torch.flatten(x, 1)
+        return self.fc(x)
+
+
+def resnet18(**kw):
+    return ResNet(BasicBlock, [2, 2, 2, 2], **kw)
+
+
+def resnet34(**kw):
+    return ResNet(BasicBlock, [3, 4, 6, 3], **kw)
+
+
+def resnet50(**kw):
+    return ResNet(Bottleneck, [3, 4, 6, 3], **kw)
+
+
+def resnet101(**kw):
+    return ResNet(Bottleneck, [3, 4, 23, 3], **kw)
+
+
+def resnet152(**kw):
+    return ResNet(Bottleneck, [3, 8, 36, 3], **kw)

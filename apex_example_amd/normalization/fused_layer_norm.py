@@ -1,0 +1,170 @@
+"""FusedLayerNorm / FusedRMSNorm (apex@f3a960f8 apex/normalization/fused_layer_norm.py,
+SURVEY.md A-13 / N-13) on the wave64 row kernels of csrc/hip/layer_norm.hip.
+
+Inputs may be fp32 / fp16 / bf16; gamma/beta may be fp32 with 16-bit inputs
+("mixed" - amp O2 keeps LayerNorm params... in the model dtype by default;
+either works).  CPU tensors run the C++ CPU path of the same extension.
+"""
+from __future__ import annotations
+
+import numbers
+
+import torch
+from torch.nn import init
+from torch.nn.parameter import Parameter
+
+from .. import _native
+
+
+def _n2(normalized_shape):
+    n = 1
+    for s in normalized_shape:
+        n *= s
+    return n
+
+
+class FusedLayerNormAffineFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, weight, bias, normalized_shape, eps):
+        C = _native.require().layer_norm
+        ctx.normalized_shape = normalized_shape
+        ctx.eps = eps
+        input_ = input.contiguous()
+        weight_ = weight.contiguous()
+        bias_ = bias.contiguous()
+        output, mean, invvar = C.forward(input_, _n2(normalized_shape), weight_, bias_, eps, False)
+        ctx.save_for_backward(input_, weight_, bias_, mean, invvar)
+        return output
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        C = _native.require().layer_norm
+        input_, weight_, bias_, mean, invvar = ctx.saved_tensors
+        grad_input, grad_weight, grad_bias = C.backward(
+            grad_output.contiguous(), input_, mean, invvar, _n2(ctx.normalized_shape), weight_,
+            ctx.needs_input_grad[1], ctx.needs_input_grad[2], False)
+        return grad_input, grad_weight, grad_bias, None, None
+
+
+class FusedLayerNormFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, normalized_shape, eps):
+        C = _native.require().layer_norm
+        ctx.normalized_shape = normalized_shape
+        ctx.eps = eps
+        input_ = input.contiguous()
+        output, mean, invvar = C.forward(input_, _n2(normalized_shape), None, None, eps, False)
+        ctx.save_for_backward(input_, mean, invvar)
+        return output
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        C = _native.require().layer_norm
+        input_, mean, invvar = ctx.saved_tensors
+        grad_input, _, _ = C.backward(grad_output.contiguous(), input_, mean, invvar,
+                                      _n2(ctx.normalized_shape), None, False, False, False)
+        return grad_input, None, None
+
+
+class FusedRMSNormAffineFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, weight, normalized_shape, eps):
+        C = _native.require().layer_norm
+        ctx.normalized_shape = normalized_shape
+        input_ = input.contiguous()
+        weight_ = weight.contiguous()
+        output, mean, invvar = C.forward(input_, _n2(normalized_shape), weight_, None, eps, True)
+        ctx.save_for_backward(input_, weight_, mean, invvar)
+        return output
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        C = _native.require().layer_norm
+        input_, weight_, mean, invvar = ctx.saved_tensors
+        grad_input, grad_weight, _ = C.backward(grad_output.contiguous(), input_, mean, invvar,
+                                                _n2(ctx.normalized_shape), weight_,
+                                                ctx.needs_input_grad[1], False, True)
+        return grad_input, grad_weight, None, None
+
+
+def fused_layer_norm_affine(input, weight, bias, normalized_shape, eps=1e-6):
+    return FusedLayerNormAffineFunction.apply(input, weight, bias, normalized_shape, eps)
+
+
+def fused_layer_norm(input, normalized_shape, eps=1e-6):
+    return FusedLayerNormFunction.apply(input, normalized_shape, eps)
+
+
+def fused_rms_norm_affine(input, weight, normalized_shape, eps=1e-6):
+    return FusedRMSNormAffineFunction.apply(input, weight, normalized_shape, eps)
+
+
+class FusedLayerNorm(torch.nn.Module):
+    r"""Applies Layer Normalization over a mini-batch of inputs (apex.normalization.FusedLayerNorm).
+
+    .. math::
+        y = \frac{x - \mathrm{E}[x]}{ \sqrt{\mathrm{Var}[x] + \epsilon}} * \gamma + \beta
+
+    Same constructor and semantics as ``torch.nn.LayerNorm``; CPU input without
+    the extension falls back to ``F.layer_norm`` (apex behaviour).
+    """
+
+    def __init__(self, normalized_shape, eps=1e-5, elementwise_affine=True):
+        super(FusedLayerNorm, self).__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (normalized_shape,)
+        self.normalized_shape = torch.Size(normalized_shape)
+        self.eps = eps
+        self.elementwise_affine = elementwise_affine
+        if self.elementwise_affine:
+            self.weight = Parameter(torch.Tensor(*normalized_shape))
+            self.bias = Parameter(torch.Tensor(*normalized_shape))
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        if self.elementwise_affine:
+            init.ones_(self.weight)
+            init.zeros_(self.bias)
+
+    def forward(self, input):
+        if not input.is_cuda and not _native.available():
+            return torch.nn.functional.layer_norm(input, self.normalized_shape, self.weight,
+                                                  self.bias, self.eps)
+        if self.elementwise_affine:
+            return FusedLayerNormAffineFunction.apply(input, self.weight, self.bias,
+                                                      self.normalized_shape, self.eps)
+        return FusedLayerNormFunction.apply(input, self.normalized_shape, self.eps)
+
+    def extra_repr(self):
+        return "{normalized_shape}, eps={eps}, elementwise_affine={elementwise_affine}".format(
+            **self.__dict__)
+
+
+class FusedRMSNorm(torch.nn.Module):
+    r"""RMS normalization: y = x / sqrt(mean(x^2) + eps) * gamma."""
+
+    def __init__(self, normalized_shape, eps=1e-5, elementwise_affine=True):
+        super().__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (normalized_shape,)
+        self.normalized_shape = torch.Size(normalized_shape)
+        self.eps = eps
+        self.elementwise_affine = elementwise_affine
+        if elementwise_affine:
+            self.weight = Parameter(torch.ones(*normalized_shape))
+        else:
+            self.register_parameter("weight", None)
+
+    def forward(self, input):
+        if self.elementwise_affine:
+            return FusedRMSNormAffineFunction.apply(input, self.weight, self.normalized_shape,
+                                                    self.eps)
+        w = torch.ones(self.normalized_shape, dtype=input.dtype, device=input.device)
+        return FusedRMSNormAffineFunction.apply(input, w, self.normalized_shape, self.eps)
+
+    def extra_repr(self):
+        return "{normalized_shape}, eps={eps}, elementwise_affine={elementwise_affine}".format(
+            **self.__dict__)

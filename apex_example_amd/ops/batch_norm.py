@@ -1,0 +1,153 @@
+"""Fused BatchNorm(+residual)(+ReLU) autograd op on the gfx950 kernels
+(csrc/hip/batch_norm.hip), shared by ``SyncBatchNorm`` and the local
+``BatchNorm2dReLU`` used by the MI355X ResNet.
+
+Forward (training): split-reduction per-channel stats -> [one packed all_gather
+of (mean, var, count) across the process group] -> combine + running-stat
+update -> y = relu(x*scale + shift + z) in one elementwise pass.
+Backward: one reduction pass (sum dy', sum dy'*(x-mean), dgamma, dbeta; the
+ReLU mask is recomputed from x, nothing extra is saved) -> [one packed
+all_reduce of the two sums] -> one elementwise pass producing dx (and dz for
+the residual branch).
+
+Works for any memory format: NCHW-contiguous runs the NCHW kernels,
+channels_last-contiguous 4-D tensors run the NHWC kernels; ``shape_channel_last``
+selects apex's channel_last=True convention (C is the LAST dimension of the
+shape).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+
+
+def _C():
+    return _native.require().bn
+
+
+def _to_logical(x, shape_channel_last):
+    if shape_channel_last:
+        C = x.size(-1)
+        return x.reshape(-1, C)
+    return x
+
+
+class BatchNormFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
+                fuse_relu, shape_channel_last):
+        C = _C()
+        orig_shape = x.shape
+        xl = _to_logical(x, shape_channel_last)
+        zl = _to_logical(z, shape_channel_last) if z is not None else None
+        mean, var = C.local_stats(xl)
+        count = xl.numel() // xl.size(1)
+        if process_group is False or not (dist.is_available() and dist.is_initialized()):
+            world = 1  # local statistics
+        else:
+            world = dist.get_world_size(process_group)
+        if world > 1:
+            pg = process_group if process_group is not None else dist.group.WORLD
+            cnt = torch.full((1,), float(count), dtype=torch.float32, device=x.device)
+            packed = torch.cat([mean, var, cnt])
+            gathered = torch.empty(world * packed.numel(), dtype=packed.dtype, device=x.device)
+            dist.all_gather_into_tensor(gathered, packed, group=pg)
+            g = gathered.view(world, -1)
+            Cn = mean.numel()
+            means, vars_, counts = g[:, :Cn], g[:, Cn:2 * Cn], g[:, 2 * Cn]
+            total = counts.sum()
+        else:
+            pg = None
+            means, vars_ = mean.view(1, -1), var.view(1, -1)
+            counts = torch.full((1,), float(count), dtype=torch.float32, device=x.device)
+            total = None
+        mean_g, invstd, _ = C.combine_stats(means, vars_, counts, float(eps), float(momentum),
+                                            running_mean, running_var)
+        y = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu))
+        ctx.save_for_backward(xl, zl, weight, bias, mean_g, invstd)
+        ctx.pg = pg
+        ctx.world = world
+        ctx.fuse_relu = bool(fuse_relu)
+        ctx.total = total
+        ctx.count = count
+        ctx.orig_shape = orig_shape
+        ctx.has_z = z is not None
+        ctx.shape_channel_last = shape_channel_last
+        return y.view(orig_shape) if shape_channel_last else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        xl, zl, weight, bias, mean, invstd = ctx.saved_tensors
+        dyl = _to_logical(dy, ctx.shape_channel_last)
+        need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
+                                                   ctx.fuse_relu, need_w)
+        if ctx.world > 1:
+            packed = torch.cat([sum_dy, sum_dy_xmu])
+            dist.all_reduce(packed, group=ctx.pg)
+            n = sum_dy.numel()
+            # normalise by the global count on the device (no host sync)
+            packed = packed / ctx.total
+            sum_dy, sum_dy_xmu = packed[:n], packed[n:]
+            total = 1.0
+        else:
+            total = float(ctx.count)
+        dx, dz = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu, total,
+                                  zl, ctx.fuse_relu, ctx.has_z)
+        if ctx.shape_channel_last:
+            dx = dx.view(ctx.orig_shape)
+            if dz is not None:
+                dz = dz.view(ctx.orig_shape)
+        return (dx, dz if ctx.has_z else None, gw if need_w else None, gb if need_w else None,
+                None, None, None, None, None, None, None)
+
+
+def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
+                   z=None, fuse_relu=False, process_group=False, shape_channel_last=False):
+    """Functional fused BN(+z)(+ReLU).  ``process_group=False`` -> local statistics."""
+    if training:
+        return BatchNormFunction.apply(x, z, weight, bias, running_mean, running_var, eps, momentum,
+                                       process_group, fuse_relu, shape_channel_last)
+    # inference: running statistics (autograd through plain torch ops)
+    if shape_channel_last:
+        xs = x.movedim(-1, 1)
+        zs = z.movedim(-1, 1) if z is not None else None
+    else:
+        xs, zs = x, z
+    y = torch.nn.functional.batch_norm(xs, running_mean, running_var, weight, bias, False, 0.0, eps)
+    if zs is not None:
+        y = y + zs
+    if fuse_relu:
+        y = torch.relu(y)
+    return y.movedim(1, -1) if shape_channel_last else y
+
+
+class BatchNorm2dReLU(torch.nn.BatchNorm2d):
+    """BatchNorm2d with optional fused residual add and ReLU on the gfx950 kernels
+    (local, per-GPU statistics).  ``forward(x, z=None)`` = relu(bn(x) + z)."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True,
+                 track_running_stats=True, fuse_relu=True, **kw):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
+        self.fuse_relu = fuse_relu
+
+    def forward(self, x, z=None):
+        if not x.is_cuda and not _native.available():
+            y = super().forward(x)
+            if z is not None:
+                y = y + z
+            return torch.relu(y) if self.fuse_relu else y
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked.add_(1)
+            if self.momentum is None:
+                momentum = 1.0 / float(self.num_batches_tracked)
+        use_batch = self.training or not self.track_running_stats
+        return batch_norm_act(x, self.weight, self.bias,
+                              self.running_mean if self.track_running_stats else None,
+                              self.running_var if self.track_running_stats else None,
+                              use_batch, momentum, self.eps, z=z, fuse_relu=self.fuse_relu,
+                              process_group=False)

@@ -1,0 +1,177 @@
+"""Shared machinery of the fused optimizers.
+
+Every fused optimizer of this package:
+
+* groups the tensors of a param group into launch sets of identical dtype
+  signature (grad, param[, 16-bit model copy]) and issues ONE multi-tensor
+  launch per set (usually one per group);
+* under amp master weights it reads the masters from the amp stash and writes
+  the 16-bit model copy inside the same kernel (``_amp_writes_model_copy``), so
+  amp's separate master->model copy pass disappears; with
+  ``materialize_master_grads=False`` it also reads the 16-bit model grads
+  directly and folds the 1/loss_scale multiply into the kernel;
+* in amp sync-free mode passes the loss scaler's device overflow flag as the
+  kernels' noop flag, and keeps step counters / first-run flags on the device,
+  so a skipped step never needs a host round trip.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+
+from .. import _native
+
+
+class FusedOptimizerBase(torch.optim.Optimizer):
+    _amp_fused = True
+    _amp_writes_model_copy = True
+
+    def __init__(self, params, defaults, set_grad_none=True, materialize_master_grads=True):
+        super().__init__(params, defaults)
+        self.set_grad_none = set_grad_none
+        self.materialize_master_grads = materialize_master_grads
+        self._dev_steps = {}
+        self._dev_flags = {}
+        self._dummy_bufs = {}
+        self.most_recent_scale = 1.0
+        self.scale_set_by_backward = False
+
+    # ------------------------------------------------------------------ helpers
+    def _dummy(self, device):
+        key = str(device)
+        b = self._dummy_bufs.get(key)
+        if b is None:
+            dev = key.split(":scratch")[0]
+            b = self._dummy_bufs[key] = torch.zeros(1, dtype=torch.int32, device=dev)
+        return b
+
+    def _amp(self):
+        stash = getattr(self, "_amp_stash", None)
+        return stash
+
+    def _noop(self, device):
+        """The flag the kernels check: the amp scaler's overflow flag (sync-free
+        dynamic scaling) or a zero buffer."""
+        stash = self._amp()
+        if stash is not None and stash.sync_free and stash.last_scaler is not None:
+            sc = stash.last_scaler
+            if sc.dynamic and sc._overflow_buf.device == torch.device(device):
+                return sc._overflow_buf
+        return self._dummy(device)
+
+    def _sync_free(self):
+        stash = self._amp()
+        return stash is not None and stash.sync_free and stash.last_scaler is not None
+
+    def _fold_scale(self):
+        """Scale argument for launch sets that read raw (loss-scaled) 16-bit grads."""
+        stash = self._amp()
+        if stash is None or stash.last_scaler is None:
+            return 1.0, False
+        sc = stash.last_scaler
+        if sc.sync_free:
+            return sc._scale_dev, True
+        return 1.0 / sc.loss_scale(), False
+
+    def _launch_sets(self, gid, group):
+        """OrderedDict key -> dict(grads, params, copies, scaled)."""
+        stash = self._amp()
+        sets = OrderedDict()
+
+        def add(key, g, p, c, scaled):
+            s = sets.get(key)
+            if s is None:
+                s = sets[key] = {"grads": [], "params": [], "copies": [] if c is not None else None,
+                                 "scaled": scaled}
+            s["grads"].append(g)
+            s["params"].append(p)
+            if c is not None:
+                s["copies"].append(c)
+
+        if stash is not None and getattr(stash, "master_weights", False) and stash.lazy_init_called:
+            fold = not self.materialize_master_grads
+            for model_p, master in zip(stash.fp16_groups[gid], stash.fp32_from_fp16_groups[gid]):
+                g = model_p.grad if fold else master.grad
+                if g is None:
+                    continue
+                if g.is_sparse:
+                    raise RuntimeError("fused optimizers do not support sparse gradients")
+                add((g.dtype, master.dtype, model_p.dtype, fold), g, master, model_p, fold)
+            for p in stash.fp32_from_fp32_groups[gid]:
+                if p.grad is None:
+                    continue
+                add((p.grad.dtype, p.dtype, None, False), p.grad, p, None, False)
+        else:
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("fused optimizers do not support sparse gradients")
+                add((p.grad.dtype, p.dtype, None, False), p.grad, p, None, False)
+        return sets
+
+    def _scale_args(self, scaled):
+        if not scaled:
+            return 1.0, False
+        return self._fold_scale()
+
+    def _dev_step(self, gid, device):
+        """int32 device counter of completed steps for group gid (sync-free mode)."""
+        t = self._dev_steps.get(gid)
+        if t is None:
+            t = torch.tensor([int(self.param_groups[gid].get("step", 0))], dtype=torch.int32,
+                             device=device)
+            self._dev_steps[gid] = t
+        return t
+
+    def _dev_flag(self, key, device, init_first_run):
+        """int32 device 'initialised' flag (0 => first run) for momentum-style state."""
+        t = self._dev_flags.get(key)
+        if t is None:
+            t = torch.tensor([0 if init_first_run else 1], dtype=torch.int32, device=device)
+            self._dev_flags[key] = t
+        return t
+
+    def _step_value(self, gid, group, device):
+        """(host step, device step tensor or None) for this step; increments host step."""
+        if self._sync_free() and device.type == "cuda":
+            return 0, self._dev_step(gid, device)
+        group["step"] = group.get("step", 0) + 1
+        return group["step"], None
+
+    def _after_step(self, gid, device, step_t, noop):
+        if step_t is not None:
+            _native.require().mt.advance_step(step_t, noop)
+
+    # ------------------------------------------------------------------ API
+    def zero_grad(self, set_to_none=None):
+        if set_to_none is None:
+            set_to_none = self.set_grad_none
+        if set_to_none:
+            for group in self.param_groups:
+                for p in group["params"]:
+                    p.grad = None
+        else:
+            grads = []
+            for group in self.param_groups:
+                for p in group["params"]:
+                    if p.grad is not None:
+                        if p.grad.requires_grad:
+                            p.grad = p.grad.detach()
+                        grads.append(p.grad)
+            if grads:
+                _native.require().mt.zero(grads)
+
+    def _materialize_steps(self):
+        for gid, t in self._dev_steps.items():
+            self.param_groups[gid]["step"] = int(t.item())
+
+    def state_dict(self):
+        self._materialize_steps()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dev_steps = {}
+        self._dev_flags = {}

@@ -1,0 +1,70 @@
+"""FusedAdam (apex@f3a960f8 apex/optimizers/fused_adam.py).
+
+``adam_w_mode=True`` (default) is decoupled weight decay (AdamW); False adds
+``weight_decay * p`` to the gradient (L2).  ``group['step']`` is kept per param
+group (Apex checkpoint format).  Under amp O2 the depth-5 kernel reads the grad,
+updates the fp32 master / exp_avg / exp_avg_sq and writes the 16-bit model copy
+in one pass; in amp sync-free mode the step counter lives on the device and is
+only advanced for non-skipped steps.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import amp_C
+from ._base import FusedOptimizerBase
+
+
+class FusedAdam(FusedOptimizerBase):
+    def __init__(self, params, lr=1e-3, bias_correction=True, betas=(0.9, 0.999), eps=1e-8,
+                 adam_w_mode=True, weight_decay=0., amsgrad=False, set_grad_none=True,
+                 materialize_master_grads=True):
+        if amsgrad:
+            raise RuntimeError("FusedAdam does not support the AMSGrad variant.")
+        defaults = dict(lr=lr, bias_correction=bias_correction, betas=betas, eps=eps,
+                        weight_decay=weight_decay)
+        super().__init__(params, defaults, set_grad_none=set_grad_none,
+                         materialize_master_grads=materialize_master_grads)
+        self.adam_w_mode = 1 if adam_w_mode else 0
+
+    @torch.no_grad()
+    def step(self, closure=None, grads=None, output_params=None, scale=None, grad_norms=None):
+        if any(p is not None for p in [grads, output_params, scale, grad_norms]):
+            raise RuntimeError("FusedAdam has been updated.  Simply initialize it identically to "
+                               "torch.optim.Adam, and call step() with no arguments.")
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+
+        for gid, group in enumerate(self.param_groups):
+            bias_correction = 1 if group["bias_correction"] else 0
+            beta1, beta2 = group["betas"]
+            sets = self._launch_sets(gid, group)
+            if not sets:
+                continue
+            dev = next(iter(sets.values()))["params"][0].device
+            step, step_t = self._step_value(gid, group, dev)
+            noop = self._noop(dev)
+            for key, s in sets.items():
+                m, v = [], []
+                for p in s["params"]:
+                    state = self.state[p]
+                    # State initialization
+                    if len(state) == 0:
+                        # Exponential moving average of gradient values
+                        state["exp_avg"] = torch.zeros_like(p)
+                        # Exponential moving average of squared gradient values
+                        state["exp_avg_sq"] = torch.zeros_like(p)
+                    m.append(state["exp_avg"])
+                    v.append(state["exp_avg_sq"])
+                lists = [s["grads"], s["params"], m, v]
+                if s["copies"] is not None:
+                    lists.append(s["copies"])
+                scale_v, inv = self._scale_args(s["scaled"])
+                amp_C.multi_tensor_adam(65536, noop, lists, group["lr"], beta1, beta2,
+                                        group["eps"], step_t if step_t is not None else step,
+                                        self.adam_w_mode, bias_correction,
+                                        group["weight_decay"], scale=scale_v, scale_inv=inv)
+            self._after_step(gid, dev, step_t, noop)
+        return loss

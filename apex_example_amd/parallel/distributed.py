@@ -1,0 +1,277 @@
+"""apex.parallel.DistributedDataParallel / Reducer for MI355X
+(apex@f3a960f8 apex/parallel/distributed.py).
+
+One process per GPU; collectives go through ``torch.distributed`` (backend
+"nccl" = RCCL over xGMI on MI355X, "gloo" on CPU).  The bucketing / overlap core
+is the C++ ``_C.reducer.Reducer``:
+
+* gradients are views into persistent flat bucket buffers (no flatten /
+  unflatten copies per step);
+* buckets are filled in gradient-arrival order (recorded on the first backward,
+  synchronised from rank 0, then fixed) and all-reduced as soon as they are
+  complete, in the same order on every rank, overlapping the rest of backward;
+* the end-of-backward epilogue makes the compute stream wait on every bucket
+  and raises if a bucket was never reduced.
+
+Bucket size (``message_size``, elements): Apex's default 1e7 elements.  On an
+8x MI355X node every GPU talks to the 7 others over point-to-point xGMI links
+(~153 GB/s each); RCCL's ring/tree channels spread one collective over those
+links, so a bucket only needs to be large enough to amortise RCCL's per-call
+latency (tens of us) - see docs/DDP_TUNING.md and tools/allreduce_sweep.py.
+"""
+from __future__ import annotations
+
+import contextlib
+import warnings
+
+import torch
+import torch.distributed as dist
+from torch.nn.modules import Module
+
+from .. import _native
+
+
+def _group_world(pg):
+    return dist.get_world_size(pg) if pg is not None else dist.get_world_size()
+
+
+def flat_dist_call(tensors, call, extra_args=None, group=None):
+    """apex flat_dist_call: coalesce per dtype, run a collective, copy back.
+    all_reduce results are averaged over the world size (apex semantics)."""
+    buckets = {}
+    for t in tensors:
+        buckets.setdefault((t.dtype, t.device), []).append(t)
+    for (dtype, device), ts in buckets.items():
+        flat = torch.cat([t.contiguous().view(-1) for t in ts])
+        kwargs = {}
+        if group is not None:
+            kwargs["group"] = group
+        if extra_args is not None:
+            call(flat, *extra_args, **kwargs)
+        else:
+            call(flat, **kwargs)
+        if call is dist.all_reduce:
+            flat.div_(_group_world(group))
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+def split_half_float_double(tensors):
+    dtypes = [torch.float16, torch.bfloat16, torch.float32, torch.float64]
+    buckets = []
+    for dtype in dtypes:
+        bucket = [t for t in tensors if t.dtype == dtype]
+        if bucket:
+            buckets.append(bucket)
+    return buckets
+
+
+def split_by_type(tensors):
+    buckets = {}
+    for t in tensors:
+        buckets.setdefault(t.dtype, []).append(t)
+    return buckets
+
+
+def extract_tensors(maybe_tensor, tensor_list):
+    if torch.is_tensor(maybe_tensor):
+        tensor_list.append(maybe_tensor)
+    else:
+        try:
+            for item in maybe_tensor:
+                extract_tensors(item, tensor_list)
+        except TypeError:
+            return
+
+
+class Reducer(object):
+    """Manual all-reduce helper (apex.parallel.Reducer): broadcast params at
+    construction, ``reduce()`` averages gradients across ranks when called."""
+
+    def __init__(self, module_or_grads_list, process_group=None):
+        self.process_group = process_group
+        if isinstance(module_or_grads_list, Module):
+            self.module = module_or_grads_list
+            flat_dist_call([p.data for p in self.module.parameters()], dist.broadcast, (0,),
+                           group=process_group)
+        else:
+            self.module = None
+            self.grads = []
+            extract_tensors(module_or_grads_list, self.grads)
+
+    def reduce(self):
+        if self.module:
+            grads = [p.grad.data for p in self.module.parameters() if p.grad is not None]
+            flat_dist_call(grads, dist.all_reduce, group=self.process_group)
+        else:
+            flat_dist_call(self.grads, dist.all_reduce, group=self.process_group)
+
+
+class DistributedDataParallel(Module):
+    """Data parallel wrapper with flat-bucket, overlapped gradient all-reduce.
+
+    Apex-compatible constructor::
+
+        DistributedDataParallel(module, message_size=10000000, delay_allreduce=False,
+            shared_param=None, allreduce_trigger_params=None, retain_allreduce_buffers=False,
+            allreduce_always_fp32=False, num_allreduce_streams=1,
+            allreduce_communicators=None, gradient_average=True,
+            gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False)
+
+    Extensions: ``process_group``, ``allow_unused`` (tolerate params without
+    grads), ``bucket_align`` (elements; views 16-B aligned for vector kernels),
+    ``use_avg_op`` (ReduceOp.AVG instead of SUM + scale; default on for RCCL).
+    """
+
+    def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,
+                 allreduce_trigger_params=None, retain_allreduce_buffers=False,
+                 allreduce_always_fp32=False, num_allreduce_streams=1,
+                 allreduce_communicators=None, gradient_average=True,
+                 gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
+                 process_group=None, allow_unused=False, bucket_align=64, use_avg_op=None):
+        super().__init__()
+        if not dist.is_initialized():
+            raise RuntimeError("DistributedDataParallel requires torch.distributed to be "
+                               "initialized (init_process_group)")
+        if shared_param is not None:
+            raise ValueError("shared_param is no longer supported as an option.  It was "
+                             "misleadingly named from the start.  It turns out overlapping "
+                             "communication with computation should work fine with shared "
+                             "parameters.  If you still wish to delay communication to the end "
+                             "of the backward pass, use delay_allreduce=True|False instead.")
+        if gradient_average_split_factor is not None:
+            print("Warning:  gradient_average_split_factor has been renamed to "
+                  "gradient_predivide_factor.  For now, gradient_average_split_factor will also "
+                  "work, but please update to gradient_predivide_factor instead.")
+            gradient_predivide_factor = gradient_average_split_factor
+
+        self.module = module
+        self.process_group = process_group
+        self.backend = dist.get_backend(process_group)
+        self.world_size = _group_world(process_group)
+        self.message_size = int(message_size)
+        self.delay_allreduce = delay_allreduce
+        self.retain_allreduce_buffers = retain_allreduce_buffers
+        self.allreduce_always_fp32 = allreduce_always_fp32
+        self.gradient_average = gradient_average
+        self.gradient_predivide_factor = gradient_predivide_factor
+        self.num_allreduce_streams = num_allreduce_streams
+        self.prof = prof
+        self.allow_unused = allow_unused
+        self.bucket_align = bucket_align
+        if use_avg_op is None:
+            use_avg_op = self.backend == "nccl"
+        self.use_avg_op = bool(use_avg_op)
+        self._trigger_params = allreduce_trigger_params
+        self.custom_allreduce_triggers = allreduce_trigger_params is not None
+
+        self._bucket_pgs = None
+        if allreduce_communicators is not None:
+            self._bucket_pgs = list(allreduce_communicators[0] if isinstance(
+                allreduce_communicators, tuple) else allreduce_communicators)
+            self.num_allreduce_streams = len(self._bucket_pgs)
+        elif num_allreduce_streams > 1:
+            ranks = list(range(self.world_size))
+            self._bucket_pgs = [dist.new_group(ranks=ranks) for _ in range(num_allreduce_streams)]
+
+        self.active_params = self._collect_params()
+        if self.backend == "nccl":
+            for p in self.active_params:
+                assert p.is_cuda, "NCCL backend only supports model parameters to be on GPU."
+
+        # broadcast parameters from rank 0 (apex: buffers are NOT broadcast)
+        if self.world_size > 1:
+            flat_dist_call([p.data for p in self.module.parameters()], dist.broadcast, (0,),
+                           group=process_group)
+        self._build_reducer()
+
+    # ------------------------------------------------------------------ internals
+    def _collect_params(self):
+        seen = set()
+        params = []
+        for p in self.module.parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                params.append(p)
+        return params
+
+    def _build_reducer(self):
+        C = _native.require()
+        pg = self.process_group if self.process_group is not None else dist.group.WORLD
+        triggers = []
+        if self._trigger_params is not None:
+            ids = {id(p) for p in self._trigger_params}
+            triggers = [i for i, p in enumerate(self.active_params) if id(p) in ids]
+        self.reducer = C.reducer.Reducer(self.active_params, pg, self.message_size,
+                                         self.allreduce_always_fp32,
+                                         float(self.gradient_predivide_factor),
+                                         self.gradient_average, self.delay_allreduce,
+                                         self.use_avg_op, triggers, int(self.bucket_align))
+        self.reducer.set_allow_unused(self.allow_unused)
+        if self._bucket_pgs:
+            self.reducer.set_bucket_process_groups(self._bucket_pgs)
+        for p in self.active_params:
+            p._amd_grad_is_bucket_view = True
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self._build_reducer()
+
+    def __getstate__(self):
+        attrs = self.__dict__.copy()
+        attrs.pop("reducer", None)
+        return attrs
+
+    # ------------------------------------------------------------------ API
+    def enable_allreduce(self):
+        self.reducer.set_enabled(True)
+
+    def disable_allreduce(self):
+        self.reducer.set_enabled(False)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (torch.nn.parallel.DDP spelling)."""
+        prev = self.reducer.enabled()
+        self.reducer.set_enabled(False)
+        try:
+            yield
+        finally:
+            self.reducer.set_enabled(prev)
+
+    @property
+    def needs_refresh(self):
+        return self.reducer.needs_refresh()
+
+    @property
+    def allreduce_buffers(self):
+        return list(self.reducer.bucket_tensors())
+
+    def bucket_layout(self):
+        """List of buckets, each a list of indices into ``active_params``."""
+        return [list(b) for b in self.reducer.layout()]
+
+    def zero_grad_buckets(self):
+        """Zero every gradient with one memset per bucket (grads stay views)."""
+        self.reducer.zero_grads()
+
+    def forward(self, *inputs, **kwargs):
+        if not self.delay_allreduce:
+            param_list = self._collect_params()
+            if (len(param_list) != len(self.active_params)
+                    or any(a is not b for a, b in zip(param_list, self.active_params))):
+                warnings.warn("DistributedDataParallel: the set of parameters requiring grad "
+                              "changed; rebuilding the gradient buckets")
+                self.reducer.remove_hooks()
+                self.active_params = param_list
+                self._build_reducer()
+        if self.prof:
+            torch.cuda.nvtx.range_push("forward pass DDP logic")
+        out = self.module(*inputs, **kwargs)
+        if self.prof:
+            torch.cuda.nvtx.range_pop()
+        return out

@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 amp O2 (bf16) training throughput, images/sec
+for the whole job (BASELINE.json metric), 1..8 MI355X, one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [...]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Step = forward + loss + amp.scale_loss backward (+ bucketed RCCL all-reduce
+overlapped with backward when N > 1) + FusedSGD step (momentum 0.9, wd 5e-5,
+fp32 master weights, bf16 model copy written in-kernel).  Synthetic ImageNet
+shaped data (224x224, 1000 classes) generated on the device per rank;
+random-init weights.  W untimed warmup steps (MIOpen solver search happens
+there), then exactly K timed steps bracketed by barrier + synchronize; the
+slowest rank's time is reported.
+
+``--impl stock`` runs the same model / data / schedule on the stock
+PyTorch-ROCm path (torch.autocast bf16 + torch.optim.SGD(fused) + torch DDP,
+plain BatchNorm) - the comparator of BASELINE.md section 2.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Baseline for vs_baseline: BASELINE.md has no published number; the comparator
+# is the stock PyTorch-ROCm path measured on the same MI355X.
+STOCK_BASELINE_IMG_S_PER_GPU = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=15)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch-size", type=int, default=256, help="per GPU")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--impl", choices=["amd", "stock"], default="amd")
+    ap.add_argument("--opt-level", default="O2")
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16")
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--no-fused-bn", action="store_true")
+    ap.add_argument("--syncbn", action="store_true", help="SyncBatchNorm across ranks")
+    ap.add_argument("--message-size", type=int, default=10_000_000, help="DDP bucket elements")
+    ap.add_argument("--materialize-master-grads", action="store_true")
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--deterministic", action="store_true")
+    ap.add_argument("--opt-step-iters", type=int, default=20)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build(args, device, world):
+    from apex_example_amd import amp
+    from apex_example_amd.models import resnet50, resnet18
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel, convert_syncbn_model
+
+    half = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    ctor = {"resnet50": resnet50, "resnet18": resnet18}[args.model]
+    fused_bn = args.impl == "amd" and not args.no_fused_bn
+    model = ctor(fused_bn=fused_bn).to(device)
+    if args.syncbn and world > 1:
+        if args.impl == "amd":
+            model = convert_syncbn_model(model)
+        else:
+            model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+    mf = torch.channels_last if not args.no_channels_last else torch.contiguous_format
+    model = model.to(memory_format=mf)
+
+    if args.impl == "amd":
+        opt = FusedSGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5,
+                       materialize_master_grads=args.materialize_master_grads)
+        model, opt = amp.initialize(model, opt, opt_level=args.opt_level, half_dtype=half,
+                                    verbosity=0)
+        if world > 1:
+            model = DistributedDataParallel(model, message_size=args.message_size)
+
+        def step(x, y):
+            out = model(x)
+            loss = F.cross_entropy(out, y)
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
+            opt.step()
+            return loss
+
+        def opt_only():
+            opt.step()
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5,
+                              fused=True)
+        scaler = torch.amp.GradScaler("cuda", enabled=(half == torch.float16))
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(
+                model, device_ids=[device.index], bucket_cap_mb=25, gradient_as_bucket_view=True)
+
+        def step(x, y):
+            with torch.autocast("cuda", dtype=half):
+                out = model(x)
+                loss = F.cross_entropy(out, y)
+            opt.zero_grad(set_to_none=True)
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+            return loss
+
+        def opt_only():
+            opt.step()
+    return model, opt, step, opt_only, mf
+
+
+def main():
+    args = parse()
+    from apex_example_amd.utils.dist import init_distributed
+
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus and env_world > 1:
+        print("warning: --gpus %d but WORLD_SIZE=%d" % (args.gpus, env_world), file=sys.stderr)
+    rank, world, device = init_distributed()
+    torch.backends.cudnn.benchmark = not args.deterministic
+    torch.backends.cudnn.deterministic = args.deterministic
+    torch.manual_seed(1234 + rank)
+
+    model, opt, step, opt_only, mf = build(args, device, world)
+    bs = args.batch_size
+    x = torch.randn(bs, 3, args.image_size, args.image_size, device=device).to(
+        memory_format=mf)
+    y = torch.randint(0, 1000, (bs,), device=device)
+
+    log(rank, "[bench] impl=%s model=%s bs/gpu=%d world=%d warmup=%d steps=%d" % (
+        args.impl, args.model, bs, world, args.warmup, args.steps))
+    t0 = time.time()
+    for i in range(args.warmup):
+        loss = step(x, y)
+        if i == 0 or (i + 1) % 5 == 0:
+            torch.cuda.synchronize()
+            log(rank, "[bench] warmup %d/%d loss %.4f (%.1fs)" % (i + 1, args.warmup, loss.item(),
+                                                              time.time() - t0))
+    torch.cuda.synchronize()
+
+    def sync_all():
+        if world > 1:
+            dist.barrier(device_ids=[device.index])
+        torch.cuda.synchronize()
+
+    sync_all()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(x, y)
+    sync_all()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    # optimizer step alone (secondary metric of BASELINE.json)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.opt_step_iters):
+        opt_only()
+    e1.record()
+    torch.cuda.synchronize()
+    opt_ms = e0.elapsed_time(e1) / args.opt_step_iters
+
+    ms_per_step = elapsed / args.steps * 1e3
+    img_s = bs * world * args.steps / elapsed
+    vs = None
+    if STOCK_BASELINE_IMG_S_PER_GPU:
+        vs = img_s / (STOCK_BASELINE_IMG_S_PER_GPU * world)
+    rec = {
+        "metric": "images/sec (whole node) ResNet-50 amp O2",
+        "value": round(img_s, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None if vs is None else round(vs, 4),
+        "dtype": args.dtype,
+        "data": "synthetic (on-device random 3x%dx%d images, random labels; random-init "
+                "weights)" % (args.image_size, args.image_size),
+        "config": {
+            "model": args.model,
+            "global_batch": bs * world,
+            "per_gpu_batch": bs,
+            "seq_len": None,
+            "image_size": args.image_size,
+            "parallelism": "dp%d" % world,
+            "impl": args.impl,
+            "opt_level": args.opt_level,
+            "optimizer": "FusedSGD(momentum=0.9, wd=5e-5)" if args.impl == "amd"
+                         else "torch.optim.SGD(fused)",
+            "channels_last": not args.no_channels_last,
+            "fused_bn": args.impl == "amd" and not args.no_fused_bn,
+            "syncbn": bool(args.syncbn and world > 1),
+            "ddp_message_size": args.message_size if world > 1 else None,
+        },
+        "optimizer_step_ms": round(opt_ms, 4),
+        "final_loss": round(final_loss, 4),
+    }
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier(device_ids=[device.index])
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

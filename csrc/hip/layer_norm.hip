@@ -1,0 +1,413 @@
+// Fused LayerNorm / RMSNorm forward + backward for gfx950.
+//
+// Behavioural spec: apex@f3a960f8 csrc/layer_norm_cuda_kernel.cu (SURVEY.md
+// N-13a..d): forward(input, normalized_shape, eps) -> (out, mean, invvar),
+// *_affine variants, backward -> dinput (+ dgamma, dbeta).
+//
+// MI355X design (not a port of apex's (32,4)-thread warp tiling):
+//  * one ROW PER WAVE64: a row of n2 <= 2048 is held in registers as VPT
+//    16-byte vectors per lane (n2 = 1024 bf16 -> 2 x 16 B per lane); mean and
+//    variance are a two-pass register computation + xor-shuffle reductions, no
+//    LDS, no Welford divisions;
+//  * the backward kernel computes dx AND accumulates dgamma/dbeta partials in
+//    the same pass: a lane owns the same 8*VPT columns for every row its wave
+//    visits, so the column sums stay in registers across rows; one LDS combine
+//    per block then a deterministic column-sum kernel (no float atomics);
+//  * a generic block-per-row path covers odd widths / unaligned rows.
+#include "amd_dev.h"
+#include "amd_kernels.h"
+
+namespace amd {
+
+constexpr int kLNThreads = 256;
+constexpr int kLNWaves = kLNThreads / kWave;
+
+template <typename F>
+static inline void ln_dispatch(DType a, F&& f) {
+  switch (a) {
+    case DType::F32: f(float{}); break;
+    case DType::F16: f(half_t{}); break;
+    case DType::BF16: f(bf16_t{}); break;
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------- forward (fast)
+template <typename T, typename TW, int VPT>
+__global__ void __launch_bounds__(kLNThreads)
+    ln_fwd_fast(const T* __restrict__ x, const TW* __restrict__ gamma, const TW* __restrict__ beta,
+                T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ invvar_out,
+                int64_t n1, int n2, float eps, int rms) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row0 = (int64_t)blockIdx.x * kLNWaves + threadIdx.x / kWave;
+  const int64_t wstride = (int64_t)gridDim.x * kLNWaves;
+  const float inv_n = 1.f / (float)n2;
+  for (int64_t row = row0; row < n1; row += wstride) {
+    const T* xr = x + row * n2;
+    float v[VPT][8];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      int col = (k * kWave + lane) * 8;
+      if (col < n2) load8(xr + col, v[k]);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[k][i] = 0.f;
+      }
+    }
+    float mu = 0.f;
+    if (!rms) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += v[k][i];
+      mu = wave_sum(s) * inv_n;
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      int col = (k * kWave + lane) * 8;
+      if (col < n2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float d = v[k][i] - mu;
+          ss = fmaf(d, d, ss);
+        }
+      }
+    }
+    const float var = wave_sum(ss) * inv_n;
+    const float iv = rsqrtf(var + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mu;
+      invvar_out[row] = iv;
+    }
+    T* yr = y + row * n2;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      int col = (k * kWave + lane) * 8;
+      if (col >= n2) continue;
+      float g[8], b[8];
+      if (gamma) load8(gamma + col, g);
+      if (beta) load8(beta + col, b);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float xh = (v[k][i] - mu) * iv;
+        o[i] = gamma ? fmaf(xh, g[i], beta ? b[i] : 0.f) : xh;
+      }
+      store8(yr + col, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward (generic)
+template <typename T, typename TW>
+__global__ void __launch_bounds__(kLNThreads)
+    ln_fwd_generic(const T* __restrict__ x, const TW* __restrict__ gamma,
+                   const TW* __restrict__ beta, T* __restrict__ y, float* __restrict__ mean_out,
+                   float* __restrict__ invvar_out, int64_t n1, int n2, float eps, int rms) {
+  __shared__ float scratch[kLNWaves];
+  const int64_t row = blockIdx.x;
+  if (row >= n1) return;
+  const T* xr = x + row * n2;
+  float mu = 0.f;
+  if (!rms) {
+    float s = 0.f;
+    for (int c = threadIdx.x; c < n2; c += blockDim.x) s += to_f32(xr[c]);
+    mu = block_sum(s, scratch) / (float)n2;
+  }
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < n2; c += blockDim.x) {
+    float d = to_f32(xr[c]) - mu;
+    ss = fmaf(d, d, ss);
+  }
+  const float var = block_sum(ss, scratch) / (float)n2;
+  const float iv = rsqrtf(var + eps);
+  if (threadIdx.x == 0) {
+    if (mean_out) mean_out[row] = mu;
+    invvar_out[row] = iv;
+  }
+  T* yr = y + row * n2;
+  for (int c = threadIdx.x; c < n2; c += blockDim.x) {
+    float xh = (to_f32(xr[c]) - mu) * iv;
+    float o = gamma ? fmaf(xh, to_f32(gamma[c]), beta ? to_f32(beta[c]) : 0.f) : xh;
+    yr[c] = from_f32<T>(o);
+  }
+}
+
+static inline int ln_vpt(int64_t n2) { return (int)((n2 + 511) / 512); }
+
+static inline bool ln_fast_ok(const void* x, const void* g, const void* b, const void* y,
+                              int64_t n2) {
+  auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
+  return n2 % 8 == 0 && n2 <= 2048 && al(x) && al(g) && al(b) && al(y);
+}
+
+static inline int ln_grid(int64_t n1) {
+  int64_t blocks = (n1 + kLNWaves - 1) / kLNWaves;
+  // enough waves to fill 256 CUs several times over; rows loop beyond that
+  if (blocks > 8192) blocks = 8192;
+  return (int)(blocks > 0 ? blocks : 1);
+}
+
+void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta, DType tw,
+                    void* y, float* mean, float* invvar, int64_t n1, int64_t n2, float eps,
+                    int rms, hipStream_t st) {
+  if (n1 == 0 || n2 == 0) return;
+  ln_dispatch(tx, [&](auto t0) {
+    ln_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      const T* xp = static_cast<const T*>(x);
+      const TW* gp = static_cast<const TW*>(gamma);
+      const TW* bp = static_cast<const TW*>(beta);
+      T* yp = static_cast<T*>(y);
+      if (ln_fast_ok(x, gamma, beta, y, n2)) {
+        int vpt = ln_vpt(n2);
+        dim3 grid(ln_grid(n1)), block(kLNThreads);
+        switch (vpt) {
+          case 1: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 1>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms); break;
+          case 2: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 2>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms); break;
+          case 3: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 3>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms); break;
+          default: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 4>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms); break;
+        }
+      } else {
+        hipLaunchKernelGGL((ln_fwd_generic<T, TW>), dim3((unsigned)n1), dim3(kLNThreads), 0, st, xp,
+                           gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms);
+      }
+    });
+  });
+}
+
+// ---------------------------------------------------------------- backward (fast, fused)
+// part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
+template <typename T, typename TW, int VPT>
+__global__ void __launch_bounds__(kLNThreads)
+    ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
+                const float* __restrict__ mean, const float* __restrict__ invvar,
+                T* __restrict__ dx, float* __restrict__ part, int64_t n1, int n2, int rms) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [kLNWaves][2][n2]
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int64_t row0 = (int64_t)blockIdx.x * kLNWaves + wid;
+  const int64_t wstride = (int64_t)gridDim.x * kLNWaves;
+  const float inv_n = 1.f / (float)n2;
+  const bool want_part = part != nullptr;
+
+  float g[VPT][8];
+  float adg[VPT][8], adb[VPT][8];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    int col = (k * kWave + lane) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      adg[k][i] = 0.f;
+      adb[k][i] = 0.f;
+      g[k][i] = 1.f;
+    }
+    if (gamma && col < n2) load8(gamma + col, g[k]);
+  }
+
+  for (int64_t row = row0; row < n1; row += wstride) {
+    const float mu = rms ? 0.f : mean[row];
+    const float iv = invvar[row];
+    float xv[VPT][8], dv[VPT][8];
+    float s1 = 0.f, s2 = 0.f;  // sum(dy*g), sum(dy*g*xhat)
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      int col = (k * kWave + lane) * 8;
+      if (col < n2) {
+        load8(x + row * n2 + col, xv[k]);
+        load8(dy + row * n2 + col, dv[k]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[k][i] = dv[k][i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float xh = (xv[k][i] - mu) * iv;
+        xv[k][i] = xh;  // keep xhat
+        float dg = dv[k][i] * g[k][i];
+        s1 += dg;
+        s2 = fmaf(dg, xh, s2);
+        if (want_part) {
+          adg[k][i] = fmaf(dv[k][i], xh, adg[k][i]);
+          adb[k][i] += dv[k][i];
+        }
+      }
+    }
+    s1 = wave_sum(s1) * inv_n;
+    s2 = wave_sum(s2) * inv_n;
+    T* dxr = dx + row * n2;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      int col = (k * kWave + lane) * 8;
+      if (col >= n2) continue;
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float dg = dv[k][i] * g[k][i];
+        float t = rms ? (dg - xv[k][i] * s2) : (dg - s1 - xv[k][i] * s2);
+        o[i] = t * iv;
+      }
+      store8(dxr + col, o);
+    }
+  }
+
+  if (!want_part) return;
+  // combine the block's waves in LDS, then one partial row pair per block
+  float* my = lds + (size_t)wid * 2 * n2;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    int col = (k * kWave + lane) * 8;
+    if (col >= n2) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      my[col + i] = adg[k][i];
+      my[n2 + col + i] = adb[k][i];
+    }
+  }
+  __syncthreads();
+  float* out = part + (size_t)blockIdx.x * 2 * n2;
+  for (int c = threadIdx.x; c < 2 * n2; c += blockDim.x) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kLNWaves; ++w) s += lds[(size_t)w * 2 * n2 + c];
+    out[c] = s;
+  }
+}
+
+// ---------------------------------------------------------------- backward (generic)
+template <typename T, typename TW>
+__global__ void __launch_bounds__(kLNThreads)
+    ln_bwd_dx_generic(const T* __restrict__ dy, const T* __restrict__ x,
+                      const TW* __restrict__ gamma, const float* __restrict__ mean,
+                      const float* __restrict__ invvar, T* __restrict__ dx, int64_t n1, int n2,
+                      int rms) {
+  __shared__ float scratch[kLNWaves];
+  const int64_t row = blockIdx.x;
+  if (row >= n1) return;
+  const float mu = rms ? 0.f : mean[row];
+  const float iv = invvar[row];
+  const T* xr = x + row * n2;
+  const T* dr = dy + row * n2;
+  float s1 = 0.f, s2 = 0.f;
+  for (int c = threadIdx.x; c < n2; c += blockDim.x) {
+    float xh = (to_f32(xr[c]) - mu) * iv;
+    float dg = to_f32(dr[c]) * (gamma ? to_f32(gamma[c]) : 1.f);
+    s1 += dg;
+    s2 = fmaf(dg, xh, s2);
+  }
+  s1 = block_sum(s1, scratch) / (float)n2;
+  s2 = block_sum(s2, scratch) / (float)n2;
+  for (int c = threadIdx.x; c < n2; c += blockDim.x) {
+    float xh = (to_f32(xr[c]) - mu) * iv;
+    float dg = to_f32(dr[c]) * (gamma ? to_f32(gamma[c]) : 1.f);
+    float t = rms ? (dg - xh * s2) : (dg - s1 - xh * s2);
+    dx[row * n2 + c] = from_f32<T>(t * iv);
+  }
+}
+
+// column partials for the generic path: grid (ceil(n2/256), nparts)
+template <typename T>
+__global__ void __launch_bounds__(kLNThreads)
+    ln_bwd_colpart_generic(const T* __restrict__ dy, const T* __restrict__ x,
+                           const float* __restrict__ mean, const float* __restrict__ invvar,
+                           float* __restrict__ part, int64_t n1, int n2, int rows_per_part,
+                           int rms) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n2) return;
+  int64_t r0 = (int64_t)blockIdx.y * rows_per_part;
+  int64_t r1 = r0 + rows_per_part;
+  if (r1 > n1) r1 = n1;
+  float ag = 0.f, ab = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    float xh = (to_f32(x[r * n2 + c]) - (rms ? 0.f : mean[r])) * invvar[r];
+    float d = to_f32(dy[r * n2 + c]);
+    ag = fmaf(d, xh, ag);
+    ab += d;
+  }
+  part[(size_t)blockIdx.y * 2 * n2 + c] = ag;
+  part[(size_t)blockIdx.y * 2 * n2 + n2 + c] = ab;
+}
+
+// sum nparts partial rows -> dgamma, dbeta (TW); fixed order -> deterministic
+template <typename TW>
+__global__ void __launch_bounds__(256)
+    ln_bwd_colsum(const float* __restrict__ part, int nparts, int n2, TW* __restrict__ dgamma,
+                  TW* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n2) return;
+  float sg = 0.f, sb = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    sg += part[(size_t)p * 2 * n2 + c];
+    sb += part[(size_t)p * 2 * n2 + n2 + c];
+  }
+  if (dgamma) dgamma[c] = from_f32<TW>(sg);
+  if (dbeta) dbeta[c] = from_f32<TW>(sb);
+}
+
+static inline int ln_bwd_blocks(int64_t n1) {
+  int64_t b = (n1 + kLNWaves - 1) / kLNWaves;
+  if (b > 1024) b = 1024;  // bounds the partial buffer (nblocks x 2 x n2 floats)
+  return (int)(b > 0 ? b : 1);
+}
+static inline int ln_generic_parts(int64_t n1) {
+  int64_t p = (n1 + 31) / 32;
+  if (p > 512) p = 512;
+  return (int)(p > 0 ? p : 1);
+}
+
+int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2) {
+  int64_t a = (int64_t)ln_bwd_blocks(n1) * 2 * n2;
+  int64_t b = (int64_t)ln_generic_parts(n1) * 2 * n2;
+  return a > b ? a : b;
+}
+
+void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, DType tw,
+                    const float* mean, const float* invvar, void* dx, void* dgamma, void* dbeta,
+                    float* part, int64_t n1, int64_t n2, int rms, hipStream_t st) {
+  if (n1 == 0 || n2 == 0) return;
+  const bool want_wb = dgamma != nullptr || dbeta != nullptr;
+  ln_dispatch(tx, [&](auto t0) {
+    ln_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      const T* dyp = static_cast<const T*>(dy);
+      const T* xp = static_cast<const T*>(x);
+      const TW* gp = static_cast<const TW*>(gamma);
+      T* dxp = static_cast<T*>(dx);
+      int nparts;
+      if (ln_fast_ok(x, gamma, nullptr, dx, n2) && ((uintptr_t)dy % 16) == 0) {
+        int vpt = ln_vpt(n2);
+        int blocks = ln_bwd_blocks(n1);
+        size_t lds = want_wb ? (size_t)kLNWaves * 2 * n2 * sizeof(float) : 0;
+        float* pp = want_wb ? part : nullptr;
+        dim3 grid(blocks), block(kLNThreads);
+        switch (vpt) {
+          case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
+          case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
+          case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
+          default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
+        }
+        nparts = blocks;
+      } else {
+        hipLaunchKernelGGL((ln_bwd_dx_generic<T, TW>), dim3((unsigned)n1), dim3(kLNThreads), 0, st,
+                           dyp, xp, gp, mean, invvar, dxp, n1, (int)n2, rms);
+        nparts = ln_generic_parts(n1);
+        if (want_wb) {
+          int rows_per_part = (int)((n1 + nparts - 1) / nparts);
+          hipLaunchKernelGGL((ln_bwd_colpart_generic<T>), dim3((unsigned)((n2 + 255) / 256), nparts),
+                             dim3(256), 0, st, dyp, xp, mean, invvar, part, n1, (int)n2,
+                             rows_per_part, rms);
+        }
+      }
+      if (want_wb) {
+        hipLaunchKernelGGL((ln_bwd_colsum<TW>), dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st,
+                           part, nparts, (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta));
+      }
+    });
+  });
+}
+
+}  // namespace amd

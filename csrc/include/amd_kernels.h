@@ -1,0 +1,178 @@
+// Host-callable launchers for every HIP kernel of the framework.
+//
+// These functions take raw device pointers, element dtypes and a hipStream_t;
+// they never allocate or synchronise, so every one of them is safe inside a
+// hipGraph capture.  The torch-facing layer (csrc/torch/*.cpp) owns tensors,
+// validation and the multi-tensor table cache.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mt_table.h"
+
+namespace amd {
+
+enum class DType : int;
+
+// A scale factor given either by value or by a device scalar; `invert` uses
+// 1/x.  This is how the loss scale reaches kernels without a host sync.
+struct ScaleArg {
+  const float* ptr;
+  float val;
+  int invert;
+};
+
+// ----- multi-tensor elementwise (amp_C.multi_tensor_scale / axpby) ---------
+void mt_scale(const MTLaunch& L, DType in, DType out, ScaleArg s, int* noop, hipStream_t st);
+void mt_check_finite(const MTLaunch& L, DType in, int* noop, hipStream_t st);
+void mt_axpby(const MTLaunch& L, DType x, DType y, DType out, ScaleArg a, ScaleArg b,
+              int arg_to_check, int* noop, hipStream_t st);
+void mt_fill_zero(const MTLaunch& L, DType t, hipStream_t st);
+
+// ----- norms (amp_C.multi_tensor_l2norm / _norm_out / max norm) ------------
+// Per-chunk partials (sum of squares, or max|x| when max_norm) -> partials[nchunks].
+void mt_norm_partials(const MTLaunch& L, DType in, int max_norm, float* partials, int* noop,
+                      hipStream_t st);
+// Reduce partials to a global norm (out_global, may be null) and per-tensor norms
+// (out_per_tensor[ntensors], may be null).  `npart_sets` partial arrays are laid out
+// back to back (stride nchunks); set k's results go to out_*[k*...].
+void mt_norm_finalize(const MTLaunch& L, const float* partials, int npart_sets, int max_norm,
+                      float* out_global, float* out_per_tensor, hipStream_t st);
+
+// ----- optimizers ----------------------------------------------------------
+struct SgdArgs {
+  float wd, momentum, dampening, lr;
+  int nesterov, first_run, wd_after_momentum;
+  ScaleArg scale;           // grad multiplier (1/loss_scale when unscale is folded in)
+  const float* lr_ptr;      // optional device lr (overrides lr)
+  int* first_run_flag;      // optional device flag: first_run = (*flag == 0)
+};
+// depth 3: [g, p, m]; depth 4: [g, p, m, p_copy]
+void mt_sgd(const MTLaunch& L, int depth, DType g, DType p, DType m, DType copy,
+            const SgdArgs& a, const int* noop, hipStream_t st);
+// after an SGD step: first_run_flag = 1 unless the step was skipped (noop set)
+void mark_step_done(int* flag, const int* noop, hipStream_t st);
+
+struct AdamArgs {
+  float lr, beta1, beta2, eps, wd;
+  int step;                 // host step (used when step_ptr == null)
+  const int* step_ptr;      // optional device step counter (count of completed steps)
+  int mode;                 // 0: L2 (g += wd*p), 1: decoupled (AdamW)
+  int bias_correction;
+  ScaleArg scale;           // grad multiplier
+  const float* lr_ptr;
+};
+// depth 4: [g, p, m, v]; depth 5: [g, p, m, v, p_copy]   (m, v share p's dtype)
+void mt_adam(const MTLaunch& L, int depth, DType g, DType p, DType copy, const AdamArgs& a,
+             const int* noop, hipStream_t st);
+// step counters: step += 1 unless noop set
+void advance_step(int* step, const int* noop, hipStream_t st);
+
+struct LambArgs {
+  float lr, beta1, beta2, eps, wd;
+  int step;
+  const int* step_ptr;
+  int mode;                 // 0: L2, 1: decoupled
+  int bias_correction;
+  int grad_averaging;
+  const float* global_grad_norm;  // device scalar (already sqrt'ed)
+  float max_grad_norm;
+  int use_nvlamb;
+  ScaleArg scale;
+  const float* lr_ptr;
+};
+// stage 1: [g, p, m, v, u] -> u (fp32 update) + partials (||p||^2, ||u||^2 per chunk)
+void mt_lamb_stage1(const MTLaunch& L, DType g, DType p, const LambArgs& a, float* partials,
+                    const int* noop, hipStream_t st);
+// stage 2: [p, u] or [p, u, p_copy]; per-tensor norms from mt_norm_finalize
+void mt_lamb_stage2(const MTLaunch& L, int depth, DType p, DType copy, const LambArgs& a,
+                    const float* param_norms, const float* update_norms, const int* noop,
+                    hipStream_t st);
+
+struct NovoArgs {
+  float lr, beta1, beta2, eps, wd;
+  int step;
+  const int* step_ptr;
+  int mode;                 // 0: L2-style (wd added to normalized grad), 1: decoupled
+  int bias_correction;
+  int grad_averaging;
+  int norm_type;            // 0: inf norm, 2: L2 norm
+  float init_zero;          // unused placeholder for API symmetry
+  ScaleArg scale;
+  const float* lr_ptr;
+};
+// NovoGrad: [g, p, m] with per-tensor second moments v[ntensors] (fp32, device)
+// `grad_norms` holds this step's per-tensor grad norms; v is blended in-kernel
+// by the first chunk of each tensor only after every chunk has read it -> the
+// blend is done by a separate tiny kernel (novograd_blend) before the update.
+void novograd_blend(float* v, const float* grad_norms, int ntensors, float beta2, int norm_type,
+                    int first_step, const int* noop, hipStream_t st);
+void mt_novograd(const MTLaunch& L, DType g, DType p, const NovoArgs& a, const float* v,
+                 const int* noop, hipStream_t st);
+
+struct AdagradArgs {
+  float lr, eps, wd;
+  int mode;                 // 0: L2, 1: decoupled
+  ScaleArg scale;
+  const float* lr_ptr;
+};
+// [g, p, h]
+void mt_adagrad(const MTLaunch& L, DType g, DType p, const AdagradArgs& a, const int* noop,
+                hipStream_t st);
+
+// ----- loss scaler state machine (device resident) --------------------------
+// if *overflow: scale = max(scale/factor, min_scale), unskipped = 0, ++skipped
+// else: ++unskipped; if unskipped == window: scale = min(scale*factor, max), unskipped = 0
+void update_loss_scale(float* scale, int* unskipped, int* skipped_total, const int* overflow,
+                       float factor, int window, float min_scale, float max_scale, int dynamic,
+                       hipStream_t st);
+
+// ----- flat buffers ---------------------------------------------------------
+// out[i] = in[i] * s (cast between dtypes), optional finiteness flag.
+void flat_scale(const void* in, DType tin, void* out, DType tout, int64_t n, ScaleArg s,
+                int* noop, hipStream_t st);
+
+// ----- LayerNorm (apex fused_layer_norm_cuda) --------------------------------
+// x[n1, n2] (T), gamma/beta [n2] (TW, nullable), y [n1,n2] (T), mean/invvar [n1] fp32
+void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta, DType tw,
+                    void* y, float* mean, float* invvar, int64_t n1, int64_t n2, float eps,
+                    int rms, hipStream_t st);
+// dx [n1,n2]; dgamma/dbeta [n2] (TW) computed if non-null. `part` workspace
+// must hold layer_norm_bwd_workspace(n1, n2) floats.
+int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2);
+void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, DType tw,
+                    const float* mean, const float* invvar, void* dx, void* dgamma, void* dbeta,
+                    float* part, int64_t n1, int64_t n2, int rms, hipStream_t st);
+
+// ----- BatchNorm / SyncBN (apex syncbn) --------------------------------------
+// Layout: NCHW  -> x viewed as [N, C, HW]; NHWC (channel-last) -> [M, C] with M = N*H*W.
+// Per-channel statistics use split reductions: partial Welford (mean, M2, count)
+// slabs then a combine, so small-C layers still cover all 256 CUs.
+int64_t bn_stats_workspace(int64_t outer, int64_t C, int64_t inner, int channel_last);
+void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
+                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st);
+// combine world_size x (mean, var_biased, count) -> mean, invstd, unbiased var; and
+// update running stats (may be null) with momentum.
+void bn_combine_stats(const float* means, const float* vars, const float* counts, int world,
+                      int64_t C, float eps, float momentum, float* mean_out, float* invstd_out,
+                      float* running_mean, DType trm, void* running_var_any, float* var_out,
+                      hipStream_t st);
+// y = (x - mean) * invstd * w + b  [+ z] [relu]
+void bn_apply(const void* x, DType tx, const float* mean, const float* invstd,
+              const void* weight, const void* bias, DType tw, const void* z, void* y,
+              int64_t outer, int64_t C, int64_t inner, int channel_last, int relu,
+              hipStream_t st);
+// per-channel sum_dy, sum_dy_xmu (fp32) and grad_weight/grad_bias (TW) ; when relu
+// is fused, dy is masked by (y > 0) where y is recomputed from x.
+void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
+                    const float* invstd, const void* weight, const void* bias, DType tw,
+                    int relu, const void* z, int64_t outer, int64_t C, int64_t inner,
+                    int channel_last, float* sum_dy, float* sum_dy_xmu, void* grad_weight,
+                    void* grad_bias, float* ws, hipStream_t st);
+// dx = (dy' - mean_dy - (x-mean)*invstd^2*mean_dy_xmu) * invstd * w ; dz = dy' if z
+void bn_backward_elemt(const void* dy, const void* x, DType tx, const float* mean,
+                       const float* invstd, const void* weight, const void* bias, DType tw,
+                       const float* sum_dy, const float* sum_dy_xmu, float inv_count,
+                       int relu, const void* z, void* dx, void* dz, int64_t outer, int64_t C,
+                       int64_t inner, int channel_last, hipStream_t st);
+
+}  // namespace amd

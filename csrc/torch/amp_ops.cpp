@@ -1,0 +1,384 @@
+// amp_C-equivalent operators: validate, pick the CPU or gfx950 path, launch.
+//
+// Python signatures are Apex-compatible at the facade level
+// (apex_example_amd/amp_C.py); here every scalar that may live on the device
+// (loss scale, lr, step counter, first-run flag) is accepted as an optional
+// tensor so the optimizer step needs no host synchronisation.
+#include "amp_ops.h"
+
+#include "../cpu/cpu_ops.h"
+#include "common.h"
+
+namespace amd {
+
+namespace {
+int* noop_ptr(at::Tensor& noop) {
+  if (!noop.defined()) return nullptr;
+  TORCH_CHECK(noop.scalar_type() == at::kInt, "noop_flag must be an int32 tensor");
+  return noop.data_ptr<int>();
+}
+cpu::Scale cscale(double v, const c10::optional<at::Tensor>& t, bool inv) {
+  return cpu::Scale{v, t.has_value() && t->defined() ? &*t : nullptr, inv};
+}
+at::Tensor* optp(c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? &*t : nullptr;
+}
+TensorLists sub(const TensorLists& l, std::initializer_list<int> idx) {
+  TensorLists r;
+  for (int i : idx) r.push_back(l[(size_t)i]);
+  return r;
+}
+}  // namespace
+
+void mt_scale_op(at::Tensor noop, const TensorLists& lists, double scale,
+                 c10::optional<at::Tensor> scale_t, bool invert) {
+  if (lists.empty() || lists[0].empty()) return;
+  bool gpu = mt_validate(lists, 2, 2);
+  if (!gpu) return cpu::scale(noop, lists, cscale(scale, scale_t, invert));
+  const MTPlan& P = mt_plan(lists);
+  mt_scale(P.L, dtype_of(lists[0][0]), dtype_of(lists[1][0]), make_scale(scale, scale_t, invert),
+           noop_ptr(noop), cur_stream());
+}
+
+// Per-dtype-group launch: the kernels are templated on the element type of each
+// slot, so lists whose tensors mix dtypes are split into homogeneous groups.
+template <typename F>
+static void by_dtype_groups(const TensorLists& lists, F&& f) {
+  const size_t n = lists[0].size();
+  std::vector<std::pair<std::vector<int>, TensorLists>> groups;
+  std::vector<std::vector<at::ScalarType>> keys;
+  for (size_t i = 0; i < n; ++i) {
+    std::vector<at::ScalarType> k;
+    for (auto& l : lists) k.push_back(l[i].scalar_type());
+    size_t g = 0;
+    for (; g < keys.size(); ++g)
+      if (keys[g] == k) break;
+    if (g == keys.size()) {
+      keys.push_back(k);
+      groups.emplace_back(std::vector<int>{}, TensorLists(lists.size()));
+    }
+    groups[g].first.push_back((int)i);
+    for (size_t d = 0; d < lists.size(); ++d) groups[g].second[d].push_back(lists[d][i]);
+  }
+  for (auto& g : groups) f(g.first, g.second);
+}
+
+void mt_scale_any_op(at::Tensor noop, const TensorLists& lists, double scale,
+                     c10::optional<at::Tensor> scale_t, bool invert) {
+  if (lists.empty() || lists[0].empty()) return;
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    mt_scale_op(noop, g, scale, scale_t, invert);
+  });
+}
+
+void mt_check_finite_op(at::Tensor noop, const std::vector<at::Tensor>& list) {
+  if (list.empty()) return;
+  TensorLists lists{list};
+  bool gpu = mt_validate(lists, 1, 1);
+  if (!gpu) return cpu::check_finite(noop, list);
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    mt_check_finite(P.L, dtype_of(g[0][0]), noop_ptr(noop), cur_stream());
+  });
+}
+
+void mt_axpby_op(at::Tensor noop, const TensorLists& lists, double a, c10::optional<at::Tensor> a_t,
+                 bool a_inv, double b, c10::optional<at::Tensor> b_t, bool b_inv,
+                 int64_t arg_to_check) {
+  if (lists.empty() || lists[0].empty()) return;
+  bool gpu = mt_validate(lists, 3, 3);
+  if (!gpu)
+    return cpu::axpby(noop, lists, cscale(a, a_t, a_inv), cscale(b, b_t, b_inv), (int)arg_to_check);
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    mt_axpby(P.L, dtype_of(g[0][0]), dtype_of(g[1][0]), dtype_of(g[2][0]), make_scale(a, a_t, a_inv),
+             make_scale(b, b_t, b_inv), (int)arg_to_check, noop_ptr(noop), cur_stream());
+  });
+}
+
+void mt_zero_op(const std::vector<at::Tensor>& list) {
+  if (list.empty()) return;
+  TensorLists lists{list};
+  bool gpu = mt_validate(lists, 1, 1);
+  if (!gpu) return cpu::zero(list);
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    mt_fill_zero(P.L, dtype_of(g[0][0]), cur_stream());
+  });
+}
+
+std::tuple<at::Tensor, at::Tensor> mt_norm_op(at::Tensor noop, const std::vector<at::Tensor>& list,
+                                              bool per_tensor, bool max_norm) {
+  TORCH_CHECK(!list.empty(), "multi_tensor norm of an empty list");
+  TensorLists lists{list};
+  bool gpu = mt_validate(lists, 1, 1);
+  auto fopt = at::TensorOptions().dtype(at::kFloat).device(list[0].device());
+  at::Tensor out = at::zeros({1}, fopt);
+  at::Tensor pt = per_tensor ? at::zeros({(int64_t)list.size()}, fopt) : at::empty({0}, fopt);
+  if (!gpu) {
+    cpu::norm(noop, list, max_norm, out, per_tensor ? &pt : nullptr);
+    return {out, pt};
+  }
+  // Mixed dtypes: norms per group, then combined on device.
+  std::vector<at::Tensor> group_globals;
+  by_dtype_groups(lists, [&](const std::vector<int>& idx, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    at::Tensor partials = at::empty({P.L.nchunks}, fopt);
+    at::Tensor gout = at::empty({1}, fopt);
+    at::Tensor gpt = per_tensor ? at::empty({P.L.ntensors}, fopt) : at::Tensor();
+    mt_norm_partials(P.L, dtype_of(g[0][0]), max_norm ? 1 : 0, partials.data_ptr<float>(),
+                     noop_ptr(noop), cur_stream());
+    mt_norm_finalize(P.L, partials.data_ptr<float>(), 1, max_norm ? 1 : 0, gout.data_ptr<float>(),
+                     per_tensor ? gpt.data_ptr<float>() : nullptr, cur_stream());
+    if (per_tensor) {
+      auto index = at::tensor(std::vector<int64_t>(idx.begin(), idx.end()),
+                              at::TensorOptions().dtype(at::kLong)).to(list[0].device(), true);
+      pt.index_copy_(0, index, gpt);
+    }
+    group_globals.push_back(gout);
+  });
+  if (group_globals.size() == 1) {
+    out = group_globals[0];
+  } else {
+    at::Tensor all = at::cat(group_globals);
+    out = max_norm ? all.max().reshape({1}) : all.pow(2).sum().sqrt().reshape({1});
+  }
+  return {out, pt};
+}
+
+void mt_sgd_op(at::Tensor noop, const TensorLists& lists, double wd, double momentum,
+               double dampening, double lr, c10::optional<at::Tensor> lr_t, bool nesterov,
+               bool first_run, c10::optional<at::Tensor> first_run_flag, bool wd_after_momentum,
+               double scale, c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  if (lists.empty() || lists[0].empty()) return;
+  bool gpu = mt_validate(lists, 3, 4);
+  if (!gpu) {
+    TORCH_CHECK(!lr_t.has_value() || !lr_t->defined(), "device lr only on GPU");
+    cpu::Sgd a{(float)wd, (float)momentum, (float)dampening, (float)lr, nesterov, first_run,
+               wd_after_momentum, cscale(scale, scale_t, scale_inv), optp(first_run_flag)};
+    return cpu::sgd(noop, lists, a);
+  }
+  SgdArgs a;
+  a.wd = (float)wd;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.lr = (float)lr;
+  a.nesterov = nesterov;
+  a.first_run = first_run;
+  a.wd_after_momentum = wd_after_momentum;
+  a.scale = make_scale(scale, scale_t, scale_inv);
+  a.lr_ptr = opt_fptr(lr_t);
+  a.first_run_flag = opt_iptr(first_run_flag);
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    DType copy = g.size() == 4 ? dtype_of(g[3][0]) : dtype_of(g[1][0]);
+    mt_sgd(P.L, (int)g.size(), dtype_of(g[0][0]), dtype_of(g[1][0]), dtype_of(g[2][0]), copy, a,
+           noop_ptr(noop), cur_stream());
+  });
+}
+
+void mt_adam_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optional<at::Tensor> lr_t,
+                double beta1, double beta2, double eps, int64_t step,
+                c10::optional<at::Tensor> step_t, int64_t mode, bool bias_correction, double wd,
+                double scale, c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  if (lists.empty() || lists[0].empty()) return;
+  bool gpu = mt_validate(lists, 4, 5);
+  if (!gpu) {
+    cpu::Adam a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (int)step,
+                optp(step_t), (int)mode, bias_correction ? 1 : 0, cscale(scale, scale_t, scale_inv)};
+    return cpu::adam(noop, lists, a);
+  }
+  AdamArgs a;
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.wd = (float)wd;
+  a.step = (int)step;
+  a.step_ptr = opt_iptr(step_t);
+  a.mode = (int)mode;
+  a.bias_correction = bias_correction ? 1 : 0;
+  a.scale = make_scale(scale, scale_t, scale_inv);
+  a.lr_ptr = opt_fptr(lr_t);
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    TORCH_CHECK(g[2][0].scalar_type() == g[1][0].scalar_type() &&
+                    g[3][0].scalar_type() == g[1][0].scalar_type(),
+                "adam: exp_avg / exp_avg_sq must match the parameter dtype");
+    const MTPlan& P = mt_plan(g);
+    DType copy = g.size() == 5 ? dtype_of(g[4][0]) : dtype_of(g[1][0]);
+    mt_adam(P.L, (int)g.size(), dtype_of(g[0][0]), dtype_of(g[1][0]), copy, a, noop_ptr(noop),
+            cur_stream());
+  });
+}
+
+void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optional<at::Tensor> lr_t,
+                double beta1, double beta2, double eps, int64_t step,
+                c10::optional<at::Tensor> step_t, bool bias_correction, double wd,
+                bool grad_averaging, int64_t mode, c10::optional<at::Tensor> global_grad_norm,
+                double max_grad_norm, bool use_nvlamb, double scale,
+                c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  if (lists.empty() || lists[0].empty()) return;
+  // lists: [g, p, m, v, u] or [g, p, m, v, u, p_copy]; u is an fp32 workspace
+  bool gpu = mt_validate(lists, 5, 6);
+  if (!gpu) {
+    cpu::Lamb a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (int)step,
+                optp(step_t), (int)mode, bias_correction ? 1 : 0, grad_averaging ? 1 : 0,
+                optp(global_grad_norm), (float)max_grad_norm, use_nvlamb,
+                cscale(scale, scale_t, scale_inv)};
+    return cpu::lamb(noop, lists, a);
+  }
+  LambArgs a;
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.wd = (float)wd;
+  a.step = (int)step;
+  a.step_ptr = opt_iptr(step_t);
+  a.mode = (int)mode;
+  a.bias_correction = bias_correction ? 1 : 0;
+  a.grad_averaging = grad_averaging ? 1 : 0;
+  a.global_grad_norm = opt_fptr(global_grad_norm);
+  a.max_grad_norm = (float)max_grad_norm;
+  a.use_nvlamb = use_nvlamb ? 1 : 0;
+  a.scale = make_scale(scale, scale_t, scale_inv);
+  a.lr_ptr = opt_fptr(lr_t);
+  auto fopt = at::TensorOptions().dtype(at::kFloat).device(lists[0][0].device());
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    for (size_t i = 0; i < g[4].size(); ++i)
+      TORCH_CHECK(g[4][i].scalar_type() == at::kFloat, "lamb: update workspace must be fp32");
+    TensorLists s1 = sub(g, {0, 1, 2, 3, 4});
+    const MTPlan& P1 = mt_plan(s1);
+    at::Tensor partials = at::empty({2 * (int64_t)P1.L.nchunks}, fopt);
+    at::Tensor norms = at::empty({2 * (int64_t)P1.L.ntensors}, fopt);
+    mt_lamb_stage1(P1.L, dtype_of(g[0][0]), dtype_of(g[1][0]), a, partials.data_ptr<float>(),
+                   noop_ptr(noop), cur_stream());
+    mt_norm_finalize(P1.L, partials.data_ptr<float>(), 2, 0, nullptr, norms.data_ptr<float>(),
+                     cur_stream());
+    TensorLists s2 = g.size() == 6 ? sub(g, {1, 4, 5}) : sub(g, {1, 4});
+    const MTPlan& P2 = mt_plan(s2);
+    DType copy = g.size() == 6 ? dtype_of(g[5][0]) : dtype_of(g[1][0]);
+    mt_lamb_stage2(P2.L, (int)s2.size(), dtype_of(g[1][0]), copy, a, norms.data_ptr<float>(),
+                   norms.data_ptr<float>() + P1.L.ntensors, noop_ptr(noop), cur_stream());
+  });
+}
+
+void mt_novograd_op(at::Tensor noop, const TensorLists& lists, at::Tensor v, at::Tensor grad_norms,
+                    bool first_step, double lr, c10::optional<at::Tensor> lr_t, double beta1,
+                    double beta2, double eps, int64_t step, c10::optional<at::Tensor> step_t,
+                    bool bias_correction, double wd, bool grad_averaging, int64_t mode,
+                    int64_t norm_type, double scale, c10::optional<at::Tensor> scale_t,
+                    bool scale_inv) {
+  if (lists.empty() || lists[0].empty()) return;
+  bool gpu = mt_validate(lists, 3, 3);
+  if (!gpu) {
+    cpu::Novo a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (int)step,
+                optp(step_t), (int)mode, bias_correction ? 1 : 0, grad_averaging ? 1 : 0,
+                (int)norm_type, cscale(scale, scale_t, scale_inv)};
+    return cpu::novograd(noop, lists, v, grad_norms, first_step, a);
+  }
+  TORCH_CHECK(v.is_cuda() && v.scalar_type() == at::kFloat && v.numel() == (int64_t)lists[0].size(),
+              "novograd: v must be a float32 device tensor with one entry per parameter");
+  NovoArgs a;
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.wd = (float)wd;
+  a.step = (int)step;
+  a.step_ptr = opt_iptr(step_t);
+  a.mode = (int)mode;
+  a.bias_correction = bias_correction ? 1 : 0;
+  a.grad_averaging = grad_averaging ? 1 : 0;
+  a.norm_type = (int)norm_type;
+  a.init_zero = 0.f;
+  a.scale = make_scale(scale, scale_t, scale_inv);
+  a.lr_ptr = opt_fptr(lr_t);
+  // grad_norms are unscaled norms of the (scaled) grads -> fold scale in on host side by caller.
+  novograd_blend(v.data_ptr<float>(), grad_norms.data_ptr<float>(), (int)v.numel(), a.beta2,
+                 a.norm_type, first_step ? 1 : 0, noop_ptr(noop), cur_stream());
+  // A single dtype group is required here because v is indexed by tensor position.
+  const MTPlan& P = mt_plan(lists);
+  for (size_t i = 1; i < lists[0].size(); ++i) {
+    TORCH_CHECK(lists[0][i].scalar_type() == lists[0][0].scalar_type() &&
+                    lists[1][i].scalar_type() == lists[1][0].scalar_type(),
+                "novograd: one dtype per launch");
+  }
+  mt_novograd(P.L, dtype_of(lists[0][0]), dtype_of(lists[1][0]), a, v.data_ptr<float>(),
+              noop_ptr(noop), cur_stream());
+}
+
+void mt_adagrad_op(at::Tensor noop, const TensorLists& lists, double lr,
+                   c10::optional<at::Tensor> lr_t, double eps, int64_t mode, double wd,
+                   double scale, c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  if (lists.empty() || lists[0].empty()) return;
+  bool gpu = mt_validate(lists, 3, 3);
+  if (!gpu) {
+    cpu::Adagrad a{(float)lr, (float)eps, (float)wd, (int)mode, cscale(scale, scale_t, scale_inv)};
+    return cpu::adagrad(noop, lists, a);
+  }
+  AdagradArgs a;
+  a.lr = (float)lr;
+  a.eps = (float)eps;
+  a.wd = (float)wd;
+  a.mode = (int)mode;
+  a.scale = make_scale(scale, scale_t, scale_inv);
+  a.lr_ptr = opt_fptr(lr_t);
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    mt_adagrad(P.L, dtype_of(g[0][0]), dtype_of(g[1][0]), a, noop_ptr(noop), cur_stream());
+  });
+}
+
+void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, c10::optional<at::Tensor> skipped,
+                          at::Tensor overflow, double factor, int64_t window, double min_scale,
+                          double max_scale, bool dynamic) {
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && unskipped.scalar_type() == at::kInt &&
+                  overflow.scalar_type() == at::kInt,
+              "update_loss_scale: bad dtypes");
+  if (!scale.is_cuda()) {
+    return cpu::update_loss_scale(scale, unskipped, optp(skipped), overflow, (float)factor,
+                                  (int)window, (float)min_scale, (float)max_scale, dynamic);
+  }
+  update_loss_scale(scale.data_ptr<float>(), unskipped.data_ptr<int>(), opt_iptr(skipped),
+                    overflow.data_ptr<int>(), (float)factor, (int)window, (float)min_scale,
+                    (float)max_scale, dynamic ? 1 : 0, cur_stream());
+}
+
+void advance_step_op(at::Tensor step, c10::optional<at::Tensor> noop) {
+  TORCH_CHECK(step.scalar_type() == at::kInt, "step counter must be int32");
+  if (!step.is_cuda()) {
+    bool skip = noop.has_value() && noop->defined() && noop->item<int>() != 0;
+    if (!skip) step.add_(1);
+    return;
+  }
+  advance_step(step.data_ptr<int>(), opt_iptr(noop), cur_stream());
+}
+
+void mark_step_done_op(at::Tensor flag, c10::optional<at::Tensor> noop) {
+  TORCH_CHECK(flag.scalar_type() == at::kInt, "flag must be int32");
+  if (!flag.is_cuda()) {
+    bool skip = noop.has_value() && noop->defined() && noop->item<int>() != 0;
+    if (!skip) flag.fill_(1);
+    return;
+  }
+  mark_step_done(flag.data_ptr<int>(), opt_iptr(noop), cur_stream());
+}
+
+void flat_scale_op(at::Tensor in, at::Tensor out, double scale, c10::optional<at::Tensor> scale_t,
+                   bool invert, c10::optional<at::Tensor> noop) {
+  TORCH_CHECK(in.is_contiguous() && (!out.defined() || out.is_contiguous()), "contiguous only");
+  if (!in.is_cuda()) {
+    float s = (float)scale;
+    if (scale_t.has_value() && scale_t->defined()) s = scale_t->item<float>();
+    if (invert) s = 1.f / s;
+    if (noop.has_value() && noop->defined() && !at::isfinite(in).all().item<bool>()) noop->fill_(1);
+    if (out.defined()) out.copy_(in.to(at::kFloat) * s);
+    return;
+  }
+  flat_scale(in.data_ptr(), dtype_of(in), out.defined() ? out.data_ptr() : nullptr,
+             out.defined() ? dtype_of(out) : dtype_of(in), in.numel(),
+             make_scale(scale, scale_t, invert), opt_iptr(noop), cur_stream());
+}
+
+}  // namespace amd

@@ -1,0 +1,51 @@
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/util/Optional.h>
+
+#include <tuple>
+#include <vector>
+
+namespace amd {
+
+using TensorLists = std::vector<std::vector<at::Tensor>>;
+using OptT = c10::optional<at::Tensor>;
+
+void mt_scale_op(at::Tensor noop, const TensorLists& lists, double scale, OptT scale_t, bool invert);
+void mt_scale_any_op(at::Tensor noop, const TensorLists& lists, double scale, OptT scale_t,
+                     bool invert);
+void mt_check_finite_op(at::Tensor noop, const std::vector<at::Tensor>& list);
+void mt_axpby_op(at::Tensor noop, const TensorLists& lists, double a, OptT a_t, bool a_inv,
+                 double b, OptT b_t, bool b_inv, int64_t arg_to_check);
+void mt_zero_op(const std::vector<at::Tensor>& list);
+std::tuple<at::Tensor, at::Tensor> mt_norm_op(at::Tensor noop, const std::vector<at::Tensor>& list,
+                                              bool per_tensor, bool max_norm);
+void mt_sgd_op(at::Tensor noop, const TensorLists& lists, double wd, double momentum,
+               double dampening, double lr, OptT lr_t, bool nesterov, bool first_run,
+               OptT first_run_flag, bool wd_after_momentum, double scale, OptT scale_t,
+               bool scale_inv);
+void mt_adam_op(at::Tensor noop, const TensorLists& lists, double lr, OptT lr_t, double beta1,
+                double beta2, double eps, int64_t step, OptT step_t, int64_t mode,
+                bool bias_correction, double wd, double scale, OptT scale_t, bool scale_inv);
+void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, OptT lr_t, double beta1,
+                double beta2, double eps, int64_t step, OptT step_t, bool bias_correction,
+                double wd, bool grad_averaging, int64_t mode, OptT global_grad_norm,
+                double max_grad_norm, bool use_nvlamb, double scale, OptT scale_t, bool scale_inv);
+void mt_novograd_op(at::Tensor noop, const TensorLists& lists, at::Tensor v, at::Tensor grad_norms,
+                    bool first_step, double lr, OptT lr_t, double beta1, double beta2, double eps,
+                    int64_t step, OptT step_t, bool bias_correction, double wd,
+                    bool grad_averaging, int64_t mode, int64_t norm_type, double scale,
+                    OptT scale_t, bool scale_inv);
+void mt_adagrad_op(at::Tensor noop, const TensorLists& lists, double lr, OptT lr_t, double eps,
+                   int64_t mode, double wd, double scale, OptT scale_t, bool scale_inv);
+void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, OptT skipped, at::Tensor overflow,
+                          double factor, int64_t window, double min_scale, double max_scale,
+                          bool dynamic);
+void advance_step_op(at::Tensor step, OptT noop);
+void mark_step_done_op(at::Tensor flag, OptT noop);
+void flat_scale_op(at::Tensor in, at::Tensor out, double scale, OptT scale_t, bool invert,
+                   OptT noop);
+
+void mt_plan_cache_clear();
+int64_t mt_plan_cache_size();
+
+}  // namespace amd

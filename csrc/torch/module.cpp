@@ -1,0 +1,79 @@
+// Python module `apex_example_amd._C`.
+//
+// Submodules mirror the Apex extension names so the Python layer can expose
+// drop-in facades: amp_C (multi-tensor ops), apex_C (flatten/unflatten),
+// fused_layer_norm_cuda, syncbn, plus `reducer` (the DDP core).
+#include <torch/extension.h>
+
+#include "amp_ops.h"
+#include "norm_ops.h"
+#include "reducer.h"
+
+namespace py = pybind11;
+using namespace amd;
+
+static at::Tensor flatten_dense(const std::vector<at::Tensor>& ts) {
+  std::vector<at::Tensor> flat;
+  flat.reserve(ts.size());
+  for (auto& t : ts) flat.push_back(t.contiguous().view({-1}));
+  if (flat.empty()) return at::empty({0});
+  return at::cat(flat);
+}
+
+static std::vector<at::Tensor> unflatten_dense(const at::Tensor& flat,
+                                               const std::vector<at::Tensor>& like) {
+  std::vector<at::Tensor> out;
+  out.reserve(like.size());
+  int64_t off = 0;
+  for (auto& t : like) {
+    int64_t n = t.numel();
+    out.push_back(flat.narrow(0, off, n).view(t.sizes()));
+    off += n;
+  }
+  return out;
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native kernels for apex_example_amd (gfx950)";
+  m.attr("arch") = "gfx950";
+
+  auto mt = m.def_submodule("mt", "multi-tensor apply ops (device-resident launch tables)");
+  mt.def("scale", &mt_scale_op, py::arg("noop"), py::arg("lists"), py::arg("scale"),
+         py::arg("scale_t") = py::none(), py::arg("invert") = false);
+  mt.def("scale_any", &mt_scale_any_op, py::arg("noop"), py::arg("lists"), py::arg("scale"),
+         py::arg("scale_t") = py::none(), py::arg("invert") = false);
+  mt.def("check_finite", &mt_check_finite_op);
+  mt.def("axpby", &mt_axpby_op);
+  mt.def("zero", &mt_zero_op);
+  mt.def("norm", &mt_norm_op, py::arg("noop"), py::arg("list"), py::arg("per_tensor") = false,
+         py::arg("max_norm") = false);
+  mt.def("sgd", &mt_sgd_op);
+  mt.def("adam", &mt_adam_op);
+  mt.def("lamb", &mt_lamb_op);
+  mt.def("novograd", &mt_novograd_op);
+  mt.def("adagrad", &mt_adagrad_op);
+  mt.def("update_loss_scale", &update_loss_scale_op);
+  mt.def("advance_step", &advance_step_op);
+  mt.def("mark_step_done", &mark_step_done_op);
+  mt.def("flat_scale", &flat_scale_op);
+  mt.def("plan_cache_clear", &mt_plan_cache_clear);
+  mt.def("plan_cache_size", &mt_plan_cache_size);
+
+  auto ac = m.def_submodule("apex_C", "flatten / unflatten (apex_C parity)");
+  ac.def("flatten", &flatten_dense);
+  ac.def("unflatten", &unflatten_dense);
+
+  auto ln = m.def_submodule("layer_norm", "fused LayerNorm / RMSNorm (wave64 row kernels)");
+  ln.def("forward", &layer_norm_forward_op);
+  ln.def("backward", &layer_norm_backward_op);
+
+  auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
+  bn.def("local_stats", &bn_local_stats_op);
+  bn.def("combine_stats", &bn_combine_stats_op);
+  bn.def("apply", &bn_apply_op);
+  bn.def("reduce_grad", &bn_reduce_grad_op);
+  bn.def("backward_elemt", &bn_backward_elemt_op);
+
+  auto rd = m.def_submodule("reducer", "DDP bucketed gradient reducer core");
+  register_reducer(rd);
+}

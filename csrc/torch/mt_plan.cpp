@@ -1,0 +1,181 @@
+// Device-resident multi-tensor launch tables, cached by tensor addresses.
+//
+// A steady-state training loop passes the same parameter / grad / state tensors
+// to the optimizer every step, so the table (TensorDesc[] + ChunkDesc[]) is built
+// and uploaded once and re-used: zero metadata traffic per step, and the launch
+// stays valid under hipGraph capture after one warm-up call.
+#include <cstring>
+#include <list>
+#include <mutex>
+#include <unordered_map>
+
+#include "common.h"
+
+namespace amd {
+
+namespace {
+
+struct Key {
+  std::vector<uint64_t> words;
+  bool operator==(const Key& o) const { return words == o.words; }
+};
+struct KeyHash {
+  size_t operator()(const Key& k) const {
+    uint64_t h = 1469598103934665603ull;
+    for (uint64_t w : k.words) {
+      h ^= w;
+      h *= 1099511628211ull;
+    }
+    return (size_t)h;
+  }
+};
+
+struct Cache {
+  std::mutex mu;
+  std::list<Key> lru;  // front = most recent
+  struct Entry {
+    MTPlan plan;
+    std::list<Key>::iterator pos;
+  };
+  std::unordered_map<Key, Entry, KeyHash> map;
+  static constexpr size_t kMax = 512;
+};
+
+Cache& cache() {
+  static Cache c;
+  return c;
+}
+
+// Same memory order of elements (strides of size-1 dims are irrelevant).
+bool same_layout(const at::Tensor& a, const at::Tensor& b) {
+  if (a.dim() != b.dim()) return a.is_contiguous() && b.is_contiguous();
+  for (int64_t k = 0; k < a.dim(); ++k) {
+    if (a.size(k) != b.size(k)) return false;
+    if (a.size(k) > 1 && a.stride(k) != b.stride(k)) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+bool mt_validate(const TensorLists& lists, int min_depth, int max_depth) {
+  TORCH_CHECK((int)lists.size() >= min_depth && (int)lists.size() <= max_depth,
+              "expected between ", min_depth, " and ", max_depth, " tensor lists, got ",
+              lists.size());
+  const size_t n = lists[0].size();
+  bool on_gpu = false;
+  bool first = true;
+  for (size_t d = 0; d < lists.size(); ++d) {
+    TORCH_CHECK(lists[d].size() == n, "tensor list ", d, " has ", lists[d].size(),
+                " tensors, expected ", n);
+    for (size_t i = 0; i < n; ++i) {
+      const at::Tensor& t = lists[d][i];
+      // Elementwise ops only need a dense block whose element order matches across
+      // the lists: contiguous, or e.g. channels_last weights with identical strides
+      // in every slot (grads, masters and state are created with preserved format).
+      TORCH_CHECK(t.is_non_overlapping_and_dense() && same_layout(t, lists[0][i]),
+                  "multi_tensor ops need dense tensors with matching strides (list ", d,
+                  ", index ", i, ")");
+      TORCH_CHECK(t.numel() == lists[0][i].numel(), "size mismatch at list ", d, " index ", i);
+      if (first) {
+        on_gpu = t.is_cuda();
+        first = false;
+      } else {
+        TORCH_CHECK(t.is_cuda() == on_gpu, "all tensors must be on the same device type");
+      }
+    }
+  }
+  return on_gpu;
+}
+
+const MTPlan& mt_plan(const TensorLists& lists) {
+  const int depth = (int)lists.size();
+  const int n = (int)lists[0].size();
+  TORCH_CHECK(depth <= kMaxDepth, "depth > kMaxDepth");
+  Key key;
+  key.words.reserve(2 + (size_t)n * (depth + 1));
+  key.words.push_back((uint64_t)depth);
+  key.words.push_back((uint64_t)n);
+  for (int i = 0; i < n; ++i) {
+    key.words.push_back((uint64_t)lists[0][i].numel());
+    for (int d = 0; d < depth; ++d) key.words.push_back((uint64_t)lists[d][i].data_ptr());
+  }
+  Cache& c = cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  auto it = c.map.find(key);
+  if (it != c.map.end()) {
+    c.lru.splice(c.lru.begin(), c.lru, it->second.pos);
+    return it->second.plan;
+  }
+
+  // Build the host image.
+  std::vector<TensorDesc> tds((size_t)n);
+  std::vector<ChunkDesc> chunks;
+  for (int i = 0; i < n; ++i) {
+    TensorDesc& td = tds[(size_t)i];
+    std::memset(&td, 0, sizeof(td));
+    td.numel = lists[0][i].numel();
+    int aligned = 1;
+    for (int d = 0; d < depth; ++d) {
+      void* p = lists[d][i].data_ptr();
+      td.ptr[d] = p;
+      if (((uintptr_t)p) % 16 != 0) aligned = 0;
+    }
+    td.aligned = aligned;
+    td.first_chunk = (int32_t)chunks.size();
+    int64_t nch = (td.numel + kTile - 1) / kTile;
+    for (int64_t k = 0; k < nch; ++k) chunks.push_back(ChunkDesc{i, (int32_t)k});
+  }
+  TORCH_CHECK(chunks.size() < (size_t)INT32_MAX, "too many chunks");
+  const size_t tbytes = tds.size() * sizeof(TensorDesc);
+  const size_t cbytes = chunks.size() * sizeof(ChunkDesc);
+  const size_t coff = (tbytes + 255) / 256 * 256;
+  const size_t total = coff + cbytes + 16;
+
+  auto dev = lists[0][0].device();
+  at::Tensor host = at::empty({(int64_t)total}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  uint8_t* hp = host.data_ptr<uint8_t>();
+  std::memset(hp, 0, total);
+  if (tbytes) std::memcpy(hp, tds.data(), tbytes);
+  if (cbytes) std::memcpy(hp + coff, chunks.data(), cbytes);
+  at::Tensor table = at::empty({(int64_t)total}, at::TensorOptions().dtype(at::kByte).device(dev));
+  table.copy_(host, /*non_blocking=*/true);
+
+  MTPlan plan;
+  plan.table = table;
+  uint8_t* base = table.data_ptr<uint8_t>();
+  plan.L.tensors = reinterpret_cast<const TensorDesc*>(base);
+  plan.L.chunks = reinterpret_cast<const ChunkDesc*>(base + coff);
+  plan.L.ntensors = n;
+  plan.L.nchunks = (int32_t)chunks.size();
+
+  if (c.map.size() >= Cache::kMax) {
+    // Evict the least recently used table; kernels that may still read it run on
+    // the current stream, so tie its lifetime to that stream.
+    const Key& old = c.lru.back();
+    auto oit = c.map.find(old);
+    if (oit != c.map.end()) {
+      oit->second.plan.table.record_stream(c10::hip::getCurrentHIPStream());
+      c.map.erase(oit);
+    }
+    c.lru.pop_back();
+  }
+  c.lru.push_front(key);
+  auto res = c.map.emplace(key, Cache::Entry{plan, c.lru.begin()});
+  return res.first->second.plan;
+}
+
+void mt_plan_cache_clear() {
+  Cache& c = cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  c.map.clear();
+  c.lru.clear();
+}
+
+int64_t mt_plan_cache_size() {
+  Cache& c = cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  return (int64_t)c.map.size();
+}
+
+}  // namespace amd

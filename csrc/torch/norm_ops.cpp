@@ -1,0 +1,300 @@
+// LayerNorm and BatchNorm operators: geometry, allocation, CPU/GPU dispatch.
+#include "norm_ops.h"
+
+#include "common.h"
+
+namespace amd {
+
+namespace {
+const void* optp(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+bool has(const OptT& t) { return t.has_value() && t->defined(); }
+}  // namespace
+
+// ============================================================================ LayerNorm
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_forward_op(at::Tensor x, int64_t n2,
+                                                                     OptT gamma, OptT beta,
+                                                                     double eps, bool rms) {
+  x = x.contiguous();
+  TORCH_CHECK(n2 > 0 && x.numel() % n2 == 0, "layer_norm: bad normalized size");
+  const int64_t n1 = x.numel() / n2;
+  auto fopt = x.options().dtype(at::kFloat);
+  if (!x.is_cuda()) {
+    at::Tensor xf = x.to(at::kFloat).view({n1, n2});
+    at::Tensor mean = rms ? at::zeros({n1}, fopt) : xf.mean(1);
+    at::Tensor xc = rms ? xf : xf - mean.unsqueeze(1);
+    at::Tensor var = xc.pow(2).mean(1);
+    at::Tensor invvar = (var + eps).rsqrt();
+    at::Tensor y = xc * invvar.unsqueeze(1);
+    if (has(gamma)) y = y * gamma->to(at::kFloat).view({1, n2});
+    if (has(beta)) y = y + beta->to(at::kFloat).view({1, n2});
+    return {y.to(x.scalar_type()).view(x.sizes()), mean, invvar};
+  }
+  at::Tensor g = has(gamma) ? gamma->contiguous() : at::Tensor();
+  at::Tensor b = has(beta) ? beta->contiguous() : at::Tensor();
+  if (g.defined() && b.defined())
+    TORCH_CHECK(g.scalar_type() == b.scalar_type(), "gamma/beta dtype mismatch");
+  at::Tensor y = at::empty_like(x);
+  at::Tensor mean = at::empty({n1}, fopt);
+  at::Tensor invvar = at::empty({n1}, fopt);
+  DType tw = g.defined() ? dtype_of(g) : (b.defined() ? dtype_of(b) : DType::F32);
+  layer_norm_fwd(x.data_ptr(), dtype_of(x), g.defined() ? g.data_ptr() : nullptr,
+                 b.defined() ? b.data_ptr() : nullptr, tw, y.data_ptr(), mean.data_ptr<float>(),
+                 invvar.data_ptr<float>(), n1, n2, (float)eps, rms ? 1 : 0, cur_stream());
+  return {y, mean, invvar};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_backward_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
+    bool need_wgrad, bool need_bgrad, bool rms) {
+  x = x.contiguous();
+  dy = dy.contiguous();
+  const int64_t n1 = x.numel() / n2;
+  if (!x.is_cuda()) {
+    at::Tensor xf = x.to(at::kFloat).view({n1, n2});
+    at::Tensor df = dy.to(at::kFloat).view({n1, n2});
+    at::Tensor xh = (rms ? xf : xf - mean.unsqueeze(1)) * invvar.unsqueeze(1);
+    at::Tensor dg = has(gamma) ? df * gamma->to(at::kFloat).view({1, n2}) : df;
+    at::Tensor s2 = (dg * xh).mean(1, true);
+    at::Tensor t = rms ? dg - xh * s2 : dg - dg.mean(1, true) - xh * s2;
+    at::Tensor dx = (t * invvar.unsqueeze(1)).to(x.scalar_type()).view(x.sizes());
+    at::Tensor dgam, dbet;
+    if (need_wgrad && has(gamma)) dgam = (df * xh).sum(0).to(gamma->scalar_type());
+    if (need_bgrad && has(gamma)) dbet = df.sum(0).to(gamma->scalar_type());
+    return {dx, dgam, dbet};
+  }
+  at::Tensor g = has(gamma) ? gamma->contiguous() : at::Tensor();
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dgam, dbet, part;
+  DType tw = g.defined() ? dtype_of(g) : DType::F32;
+  if (need_wgrad && g.defined()) dgam = at::empty_like(g);
+  if (need_bgrad && g.defined()) dbet = at::empty_like(g);
+  if (dgam.defined() || dbet.defined())
+    part = at::empty({layer_norm_bwd_workspace(n1, n2)}, x.options().dtype(at::kFloat));
+  layer_norm_bwd(dy.data_ptr(), x.data_ptr(), dtype_of(x), g.defined() ? g.data_ptr() : nullptr,
+                 tw, mean.data_ptr<float>(), invvar.data_ptr<float>(), dx.data_ptr(),
+                 dgam.defined() ? dgam.data_ptr() : nullptr,
+                 dbet.defined() ? dbet.data_ptr() : nullptr,
+                 part.defined() ? part.data_ptr<float>() : nullptr, n1, n2, rms ? 1 : 0,
+                 cur_stream());
+  return {dx, dgam, dbet};
+}
+
+// ============================================================================ BatchNorm
+namespace {
+struct BNView {
+  int64_t outer, C, inner;
+  int cl;
+  bool cl4;  // 4-D tensor stored channels_last
+};
+
+BNView bn_view(const at::Tensor& x) {
+  TORCH_CHECK(x.dim() >= 2, "batch norm expects [N, C, ...]");
+  BNView v;
+  const int64_t N = x.size(0), C = x.size(1);
+  int64_t HW = 1;
+  for (int64_t d = 2; d < x.dim(); ++d) HW *= x.size(d);
+  v.C = C;
+  v.cl4 = false;
+  if (HW == 1) {
+    v.outer = N;
+    v.inner = 1;
+    v.cl = 1;
+  } else if (x.dim() == 4 && !x.is_contiguous() &&
+             x.is_contiguous(at::MemoryFormat::ChannelsLast)) {
+    v.outer = N * HW;
+    v.inner = 1;
+    v.cl = 1;
+    v.cl4 = true;
+  } else {
+    v.outer = N;
+    v.inner = HW;
+    v.cl = 0;
+  }
+  return v;
+}
+
+at::Tensor conform(const at::Tensor& t, const BNView& v) {
+  return v.cl4 ? t.contiguous(at::MemoryFormat::ChannelsLast) : t.contiguous();
+}
+
+std::vector<int64_t> reduce_dims(const at::Tensor& x) {
+  std::vector<int64_t> d{0};
+  for (int64_t i = 2; i < x.dim(); ++i) d.push_back(i);
+  return d;
+}
+
+at::Tensor chan(const at::Tensor& t, int64_t dim) {
+  std::vector<int64_t> shape((size_t)dim, 1);
+  shape[1] = t.numel();
+  return t.view(shape);
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> bn_local_stats_op(at::Tensor x) {
+  BNView v = bn_view(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  if (!x.is_cuda()) {
+    at::Tensor xf = x.to(at::kFloat);
+    auto dims = reduce_dims(x);
+    at::Tensor mean = xf.mean(dims);
+    at::Tensor var = xf.var(dims, /*unbiased=*/false);
+    return {mean, var};
+  }
+  x = conform(x, v);
+  at::Tensor mean = at::empty({v.C}, fopt), var = at::empty({v.C}, fopt);
+  at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
+  bn_local_stats(x.data_ptr(), dtype_of(x), v.outer, v.C, v.inner, v.cl, mean.data_ptr<float>(),
+                 var.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+  return {mean, var};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor means,
+                                                                   at::Tensor vars,
+                                                                   at::Tensor counts, double eps,
+                                                                   double momentum,
+                                                                   OptT running_mean,
+                                                                   OptT running_var) {
+  means = means.contiguous().to(at::kFloat);
+  vars = vars.contiguous().to(at::kFloat);
+  counts = counts.contiguous().to(at::kFloat);
+  const int64_t world = means.dim() == 1 ? 1 : means.size(0);
+  const int64_t C = means.size(-1);
+  const bool rs = has(running_mean) && has(running_var);
+  const bool fast_rs = !rs || (running_mean->scalar_type() == at::kFloat &&
+                               running_var->scalar_type() == at::kFloat &&
+                               running_mean->is_contiguous() && running_var->is_contiguous());
+  if (!means.is_cuda() || !fast_rs) {
+    at::Tensor m2 = means.view({world, C}), v2 = vars.view({world, C});
+    at::Tensor n = counts.view({world, 1});
+    at::Tensor N = n.sum();
+    at::Tensor mean = (m2 * n).sum(0) / N;
+    at::Tensor M2 = (v2 * n).sum(0) + ((m2 - mean.unsqueeze(0)).pow(2) * n).sum(0);
+    at::Tensor var_b = M2 / N;
+    at::Tensor invstd = (var_b + eps).rsqrt();
+    if (rs) {
+      at::Tensor unb = at::where(N > 1, M2 / (N - 1), var_b);
+      c10::NoGradGuard ng;
+      running_mean->mul_(1.0 - momentum).add_(mean.to(running_mean->scalar_type()), momentum);
+      running_var->mul_(1.0 - momentum).add_(unb.to(running_var->scalar_type()), momentum);
+    }
+    return {mean, invstd, var_b};
+  }
+  auto fopt = means.options();
+  at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), var = at::empty({C}, fopt);
+  bn_combine_stats(means.data_ptr<float>(), vars.data_ptr<float>(), counts.data_ptr<float>(),
+                   (int)world, C, (float)eps, (float)momentum, mean.data_ptr<float>(),
+                   invstd.data_ptr<float>(), rs ? running_mean->data_ptr<float>() : nullptr,
+                   DType::F32, rs ? running_var->data_ptr() : nullptr, var.data_ptr<float>(),
+                   cur_stream());
+  return {mean, invstd, var};
+}
+
+at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+                       OptT z, bool relu) {
+  BNView v = bn_view(x);
+  if (!x.is_cuda()) {
+    const int64_t d = x.dim();
+    at::Tensor sc = invstd * (has(weight) ? weight->to(at::kFloat) : at::ones_like(invstd));
+    at::Tensor sh = (has(bias) ? bias->to(at::kFloat) : at::zeros_like(mean)) - mean * sc;
+    at::Tensor y = x.to(at::kFloat) * chan(sc, d) + chan(sh, d);
+    if (has(z)) y = y + z->to(at::kFloat);
+    if (relu) y = y.clamp_min(0);
+    return y.to(x.scalar_type());
+  }
+  x = conform(x, v);
+  at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
+  at::Tensor y = at::empty_like(x);
+  DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
+  at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
+  at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
+  bn_apply(x.data_ptr(), dtype_of(x), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+           w.defined() ? w.data_ptr() : nullptr, b.defined() ? b.data_ptr() : nullptr, tw,
+           zc.defined() ? zc.data_ptr() : nullptr, y.data_ptr(), v.outer, v.C, v.inner, v.cl,
+           relu ? 1 : 0, cur_stream());
+  return y;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+    OptT z, bool relu, bool need_wgrad) {
+  BNView v = bn_view(x);
+  if (!x.is_cuda()) {
+    const int64_t d = x.dim();
+    at::Tensor xf = x.to(at::kFloat), df = dy.to(at::kFloat);
+    if (relu) {
+      at::Tensor y = bn_apply_op(x, mean, invstd, weight, bias, z, false).to(at::kFloat);
+      df = df * (y > 0).to(at::kFloat);
+    }
+    auto dims = reduce_dims(x);
+    at::Tensor sum_dy = df.sum(dims);
+    at::Tensor sum_dy_xmu = (df * (xf - chan(mean, d))).sum(dims);
+    at::Tensor gw, gb;
+    if (need_wgrad && has(weight)) {
+      gw = (sum_dy_xmu * invstd).to(weight->scalar_type());
+      gb = sum_dy.to(weight->scalar_type());
+    }
+    return {sum_dy, sum_dy_xmu, gw, gb};
+  }
+  x = conform(x, v);
+  dy = conform(dy, v);
+  at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor sum_dy = at::empty({v.C}, fopt), sum_dy_xmu = at::empty({v.C}, fopt);
+  at::Tensor gw, gb;
+  DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
+  if (need_wgrad && has(weight)) {
+    gw = at::empty_like(*weight);
+    gb = at::empty_like(*weight);
+  }
+  at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
+  at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
+  at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
+  bn_reduce_grad(dy.data_ptr(), x.data_ptr(), dtype_of(x), mean.data_ptr<float>(),
+                 invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
+                 b.defined() ? b.data_ptr() : nullptr, tw, relu ? 1 : 0,
+                 zc.defined() ? zc.data_ptr() : nullptr, v.outer, v.C, v.inner, v.cl,
+                 sum_dy.data_ptr<float>(), sum_dy_xmu.data_ptr<float>(),
+                 gw.defined() ? gw.data_ptr() : nullptr, gb.defined() ? gb.data_ptr() : nullptr,
+                 ws.data_ptr<float>(), cur_stream());
+  return {sum_dy, sum_dy_xmu, gw, gb};
+}
+
+std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tensor x,
+                                                        at::Tensor mean, at::Tensor invstd,
+                                                        OptT weight, OptT bias, at::Tensor sum_dy,
+                                                        at::Tensor sum_dy_xmu, double count,
+                                                        OptT z, bool relu, bool want_dz) {
+  BNView v = bn_view(x);
+  if (!x.is_cuda()) {
+    const int64_t d = x.dim();
+    at::Tensor xf = x.to(at::kFloat), df = dy.to(at::kFloat);
+    if (relu) {
+      at::Tensor y = bn_apply_op(x, mean, invstd, weight, bias, z, false).to(at::kFloat);
+      df = df * (y > 0).to(at::kFloat);
+    }
+    at::Tensor w = has(weight) ? weight->to(at::kFloat) : at::ones_like(invstd);
+    at::Tensor mdy = sum_dy / count, mdyx = sum_dy_xmu / count;
+    at::Tensor dx = (df - chan(mdy, d) - (xf - chan(mean, d)) * chan(invstd * invstd * mdyx, d)) *
+                    chan(invstd * w, d);
+    at::Tensor dz = want_dz ? df.to(x.scalar_type()) : at::Tensor();
+    return {dx.to(x.scalar_type()), dz};
+  }
+  x = conform(x, v);
+  dy = conform(dy, v);
+  at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dz = want_dz ? at::empty_like(x) : at::Tensor();
+  DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
+  at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
+  at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
+  bn_backward_elemt(dy.data_ptr(), x.data_ptr(), dtype_of(x), mean.data_ptr<float>(),
+                    invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
+                    b.defined() ? b.data_ptr() : nullptr, tw, sum_dy.data_ptr<float>(),
+                    sum_dy_xmu.data_ptr<float>(), (float)(1.0 / count), relu ? 1 : 0,
+                    zc.defined() ? zc.data_ptr() : nullptr, dx.data_ptr(),
+                    dz.defined() ? dz.data_ptr() : nullptr, v.outer, v.C, v.inner, v.cl,
+                    cur_stream());
+  return {dx, dz};
+}
+
+}  // namespace amd

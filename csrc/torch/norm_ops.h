@@ -1,0 +1,38 @@
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/util/Optional.h>
+
+#include <tuple>
+
+namespace amd {
+
+using OptT = c10::optional<at::Tensor>;
+
+// LayerNorm / RMSNorm over the trailing `n2` elements of x.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_forward_op(at::Tensor x, int64_t n2,
+                                                                     OptT gamma, OptT beta,
+                                                                     double eps, bool rms);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_backward_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
+    bool need_wgrad, bool need_bgrad, bool rms);
+
+// BatchNorm building blocks (local / synchronized).
+std::tuple<at::Tensor, at::Tensor> bn_local_stats_op(at::Tensor x);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor means,
+                                                                   at::Tensor vars,
+                                                                   at::Tensor counts, double eps,
+                                                                   double momentum,
+                                                                   OptT running_mean,
+                                                                   OptT running_var);
+at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+                       OptT z, bool relu);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+    OptT z, bool relu, bool need_wgrad);
+std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tensor x,
+                                                        at::Tensor mean, at::Tensor invstd,
+                                                        OptT weight, OptT bias, at::Tensor sum_dy,
+                                                        at::Tensor sum_dy_xmu, double count,
+                                                        OptT z, bool relu, bool want_dz);
+
+}  // namespace amd

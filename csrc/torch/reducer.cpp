@@ -1,0 +1,412 @@
+// DDP gradient reducer core (apex.parallel.DistributedDataParallel semantics).
+//
+// Behavioural spec: apex@f3a960f8 apex/parallel/distributed.py (SURVEY.md A-14,
+// call stack §3.4).  MI355X-native design:
+//  * gradients live as VIEWS into persistent per-bucket flat buffers
+//    (param.grad aliases the bucket), so apex_C.flatten / unflatten copies and
+//    the multi_tensor_scale "unflatten" pass disappear;
+//  * the grad-ready hook is a C++ post-hook on each parameter's AccumulateGrad
+//    node (no Python, no GIL on the backward critical path);
+//  * a bucket is handed to the process group (RCCL over xGMI on MI355X; gloo on
+//    CPU) the moment it is complete AND every earlier bucket has been launched,
+//    so all ranks issue collectives in the same order; ProcessGroupNCCL runs
+//    them on its own stream, overlapped with the rest of backward;
+//  * averaging uses ncclAvg (ReduceOp::AVG) when possible -> no post-scale pass;
+//  * iteration 1 records the real grad-arrival order, rank 0 broadcasts it
+//    (apex sync_bucket_structure) and the buckets are rebuilt in that order;
+//  * end-of-backward epilogue (engine final callback) makes the compute stream
+//    wait on every bucket's collective and checks that every bucket was reduced.
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/autograd/utils/lambda_post_hook.h>
+#include <torch/csrc/autograd/variable.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/extension.h>
+#include <ATen/record_function.h>
+
+#include <memory>
+#include <mutex>
+
+#include "reducer.h"
+
+namespace amd {
+
+namespace {
+
+struct Bucket {
+  at::ScalarType dtype;
+  std::vector<int64_t> params;
+  std::vector<int64_t> offsets;
+  int64_t numel = 0;
+  at::Tensor flat;
+  at::Tensor comm;
+  int pending = 0;
+  bool launched = false;
+  c10::intrusive_ptr<c10d::Work> work;
+};
+
+class Reducer : public std::enable_shared_from_this<Reducer> {
+ public:
+  Reducer(std::vector<at::Tensor> params, c10::intrusive_ptr<c10d::ProcessGroup> pg,
+          int64_t message_size, bool allreduce_always_fp32, double predivide,
+          bool gradient_average, bool delay_allreduce, bool use_avg_op,
+          std::vector<int64_t> trigger_params, int64_t align)
+      : params_(std::move(params)),
+        pg_(std::move(pg)),
+        message_size_(message_size > 0 ? message_size : 1),
+        fp32_(allreduce_always_fp32),
+        predivide_(predivide),
+        average_(gradient_average),
+        delay_(delay_allreduce),
+        use_avg_(use_avg_op),
+        align_(align > 0 ? align : 1) {
+    world_ = pg_ ? pg_->getSize() : 1;
+    rank_ = pg_ ? pg_->getRank() : 0;
+    for (int64_t t : trigger_params) triggers_.insert(t);
+    std::vector<int64_t> order;
+    for (int64_t i = (int64_t)params_.size() - 1; i >= 0; --i) order.push_back(i);
+    build_layout(order);
+    seen_.assign(params_.size(), 0);
+  }
+
+  ~Reducer() { remove_hooks(); }
+
+  void install_hooks() {
+    std::weak_ptr<Reducer> weak = shared_from_this();
+    for (size_t i = 0; i < params_.size(); ++i) {
+      auto acc = torch::autograd::impl::grad_accumulator(params_[i]);
+      TORCH_CHECK(acc, "parameter ", i, " has no grad accumulator (requires_grad=False?)");
+      const int64_t idx = (int64_t)i;
+      auto key = acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+          [weak, idx](const torch::autograd::variable_list& outputs,
+                      const torch::autograd::variable_list&) {
+            if (auto self = weak.lock()) self->mark_ready(idx);
+            return outputs;
+          }));
+      accs_.push_back(acc);
+      hook_keys_.push_back(key);
+    }
+  }
+
+  void remove_hooks() {
+    for (size_t i = 0; i < accs_.size(); ++i) accs_[i]->del_post_hook(hook_keys_[i]);
+    accs_.clear();
+    hook_keys_.clear();
+  }
+
+  // ---- hook path (autograd engine thread) ---------------------------------
+  void mark_ready(int64_t i) {
+    std::lock_guard<std::mutex> g(mu_);
+    attach_view(i);
+    if (!enabled_) return;
+    if (!callback_queued_) {
+      callback_queued_ = true;
+      std::weak_ptr<Reducer> weak = shared_from_this();
+      torch::autograd::Engine::get_default_engine().queue_callback([weak]() {
+        if (auto self = weak.lock()) self->finalize();
+      });
+    }
+    TORCH_CHECK(!seen_[(size_t)i],
+                "DistributedDataParallel: parameter ", i,
+                " received a gradient twice in one backward pass; use delay_allreduce=True "
+                "(or disable_allreduce()) for multiple backward passes per step");
+    seen_[(size_t)i] = 1;
+    if (refresh_) {
+      arrival_.push_back(i);
+      return;
+    }
+    if (delay_) return;
+    Bucket& b = buckets_[(size_t)bucket_of_[(size_t)i]];
+    b.pending -= 1;
+    while (next_ < (int64_t)buckets_.size() && buckets_[(size_t)next_].pending == 0)
+      launch(next_++);
+  }
+
+  void finalize() {
+    std::lock_guard<std::mutex> g(mu_);
+    callback_queued_ = false;
+    if (!enabled_) return;
+    if (refresh_) {
+      rebuild_from_arrival();
+      for (size_t b = 0; b < buckets_.size(); ++b) launch((int64_t)b);
+      refresh_ = false;
+    } else if (delay_) {
+      for (size_t b = 0; b < buckets_.size(); ++b) launch((int64_t)b);
+    } else if (next_ != (int64_t)buckets_.size()) {
+      std::vector<int64_t> missing;
+      for (size_t i = 0; i < params_.size(); ++i)
+        if (!seen_[i]) missing.push_back((int64_t)i);
+      if (allow_unused_) {
+        // unused parameters keep zero grads in their bucket; launch the rest in order
+        for (int64_t m : missing) {
+          attach_view(m);
+          buckets_[(size_t)bucket_of_[(size_t)m]].pending -= 1;
+        }
+        while (next_ < (int64_t)buckets_.size()) launch(next_++);
+      } else {
+        const int64_t reduced = next_;
+        // drain what was launched so no collective is left dangling
+        for (auto& b : buckets_) complete(b);
+        reset_iteration();
+        TORCH_CHECK(false, "DistributedDataParallel epilogue: only ", reduced, " of ",
+                    buckets_.size(), " buckets were reduced; ", missing.size(),
+                    " parameter(s) received no gradient (first missing index ",
+                    missing.empty() ? -1 : missing[0],
+                    "). Pass allow_unused=True or delay_allreduce=True.");
+      }
+    }
+    for (auto& b : buckets_) complete(b);
+    reset_iteration();
+  }
+
+  // ---- python-facing helpers ---------------------------------------------
+  void set_enabled(bool e) { enabled_ = e; }
+  // apex num_allreduce_streams / allreduce_communicators: bucket b goes to
+  // bucket_pgs[b % n] (separate RCCL communicators -> separate streams).
+  void set_bucket_process_groups(std::vector<c10::intrusive_ptr<c10d::ProcessGroup>> pgs) {
+    std::lock_guard<std::mutex> g(mu_);
+    bucket_pgs_ = std::move(pgs);
+  }
+  bool enabled() const { return enabled_; }
+  void set_allow_unused(bool a) { allow_unused_ = a; }
+  void force_refresh() {
+    std::lock_guard<std::mutex> g(mu_);
+    refresh_ = true;
+  }
+  bool needs_refresh() const { return refresh_; }
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  std::vector<std::vector<int64_t>> layout() const {
+    std::vector<std::vector<int64_t>> r;
+    for (auto& b : buckets_) r.push_back(b.params);
+    return r;
+  }
+  std::vector<at::Tensor> bucket_tensors() const {
+    std::vector<at::Tensor> r;
+    for (auto& b : buckets_) r.push_back(b.flat);
+    return r;
+  }
+  std::vector<int64_t> bucket_numels() const {
+    std::vector<int64_t> r;
+    for (auto& b : buckets_) r.push_back(b.numel);
+    return r;
+  }
+  // Attach every parameter's grad to its bucket view (zeros for missing grads).
+  void attach_all() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < params_.size(); ++i) attach_view((int64_t)i);
+  }
+  // Zero every bucket in one memset per bucket (grads stay views).
+  void zero_grads() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& b : buckets_) b.flat.zero_();
+    for (size_t i = 0; i < params_.size(); ++i) attach_view((int64_t)i);
+  }
+
+ private:
+  at::Tensor view_of(int64_t i) const { return views_[(size_t)i]; }
+
+  void attach_view(int64_t i) {
+    at::Tensor& p = params_[(size_t)i];
+    at::Tensor& grad = p.mutable_grad();
+    const at::Tensor& v = views_[(size_t)i];
+    if (grad.defined() && grad.is_same(v)) return;
+    c10::NoGradGuard ng;
+    if (grad.defined()) v.copy_(grad);
+    else v.zero_();
+    grad = v;
+  }
+
+  void build_layout(const std::vector<int64_t>& order) {
+    std::vector<Bucket> nb;
+    std::vector<int64_t> bucket_of(params_.size(), -1), offset_of(params_.size(), 0);
+    std::map<at::ScalarType, Bucket> open;
+    auto close = [&](at::ScalarType t) {
+      auto it = open.find(t);
+      if (it == open.end() || it->second.params.empty()) return;
+      nb.push_back(std::move(it->second));
+      open.erase(it);
+    };
+    for (int64_t i : order) {
+      const at::Tensor& p = params_[(size_t)i];
+      at::ScalarType t = p.scalar_type();
+      Bucket& b = open[t];
+      b.dtype = t;
+      int64_t off = (b.numel + align_ - 1) / align_ * align_;
+      b.params.push_back(i);
+      b.offsets.push_back(off);
+      b.numel = off + p.numel();
+      if (b.numel >= message_size_ || triggers_.count(i)) close(t);
+    }
+    // close the remaining open buckets in the order of their first parameter
+    std::vector<std::pair<size_t, at::ScalarType>> rest;
+    for (auto& kv : open) {
+      auto pos = std::find(order.begin(), order.end(), kv.second.params.front()) - order.begin();
+      rest.push_back({(size_t)pos, kv.first});
+    }
+    std::sort(rest.begin(), rest.end());
+    for (auto& r : rest) close(r.second);
+
+    std::vector<at::Tensor> new_views(params_.size());
+    for (size_t b = 0; b < nb.size(); ++b) {
+      Bucket& B = nb[b];
+      const at::Tensor& p0 = params_[(size_t)B.params[0]];
+      int64_t padded = (B.numel + align_ - 1) / align_ * align_;
+      B.flat = at::zeros({padded}, p0.options().dtype(B.dtype));
+      for (size_t k = 0; k < B.params.size(); ++k) {
+        int64_t i = B.params[k];
+        const at::Tensor& p = params_[(size_t)i];
+        bucket_of[(size_t)i] = (int64_t)b;
+        offset_of[(size_t)i] = B.offsets[k];
+        // same strides as the parameter (channels_last weights keep their layout)
+        new_views[(size_t)i] = B.flat.as_strided(p.sizes(), p.strides(), B.offsets[k]);
+      }
+      B.pending = (int)B.params.size();
+    }
+    // migrate existing gradients into the new views
+    if (!views_.empty()) {
+      c10::NoGradGuard ng;
+      for (size_t i = 0; i < params_.size(); ++i) {
+        at::Tensor& grad = params_[i].mutable_grad();
+        if (grad.defined()) {
+          new_views[i].copy_(grad);
+          grad = new_views[i];
+        }
+      }
+    }
+    buckets_ = std::move(nb);
+    bucket_of_ = std::move(bucket_of);
+    views_ = std::move(new_views);
+  }
+
+  void rebuild_from_arrival() {
+    std::vector<int64_t> order = arrival_;
+    std::vector<char> in(params_.size(), 0);
+    for (int64_t i : order) in[(size_t)i] = 1;
+    for (int64_t i = (int64_t)params_.size() - 1; i >= 0; --i)
+      if (!in[(size_t)i]) order.push_back(i);
+    if (world_ > 1) {
+      // rank 0's order wins (apex sync_bucket_structure)
+      at::Tensor t = at::tensor(order, at::TensorOptions().dtype(at::kLong));
+      at::Tensor dev_t = t.to(params_[0].device());
+      std::vector<at::Tensor> v{dev_t};
+      c10d::BroadcastOptions opts;
+      opts.rootRank = 0;
+      pg_->broadcast(v, opts)->wait();
+      at::Tensor back = dev_t.cpu();
+      const int64_t* pp = back.data_ptr<int64_t>();
+      order.assign(pp, pp + back.numel());
+    }
+    build_layout(order);
+    arrival_.clear();
+  }
+
+  void launch(int64_t bi) {
+    Bucket& B = buckets_[(size_t)bi];
+    if (B.launched) return;
+    B.launched = true;
+    if (world_ <= 1) return;
+    c10::NoGradGuard ng;
+    if (predivide_ != 1.0) B.flat.mul_(1.0 / predivide_);
+    B.comm = (fp32_ && B.dtype != at::kFloat) ? B.flat.to(at::kFloat) : B.flat;
+    c10d::AllreduceOptions opts;
+    const bool avg = use_avg_ && average_ && predivide_ == 1.0;
+    opts.reduceOp = avg ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
+    std::vector<at::Tensor> v{B.comm};
+    RECORD_FUNCTION("apex_amd::ddp_allreduce_bucket", std::vector<c10::IValue>({B.comm}));
+    auto& pg = (bucket_pgs_.empty()) ? pg_ : bucket_pgs_[(size_t)bi % bucket_pgs_.size()];
+    B.work = pg->allreduce(v, opts);
+  }
+
+  void complete(Bucket& B) {
+    if (!B.launched || world_ <= 1) return;
+    if (B.work) B.work->wait();
+    c10::NoGradGuard ng;
+    const bool avg = use_avg_ && average_ && predivide_ == 1.0;
+    double factor = 1.0;
+    if (!avg && average_) factor = predivide_ / (double)world_;
+    if (!B.comm.is_same(B.flat)) {
+      if (factor != 1.0) B.flat.copy_(B.comm.mul_(factor));
+      else B.flat.copy_(B.comm);
+    } else if (factor != 1.0) {
+      B.flat.mul_(factor);
+    }
+    B.work.reset();
+    B.comm = at::Tensor();
+  }
+
+  void reset_iteration() {
+    for (auto& b : buckets_) {
+      b.pending = (int)b.params.size();
+      b.launched = false;
+      b.work.reset();
+    }
+    next_ = 0;
+    std::fill(seen_.begin(), seen_.end(), 0);
+  }
+
+  std::vector<at::Tensor> params_;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  std::vector<c10::intrusive_ptr<c10d::ProcessGroup>> bucket_pgs_;
+  int64_t message_size_;
+  bool fp32_;
+  double predivide_;
+  bool average_, delay_, use_avg_;
+  int64_t align_;
+  int world_ = 1, rank_ = 0;
+  std::set<int64_t> triggers_;
+
+  std::vector<Bucket> buckets_;
+  std::vector<int64_t> bucket_of_;
+  std::vector<at::Tensor> views_;
+  std::vector<int64_t> arrival_;
+  std::vector<char> seen_;
+  int64_t next_ = 0;
+  bool refresh_ = true;
+  bool enabled_ = true;
+  bool allow_unused_ = false;
+  bool callback_queued_ = false;
+  std::mutex mu_;
+
+  std::vector<std::shared_ptr<torch::autograd::Node>> accs_;
+  std::vector<uintptr_t> hook_keys_;
+};
+
+std::shared_ptr<Reducer> make_reducer(std::vector<at::Tensor> params,
+                                      c10::intrusive_ptr<c10d::ProcessGroup> pg,
+                                      int64_t message_size, bool allreduce_always_fp32,
+                                      double predivide, bool gradient_average,
+                                      bool delay_allreduce, bool use_avg_op,
+                                      std::vector<int64_t> trigger_params, int64_t align) {
+  auto r = std::make_shared<Reducer>(std::move(params), std::move(pg), message_size,
+                                     allreduce_always_fp32, predivide, gradient_average,
+                                     delay_allreduce, use_avg_op, std::move(trigger_params), align);
+  r->install_hooks();
+  return r;
+}
+
+}  // namespace
+
+void register_reducer(pybind11::module_& m) {
+  namespace py = pybind11;
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init(&make_reducer), py::arg("params"), py::arg("process_group"),
+           py::arg("message_size") = 10000000, py::arg("allreduce_always_fp32") = false,
+           py::arg("gradient_predivide_factor") = 1.0, py::arg("gradient_average") = true,
+           py::arg("delay_allreduce") = false, py::arg("use_avg_op") = true,
+           py::arg("trigger_params") = std::vector<int64_t>{}, py::arg("align") = 64)
+      .def("set_enabled", &Reducer::set_enabled)
+      .def("set_bucket_process_groups", &Reducer::set_bucket_process_groups)
+      .def("enabled", &Reducer::enabled)
+      .def("set_allow_unused", &Reducer::set_allow_unused)
+      .def("force_refresh", &Reducer::force_refresh)
+      .def("needs_refresh", &Reducer::needs_refresh)
+      .def("num_buckets", &Reducer::num_buckets)
+      .def("layout", &Reducer::layout)
+      .def("bucket_tensors", &Reducer::bucket_tensors)
+      .def("bucket_numels", &Reducer::bucket_numels)
+      .def("attach_all", &Reducer::attach_all)
+      .def("zero_grads", &Reducer::zero_grads)
+      .def("remove_hooks", &Reducer::remove_hooks);
+}
+
+}  // namespace amd

@@ -1,0 +1,315 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32/fp64 references
+(and against the extension's own C++ CPU path, which is tested separately
+against torch on CPU)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def C():
+    from apex_example_amd import _native
+
+    return _native.require()
+
+
+def _tensors(sizes, dtype, dev=DEV, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return [torch.randn(n, generator=g).to(dev, dtype) for n in sizes]
+
+
+SIZES = [1, 7, 8, 63, 64, 1000, 8191, 8192, 8193, 65536 * 2 + 5, 333333]
+
+
+@pytest.mark.parametrize("tin", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("tout", [torch.float32, torch.float16, torch.bfloat16])
+def test_mt_scale(tin, tout):
+    xs = _tensors(SIZES, tin)
+    ys = [torch.empty(x.numel(), device=DEV, dtype=tout) for x in xs]
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C().mt.scale(noop, [xs, ys], 0.25)
+    torch.cuda.synchronize()
+    assert noop.item() == 0
+    for x, y in zip(xs, ys):
+        torch.testing.assert_close(y.float(), (x.float() * 0.25).to(tout).float(), rtol=0, atol=0)
+
+
+def test_mt_scale_device_scalar_and_overflow():
+    xs = _tensors(SIZES, torch.bfloat16)
+    ys = [torch.empty(x.numel(), device=DEV, dtype=torch.float32) for x in xs]
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    s = torch.tensor([8.0], device=DEV)
+    C().mt.scale(noop, [xs, ys], 1.0, s, True)
+    for x, y in zip(xs, ys):
+        torch.testing.assert_close(y, x.float() / 8.0)
+    assert noop.item() == 0
+    for pos in [0, 8191, 8192, 333332]:
+        xs[-1][pos] = float("inf") if pos % 2 else float("nan")
+        noop.zero_()
+        C().mt.scale(noop, [xs, ys], 1.0)
+        assert noop.item() == 1
+        xs[-1][pos] = 0.0
+
+
+def test_mt_misaligned_views():
+    base = torch.randn(100003, device=DEV)
+    xs = [base[1:5001], base[7:20007], base[3:3]]
+    ys = [torch.empty_like(x) for x in xs]
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C().mt.scale(noop, [xs, ys], 3.0)
+    for x, y in zip(xs, ys):
+        torch.testing.assert_close(y, x * 3)
+
+
+def test_mt_many_tensors_one_launch():
+    xs = _tensors([17 + i for i in range(700)], torch.float32)
+    ys = [torch.empty_like(x) for x in xs]
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C().mt.scale(noop, [xs, ys], -1.0)
+    for x, y in zip(xs, ys):
+        torch.testing.assert_close(y, -x)
+
+
+def test_mt_axpby():
+    xs = _tensors(SIZES, torch.float16, seed=1)
+    ys = _tensors(SIZES, torch.float32, seed=2)
+    outs = [torch.empty(x.numel(), device=DEV) for x in xs]
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C().mt.axpby(noop, [xs, ys, outs], 0.5, None, False, 2.0, None, False, -1)
+    for x, y, o in zip(xs, ys, outs):
+        torch.testing.assert_close(o, 0.5 * x.float() + 2.0 * y, rtol=1e-6, atol=1e-6)
+    ys[3][0] = float("inf")
+    C().mt.axpby(noop, [xs, ys, outs], 0.5, None, False, 2.0, None, False, 0)
+    assert noop.item() == 0  # only x checked
+    C().mt.axpby(noop, [xs, ys, outs], 0.5, None, False, 2.0, None, False, 1)
+    assert noop.item() == 1
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_mt_l2norm(dt):
+    xs = _tensors(SIZES, dt, seed=3)
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    n, pt = C().mt.norm(noop, xs, True, False)
+    ref = torch.cat([x.double().flatten() for x in xs]).norm()
+    assert math.isclose(n.item(), ref.item(), rel_tol=1e-5)
+    for x, v in zip(xs, pt):
+        assert math.isclose(v.item(), x.double().norm().item(), rel_tol=1e-5, abs_tol=1e-6)
+    mx, ptm = C().mt.norm(noop, xs, True, True)
+    assert mx.item() == max(x.abs().max().item() for x in xs)
+    # determinism: bitwise identical on repeat
+    n2, _ = C().mt.norm(noop, xs, True, False)
+    assert n.item() == n2.item()
+
+
+def _cpu_gpu(fn):
+    """Run fn(device) on CPU and GPU (same data), return both results."""
+    return fn("cpu"), fn(DEV)
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+@pytest.mark.parametrize("wd_after", [False, True])
+def test_fused_sgd_matches_torch(nesterov, wd_after):
+    from apex_example_amd.optimizers import FusedSGD
+
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV, requires_grad=True) for n in [10, 8200, 3000]]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    o1 = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=0.01 if not wd_after else 0.0,
+                  nesterov=nesterov, wd_after_momentum=wd_after)
+    o2 = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=0.01 if not wd_after else 0.0,
+                         nesterov=nesterov)
+    for it in range(4):
+        gs = [torch.randn_like(p) for p in ps]
+        for p, r, g in zip(ps, ref, gs):
+            p.grad = g.clone()
+            r.grad = g.clone()
+        o1.step()
+        o2.step()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("adam_w", [True, False])
+def test_fused_adam_matches_torch(adam_w):
+    from apex_example_amd.optimizers import FusedAdam
+
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV, requires_grad=True) for n in [10, 9000, 257]]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    o1 = FusedAdam(ps, lr=1e-2, weight_decay=0.1, adam_w_mode=adam_w)
+    o2 = (torch.optim.AdamW if adam_w else torch.optim.Adam)(ref, lr=1e-2, weight_decay=0.1)
+    for it in range(5):
+        for p, r in zip(ps, ref):
+            g = torch.randn_like(p)
+            p.grad = g.clone()
+            r.grad = g.clone()
+        o1.step()
+        o2.step()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-5)
+    assert o1.param_groups[0]["step"] == 5
+
+
+def _ref_lamb(params, grads, m, v, step, lr, b1, b2, eps, wd, max_norm):
+    gn = torch.cat([g.double().flatten() for g in grads]).norm().item()
+    clip = gn / max_norm if gn > max_norm else 1.0
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    for i, (p, g) in enumerate(zip(params, grads)):
+        gi = g / clip
+        m[i] = b1 * m[i] + (1 - b1) * gi
+        v[i] = b2 * v[i] + (1 - b2) * gi * gi
+        u = (m[i] / bc1) / ((v[i] / bc2).sqrt() + eps) + wd * p
+        pn, un = p.norm(), u.norm()
+        ratio = (pn / un) if (pn > 0 and un > 0) else 1.0
+        p -= lr * ratio * u
+
+
+def test_fused_lamb_matches_reference():
+    from apex_example_amd.optimizers import FusedLAMB
+
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV, requires_grad=True) for n in [1024, 20000, 3]]
+    ref = [p.detach().clone() for p in ps]
+    m = [torch.zeros_like(p) for p in ref]
+    v = [torch.zeros_like(p) for p in ref]
+    opt = FusedLAMB(ps, lr=1e-2, weight_decay=0.01, max_grad_norm=1.0)
+    for step in range(1, 4):
+        gs = [torch.randn_like(p) * 3 for p in ps]
+        for p, g in zip(ps, gs):
+            p.grad = g.clone()
+        opt.step()
+        _ref_lamb(ref, gs, m, v, step, 1e-2, 0.9, 0.999, 1e-6, 0.01, 1.0)
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.detach(), r, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("opt_name", ["FusedNovoGrad", "FusedAdagrad", "FusedLAMB", "FusedAdam",
+                                      "FusedSGD"])
+def test_optimizer_gpu_matches_cpu_path(opt_name):
+    import apex_example_amd.optimizers as O
+
+    torch.manual_seed(0)
+    cls = getattr(O, opt_name)
+    kw = {"lr": 1e-2}
+    if opt_name == "FusedSGD":
+        kw["momentum"] = 0.9
+    base = [torch.randn(n) for n in [100, 9000, 17]]
+    res = {}
+    for dev in ["cpu", DEV]:
+        ps = [b.clone().to(dev).requires_grad_(True) for b in base]
+        opt = cls(ps, **kw)
+        g = torch.Generator().manual_seed(5)
+        for _ in range(3):
+            for p in ps:
+                p.grad = torch.randn(p.shape, generator=g).to(dev)
+            opt.step()
+        res[dev] = [p.detach().cpu() for p in ps]
+    for a, b in zip(res["cpu"], res[DEV]):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-6)
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("shape", [(64, 1024), (3, 7, 768), (33, 4096), (10, 1000), (5, 2048),
+                                   (2, 64)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+def test_layer_norm_fwd_bwd(shape, dt):
+    from apex_example_amd.normalization import FusedLayerNorm
+
+    torch.manual_seed(0)
+    n2 = shape[-1]
+    x = torch.randn(*shape, device=DEV, dtype=dt) * 2 + 0.5
+    ln = FusedLayerNorm(n2).to(DEV).to(dt)
+    with torch.no_grad():
+        ln.weight.normal_()
+        ln.bias.normal_()
+    ref = torch.nn.LayerNorm(n2).to(DEV)
+    ref.load_state_dict({k: v.float() for k, v in ln.state_dict().items()})
+    xa = x.clone().requires_grad_(True)
+    xb = x.float().clone().requires_grad_(True)
+    ya = ln(xa)
+    yb = ref(xb)
+    tol = dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(ya.float(), yb, **tol)
+    dy = torch.randn_like(yb)
+    ya.backward(dy.to(dt))
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad.float(), xb.grad, **tol)
+    gtol = dict(rtol=1e-4, atol=1e-3) if dt == torch.float32 else dict(rtol=5e-2, atol=5e-1)
+    torch.testing.assert_close(ln.weight.grad.float(), ref.weight.grad, **gtol)
+    torch.testing.assert_close(ln.bias.grad.float(), ref.bias.grad, **gtol)
+
+
+def test_rms_norm():
+    from apex_example_amd.normalization import FusedRMSNorm
+
+    x = torch.randn(16, 1024, device=DEV, requires_grad=True)
+    m = FusedRMSNorm(1024).to(DEV)
+    y = m(x)
+    xr = x.detach().clone().requires_grad_(True)
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * m.weight.detach()
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------------------ BatchNorm
+@pytest.mark.parametrize("fmt", ["nchw", "nhwc"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 24, 7, 7), (2, 256, 28, 28)])
+def test_fused_bn(fmt, dt, relu, res, shape):
+    from apex_example_amd.ops import BatchNorm2dReLU
+
+    torch.manual_seed(0)
+    C_ = shape[1]
+    mf = torch.channels_last if fmt == "nhwc" else torch.contiguous_format
+    x = (torch.randn(*shape, device=DEV) * 3 + 1).to(dt).to(memory_format=mf)
+    z = torch.randn(*shape, device=DEV).to(dt).to(memory_format=mf) if res else None
+    bn = BatchNorm2dReLU(C_, fuse_relu=relu).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_()
+    ref = torch.nn.BatchNorm2d(C_).to(DEV)
+    ref.load_state_dict({k: v for k, v in bn.state_dict().items()})
+    xa = x.clone().requires_grad_(True)
+    za = z.clone().requires_grad_(True) if res else None
+    xb = x.float().clone().requires_grad_(True)
+    zb = z.float().clone().requires_grad_(True) if res else None
+    ya = bn(xa, za)
+    yb = ref(xb)
+    if res:
+        yb = yb + zb
+    if relu:
+        yb = torch.relu(yb)
+    tol = dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(ya.float(), yb, **tol)
+    assert ya.is_contiguous(memory_format=mf)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
+    dy = torch.randn_like(yb)
+    ya.backward(dy.to(dt))
+    yb.backward(dy)
+    gt = dict(rtol=1e-3, atol=1e-3) if dt == torch.float32 else dict(rtol=5e-2, atol=6e-2)
+    torch.testing.assert_close(xa.grad.float(), xb.grad, **gt)
+    if res:
+        torch.testing.assert_close(za.grad.float(), zb.grad, **gt)
+    wt = dict(rtol=1e-3, atol=1e-2) if dt == torch.float32 else dict(rtol=5e-2, atol=1.0)
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, **wt)
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, **wt)
+
+
+def test_bn_stats_large_mean_no_cancellation():
+    x = (torch.randn(64, 32, 16, 16, device=DEV) * 0.01 + 1000.0).to(
+        memory_format=torch.channels_last)
+    mean, var = C().bn.local_stats(x)
+    xr = x.double()
+    torch.testing.assert_close(mean.double(), xr.mean((0, 2, 3)), rtol=1e-6, atol=1e-4)
+    torch.testing.assert_close(var.double(), xr.var((0, 2, 3), unbiased=False), rtol=2e-2,
+                               atol=1e-6)
