@@ -160,10 +160,12 @@ def main():
         torch.cuda.synchronize()
 
     sync_all()
+    torch.cuda.nvtx.range_push("timed_steps")
     t_start = time.perf_counter()
     for _ in range(args.steps):
         loss = step(x, y)
     sync_all()
+    torch.cuda.nvtx.range_pop()
     elapsed = time.perf_counter() - t_start
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)

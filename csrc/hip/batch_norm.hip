@@ -100,16 +100,28 @@ __global__ void __launch_bounds__(kBNThreads)
   if (active) {
     if (vec) load8(x + c0, k);  // row 0 of the whole tensor: same shift in every split
     else k[0] = to_f32(x[c0]);
-    for (int64_t r = r0 + ri; r < r1; r += rows_iter) {
-      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (vec) load8(x + r * C + c0, v);
-      else v[0] = to_f32(x[r * C + c0]) - 0.f;
+    // 4 rows in flight per thread (independent 16-B loads) before accumulating
+    constexpr int U = 4;
+    for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
+      float v[U][8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float d = v[i] - k[i];
-        s1[i] += d;
-        s2[i] = fmaf(d, d, s2[i]);
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = r + (int64_t)u * rows_iter;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[u][i] = k[i];  // contributes d = 0 when unused
+        if (rr < r1) {
+          if (vec) load8(x + rr * C + c0, v[u]);
+          else v[u][0] = to_f32(x[rr * C + c0]);
+        }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float d = v[u][i] - k[i];
+          s1[i] += d;
+          s2[i] = fmaf(d, d, s2[i]);
+        }
     }
   }
   // combine the rows_iter row-groups of the block through LDS
@@ -185,25 +197,67 @@ __global__ void __launch_bounds__(kBNThreads)
   }
 }
 
+// Sum the [split][2][C] slab over splits for 8 channels per workgroup: every
+// thread accumulates a strided subset of the splits (16 partial sums in
+// registers), then wave64 xor-shuffles + one LDS pass across the 4 waves.  A
+// channel's splits are thereby read by 256 threads in parallel (the naive
+// thread-per-channel loop serialised 1024 dependent loads per channel).
+constexpr int kFinCh = 8;
+// Result: out[k] = sum of first-half partials of channel c0+k, out[kFinCh+k] =
+// second half; valid for every thread after the call.
+__device__ __forceinline__ void slab_sum8(const float* __restrict__ slab, int splits, int C, int c0,
+                                          float* out /* __shared__ [2*kFinCh] */) {
+  __shared__ float red[kBNThreads / kWave][2 * kFinCh];
+  float a[2 * kFinCh];
+#pragma unroll
+  for (int k = 0; k < 2 * kFinCh; ++k) a[k] = 0.f;
+  for (int s = threadIdx.x; s < splits; s += blockDim.x) {
+    const float* row = slab + (size_t)s * 2 * C;
+#pragma unroll
+    for (int k = 0; k < kFinCh; ++k) {
+      if (c0 + k < C) {
+        a[k] += row[c0 + k];
+        a[kFinCh + k] += row[C + c0 + k];
+      }
+    }
+  }
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < 2 * kFinCh; ++k) a[k] = wave_sum(a[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 2 * kFinCh; ++k) red[wid][k] = a[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kFinCh) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t += red[w][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
 // sum slabs -> mean, var_biased (per channel); shift re-read from x
 template <typename T>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kBNThreads)
     stats_finalize(const T* __restrict__ x, const float* __restrict__ slab, int splits, int C,
                    int64_t count, int64_t shift_stride, float* __restrict__ mean,
                    float* __restrict__ var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < splits; ++s) {
-    s1 += slab[(size_t)s * 2 * C + c];
-    s2 += slab[(size_t)s * 2 * C + C + c];
+  __shared__ float sums[2 * kFinCh];
+  const int c0 = blockIdx.x * kFinCh;
+  slab_sum8(slab, splits, C, c0, sums);
+  const int k = threadIdx.x;
+  if (k < kFinCh && c0 + k < C) {
+    const int c = c0 + k;
+    const float shift = to_f32(x[(int64_t)c * shift_stride]);
+    double m = (double)sums[k] / (double)count;
+    double v = (double)sums[kFinCh + k] / (double)count - m * m;
+    mean[c] = (float)(shift + m);
+    var[c] = (float)(v > 0.0 ? v : 0.0);
   }
-  const float k = to_f32(x[(int64_t)c * shift_stride]);
-  double m = s1 / (double)count;
-  double v = s2 / (double)count - m * m;
-  mean[c] = (float)(k + m);
-  var[c] = (float)(v > 0.0 ? v : 0.0);
 }
+
+static inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + kFinCh - 1) / kFinCh)); }
 
 int64_t bn_stats_workspace(int64_t outer, int64_t C, int64_t inner, int channel_last) {
   BNGeom g = bn_geom(outer, C, inner, channel_last, true);
@@ -224,12 +278,12 @@ void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t i
     if (channel_last) {
       hipLaunchKernelGGL((stats_nhwc<T>), dim3(g.splits, g.cblocks), dim3(kBNThreads), 0, st, xp,
                          outer, (int)C, g.ctile, g.rows_iter, g.vec ? 1 : 0, ws);
-      hipLaunchKernelGGL((stats_finalize<T>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, xp,
+      hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp,
                          ws, g.splits, (int)C, count, (int64_t)1, mean, var_biased);
     } else {
       hipLaunchKernelGGL((stats_nchw<T>), dim3(g.splits, (unsigned)C), dim3(kBNThreads), 0, st, xp,
                          outer, (int)C, inner, g.vec ? 1 : 0, ws);
-      hipLaunchKernelGGL((stats_finalize<T>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, xp,
+      hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp,
                          ws, g.splits, (int)C, count, inner, mean, var_biased);
     }
   });
@@ -442,29 +496,39 @@ __global__ void __launch_bounds__(kBNThreads)
       chan_affine(mean, invstd, wload<T, TW>(w, c0 + i, 1.f), wload<T, TW>(b, c0 + i, 0.f), c0 + i,
                   sc[i], sh[i]);
     }
-    for (int64_t r = r0 + ri; r < r1; r += rows_iter) {
-      float xv[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      float zv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (vec) {
-        load8(x + r * C + c0, xv);
-        load8(dy + r * C + c0, dv);
-        if (relu && z) load8(z + r * C + c0, zv);
-      } else {
-        xv[0] = to_f32(x[r * C + c0]);
-        dv[0] = to_f32(dy[r * C + c0]);
-        if (relu && z) zv[0] = to_f32(z[r * C + c0]);
+    constexpr int U = 2;  // 2 rows x (x, dy[, z]) 16-B loads in flight per thread
+    for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
+      float xv[U][8], dv[U][8], zv[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = r + (int64_t)u * rows_iter;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[u][i] = dv[u][i] = zv[u][i] = 0.f;  // dy=0: no contribution
+        if (rr < r1) {
+          if (vec) {
+            load8(x + rr * C + c0, xv[u]);
+            load8(dy + rr * C + c0, dv[u]);
+            if (relu && z) load8(z + rr * C + c0, zv[u]);
+          } else {
+            xv[u][0] = to_f32(x[rr * C + c0]);
+            dv[u][0] = to_f32(dy[rr * C + c0]);
+            if (relu && z) zv[u][0] = to_f32(z[rr * C + c0]);
+          }
+        }
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float d = dv[i];
-        if (relu) {
-          float o = fmaf(xv[i], sc[i], sh[i]);
-          if (z) o += zv[i];
-          d = o > 0.f ? d : 0.f;
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float d = dv[u][i];
+          if (relu) {
+            float o = fmaf(xv[u][i], sc[i], sh[i]);
+            if (z) o += zv[u][i];
+            d = o > 0.f ? d : 0.f;
+          }
+          s1[i] += d;
+          s2[i] = fmaf(d, xv[u][i] - mu[i], s2[i]);
         }
-        s1[i] += d;
-        s2[i] = fmaf(d, xv[i] - mu[i], s2[i]);
-      }
     }
   }
   __shared__ float lds[2][kBNThreads * 8];
@@ -559,21 +623,22 @@ __global__ void __launch_bounds__(kBNThreads)
 }
 
 template <typename TW>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kBNThreads)
     reduce_finalize(const float* __restrict__ slab, int splits, int C,
                     const float* __restrict__ invstd, float* __restrict__ sum_dy,
                     float* __restrict__ sum_dy_xmu, TW* __restrict__ gw, TW* __restrict__ gb) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int s = 0; s < splits; ++s) {
-    s1 += slab[(size_t)s * 2 * C + c];
-    s2 += slab[(size_t)s * 2 * C + C + c];
+  __shared__ float sums[2 * kFinCh];
+  const int c0 = blockIdx.x * kFinCh;
+  slab_sum8(slab, splits, C, c0, sums);
+  const int k = threadIdx.x;
+  if (k < kFinCh && c0 + k < C) {
+    const int c = c0 + k;
+    const float s1 = sums[k], s2 = sums[kFinCh + k];
+    sum_dy[c] = s1;
+    sum_dy_xmu[c] = s2;
+    if (gw) gw[c] = from_f32<TW>(s2 * invstd[c]);
+    if (gb) gb[c] = from_f32<TW>(s1);
   }
-  sum_dy[c] = s1;
-  sum_dy_xmu[c] = s2;
-  if (gw) gw[c] = from_f32<TW>(s2 * invstd[c]);
-  if (gb) gb[c] = from_f32<TW>(s1);
 }
 
 void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
@@ -601,7 +666,7 @@ void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                            st, dyp, xp, mean, invstd, wp, bp, zp, relu, outer, (int)C, inner,
                            g.vec ? 1 : 0, ws);
       }
-      hipLaunchKernelGGL((reduce_finalize<TW>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st,
+      hipLaunchKernelGGL((reduce_finalize<TW>), fin_grid(C), dim3(kBNThreads), 0, st,
                          ws, g.splits, (int)C, invstd, sum_dy, sum_dy_xmu,
                          static_cast<TW*>(grad_weight), static_cast<TW*>(grad_bias));
     });

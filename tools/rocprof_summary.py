@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace (CSV) into a per-kernel table.
+
+    rocprofv3 --kernel-trace --marker-trace --output-format csv -d OUT -o run -- python bench.py ...
+    python tools/rocprof_summary.py OUT [--range timed_steps] [--top 40] [--md out.md]
+
+With ``--range NAME`` only kernels that START inside the roctx range(s) called
+NAME (bench.py marks its timed steps with "timed_steps") are counted, so the
+MIOpen solver search of the warmup does not pollute the table.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def _find(root, pattern):
+    hits = glob.glob(os.path.join(root, "**", pattern), recursive=True)
+    return sorted(hits)
+
+
+def _short(name, n=110):
+    name = re.sub(r"\s+", " ", name)
+    return name if len(name) <= n else name[: n - 3] + "..."
+
+
+def load_ranges(root, range_name):
+    files = _find(root, "*marker_api_trace.csv")
+    ranges = []
+    for f in files:
+        with open(f) as fh:
+            rd = csv.DictReader(fh)
+            for row in rd:
+                # the range name sits in "Function"/"Message" depending on the
+                # rocprofv3 version: accept it in any text column
+                if not any(range_name in (v or "") for k, v in row.items()
+                           if "Timestamp" not in (k or "")):
+                    continue
+                s = int(row.get("Start_Timestamp") or row.get("Start") or 0)
+                e = int(row.get("End_Timestamp") or row.get("End") or 0)
+                if e > s:
+                    ranges.append((s, e))
+            if not ranges:
+                print("marker columns: %s" % (rd.fieldnames,), file=sys.stderr)
+    return ranges
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--range", default=None)
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--md", default=None)
+    ap.add_argument("--steps", type=int, default=None, help="divide totals per step")
+    a = ap.parse_args(argv)
+
+    files = _find(a.root, "*kernel_trace.csv")
+    if not files:
+        print("no kernel_trace.csv under", a.root)
+        return 1
+    ranges = load_ranges(a.root, a.range) if a.range else []
+    if a.range and not ranges:
+        print("warning: range %r not found; using the whole trace" % a.range, file=sys.stderr)
+
+    tot = defaultdict(float)
+    cnt = defaultdict(int)
+    t_min, t_max = None, None
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                s = int(row["Start_Timestamp"])
+                e = int(row["End_Timestamp"])
+                if ranges and not any(r0 <= s <= r1 for r0, r1 in ranges):
+                    continue
+                name = row.get("Kernel_Name", "?")
+                tot[name] += (e - s) / 1e3  # us
+                cnt[name] += 1
+                t_min = s if t_min is None else min(t_min, s)
+                t_max = e if t_max is None else max(t_max, e)
+    total = sum(tot.values())
+    span = (t_max - t_min) / 1e3 if t_min is not None else 0.0
+    rows = sorted(tot.items(), key=lambda kv: -kv[1])
+    div = a.steps or 1
+    lines = []
+    lines.append("| # | kernel | calls | total us%s | %% of kernel time |" % (
+        "/step" if a.steps else ""))
+    lines.append("|---|---|---|---|---|")
+    for i, (k, v) in enumerate(rows[: a.top]):
+        lines.append("| %d | `%s` | %d | %.1f | %.1f |" % (i + 1, _short(k), cnt[k] // div,
+                                                         v / div, 100.0 * v / total))
+    head = ("kernels: %d distinct, %d dispatches; summed kernel time %.1f us; window %.1f us "
+            "(busy %.1f%%)" % (len(tot), sum(cnt.values()), total, span,
+                               100.0 * total / span if span else 0.0))
+    out = head + "\n\n" + "\n".join(lines) + "\n"
+    print(out)
+    if a.md:
+        with open(a.md, "w") as fh:
+            fh.write(out)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
