@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--materialize-master-grads", action="store_true")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--deterministic", action="store_true")
+    # MIOpen immediate mode measured as fast as exhaustive find for this model on
+    # MI355X (docs/PERF.md) and it avoids ~200 s of solver search on a fresh box.
+    ap.add_argument("--cudnn-benchmark", action="store_true",
+                    help="MIOpen find (solver search) instead of immediate mode")
     ap.add_argument("--opt-step-iters", type=int, default=20)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -133,7 +137,7 @@ def main():
     if env_world != args.gpus and env_world > 1:
         print("warning: --gpus %d but WORLD_SIZE=%d" % (args.gpus, env_world), file=sys.stderr)
     rank, world, device = init_distributed()
-    torch.backends.cudnn.benchmark = not args.deterministic
+    torch.backends.cudnn.benchmark = (not args.deterministic) and args.cudnn_benchmark
     torch.backends.cudnn.deterministic = args.deterministic
     torch.manual_seed(1234 + rank)
 

@@ -1,0 +1,386 @@
+// Channels-last (NHWC) BatchNorm kernels for gfx950: x viewed as [M, C],
+// M = N*H*W.  apex csrc/welford.cu *_c_last semantics.
+//
+// Layout of work: a lane owns W = 8 consecutive channels (one 16-byte bf16
+// load, VEC path) or 1 channel (scalar path for C % 8 != 0 / unaligned data);
+// `ctile` lanes cover a row segment of up to 512 channels and the remaining
+// lanes of the 256-thread workgroup take further rows (rows_iter >= 4), so the
+// per-channel constants and accumulators of a lane never change while it
+// streams rows.  Every loop keeps 2-4 independent rows (16-B loads) in flight
+// per lane.  Reductions write per-split partial slabs summed by the shared
+// finalize kernel (bn_common.h): deterministic, no atomics.
+#include "bn_common.h"
+
+namespace amd {
+
+namespace {
+
+struct NGeom {
+  int ctile, rows_iter, cblocks;
+};
+
+NGeom ngeom(int64_t C, bool vec) {
+  NGeom g;
+  int64_t cv = vec ? C / 8 : C;
+  g.ctile = (int)(cv < 64 ? cv : 64);
+  if (g.ctile < 1) g.ctile = 1;
+  g.rows_iter = kBNThreads / g.ctile;
+  g.cblocks = (int)((cv + g.ctile - 1) / g.ctile);
+  return g;
+}
+
+int reduce_splits(int64_t M, const NGeom& g) {
+  int64_t want = (M + (int64_t)g.rows_iter * 32 - 1) / ((int64_t)g.rows_iter * 32);
+  int64_t cap = 2048 / g.cblocks;
+  if (cap < 1) cap = 1;
+  if (want > cap) want = cap;
+  return (int)(want < 1 ? 1 : want);
+}
+
+int elem_blocks(int64_t M, const NGeom& g) {
+  int64_t want = (M + (int64_t)g.rows_iter * 4 - 1) / ((int64_t)g.rows_iter * 4);
+  int64_t cap = 8192 / g.cblocks;
+  if (cap < 1) cap = 1;
+  if (want > cap) want = cap;
+  return (int)(want < 1 ? 1 : want);
+}
+
+template <typename T, int W>
+__device__ __forceinline__ void ldw(const T* p, float (&v)[W]) {
+  if constexpr (W == 8) load8(p, v);
+  else v[0] = to_f32(p[0]);
+}
+template <typename T, int W>
+__device__ __forceinline__ void stw(T* p, const float (&v)[W]) {
+  if constexpr (W == 8) store8(p, v);
+  else p[0] = from_f32<T>(v[0]);
+}
+
+// combine the rows_iter row-groups of a block (same lane channel set) via LDS and
+// write the block's partial slab row: slab[blockIdx.x][0|1][C]
+template <int W>
+__device__ __forceinline__ void block_slab_write(float (&s1)[W], float (&s2)[W], int ci, int ri,
+                                                 int ctile, int rows_iter, int c0, int C,
+                                                 float* __restrict__ slab) {
+  __shared__ float lds[2][kBNThreads * W];
+  if (threadIdx.x < rows_iter * ctile) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      lds[0][(ri * ctile + ci) * W + i] = s1[i];
+      lds[1][(ri * ctile + ci) * W + i] = s2[i];
+    }
+  }
+  __syncthreads();
+  if (ri == 0 && c0 < C) {
+    for (int r = 1; r < rows_iter; ++r) {
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        s1[i] += lds[0][(r * ctile + ci) * W + i];
+        s2[i] += lds[1][(r * ctile + ci) * W + i];
+      }
+    }
+    float* o = slab + (size_t)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      o[c0 + i] = s1[i];
+      o[C + c0 + i] = s2[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- statistics
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(kBNThreads)
+    stats_k(const T* __restrict__ x, int64_t M, int C, int ctile, int rows_iter,
+            float* __restrict__ slab) {
+  constexpr int W = VEC ? 8 : 1;
+  constexpr int U = 4;
+  const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
+  const int c0 = (blockIdx.y * ctile + ci) * W;
+  const bool active = ri < rows_iter && c0 < C;
+  const int64_t per = (M + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = r0 + per < M ? r0 + per : M;
+  float k[W], s1[W], s2[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) k[i] = s1[i] = s2[i] = 0.f;
+  if (active) {
+    ldw<T, W>(x + c0, k);  // shift = row 0: identical in every split
+    for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
+      float v[U][W];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = r + (int64_t)u * rows_iter;
+#pragma unroll
+        for (int i = 0; i < W; ++i) v[u][i] = k[i];  // unused slot -> d = 0
+        if (rr < r1) ldw<T, W>(x + rr * C + c0, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+          const float d = v[u][i] - k[i];
+          s1[i] += d;
+          s2[i] = fmaf(d, d, s2[i]);
+        }
+    }
+  }
+  block_slab_write<W>(s1, s2, ci, ri, ctile, rows_iter, c0, C, slab);
+}
+
+// ---------------------------------------------------------------- apply
+template <typename T, typename TW, bool VEC>
+__global__ void __launch_bounds__(kBNThreads)
+    apply_k(const T* __restrict__ x, const float* __restrict__ mean,
+            const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
+            const T* __restrict__ z, T* __restrict__ y, int64_t M, int C, int ctile, int rows_iter,
+            int relu) {
+  constexpr int W = VEC ? 8 : 1;
+  constexpr int U = 2;
+  const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
+  const int c0 = (blockIdx.y * ctile + ci) * W;
+  if (ri >= rows_iter || c0 >= C) return;
+  float sc[W], sh[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i)
+    chan_affine(mean, invstd, wload(w, c0 + i, 1.f), wload(b, c0 + i, 0.f), c0 + i, sc[i], sh[i]);
+  const int64_t stride = (int64_t)gridDim.x * rows_iter;
+  for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
+    float v[U][W], zz[U][W];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = r + (int64_t)u * stride;
+      if (rr < M) {
+        ldw<T, W>(x + rr * C + c0, v[u]);
+        if (z) ldw<T, W>(z + rr * C + c0, zz[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = r + (int64_t)u * stride;
+      if (rr >= M) continue;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        float o = fmaf(v[u][i], sc[i], sh[i]);
+        if (z) o += zz[u][i];
+        v[u][i] = relu ? fmaxf(o, 0.f) : o;
+      }
+      stw<T, W>(y + rr * C + c0, v[u]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward reduce
+template <typename T, typename TW, bool VEC>
+__global__ void __launch_bounds__(kBNThreads)
+    reduce_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
+             const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
+             const T* __restrict__ z, int relu, int64_t M, int C, int ctile, int rows_iter,
+             float* __restrict__ slab) {
+  constexpr int W = VEC ? 8 : 1;
+  constexpr int U = 2;
+  const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
+  const int c0 = (blockIdx.y * ctile + ci) * W;
+  const bool active = ri < rows_iter && c0 < C;
+  const int64_t per = (M + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = r0 + per < M ? r0 + per : M;
+  float mu[W], sc[W], sh[W], s1[W], s2[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) mu[i] = sc[i] = sh[i] = s1[i] = s2[i] = 0.f;
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      mu[i] = mean[c0 + i];
+      chan_affine(mean, invstd, wload(w, c0 + i, 1.f), wload(b, c0 + i, 0.f), c0 + i, sc[i],
+                  sh[i]);
+    }
+    for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
+      float xv[U][W], dv[U][W], zv[U][W];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = r + (int64_t)u * rows_iter;
+#pragma unroll
+        for (int i = 0; i < W; ++i) xv[u][i] = dv[u][i] = zv[u][i] = 0.f;  // dy = 0: no-op
+        if (rr < r1) {
+          ldw<T, W>(x + rr * C + c0, xv[u]);
+          ldw<T, W>(dy + rr * C + c0, dv[u]);
+          if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+          float d = dv[u][i];
+          if (relu) {
+            float o = fmaf(xv[u][i], sc[i], sh[i]);
+            if (z) o += zv[u][i];
+            d = o > 0.f ? d : 0.f;
+          }
+          s1[i] += d;
+          s2[i] = fmaf(d, xv[u][i] - mu[i], s2[i]);
+        }
+    }
+  }
+  block_slab_write<W>(s1, s2, ci, ri, ctile, rows_iter, c0, C, slab);
+}
+
+// ---------------------------------------------------------------- backward elementwise
+// dx = dy'*k1 + x*k2 + k3  with  k1 = invstd*w, k2 = -invstd^3*w*mean(dy'(x-mu)),
+//                                 k3 = -invstd*w*mean(dy') - k2*mu ;  dz = dy'
+template <typename T, typename TW, bool VEC>
+__global__ void __launch_bounds__(kBNThreads)
+    backward_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
+               const float* __restrict__ invstd, const TW* __restrict__ w,
+               const TW* __restrict__ b, const float* __restrict__ sum_dy,
+               const float* __restrict__ sum_dy_xmu, float inv_n, int relu,
+               const T* __restrict__ z, T* __restrict__ dx, T* __restrict__ dz, int64_t M, int C,
+               int ctile, int rows_iter) {
+  constexpr int W = VEC ? 8 : 1;
+  constexpr int U = 2;
+  const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
+  const int c0 = (blockIdx.y * ctile + ci) * W;
+  if (ri >= rows_iter || c0 >= C) return;
+  float sc[W], sh[W], k1[W], k2[W], k3[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int c = c0 + i;
+    const float wc = wload(w, c, 1.f);
+    chan_affine(mean, invstd, wc, wload(b, c, 0.f), c, sc[i], sh[i]);
+    const float is = invstd[c];
+    const float mdy = sum_dy[c] * inv_n, mdyx = sum_dy_xmu[c] * inv_n;
+    k1[i] = is * wc;
+    k2[i] = -is * is * is * wc * mdyx;
+    k3[i] = -is * wc * mdy - k2[i] * mean[c];
+  }
+  const int64_t stride = (int64_t)gridDim.x * rows_iter;
+  for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
+    float xv[U][W], dv[U][W], zv[U][W];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = r + (int64_t)u * stride;
+      if (rr < M) {
+        ldw<T, W>(x + rr * C + c0, xv[u]);
+        ldw<T, W>(dy + rr * C + c0, dv[u]);
+        if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = r + (int64_t)u * stride;
+      if (rr >= M) continue;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        float d = dv[u][i];
+        if (relu) {
+          float o = fmaf(xv[u][i], sc[i], sh[i]);
+          if (z) o += zv[u][i];
+          d = o > 0.f ? d : 0.f;
+        }
+        dv[u][i] = d;
+        xv[u][i] = fmaf(d, k1[i], fmaf(xv[u][i], k2[i], k3[i]));
+      }
+      stw<T, W>(dx + rr * C + c0, xv[u]);
+      if (dz) stw<T, W>(dz + rr * C + c0, dv[u]);
+    }
+  }
+}
+
+template <typename F>
+void vec_dispatch(bool vec, F&& f) {
+  if (vec) f(std::true_type{});
+  else f(std::false_type{});
+}
+
+}  // namespace
+
+int64_t nhwc_splits(int64_t M, int64_t C, bool vec) { return reduce_splits(M, ngeom(C, vec)); }
+
+void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, float* mean, float* var,
+                float* ws, hipStream_t st) {
+  const bool vec = (C % 8 == 0) && all_aligned({x});
+  const NGeom g = ngeom(C, vec);
+  const int splits = reduce_splits(M, g);
+  bn_dispatch(tx, [&](auto t0) {
+    using T = decltype(t0);
+    const T* xp = static_cast<const T*>(x);
+    vec_dispatch(vec, [&](auto V) {
+      hipLaunchKernelGGL((stats_k<T, decltype(V)::value>), dim3(splits, g.cblocks),
+                         dim3(kBNThreads), 0, st, xp, M, (int)C, g.ctile, g.rows_iter, ws);
+    });
+    hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp, ws, splits,
+                       (int)C, M, (int64_t)1, mean, var);
+  });
+}
+
+void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
+                const void* b, DType tw, const void* z, void* y, int64_t M, int64_t C, int relu,
+                hipStream_t st) {
+  const bool vec = (C % 8 == 0) && all_aligned({x, z, y});
+  const NGeom g = ngeom(C, vec);
+  const int blocks = elem_blocks(M, g);
+  bn_dispatch(tx, [&](auto t0) {
+    bn_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      vec_dispatch(vec, [&](auto V) {
+        hipLaunchKernelGGL((apply_k<T, TW, decltype(V)::value>), dim3(blocks, g.cblocks),
+                           dim3(kBNThreads), 0, st, static_cast<const T*>(x), mean, invstd,
+                           static_cast<const TW*>(w), static_cast<const TW*>(b),
+                           static_cast<const T*>(z), static_cast<T*>(y), M, (int)C, g.ctile,
+                           g.rows_iter, relu);
+      });
+    });
+  });
+}
+
+void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, const float* invstd,
+                 const void* w, const void* b, DType tw, int relu, const void* z, int64_t M,
+                 int64_t C, float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, float* ws,
+                 hipStream_t st) {
+  const bool vec = (C % 8 == 0) && all_aligned({dy, x, z});
+  const NGeom g = ngeom(C, vec);
+  const int splits = reduce_splits(M, g);
+  bn_dispatch(tx, [&](auto t0) {
+    bn_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      vec_dispatch(vec, [&](auto V) {
+        hipLaunchKernelGGL((reduce_k<T, TW, decltype(V)::value>), dim3(splits, g.cblocks),
+                           dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
+                           static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
+                           static_cast<const TW*>(b), static_cast<const T*>(z), relu, M, (int)C,
+                           g.ctile, g.rows_iter, ws);
+      });
+      hipLaunchKernelGGL((reduce_finalize<TW>), fin_grid(C), dim3(kBNThreads), 0, st, ws, splits,
+                         (int)C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
+                         static_cast<TW*>(gb));
+    });
+  });
+}
+
+void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
+                   const float* invstd, const void* w, const void* b, DType tw,
+                   const float* sum_dy, const float* sum_dy_xmu, float inv_count, int relu,
+                   const void* z, void* dx, void* dz, int64_t M, int64_t C, hipStream_t st) {
+  const bool vec = (C % 8 == 0) && all_aligned({dy, x, z, dx, dz});
+  const NGeom g = ngeom(C, vec);
+  const int blocks = elem_blocks(M, g);
+  bn_dispatch(tx, [&](auto t0) {
+    bn_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      vec_dispatch(vec, [&](auto V) {
+        hipLaunchKernelGGL((backward_k<T, TW, decltype(V)::value>), dim3(blocks, g.cblocks),
+                           dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
+                           static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
+                           static_cast<const TW*>(b), sum_dy, sum_dy_xmu, inv_count, relu,
+                           static_cast<const T*>(z), static_cast<T*>(dx), static_cast<T*>(dz), M,
+                           (int)C, g.ctile, g.rows_iter);
+      });
+    });
+  });
+}
+
+}  // namespace amd

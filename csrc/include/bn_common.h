@@ -1,0 +1,133 @@
+// Shared pieces of the BatchNorm kernels (NCHW: batch_norm.hip, NHWC: bn_nhwc.hip).
+#pragma once
+#include "amd_dev.h"
+#include "amd_kernels.h"
+
+namespace amd {
+
+constexpr int kBNThreads = 256;
+
+template <typename F>
+static inline void bn_dispatch(DType a, F&& f) {
+  switch (a) {
+    case DType::F32: f(float{}); break;
+    case DType::F16: f(half_t{}); break;
+    case DType::BF16: f(bf16_t{}); break;
+    default: break;
+  }
+}
+
+static inline bool all_aligned(std::initializer_list<const void*> ps) {
+  for (const void* p : ps)
+    if (p && ((uintptr_t)p % 16) != 0) return false;
+  return true;
+}
+
+// y = x*sc + sh with sc = invstd*w, sh = b - mean*sc
+__device__ __forceinline__ void chan_affine(const float* mean, const float* invstd, float w,
+                                            float b, int c, float& sc, float& sh) {
+  float is = invstd[c];
+  sc = is * w;
+  sh = b - mean[c] * sc;
+}
+
+template <typename TW>
+__device__ __forceinline__ float wload(const TW* p, int c, float dflt) {
+  return p ? to_f32(p[c]) : dflt;
+}
+
+// Sum a [split][2][C] partial slab over splits for 8 channels per workgroup:
+// every thread accumulates a strided subset of the splits, then wave64
+// xor-shuffles + one LDS pass across the 4 waves (fixed order: deterministic).
+constexpr int kFinCh = 8;
+__device__ __forceinline__ void slab_sum8(const float* __restrict__ slab, int splits, int C, int c0,
+                                          float* out /* __shared__ [2*kFinCh] */) {
+  __shared__ float red[kBNThreads / kWave][2 * kFinCh];
+  float a[2 * kFinCh];
+#pragma unroll
+  for (int k = 0; k < 2 * kFinCh; ++k) a[k] = 0.f;
+  for (int s = threadIdx.x; s < splits; s += blockDim.x) {
+    const float* row = slab + (size_t)s * 2 * C;
+#pragma unroll
+    for (int k = 0; k < kFinCh; ++k) {
+      if (c0 + k < C) {
+        a[k] += row[c0 + k];
+        a[kFinCh + k] += row[C + c0 + k];
+      }
+    }
+  }
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < 2 * kFinCh; ++k) a[k] = wave_sum(a[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 2 * kFinCh; ++k) red[wid][k] = a[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kFinCh) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t += red[w][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// slab of shifted sums -> mean, var_biased; the shift is re-read from x
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+    stats_finalize(const T* __restrict__ x, const float* __restrict__ slab, int splits, int C,
+                   int64_t count, int64_t shift_stride, float* __restrict__ mean,
+                   float* __restrict__ var) {
+  __shared__ float sums[2 * kFinCh];
+  const int c0 = blockIdx.x * kFinCh;
+  slab_sum8(slab, splits, C, c0, sums);
+  const int k = threadIdx.x;
+  if (k < kFinCh && c0 + k < C) {
+    const int c = c0 + k;
+    const float shift = to_f32(x[(int64_t)c * shift_stride]);
+    double m = (double)sums[k] / (double)count;
+    double v = (double)sums[kFinCh + k] / (double)count - m * m;
+    mean[c] = (float)(shift + m);
+    var[c] = (float)(v > 0.0 ? v : 0.0);
+  }
+}
+
+// slab of (sum dy', sum dy'*(x-mean)) -> sums + grad_weight/grad_bias
+template <typename TW>
+__global__ void __launch_bounds__(kBNThreads)
+    reduce_finalize(const float* __restrict__ slab, int splits, int C,
+                    const float* __restrict__ invstd, float* __restrict__ sum_dy,
+                    float* __restrict__ sum_dy_xmu, TW* __restrict__ gw, TW* __restrict__ gb) {
+  __shared__ float sums[2 * kFinCh];
+  const int c0 = blockIdx.x * kFinCh;
+  slab_sum8(slab, splits, C, c0, sums);
+  const int k = threadIdx.x;
+  if (k < kFinCh && c0 + k < C) {
+    const int c = c0 + k;
+    const float s1 = sums[k], s2 = sums[kFinCh + k];
+    sum_dy[c] = s1;
+    sum_dy_xmu[c] = s2;
+    if (gw) gw[c] = from_f32<TW>(s2 * invstd[c]);
+    if (gb) gb[c] = from_f32<TW>(s1);
+  }
+}
+
+static inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + kFinCh - 1) / kFinCh)); }
+
+// ---- NHWC launchers (bn_nhwc.hip) -------------------------------------------
+int64_t nhwc_splits(int64_t M, int64_t C, bool vec);
+void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, float* mean, float* var,
+                float* ws, hipStream_t st);
+void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
+                const void* b, DType tw, const void* z, void* y, int64_t M, int64_t C, int relu,
+                hipStream_t st);
+void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, const float* invstd,
+                 const void* w, const void* b, DType tw, int relu, const void* z, int64_t M,
+                 int64_t C, float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, float* ws,
+                 hipStream_t st);
+void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
+                   const float* invstd, const void* w, const void* b, DType tw,
+                   const float* sum_dy, const float* sum_dy_xmu, float inv_count, int relu,
+                   const void* z, void* dx, void* dz, int64_t M, int64_t C, hipStream_t st);
+
+}  // namespace amd

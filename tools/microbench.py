@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmarks on one MI355X (interleaved A/B in one process).
+
+    python tools/microbench.py bn      # fused BN kernels vs HBM copy roofline vs MIOpen BN
+    python tools/microbench.py conv1x1 # ResNet-50 1x1 convs: MIOpen conv vs GEMM (hipBLASLt)
+    python tools/microbench.py optim   # optimizer step bandwidth (ResNet-50 / BERT-large sizes)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=20, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+BN_SHAPES = [  # (N, C, H, W) ResNet-50 @ bs256 NHWC
+    (256, 64, 112, 112), (256, 64, 56, 56), (256, 256, 56, 56), (256, 128, 28, 28),
+    (256, 512, 28, 28), (256, 256, 14, 14), (256, 1024, 14, 14), (256, 2048, 7, 7),
+    (256, 512, 7, 7),
+]
+
+
+def bench_bn(args):
+    from apex_example_amd import _native
+
+    C_ = _native.require().bn
+    dev = "cuda"
+    print("| shape (NHWC bf16) | MB/tensor | copy TB/s | stats | apply+relu | apply+z+relu | "
+          "reduce+relu+z | bwd+relu+z | MIOpen fwd | MIOpen bwd |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
+    for (n, c, h, w) in BN_SHAPES:
+        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        z = torch.randn_like(x)
+        dy = torch.randn_like(x)
+        wt = torch.ones(c, device=dev)
+        bs = torch.zeros(c, device=dev)
+        nb = x.numel() * 2
+        mb = nb / 1e6
+        t_copy = timeit(lambda: x.clone())
+        mean, var = C_.local_stats(x)
+        invstd = (var + 1e-5).rsqrt()
+        t_stats = timeit(lambda: C_.local_stats(x))
+        t_apply = timeit(lambda: C_.apply(x, mean, invstd, wt, bs, None, True))
+        t_applyz = timeit(lambda: C_.apply(x, mean, invstd, wt, bs, z, True))
+        t_red = timeit(lambda: C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True))
+        s1, s2, _, _ = C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True)
+        t_bwd = timeit(lambda: C_.backward_elemt(dy, x, mean, invstd, wt, bs, s1, s2,
+                                                 float(n * h * w), z, True, True))
+        bn = torch.nn.BatchNorm2d(c).to(dev)
+        xr = x.detach().requires_grad_(True)
+        t_mf = timeit(lambda: F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                                           True, 0.1, 1e-5))
+        yb = F.batch_norm(xr, bn.running_mean, bn.running_var, bn.weight, bn.bias, True, 0.1, 1e-5)
+
+        def mb_bwd():
+            torch.autograd.grad(yb, xr, dy, retain_graph=True)
+
+        t_mb = timeit(mb_bwd)
+
+        def tbs(nbytes, t):
+            return "%.0f us (%.2f TB/s)" % (t, nbytes / (t * 1e-6) / 1e12)
+
+        print("| %s | %.0f | %.2f | %s | %s | %s | %s | %s | %s | %s |" % (
+            (n, c, h, w), mb, 2 * nb / (t_copy * 1e-6) / 1e12, tbs(nb, t_stats),
+            tbs(2 * nb, t_apply), tbs(3 * nb, t_applyz), tbs(3 * nb, t_red), tbs(5 * nb, t_bwd),
+            tbs(2 * nb, t_mf), tbs(3 * nb, t_mb)))
+
+
+def bench_conv1x1(args):
+    dev = "cuda"
+    torch.backends.cudnn.benchmark = False
+    shapes = [(256, 64, 256, 56), (256, 256, 64, 56), (256, 256, 128, 56), (256, 128, 512, 28),
+              (256, 512, 128, 28), (256, 512, 256, 28), (256, 256, 1024, 14),
+              (256, 1024, 256, 14), (256, 1024, 512, 14), (256, 512, 2048, 7),
+              (256, 2048, 512, 7)]
+    print("| N,Cin,Cout,HW | GFLOP | MIOpen fwd | GEMM fwd | MIOpen dgrad | GEMM dgrad | "
+          "MIOpen wgrad | GEMM wgrad |")
+    print("|---|---|---|---|---|---|---|---|")
+    for (n, ci, co, hw) in shapes:
+        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = torch.randn(co, ci, 1, 1, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy = torch.randn(n, co, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        M = n * hw * hw
+        gf = 2 * M * ci * co / 1e9
+        x2 = x.permute(0, 2, 3, 1).reshape(M, ci)
+        dy2 = dy.permute(0, 2, 3, 1).reshape(M, co)
+        w2 = w.reshape(co, ci)
+        t_cf = timeit(lambda: F.conv2d(x, w))
+        t_gf = timeit(lambda: torch.mm(x2, w2.t()))
+        t_cd = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (True, False, False)))
+        t_gd = timeit(lambda: torch.mm(dy2, w2))
+        t_cw = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (False, True, False)))
+        t_gw = timeit(lambda: torch.mm(dy2.t(), x2))
+
+        def tf(t):
+            return "%.0f us (%.0f TF)" % (t, gf / (t * 1e-6) / 1e3)
+
+        print("| %d,%d,%d,%d | %.1f | %s | %s | %s | %s | %s | %s |" % (
+            n, ci, co, hw, gf, tf(t_cf), tf(t_gf), tf(t_cd), tf(t_gd), tf(t_cw), tf(t_gw)))
+
+
+def bench_optim(args):
+    from apex_example_amd.optimizers import FusedAdam, FusedSGD
+    from apex_example_amd.models import resnet50
+
+    dev = "cuda"
+    m = resnet50().to(dev)
+    ps = [p for p in m.parameters()]
+    n = sum(p.numel() for p in ps)
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    o = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    o.step()
+    t = timeit(lambda: o.step())
+    print("FusedSGD fp32 ResNet-50 (%d params, 161 tensors): %.1f us, %.2f TB/s (16 B/param)" % (
+        n, t, 16 * n / (t * 1e-6) / 1e12))
+    ref = torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
+    ref.step()
+    t2 = timeit(lambda: ref.step())
+    print("torch.optim.SGD(fused) same: %.1f us" % t2)
+    oa = FusedAdam(ps, lr=1e-3)
+    oa.step()
+    t3 = timeit(lambda: oa.step())
+    print("FusedAdam fp32 ResNet-50: %.1f us, %.2f TB/s (28 B/param)" % (
+        t3, 28 * n / (t3 * 1e-6) / 1e12))
+    ra = torch.optim.AdamW(ps, lr=1e-3, fused=True)
+    ra.step()
+    t4 = timeit(lambda: ra.step())
+    print("torch.optim.AdamW(fused) same: %.1f us" % t4)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["bn", "conv1x1", "optim"])
+    a = ap.parse_args()
+    {"bn": bench_bn, "conv1x1": bench_conv1x1, "optim": bench_optim}[a.what](a)
+
+
+if __name__ == "__main__":
+    main()
