@@ -201,7 +201,9 @@ class LossScaler(object):
                     self._scale_dev, self._unskipped_dev, self._skipped_dev, self._overflow_buf,
                     float(self._scale_factor), int(self._scale_seq_len),
                     float(self._min_loss_scale or 0.0), float(self._max_loss_scale), True)
-                self._post_report()
+                if not (self._device.type == "cuda"
+                        and torch.cuda.is_current_stream_capturing()):
+                    self._post_report()  # (inside a hipGraph capture: poll via skipped_steps())
             else:
                 self._unskipped_dev.add_(1)
             return False
@@ -252,7 +254,8 @@ class LossScaler(object):
 
     def poll(self):
         """Print pending overflow messages whose data already reached the host."""
-        if self.sync_free:
+        if self.sync_free and not (self._device.type == "cuda"
+                                   and torch.cuda.is_current_stream_capturing()):
             self._poll_report()
 
     def skipped_steps(self):

@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
+from ..ops.conv import Conv2d1x1
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
@@ -20,7 +21,9 @@ def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
                      groups=groups, bias=False, dilation=dilation)
 
 
-def conv1x1(in_planes, out_planes, stride=1):
+def conv1x1(in_planes, out_planes, stride=1, gemm=False):
+    if gemm:
+        return Conv2d1x1(in_planes, out_planes, stride=stride)
     return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
 
 
@@ -51,7 +54,7 @@ class BasicBlock(nn.Module):
     expansion = 1
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, fused_bn=False,
-                 zero_init_residual=False):
+                 zero_init_residual=False, gemm_1x1=False):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
         self.bn1 = _BNAct(planes, True, fused_bn)
@@ -69,14 +72,14 @@ class Bottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, fused_bn=False,
-                 zero_init_residual=False):
+                 zero_init_residual=False, gemm_1x1=False):
         super().__init__()
         width = planes
-        self.conv1 = conv1x1(inplanes, width)
+        self.conv1 = conv1x1(inplanes, width, gemm=gemm_1x1)
         self.bn1 = _BNAct(width, True, fused_bn)
         self.conv2 = conv3x3(width, width, stride)
         self.bn2 = _BNAct(width, True, fused_bn)
-        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.conv3 = conv1x1(width, planes * self.expansion, gemm=gemm_1x1)
         self.bn3 = _BNAct(planes * self.expansion, True, fused_bn, zero_init_residual)
         self.downsample = downsample
 
@@ -88,9 +91,9 @@ class Bottleneck(nn.Module):
 
 
 class _Downsample(nn.Module):
-    def __init__(self, inplanes, outplanes, stride, fused_bn):
+    def __init__(self, inplanes, outplanes, stride, fused_bn, gemm_1x1=False):
         super().__init__()
-        self.conv = conv1x1(inplanes, outplanes, stride)
+        self.conv = conv1x1(inplanes, outplanes, stride, gemm=gemm_1x1)
         self.bn = _BNAct(outplanes, False, fused_bn)
 
     def forward(self, x):
@@ -98,9 +101,11 @@ class _Downsample(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, block, layers, num_classes=1000, fused_bn=False, zero_init_residual=False):
+    def __init__(self, block, layers, num_classes=1000, fused_bn=False, zero_init_residual=False,
+                 gemm_1x1=False):
         super().__init__()
         self.fused_bn = fused_bn
+        self.gemm_1x1 = gemm_1x1
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = _BNAct(self.inplanes, True, fused_bn)
@@ -119,13 +124,13 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = _Downsample(self.inplanes, planes * block.expansion, stride,
-                                     self.fused_bn)
+                                     self.fused_bn, self.gemm_1x1)
         layers = [block(self.inplanes, planes, stride, downsample, self.fused_bn,
-                        zero_init_residual)]
+                        zero_init_residual, self.gemm_1x1)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
             layers.append(block(self.inplanes, planes, fused_bn=self.fused_bn,
-                                zero_init_residual=zero_init_residual))
+                                zero_init_residual=zero_init_residual, gemm_1x1=self.gemm_1x1))
         return nn.Sequential(*layers)
 
     def forward(self, x):

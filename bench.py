@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--syncbn", action="store_true", help="SyncBatchNorm across ranks")
     ap.add_argument("--message-size", type=int, default=10_000_000, help="DDP bucket elements")
     ap.add_argument("--materialize-master-grads", action="store_true")
+    ap.add_argument("--no-gemm-1x1", action="store_true",
+                    help="keep MIOpen for the stride-1 1x1 convs (default: hipBLASLt GEMM)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step in a hipGraph and replay it")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--deterministic", action="store_true")
     # MIOpen immediate mode measured as fast as exhaustive find for this model on
@@ -78,7 +82,8 @@ def build(args, device, world):
     half = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     ctor = {"resnet50": resnet50, "resnet18": resnet18}[args.model]
     fused_bn = args.impl == "amd" and not args.no_fused_bn
-    model = ctor(fused_bn=fused_bn).to(device)
+    gemm_1x1 = args.impl == "amd" and not args.no_gemm_1x1
+    model = ctor(fused_bn=fused_bn, gemm_1x1=gemm_1x1).to(device)
     if args.syncbn and world > 1:
         if args.impl == "amd":
             model = convert_syncbn_model(model)
@@ -158,6 +163,30 @@ def main():
                                                               time.time() - t0))
     torch.cuda.synchronize()
 
+    if args.graph:
+        if world > 1:
+            raise SystemExit("--graph is single-GPU only in this version")
+        # warm the capture path on a side stream (allocator pools, plan caches)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                step(x, y)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = step(x, y)
+        torch.cuda.synchronize()
+        log(rank, "[bench] captured the training step in a hipGraph")
+        eager_step = step
+
+        def step(x_, y_):  # noqa: F811  (replay: same work, one launch)
+            graph.replay()
+            return static_loss
+
+        step(x, y)
+        torch.cuda.synchronize()
+
     def sync_all():
         if world > 1:
             dist.barrier(device_ids=[device.index])
@@ -221,6 +250,8 @@ def main():
             "fused_bn": args.impl == "amd" and not args.no_fused_bn,
             "syncbn": bool(args.syncbn and world > 1),
             "ddp_message_size": args.message_size if world > 1 else None,
+            "gemm_1x1": args.impl == "amd" and not args.no_gemm_1x1,
+            "hip_graph": bool(args.graph),
         },
         "optimizer_step_ms": round(opt_ms, 4),
         "final_loss": round(final_loss, 4),

@@ -56,6 +56,8 @@ using TensorLists = std::vector<std::vector<at::Tensor>>;
 // Validates `lists` and returns the (cached) device launch table.
 struct MTPlan {
   at::Tensor table;  // device bytes (kept alive by the cache)
+  at::Tensor host;   // pinned source image (kept alive: graph-captured copies re-read it)
+  bool captured = false;  // built inside a graph capture: never evicted
   MTLaunch L;
 };
 const MTPlan& mt_plan(const TensorLists& lists);

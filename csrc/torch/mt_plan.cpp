@@ -9,6 +9,9 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <c10/hip/HIPException.h>
+#include <c10/hip/HIPGraphsC10Utils.h>
+
 #include "common.h"
 
 namespace amd {
@@ -105,6 +108,9 @@ const MTPlan& mt_plan(const TensorLists& lists) {
   auto it = c.map.find(key);
   if (it != c.map.end()) {
     c.lru.splice(c.lru.begin(), c.lru, it->second.pos);
+    // a table referenced by a captured graph must outlive the graph: pin it
+    if (c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None)
+      it->second.plan.captured = true;
     return it->second.plan;
   }
 
@@ -139,10 +145,17 @@ const MTPlan& mt_plan(const TensorLists& lists) {
   if (tbytes) std::memcpy(hp, tds.data(), tbytes);
   if (cbytes) std::memcpy(hp + coff, chunks.data(), cbytes);
   at::Tensor table = at::empty({(int64_t)total}, at::TensorOptions().dtype(at::kByte).device(dev));
-  table.copy_(host, /*non_blocking=*/true);
+  // Raw async copy from a pinned image that the plan keeps alive for its whole
+  // lifetime: valid both eagerly and inside a hipGraph capture (the captured
+  // memcpy node re-reads this same, never-reused host buffer on every replay).
+  C10_HIP_CHECK(hipMemcpyAsync(table.data_ptr(), hp, total, hipMemcpyHostToDevice,
+                               c10::hip::getCurrentHIPStream().stream()));
 
   MTPlan plan;
   plan.table = table;
+  plan.host = host;
+  plan.captured = c10::hip::currentStreamCaptureStatusMayInitCtx() !=
+                  c10::hip::CaptureStatus::None;
   uint8_t* base = table.data_ptr<uint8_t>();
   plan.L.tensors = reinterpret_cast<const TensorDesc*>(base);
   plan.L.chunks = reinterpret_cast<const ChunkDesc*>(base + coff);
@@ -150,15 +163,18 @@ const MTPlan& mt_plan(const TensorLists& lists) {
   plan.L.nchunks = (int32_t)chunks.size();
 
   if (c.map.size() >= Cache::kMax) {
-    // Evict the least recently used table; kernels that may still read it run on
-    // the current stream, so tie its lifetime to that stream.
-    const Key& old = c.lru.back();
-    auto oit = c.map.find(old);
-    if (oit != c.map.end()) {
+    // Evict the least recently used table that no captured graph refers to;
+    // kernels that may still read it run on the current stream, so tie its
+    // lifetime to that stream.
+    for (auto it2 = c.lru.end(); it2 != c.lru.begin();) {
+      --it2;
+      auto oit = c.map.find(*it2);
+      if (oit == c.map.end() || oit->second.plan.captured) continue;
       oit->second.plan.table.record_stream(c10::hip::getCurrentHIPStream());
       c.map.erase(oit);
+      c.lru.erase(it2);
+      break;
     }
-    c.lru.pop_back();
   }
   c.lru.push_front(key);
   auto res = c.map.emplace(key, Cache::Entry{plan, c.lru.begin()});

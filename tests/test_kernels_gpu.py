@@ -313,3 +313,26 @@ def test_bn_stats_large_mean_no_cancellation():
     torch.testing.assert_close(mean.double(), xr.mean((0, 2, 3)), rtol=1e-6, atol=1e-4)
     torch.testing.assert_close(var.double(), xr.var((0, 2, 3), unbiased=False), rtol=2e-2,
                                atol=1e-6)
+
+
+# ------------------------------------------------------------------ 1x1 conv as GEMM
+@pytest.mark.parametrize("shape", [(4, 64, 256, 14), (2, 256, 64, 7), (3, 24, 40, 5)])
+def test_conv1x1_gemm_matches_conv(shape):
+    from apex_example_amd.ops.conv import Conv2d1x1
+
+    n, ci, co, hw = shape
+    torch.manual_seed(0)
+    m = Conv2d1x1(ci, co).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(n, ci, hw, hw, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    xr = x.detach().float().clone().requires_grad_(True)
+    wr = m.weight.detach().float().clone().requires_grad_(True)
+    y = m(x)
+    yr = F.conv2d(xr, wr)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=1e-1)
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=5e-1)
