@@ -118,9 +118,10 @@ def lazy_init_with_master_weights(self):
 
 
 def post_backward_models_are_masters(scaler, params, stashed_grads, scale_override=None):
-    grads_have_scale, stashed_have_scale, out_scale = scaler.loss_scale(), 1.0, 1.0
+    # (never read scaler.loss_scale() here: in sync-free mode that is a host sync)
+    grads_have_scale, out_scale = None, 1.0
     if scale_override is not None:
-        grads_have_scale, stashed_have_scale, out_scale = scale_override
+        grads_have_scale, _, out_scale = scale_override
 
     # This is a lot of python overhead...
     grads_needing_unscale = []

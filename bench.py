@@ -166,13 +166,17 @@ def main():
     if args.graph:
         if world > 1:
             raise SystemExit("--graph is single-GPU only in this version")
-        # warm the capture path on a side stream (allocator pools, plan caches)
+        # drop every reference to an eager autograd graph (its AccumulateGrad
+        # nodes would pin the default stream), then warm the capture path on a
+        # side stream (allocator pools, multi-tensor plan caches)
+        del loss
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for _ in range(2):
+            for _ in range(3):
                 step(x, y)
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             static_loss = step(x, y)

@@ -321,3 +321,34 @@ void advance_step(int* step, const int* noop, hipStream_t st) {
 }
 
 }  // namespace amd
+
+namespace amd {
+
+// Device memcpy whose SOURCE travels in the kernel arguments: usable while a
+// hipGraph is being captured (no host buffer is referenced by the graph, and
+// no pinned allocation is needed) - used to upload multi-tensor launch tables
+// that are first built during a capture.
+struct ArgChunk {
+  uint32_t nbytes;
+  uint32_t pad;
+  uint8_t data[3584];
+};
+
+__global__ void __launch_bounds__(256) copy_from_args_kernel(uint8_t* dst, ArgChunk c) {
+  for (uint32_t i = threadIdx.x; i < c.nbytes; i += blockDim.x) dst[i] = c.data[i];
+}
+
+void upload_by_args(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  uint8_t* d = static_cast<uint8_t*>(dst);
+  for (size_t off = 0; off < bytes; off += sizeof(ArgChunk::data)) {
+    ArgChunk c;
+    size_t n = bytes - off < sizeof(c.data) ? bytes - off : sizeof(c.data);
+    c.nbytes = (uint32_t)n;
+    c.pad = 0;
+    for (size_t i = 0; i < n; ++i) c.data[i] = s[off + i];
+    hipLaunchKernelGGL(copy_from_args_kernel, dim3(1), dim3(256), 0, st, d + off, c);
+  }
+}
+
+}  // namespace amd

@@ -128,6 +128,9 @@ void update_loss_scale(float* scale, int* unskipped, int* skipped_total, const i
 
 // ----- flat buffers ---------------------------------------------------------
 // out[i] = in[i] * s (cast between dtypes), optional finiteness flag.
+// Copy host bytes to device memory through kernel arguments (graph-capture safe).
+void upload_by_args(void* dst, const void* src, size_t bytes, hipStream_t st);
+
 void flat_scale(const void* in, DType tin, void* out, DType tout, int64_t n, ScaleArg s,
                 int* noop, hipStream_t st);
 

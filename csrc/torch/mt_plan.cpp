@@ -139,23 +139,32 @@ const MTPlan& mt_plan(const TensorLists& lists) {
   const size_t total = coff + cbytes + 16;
 
   auto dev = lists[0][0].device();
-  at::Tensor host = at::empty({(int64_t)total}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-  uint8_t* hp = host.data_ptr<uint8_t>();
-  std::memset(hp, 0, total);
-  if (tbytes) std::memcpy(hp, tds.data(), tbytes);
-  if (cbytes) std::memcpy(hp + coff, chunks.data(), cbytes);
+  const bool capturing =
+      c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None;
   at::Tensor table = at::empty({(int64_t)total}, at::TensorOptions().dtype(at::kByte).device(dev));
-  // Raw async copy from a pinned image that the plan keeps alive for its whole
-  // lifetime: valid both eagerly and inside a hipGraph capture (the captured
-  // memcpy node re-reads this same, never-reused host buffer on every replay).
-  C10_HIP_CHECK(hipMemcpyAsync(table.data_ptr(), hp, total, hipMemcpyHostToDevice,
-                               c10::hip::getCurrentHIPStream().stream()));
+  at::Tensor host;
+  if (!capturing) {
+    // eager: one async copy from a pinned image kept alive with the plan
+    host = at::empty({(int64_t)total}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+    uint8_t* hp = host.data_ptr<uint8_t>();
+    std::memset(hp, 0, total);
+    if (tbytes) std::memcpy(hp, tds.data(), tbytes);
+    if (cbytes) std::memcpy(hp + coff, chunks.data(), cbytes);
+    C10_HIP_CHECK(hipMemcpyAsync(table.data_ptr(), hp, total, hipMemcpyHostToDevice,
+                                 c10::hip::getCurrentHIPStream().stream()));
+  } else {
+    // inside a hipGraph capture no pinned allocation is allowed: the image
+    // travels in kernel arguments, captured by value into the graph
+    std::vector<uint8_t> img(total, 0);
+    if (tbytes) std::memcpy(img.data(), tds.data(), tbytes);
+    if (cbytes) std::memcpy(img.data() + coff, chunks.data(), cbytes);
+    upload_by_args(table.data_ptr(), img.data(), total, c10::hip::getCurrentHIPStream().stream());
+  }
 
   MTPlan plan;
   plan.table = table;
   plan.host = host;
-  plan.captured = c10::hip::currentStreamCaptureStatusMayInitCtx() !=
-                  c10::hip::CaptureStatus::None;
+  plan.captured = capturing;
   uint8_t* base = table.data_ptr<uint8_t>();
   plan.L.tensors = reinterpret_cast<const TensorDesc*>(base);
   plan.L.chunks = reinterpret_cast<const ChunkDesc*>(base + coff);
