@@ -32,6 +32,7 @@ TensorLists sub(const TensorLists& l, std::initializer_list<int> idx) {
 
 void mt_scale_op(at::Tensor noop, const TensorLists& lists, double scale,
                  c10::optional<at::Tensor> scale_t, bool invert) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   bool gpu = mt_validate(lists, 2, 2);
   if (!gpu) return cpu::scale(noop, lists, cscale(scale, scale_t, invert));
@@ -65,6 +66,7 @@ static void by_dtype_groups(const TensorLists& lists, F&& f) {
 
 void mt_scale_any_op(at::Tensor noop, const TensorLists& lists, double scale,
                      c10::optional<at::Tensor> scale_t, bool invert) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
     mt_scale_op(noop, g, scale, scale_t, invert);
@@ -72,6 +74,7 @@ void mt_scale_any_op(at::Tensor noop, const TensorLists& lists, double scale,
 }
 
 void mt_check_finite_op(at::Tensor noop, const std::vector<at::Tensor>& list) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (list.empty()) return;
   TensorLists lists{list};
   bool gpu = mt_validate(lists, 1, 1);
@@ -85,6 +88,7 @@ void mt_check_finite_op(at::Tensor noop, const std::vector<at::Tensor>& list) {
 void mt_axpby_op(at::Tensor noop, const TensorLists& lists, double a, c10::optional<at::Tensor> a_t,
                  bool a_inv, double b, c10::optional<at::Tensor> b_t, bool b_inv,
                  int64_t arg_to_check) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   bool gpu = mt_validate(lists, 3, 3);
   if (!gpu)
@@ -97,6 +101,7 @@ void mt_axpby_op(at::Tensor noop, const TensorLists& lists, double a, c10::optio
 }
 
 void mt_zero_op(const std::vector<at::Tensor>& list) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (list.empty()) return;
   TensorLists lists{list};
   bool gpu = mt_validate(lists, 1, 1);
@@ -109,6 +114,7 @@ void mt_zero_op(const std::vector<at::Tensor>& list) {
 
 std::tuple<at::Tensor, at::Tensor> mt_norm_op(at::Tensor noop, const std::vector<at::Tensor>& list,
                                               bool per_tensor, bool max_norm) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   TORCH_CHECK(!list.empty(), "multi_tensor norm of an empty list");
   TensorLists lists{list};
   bool gpu = mt_validate(lists, 1, 1);
@@ -150,6 +156,7 @@ void mt_sgd_op(at::Tensor noop, const TensorLists& lists, double wd, double mome
                double dampening, double lr, c10::optional<at::Tensor> lr_t, bool nesterov,
                bool first_run, c10::optional<at::Tensor> first_run_flag, bool wd_after_momentum,
                double scale, c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   bool gpu = mt_validate(lists, 3, 4);
   if (!gpu) {
@@ -181,6 +188,7 @@ void mt_adam_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optio
                 double beta1, double beta2, double eps, int64_t step,
                 c10::optional<at::Tensor> step_t, int64_t mode, bool bias_correction, double wd,
                 double scale, c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   bool gpu = mt_validate(lists, 4, 5);
   if (!gpu) {
@@ -217,6 +225,7 @@ void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optio
                 bool grad_averaging, int64_t mode, c10::optional<at::Tensor> global_grad_norm,
                 double max_grad_norm, bool use_nvlamb, double scale,
                 c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   // lists: [g, p, m, v, u] or [g, p, m, v, u, p_copy]; u is an fp32 workspace
   bool gpu = mt_validate(lists, 5, 6);
@@ -269,6 +278,7 @@ void mt_novograd_op(at::Tensor noop, const TensorLists& lists, at::Tensor v, at:
                     bool bias_correction, double wd, bool grad_averaging, int64_t mode,
                     int64_t norm_type, double scale, c10::optional<at::Tensor> scale_t,
                     bool scale_inv) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   bool gpu = mt_validate(lists, 3, 3);
   if (!gpu) {
@@ -311,6 +321,7 @@ void mt_novograd_op(at::Tensor noop, const TensorLists& lists, at::Tensor v, at:
 void mt_adagrad_op(at::Tensor noop, const TensorLists& lists, double lr,
                    c10::optional<at::Tensor> lr_t, double eps, int64_t mode, double wd,
                    double scale, c10::optional<at::Tensor> scale_t, bool scale_inv) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
   bool gpu = mt_validate(lists, 3, 3);
   if (!gpu) {
@@ -333,6 +344,7 @@ void mt_adagrad_op(at::Tensor noop, const TensorLists& lists, double lr,
 void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, c10::optional<at::Tensor> skipped,
                           at::Tensor overflow, double factor, int64_t window, double min_scale,
                           double max_scale, bool dynamic) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   TORCH_CHECK(scale.scalar_type() == at::kFloat && unskipped.scalar_type() == at::kInt &&
                   overflow.scalar_type() == at::kInt,
               "update_loss_scale: bad dtypes");
@@ -346,6 +358,7 @@ void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, c10::optional<
 }
 
 void advance_step_op(at::Tensor step, c10::optional<at::Tensor> noop) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   TORCH_CHECK(step.scalar_type() == at::kInt, "step counter must be int32");
   if (!step.is_cuda()) {
     bool skip = noop.has_value() && noop->defined() && noop->item<int>() != 0;
@@ -356,6 +369,7 @@ void advance_step_op(at::Tensor step, c10::optional<at::Tensor> noop) {
 }
 
 void mark_step_done_op(at::Tensor flag, c10::optional<at::Tensor> noop) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   TORCH_CHECK(flag.scalar_type() == at::kInt, "flag must be int32");
   if (!flag.is_cuda()) {
     bool skip = noop.has_value() && noop->defined() && noop->item<int>() != 0;
@@ -367,6 +381,7 @@ void mark_step_done_op(at::Tensor flag, c10::optional<at::Tensor> noop) {
 
 void flat_scale_op(at::Tensor in, at::Tensor out, double scale, c10::optional<at::Tensor> scale_t,
                    bool invert, c10::optional<at::Tensor> noop) {
+  c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   TORCH_CHECK(in.is_contiguous() && (!out.defined() || out.is_contiguous()), "contiguous only");
   if (!in.is_cuda()) {
     float s = (float)scale;

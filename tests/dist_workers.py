@@ -1,0 +1,170 @@
+"""Worker functions for the multi-process (gloo, CPU) distributed tests.
+
+Each worker initialises torch.distributed on 127.0.0.1, runs one scenario and
+writes its results with torch.save to <out>/rank<r>.pt (files this test suite
+writes itself)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(rank, world, port, fn_name, out, kw):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = globals()[fn_name](rank, world, **kw)
+        torch.save(res, os.path.join(out, "rank%d.pt" % rank))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run(fn_name, world, out, **kw):
+    mp.spawn(_entry, args=(world, free_port(), fn_name, out, kw), nprocs=world, join=True)
+    return [torch.load(os.path.join(out, "rank%d.pt" % r), weights_only=False)
+            for r in range(world)]
+
+
+def _mlp():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 32), nn.ReLU(),
+                         nn.Linear(32, 4))
+
+
+def _data(n=8, seed=123):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, 16, generator=g), torch.randint(0, 4, (n,), generator=g)
+
+
+# ---------------------------------------------------------------------- DDP
+def ddp_grads(rank, world, message_size=10_000_000, delay=False, predivide=1.0, average=True,
+              fp32=False, iters=2, streams=1):
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    model = _mlp()
+    if rank == 1:  # different init on rank 1: DDP must broadcast rank 0's params
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(1.0)
+    ddp = DistributedDataParallel(model, message_size=message_size, delay_allreduce=delay,
+                                  gradient_predivide_factor=predivide, gradient_average=average,
+                                  allreduce_always_fp32=fp32, num_allreduce_streams=streams)
+    x, y = _data(8 * world)
+    xs, ys = x.chunk(world)[rank], y.chunk(world)[rank]
+    out = {}
+    for it in range(iters):
+        for p in model.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        loss = F.cross_entropy(ddp(xs), ys)
+        loss.backward()
+        out["grads%d" % it] = [p.grad.detach().clone() for p in model.parameters()]
+    out["params"] = [p.detach().clone() for p in model.parameters()]
+    out["layout"] = ddp.bucket_layout()
+    out["views"] = all(getattr(p, "_amd_grad_is_bucket_view", False) for p in model.parameters())
+    return out
+
+
+def ddp_train_amp(rank, world, inject_rank=-1):
+    """amp O2 (bf16, CPU) + DDP + FusedSGD: training + overflow consensus."""
+    from apex_example_amd import amp
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    model = _mlp()
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
+    model, opt = amp.initialize(model, opt, opt_level="O2", half_dtype=torch.bfloat16,
+                                verbosity=0)
+    ddp = DistributedDataParallel(model, message_size=200)
+    x, y = _data(8 * world, seed=7)
+    xs, ys = x.chunk(world)[rank], y.chunk(world)[rank]
+    losses = []
+    for it in range(4):
+        loss = F.cross_entropy(ddp(xs), ys)
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        if it == 2:
+            before = [p.detach().clone() for p in amp.master_params(opt)]
+        opt.step()
+        if it == 2:
+            after = [p.detach().clone() for p in amp.master_params(opt)]
+        losses.append(loss.item())
+        if it == 1 and rank == inject_rank:
+            xs = xs.clone()
+            xs[0, 0] = float("inf")
+        elif it == 2:
+            xs = x.chunk(world)[rank]
+    return {"losses": losses, "scale": amp.state_dict()["loss_scaler0"]["loss_scale"],
+            "skipped_unchanged": all(torch.equal(a, b) for a, b in zip(before, after)),
+            "masters": [p.detach().clone() for p in amp.master_params(opt)]}
+
+
+def reducer_manual(rank, world):
+    from apex_example_amd.parallel import Reducer
+
+    model = _mlp()
+    if rank == 1:
+        with torch.no_grad():
+            for p in model.parameters():
+                p.mul_(3.0)
+    red = Reducer(model)
+    for p in model.parameters():
+        p.grad = torch.full_like(p, float(rank + 1))
+    red.reduce()
+    return {"params": [p.detach().clone() for p in model.parameters()],
+            "grads": [p.grad.clone() for p in model.parameters()]}
+
+
+# ---------------------------------------------------------------------- SyncBN
+def syncbn_step(rank, world, sizes=(4, 6), channel_last=False, fuse_relu=False, python=False,
+                fmt="nchw"):
+    from apex_example_amd.parallel import SyncBatchNorm, SyncBatchNormPython
+
+    cls = SyncBatchNormPython if python else SyncBatchNorm
+    torch.manual_seed(0)
+    C = 8
+    full = torch.randn(sum(sizes), C, 5, 5) * 2 + 1
+    off = sum(sizes[:rank])
+    x = full[off:off + sizes[rank]].clone()
+    if fmt == "nhwc":
+        x = x.to(memory_format=torch.channels_last)
+    if channel_last:
+        x = x.permute(0, 2, 3, 1).contiguous()
+    x.requires_grad_(True)
+    bn = cls(C, channel_last=channel_last, fuse_relu=fuse_relu)
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+        bn.bias.copy_(torch.linspace(-1, 1, C))
+    y = bn(x)
+    g = torch.Generator().manual_seed(99)
+    dy_full = torch.randn(sum(sizes), C, 5, 5, generator=g)
+    dy = dy_full[off:off + sizes[rank]]
+    if channel_last:
+        dy = dy.permute(0, 2, 3, 1)
+    (y * dy).sum().backward()
+    return {"y": y.detach(), "dx": x.grad.detach(), "dw": bn.weight.grad.clone(),
+            "db": bn.bias.grad.clone(), "rm": bn.running_mean.clone(),
+            "rv": bn.running_var.clone()}
+
+
+def syncbn_groups(rank, world):
+    from apex_example_amd.parallel import create_syncbn_process_group
+
+    g = create_syncbn_process_group(2)
+    return {"group_size": dist.get_world_size(g), "group_rank": dist.get_rank(g)}

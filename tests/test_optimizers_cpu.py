@@ -1,0 +1,178 @@
+"""Fused optimizers vs torch.optim / Python references (C++ CPU path)."""
+import math
+
+import pytest
+import torch
+
+from apex_example_amd.optimizers import FusedAdagrad, FusedAdam, FusedLAMB, FusedNovoGrad, FusedSGD
+from apex_example_amd.parallel import LARC
+
+
+def _pair(sizes=(10, 300, 7)):
+    torch.manual_seed(0)
+    ps = [torch.randn(n, requires_grad=True) for n in sizes]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    return ps, ref
+
+
+def _set_grads(a, b, seed):
+    g = torch.Generator().manual_seed(seed)
+    for p, r in zip(a, b):
+        gr = torch.randn(p.shape, generator=g)
+        p.grad = gr.clone()
+        r.grad = gr.clone()
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_fused_sgd(nesterov):
+    ps, ref = _pair()
+    o1 = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=nesterov)
+    o2 = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=nesterov)
+    for i in range(4):
+        _set_grads(ps, ref, i)
+        o1.step()
+        o2.step()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r)
+
+
+def test_fused_sgd_dampening_and_state_dict():
+    ps, ref = _pair()
+    o1 = FusedSGD(ps, lr=0.1, momentum=0.9, dampening=0.1)
+    o2 = torch.optim.SGD(ref, lr=0.1, momentum=0.9, dampening=0.1)
+    for i in range(3):
+        _set_grads(ps, ref, i)
+        o1.step()
+        o2.step()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r)
+    sd = o1.state_dict()
+    assert "momentum_buffer" in sd["state"][0]
+
+
+@pytest.mark.parametrize("adam_w_mode,cls", [(True, torch.optim.AdamW), (False, torch.optim.Adam)])
+def test_fused_adam(adam_w_mode, cls):
+    ps, ref = _pair()
+    o1 = FusedAdam(ps, lr=1e-2, weight_decay=0.05, adam_w_mode=adam_w_mode)
+    o2 = cls(ref, lr=1e-2, weight_decay=0.05)
+    for i in range(5):
+        _set_grads(ps, ref, i)
+        o1.step()
+        o2.step()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
+    assert o1.param_groups[0]["step"] == 5  # per-group step (apex checkpoint format)
+
+
+def test_fused_adam_rejects_amsgrad_and_legacy_step():
+    with pytest.raises(RuntimeError):
+        FusedAdam([torch.zeros(1, requires_grad=True)], amsgrad=True)
+    o = FusedAdam([torch.zeros(1, requires_grad=True)])
+    with pytest.raises(RuntimeError, match="FusedAdam has been updated"):
+        o.step(grads=[1])
+
+
+def _ref_lamb(ps, grads, state, step, lr, b1, b2, eps, wd, max_norm, adam_w=True):
+    gn = math.sqrt(sum(float((g.double() ** 2).sum()) for g in grads))
+    clip = gn / max_norm if gn > max_norm else 1.0
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    for i, (p, g) in enumerate(zip(ps, grads)):
+        m, v = state[i]
+        gi = g / clip
+        if not adam_w:
+            gi = gi + wd * p
+        m.mul_(b1).add_(gi, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gi, gi, value=1 - b2)
+        u = (m / bc1) / ((v / bc2).sqrt() + eps)
+        if adam_w:
+            u = u + wd * p
+        pn, un = p.norm(), u.norm()
+        ratio = (pn / un).item() if (pn > 0 and un > 0) else 1.0
+        p.sub_(lr * ratio * u)
+
+
+@pytest.mark.parametrize("adam_w_mode", [True, False])
+def test_fused_lamb(adam_w_mode):
+    ps, _ = _pair((64, 1000))
+    ref = [p.detach().clone() for p in ps]
+    st = [(torch.zeros_like(p), torch.zeros_like(p)) for p in ref]
+    opt = FusedLAMB(ps, lr=1e-2, weight_decay=0.01, adam_w_mode=adam_w_mode, max_grad_norm=1.0)
+    for step in range(1, 4):
+        g = torch.Generator().manual_seed(step)
+        grads = [torch.randn(p.shape, generator=g) * 2 for p in ps]
+        for p, gr in zip(ps, grads):
+            p.grad = gr.clone()
+        opt.step()
+        _ref_lamb(ref, grads, st, step, 1e-2, 0.9, 0.999, 1e-6, 0.01, 1.0, adam_w_mode)
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.detach(), r, rtol=1e-4, atol=1e-6)
+
+
+def test_fused_novograd_reference():
+    ps, _ = _pair((50, 200))
+    ref = [p.detach().clone() for p in ps]
+    m = [torch.zeros_like(p) for p in ref]
+    v = [0.0 for _ in ref]
+    b1, b2, lr, eps, wd = 0.95, 0.98, 1e-2, 1e-8, 0.01
+    opt = FusedNovoGrad(ps, lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    for step in range(1, 4):
+        g = torch.Generator().manual_seed(step)
+        grads = [torch.randn(p.shape, generator=g) for p in ps]
+        for p, gr in zip(ps, grads):
+            p.grad = gr.clone()
+        opt.step()
+        bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+        for i, (p, gr) in enumerate(zip(ref, grads)):
+            n = gr.norm().item()
+            v[i] = n if step == 1 else math.sqrt(b2 * v[i] ** 2 + (1 - b2) * n * n)
+            ghat = gr / (v[i] / math.sqrt(bc2) + eps)
+            m[i].mul_(b1).add_(ghat, alpha=1 - b1)
+            p.sub_(lr * (m[i] / bc1 + wd * p))
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.detach(), r, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_adagrad_matches_torch():
+    ps, ref = _pair()
+    o1 = FusedAdagrad(ps, lr=0.1, eps=1e-10, weight_decay=0.01)
+    o2 = torch.optim.Adagrad(ref, lr=0.1, eps=1e-10, weight_decay=0.01)
+    for i in range(4):
+        _set_grads(ps, ref, i)
+        o1.step()
+        o2.step()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
+
+
+def test_zero_grad_set_none_default():
+    ps, _ = _pair()
+    o = FusedAdam(ps)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    o.zero_grad()
+    assert all(p.grad is None for p in ps)
+    o2 = FusedSGD(ps, lr=0.1)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    o2.zero_grad()
+    assert all(float(p.grad.abs().sum()) == 0 for p in ps)
+
+
+@pytest.mark.parametrize("clip", [True, False])
+def test_larc(clip):
+    torch.manual_seed(0)
+    ps = [torch.randn(20, requires_grad=True), torch.randn(30, requires_grad=True)]
+    ref = [p.detach().clone() for p in ps]
+    opt = LARC(torch.optim.SGD(ps, lr=0.1, weight_decay=1e-3), trust_coefficient=0.02, clip=clip)
+    grads = [torch.randn_like(p) for p in ps]
+    for p, g in zip(ps, grads):
+        p.grad = g.clone()
+    opt.step()
+    assert opt.param_groups[0]["weight_decay"] == 1e-3  # restored
+    for p, r, g in zip(ps, ref, grads):
+        pn, gn = r.norm(), g.norm()
+        alr = 0.02 * pn / (gn + pn * 1e-3 + 1e-8)
+        if clip:
+            alr = min(alr / 0.1, 1.0)
+        exp = r - 0.1 * (g + 1e-3 * r) * alr
+        torch.testing.assert_close(p.detach(), exp, rtol=1e-5, atol=1e-6)

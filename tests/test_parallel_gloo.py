@@ -1,0 +1,145 @@
+"""Multi-process DDP / SyncBN / Reducer tests on CPU with the gloo backend
+(world_size 2 and 3), mirroring apex tests/distributed."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dist_workers as W
+
+
+def _single_process_grads():
+    model = W._mlp()
+    x, y = W._data(16)
+    loss = F.cross_entropy(model(x), y)
+    loss.backward()
+    return [p.grad.clone() for p in model.parameters()]
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),
+    dict(message_size=300),            # several buckets, overlapped launches
+    dict(message_size=1),              # one bucket per parameter
+    dict(delay=True),                  # all buckets at the end of backward
+    dict(predivide=2.0, message_size=500),
+    dict(fp32=True, message_size=700),
+    dict(streams=2, message_size=300),  # round-robin over two communicators
+])
+def test_ddp_matches_full_batch(tmp_path, kw):
+    res = W.run("ddp_grads", 2, str(tmp_path), **kw)
+    ref = _single_process_grads()
+    for r in res:
+        assert r["views"]
+        for it in range(2):
+            for g, gr in zip(r["grads%d" % it], ref):
+                torch.testing.assert_close(g, gr, rtol=1e-5, atol=1e-6)
+    # identical bucket layout and params on every rank (rank 0's broadcast wins)
+    assert res[0]["layout"] == res[1]["layout"]
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        assert torch.equal(a, b)
+    if kw.get("message_size") == 1:
+        assert len(res[0]["layout"]) == 6
+
+
+def test_ddp_sum_without_average(tmp_path):
+    res = W.run("ddp_grads", 2, str(tmp_path), average=False)
+    ref = _single_process_grads()
+    for g, gr in zip(res[0]["grads0"], ref):
+        torch.testing.assert_close(g, 2 * gr, rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_world3(tmp_path):
+    res = W.run("ddp_grads", 3, str(tmp_path), message_size=400)
+    model = W._mlp()
+    x, y = W._data(24)
+    F.cross_entropy(model(x), y).backward()
+    for r in res:
+        for g, p in zip(r["grads0"], model.parameters()):
+            torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_amp_ddp_training_and_overflow_consensus(tmp_path):
+    res = W.run("ddp_train_amp", 2, str(tmp_path), inject_rank=1)
+    # rank 1 saw inf at iteration 2; after the all-reduce BOTH ranks skip
+    for r in res:
+        assert r["skipped_unchanged"]
+        assert r["scale"] == 32768.0
+    for a, b in zip(res[0]["masters"], res[1]["masters"]):
+        assert torch.equal(a, b)
+
+
+def test_manual_reducer(tmp_path):
+    res = W.run("reducer_manual", 2, str(tmp_path))
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        assert torch.equal(a, b)
+    for g in res[0]["grads"]:
+        assert torch.allclose(g, torch.full_like(g, 1.5))
+
+
+def _bn_reference(sizes, fmt="nchw", fuse_relu=False):
+    torch.manual_seed(0)
+    C = 8
+    full = (torch.randn(sum(sizes), C, 5, 5) * 2 + 1).requires_grad_(True)
+    bn = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+        bn.bias.copy_(torch.linspace(-1, 1, C))
+    y = bn(full)
+    if fuse_relu:
+        y = torch.relu(y)
+    g = torch.Generator().manual_seed(99)
+    dy = torch.randn(sum(sizes), C, 5, 5, generator=g)
+    (y * dy).sum().backward()
+    return y.detach(), full.grad, bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var
+
+
+@pytest.mark.parametrize("python", [False, True])
+@pytest.mark.parametrize("sizes", [(4, 4), (3, 7)])
+def test_syncbn_matches_global_batch_bn(tmp_path, python, sizes):
+    res = W.run("syncbn_step", 2, str(tmp_path), sizes=sizes, python=python)
+    y, dx, dw, db, rm, rv = _bn_reference(sizes)
+    off = 0
+    for r, n in zip(res, sizes):
+        torch.testing.assert_close(r["y"], y[off:off + n], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(r["dx"], dx[off:off + n], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(r["rm"], rm, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(r["rv"], rv, rtol=1e-5, atol=1e-6)
+        off += n
+    # weight/bias grads are LOCAL (DDP all-reduces them): they sum to the global ones
+    torch.testing.assert_close(res[0]["dw"] + res[1]["dw"], dw, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(res[0]["db"] + res[1]["db"], db, rtol=1e-4, atol=1e-4)
+
+
+def test_syncbn_channels_last_format_and_fused_relu(tmp_path):
+    sizes = (4, 4)
+    res = W.run("syncbn_step", 2, str(tmp_path), sizes=sizes, fmt="nhwc", fuse_relu=True)
+    y, dx, *_ = _bn_reference(sizes, fuse_relu=True)
+    torch.testing.assert_close(res[1]["y"], y[4:], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(res[1]["dx"], dx[4:], rtol=1e-4, atol=1e-5)
+
+
+def test_syncbn_apex_channel_last_shape(tmp_path):
+    sizes = (4, 4)
+    res = W.run("syncbn_step", 2, str(tmp_path), sizes=sizes, channel_last=True)
+    y, dx, *_ = _bn_reference(sizes)
+    torch.testing.assert_close(res[0]["y"], y[:4].permute(0, 2, 3, 1), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(res[0]["dx"], dx[:4].permute(0, 2, 3, 1), rtol=1e-4, atol=1e-5)
+
+
+def test_create_syncbn_process_group(tmp_path):
+    res = W.run("syncbn_groups", 4, str(tmp_path))
+    assert [r["group_size"] for r in res] == [2, 2, 2, 2]
+    assert [r["group_rank"] for r in res] == [0, 1, 0, 1]
+
+
+def test_convert_syncbn_model():
+    from apex_example_amd.parallel import SyncBatchNorm, convert_syncbn_model
+    from apex_example_amd.models import resnet18
+
+    m = resnet18(num_classes=10)
+    rm = m.bn1.bn.running_mean
+    m2 = convert_syncbn_model(m)
+    bns = [mod for mod in m2.modules() if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm)]
+    assert bns and all(isinstance(b, SyncBatchNorm) for b in bns)
+    assert m2.bn1.bn.running_mean is rm  # running buffers shared
+    inst = torch.nn.InstanceNorm2d(4)
+    assert convert_syncbn_model(inst) is inst
