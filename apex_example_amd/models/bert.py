@@ -1,0 +1,176 @@
+"""BERT (Devlin et al. 2018) for pre-training, defined in-repo (no transformers
+download): post-LN encoder with FusedLayerNorm, fused QKV projection, PyTorch
+SDPA attention (CK / AOTriton flash attention on ROCm), masked-LM head on the
+gathered masked positions only (NVIDIA's pretraining recipe, max_predictions
+per sequence) with the decoder tied to the word embeddings, and the NSP head.
+
+bert_large(): 24 layers, hidden 1024, 16 heads, FFN 4096, vocab 30522 (padded to
+a multiple of 8 optionally), 512 positions.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..normalization import FusedLayerNorm
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden_size: int = 1024
+    num_hidden_layers: int = 24
+    num_attention_heads: int = 16
+    intermediate_size: int = 4096
+    hidden_dropout_prob: float = 0.1
+    attention_probs_dropout_prob: float = 0.1
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    initializer_range: float = 0.02
+    layer_norm_eps: float = 1e-12
+    fused_layer_norm: bool = True
+
+
+def _ln(cfg, n):
+    if cfg.fused_layer_norm:
+        return FusedLayerNorm(n, eps=cfg.layer_norm_eps)
+    return nn.LayerNorm(n, eps=cfg.layer_norm_eps)
+
+
+class BertEmbeddings(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.position_embeddings = nn.Embedding(cfg.max_position_embeddings, cfg.hidden_size)
+        self.token_type_embeddings = nn.Embedding(cfg.type_vocab_size, cfg.hidden_size)
+        self.LayerNorm = _ln(cfg, cfg.hidden_size)
+        self.dropout = nn.Dropout(cfg.hidden_dropout_prob)
+
+    def forward(self, input_ids, token_type_ids):
+        s = input_ids.size(1)
+        pos = torch.arange(s, device=input_ids.device).unsqueeze(0)
+        e = self.word_embeddings(input_ids) + self.position_embeddings(pos) + \
+            self.token_type_embeddings(token_type_ids)
+        return self.dropout(self.LayerNorm(e))
+
+
+class BertSelfAttention(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.h = cfg.num_attention_heads
+        self.d = cfg.hidden_size // cfg.num_attention_heads
+        self.qkv = nn.Linear(cfg.hidden_size, 3 * cfg.hidden_size)
+        self.dense = nn.Linear(cfg.hidden_size, cfg.hidden_size)
+        self.p = cfg.attention_probs_dropout_prob
+
+    def forward(self, x, attn_mask=None):
+        b, s, hd = x.shape
+        qkv = self.qkv(x).view(b, s, 3, self.h, self.d).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask,
+                                           dropout_p=self.p if self.training else 0.0)
+        o = o.transpose(1, 2).reshape(b, s, hd)
+        return self.dense(o)
+
+
+class BertLayer(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.attention = BertSelfAttention(cfg)
+        self.attn_dropout = nn.Dropout(cfg.hidden_dropout_prob)
+        self.attn_ln = _ln(cfg, cfg.hidden_size)
+        self.intermediate = nn.Linear(cfg.hidden_size, cfg.intermediate_size)
+        self.output = nn.Linear(cfg.intermediate_size, cfg.hidden_size)
+        self.out_dropout = nn.Dropout(cfg.hidden_dropout_prob)
+        self.out_ln = _ln(cfg, cfg.hidden_size)
+
+    def forward(self, x, attn_mask=None):
+        x = self.attn_ln(x + self.attn_dropout(self.attention(x, attn_mask)))
+        h = F.gelu(self.intermediate(x))
+        return self.out_ln(x + self.out_dropout(self.output(h)))
+
+
+class BertModel(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.config = cfg
+        self.embeddings = BertEmbeddings(cfg)
+        self.layers = nn.ModuleList([BertLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.pooler = nn.Linear(cfg.hidden_size, cfg.hidden_size)
+
+    def forward(self, input_ids, token_type_ids, attention_mask=None):
+        x = self.embeddings(input_ids, token_type_ids)
+        mask = None
+        if attention_mask is not None:
+            # [b, s] 1 = keep -> additive [b, 1, 1, s]
+            mask = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0
+        for layer in self.layers:
+            x = layer(x, mask)
+        pooled = torch.tanh(self.pooler(x[:, 0]))
+        return x, pooled
+
+
+class BertForPreTraining(nn.Module):
+    """Returns (masked-LM logits at the masked positions, NSP logits)."""
+
+    def __init__(self, cfg: BertConfig):
+        super().__init__()
+        self.config = cfg
+        self.bert = BertModel(cfg)
+        self.transform = nn.Linear(cfg.hidden_size, cfg.hidden_size)
+        self.transform_ln = _ln(cfg, cfg.hidden_size)
+        self.decoder_bias = nn.Parameter(torch.zeros(cfg.vocab_size))
+        self.nsp = nn.Linear(cfg.hidden_size, 2)
+        self.apply(self._init)
+
+    def _init(self, m):
+        std = self.config.initializer_range
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, std=std)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, std=std)
+
+    def forward(self, input_ids, token_type_ids, masked_positions, attention_mask=None):
+        seq, pooled = self.bert(input_ids, token_type_ids, attention_mask)
+        b, s, h = seq.shape
+        idx = masked_positions + (torch.arange(b, device=seq.device) * s).unsqueeze(1)
+        sel = seq.reshape(b * s, h).index_select(0, idx.reshape(-1))
+        t = self.transform_ln(F.gelu(self.transform(sel)))
+        logits = F.linear(t, self.bert.embeddings.word_embeddings.weight, self.decoder_bias)
+        return logits, self.nsp(pooled)
+
+
+def pretraining_loss(mlm_logits, nsp_logits, mlm_labels, nsp_labels):
+    mlm = F.cross_entropy(mlm_logits.float(), mlm_labels.reshape(-1), ignore_index=-1)
+    nsp = F.cross_entropy(nsp_logits.float(), nsp_labels)
+    return mlm + nsp
+
+
+def bert_large(**kw):
+    return BertForPreTraining(BertConfig(**kw))
+
+
+def bert_base(**kw):
+    kw.setdefault("hidden_size", 768)
+    kw.setdefault("num_hidden_layers", 12)
+    kw.setdefault("num_attention_heads", 12)
+    kw.setdefault("intermediate_size", 3072)
+    return BertForPreTraining(BertConfig(**kw))
+
+
+def synthetic_batch(cfg: BertConfig, batch, seq_len, max_pred, device, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ids = torch.randint(0, cfg.vocab_size, (batch, seq_len), generator=g)
+    tt = torch.zeros(batch, seq_len, dtype=torch.long)
+    tt[:, seq_len // 2:] = 1
+    pos = torch.stack([torch.randperm(seq_len, generator=g)[:max_pred].sort().values
+                       for _ in range(batch)])
+    labels = torch.randint(0, cfg.vocab_size, (batch, max_pred), generator=g)
+    nsp = torch.randint(0, 2, (batch,), generator=g)
+    return [t.to(device) for t in (ids, tt, pos, labels, nsp)]

@@ -1,0 +1,130 @@
+"""GPT-2 (Radford et al. 2019) language model defined in-repo: pre-LN decoder
+blocks with FusedLayerNorm, causal SDPA attention (flash attention on ROCm),
+tanh-GELU MLP and an LM head tied to the token embedding.
+
+gpt2_medium(): 24 layers, d_model 1024, 16 heads, vocab 50257, 1024 positions
+= 354,823,168 parameters in 292 tensors.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..normalization import FusedLayerNorm
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 1024
+    n_layer: int = 24
+    n_head: int = 16
+    resid_pdrop: float = 0.1
+    embd_pdrop: float = 0.1
+    attn_pdrop: float = 0.1
+    layer_norm_epsilon: float = 1e-5
+    initializer_range: float = 0.02
+    fused_layer_norm: bool = True
+
+
+def _ln(cfg, n):
+    if cfg.fused_layer_norm:
+        return FusedLayerNorm(n, eps=cfg.layer_norm_epsilon)
+    return nn.LayerNorm(n, eps=cfg.layer_norm_epsilon)
+
+
+class GPT2Attention(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.h = cfg.n_head
+        self.d = cfg.n_embd // cfg.n_head
+        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.p = cfg.attn_pdrop
+        self.resid_dropout = nn.Dropout(cfg.resid_pdrop)
+
+    def forward(self, x):
+        b, s, e = x.shape
+        qkv = self.c_attn(x).view(b, s, 3, self.h, self.d).permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], is_causal=True,
+                                           dropout_p=self.p if self.training else 0.0)
+        o = o.transpose(1, 2).reshape(b, s, e)
+        return self.resid_dropout(self.c_proj(o))
+
+
+class GPT2MLP(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.dropout = nn.Dropout(cfg.resid_pdrop)
+
+    def forward(self, x):
+        return self.dropout(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+
+
+class GPT2Block(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.ln_1 = _ln(cfg, cfg.n_embd)
+        self.attn = GPT2Attention(cfg)
+        self.ln_2 = _ln(cfg, cfg.n_embd)
+        self.mlp = GPT2MLP(cfg)
+
+    def forward(self, x):
+        x = x + self.attn(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class GPT2LMHeadModel(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.config = cfg
+        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.drop = nn.Dropout(cfg.embd_pdrop)
+        self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = _ln(cfg, cfg.n_embd)
+        self.apply(self._init)
+        # GPT-2: scale the residual projections by 1/sqrt(2 * n_layer)
+        for name, p in self.named_parameters():
+            if name.endswith("c_proj.weight"):
+                nn.init.normal_(p, std=cfg.initializer_range / (2 * cfg.n_layer) ** 0.5)
+
+    def _init(self, m):
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, std=self.config.initializer_range)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, std=self.config.initializer_range)
+
+    def forward(self, input_ids):
+        s = input_ids.size(1)
+        pos = torch.arange(s, device=input_ids.device).unsqueeze(0)
+        x = self.drop(self.wte(input_ids) + self.wpe(pos))
+        for block in self.h:
+            x = block(x)
+        x = self.ln_f(x)
+        return F.linear(x, self.wte.weight)  # tied LM head
+
+
+def lm_loss(logits, input_ids):
+    """Next-token cross entropy (fp32 softmax)."""
+    return F.cross_entropy(logits[:, :-1].reshape(-1, logits.size(-1)).float(),
+                           input_ids[:, 1:].reshape(-1))
+
+
+def gpt2_medium(**kw):
+    return GPT2LMHeadModel(GPT2Config(**kw))
+
+
+def gpt2_small(**kw):
+    kw.setdefault("n_embd", 768)
+    kw.setdefault("n_layer", 12)
+    kw.setdefault("n_head", 12)
+    return GPT2LMHeadModel(GPT2Config(**kw))

@@ -9,13 +9,18 @@ Step = forward + loss + amp.scale_loss backward (+ bucketed RCCL all-reduce
 overlapped with backward when N > 1) + FusedSGD step (momentum 0.9, wd 5e-5,
 fp32 master weights, bf16 model copy written in-kernel).  Synthetic ImageNet
 shaped data (224x224, 1000 classes) generated on the device per rank;
-random-init weights.  W untimed warmup steps (MIOpen solver search happens
-there), then exactly K timed steps bracketed by barrier + synchronize; the
-slowest rank's time is reported.
+random-init weights.  W untimed warmup steps, then exactly K timed steps
+bracketed by barrier + synchronize; the slowest rank's time is reported.
+
+Other BASELINE.json configs (same harness):
+  --model bert_large   BERT-large pretraining, amp O2 + FusedLAMB + FusedLayerNorm
+                       (sequences/sec; seq 512, 80 masked predictions / sequence)
+  --model gpt2_medium  GPT-2-medium LM, amp O1 fp16 + FusedAdam, dynamic loss
+                       scaling (tokens/sec; seq 1024)
 
 ``--impl stock`` runs the same model / data / schedule on the stock
-PyTorch-ROCm path (torch.autocast bf16 + torch.optim.SGD(fused) + torch DDP,
-plain BatchNorm) - the comparator of BASELINE.md section 2.
+PyTorch-ROCm path (torch.autocast + torch.optim fused + torch DDP, plain
+BatchNorm / LayerNorm) - the comparator of BASELINE.md section 2.
 """
 from __future__ import annotations
 
@@ -32,9 +37,10 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Baseline for vs_baseline: BASELINE.md has no published number; the comparator
-# is the stock PyTorch-ROCm path measured on the same MI355X.
-STOCK_BASELINE_IMG_S_PER_GPU = None
+# vs_baseline: BASELINE.md publishes no number for the reference; the comparator
+# is the stock PyTorch-ROCm path measured on MI355X with this same harness
+# (BASELINE.md section 2), per GPU, bs 256.
+STOCK_BASELINE_PER_GPU = {"resnet50": 6011.4}
 
 
 def parse():
@@ -42,12 +48,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=15)
-    ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--batch-size", type=int, default=256, help="per GPU")
+    ap.add_argument("--model", default="resnet50",
+                    choices=["resnet50", "resnet18", "bert_large", "gpt2_medium"])
+    ap.add_argument("--batch-size", type=int, default=None, help="per GPU")
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--impl", choices=["amd", "stock"], default="amd")
-    ap.add_argument("--opt-level", default="O2")
-    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16")
+    ap.add_argument("--opt-level", default=None)
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default=None)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true")
     ap.add_argument("--syncbn", action="store_true", help="SyncBatchNorm across ranks")
@@ -57,10 +65,10 @@ def parse():
                     help="keep MIOpen for the stride-1 1x1 convs (default: hipBLASLt GEMM)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step in a hipGraph and replay it")
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--deterministic", action="store_true")
-    # MIOpen immediate mode measured as fast as exhaustive find for this model on
-    # MI355X (docs/PERF.md) and it avoids ~200 s of solver search on a fresh box.
+    # MIOpen immediate mode measured as fast as exhaustive find for ResNet-50 on
+    # MI355X (docs/PERF.md) and avoids ~200 s of solver search on a fresh box.
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="MIOpen find (solver search) instead of immediate mode")
     ap.add_argument("--opt-step-iters", type=int, default=20)
@@ -73,13 +81,20 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build(args, device, world):
+class Workload:
+    """step(batch) -> loss, opt_only(), batch, units/step/GPU, metric, unit, config."""
+
+
+def build_resnet(args, device, world):
     from apex_example_amd import amp
-    from apex_example_amd.models import resnet50, resnet18
+    from apex_example_amd.models import resnet18, resnet50
     from apex_example_amd.optimizers import FusedSGD
     from apex_example_amd.parallel import DistributedDataParallel, convert_syncbn_model
 
-    half = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    half = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    bs = args.batch_size or 256
+    lr = args.lr or 0.1
+    opt_level = args.opt_level or "O2"
     ctor = {"resnet50": resnet50, "resnet18": resnet18}[args.model]
     fused_bn = args.impl == "amd" and not args.no_fused_bn
     gemm_1x1 = args.impl == "amd" and not args.no_gemm_1x1
@@ -91,47 +106,180 @@ def build(args, device, world):
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
     mf = torch.channels_last if not args.no_channels_last else torch.contiguous_format
     model = model.to(memory_format=mf)
-
+    x = torch.randn(bs, 3, args.image_size, args.image_size, device=device).to(memory_format=mf)
+    y = torch.randint(0, 1000, (bs,), device=device)
+    w = Workload()
     if args.impl == "amd":
-        opt = FusedSGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5,
+        opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5,
                        materialize_master_grads=args.materialize_master_grads)
-        model, opt = amp.initialize(model, opt, opt_level=args.opt_level, half_dtype=half,
+        model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half,
                                     verbosity=0)
         if world > 1:
             model = DistributedDataParallel(model, message_size=args.message_size)
 
-        def step(x, y):
-            out = model(x)
-            loss = F.cross_entropy(out, y)
+        def step(b):
+            out = model(b[0])
+            loss = F.cross_entropy(out, b[1])
             opt.zero_grad()
             with amp.scale_loss(loss, opt) as scaled:
                 scaled.backward()
             opt.step()
             return loss
-
-        def opt_only():
-            opt.step()
     else:
-        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5,
+        opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5,
                               fused=True)
         scaler = torch.amp.GradScaler("cuda", enabled=(half == torch.float16))
         if world > 1:
             model = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[device.index], bucket_cap_mb=25, gradient_as_bucket_view=True)
 
-        def step(x, y):
+        def step(b):
             with torch.autocast("cuda", dtype=half):
-                out = model(x)
-                loss = F.cross_entropy(out, y)
+                loss = F.cross_entropy(model(b[0]), b[1])
             opt.zero_grad(set_to_none=True)
             scaler.scale(loss).backward()
             scaler.step(opt)
             scaler.update()
             return loss
+    w.step, w.opt_only, w.batch = step, opt.step, (x, y)
+    w.units = bs
+    w.metric = "images/sec (whole node) ResNet-50 amp O2" if args.model == "resnet50" else \
+        "images/sec (whole node) %s amp %s" % (args.model, opt_level)
+    w.unit = "images/s"
+    w.dtype = "bf16" if half == torch.bfloat16 else "fp16"
+    w.data = ("synthetic (on-device random 3x%dx%d images, random labels; random-init "
+              "weights)" % (args.image_size, args.image_size))
+    w.config = {
+        "model": args.model, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
+        "image_size": args.image_size, "parallelism": "dp%d" % world, "impl": args.impl,
+        "opt_level": opt_level,
+        "optimizer": "FusedSGD(momentum=0.9, wd=5e-5)" if args.impl == "amd"
+                     else "torch.optim.SGD(fused)",
+        "channels_last": not args.no_channels_last, "fused_bn": fused_bn,
+        "syncbn": bool(args.syncbn and world > 1),
+        "ddp_message_size": args.message_size if world > 1 else None,
+        "gemm_1x1": gemm_1x1, "hip_graph": bool(args.graph),
+    }
+    return w
 
-        def opt_only():
+
+def build_bert(args, device, world):
+    from apex_example_amd import amp
+    from apex_example_amd.models.bert import (BertConfig, BertForPreTraining, pretraining_loss,
+                                              synthetic_batch)
+    from apex_example_amd.optimizers import FusedLAMB
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    half = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    bs = args.batch_size or 32
+    seq = args.seq_len or 512
+    max_pred = 80 if seq >= 512 else 20
+    opt_level = args.opt_level or "O2"
+    cfg = BertConfig(fused_layer_norm=(args.impl == "amd"))
+    model = BertForPreTraining(cfg).to(device)
+    batch = synthetic_batch(cfg, bs, seq, max_pred, device, seed=17 + (
+        dist.get_rank() if world > 1 else 0))
+    w = Workload()
+    if args.impl == "amd":
+        opt = FusedLAMB(model.parameters(), lr=args.lr or 6e-3, weight_decay=0.01,
+                        max_grad_norm=1.0, materialize_master_grads=args.materialize_master_grads)
+        model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
+        if world > 1:
+            model = DistributedDataParallel(model, message_size=args.message_size)
+
+        def step(b):
+            mlm, nsp = model(b[0], b[1], b[2])
+            loss = pretraining_loss(mlm, nsp, b[3], b[4])
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
             opt.step()
-    return model, opt, step, opt_only, mf
+            return loss
+        optname = "FusedLAMB(wd=0.01, max_grad_norm=1.0)"
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 1e-4, weight_decay=0.01,
+                                fused=True)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index])
+
+        def step(b):
+            with torch.autocast("cuda", dtype=half):
+                mlm, nsp = model(b[0], b[1], b[2])
+                loss = pretraining_loss(mlm, nsp, b[3], b[4])
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            return loss
+        optname = "torch.optim.AdamW(fused) (torch has no LAMB)"
+    w.step, w.opt_only, w.batch = step, opt.step, batch
+    w.units = bs
+    w.metric = "sequences/sec (whole node) BERT-large pretrain amp %s" % opt_level
+    w.unit = "sequences/s"
+    w.dtype = "bf16" if half == torch.bfloat16 else "fp16"
+    w.data = "synthetic token ids / segment ids / masked positions; random-init weights"
+    w.config = {"model": "bert_large", "global_batch": bs * world, "per_gpu_batch": bs,
+                "seq_len": seq, "max_predictions": max_pred, "parallelism": "dp%d" % world,
+                "impl": args.impl, "opt_level": opt_level, "optimizer": optname,
+                "fused_layer_norm": args.impl == "amd"}
+    return w
+
+
+def build_gpt2(args, device, world):
+    from apex_example_amd import amp
+    from apex_example_amd.models.gpt2 import GPT2Config, GPT2LMHeadModel, lm_loss
+    from apex_example_amd.optimizers import FusedAdam
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    half = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    bs = args.batch_size or 8
+    seq = args.seq_len or 1024
+    opt_level = args.opt_level or "O1"
+    cfg = GPT2Config(fused_layer_norm=(args.impl == "amd"))
+    model = GPT2LMHeadModel(cfg).to(device)
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, cfg.vocab_size, (bs, seq), generator=g).to(device)
+    w = Workload()
+    if args.impl == "amd":
+        opt = FusedAdam(model.parameters(), lr=args.lr or 1.5e-4, weight_decay=0.01)
+        model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
+        if world > 1:
+            model = DistributedDataParallel(model, message_size=args.message_size)
+
+        def step(b):
+            loss = lm_loss(model(b[0]), b[0])
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
+            opt.step()
+            return loss
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 1.5e-4, weight_decay=0.01,
+                                fused=True)
+        scaler = torch.amp.GradScaler("cuda", enabled=(half == torch.float16))
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index])
+
+        def step(b):
+            with torch.autocast("cuda", dtype=half):
+                loss = lm_loss(model(b[0]), b[0])
+            opt.zero_grad(set_to_none=True)
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+            return loss
+    w.step, w.opt_only, w.batch = step, opt.step, (ids,)
+    w.units = bs * seq
+    w.metric = "tokens/sec (whole node) GPT-2-medium amp %s" % opt_level
+    w.unit = "tokens/s"
+    w.dtype = "bf16" if half == torch.bfloat16 else "fp16"
+    w.data = "synthetic token ids; random-init weights"
+    w.config = {"model": "gpt2_medium", "global_batch": bs * world, "per_gpu_batch": bs,
+                "seq_len": seq, "parallelism": "dp%d" % world, "impl": args.impl,
+                "opt_level": opt_level,
+                "optimizer": "FusedAdam(wd=0.01)" if args.impl == "amd"
+                             else "torch.optim.AdamW(fused)",
+                "fused_layer_norm": args.impl == "amd"}
+    return w
 
 
 def main():
@@ -146,17 +294,20 @@ def main():
     torch.backends.cudnn.deterministic = args.deterministic
     torch.manual_seed(1234 + rank)
 
-    model, opt, step, opt_only, mf = build(args, device, world)
-    bs = args.batch_size
-    x = torch.randn(bs, 3, args.image_size, args.image_size, device=device).to(
-        memory_format=mf)
-    y = torch.randint(0, 1000, (bs,), device=device)
+    if args.model.startswith("resnet"):
+        w = build_resnet(args, device, world)
+    elif args.model == "bert_large":
+        w = build_bert(args, device, world)
+    else:
+        w = build_gpt2(args, device, world)
+    step, batch = w.step, w.batch
 
-    log(rank, "[bench] impl=%s model=%s bs/gpu=%d world=%d warmup=%d steps=%d" % (
-        args.impl, args.model, bs, world, args.warmup, args.steps))
+    log(rank, "[bench] impl=%s model=%s units/gpu/step=%d world=%d warmup=%d steps=%d" % (
+        args.impl, args.model, w.units, world, args.warmup, args.steps))
     t0 = time.time()
+    loss = None
     for i in range(args.warmup):
-        loss = step(x, y)
+        loss = step(batch)
         if i == 0 or (i + 1) % 5 == 0:
             torch.cuda.synchronize()
             log(rank, "[bench] warmup %d/%d loss %.4f (%.1fs)" % (i + 1, args.warmup, loss.item(),
@@ -174,21 +325,20 @@ def main():
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(3):
-                step(x, y)
+                step(batch)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            static_loss = step(x, y)
+            static_loss = step(batch)
         torch.cuda.synchronize()
         log(rank, "[bench] captured the training step in a hipGraph")
-        eager_step = step
 
-        def step(x_, y_):  # noqa: F811  (replay: same work, one launch)
+        def step(b):  # noqa: F811  (replay: same work, one launch)
             graph.replay()
             return static_loss
 
-        step(x, y)
+        step(batch)
         torch.cuda.synchronize()
 
     def sync_all():
@@ -200,7 +350,7 @@ def main():
     torch.cuda.nvtx.range_push("timed_steps")
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        loss = step(x, y)
+        loss = step(batch)
     sync_all()
     torch.cuda.nvtx.range_pop()
     elapsed = time.perf_counter() - t_start
@@ -215,48 +365,31 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.opt_step_iters):
-        opt_only()
+        w.opt_only()
     e1.record()
     torch.cuda.synchronize()
     opt_ms = e0.elapsed_time(e1) / args.opt_step_iters
 
     ms_per_step = elapsed / args.steps * 1e3
-    img_s = bs * world * args.steps / elapsed
-    vs = None
-    if STOCK_BASELINE_IMG_S_PER_GPU:
-        vs = img_s / (STOCK_BASELINE_IMG_S_PER_GPU * world)
+    value = w.units * world * args.steps / elapsed
+    base = STOCK_BASELINE_PER_GPU.get(args.model) if args.impl == "amd" else None
+    if args.model.startswith("resnet") and (w.config.get("per_gpu_batch") != 256
+                                            or args.image_size != 224):
+        base = None
     rec = {
-        "metric": "images/sec (whole node) ResNet-50 amp O2",
-        "value": round(img_s, 2),
-        "unit": "images/s",
+        "metric": w.metric,
+        "value": round(value, 2),
+        "unit": w.unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None if vs is None else round(vs, 4),
-        "dtype": args.dtype,
-        "data": "synthetic (on-device random 3x%dx%d images, random labels; random-init "
-                "weights)" % (args.image_size, args.image_size),
-        "config": {
-            "model": args.model,
-            "global_batch": bs * world,
-            "per_gpu_batch": bs,
-            "seq_len": None,
-            "image_size": args.image_size,
-            "parallelism": "dp%d" % world,
-            "impl": args.impl,
-            "opt_level": args.opt_level,
-            "optimizer": "FusedSGD(momentum=0.9, wd=5e-5)" if args.impl == "amd"
-                         else "torch.optim.SGD(fused)",
-            "channels_last": not args.no_channels_last,
-            "fused_bn": args.impl == "amd" and not args.no_fused_bn,
-            "syncbn": bool(args.syncbn and world > 1),
-            "ddp_message_size": args.message_size if world > 1 else None,
-            "gemm_1x1": args.impl == "amd" and not args.no_gemm_1x1,
-            "hip_graph": bool(args.graph),
-        },
+        "vs_baseline": round(value / (base * world), 4) if base else None,
+        "dtype": w.dtype,
+        "data": w.data,
+        "config": w.config,
         "optimizer_step_ms": round(opt_ms, 4),
         "final_loss": round(final_loss, 4),
     }

@@ -1,0 +1,83 @@
+"""Transformer configs of BASELINE.json on the GPU (reduced depth so the suite
+stays fast): BERT amp O2 + FusedLAMB + FusedLayerNorm, GPT-2 amp O1 fp16 +
+FusedAdam including the dynamic-loss-scale overflow-skip path."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _amp():
+    from apex_example_amd import amp
+    return amp
+
+
+def test_bert_o2_fused_lamb_trains_and_matches_stock_forward():
+    from apex_example_amd.models.bert import BertConfig, BertForPreTraining, pretraining_loss, \
+        synthetic_batch
+    from apex_example_amd.optimizers import FusedLAMB
+
+    amp = _amp()
+    cfg = BertConfig(num_hidden_layers=2, hidden_dropout_prob=0.0,
+                     attention_probs_dropout_prob=0.0)
+    torch.manual_seed(0)
+    m = BertForPreTraining(cfg).cuda()
+    cfg_ref = BertConfig(num_hidden_layers=2, fused_layer_norm=False, hidden_dropout_prob=0.0,
+                         attention_probs_dropout_prob=0.0)
+    ref = BertForPreTraining(cfg_ref).cuda()
+    ref.load_state_dict(m.state_dict())
+    b = synthetic_batch(cfg, 4, 128, 20, "cuda", seed=3)
+    with torch.no_grad():
+        a1, n1 = m(b[0], b[1], b[2])
+        a2, n2 = ref(b[0], b[1], b[2])
+    torch.testing.assert_close(a1, a2, rtol=2e-3, atol=2e-3)
+
+    opt = FusedLAMB(m.parameters(), lr=2e-3, materialize_master_grads=False)
+    m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
+    assert next(m.parameters()).dtype == torch.bfloat16
+    losses = []
+    for _ in range(10):
+        loss = pretraining_loss(*m(b[0], b[1], b[2]), b[3], b[4])
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0] - 0.5, losses
+    # bf16 model copy written by the optimizer kernel equals the fp32 masters
+    for p, mp in zip(m.parameters(), amp.master_params(opt)):
+        torch.testing.assert_close(p.float(), mp.to(torch.bfloat16).float())
+
+
+def test_gpt2_o1_fp16_fused_adam_overflow_skip():
+    from apex_example_amd.models.gpt2 import GPT2Config, GPT2LMHeadModel, lm_loss
+    from apex_example_amd.optimizers import FusedAdam
+
+    amp = _amp()
+    cfg = GPT2Config(n_layer=2, resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)
+    torch.manual_seed(0)
+    m = GPT2LMHeadModel(cfg).cuda()
+    opt = FusedAdam(m.parameters(), lr=3e-4)
+    m, opt = amp.initialize(m, opt, opt_level="O1", verbosity=0)
+    assert next(m.parameters()).dtype == torch.float32
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device="cuda")
+    losses = []
+    for it in range(8):
+        logits = m(ids)
+        assert logits.dtype == torch.float16
+        loss = lm_loss(logits, ids)
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+            if it == 4:  # poison one gradient: the step must be skipped, the scale halved
+                scale_before = amp.state_dict()["loss_scaler0"]["loss_scale"]
+                before = [p.detach().clone() for p in m.parameters()]
+                next(m.parameters()).grad[0, 0] = float("inf")
+        opt.step()
+        if it == 4:
+            torch.cuda.synchronize()
+            for p, q in zip(m.parameters(), before):
+                assert torch.equal(p, q)
+            assert amp.state_dict()["loss_scaler0"]["loss_scale"] == scale_before / 2
+        losses.append(loss.item())
+    assert losses[-1] < losses[0], losses
