@@ -58,6 +58,28 @@ def _zero_or_none(params):
         amp_C.multi_tensor_zero(65536, None, [views])
 
 
+def _stash_grad(stash, param):
+    """Take a param's current grad out of the way of the next backward (Apex
+    grad-copy elision) and return what must be added back after unscaling.
+
+    A grad that is a DDP bucket view must stay attached (the reducer all-reduces
+    the bucket in place), so it cannot simply be set to None: if it is known to
+    be zero (zero_grad ran since the last backward) nothing is stashed;
+    otherwise its (already unscaled) content is saved and the view zeroed."""
+    g = param.grad
+    if g is None:
+        return None
+    if getattr(param, "_amd_grad_is_bucket_view", False):
+        if getattr(stash, "model_grads_zeroed", False):
+            return None
+        saved = g.detach().clone()
+        with torch.no_grad():
+            g.zero_()
+        return saved
+    param.grad = None
+    return g
+
+
 def _master_params_to_model_params(self):
     stash = self._amp_stash
     if multi_tensor_applier.available:
@@ -159,15 +181,14 @@ def prepare_backward_with_master_weights(self):
     self._amp_lazy_init()
     _zero_or_none(stash.all_fp16_params)
     for i, param in enumerate(stash.all_fp32_from_fp32_params):
-        stash.all_fp32_from_fp32_grad_stash[i] = param.grad
-        # Set up to leverage grad copy elision:
-        param.grad = None
+        stash.all_fp32_from_fp32_grad_stash[i] = _stash_grad(stash, param)
 
 
 def post_backward_with_master_weights(self, scaler):
     stash = self._amp_stash
     self._amp_lazy_init()
 
+    stash.model_grads_zeroed = False
     if _folds_unscale(self):
         # fused optimizer reads the 16-bit grads itself: overflow check only
         grads = [p.grad for p in stash.all_fp16_params if p.grad is not None]
@@ -231,17 +252,15 @@ def prepare_backward_no_master_weights(self):
     stash = self._amp_stash
     self._amp_lazy_init()
     for i, param in enumerate(stash.all_fp16_params):
-        stash.all_fp16_grad_stash[i] = param.grad
-        # Set up to leverage grad copy elision:
-        param.grad = None
+        stash.all_fp16_grad_stash[i] = _stash_grad(stash, param)
     for i, param in enumerate(stash.all_fp32_params):
-        stash.all_fp32_grad_stash[i] = param.grad
-        param.grad = None
+        stash.all_fp32_grad_stash[i] = _stash_grad(stash, param)
 
 
 def post_backward_no_master_weights(self, scaler):
     stash = self._amp_stash
     self._amp_lazy_init()
+    stash.model_grads_zeroed = False
     split_types = ((stash.all_fp16_params, stash.all_fp16_grad_stash),
                    (stash.all_fp32_params, stash.all_fp32_grad_stash))
     for params, stashed_grads in split_types:
@@ -328,6 +347,7 @@ def _process_optimizer(optimizer, properties):
                 else:
                     for v in views:
                         v.zero_()
+            stash.model_grads_zeroed = True
             # Clear the master grads that are independent of model grads
             for param in self._amp_stash.all_fp32_from_fp16_params:
                 param.grad = None

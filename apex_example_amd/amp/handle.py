@@ -7,6 +7,7 @@ import warnings
 
 import torch
 
+from ..utils import fault as _fault
 from ._amp_state import _amp_state, maybe_print
 
 
@@ -65,6 +66,7 @@ def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False,
         for optimizer in optimizers:
             optimizer._amp_stash.params_have_scaled_gradients = True
     else:
+        _fault.on_backward_end(optimizers)
         loss_scaler.clear_overflow_state()
         for optimizer in optimizers:
             optimizer._post_amp_backward(loss_scaler)

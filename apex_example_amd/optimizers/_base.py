@@ -146,22 +146,27 @@ class FusedOptimizerBase(torch.optim.Optimizer):
 
     # ------------------------------------------------------------------ API
     def zero_grad(self, set_to_none=None):
+        """Apex semantics (set_grad_none -> None, else zero in place).  Grads that
+        are DDP bucket views are always zeroed in place so they stay views
+        (one multi-tensor launch); the amp stash learns that they are zero."""
         if set_to_none is None:
             set_to_none = self.set_grad_none
-        if set_to_none:
-            for group in self.param_groups:
-                for p in group["params"]:
+        grads = []
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if set_to_none and not getattr(p, "_amd_grad_is_bucket_view", False):
                     p.grad = None
-        else:
-            grads = []
-            for group in self.param_groups:
-                for p in group["params"]:
-                    if p.grad is not None:
-                        if p.grad.requires_grad:
-                            p.grad = p.grad.detach()
-                        grads.append(p.grad)
-            if grads:
-                _native.require().mt.zero(grads)
+                    continue
+                if p.grad.requires_grad:
+                    p.grad = p.grad.detach()
+                grads.append(p.grad)
+        if grads:
+            _native.require().mt.zero(grads)
+        stash = self._amp()
+        if stash is not None:
+            stash.model_grads_zeroed = True
 
     def _materialize_steps(self):
         for gid, t in self._dev_steps.items():

@@ -331,20 +331,69 @@ __global__ void __launch_bounds__(kLNThreads)
   part[(size_t)blockIdx.y * 2 * n2 + n2 + c] = ab;
 }
 
-// sum nparts partial rows -> dgamma, dbeta (TW); fixed order -> deterministic
-template <typename TW>
+// sum nparts partial rows -> dgamma, dbeta (TW); fixed order -> deterministic.
+// A partial row is [dgamma(n2) | dbeta(n2)] = 2*n2 contiguous floats.  Block =
+// 8 column lanes x 32 row lanes; a lane owns 4 adjacent columns (one 16-byte
+// load per partial row when n2 is even), the 32 row lanes stride over the
+// partials and are combined through LDS.  Grid = ceil(2*n2 / 32) blocks.
+constexpr int kCSColLanes = 8, kCSRowLanes = 32, kCSCols = 4 * kCSColLanes;
+
+template <typename TW, bool VEC4>
 __global__ void __launch_bounds__(256)
     ln_bwd_colsum(const float* __restrict__ part, int nparts, int n2, TW* __restrict__ dgamma,
                   TW* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n2) return;
-  float sg = 0.f, sb = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    sg += part[(size_t)p * 2 * n2 + c];
-    sb += part[(size_t)p * 2 * n2 + n2 + c];
+  __shared__ float4 red[kCSRowLanes][kCSColLanes];
+  const int cl = threadIdx.x % kCSColLanes;
+  const int rl = threadIdx.x / kCSColLanes;
+  const int width = 2 * n2;
+  const int c0 = blockIdx.x * kCSCols + cl * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < width) {
+    if (VEC4) {
+      const float* base = part + c0;
+      int p = rl;
+      for (; p + kCSRowLanes < nparts; p += 2 * kCSRowLanes) {  // two loads in flight
+        float4 a = *reinterpret_cast<const float4*>(base + (size_t)p * width);
+        float4 b = *reinterpret_cast<const float4*>(base + (size_t)(p + kCSRowLanes) * width);
+        acc.x += a.x + b.x; acc.y += a.y + b.y; acc.z += a.z + b.z; acc.w += a.w + b.w;
+      }
+      if (p < nparts) {
+        float4 a = *reinterpret_cast<const float4*>(base + (size_t)p * width);
+        acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+      }
+    } else {
+      for (int p = rl; p < nparts; p += kCSRowLanes) {
+        const float* r = part + (size_t)p * width + c0;
+        acc.x += r[0];
+        if (c0 + 1 < width) acc.y += r[1];
+        if (c0 + 2 < width) acc.z += r[2];
+        if (c0 + 3 < width) acc.w += r[3];
+      }
+    }
   }
-  if (dgamma) dgamma[c] = from_f32<TW>(sg);
-  if (dbeta) dbeta[c] = from_f32<TW>(sb);
+  red[rl][cl] = acc;
+  __syncthreads();
+  for (int h = kCSRowLanes / 2; h > 0; h >>= 1) {
+    if (rl < h) {
+      float4 o = red[rl + h][cl];
+      float4& m = red[rl][cl];
+      m.x += o.x; m.y += o.y; m.z += o.z; m.w += o.w;
+    }
+    __syncthreads();
+  }
+  if (rl == 0 && c0 < width) {
+    float v[4] = {red[0][cl].x, red[0][cl].y, red[0][cl].z, red[0][cl].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int c = c0 + i;
+      if (c >= width) break;
+      if (c < n2) {
+        if (dgamma) dgamma[c] = from_f32<TW>(v[i]);
+      } else if (dbeta) {
+        dbeta[c - n2] = from_f32<TW>(v[i]);
+      }
+    }
+  }
 }
 
 static inline int ln_bwd_blocks(int64_t n1) {
@@ -403,8 +452,13 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
         }
       }
       if (want_wb) {
-        hipLaunchKernelGGL((ln_bwd_colsum<TW>), dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st,
-                           part, nparts, (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta));
+        dim3 cgrid((unsigned)((2 * n2 + kCSCols - 1) / kCSCols));
+        if (n2 % 2 == 0 && ((uintptr_t)part % 16) == 0)
+          hipLaunchKernelGGL((ln_bwd_colsum<TW, true>), cgrid, dim3(256), 0, st, part, nparts,
+                             (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta));
+        else
+          hipLaunchKernelGGL((ln_bwd_colsum<TW, false>), cgrid, dim3(256), 0, st, part, nparts,
+                             (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta));
       }
     });
   });

@@ -168,3 +168,41 @@ def syncbn_groups(rank, world):
 
     g = create_syncbn_process_group(2)
     return {"group_size": dist.get_world_size(g), "group_rank": dist.get_rank(g)}
+
+
+def ddp_amp_vs_local(rank, world, opt_level="O2", fused=False, iters=3):
+    """Identical data on every rank: apex-DDP-averaged grads must equal the grads
+    of an undistributed copy, for the fp32 params amp stashes between
+    backward passes (bucket-view grads must not alias the stash)."""
+    from apex_example_amd import amp
+    from apex_example_amd.optimizers import FusedAdam
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    def make():
+        torch.manual_seed(0)
+        return nn.Sequential(nn.Linear(16, 32), nn.BatchNorm1d(32), nn.ReLU(), nn.Linear(32, 4))
+
+    ma, mb = make(), make()
+    if fused:
+        oa, ob = FusedAdam(ma.parameters(), lr=1e-2), FusedAdam(mb.parameters(), lr=1e-2)
+    else:
+        oa = torch.optim.SGD(ma.parameters(), lr=0.1, momentum=0.9)
+        ob = torch.optim.SGD(mb.parameters(), lr=0.1, momentum=0.9)
+    [ma, mb], [oa, ob] = amp.initialize([ma, mb], [oa, ob], opt_level=opt_level,
+                                        half_dtype=torch.bfloat16, num_losses=2, verbosity=0)
+    ddp = DistributedDataParallel(ma, message_size=100)
+    x, y = _data(8, seed=11)
+    diffs = []
+    for it in range(iters):
+        for lid, (mod, opt) in enumerate(((ddp, oa), (mb, ob))):
+            loss = F.cross_entropy(mod(x).float(), y)
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt, loss_id=lid) as s:
+                s.backward()
+        ga = [p.grad.float().clone() for p in amp.master_params(oa)]
+        gb = [p.grad.float().clone() for p in amp.master_params(ob)]
+        diffs.append(max(float((a - b).abs().max() / (b.abs().max() + 1e-6))
+                         for a, b in zip(ga, gb)))
+        oa.step()
+        ob.step()
+    return {"diffs": diffs}

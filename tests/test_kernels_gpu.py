@@ -215,7 +215,7 @@ def test_optimizer_gpu_matches_cpu_path(opt_name):
 
 # ------------------------------------------------------------------ LayerNorm
 @pytest.mark.parametrize("shape", [(64, 1024), (3, 7, 768), (33, 4096), (10, 1000), (5, 2048),
-                                   (2, 64)])
+                                   (2, 64), (9, 777), (5000, 1024), (4100, 998)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_layer_norm_fwd_bwd(shape, dt):
     from apex_example_amd.normalization import FusedLayerNorm

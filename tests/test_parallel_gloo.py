@@ -143,3 +143,10 @@ def test_convert_syncbn_model():
     assert m2.bn1.bn.running_mean is rm  # running buffers shared
     inst = torch.nn.InstanceNorm2d(4)
     assert convert_syncbn_model(inst) is inst
+
+
+@pytest.mark.parametrize("opt_level,fused", [("O2", False), ("O1", True), ("O3", False)])
+def test_ddp_amp_stashed_fp32_grads(tmp_path, opt_level, fused):
+    res = W.run("ddp_amp_vs_local", 2, str(tmp_path), opt_level=opt_level, fused=fused)
+    for r in res:
+        assert max(r["diffs"]) < 2e-2, r["diffs"]

@@ -3,7 +3,9 @@
 
     python tools/microbench.py bn      # fused BN kernels vs HBM copy roofline vs MIOpen BN
     python tools/microbench.py conv1x1 # ResNet-50 1x1 convs: MIOpen conv vs GEMM (hipBLASLt)
-    python tools/microbench.py optim   # optimizer step bandwidth (ResNet-50 / BERT-large sizes)
+    python tools/microbench.py optim   # optimizer step bandwidth (ResNet-50 sizes)
+    python tools/microbench.py ln      # FusedLayerNorm fwd/bwd vs torch LayerNorm
+    python tools/microbench.py lamb    # FusedLAMB / FusedAdam on BERT-large's 336M params
 """
 from __future__ import annotations
 
@@ -152,11 +154,61 @@ def bench_optim(args):
     print("torch.optim.AdamW(fused) same: %.1f us" % t4)
 
 
+def bench_ln(args):
+    from apex_example_amd.normalization import FusedLayerNorm
+
+    dev = "cuda"
+    print("| rows x n2 (dtype) | MB in | fused fwd | torch fwd | fused bwd (dx,dg,db) | torch bwd |")
+    print("|---|---|---|---|---|---|")
+    for (rows, n2, dt) in [(16384, 1024, torch.bfloat16), (8192, 1024, torch.float32),
+                           (16384, 768, torch.bfloat16), (4096, 4096, torch.bfloat16),
+                           (65536, 1024, torch.bfloat16)]:
+        x = torch.randn(rows, n2, device=dev, dtype=dt, requires_grad=True)
+        dy = torch.randn(rows, n2, device=dev, dtype=dt)
+        fl = FusedLayerNorm(n2).to(dev).to(dt)
+        tl = torch.nn.LayerNorm(n2).to(dev).to(dt)
+        nb = x.numel() * x.element_size()
+        res = []
+        for m in (fl, tl):
+            tf = timeit(lambda: m(x))
+            y = m(x)
+            tb = timeit(lambda: torch.autograd.grad(y, [x, m.weight, m.bias], dy,
+                                                    retain_graph=True))
+            res.append((tf, tb))
+
+        def tbs(nbytes, t):
+            return "%.1f us (%.2f TB/s)" % (t, nbytes / (t * 1e-6) / 1e12)
+
+        print("| %dx%d (%s) | %.1f | %s | %s | %s | %s |" % (
+            rows, n2, str(dt).split(".")[1], nb / 1e6, tbs(2 * nb, res[0][0]),
+            tbs(2 * nb, res[1][0]), tbs(3 * nb, res[0][1]), tbs(3 * nb, res[1][1])))
+
+
+def bench_lamb(args):
+    from apex_example_amd.optimizers import FusedAdam, FusedLAMB
+    from apex_example_amd.models.bert import bert_large
+
+    dev = "cuda"
+    m = bert_large().to(dev)
+    ps = list(m.parameters())
+    n = sum(p.numel() for p in ps)
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    for name, o, bpp in [("FusedLAMB", FusedLAMB(ps, lr=1e-3, weight_decay=0.01), 32),
+                         ("FusedAdam", FusedAdam(ps, lr=1e-3, weight_decay=0.01), 28),
+                         ("torch AdamW(fused)", torch.optim.AdamW(ps, lr=1e-3, fused=True), 28)]:
+        o.step()
+        t = timeit(lambda: o.step(), iters=10)
+        print("%s fp32 BERT-large (%d params, %d tensors): %.0f us, %.2f TB/s (%d B/param min)" % (
+            name, n, len(ps), t, bpp * n / (t * 1e-6) / 1e12, bpp))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "conv1x1", "optim"])
+    ap.add_argument("what", choices=["bn", "conv1x1", "optim", "ln", "lamb"])
     a = ap.parse_args()
-    {"bn": bench_bn, "conv1x1": bench_conv1x1, "optim": bench_optim}[a.what](a)
+    {"bn": bench_bn, "conv1x1": bench_conv1x1, "optim": bench_optim, "ln": bench_ln,
+     "lamb": bench_lamb}[a.what](a)
 
 
 if __name__ == "__main__":
