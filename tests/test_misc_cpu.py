@@ -1,0 +1,80 @@
+"""MLP (apex.mlp parity), pyprof signatures / trace attribution, on CPU."""
+import csv
+
+import pytest
+import torch
+
+
+@pytest.mark.parametrize("activation", ["relu", "sigmoid", "none"])
+@pytest.mark.parametrize("bias", [True, False])
+def test_mlp_matches_sequential(activation, bias):
+    from apex_example_amd.mlp import MLP
+
+    torch.manual_seed(0)
+    sizes = [24, 32, 16, 8]
+    mlp = MLP(sizes, bias=bias, activation=activation).double()
+    layers = []
+    for i in range(len(sizes) - 1):
+        lin = torch.nn.Linear(sizes[i], sizes[i + 1], bias=bias).double()
+        with torch.no_grad():
+            lin.weight.copy_(mlp.weights[i])
+            if bias:
+                lin.bias.copy_(mlp.biases[i])
+        layers.append(lin)
+        if activation == "relu":
+            layers.append(torch.nn.ReLU())
+        elif activation == "sigmoid":
+            layers.append(torch.nn.Sigmoid())
+    ref = torch.nn.Sequential(*layers)
+    x = torch.randn(5, 24, dtype=torch.double, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    y, yr = mlp(x), ref(xr)
+    torch.testing.assert_close(y, yr)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(x.grad, xr.grad)
+    for i in range(len(sizes) - 1):
+        torch.testing.assert_close(mlp.weights[i].grad, layers[i * (1 if activation == "none" else 2)].weight.grad)
+
+
+def test_mlp_gradcheck():
+    from apex_example_amd.mlp import MLP
+
+    torch.manual_seed(1)
+    mlp = MLP([4, 6, 3], activation="sigmoid").double()
+    x = torch.randn(3, 4, dtype=torch.double, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda inp: mlp(inp), (x,))
+
+
+def test_pyprof_signature_and_flops():
+    from apex_example_amd import pyprof
+    from apex_example_amd.pyprof.flops import op_flops
+
+    sig = pyprof.signature(torch.matmul, (torch.zeros(4, 8, 16), torch.zeros(16, 32)))
+    assert sig == "matmul(4x8x16 float32, 16x32 float32)"
+    fl, nb = op_flops(sig)
+    assert fl == 2 * 4 * 8 * 16 * 32 and nb == (4 * 8 * 16 + 16 * 32) * 4
+    with pyprof.annotate():  # no GPU: a transparent mode
+        assert torch.add(torch.ones(2), 1).sum().item() == 4.0
+
+
+def test_pyprof_parse_attribution(tmp_path):
+    from apex_example_amd.pyprof.parse import attribute, report
+
+    with open(tmp_path / "run_marker_api_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Function", "Start_Timestamp", "End_Timestamp"])
+        w.writerow(["linear(8x16 float32, 32x16 float32)", 100, 200])
+        w.writerow(["relu(8x32 float32)", 150, 180])
+    with open(tmp_path / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Correlation_Id"])
+        w.writerow(["gemm", 110, 140, 1])
+        w.writerow(["relu_k", 160, 170, 2])
+        w.writerow(["other", 500, 510, 3])
+    per_op, per_kernel = attribute(str(tmp_path))
+    assert per_op["linear(8x16 float32, 32x16 float32)"][0] == 1
+    assert per_op["relu(8x32 float32)"][0] == 1  # innermost range wins
+    assert per_op["<unattributed>"][0] == 1
+    assert "linear" in report(per_op)
