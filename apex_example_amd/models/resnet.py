@@ -84,8 +84,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
+        if self.downsample is None and isinstance(self.conv1, Conv2d1x1):
+            # identity block: the residual-gradient add rides in conv1's dgrad GEMM
+            out, identity = self.conv1.forward_with_skip(x)
+        else:
+            identity = x if self.downsample is None else self.downsample(x)
+            out = self.conv1(x)
+        out = self.bn1(out)
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), identity)
 

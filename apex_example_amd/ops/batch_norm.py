@@ -37,17 +37,31 @@ def _to_logical(x, shape_channel_last):
 class BatchNormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
-                fuse_relu, shape_channel_last):
+                fuse_relu, shape_channel_last, num_batches_tracked=None):
         C = _C()
         orig_shape = x.shape
         xl = _to_logical(x, shape_channel_last)
         zl = _to_logical(z, shape_channel_last) if z is not None else None
-        mean, var = C.local_stats(xl)
         count = xl.numel() // xl.size(1)
         if process_group is False or not (dist.is_available() and dist.is_initialized()):
             world = 1  # local statistics
         else:
             world = dist.get_world_size(process_group)
+        if world == 1 and xl.is_cuda:
+            # one stats launch + one finalize (mean, invstd, running stats and
+            # num_batches_tracked in the same kernel) + one apply launch
+            y, mean_g, invstd = C.forward_local(xl, weight, bias, running_mean, running_var,
+                                                num_batches_tracked, float(eps), float(momentum),
+                                                zl, bool(fuse_relu))
+            ctx.save_for_backward(xl, zl, weight, bias, mean_g, invstd)
+            ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = None, 1, bool(fuse_relu), \
+                None, count
+            ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
+                shape_channel_last
+            return y.view(orig_shape) if shape_channel_last else y
+        if num_batches_tracked is not None:
+            num_batches_tracked.add_(1)
+        mean, var = C.local_stats(xl)
         if world > 1:
             pg = process_group if process_group is not None else dist.group.WORLD
             cnt = torch.full((1,), float(count), dtype=torch.float32, device=x.device)
@@ -102,15 +116,18 @@ class BatchNormFunction(torch.autograd.Function):
             if dz is not None:
                 dz = dz.view(ctx.orig_shape)
         return (dx, dz if ctx.has_z else None, gw if need_w else None, gb if need_w else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
-                   z=None, fuse_relu=False, process_group=False, shape_channel_last=False):
-    """Functional fused BN(+z)(+ReLU).  ``process_group=False`` -> local statistics."""
+                   z=None, fuse_relu=False, process_group=False, shape_channel_last=False,
+                   num_batches_tracked=None):
+    """Functional fused BN(+z)(+ReLU).  ``process_group=False`` -> local statistics.
+    ``num_batches_tracked`` (int64 tensor) is incremented on the device."""
     if training:
         return BatchNormFunction.apply(x, z, weight, bias, running_mean, running_var, eps, momentum,
-                                       process_group, fuse_relu, shape_channel_last)
+                                       process_group, fuse_relu, shape_channel_last,
+                                       num_batches_tracked)
     # inference: running statistics (autograd through plain torch ops)
     if shape_channel_last:
         xs = x.movedim(-1, 1)
@@ -141,13 +158,16 @@ class BatchNorm2dReLU(torch.nn.BatchNorm2d):
                 y = y + z
             return torch.relu(y) if self.fuse_relu else y
         momentum = 0.0 if self.momentum is None else self.momentum
+        nbt = None
         if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
-            if self.momentum is None:
+            if self.momentum is None:  # cumulative average needs the count on the host
+                self.num_batches_tracked.add_(1)
                 momentum = 1.0 / float(self.num_batches_tracked)
+            else:
+                nbt = self.num_batches_tracked  # incremented inside the stats kernel
         use_batch = self.training or not self.track_running_stats
         return batch_norm_act(x, self.weight, self.bias,
                               self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
                               use_batch, momentum, self.eps, z=z, fuse_relu=self.fuse_relu,
-                              process_group=False)
+                              process_group=False, num_batches_tracked=nbt)

@@ -60,12 +60,17 @@ class SyncBatchNorm(_BatchNorm):
             return F.batch_norm(input, self.running_mean, self.running_var, self.weight,
                                 self.bias, False, 0.0, self.eps)
         exponential_average_factor = 0.0
+        nbt = None
         if self.training and self.track_running_stats:
-            self.num_batches_tracked += 1
             if self.momentum is None:
+                self.num_batches_tracked += 1
                 exponential_average_factor = 1.0 / float(self.num_batches_tracked)
             else:
                 exponential_average_factor = self.momentum
+                if _native.available():
+                    nbt = self.num_batches_tracked  # incremented by the BN op on the device
+                else:
+                    self.num_batches_tracked += 1
         use_batch = self.training or not self.track_running_stats
         if not use_batch:
             from ..ops.batch_norm import batch_norm_act
@@ -82,7 +87,7 @@ class SyncBatchNorm(_BatchNorm):
                                        self.running_mean if self.track_running_stats else None,
                                        self.running_var if self.track_running_stats else None,
                                        self.eps, exponential_average_factor, pg, self.fuse_relu,
-                                       channel_last)
+                                       channel_last, nbt)
 
 
 class _PySyncBNFunction(torch.autograd.Function):

@@ -281,11 +281,11 @@ int64_t bn_stats_workspace(int64_t outer, int64_t C, int64_t inner, int channel_
   return s * 2 * C;
 }
 
-void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
-                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st) {
+static void local_stats_impl(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
+                             int channel_last, const BNStatsOut& out, float* ws, hipStream_t st) {
   const int64_t count = outer * inner;
   if (count == 0 || C == 0) return;
-  if (channel_last) return nhwc_stats(x, tx, outer, C, mean, var_biased, ws, st);
+  if (channel_last) return nhwc_stats(x, tx, outer, C, out, ws, st);
   const int splits = nchw_splits(outer, C, inner);
   const int vec = nchw_vec(inner, {x}) ? 1 : 0;
   bn_dispatch(tx, [&](auto t0) {
@@ -294,8 +294,22 @@ void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t i
     hipLaunchKernelGGL((stats_nchw<T>), dim3(splits, (unsigned)C), dim3(kBNThreads), 0, st, xp,
                        outer, (int)C, inner, vec, ws);
     hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp, ws, splits,
-                       (int)C, count, inner, mean, var_biased);
+                       (int)C, count, inner, out);
   });
+}
+
+void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
+                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st) {
+  BNStatsOut out{mean, var_biased, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f};
+  local_stats_impl(x, tx, outer, C, inner, channel_last, out, ws, st);
+}
+
+void bn_local_train_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
+                          int channel_last, float* mean, float* invstd, float* running_mean,
+                          float* running_var, long long* nbt, float eps, float momentum, float* ws,
+                          hipStream_t st) {
+  BNStatsOut out{mean, nullptr, invstd, running_mean, running_var, nbt, eps, momentum};
+  local_stats_impl(x, tx, outer, C, inner, channel_last, out, ws, st);
 }
 
 void bn_combine_stats(const float* means, const float* vars, const float* counts, int world,

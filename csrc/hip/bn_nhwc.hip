@@ -297,8 +297,8 @@ void vec_dispatch(bool vec, F&& f) {
 
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec) { return reduce_splits(M, ngeom(C, vec)); }
 
-void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, float* mean, float* var,
-                float* ws, hipStream_t st) {
+void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
+                hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({x});
   const NGeom g = ngeom(C, vec);
   const int splits = reduce_splits(M, g);
@@ -310,7 +310,7 @@ void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, float* mean, floa
                          dim3(kBNThreads), 0, st, xp, M, (int)C, g.ctile, g.rows_iter, ws);
     });
     hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp, ws, splits,
-                       (int)C, M, (int64_t)1, mean, var);
+                       (int)C, M, (int64_t)1, out);
   });
 }
 

@@ -153,6 +153,12 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
 int64_t bn_stats_workspace(int64_t outer, int64_t C, int64_t inner, int channel_last);
 void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
                     int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st);
+// local (single-GPU) training stats: mean, invstd, running-stat update and
+// num_batches_tracked += 1 in the finalize kernel
+void bn_local_train_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
+                          int channel_last, float* mean, float* invstd, float* running_mean,
+                          float* running_var, long long* nbt, float eps, float momentum, float* ws,
+                          hipStream_t st);
 // combine world_size x (mean, var_biased, count) -> mean, invstd, unbiased var; and
 // update running stats (may be null) with momentum.
 void bn_combine_stats(const float* means, const float* vars, const float* counts, int world,

@@ -72,12 +72,26 @@ __device__ __forceinline__ void slab_sum8(const float* __restrict__ slab, int sp
   __syncthreads();
 }
 
-// slab of shifted sums -> mean, var_biased; the shift is re-read from x
+// Where the statistics go.  Plain mode: mean + biased var (for the SyncBN
+// all_gather).  Local-training mode (invstd != nullptr): mean + invstd and, in
+// the same kernel, the running-stat momentum update (unbiased var) and the
+// module's num_batches_tracked += 1, replacing the separate combine / fill /
+// counter launches of a local BatchNorm forward.
+struct BNStatsOut {
+  float* mean;
+  float* var;             // biased var (plain mode) or nullptr
+  float* invstd;          // local-training mode
+  float* running_mean;    // optional (fp32)
+  float* running_var;     // optional (fp32)
+  long long* nbt;         // optional num_batches_tracked (int64)
+  float eps, momentum;
+};
+
+// slab of shifted sums -> statistics; the shift is re-read from x
 template <typename T>
 __global__ void __launch_bounds__(kBNThreads)
     stats_finalize(const T* __restrict__ x, const float* __restrict__ slab, int splits, int C,
-                   int64_t count, int64_t shift_stride, float* __restrict__ mean,
-                   float* __restrict__ var) {
+                   int64_t count, int64_t shift_stride, BNStatsOut out) {
   __shared__ float sums[2 * kFinCh];
   const int c0 = blockIdx.x * kFinCh;
   slab_sum8(slab, splits, C, c0, sums);
@@ -87,8 +101,17 @@ __global__ void __launch_bounds__(kBNThreads)
     const float shift = to_f32(x[(int64_t)c * shift_stride]);
     double m = (double)sums[k] / (double)count;
     double v = (double)sums[kFinCh + k] / (double)count - m * m;
-    mean[c] = (float)(shift + m);
-    var[c] = (float)(v > 0.0 ? v : 0.0);
+    if (v < 0.0) v = 0.0;
+    const float mean = (float)(shift + m);
+    out.mean[c] = mean;
+    if (out.var) out.var[c] = (float)v;
+    if (out.invstd) out.invstd[c] = rsqrtf((float)v + out.eps);
+    if (out.running_mean) {
+      const double unb = count > 1 ? v * (double)count / (double)(count - 1) : v;
+      out.running_mean[c] = (1.f - out.momentum) * out.running_mean[c] + out.momentum * mean;
+      out.running_var[c] = (1.f - out.momentum) * out.running_var[c] + out.momentum * (float)unb;
+    }
+    if (out.nbt && c == 0) *out.nbt += 1;
   }
 }
 
@@ -116,8 +139,8 @@ static inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + kFinCh - 1)
 
 // ---- NHWC launchers (bn_nhwc.hip) -------------------------------------------
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec);
-void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, float* mean, float* var,
-                float* ws, hipStream_t st);
+void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
+                hipStream_t st);
 void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
                 const void* b, DType tw, const void* z, void* y, int64_t M, int64_t C, int relu,
                 hipStream_t st);

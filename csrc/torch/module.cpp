@@ -71,6 +71,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bn.def("local_stats", &bn_local_stats_op);
   bn.def("combine_stats", &bn_combine_stats_op);
   bn.def("apply", &bn_apply_op);
+  bn.def("forward_local", &bn_forward_local_op);
   bn.def("reduce_grad", &bn_reduce_grad_op);
   bn.def("backward_elemt", &bn_backward_elemt_op);
 

@@ -189,6 +189,42 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
   return {mean, invstd, var};
 }
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
+    at::Tensor x, OptT weight, OptT bias, OptT running_mean, OptT running_var, OptT nbt,
+    double eps, double momentum, OptT z, bool relu) {
+  c10::NoGradGuard no_grad_;
+  const bool rs = has(running_mean) && has(running_var);
+  auto f32c = [](const OptT& t) {
+    return t->scalar_type() == at::kFloat && t->is_contiguous() && t->is_cuda();
+  };
+  const bool fast = x.is_cuda() && (!rs || (f32c(running_mean) && f32c(running_var))) &&
+                    (!has(nbt) || (nbt->scalar_type() == at::kLong && nbt->is_cuda()));
+  if (!fast) {
+    auto st = bn_local_stats_op(x);
+    BNView v = bn_view(x);
+    at::Tensor counts = at::full({1}, (double)(v.outer * v.inner),
+                                 x.options().dtype(at::kFloat));
+    auto cs = bn_combine_stats_op(std::get<0>(st), std::get<1>(st), counts, eps, momentum,
+                                  running_mean, running_var);
+    if (has(nbt)) nbt->add_(1);
+    at::Tensor y = bn_apply_op(x, std::get<0>(cs), std::get<1>(cs), weight, bias, z, relu);
+    return {y, std::get<0>(cs), std::get<1>(cs)};
+  }
+  BNView v = bn_view(x);
+  x = conform(x, v);
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({v.C}, fopt), invstd = at::empty({v.C}, fopt);
+  at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
+  bn_local_train_stats(x.data_ptr(), dtype_of(x), v.outer, v.C, v.inner, v.cl,
+                       mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                       rs ? running_mean->data_ptr<float>() : nullptr,
+                       rs ? running_var->data_ptr<float>() : nullptr,
+                       has(nbt) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr,
+                       (float)eps, (float)momentum, ws.data_ptr<float>(), cur_stream());
+  at::Tensor y = bn_apply_op(x, mean, invstd, weight, bias, z, relu);
+  return {y, mean, invstd};
+}
+
 at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
                        OptT z, bool relu) {
   BNView v = bn_view(x);

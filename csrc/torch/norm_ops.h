@@ -24,6 +24,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
                                                                    double momentum,
                                                                    OptT running_mean,
                                                                    OptT running_var);
+// Local (per-GPU statistics) training forward: stats + running-stat update +
+// num_batches_tracked += 1 + normalize(+z)(+ReLU).  Returns (y, mean, invstd).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
+    at::Tensor x, OptT weight, OptT bias, OptT running_mean, OptT running_var, OptT nbt,
+    double eps, double momentum, OptT z, bool relu);
 at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
                        OptT z, bool relu);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(

@@ -336,3 +336,66 @@ def test_conv1x1_gemm_matches_conv(shape):
     yr.backward(dy)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=1e-1)
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=5e-1)
+
+
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_local_forward_running_stats(cl, dt):
+    """bn.forward_local: stats + running-stat momentum update + num_batches_tracked
+    in the finalize kernel, vs torch BatchNorm2d over several steps."""
+    from apex_example_amd.ops.batch_norm import BatchNorm2dReLU
+
+    torch.manual_seed(0)
+    m = BatchNorm2dReLU(64, fuse_relu=False).to(DEV)
+    ref = torch.nn.BatchNorm2d(64).to(DEV)
+    mf = torch.channels_last if cl else torch.contiguous_format
+    for it in range(3):
+        x = (torch.randn(8, 64, 9, 9, device=DEV) * (it + 1) + it).to(dt).to(memory_format=mf)
+        y = m(x)
+        yr = ref(x.float())
+        tol = dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+        torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(m.running_mean, ref.running_mean, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(m.running_var, ref.running_var, rtol=1e-4, atol=1e-3)
+    assert int(m.num_batches_tracked) == 3
+
+
+def test_conv1x1_skip_fused_residual_grad():
+    """Conv1x1SkipFunction: dx = dskip + dy @ W in one GEMM (beta = 1)."""
+    from apex_example_amd.ops.conv import Conv2d1x1
+
+    torch.manual_seed(0)
+    m = Conv2d1x1(64, 32).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 64, 8, 8, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y, skip = m.forward_with_skip(x)
+    assert torch.equal(skip, x)
+    out = (y.float() ** 2).sum() + (skip.float() * 3).sum()
+    out.backward()
+    xr = x.detach().float().clone().requires_grad_(True)
+    wr = m.weight.detach().float().clone().requires_grad_(True)
+    outr = (F.conv2d(xr, wr) ** 2).sum() + (xr * 3).sum()
+    outr.backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=2e-1)
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=3e-2, atol=1.0)
+
+
+def test_resnet50_fused_vs_plain_forward_backward():
+    """ResNet-50 with the fused BN / GEMM-1x1 / skip-GEMM paths matches the plain
+    torch modules (fp32, same weights) on one training step's loss and grads."""
+    from apex_example_amd.models import resnet50
+
+    torch.manual_seed(0)
+    a = resnet50(num_classes=10, fused_bn=True, gemm_1x1=True).to(DEV)
+    b = resnet50(num_classes=10).to(DEV)
+    b.load_state_dict(a.state_dict())
+    a = a.to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device=DEV).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=DEV)
+    la = F.cross_entropy(a(x), y)
+    lb = F.cross_entropy(b(x), y)
+    torch.testing.assert_close(la, lb, rtol=1e-3, atol=1e-3)
+    la.backward()
+    lb.backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-3, msg=n)
