@@ -78,8 +78,10 @@ class Conv1x1SkipFunction(torch.autograd.Function):
             else:
                 w2 = weight.reshape(co, ci)
                 if dskip is not None:
+                    # accumulate in place into the residual gradient (a fresh buffer
+                    # from the BN backward): C += dy @ W, no copy of C first
                     dskip = dskip.contiguous(memory_format=torch.channels_last)
-                    dx2 = torch.addmm(_as_rows(dskip), _as_rows(dy), w2)
+                    dx2 = _as_rows(dskip).addmm_(_as_rows(dy), w2)
                 else:
                     dx2 = torch.mm(_as_rows(dy), w2)
                 dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)

@@ -29,17 +29,37 @@ NGeom ngeom(int64_t C, bool vec) {
   return g;
 }
 
+}  // namespace
+
+BNTuning& bn_tuning() {
+  static BNTuning t;
+  return t;
+}
+
+namespace {
+
+// reduction grid: rows per thread `red_rpt`, at most `red_cap` blocks in total,
+// but at least `red_min` blocks (when every thread still gets >= 2 rows) so
+// small layers fill the 256 CUs
 int reduce_splits(int64_t M, const NGeom& g) {
-  int64_t want = (M + (int64_t)g.rows_iter * 32 - 1) / ((int64_t)g.rows_iter * 32);
-  int64_t cap = 2048 / g.cblocks;
+  const BNTuning& t = bn_tuning();
+  int64_t want = (M + (int64_t)g.rows_iter * t.red_rpt - 1) / ((int64_t)g.rows_iter * t.red_rpt);
+  const int64_t floor_splits = t.red_min / g.cblocks;
+  const int64_t max_by_rows = M / ((int64_t)g.rows_iter * 2);
+  if (want < floor_splits) want = floor_splits < max_by_rows ? floor_splits : max_by_rows;
+  int64_t cap = t.red_cap / g.cblocks;
   if (cap < 1) cap = 1;
   if (want > cap) want = cap;
   return (int)(want < 1 ? 1 : want);
 }
 
 int elem_blocks(int64_t M, const NGeom& g) {
-  int64_t want = (M + (int64_t)g.rows_iter * 4 - 1) / ((int64_t)g.rows_iter * 4);
-  int64_t cap = 8192 / g.cblocks;
+  const BNTuning& t = bn_tuning();
+  int64_t want = (M + (int64_t)g.rows_iter * t.elem_rpt - 1) / ((int64_t)g.rows_iter * t.elem_rpt);
+  const int64_t floor_blocks = t.elem_min / g.cblocks;
+  const int64_t max_by_rows = M / ((int64_t)g.rows_iter * 2);
+  if (want < floor_blocks) want = floor_blocks < max_by_rows ? floor_blocks : max_by_rows;
+  int64_t cap = t.elem_cap / g.cblocks;
   if (cap < 1) cap = 1;
   if (want > cap) want = cap;
   return (int)(want < 1 ? 1 : want);
@@ -294,6 +314,23 @@ void vec_dispatch(bool vec, F&& f) {
 }
 
 }  // namespace
+
+void bn_set_tuning(int red_rpt, int red_cap, int red_min, int elem_rpt, int elem_cap,
+                   int elem_min) {
+  BNTuning& t = bn_tuning();
+  if (red_rpt > 0) t.red_rpt = red_rpt;
+  if (red_cap > 0) t.red_cap = red_cap;
+  if (red_min >= 0) t.red_min = red_min;
+  if (elem_rpt > 0) t.elem_rpt = elem_rpt;
+  if (elem_cap > 0) t.elem_cap = elem_cap;
+  if (elem_min >= 0) t.elem_min = elem_min;
+}
+
+void bn_get_tuning(int* o) {
+  const BNTuning& t = bn_tuning();
+  o[0] = t.red_rpt; o[1] = t.red_cap; o[2] = t.red_min;
+  o[3] = t.elem_rpt; o[4] = t.elem_cap; o[5] = t.elem_min;
+}
 
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec) { return reduce_splits(M, ngeom(C, vec)); }
 

@@ -151,6 +151,9 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
 // Per-channel statistics use split reductions: partial Welford (mean, M2, count)
 // slabs then a combine, so small-C layers still cover all 256 CUs.
 int64_t bn_stats_workspace(int64_t outer, int64_t C, int64_t inner, int channel_last);
+// NHWC BN grid-sizing knobs (-1 keeps a value); get returns the 6 current values
+void bn_set_tuning(int red_rpt, int red_cap, int red_min, int elem_rpt, int elem_cap, int elem_min);
+void bn_get_tuning(int* out6);
 void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
                     int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st);
 // local (single-GPU) training stats: mean, invstd, running-stat update and

@@ -138,6 +138,15 @@ __global__ void __launch_bounds__(kBNThreads)
 static inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + kFinCh - 1) / kFinCh)); }
 
 // ---- NHWC launchers (bn_nhwc.hip) -------------------------------------------
+// Grid sizing knobs (rows per thread, block caps/floors); settable at run time
+// for tuning sweeps (tools/microbench.py bn-tune).
+// Defaults from the ResNet-50-weighted sweep on MI355X (profiles/bn_tune.txt):
+// reductions -8 %, elementwise passes -18 % vs the first sizing (32/2048, 4/8192).
+struct BNTuning {
+  int red_rpt = 64, red_cap = 1024, red_min = 512;
+  int elem_rpt = 16, elem_cap = 16384, elem_min = 0;
+};
+BNTuning& bn_tuning();
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec);
 void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
                 hipStream_t st);

@@ -5,6 +5,7 @@
 // fused_layer_norm_cuda, syncbn, plus `reducer` (the DDP core).
 #include <torch/extension.h>
 
+#include "amd_kernels.h"
 #include "amp_ops.h"
 #include "norm_ops.h"
 #include "reducer.h"
@@ -72,6 +73,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bn.def("combine_stats", &bn_combine_stats_op);
   bn.def("apply", &bn_apply_op);
   bn.def("forward_local", &bn_forward_local_op);
+  bn.def("set_tuning", &bn_set_tuning, py::arg("red_rpt") = -1, py::arg("red_cap") = -1,
+         py::arg("red_min") = -1, py::arg("elem_rpt") = -1, py::arg("elem_cap") = -1,
+         py::arg("elem_min") = -1);
+  bn.def("get_tuning", []() {
+    int o[6];
+    bn_get_tuning(o);
+    return std::vector<int>(o, o + 6);
+  });
   bn.def("reduce_grad", &bn_reduce_grad_op);
   bn.def("backward_elemt", &bn_backward_elemt_op);
 

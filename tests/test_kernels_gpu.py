@@ -381,21 +381,24 @@ def test_conv1x1_skip_fused_residual_grad():
 
 
 def test_resnet50_fused_vs_plain_forward_backward():
-    """ResNet-50 with the fused BN / GEMM-1x1 / skip-GEMM paths matches the plain
-    torch modules (fp32, same weights) on one training step's loss and grads."""
+    """ResNet-50 with the fused BN / GEMM-1x1 / skip-GEMM paths vs a CPU float64
+    reference (same weights): loss and every parameter grad.  (Plain torch fp32
+    on MIOpen is itself ~2-3 % off fp64 on the worst, cancellation-heavy BN bias
+    grads at this tiny batch, hence the bound on the worst tensor.)"""
     from apex_example_amd.models import resnet50
 
     torch.manual_seed(0)
-    a = resnet50(num_classes=10, fused_bn=True, gemm_1x1=True).to(DEV)
-    b = resnet50(num_classes=10).to(DEV)
-    b.load_state_dict(a.state_dict())
-    a = a.to(memory_format=torch.channels_last)
-    x = torch.randn(4, 3, 64, 64, device=DEV).to(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (4,), device=DEV)
-    la = F.cross_entropy(a(x), y)
-    lb = F.cross_entropy(b(x), y)
-    torch.testing.assert_close(la, lb, rtol=1e-3, atol=1e-3)
+    a = resnet50(num_classes=10, fused_bn=True, gemm_1x1=True)
+    ref = resnet50(num_classes=10).double()
+    ref.load_state_dict(a.state_dict())
+    a = a.to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64)
+    y = torch.randint(0, 10, (4,))
+    la = F.cross_entropy(a(x.to(DEV).to(memory_format=torch.channels_last)), y.to(DEV))
+    lr = F.cross_entropy(ref(x.double()), y)
+    assert abs(la.item() - lr.item()) < 1e-4
     la.backward()
-    lb.backward()
-    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
-        torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-3, msg=n)
+    lr.backward()
+    errs = sorted(float((pa.grad.double().cpu() - pb.grad).norm() / pb.grad.norm())
+                  for pa, pb in zip(a.parameters(), ref.parameters()))
+    assert errs[-1] < 6e-2 and errs[len(errs) // 2] < 1e-2, (errs[-3:], errs[len(errs) // 2])

@@ -1,0 +1,31 @@
+"""ResNet-50 grad parity of the fused paths vs a CPU float64 reference."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch
+import torch.nn.functional as F
+from apex_example_amd.models import resnet50
+
+torch.manual_seed(0)
+base = resnet50(num_classes=10)
+sd = base.state_dict()
+x = torch.randn(4, 3, 64, 64)
+y = torch.randint(0, 10, (4,))
+ref = resnet50(num_classes=10).double()
+ref.load_state_dict(sd)
+lr = F.cross_entropy(ref(x.double()), y)
+lr.backward()
+gref = {n: p.grad for n, p in ref.named_parameters()}
+for fused, gemm, cl in [(False, False, False), (False, False, True), (True, False, True),
+                        (False, True, True), (True, True, True)]:
+    m = resnet50(num_classes=10, fused_bn=fused, gemm_1x1=gemm).cuda()
+    m.load_state_dict(sd)
+    xx = x.cuda()
+    if cl:
+        m = m.to(memory_format=torch.channels_last)
+        xx = xx.to(memory_format=torch.channels_last)
+    l = F.cross_entropy(m(xx), y.cuda())
+    l.backward()
+    errs = sorted(((float((p.grad.double().cpu() - gref[n]).norm() / gref[n].norm()), n)
+                   for n, p in m.named_parameters()), reverse=True)
+    print("fused=%d gemm=%d cl=%d loss %.6f (ref %.6f) worst %s" % (
+        fused, gemm, cl, l.item(), lr.item(), [(round(e, 4), n) for e, n in errs[:3]]), flush=True)

@@ -86,6 +86,86 @@ def bench_bn(args):
             tbs(2 * nb, t_mf), tbs(3 * nb, t_mb)))
 
 
+# (N, C, H, W) -> number of BN layers of that shape in ResNet-50 (bs 256)
+R50_BN = {(256, 64, 112, 112): 1, (256, 64, 56, 56): 6, (256, 256, 56, 56): 4,
+          (256, 128, 56, 56): 1, (256, 128, 28, 28): 7, (256, 512, 28, 28): 5,
+          (256, 256, 28, 28): 1, (256, 256, 14, 14): 11, (256, 1024, 14, 14): 7,
+          (256, 512, 14, 14): 1, (256, 512, 7, 7): 5, (256, 2048, 7, 7): 4}
+
+
+def bench_bn_tune(args):
+    """Sweep the NHWC BN grid-sizing knobs; report the ResNet-50-weighted total
+    (forward stats+finalize+apply, backward reduce+finalize+elementwise) per config."""
+    from apex_example_amd import _native
+
+    C_ = _native.require().bn
+    dev = "cuda"
+    data = {}
+    for (n, c, h, w), cnt in R50_BN.items():
+        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        data[(n, c, h, w)] = (x, torch.randn_like(x), torch.randn_like(x), torch.ones(c, device=dev),
+                              torch.zeros(c, device=dev), cnt)
+    default = C_.get_tuning()
+
+    def run_red():
+        tot = 0.0
+        per = {}
+        for shp, (x, z, dy, wt, bs, cnt) in data.items():
+            t1 = timeit(lambda: C_.local_stats(x), iters=10, warmup=3)
+            mean, var = C_.local_stats(x)
+            invstd = (var + 1e-5).rsqrt()
+            t2 = timeit(lambda: C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True),
+                        iters=10, warmup=3)
+            per[shp] = (t1, t2)
+            tot += cnt * (t1 + t2)
+        return tot, per
+
+    def run_elem():
+        tot = 0.0
+        per = {}
+        for shp, (x, z, dy, wt, bs, cnt) in data.items():
+            mean, var = C_.local_stats(x)
+            invstd = (var + 1e-5).rsqrt()
+            s1, s2, _, _ = C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True)
+            t1 = timeit(lambda: C_.apply(x, mean, invstd, wt, bs, z, True), iters=10, warmup=3)
+            t2 = timeit(lambda: C_.backward_elemt(dy, x, mean, invstd, wt, bs, s1, s2,
+                                                  float(x.numel() // x.size(1)), z, True, True),
+                        iters=10, warmup=3)
+            per[shp] = (t1, t2)
+            tot += cnt * (t1 + t2)
+        return tot, per
+
+    print("default", default)
+    res = []
+    for rpt in (8, 16, 32, 64):
+        for cap in (1024, 2048, 4096):
+            for mn in (0, 512, 1024):
+                C_.set_tuning(red_rpt=rpt, red_cap=cap, red_min=mn)
+                tot, per = run_red()
+                res.append((tot, rpt, cap, mn, per))
+                print("reduce rpt=%d cap=%d min=%d: %.0f us (R50-weighted)" % (rpt, cap, mn, tot),
+                      flush=True)
+    res.sort(key=lambda r: r[0])
+    print("BEST reduce:", res[0][1:4], "%.0f us" % res[0][0])
+    for shp, (a, b) in res[0][4].items():
+        print("   ", shp, "stats %.1f us, reduce %.1f us" % (a, b))
+    C_.set_tuning(red_rpt=default[0], red_cap=default[1], red_min=default[2])
+    res = []
+    for rpt in (2, 4, 8, 16, 32):
+        for cap in (4096, 8192, 16384):
+            for mn in (0, 1024, 2048):
+                C_.set_tuning(elem_rpt=rpt, elem_cap=cap, elem_min=mn)
+                tot, per = run_elem()
+                res.append((tot, rpt, cap, mn, per))
+                print("elem rpt=%d cap=%d min=%d: %.0f us (R50-weighted)" % (rpt, cap, mn, tot),
+                      flush=True)
+    res.sort(key=lambda r: r[0])
+    print("BEST elem:", res[0][1:4], "%.0f us" % res[0][0])
+    for shp, (a, b) in res[0][4].items():
+        print("   ", shp, "apply %.1f us, backward %.1f us" % (a, b))
+
+
 def bench_conv1x1(args):
     dev = "cuda"
     torch.backends.cudnn.benchmark = False
@@ -205,10 +285,10 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "conv1x1", "optim", "ln", "lamb"])
+    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "optim", "ln", "lamb"])
     a = ap.parse_args()
-    {"bn": bench_bn, "conv1x1": bench_conv1x1, "optim": bench_optim, "ln": bench_ln,
-     "lamb": bench_lamb}[a.what](a)
+    {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
+     "ln": bench_ln, "lamb": bench_lamb}[a.what](a)
 
 
 if __name__ == "__main__":
