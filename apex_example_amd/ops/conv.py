@@ -5,15 +5,40 @@ A stride-1 1x1 convolution over an NHWC tensor is exactly
 already that matrix in memory (channels_last), so forward and data-gradient are
 library GEMMs (hipBLASLt via ``torch.mm``) with no layout change.  Measured on
 MI355X at ResNet-50 bs256 shapes (tools/microbench.py conv1x1, docs/PERF.md),
-hipBLASLt beats MIOpen's 1x1 forward/dgrad kernels by 1.2-4x; MIOpen's weight
-gradient (long-K reduction over M) stays faster than the GEMM library's choice,
-so the weight gradient keeps the MIOpen path.
+hipBLASLt beats MIOpen's 1x1 forward/dgrad kernels by 1.2-4x.
+
+The weight gradient dW[co, ci] = sum_m dY[m, co] X[m, ci] is a long-K GEMM
+(K = N*H*W up to 802,816) with a tiny output, which a single GEMM cannot spread
+over 256 CUs.  It runs split-K: the M rows are cut into S chunks, one batched
+hipBLASLt GEMM computes the S partial products with fp32 output, and one sum
+reduces them - ~2x faster than MIOpen's wgrad on ResNet-50's layer2-4 shapes
+(tools/microbench.py wgrad, profiles/microbench_wgrad.txt).  S targets ~3k rows
+per chunk.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+
+def _split_k(m):
+    s = 1
+    while s < 128 and m % (2 * s) == 0 and m // (2 * s) >= 2048:
+        s *= 2
+    return s
+
+
+def wgrad_1x1(dy_rows, x_rows, out_dtype):
+    """dW[co, ci] = dy_rows^T @ x_rows, split-K over the rows (fp32 partials)."""
+    m, co = dy_rows.shape
+    ci = x_rows.shape[1]
+    S = _split_k(m)
+    if S == 1:
+        return torch.mm(dy_rows.t(), x_rows, out_dtype=torch.float32).to(out_dtype)
+    a = dy_rows.view(S, m // S, co).transpose(1, 2)
+    b = x_rows.view(S, m // S, ci)
+    return torch.bmm(a, b, out_dtype=torch.float32).sum(0).to(out_dtype)
 
 
 def _as_rows(t):
@@ -42,9 +67,7 @@ class Conv1x1GemmFunction(torch.autograd.Function):
             dx2 = torch.mm(_as_rows(dy), weight.reshape(co, ci))
             dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(
-                dy, x, weight, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
-                (False, True, False))[1]
+            dw = wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype).view(weight.shape)
         return dx, dw
 
 
@@ -86,9 +109,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                     dx2 = torch.mm(_as_rows(dy), w2)
                 dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and dy is not None:
-            dw = torch.ops.aten.convolution_backward(
-                dy, x, weight, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
-                (False, True, False))[1]
+            dw = wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype).view(weight.shape)
         return dx, dw
 
 

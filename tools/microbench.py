@@ -204,6 +204,54 @@ def bench_conv1x1(args):
             n, ci, co, hw, gf, tf(t_cf), tf(t_gf), tf(t_cd), tf(t_gd), tf(t_cw), tf(t_gw)))
 
 
+def bench_wgrad(args):
+    """1x1-conv weight gradient dW[co,ci] = sum_m dY[m,co] X[m,ci]: MIOpen vs
+    split-K hipBLASLt (bmm over S row-chunks with fp32 output, then a sum)."""
+    dev = "cuda"
+    torch.backends.cudnn.benchmark = False
+    shapes = [(256, 64, 256, 56), (256, 256, 64, 56), (256, 256, 128, 56), (256, 128, 512, 28),
+              (256, 512, 128, 28), (256, 512, 256, 28), (256, 256, 1024, 14),
+              (256, 1024, 256, 14), (256, 1024, 512, 14), (256, 512, 2048, 7),
+              (256, 2048, 512, 7)]
+    print("| N,Cin,Cout,HW | GFLOP | MIOpen wgrad | " + " | ".join(
+        "splitK %d" % s for s in (1, 2, 4, 8, 16, 32, 64, 128, 256)) + " |")
+    print("|---|---|---|" + "---|" * 9)
+    for (n, ci, co, hw) in shapes:
+        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = torch.randn(co, ci, 1, 1, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy = torch.randn(n, co, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        M = n * hw * hw
+        gf = 2 * M * ci * co / 1e9
+        x2 = x.permute(0, 2, 3, 1).reshape(M, ci)
+        dy2 = dy.permute(0, 2, 3, 1).reshape(M, co)
+        t_cw = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (False, True, False)))
+        ref = torch.ops.aten.convolution_backward(
+            dy, x, w, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
+            (False, True, False))[1].float().reshape(co, ci)
+        cells = []
+        for S in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+            if M % S:
+                cells.append("-")
+                continue
+            a = dy2.view(S, M // S, co).transpose(1, 2)   # [S, co, m]
+            b = x2.view(S, M // S, ci)                     # [S, m, ci]
+
+            def f():
+                return torch.bmm(a, b, out_dtype=torch.float32).sum(0).to(torch.bfloat16)
+
+            out = f().float()
+            err = float((out - ref).norm() / ref.norm())
+            t = timeit(f)
+            cells.append("%.0f us (%.0f TF)%s" % (t, gf / (t * 1e-6) / 1e3,
+                                                  "" if err < 1e-2 else " ERR %.3f" % err))
+        print("| %d,%d,%d,%d | %.1f | %.0f us (%.0f TF) | %s |" % (
+            n, ci, co, hw, gf, t_cw, gf / (t_cw * 1e-6) / 1e3, " | ".join(cells)), flush=True)
+
+
 def bench_optim(args):
     from apex_example_amd.optimizers import FusedAdam, FusedSGD
     from apex_example_amd.models import resnet50
@@ -285,10 +333,10 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "optim", "ln", "lamb"])
+    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "optim", "ln", "lamb"])
     a = ap.parse_args()
     {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
-     "ln": bench_ln, "lamb": bench_lamb}[a.what](a)
+     "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad}[a.what](a)
 
 
 if __name__ == "__main__":
