@@ -14,6 +14,7 @@ import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
 from ..ops.conv import Conv2d1x1
+from ..ops.pool import MaxPool2dNHWC
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
@@ -114,7 +115,8 @@ class ResNet(nn.Module):
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = _BNAct(self.inplanes, True, fused_bn)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        pool = MaxPool2dNHWC if fused_bn else nn.MaxPool2d
+        self.maxpool = pool(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0], 1, zero_init_residual)
         self.layer2 = self._make_layer(block, 128, layers[1], 2, zero_init_residual)
         self.layer3 = self._make_layer(block, 256, layers[2], 2, zero_init_residual)

@@ -8,6 +8,7 @@
 #include "amd_kernels.h"
 #include "amp_ops.h"
 #include "norm_ops.h"
+#include "pool_ops.h"
 #include "reducer.h"
 
 namespace py = pybind11;
@@ -67,6 +68,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto ln = m.def_submodule("layer_norm", "fused LayerNorm / RMSNorm (wave64 row kernels)");
   ln.def("forward", &layer_norm_forward_op);
   ln.def("backward", &layer_norm_backward_op);
+
+  auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
+  pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
+  pool.def("max_bwd", &maxpool2d_nhwc_bwd_op);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);

@@ -1,0 +1,44 @@
+// Torch bindings for the NHWC max-pooling kernels (csrc/hip/pool.hip).
+#include "pool_ops.h"
+
+#include "common.h"
+
+namespace amd {
+
+namespace {
+int64_t out_size(int64_t in, int64_t k, int64_t s, int64_t p) { return (in + 2 * p - k) / s + 1; }
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_fwd_op(at::Tensor x, int64_t k, int64_t s,
+                                                         int64_t p) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4, "maxpool2d_nhwc: 4-D GPU tensor expected");
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && p <= k / 2, "unsupported pool geometry");
+  x = x.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = out_size(H, k, s, p), OW = out_size(W, k, s, p);
+  TORCH_CHECK(OH > 0 && OW > 0, "pool output is empty");
+  auto opt = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  at::Tensor y = at::empty({N, C, OH, OW}, opt);
+  at::Tensor idx = at::empty({N, C, OH, OW}, opt.dtype(at::kByte));
+  maxpool2d_nhwc_fwd(x.data_ptr(), dtype_of(x), y.data_ptr(), idx.data_ptr<uint8_t>(), (int)N,
+                     (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p,
+                     cur_stream());
+  return {y, idx};
+}
+
+at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W, int64_t k,
+                                 int64_t s, int64_t p) {
+  c10::NoGradGuard no_grad_;
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  idx = idx.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == at::kByte, "bad pool index");
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool2d_nhwc_bwd(dy.data_ptr(), idx.data_ptr<uint8_t>(), dtype_of(dy), dx.data_ptr(), (int)N,
+                     (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p,
+                     cur_stream());
+  return dx;
+}
+
+}  // namespace amd

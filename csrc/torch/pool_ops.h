@@ -1,0 +1,14 @@
+#pragma once
+#include <ATen/ATen.h>
+
+#include <tuple>
+
+namespace amd {
+
+// NHWC (channels_last) max pooling: forward returns (y, tap index per element).
+std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_fwd_op(at::Tensor x, int64_t k, int64_t s,
+                                                         int64_t p);
+at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W, int64_t k,
+                                 int64_t s, int64_t p);
+
+}  // namespace amd

@@ -404,3 +404,24 @@ def test_resnet50_fused_vs_plain_forward_backward():
     errs = sorted(float((pa.grad.double().cpu() - pb.grad).norm() / pb.grad.norm())
                   for pa, pb in zip(a.parameters(), ref.parameters()))
     assert errs[-1] < 1.5e-1 and errs[len(errs) // 2] < 8e-2, (errs[-3:], errs[len(errs) // 2])
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 24, 9, 11), 3, 2, 1),
+                                         ((3, 16, 8, 8), 2, 2, 0), ((2, 5, 7, 7), 3, 1, 1)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_maxpool_nhwc(shape, k, s, p, dt):
+    from apex_example_amd.ops.pool import MaxPool2dNHWC
+
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=DEV).to(dt).to(memory_format=torch.channels_last)
+    x[0, 0, 0, :3] = 1.0  # ties inside a window: first max wins, as torch
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    ya = MaxPool2dNHWC(k, s, p)(xa)
+    yb = F.max_pool2d(xb, k, s, p)
+    torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+    dy = torch.randn_like(yb)
+    ya.backward(dy)
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-2 if dt != torch.float32 else 1e-6,
+                               atol=1e-2 if dt != torch.float32 else 1e-6)
