@@ -293,8 +293,7 @@ static void local_stats_impl(const void* x, DType tx, int64_t outer, int64_t C, 
     const T* xp = static_cast<const T*>(x);
     hipLaunchKernelGGL((stats_nchw<T>), dim3(splits, (unsigned)C), dim3(kBNThreads), 0, st, xp,
                        outer, (int)C, inner, vec, ws);
-    hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp, ws, splits,
-                       (int)C, count, inner, out);
+    launch_stats_finalize<T>(xp, ws, splits, C, count, inner, out, st);
   });
 }
 
@@ -362,9 +361,8 @@ void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                          static_cast<const T*>(dy), static_cast<const T*>(x), mean, invstd,
                          static_cast<const TW*>(weight), static_cast<const TW*>(bias),
                          static_cast<const T*>(z), relu, outer, (int)C, inner, vec, ws);
-      hipLaunchKernelGGL((reduce_finalize<TW>), fin_grid(C), dim3(kBNThreads), 0, st, ws, splits,
-                         (int)C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(grad_weight),
-                         static_cast<TW*>(grad_bias));
+      launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(grad_weight),
+                         static_cast<TW*>(grad_bias), st);
     });
   });
 }

@@ -346,8 +346,7 @@ void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut&
       hipLaunchKernelGGL((stats_k<T, decltype(V)::value>), dim3(splits, g.cblocks),
                          dim3(kBNThreads), 0, st, xp, M, (int)C, g.ctile, g.rows_iter, ws);
     });
-    hipLaunchKernelGGL((stats_finalize<T>), fin_grid(C), dim3(kBNThreads), 0, st, xp, ws, splits,
-                       (int)C, M, (int64_t)1, out);
+    launch_stats_finalize<T>(xp, ws, splits, C, M, (int64_t)1, out, st);
   });
 }
 
@@ -390,9 +389,8 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
                            static_cast<const TW*>(b), static_cast<const T*>(z), relu, M, (int)C,
                            g.ctile, g.rows_iter, ws);
       });
-      hipLaunchKernelGGL((reduce_finalize<TW>), fin_grid(C), dim3(kBNThreads), 0, st, ws, splits,
-                         (int)C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
-                         static_cast<TW*>(gb));
+      launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
+                         static_cast<TW*>(gb), st);
     });
   });
 }

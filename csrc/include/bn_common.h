@@ -3,6 +3,8 @@
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
+#include <type_traits>
+
 namespace amd {
 
 constexpr int kBNThreads = 256;
@@ -36,35 +38,36 @@ __device__ __forceinline__ float wload(const TW* p, int c, float dflt) {
   return p ? to_f32(p[c]) : dflt;
 }
 
-// Sum a [split][2][C] partial slab over splits for 8 channels per workgroup:
+// Sum a [split][2][C] partial slab over splits for CH channels per workgroup:
 // every thread accumulates a strided subset of the splits, then wave64
 // xor-shuffles + one LDS pass across the 4 waves (fixed order: deterministic).
-constexpr int kFinCh = 8;
-__device__ __forceinline__ void slab_sum8(const float* __restrict__ slab, int splits, int C, int c0,
-                                          float* out /* __shared__ [2*kFinCh] */) {
-  __shared__ float red[kBNThreads / kWave][2 * kFinCh];
-  float a[2 * kFinCh];
+// CH is picked per layer (fin_ch) so narrow layers still get >= 64 workgroups.
+template <int CH>
+__device__ __forceinline__ void slab_sum(const float* __restrict__ slab, int splits, int C, int c0,
+                                         float* out /* __shared__ [2*CH] */) {
+  __shared__ float red[kBNThreads / kWave][2 * CH];
+  float a[2 * CH];
 #pragma unroll
-  for (int k = 0; k < 2 * kFinCh; ++k) a[k] = 0.f;
+  for (int k = 0; k < 2 * CH; ++k) a[k] = 0.f;
   for (int s = threadIdx.x; s < splits; s += blockDim.x) {
     const float* row = slab + (size_t)s * 2 * C;
 #pragma unroll
-    for (int k = 0; k < kFinCh; ++k) {
+    for (int k = 0; k < CH; ++k) {
       if (c0 + k < C) {
         a[k] += row[c0 + k];
-        a[kFinCh + k] += row[C + c0 + k];
+        a[CH + k] += row[C + c0 + k];
       }
     }
   }
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
 #pragma unroll
-  for (int k = 0; k < 2 * kFinCh; ++k) a[k] = wave_sum(a[k]);
+  for (int k = 0; k < 2 * CH; ++k) a[k] = wave_sum(a[k]);
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 2 * kFinCh; ++k) red[wid][k] = a[k];
+    for (int k = 0; k < 2 * CH; ++k) red[wid][k] = a[k];
   }
   __syncthreads();
-  if (threadIdx.x < 2 * kFinCh) {
+  if (threadIdx.x < 2 * CH) {
     float t = 0.f;
     for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t += red[w][threadIdx.x];
     out[threadIdx.x] = t;
@@ -88,19 +91,19 @@ struct BNStatsOut {
 };
 
 // slab of shifted sums -> statistics; the shift is re-read from x
-template <typename T>
+template <typename T, int CH>
 __global__ void __launch_bounds__(kBNThreads)
     stats_finalize(const T* __restrict__ x, const float* __restrict__ slab, int splits, int C,
                    int64_t count, int64_t shift_stride, BNStatsOut out) {
-  __shared__ float sums[2 * kFinCh];
-  const int c0 = blockIdx.x * kFinCh;
-  slab_sum8(slab, splits, C, c0, sums);
+  __shared__ float sums[2 * CH];
+  const int c0 = blockIdx.x * CH;
+  slab_sum<CH>(slab, splits, C, c0, sums);
   const int k = threadIdx.x;
-  if (k < kFinCh && c0 + k < C) {
+  if (k < CH && c0 + k < C) {
     const int c = c0 + k;
     const float shift = to_f32(x[(int64_t)c * shift_stride]);
     double m = (double)sums[k] / (double)count;
-    double v = (double)sums[kFinCh + k] / (double)count - m * m;
+    double v = (double)sums[CH + k] / (double)count - m * m;
     if (v < 0.0) v = 0.0;
     const float mean = (float)(shift + m);
     out.mean[c] = mean;
@@ -116,18 +119,18 @@ __global__ void __launch_bounds__(kBNThreads)
 }
 
 // slab of (sum dy', sum dy'*(x-mean)) -> sums + grad_weight/grad_bias
-template <typename TW>
+template <typename TW, int CH>
 __global__ void __launch_bounds__(kBNThreads)
     reduce_finalize(const float* __restrict__ slab, int splits, int C,
                     const float* __restrict__ invstd, float* __restrict__ sum_dy,
                     float* __restrict__ sum_dy_xmu, TW* __restrict__ gw, TW* __restrict__ gb) {
-  __shared__ float sums[2 * kFinCh];
-  const int c0 = blockIdx.x * kFinCh;
-  slab_sum8(slab, splits, C, c0, sums);
+  __shared__ float sums[2 * CH];
+  const int c0 = blockIdx.x * CH;
+  slab_sum<CH>(slab, splits, C, c0, sums);
   const int k = threadIdx.x;
-  if (k < kFinCh && c0 + k < C) {
+  if (k < CH && c0 + k < C) {
     const int c = c0 + k;
-    const float s1 = sums[k], s2 = sums[kFinCh + k];
+    const float s1 = sums[k], s2 = sums[CH + k];
     sum_dy[c] = s1;
     sum_dy_xmu[c] = s2;
     if (gw) gw[c] = from_f32<TW>(s2 * invstd[c]);
@@ -135,7 +138,42 @@ __global__ void __launch_bounds__(kBNThreads)
   }
 }
 
-static inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + kFinCh - 1) / kFinCh)); }
+// channels per finalize workgroup: keep >= ~128 workgroups where C allows
+static inline int fin_ch(int64_t C) { return C >= 1024 ? 8 : C >= 512 ? 4 : C >= 256 ? 2 : 1; }
+
+template <typename F>
+static inline void fin_dispatch(int64_t C, F&& f) {
+  switch (fin_ch(C)) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    default: f(std::integral_constant<int, 8>{}); break;
+  }
+}
+
+template <typename T>
+static inline void launch_stats_finalize(const T* x, const float* slab, int splits, int64_t C,
+                                         int64_t count, int64_t shift_stride,
+                                         const BNStatsOut& out, hipStream_t st) {
+  fin_dispatch(C, [&](auto ch) {
+    constexpr int CH = decltype(ch)::value;
+    hipLaunchKernelGGL((stats_finalize<T, CH>), dim3((unsigned)((C + CH - 1) / CH)),
+                       dim3(kBNThreads), 0, st, x, slab, splits, (int)C, count, shift_stride,
+                       out);
+  });
+}
+
+template <typename TW>
+static inline void launch_reduce_finalize(const float* slab, int splits, int64_t C,
+                                          const float* invstd, float* sum_dy, float* sum_dy_xmu,
+                                          TW* gw, TW* gb, hipStream_t st) {
+  fin_dispatch(C, [&](auto ch) {
+    constexpr int CH = decltype(ch)::value;
+    hipLaunchKernelGGL((reduce_finalize<TW, CH>), dim3((unsigned)((C + CH - 1) / CH)),
+                       dim3(kBNThreads), 0, st, slab, splits, (int)C, invstd, sum_dy, sum_dy_xmu,
+                       gw, gb);
+  });
+}
 
 // ---- NHWC launchers (bn_nhwc.hip) -------------------------------------------
 // Grid sizing knobs (rows per thread, block caps/floors); settable at run time
