@@ -21,6 +21,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import _native
+
 
 def _split_k(m):
     s = 1
@@ -136,3 +138,51 @@ class Conv2d1x1(nn.Conv2d):
         return (self.stride == (1, 1) and self.bias is None and x.is_cuda and x.dim() == 4
                 and x.is_contiguous(memory_format=torch.channels_last)
                 and x.dtype == self.weight.dtype and self.groups == 1)
+
+
+def _rot_weight(weight):
+    """W'[ci, co, r, s] = W[co, ci, 2-r, 2-s]: the data gradient of a 3x3 stride-1
+    pad-1 conv is the same conv applied to dY with W'."""
+    return weight.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
+class Conv3x3Function(torch.autograd.Function):
+    """3x3 / stride 1 / pad 1 NHWC bf16 conv on the MFMA implicit-GEMM kernel
+    (csrc/hip/conv_igemm.hip) for forward and data gradient; MIOpen computes
+    the weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        ctx.save_for_backward(x, weight)
+        return _native.require().conv.conv3x3_fwd(x, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _native.require().conv.conv3x3_fwd(dy, _rot_weight(weight))
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(
+                dy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                (False, True, False))[1]
+        return dx, dw
+
+
+class Conv2d3x3(nn.Conv2d):
+    """nn.Conv2d(k=3, padding=1) whose stride-1 channels-last bf16 GPU path runs
+    the MFMA implicit-GEMM kernel; everything else uses the regular conv."""
+
+    def __init__(self, in_planes, out_planes, stride=1, bias=False):
+        super().__init__(in_planes, out_planes, kernel_size=3, stride=stride, padding=1,
+                         bias=bias)
+
+    def forward(self, x):
+        if (self.stride == (1, 1) and self.bias is None and x.is_cuda and x.dim() == 4
+                and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last) and self.groups == 1
+                and self.in_channels % 64 == 0 and self.out_channels % 64 == 0):
+            return Conv3x3Function.apply(x, self.weight)
+        return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
+                        self.groups)

@@ -193,4 +193,9 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
 void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
                         int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 
+// ---- implicit-GEMM 3x3 stride-1 pad-1 conv, NHWC bf16, MFMA (conv_igemm.hip) ----
+bool conv3x3_nhwc_supported(int Cin, int Cout);
+void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin,
+                      int Cout, hipStream_t st);
+
 }  // namespace amd

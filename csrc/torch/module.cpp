@@ -72,6 +72,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
   pool.def("max_bwd", &maxpool2d_nhwc_bwd_op);
+  auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
+  conv.def("conv3x3_fwd", &conv3x3_nhwc_fwd_op);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);

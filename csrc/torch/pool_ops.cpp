@@ -42,3 +42,25 @@ at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64
 }
 
 }  // namespace amd
+
+namespace amd {
+
+at::Tensor conv3x3_nhwc_fwd_op(at::Tensor x, at::Tensor w) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4, "conv3x3: 4-D GPU tensors expected");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+              "conv3x3: bf16 only");
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = w.size(0);
+  TORCH_CHECK(w.size(1) == Cin && w.size(2) == 3 && w.size(3) == 3, "conv3x3: weight shape");
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv3x3: channels must be x64");
+  TORCH_CHECK(N * H * W < (int64_t)1 << 31, "conv3x3: too many pixels");
+  x = x.contiguous(at::MemoryFormat::ChannelsLast);
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);  // [Cout][3][3][Cin] in memory
+  at::Tensor y = at::empty({N, Cout, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  conv3x3_nhwc_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)Cin,
+                   (int)Cout, cur_stream());
+  return y;
+}
+
+}  // namespace amd

@@ -11,4 +11,7 @@ std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_fwd_op(at::Tensor x, int64_t k
 at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W, int64_t k,
                                  int64_t s, int64_t p);
 
+// 3x3 stride-1 pad-1 conv, NHWC bf16, implicit GEMM on MFMA (conv_igemm.hip)
+at::Tensor conv3x3_nhwc_fwd_op(at::Tensor x, at::Tensor w);
+
 }  // namespace amd

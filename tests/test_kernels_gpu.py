@@ -425,3 +425,30 @@ def test_maxpool_nhwc(shape, k, s, p, dt):
     yb.backward(dy)
     torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-2 if dt != torch.float32 else 1e-6,
                                atol=1e-2 if dt != torch.float32 else 1e-6)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 9, 9), (2, 128, 128, 5, 7), (3, 64, 192, 8, 8),
+                                   (1, 256, 64, 14, 14), (2, 64, 128, 1, 1)])
+def test_conv3x3_mfma_igemm(shape):
+    """MFMA implicit-GEMM 3x3 conv (fwd + dgrad via rotated weights) vs fp32 conv."""
+    from apex_example_amd.ops.conv import Conv2d3x3
+
+    n, ci, co, h, w = shape
+    torch.manual_seed(0)
+    m = Conv2d3x3(ci, co).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(n, ci, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    xr = x.detach().float().clone().requires_grad_(True)
+    wr = m.weight.detach().float().clone().requires_grad_(True)
+    y = m(x)
+    yr = F.conv2d(xr, wr, padding=1)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    scale = yr.abs().max().item()
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2 * scale)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy)
+    gs = xr.grad.abs().max().item()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * gs)
+    ws = wr.grad.abs().max().item()
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=2e-2 * ws)

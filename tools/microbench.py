@@ -252,6 +252,40 @@ def bench_wgrad(args):
             n, ci, co, hw, gf, t_cw, gf / (t_cw * 1e-6) / 1e3, " | ".join(cells)), flush=True)
 
 
+def bench_conv3x3(args):
+    """3x3 stride-1 convs of ResNet-50: MIOpen vs the MFMA implicit-GEMM kernel."""
+    from apex_example_amd import _native
+    from apex_example_amd.ops.conv import _rot_weight
+
+    cv = _native.require().conv
+    dev = "cuda"
+    torch.backends.cudnn.benchmark = False
+    print("| N,C,K,HW | GFLOP | MIOpen fwd | MFMA fwd | MIOpen dgrad | MFMA dgrad (+rot) | max rel err |")
+    print("|---|---|---|---|---|---|---|")
+    for (n, c, k, hw) in [(256, 64, 64, 56), (256, 128, 128, 28), (256, 256, 256, 14),
+                          (256, 512, 512, 7)]:
+        x = torch.randn(n, c, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = (torch.randn(k, c, 3, 3, device=dev, dtype=torch.bfloat16) * 0.05).to(
+            memory_format=torch.channels_last)
+        dy = torch.randn(n, k, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        gf = 2 * n * hw * hw * c * k * 9 / 1e9
+        t_mf = timeit(lambda: F.conv2d(x, w, padding=1))
+        t_of = timeit(lambda: cv.conv3x3_fwd(x, w))
+        t_md = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1, (True, False, False)))
+        t_od = timeit(lambda: cv.conv3x3_fwd(dy, _rot_weight(w)))
+        ref = F.conv2d(x, w, padding=1).float()
+        err = float((cv.conv3x3_fwd(x, w).float() - ref).abs().max() / ref.abs().max())
+
+        def tf(t):
+            return "%.0f us (%.0f TF)" % (t, gf / (t * 1e-6) / 1e3)
+
+        print("| %d,%d,%d,%d | %.1f | %s | %s | %s | %s | %.2e |" % (
+            n, c, k, hw, gf, tf(t_mf), tf(t_of), tf(t_md), tf(t_od), err), flush=True)
+
+
 def bench_optim(args):
     from apex_example_amd.optimizers import FusedAdam, FusedSGD
     from apex_example_amd.models import resnet50
@@ -333,10 +367,11 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "optim", "ln", "lamb"])
+    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "optim", "ln", "lamb"])
     a = ap.parse_args()
     {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
-     "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad}[a.what](a)
+     "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
+     "conv3x3": bench_conv3x3}[a.what](a)
 
 
 if __name__ == "__main__":
