@@ -1,6 +1,8 @@
 """ResNet family (He et al. 2015, v1.5: stride on the 3x3 conv), defined in-repo
 (torchvision is not available).  ResNet-50 = 25,557,032 parameters in 161 tensors.
 
+``gemm_1x1=True`` runs the stride-1 1x1 convs as hipBLASLt GEMMs and the
+stride-1 3x3 convs on the MFMA implicit-GEMM kernel (ops/conv.py).
 ``fused_bn=True`` replaces each BatchNorm(+ReLU)(+residual add) with the fused
 gfx950 op ``BatchNorm2dReLU`` (one stats pass + one elementwise pass forward,
 one reduction + one elementwise pass backward, ReLU and the residual add folded
@@ -13,11 +15,13 @@ import torch
 import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
-from ..ops.conv import Conv2d1x1
+from ..ops.conv import Conv2d1x1, Conv2d3x3
 from ..ops.pool import MaxPool2dNHWC
 
 
-def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
+def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1, mfma=False):
+    if mfma and stride == 1 and groups == 1 and dilation == 1:
+        return Conv2d3x3(in_planes, out_planes)
     return nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation,
                      groups=groups, bias=False, dilation=dilation)
 
@@ -57,9 +61,9 @@ class BasicBlock(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None, fused_bn=False,
                  zero_init_residual=False, gemm_1x1=False):
         super().__init__()
-        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.conv1 = conv3x3(inplanes, planes, stride, mfma=gemm_1x1)
         self.bn1 = _BNAct(planes, True, fused_bn)
-        self.conv2 = conv3x3(planes, planes)
+        self.conv2 = conv3x3(planes, planes, mfma=gemm_1x1)
         self.bn2 = _BNAct(planes, True, fused_bn, zero_init_residual)
         self.downsample = downsample
 
@@ -78,7 +82,7 @@ class Bottleneck(nn.Module):
         width = planes
         self.conv1 = conv1x1(inplanes, width, gemm=gemm_1x1)
         self.bn1 = _BNAct(width, True, fused_bn)
-        self.conv2 = conv3x3(width, width, stride)
+        self.conv2 = conv3x3(width, width, stride, mfma=gemm_1x1)
         self.bn2 = _BNAct(width, True, fused_bn)
         self.conv3 = conv1x1(width, planes * self.expansion, gemm=gemm_1x1)
         self.bn3 = _BNAct(planes * self.expansion, True, fused_bn, zero_init_residual)
