@@ -147,9 +147,9 @@ def _rot_weight(weight):
 
 
 class Conv3x3Function(torch.autograd.Function):
-    """3x3 / stride 1 / pad 1 NHWC bf16 conv on the MFMA implicit-GEMM kernel
-    (csrc/hip/conv_igemm.hip) for forward and data gradient; MIOpen computes
-    the weight gradient."""
+    """3x3 / stride 1 / pad 1 NHWC bf16 conv on the MFMA implicit-GEMM kernels
+    (csrc/hip/conv_igemm.hip): forward, data gradient (same kernel, rotated
+    weights) and weight gradient (split-K over pixels, transposed LDS reads)."""
 
     @staticmethod
     def forward(ctx, x, weight):
@@ -164,9 +164,7 @@ class Conv3x3Function(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _native.require().conv.conv3x3_fwd(dy, _rot_weight(weight))
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(
-                dy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
-                (False, True, False))[1]
+            dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype)
         return dx, dw
 
 

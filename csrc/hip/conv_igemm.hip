@@ -190,9 +190,222 @@ __global__ void __launch_bounds__(kCT, 2)
   }
 }
 
+
+// ============================================================================
+// Weight gradient: dW[co, r, s, ci] = sum_p dY[p, co] * x[shift_rs(p), ci].
+// Per tap (r, s) a GEMM with rows = co, cols = ci and K = output pixels, split
+// over pixel ranges (grid.y) for parallelism; fp32 partials [split][tap][co][ci]
+// are summed by wgrad_reduce_k.  Both operands arrive pixel-major ([k][col]), so
+// the MFMA fragments (8 consecutive k per lane) are read with ds_read_b64_tr_b16
+// transposed reads from LDS images whose 16-byte chunks carry a row swizzle that
+// keeps each 32-lane half of a transposed read conflict-free (8 rows apart,
+// 2 chunks each -> 16 distinct bank slots).
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+template <int RB>  // row bytes: 128 or 256
+__device__ __forceinline__ int tr_swz(int row, int chunk) {
+  if constexpr (RB == 256) {
+    return row * 256 + ((chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+  } else {
+    return row * 128 + ((chunk ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1)) << 4);
+  }
+}
+
+// 8 consecutive k (rows kb..kb+7) of column (c0 + lane&15) as an MFMA fragment
+template <int RB>
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned char* T, int kb, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = c0 + 4 * p;               // element column of this lane's 4-wide piece
+  const int chunk = col >> 3, half = (col >> 2) & 1;
+  const unsigned char* a0 = T + tr_swz<RB>(kb + q, chunk) + 8 * half;
+  const unsigned char* a1 = T + tr_swz<RB>(kb + 4 + q, chunk) + 8 * half;
+  v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)a0);
+  v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)a1);
+  bf16x8 f;
+  v4s_t* fp = reinterpret_cast<v4s_t*>(&f);
+  fp[0] = lo;
+  fp[1] = hi;
+  return f;
+}
+
+__device__ __forceinline__ int fdiv(int a, int b, float inv) {
+  int q = (int)((float)a * inv);
+  int r = a - q * b;
+  if (r < 0) --q;
+  else if (r >= b) ++q;
+  return q;
+}
+
+template <int BM, int BN, int NB>
+__global__ void __launch_bounds__(kCT, 2)
+    conv3x3_wgrad_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                    float* __restrict__ part, int H, int W, int Cin, int Cout, int M, int pps) {
+  constexpr int BK = 64;                         // pixels per K-tile
+  constexpr int RA = BM * 2, RBb = BN * 2;       // row bytes of the A / B images
+  constexpr int A_BYTES = BK * RA, B_BYTES = BK * RBb, BUF = A_BYTES + B_BYTES;
+  constexpr int CA = RA / 16, CB = RBb / 16;     // 16-byte chunks per row
+  constexpr int AI = A_BYTES / 1024 / 4, BI = B_BYTES / 1024 / 4;  // glds per wave
+  constexpr int G = AI + BI;
+  constexpr int TM = BM / 2, TN = BN / 2;        // 2x2 waves
+  constexpr int FM = TM / 16, FN = TN / 16;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[NB * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ci_tiles = Cin / BN, co_tiles = Cout / BM;
+  int t = blockIdx.x;
+  const int tap = t % 9;
+  t /= 9;
+  const int cit = t % ci_tiles, cot = t / ci_tiles;
+  const int co0 = cot * BM, ci0 = cit * BN;
+  const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+  const int p_begin = blockIdx.y * pps;
+  int p_end = p_begin + pps;
+  if (p_end > M) p_end = M;
+  const int KT = (p_end - p_begin + BK - 1) / BK;
+  const float invW = 1.f / (float)W, invH = 1.f / (float)H;
+  const int shift = dr * W + ds;
+
+  // glds lane geometry (per 1 KiB wave-instruction: 1024/RA rows of the A image)
+  constexpr int ARPI = 1024 / RA, BRPI = 1024 / RBb;  // rows per instruction
+  const int arow_l = lane / CA, apch = lane % CA;
+  const int brow_l = lane / CB, bpch = lane % CB;
+
+#define WG_ISSUE(kt_)                                                                        \
+  {                                                                                          \
+    unsigned char* A_ = lds + ((kt_) % NB) * BUF;                                            \
+    unsigned char* B_ = A_ + A_BYTES;                                                        \
+    const int pk_ = p_begin + (kt_) * BK;                                                    \
+    _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                         \
+      const int row = (wid * AI + q) * ARPI + arow_l;                                        \
+      const int chunk = (tr_swz<RA>(row, apch) - row * RA) >> 4; /* = apch ^ f(row) */      \
+      const int pix = pk_ + row;                                                             \
+      const void* src = pix < p_end ? (const void*)(dy + (int64_t)pix * Cout + co0 + chunk * 8) \
+                                     : (const void*)g_zero16;                                \
+      glds16(src, A_ + (wid * AI + q) * 1024);                                               \
+    }                                                                                        \
+    _Pragma("unroll") for (int q = 0; q < BI; ++q) {                                         \
+      const int row = (wid * BI + q) * BRPI + brow_l;                                        \
+      const int chunk = (tr_swz<RBb>(row, bpch) - row * RBb) >> 4;                           \
+      const int pix = pk_ + row;                                                             \
+      const int tq = fdiv(pix, W, invW);                                                     \
+      const int w_ = pix - tq * W;                                                           \
+      const int h_ = tq - fdiv(tq, H, invH) * H;                                             \
+      const int hh = h_ + dr, ww = w_ + ds;                                                  \
+      const bool ok = pix < p_end && hh >= 0 && hh < H && ww >= 0 && ww < W;                 \
+      const void* src = ok ? (const void*)(x + (int64_t)(pix + shift) * Cin + ci0 + chunk * 8) \
+                           : (const void*)g_zero16;                                          \
+      glds16(src, B_ + (wid * BI + q) * 1024);                                               \
+    }                                                                                        \
+  }
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < KT) WG_ISSUE(p);
+
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + NB - 2 < KT) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NB - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + NB - 1 < KT) WG_ISSUE(kt + NB - 1);
+    const unsigned char* A = lds + (kt % NB) * BUF;
+    const unsigned char* B = A + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kb = ks * 32 + (lane >> 4) * 8;
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = tr_frag<RA>(A, kb, wm * TM + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = tr_frag<RBb>(B, kb, wn * TN + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef WG_ISSUE
+
+  // partial tile: rows = co (4 per lane group), cols = ci (lane & 15)
+  float* out = part + ((int64_t)blockIdx.y * 9 + tap) * Cout * Cin;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wm * TM + i * 16 + fg * 4 + e;
+        const int ci = ci0 + wn * TN + j * 16 + fr;
+        out[(int64_t)co * Cin + ci] = acc[i][j][e];
+      }
+}
+
+// dW[co][tap][ci] (KRSC) = sum over splits of part[split][tap][co][ci]
+template <typename TO>
+__global__ void __launch_bounds__(256)
+    wgrad_reduce_k(const float* __restrict__ part, int S, int Cout, int Cin, TO* __restrict__ dw) {
+  const int64_t total = (int64_t)9 * Cout * Cin;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(e % Cin);
+    const int64_t r = e / Cin;
+    const int co = (int)(r % Cout);
+    const int tap = (int)(r / Cout);
+    float sum = 0.f;
+    for (int s = 0; s < S; ++s) sum += part[(int64_t)s * total + e];
+    dw[((int64_t)co * 9 + tap) * Cin + ci] = from_f32<TO>(sum);
+  }
+}
 }  // namespace
 
 bool conv3x3_nhwc_supported(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
+
+int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout) {
+  const int M = N * H * W;
+  const int bm = (Cout % 128 == 0 && Cin % 128 == 0) ? 128 : 64;
+  const int tiles = (Cout / bm) * (Cin / bm) * 9;
+  int S = (1536 + tiles - 1) / tiles;
+  const int max_s = M / (64 * 4);  // >= 4 K-tiles per split
+  if (S > max_s) S = max_s;
+  return S < 1 ? 1 : S;
+}
+
+void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
+                        int N, int H, int W, int Cin, int Cout, int S, hipStream_t st) {
+  const int M = N * H * W;
+  int pps = (M + S - 1) / S;
+  pps = (pps + 63) / 64 * 64;
+  const auto* dyp = static_cast<const bf16_t*>(dy);
+  const auto* xp = static_cast<const bf16_t*>(x);
+  if (Cout % 128 == 0 && Cin % 128 == 0) {
+    const int tiles = (Cout / 128) * (Cin / 128) * 9;
+    hipLaunchKernelGGL((conv3x3_wgrad_k<128, 128, 2>), dim3(tiles, S), dim3(kCT), 0, st, dyp, xp,
+                       part, H, W, Cin, Cout, M, pps);
+  } else {
+    const int tiles = (Cout / 64) * (Cin / 64) * 9;
+    hipLaunchKernelGGL((conv3x3_wgrad_k<64, 64, 3>), dim3(tiles, S), dim3(kCT), 0, st, dyp, xp,
+                       part, H, W, Cin, Cout, M, pps);
+  }
+  const int64_t total = (int64_t)9 * Cout * Cin;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  if (dw_fp32)
+    hipLaunchKernelGGL((wgrad_reduce_k<float>), dim3(blocks), dim3(256), 0, st, part, S, Cout, Cin,
+                       static_cast<float*>(dw));
+  else
+    hipLaunchKernelGGL((wgrad_reduce_k<bf16_t>), dim3(blocks), dim3(256), 0, st, part, S, Cout,
+                       Cin, static_cast<bf16_t*>(dw));
+}
 
 void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin,
                       int Cout, hipStream_t st) {

@@ -63,4 +63,26 @@ at::Tensor conv3x3_nhwc_fwd_op(at::Tensor x, at::Tensor w) {
   return y;
 }
 
+at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && dy.dim() == 4, "conv3x3_wgrad: 4-D GPU tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16,
+              "conv3x3_wgrad: bf16 only");
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv3x3_wgrad: shapes");
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv3x3_wgrad: channels must be x64");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv3x3_wgrad: out dtype");
+  x = x.contiguous(at::MemoryFormat::ChannelsLast);
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  const int S = conv3x3_wgrad_splits((int)N, (int)H, (int)W, (int)Cin, (int)Cout);
+  at::Tensor part = at::empty({(int64_t)S * 9 * Cout * Cin}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({Cout, Cin, 3, 3},
+                            x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  conv3x3_nhwc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(),
+                     out_dtype == at::kFloat, (int)N, (int)H, (int)W, (int)Cin, (int)Cout, S,
+                     cur_stream());
+  return dw;
+}
+
 }  // namespace amd
