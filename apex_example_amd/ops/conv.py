@@ -140,6 +140,9 @@ class Conv2d1x1(nn.Conv2d):
                 and x.dtype == self.weight.dtype and self.groups == 1)
 
 
+_MFMA_WGRAD_MIN_W = 48
+
+
 def _rot_weight(weight):
     """W'[ci, co, r, s] = W[co, ci, 2-r, 2-s]: the data gradient of a 3x3 stride-1
     pad-1 conv is the same conv applied to dY with W'."""
@@ -164,7 +167,14 @@ class Conv3x3Function(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _native.require().conv.conv3x3_fwd(dy, _rot_weight(weight))
         if ctx.needs_input_grad[1]:
-            dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype)
+            # the all-taps MFMA wgrad kernel beats MIOpen on the 56x56 layers only
+            # (profiles/microbench_conv3x3.txt); its strip is sized for W <= 56
+            if 56 >= x.size(3) >= _MFMA_WGRAD_MIN_W:
+                dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype)
+            else:
+                dw = torch.ops.aten.convolution_backward(
+                    dy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                    (False, True, False))[1]
         return dx, dw
 
 

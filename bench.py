@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 # vs_baseline: BASELINE.md publishes no number for the reference; the comparator
 # is the stock PyTorch-ROCm path measured on MI355X with this same harness
 # (BASELINE.md section 2), per GPU, bs 256.
-STOCK_BASELINE_PER_GPU = {"resnet50": 6011.4}
+STOCK_BASELINE_PER_GPU = {"resnet50": 6011.4}  # BASELINE.md section 2
 
 
 def parse():

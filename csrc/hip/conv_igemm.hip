@@ -77,26 +77,34 @@ __global__ void __launch_bounds__(kCT, 2)
   // instructions of 8 rows; lane -> (row = base + lane/8, physical chunk lane%8)
   // fetching the logical chunk that the swizzle stores at that position.
   const int lrow = lane >> 3, pchunk = lane & 7;
-  int an[AI], ah[AI], aw[AI], ach[AI];
-  bool aval[AI];
+  // per DMA row: source pointer at tap (1,1) / channel chunk, and a 9-bit mask of
+  // the taps whose shifted pixel is inside the image (so the K loop only adds a
+  // wave-uniform offset and tests one bit per row)
+  const bf16_t* abase[AI];
+  unsigned amask[AI];
 #pragma unroll
   for (int q = 0; q < AI; ++q) {
     const int row = wid * (kBM / 4) + q * 8 + lrow;
-    ach[q] = pchunk ^ ((row >> 1) & 7);
+    const int ch = pchunk ^ ((row >> 1) & 7);
     const int m = m0 + row;
-    aval[q] = m < M;
-    const int mm = aval[q] ? m : 0;
-    an[q] = mm / HW;
-    const int rem = mm - an[q] * HW;
-    ah[q] = rem / W;
-    aw[q] = rem - ah[q] * W;
+    const int mm = m < M ? m : 0;
+    const int n = mm / HW;
+    const int rem = mm - n * HW;
+    const int h = rem / W, w = rem - (rem / W) * W;
+    abase[q] = x + (int64_t)mm * Cin + ch * 8;
+    unsigned mk = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = h + t / 3 - 1, ww = w + t % 3 - 1;
+      if (m < M && hh >= 0 && hh < H && ww >= 0 && ww < W) mk |= 1u << t;
+    }
+    amask[q] = mk;
   }
-  int bco[BI], bch[BI];
+  const bf16_t* bbase[BI];
 #pragma unroll
   for (int q = 0; q < BI; ++q) {
     const int row = wid * (BN / 4) + q * 8 + lrow;
-    bch[q] = pchunk ^ ((row >> 1) & 7);
-    bco[q] = n0 + row;
+    bbase[q] = wt + (int64_t)(n0 + row) * 9 * Cin + (pchunk ^ ((row >> 1) & 7)) * 8;
   }
   const int kc_per_tap = Cin / kBK;
   const int KT = 9 * kc_per_tap;
@@ -105,20 +113,17 @@ __global__ void __launch_bounds__(kCT, 2)
   {                                                                                         \
     const int tap_ = (kt_) / kc_per_tap;                                                    \
     const int c0_ = ((kt_) - tap_ * kc_per_tap) * kBK;                                      \
-    const int dr_ = tap_ / 3 - 1, ds_ = tap_ % 3 - 1;                                       \
+    const int64_t aoff_ = (int64_t)((tap_ / 3 - 1) * W + (tap_ % 3 - 1)) * Cin + c0_;       \
+    const int boff_ = tap_ * Cin + c0_;                                                     \
     unsigned char* A_ = lds + ((kt_) % NB) * BUF;                                           \
     unsigned char* B_ = A_ + A_BYTES;                                                       \
     _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                        \
-      const int hh = ah[q] + dr_, ww = aw[q] + ds_;                                         \
-      const bool ok = aval[q] && hh >= 0 && hh < H && ww >= 0 && ww < W;                    \
-      const bf16_t* src = x + (((int64_t)an[q] * H + hh) * W + ww) * Cin + c0_ + ach[q] * 8; \
-      glds16(ok ? (const void*)src : (const void*)g_zero16,                                 \
+      const bool ok = (amask[q] >> tap_) & 1u;                                              \
+      glds16(ok ? (const void*)(abase[q] + aoff_) : (const void*)g_zero16,                  \
              A_ + (wid * (kBM / 4) + q * 8) * kRowBytes);                                   \
     }                                                                                       \
-    _Pragma("unroll") for (int q = 0; q < BI; ++q) {                                        \
-      const bf16_t* src = wt + ((int64_t)bco[q] * 9 + tap_) * Cin + c0_ + bch[q] * 8;       \
-      glds16(src, B_ + (wid * (BN / 4) + q * 8) * kRowBytes);                               \
-    }                                                                                       \
+    _Pragma("unroll") for (int q = 0; q < BI; ++q)                                          \
+      glds16(bbase[q] + boff_, B_ + (wid * (BN / 4) + q * 8) * kRowBytes);                  \
   }
 
   f32x4_t acc[FM][FN];
@@ -228,6 +233,28 @@ __device__ __forceinline__ bf16x8 tr_frag(const unsigned char* T, int kb, int c0
   return f;
 }
 
+__device__ __forceinline__ bf16x8 tr_pair(const unsigned char* T, unsigned lo, unsigned hi) {
+  v4s_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(T + lo));
+  v4s_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(T + hi));
+  bf16x8 f;
+  v4s_t* fp = reinterpret_cast<v4s_t*>(&f);
+  fp[0] = a;
+  fp[1] = b;
+  return f;
+}
+
+// byte offsets of the two transposed reads (k rows kb..kb+3 / kb+4..kb+7) of column
+// block c0 for this lane; column block c0+16 is the same with bit 5 flipped
+// (its chunk index differs by 2 with no carry)
+template <int RB>
+__device__ __forceinline__ void tr_offsets(int kb, int c0, int lane, unsigned& lo, unsigned& hi) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = c0 + 4 * p;
+  const int chunk = col >> 3, half = (col >> 2) & 1;
+  lo = (unsigned)(tr_swz<RB>(kb + q, chunk) + 8 * half);
+  hi = (unsigned)(tr_swz<RB>(kb + 4 + q, chunk) + 8 * half);
+}
+
 __device__ __forceinline__ int fdiv(int a, int b, float inv) {
   int q = (int)((float)a * inv);
   int r = a - q * b;
@@ -236,78 +263,94 @@ __device__ __forceinline__ int fdiv(int a, int b, float inv) {
   return q;
 }
 
-template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(kCT, 2)
-    conv3x3_wgrad_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                    float* __restrict__ part, int H, int W, int Cin, int Cout, int M, int pps) {
-  constexpr int BK = 64;                         // pixels per K-tile
-  constexpr int RA = BM * 2, RBb = BN * 2;       // row bytes of the A / B images
-  constexpr int A_BYTES = BK * RA, B_BYTES = BK * RBb, BUF = A_BYTES + B_BYTES;
-  constexpr int CA = RA / 16, CB = RBb / 16;     // 16-byte chunks per row
-  constexpr int AI = A_BYTES / 1024 / 4, BI = B_BYTES / 1024 / 4;  // glds per wave
-  constexpr int G = AI + BI;
-  constexpr int TM = BM / 2, TN = BN / 2;        // 2x2 waves
-  constexpr int FM = TM / 16, FN = TN / 16;
+// All 9 taps per workgroup.  The GEMM K index runs over output pixels laid out
+// in the zero-PADDED row width Wp = W + 2 (q = h*Wp + w', the 2 extra columns
+// per row are dummy K rows whose dY is zero), because then the input a tap
+// (r, s) needs is x_padded[q + r*Wp + s]: for a K-tile of BK consecutive q all
+// 9 taps read ONE contiguous strip of the padded input (BK + 2*Wp + 2 rows),
+// loaded once, instead of 9 separate shifted tiles.  Padding = zero-page lanes.
+constexpr int kWgBK = 64, kWgMaxW = 56;
+constexpr int kWgStrip = kWgBK + 2 * (kWgMaxW + 2) + 2;   // 182 rows max
+constexpr int kWgStripI = (kWgStrip + 31) / 32;            // glds per wave (8 rows each)
+
+template <int NB>
+__global__ void __launch_bounds__(kCT, 1)
+    conv3x3_wgrad9_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                     float* __restrict__ part, int H, int W, int Cin, int Cout, int kpi,
+                     int kps, int total_kt) {
+  constexpr int BM = 64, BN = 64, BK = kWgBK, RB = 128;
+  constexpr int A_BYTES = BK * RB;                       // 8 KiB
+  constexpr int S_BYTES = kWgStripI * 4 * 1024;          // strip rows, 1 KiB per instruction
+  constexpr int BUF = A_BYTES + S_BYTES;
+  constexpr int AI = A_BYTES / 1024 / 4;                 // 2 glds per wave
+  constexpr int G = AI + kWgStripI;
+  constexpr int FM = 2, FN = 2;                          // 2x2 waves of 32x32 per tap
   __shared__ __attribute__((aligned(1024))) unsigned char lds[NB * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int ci_tiles = Cin / BN, co_tiles = Cout / BM;
-  int t = blockIdx.x;
-  const int tap = t % 9;
-  t /= 9;
-  const int cit = t % ci_tiles, cot = t / ci_tiles;
+  const int ci_tiles = Cin / BN;
+  const int cit = blockIdx.x % ci_tiles, cot = blockIdx.x / ci_tiles;
   const int co0 = cot * BM, ci0 = cit * BN;
-  const int dr = tap / 3 - 1, ds = tap % 3 - 1;
-  const int p_begin = blockIdx.y * pps;
-  int p_end = p_begin + pps;
-  if (p_end > M) p_end = M;
-  const int KT = (p_end - p_begin + BK - 1) / BK;
-  const float invW = 1.f / (float)W, invH = 1.f / (float)H;
-  const int shift = dr * W + ds;
+  const int kt_begin = blockIdx.y * kps;
+  int kt_end = kt_begin + kps;
+  if (kt_end > total_kt) kt_end = total_kt;
+  const int KT = kt_end - kt_begin;
+  const int Wp = W + 2, HWp = H * Wp;
+  const float invWp = 1.f / (float)Wp;
+  const int lrow = lane >> 3, pch = lane & 7;
 
-  // glds lane geometry (per 1 KiB wave-instruction: 1024/RA rows of the A image)
-  constexpr int ARPI = 1024 / RA, BRPI = 1024 / RBb;  // rows per instruction
-  const int arow_l = lane / CA, apch = lane % CA;
-  const int brow_l = lane / CB, bpch = lane % CB;
-
-#define WG_ISSUE(kt_)                                                                        \
-  {                                                                                          \
-    unsigned char* A_ = lds + ((kt_) % NB) * BUF;                                            \
-    unsigned char* B_ = A_ + A_BYTES;                                                        \
-    const int pk_ = p_begin + (kt_) * BK;                                                    \
-    _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                         \
-      const int row = (wid * AI + q) * ARPI + arow_l;                                        \
-      const int chunk = (tr_swz<RA>(row, apch) - row * RA) >> 4; /* = apch ^ f(row) */      \
-      const int pix = pk_ + row;                                                             \
-      const void* src = pix < p_end ? (const void*)(dy + (int64_t)pix * Cout + co0 + chunk * 8) \
-                                     : (const void*)g_zero16;                                \
-      glds16(src, A_ + (wid * AI + q) * 1024);                                               \
-    }                                                                                        \
-    _Pragma("unroll") for (int q = 0; q < BI; ++q) {                                         \
-      const int row = (wid * BI + q) * BRPI + brow_l;                                        \
-      const int chunk = (tr_swz<RBb>(row, bpch) - row * RBb) >> 4;                           \
-      const int pix = pk_ + row;                                                             \
-      const int tq = fdiv(pix, W, invW);                                                     \
-      const int w_ = pix - tq * W;                                                           \
-      const int h_ = tq - fdiv(tq, H, invH) * H;                                             \
-      const int hh = h_ + dr, ww = w_ + ds;                                                  \
-      const bool ok = pix < p_end && hh >= 0 && hh < H && ww >= 0 && ww < W;                 \
-      const void* src = ok ? (const void*)(x + (int64_t)(pix + shift) * Cin + ci0 + chunk * 8) \
-                           : (const void*)g_zero16;                                          \
-      glds16(src, B_ + (wid * BI + q) * 1024);                                               \
-    }                                                                                        \
+#define WG9_ISSUE(i_)                                                                          \
+  {                                                                                            \
+    const int gkt = kt_begin + (i_);                                                           \
+    const int n_ = gkt / kpi;                                                                  \
+    const int q0 = (gkt - n_ * kpi) * BK;                                                      \
+    unsigned char* A_ = lds + ((i_) % NB) * BUF;                                               \
+    unsigned char* S_ = A_ + A_BYTES;                                                          \
+    _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                           \
+      const int row = (wid * AI + q) * 8 + lrow;                                               \
+      const int chunk = (tr_swz<RB>(row, pch) - row * RB) >> 4;                                \
+      const int qq = q0 + row;                                                                 \
+      const int h_ = fdiv(qq, Wp, invWp), w_ = qq - h_ * Wp;                                   \
+      const bool ok = qq < HWp && w_ < W;                                                      \
+      const void* src = ok ? (const void*)(dy + (((int64_t)n_ * H + h_) * W + w_) * Cout + co0 + chunk * 8) \
+                           : (const void*)g_zero16;                                            \
+      glds16(src, A_ + (wid * AI + q) * 1024);                                                 \
+    }                                                                                          \
+    _Pragma("unroll") for (int q = 0; q < kWgStripI; ++q) {                                    \
+      const int row = (q * 4 + wid) * 8 + lrow;                                                \
+      const int chunk = (tr_swz<RB>(row, pch) - row * RB) >> 4;                                \
+      const int P = q0 + row;                                                                  \
+      const int hp = fdiv(P, Wp, invWp), wp = P - hp * Wp;                                     \
+      const bool ok = hp >= 1 && hp <= H && wp >= 1 && wp <= W;                                \
+      const void* src = ok ? (const void*)(x + (((int64_t)n_ * H + hp - 1) * W + wp - 1) * Cin + ci0 + chunk * 8) \
+                           : (const void*)g_zero16;                                            \
+      glds16(src, S_ + (q * 4 + wid) * 1024);                                                  \
+    }                                                                                          \
   }
 
-  f32x4_t acc[FM][FN];
+  f32x4_t acc[9][FM][FN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // loop-invariant transposed-read offsets: A (2 ks) and the strip (2 ks x 9 taps)
+  unsigned alo[2], ahi[2], slo[2][9], shi[2][9];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int kb = ks * 32 + (lane >> 4) * 8;
+    tr_offsets<RB>(kb, wm * 32, lane, alo[ks], ahi[ks]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      tr_offsets<RB>(kb + (t / 3) * Wp + (t % 3), wn * 32, lane, slo[ks][t], shi[ks][t]);
+  }
 
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
-    if (p < KT) WG_ISSUE(p);
+    if (p < KT) WG9_ISSUE(p);
 
   for (int kt = 0; kt < KT; ++kt) {
     if (kt + NB - 2 < KT) {
@@ -316,94 +359,133 @@ __global__ void __launch_bounds__(kCT, 2)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
-    if (kt + NB - 1 < KT) WG_ISSUE(kt + NB - 1);
+    if (kt + NB - 1 < KT) WG9_ISSUE(kt + NB - 1);
     const unsigned char* A = lds + (kt % NB) * BUF;
-    const unsigned char* B = A + A_BYTES;
+    const unsigned char* S = A + A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int kb = ks * 32 + (lane >> 4) * 8;
-      bf16x8 af[FM], bfr[FN];
+      bf16x8 af[FM];
+      af[0] = tr_pair(A, alo[ks], ahi[ks]);
+      af[1] = tr_pair(A, alo[ks] ^ 32u, ahi[ks] ^ 32u);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = tr_frag<RA>(A, kb, wm * TM + i * 16, lane);
+      for (int t = 0; t < 9; ++t) {
+        bf16x8 bfr[FN];
+        bfr[0] = tr_pair(S, slo[ks][t], shi[ks][t]);
+        bfr[1] = tr_pair(S, slo[ks][t] ^ 32u, shi[ks][t] ^ 32u);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = tr_frag<RBb>(B, kb, wn * TN + j * 16, lane);
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)
+            acc[t][i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+      }
     }
   }
-#undef WG_ISSUE
+#undef WG9_ISSUE
 
-  // partial tile: rows = co (4 per lane group), cols = ci (lane & 15)
-  float* out = part + ((int64_t)blockIdx.y * 9 + tap) * Cout * Cin;
   const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int t = 0; t < 9; ++t) {
+    float* out = part + ((int64_t)blockIdx.y * 9 + t) * Cout * Cin;
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int co = co0 + wm * TM + i * 16 + fg * 4 + e;
-        const int ci = ci0 + wn * TN + j * 16 + fr;
-        out[(int64_t)co * Cin + ci] = acc[i][j][e];
-      }
-}
-
-// dW[co][tap][ci] (KRSC) = sum over splits of part[split][tap][co][ci]
-template <typename TO>
-__global__ void __launch_bounds__(256)
-    wgrad_reduce_k(const float* __restrict__ part, int S, int Cout, int Cin, TO* __restrict__ dw) {
-  const int64_t total = (int64_t)9 * Cout * Cin;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int ci = (int)(e % Cin);
-    const int64_t r = e / Cin;
-    const int co = (int)(r % Cout);
-    const int tap = (int)(r / Cout);
-    float sum = 0.f;
-    for (int s = 0; s < S; ++s) sum += part[(int64_t)s * total + e];
-    dw[((int64_t)co * 9 + tap) * Cin + ci] = from_f32<TO>(sum);
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + wm * 32 + i * 16 + fg * 4 + e;
+          const int ci = ci0 + wn * 32 + j * 16 + fr;
+          out[(int64_t)co * Cin + ci] = acc[t][i][j][e];
+        }
   }
 }
+
+// Split-K partial reduction, two stages so that thousands of threads each keep
+// several independent 16-byte loads in flight: stage 1 sums groups of splits
+// (grid.y = group), stage 2 sums the groups and writes dW (KRSC, bf16 / fp32).
+constexpr int kRedGroup = 16;  // splits per stage-1 group
+
+__global__ void __launch_bounds__(256)
+    wgrad_reduce1_k(const float4* __restrict__ part, int S, int64_t total4,
+                    float4* __restrict__ stage) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total4) return;
+  const int s0 = blockIdx.y * kRedGroup;
+  int s1 = s0 + kRedGroup;
+  if (s1 > S) s1 = S;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  int s = s0;
+  for (; s + 1 < s1; s += 2) {
+    const float4 u = part[(int64_t)s * total4 + e], v = part[(int64_t)(s + 1) * total4 + e];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  }
+  if (s < s1) {
+    const float4 u = part[(int64_t)s * total4 + e];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+  }
+  stage[(int64_t)blockIdx.y * total4 + e] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// dW[co][tap][ci] (KRSC) = sum over groups of stage[group][tap][co][ci]
+template <typename TO>
+__global__ void __launch_bounds__(256)
+    wgrad_reduce2_k(const float* __restrict__ stage, int Gn, int Cout, int Cin, TO* __restrict__ dw) {
+  const int64_t total = (int64_t)9 * Cout * Cin;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int ci = (int)(e % Cin);
+  const int64_t r = e / Cin;
+  const int co = (int)(r % Cout);
+  const int tap = (int)(r / Cout);
+  float sum = 0.f;
+  for (int g = 0; g < Gn; ++g) sum += stage[(int64_t)g * total + e];
+  dw[((int64_t)co * 9 + tap) * Cin + ci] = from_f32<TO>(sum);
+}
+
 }  // namespace
 
 bool conv3x3_nhwc_supported(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
 
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout) {
-  const int M = N * H * W;
-  const int bm = (Cout % 128 == 0 && Cin % 128 == 0) ? 128 : 64;
-  const int tiles = (Cout / bm) * (Cin / bm) * 9;
-  int S = (1536 + tiles - 1) / tiles;
-  const int max_s = M / (64 * 4);  // >= 4 K-tiles per split
+  const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;  // K-tiles per image
+  const int total = N * kpi;
+  const int tiles = (Cout / 64) * (Cin / 64);
+  int S = (512 + tiles - 1) / tiles;                  // ~2 workgroups per CU
+  const int max_s = total / 8;                         // >= 8 K-tiles per workgroup
   if (S > max_s) S = max_s;
   return S < 1 ? 1 : S;
 }
 
+bool conv3x3_wgrad_supported(int W) { return W <= kWgMaxW; }
+
+int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout) {
+  return (int64_t)(S + (S + kRedGroup - 1) / kRedGroup) * 9 * Cout * Cin;
+}
+
 void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
                         int N, int H, int W, int Cin, int Cout, int S, hipStream_t st) {
-  const int M = N * H * W;
-  int pps = (M + S - 1) / S;
-  pps = (pps + 63) / 64 * 64;
-  const auto* dyp = static_cast<const bf16_t*>(dy);
-  const auto* xp = static_cast<const bf16_t*>(x);
-  if (Cout % 128 == 0 && Cin % 128 == 0) {
-    const int tiles = (Cout / 128) * (Cin / 128) * 9;
-    hipLaunchKernelGGL((conv3x3_wgrad_k<128, 128, 2>), dim3(tiles, S), dim3(kCT), 0, st, dyp, xp,
-                       part, H, W, Cin, Cout, M, pps);
-  } else {
-    const int tiles = (Cout / 64) * (Cin / 64) * 9;
-    hipLaunchKernelGGL((conv3x3_wgrad_k<64, 64, 3>), dim3(tiles, S), dim3(kCT), 0, st, dyp, xp,
-                       part, H, W, Cin, Cout, M, pps);
-  }
-  const int64_t total = (int64_t)9 * Cout * Cin;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;
+  const int total = N * kpi;
+  const int kps = (total + S - 1) / S;
+  const int tiles = (Cout / 64) * (Cin / 64);
+  hipLaunchKernelGGL((conv3x3_wgrad9_k<3>), dim3(tiles, S), dim3(kCT), 0, st,
+                     static_cast<const bf16_t*>(dy), static_cast<const bf16_t*>(x), part, H, W,
+                     Cin, Cout, kpi, kps, total);
+  // two-stage reduction; `part` holds S partial slabs followed by ceil(S/16)
+  // stage-1 slabs (conv3x3_wgrad_workspace)
+  const int64_t nout = (int64_t)9 * Cout * Cin;
+  const int Gn = (S + kRedGroup - 1) / kRedGroup;
+  float* stage = part + (int64_t)S * nout;
+  const int64_t n4 = nout / 4;
+  hipLaunchKernelGGL(wgrad_reduce1_k, dim3((unsigned)((n4 + 255) / 256), Gn), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(part), S, n4, reinterpret_cast<float4*>(stage));
+  const unsigned blocks = (unsigned)((nout + 255) / 256);
   if (dw_fp32)
-    hipLaunchKernelGGL((wgrad_reduce_k<float>), dim3(blocks), dim3(256), 0, st, part, S, Cout, Cin,
-                       static_cast<float*>(dw));
+    hipLaunchKernelGGL((wgrad_reduce2_k<float>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
+                       Cin, static_cast<float*>(dw));
   else
-    hipLaunchKernelGGL((wgrad_reduce_k<bf16_t>), dim3(blocks), dim3(256), 0, st, part, S, Cout,
+    hipLaunchKernelGGL((wgrad_reduce2_k<bf16_t>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
                        Cin, static_cast<bf16_t*>(dw));
 }
 

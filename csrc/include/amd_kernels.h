@@ -200,6 +200,8 @@ void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W
 // weight gradient: split-K over pixels into fp32 partials [S][9][Cout][Cin], then a
 // reduce into dW (KRSC, bf16 or fp32)
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout);
+bool conv3x3_wgrad_supported(int W);
+int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout);  // floats
 void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
                         int N, int H, int W, int Cin, int Cout, int S, hipStream_t st);
 

@@ -76,7 +76,9 @@ at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out
   x = x.contiguous(at::MemoryFormat::ChannelsLast);
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   const int S = conv3x3_wgrad_splits((int)N, (int)H, (int)W, (int)Cin, (int)Cout);
-  at::Tensor part = at::empty({(int64_t)S * 9 * Cout * Cin}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(conv3x3_wgrad_supported((int)W), "conv3x3_wgrad: width > 56 unsupported");
+  at::Tensor part = at::empty({conv3x3_wgrad_workspace(S, (int)Cin, (int)Cout)},
+                              x.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({Cout, Cin, 3, 3},
                             x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
   conv3x3_nhwc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(),

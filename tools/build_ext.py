@@ -127,6 +127,14 @@ def build(jobs: int | None = None, verbose: bool = False, clean: bool = False) -
             "-ltorch_hip", "-ltorch_python", "-Wl,-rpath," + tlib,
         ]
         _run(link, verbose)
+        # an unresolved symbol only shows at dlopen: check the fresh .so in a child
+        chk = subprocess.run([sys.executable, "-c", "import torch, importlib.util as u; "
+                              "s = u.spec_from_file_location('_C', %r); "
+                              "u.module_from_spec(s)" % out],
+                             capture_output=True, text=True)
+        if chk.returncode != 0:
+            os.remove(out)
+            raise RuntimeError("built extension does not load:\n" + chk.stderr[-2000:])
     print("built %s (%d objects rebuilt, %.1fs)" % (os.path.relpath(out, ROOT), len(todo),
                                                    time.time() - t0), flush=True)
     return out
