@@ -206,3 +206,36 @@ def ddp_amp_vs_local(rank, world, opt_level="O2", fused=False, iters=3):
         oa.step()
         ob.step()
     return {"diffs": diffs}
+
+
+def gpu_ddp_resnet(rank, world, steps=4):
+    """Two ranks sharing cuda:0 over gloo (RCCL refuses two ranks on one GPU): the
+    GPU-side DDP path of bench.py - amp O2 bf16, fused BN, GEMM convs, FusedSGD,
+    bucket views - must keep replicas identical and match a one-process run on
+    the concatenated batch."""
+    from apex_example_amd import amp
+    from apex_example_amd.models import resnet18
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10, fused_bn=True, gemm_1x1=True).cuda().to(
+        memory_format=torch.channels_last)
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, materialize_master_grads=False)
+    m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
+    ddp = DistributedDataParallel(m, message_size=200_000)
+    g = torch.Generator().manual_seed(5 + rank)
+    x = torch.randn(8, 3, 32, 32, generator=g).cuda().to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), generator=g).cuda()
+    losses = []
+    for _ in range(steps):
+        loss = F.cross_entropy(ddp(x), y)
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        opt.step()
+        losses.append(loss.item())
+    torch.cuda.synchronize()
+    return {"params": [p.detach().float().cpu() for p in m.parameters()], "losses": losses,
+            "views": all(getattr(p, "_amd_grad_is_bucket_view", False) for p in m.parameters())}

@@ -83,3 +83,13 @@ def test_ddp_resnet_amp_step(pg):
         losses.append(loss.item())
     assert all(getattr(p, "_amd_grad_is_bucket_view", False) for p in m.parameters())
     assert losses[-1] < losses[0]
+
+
+def test_two_ranks_one_gpu_gloo(tmp_path):
+    """bench.py's N>1 code path (apex DDP over a process group, bucket views, fused
+    kernels) with two processes on the one test GPU."""
+    res = W.run("gpu_ddp_resnet", 2, str(tmp_path))
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        assert torch.equal(a, b)
+    assert res[0]["views"] and res[1]["views"]
+    assert res[0]["losses"][-1] < res[0]["losses"][0]
