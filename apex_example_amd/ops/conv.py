@@ -17,6 +17,8 @@ per chunk.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -40,7 +42,11 @@ def wgrad_1x1(dy_rows, x_rows, out_dtype):
         return torch.mm(dy_rows.t(), x_rows, out_dtype=torch.float32).to(out_dtype)
     a = dy_rows.view(S, m // S, co).transpose(1, 2)
     b = x_rows.view(S, m // S, ci)
-    return torch.bmm(a, b, out_dtype=torch.float32).sum(0).to(out_dtype)
+    part = torch.bmm(a, b, out_dtype=torch.float32)
+    if _USE_SPLITK_REDUCE and out_dtype in (torch.bfloat16, torch.float32) and (co * ci) % 4 == 0:
+        # one two-stage slab reduction writing the weight dtype directly
+        return _native.require().conv.splitk_reduce(part, out_dtype)
+    return part.sum(0).to(out_dtype)
 
 
 def _as_rows(t):
@@ -141,11 +147,16 @@ class Conv2d1x1(nn.Conv2d):
 
 
 _MFMA_WGRAD_MIN_W = 48
+# A/B switches for the reduction / rotation kernels (tools, docs/PERF.md)
+_USE_SPLITK_REDUCE = os.environ.get("APEX_AMD_SPLITK_REDUCE", "1") == "1"
+_USE_ROT_KERNEL = os.environ.get("APEX_AMD_ROT_KERNEL", "1") == "1"
 
 
 def _rot_weight(weight):
     """W'[ci, co, r, s] = W[co, ci, 2-r, 2-s]: the data gradient of a 3x3 stride-1
-    pad-1 conv is the same conv applied to dY with W'."""
+    pad-1 conv is the same conv applied to dY with W' (one tiled-transpose kernel)."""
+    if _USE_ROT_KERNEL and weight.is_cuda and weight.element_size() == 2:
+        return _native.require().conv.rot_weight(weight)
     return weight.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
 
 

@@ -430,8 +430,9 @@ __global__ void __launch_bounds__(256)
 // dW[co][tap][ci] (KRSC) = sum over groups of stage[group][tap][co][ci]
 template <typename TO>
 __global__ void __launch_bounds__(256)
-    wgrad_reduce2_k(const float* __restrict__ stage, int Gn, int Cout, int Cin, TO* __restrict__ dw) {
-  const int64_t total = (int64_t)9 * Cout * Cin;
+    wgrad_reduce2_k(const float* __restrict__ stage, int Gn, int Cout, int Cin, TO* __restrict__ dw,
+                    int taps) {
+  const int64_t total = (int64_t)taps * Cout * Cin;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int ci = (int)(e % Cin);
@@ -440,7 +441,25 @@ __global__ void __launch_bounds__(256)
   const int tap = (int)(r / Cout);
   float sum = 0.f;
   for (int g = 0; g < Gn; ++g) sum += stage[(int64_t)g * total + e];
-  dw[((int64_t)co * 9 + tap) * Cin + ci] = from_f32<TO>(sum);
+  dw[((int64_t)co * taps + tap) * Cin + ci] = from_f32<TO>(sum);
+}
+
+// W'[ci][8-t][co] = W[co][t][ci]: the 180-degree-rotated, in/out-swapped 3x3
+// filter of the data gradient, as a 64x64 LDS-tiled transpose per tap
+__global__ void __launch_bounds__(256)
+    rot_weight_k(const uint16_t* __restrict__ w, uint16_t* __restrict__ out, int Cout, int Cin) {
+  __shared__ uint16_t tile[64][66];
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64, t = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  for (int r = ty; r < 64; r += 4) {
+    const int co = co0 + r, ci = ci0 + tx;
+    tile[r][tx] = (co < Cout && ci < Cin) ? w[((int64_t)co * 9 + t) * Cin + ci] : 0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < Cin && co < Cout) out[((int64_t)ci * 9 + (8 - t)) * Cout + co] = tile[tx][r];
+  }
 }
 
 }  // namespace
@@ -483,10 +502,35 @@ void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bo
   const unsigned blocks = (unsigned)((nout + 255) / 256);
   if (dw_fp32)
     hipLaunchKernelGGL((wgrad_reduce2_k<float>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<float*>(dw));
+                       Cin, static_cast<float*>(dw), 9);
   else
     hipLaunchKernelGGL((wgrad_reduce2_k<bf16_t>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<bf16_t*>(dw));
+                       Cin, static_cast<bf16_t*>(dw), 9);
+}
+
+int64_t splitk_reduce_workspace(int S, int64_t n) {
+  return (int64_t)((S + kRedGroup - 1) / kRedGroup) * n;
+}
+
+void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, void* out,
+                   bool out_fp32, hipStream_t st) {
+  const int64_t n = (int64_t)Cout * Cin;
+  const int Gn = (S + kRedGroup - 1) / kRedGroup;
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(wgrad_reduce1_k, dim3((unsigned)((n4 + 255) / 256), Gn), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(part), S, n4, reinterpret_cast<float4*>(stage));
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (out_fp32)
+    hipLaunchKernelGGL((wgrad_reduce2_k<float>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
+                       Cin, static_cast<float*>(out), 1);
+  else
+    hipLaunchKernelGGL((wgrad_reduce2_k<bf16_t>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
+                       Cin, static_cast<bf16_t*>(out), 1);
+}
+
+void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st) {
+  hipLaunchKernelGGL(rot_weight_k, dim3((Cout + 63) / 64, (Cin + 63) / 64, 9), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin);
 }
 
 void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin,

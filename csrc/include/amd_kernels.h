@@ -202,6 +202,12 @@ void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout);
 bool conv3x3_wgrad_supported(int W);
 int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout);  // floats
+// generic split-K slab reduction: out[co][ci] = sum_s part[s][co][ci] (n % 4 == 0)
+int64_t splitk_reduce_workspace(int S, int64_t n);
+void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, void* out,
+                   bool out_fp32, hipStream_t st);
+// 16-bit W'[ci][2-r][2-s][co] = W[co][r][s][ci] (data-gradient filter)
+void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
 void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
                         int N, int H, int W, int Cin, int Cout, int S, hipStream_t st);
 

@@ -75,6 +75,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
   conv.def("conv3x3_fwd", &conv3x3_nhwc_fwd_op);
   conv.def("conv3x3_wgrad", &conv3x3_nhwc_wgrad_op);
+  conv.def("splitk_reduce", &splitk_reduce_op);
+  conv.def("rot_weight", &conv3x3_rot_weight_op);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);

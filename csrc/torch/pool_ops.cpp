@@ -87,4 +87,29 @@ at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out
   return dw;
 }
 
+at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&
+                  part.is_contiguous(), "splitk_reduce: contiguous fp32 [S, M, N] expected");
+  const int64_t S = part.size(0), M = part.size(1), N = part.size(2);
+  TORCH_CHECK((M * N) % 4 == 0, "splitk_reduce: M*N must be a multiple of 4");
+  at::Tensor stage = at::empty({splitk_reduce_workspace((int)S, M * N)}, part.options());
+  at::Tensor out = at::empty({M, N}, part.options().dtype(out_dtype));
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "splitk_reduce: out dtype");
+  splitk_reduce(part.data_ptr<float>(), (int)S, (int)M, (int)N, stage.data_ptr<float>(),
+                out.data_ptr(), out_dtype == at::kFloat, cur_stream());
+  return out;
+}
+
+at::Tensor conv3x3_rot_weight_op(at::Tensor w) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                  w.element_size() == 2, "rot_weight: 16-bit [Cout, Cin, 3, 3] expected");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  at::Tensor out = at::empty({Cin, Cout, 3, 3}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  conv3x3_rot_weight(w.data_ptr(), out.data_ptr(), (int)Cout, (int)Cin, cur_stream());
+  return out;
+}
+
 }  // namespace amd

@@ -16,4 +16,7 @@ at::Tensor conv3x3_nhwc_fwd_op(at::Tensor x, at::Tensor w);
 // its weight gradient (split-K MFMA + reduce), returned as [Cout, Cin, 3, 3] channels_last
 at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype);
 
+at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype);
+at::Tensor conv3x3_rot_weight_op(at::Tensor w);
+
 }  // namespace amd

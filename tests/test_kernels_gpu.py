@@ -452,3 +452,18 @@ def test_conv3x3_mfma_igemm(shape):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * gs)
     ws = wr.grad.abs().max().item()
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=2e-2 * ws)
+
+
+def test_rot_weight_and_splitk_reduce():
+    from apex_example_amd import _native
+
+    cv = _native.require().conv
+    w = torch.randn(192, 64, 3, 3, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    ref = w.flip(2, 3).transpose(0, 1)
+    assert torch.equal(cv.rot_weight(w), ref)
+    part = torch.randn(37, 96, 40, device=DEV)
+    torch.testing.assert_close(cv.splitk_reduce(part, torch.float32), part.sum(0), rtol=1e-5,
+                               atol=1e-5)
+    torch.testing.assert_close(cv.splitk_reduce(part, torch.bfloat16).float(), part.sum(0),
+                               rtol=1e-2, atol=5e-2)
