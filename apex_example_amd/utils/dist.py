@@ -42,11 +42,16 @@ def init_distributed(backend=None, rank=None, world_size=None, local=None, timeo
     rank = int(os.environ.get("RANK", "0")) if rank is None else rank
     world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else world_size
     local = local_rank() if local is None else local
+    # test hooks: run every rank on one device / force the collective backend
+    # (rehearsing the multi-process path on a single-GPU box)
+    if os.environ.get("APEX_AMD_SINGLE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("APEX_AMD_DIST_BACKEND", backend)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     # dmabuf IPC is the only mode the MI355X host driver supports
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    use_gpu = torch.cuda.is_available() and os.environ.get("APEX_AMD_FORCE_CPU") != "1"
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
     if use_gpu:
@@ -57,7 +62,7 @@ def init_distributed(backend=None, rank=None, world_size=None, local=None, timeo
     if world_size > 1 and not dist.is_initialized():
         kw = dict(backend=backend, init_method="env://", world_size=world_size, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu and device_id_binding:
+        if use_gpu and device_id_binding and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
     return rank, world_size, device

@@ -284,7 +284,7 @@ def build_gpt2(args, device, world):
 
 def main():
     args = parse()
-    from apex_example_amd.utils.dist import init_distributed
+    from apex_example_amd.utils.dist import barrier, init_distributed
 
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world != args.gpus and env_world > 1:
@@ -343,7 +343,7 @@ def main():
 
     def sync_all():
         if world > 1:
-            dist.barrier(device_ids=[device.index])
+            barrier()
         torch.cuda.synchronize()
 
     sync_all()
@@ -400,7 +400,7 @@ def main():
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     if world > 1:
-        dist.barrier(device_ids=[device.index])
+        barrier()
         dist.destroy_process_group()
 
 
