@@ -211,4 +211,20 @@ void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t
 void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
                         int N, int H, int W, int Cin, int Cout, int S, hipStream_t st);
 
+// ---- fused attention, head dim 64 (attention.hip) ---------------------------
+struct AttnLaunch {
+  const void* q;
+  const void* k;
+  const void* v;
+  int64_t qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh;  // element strides of [B,S,H,64] views
+  void* o;      // [B][S][H][64] contiguous
+  float* lse;   // [B][H][S]
+  int B, H, S;
+  float scale, dropout;
+  uint32_t seed;
+  bool causal;
+  DType dtype;  // BF16 or F16
+};
+void attn_fwd(const AttnLaunch& L, hipStream_t st);
+
 }  // namespace amd

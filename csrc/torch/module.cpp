@@ -7,6 +7,7 @@
 
 #include "amd_kernels.h"
 #include "amp_ops.h"
+#include "attn_ops.h"
 #include "norm_ops.h"
 #include "pool_ops.h"
 #include "reducer.h"
@@ -68,6 +69,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto ln = m.def_submodule("layer_norm", "fused LayerNorm / RMSNorm (wave64 row kernels)");
   ln.def("forward", &layer_norm_forward_op);
   ln.def("backward", &layer_norm_backward_op);
+
+  auto attn = m.def_submodule("attn", "fused attention (head dim 64, MFMA, gfx950)");
+  attn.def("fwd", &attn_fwd_op);
 
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);

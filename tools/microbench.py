@@ -296,6 +296,34 @@ def bench_conv3x3(args):
             werr), flush=True)
 
 
+def bench_attn(args):
+    """SDPA fwd+bwd at the BERT-large / GPT-2-medium shapes: AOTriton vs CK flash."""
+    dev = "cuda"
+    shapes = [("bert-large", 32, 16, 512, 64, False), ("gpt2-medium", 8, 16, 1024, 64, True)]
+    for lib in ("default", "ck"):
+        try:
+            torch.backends.cuda.preferred_rocm_fa_library(lib)
+        except Exception as e:  # noqa: BLE001
+            print("backend %s unavailable: %s" % (lib, e))
+            continue
+        for name, b, h, s_, d, causal in shapes:
+            q, k, v = (torch.randn(b, h, s_, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
+                       for _ in range(3))
+            do = torch.randn(b, h, s_, d, device=dev, dtype=torch.bfloat16)
+            f = lambda: F.scaled_dot_product_attention(q, k, v, is_causal=causal)  # noqa: E731
+            try:
+                tf_ = timeit(f)
+                o = f()
+                tb = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True))
+            except Exception as e:  # noqa: BLE001
+                print("%s %s failed: %s" % (lib, name, str(e)[:200]))
+                continue
+            fl = 4 * b * h * s_ * s_ * d * (0.5 if causal else 1.0)
+            print("%-8s %-12s fwd %.0f us (%.0f TF)  bwd %.0f us (%.0f TF)" % (
+                lib, name, tf_, fl / (tf_ * 1e-6) / 1e12, tb, 2.5 * fl / (tb * 1e-6) / 1e12),
+                flush=True)
+
+
 def bench_optim(args):
     from apex_example_amd.optimizers import FusedAdam, FusedSGD
     from apex_example_amd.models import resnet50
@@ -377,11 +405,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "optim", "ln", "lamb"])
+    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "optim", "ln", "lamb",
+                             "attn"])
     a = ap.parse_args()
     {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
-     "conv3x3": bench_conv3x3}[a.what](a)
+     "conv3x3": bench_conv3x3, "attn": bench_attn}[a.what](a)
 
 
 if __name__ == "__main__":
