@@ -1,6 +1,7 @@
 """BERT (Devlin et al. 2018) for pre-training, defined in-repo (no transformers
-download): post-LN encoder with FusedLayerNorm, fused QKV projection, PyTorch
-SDPA attention (CK / AOTriton flash attention on ROCm), masked-LM head on the
+download): post-LN encoder with FusedLayerNorm, fused QKV projection, the gfx950 fused
+attention kernels (ops/attention.py; PyTorch SDPA when a padding mask is given
+or off-GPU), masked-LM head on the
 gathered masked positions only (NVIDIA's pretraining recipe, max_predictions
 per sequence) with the decoder tied to the word embeddings, and the NSP head.
 
@@ -17,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..normalization import FusedLayerNorm
+from ..ops import attention as fused_attn
 
 
 @dataclass
@@ -33,6 +35,7 @@ class BertConfig:
     initializer_range: float = 0.02
     layer_norm_eps: float = 1e-12
     fused_layer_norm: bool = True
+    fused_attention: bool = True
 
 
 def _ln(cfg, n):
@@ -66,13 +69,18 @@ class BertSelfAttention(nn.Module):
         self.qkv = nn.Linear(cfg.hidden_size, 3 * cfg.hidden_size)
         self.dense = nn.Linear(cfg.hidden_size, cfg.hidden_size)
         self.p = cfg.attention_probs_dropout_prob
+        self.fused = cfg.fused_attention
 
     def forward(self, x, attn_mask=None):
         b, s, hd = x.shape
-        qkv = self.qkv(x).view(b, s, 3, self.h, self.d).permute(2, 0, 3, 1, 4)
+        qkv = self.qkv(x).view(b, s, 3, self.h, self.d)
+        p = self.p if self.training else 0.0
+        if self.fused and attn_mask is None and fused_attn.supported(qkv, self.d):
+            o = fused_attn.fused_attention_qkv(qkv, causal=False, dropout_p=p)
+            return self.dense(o.view(b, s, hd))
+        qkv = qkv.permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
-        o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask,
-                                           dropout_p=self.p if self.training else 0.0)
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=p)
         o = o.transpose(1, 2).reshape(b, s, hd)
         return self.dense(o)
 

@@ -1,5 +1,6 @@
 """GPT-2 (Radford et al. 2019) language model defined in-repo: pre-LN decoder
-blocks with FusedLayerNorm, causal SDPA attention (flash attention on ROCm),
+blocks with FusedLayerNorm, causal attention on the gfx950 fused attention
+kernels (ops/attention.py; PyTorch SDPA off-GPU / fp32),
 tanh-GELU MLP and an LM head tied to the token embedding.
 
 gpt2_medium(): 24 layers, d_model 1024, 16 heads, vocab 50257, 1024 positions
@@ -14,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..normalization import FusedLayerNorm
+from ..ops import attention as fused_attn
 
 
 @dataclass
@@ -29,6 +31,7 @@ class GPT2Config:
     layer_norm_epsilon: float = 1e-5
     initializer_range: float = 0.02
     fused_layer_norm: bool = True
+    fused_attention: bool = True
 
 
 def _ln(cfg, n):
@@ -46,12 +49,17 @@ class GPT2Attention(nn.Module):
         self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
         self.p = cfg.attn_pdrop
         self.resid_dropout = nn.Dropout(cfg.resid_pdrop)
+        self.fused = cfg.fused_attention
 
     def forward(self, x):
         b, s, e = x.shape
-        qkv = self.c_attn(x).view(b, s, 3, self.h, self.d).permute(2, 0, 3, 1, 4)
-        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], is_causal=True,
-                                           dropout_p=self.p if self.training else 0.0)
+        qkv = self.c_attn(x).view(b, s, 3, self.h, self.d)
+        p = self.p if self.training else 0.0
+        if self.fused and fused_attn.supported(qkv, self.d):
+            o = fused_attn.fused_attention_qkv(qkv, causal=True, dropout_p=p).view(b, s, e)
+            return self.resid_dropout(self.c_proj(o))
+        qkv = qkv.permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], is_causal=True, dropout_p=p)
         o = o.transpose(1, 2).reshape(b, s, e)
         return self.resid_dropout(self.c_proj(o))
 

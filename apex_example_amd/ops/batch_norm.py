@@ -5,10 +5,12 @@
 Forward (training): split-reduction per-channel stats -> [one packed all_gather
 of (mean, var, count) across the process group] -> combine + running-stat
 update -> y = relu(x*scale + shift + z) in one elementwise pass.
-Backward: one reduction pass (sum dy', sum dy'*(x-mean), dgamma, dbeta; the
-ReLU mask is recomputed from x, nothing extra is saved) -> [one packed
-all_reduce of the two sums] -> one elementwise pass producing dx (and dz for
-the residual branch).
+Backward: one reduction pass (sum dy', sum dy'*(x-mean), dgamma, dbeta) ->
+[one packed all_reduce of the two sums] -> one elementwise pass producing dx
+(and dz for the residual branch).  The ReLU condition is recomputed from x when
+there is no residual; with a residual z (relu(bn(x) + z), every bottleneck's
+last BN) the forward writes a 1-bit-per-element ReLU mask instead, so backward
+reads 1/16 of z's bytes (twice) and z is not kept alive.
 
 Works for any memory format: NCHW-contiguous runs the NCHW kernels,
 channels_last-contiguous 4-D tensors run the NHWC kernels; ``shape_channel_last``
@@ -47,13 +49,16 @@ class BatchNormFunction(torch.autograd.Function):
             world = 1  # local statistics
         else:
             world = dist.get_world_size(process_group)
+        want_mask = bool(fuse_relu) and zl is not None and xl.is_cuda
         if world == 1 and xl.is_cuda:
             # one stats launch + one finalize (mean, invstd, running stats and
             # num_batches_tracked in the same kernel) + one apply launch
-            y, mean_g, invstd = C.forward_local(xl, weight, bias, running_mean, running_var,
-                                                num_batches_tracked, float(eps), float(momentum),
-                                                zl, bool(fuse_relu))
-            ctx.save_for_backward(xl, zl, weight, bias, mean_g, invstd)
+            y, mean_g, invstd, mask = C.forward_local(xl, weight, bias, running_mean,
+                                                      running_var, num_batches_tracked,
+                                                      float(eps), float(momentum), zl,
+                                                      bool(fuse_relu), want_mask)
+            ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd,
+                                  mask)
             ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = None, 1, bool(fuse_relu), \
                 None, count
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
@@ -79,8 +84,11 @@ class BatchNormFunction(torch.autograd.Function):
             total = None
         mean_g, invstd, _ = C.combine_stats(means, vars_, counts, float(eps), float(momentum),
                                             running_mean, running_var)
-        y = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu))
-        ctx.save_for_backward(xl, zl, weight, bias, mean_g, invstd)
+        if want_mask:
+            y, mask = C.apply_mask(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu))
+        else:
+            y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
+        ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd, mask)
         ctx.pg = pg
         ctx.world = world
         ctx.fuse_relu = bool(fuse_relu)
@@ -94,11 +102,11 @@ class BatchNormFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _C()
-        xl, zl, weight, bias, mean, invstd = ctx.saved_tensors
+        xl, zl, weight, bias, mean, invstd, mask = ctx.saved_tensors
         dyl = _to_logical(dy, ctx.shape_channel_last)
         need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
-                                                   ctx.fuse_relu, need_w)
+                                                   ctx.fuse_relu, need_w, mask=mask)
         if ctx.world > 1:
             packed = torch.cat([sum_dy, sum_dy_xmu])
             dist.all_reduce(packed, group=ctx.pg)
@@ -110,7 +118,7 @@ class BatchNormFunction(torch.autograd.Function):
         else:
             total = float(ctx.count)
         dx, dz = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu, total,
-                                  zl, ctx.fuse_relu, ctx.has_z)
+                                  zl, ctx.fuse_relu, ctx.has_z, mask=mask)
         if ctx.shape_channel_last:
             dx = dx.view(ctx.orig_shape)
             if dz is not None:

@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default=None)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true")
+    ap.add_argument("--no-fused-attn", action="store_true",
+                    help="transformers: PyTorch SDPA instead of the gfx950 attention kernels")
     ap.add_argument("--syncbn", action="store_true", help="SyncBatchNorm across ranks")
     ap.add_argument("--message-size", type=int, default=10_000_000, help="DDP bucket elements")
     ap.add_argument("--materialize-master-grads", action="store_true")
@@ -175,7 +177,8 @@ def build_bert(args, device, world):
     seq = args.seq_len or 512
     max_pred = 80 if seq >= 512 else 20
     opt_level = args.opt_level or "O2"
-    cfg = BertConfig(fused_layer_norm=(args.impl == "amd"))
+    cfg = BertConfig(fused_layer_norm=(args.impl == "amd"),
+                     fused_attention=(args.impl == "amd" and not args.no_fused_attn))
     model = BertForPreTraining(cfg).to(device)
     batch = synthetic_batch(cfg, bs, seq, max_pred, device, seed=17 + (
         dist.get_rank() if world > 1 else 0))
@@ -220,7 +223,8 @@ def build_bert(args, device, world):
     w.config = {"model": "bert_large", "global_batch": bs * world, "per_gpu_batch": bs,
                 "seq_len": seq, "max_predictions": max_pred, "parallelism": "dp%d" % world,
                 "impl": args.impl, "opt_level": opt_level, "optimizer": optname,
-                "fused_layer_norm": args.impl == "amd"}
+                "fused_layer_norm": args.impl == "amd",
+                "fused_attention": cfg.fused_attention}
     return w
 
 
@@ -234,7 +238,8 @@ def build_gpt2(args, device, world):
     bs = args.batch_size or 8
     seq = args.seq_len or 1024
     opt_level = args.opt_level or "O1"
-    cfg = GPT2Config(fused_layer_norm=(args.impl == "amd"))
+    cfg = GPT2Config(fused_layer_norm=(args.impl == "amd"),
+                     fused_attention=(args.impl == "amd" and not args.no_fused_attn))
     model = GPT2LMHeadModel(cfg).to(device)
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(0, cfg.vocab_size, (bs, seq), generator=g).to(device)
@@ -278,7 +283,8 @@ def build_gpt2(args, device, world):
                 "opt_level": opt_level,
                 "optimizer": "FusedAdam(wd=0.01)" if args.impl == "amd"
                              else "torch.optim.AdamW(fused)",
-                "fused_layer_norm": args.impl == "amd"}
+                "fused_layer_norm": args.impl == "amd",
+                "fused_attention": cfg.fused_attention}
     return w
 
 

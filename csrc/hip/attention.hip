@@ -3,9 +3,11 @@
 // v_mfma_f32_32x32x16_{bf16,f16}, written for CDNA4 rather than ported.
 //
 // Layouts: q, k, v are [B, S, H, 64] views with arbitrary batch / sequence /
-// head strides (e.g. slices of a fused qkv projection - no copies); o and the
-// gradients are written as contiguous [B, S, H, 64] (so `.view(B, S, H*64)`
-// is free); lse is [B, H, S] fp32 in log2 units.
+// head strides (e.g. slices of a fused qkv projection - no copies); o is written
+// as contiguous [B, S, H, 64] (so `.view(B, S, H*64)` is free); the gradients
+// go to caller-provided strided [B, S, H, 64] views (e.g. slices of one packed
+// dqkv buffer); lse is [B, H, Sp] fp32 in log2 units with the row stride Sp a
+// multiple of 64 (so the backward can DMA 64-query tiles of it).
 //
 // Forward (one wave = 32 queries, workgroup = 4 waves = 128 queries):
 //   * "swapped" QK^T: S^T = K . Q^T so a lane owns one query's scores (column
@@ -23,7 +25,7 @@
 // keys, loops over queries, "unswapped" S = Q.K^T so dV = P^T.dO and
 // dK = dS^T.Q sum over the register rows) and a dQ kernel (workgroup owns 128
 // queries, swapped orientation so dQ = dS.K sums over register rows) - no
-// atomics, no LDS transposes of score tiles.
+// atomics (bitwise reproducible), no LDS transposes of score tiles.
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -123,14 +125,30 @@ __device__ __forceinline__ typename Frag<T>::v8 acc_frag(const f32x16_t& x, int 
   return __builtin_bit_cast(typename Frag<T>::v8, *reinterpret_cast<uint4*>(w));
 }
 
+// a 32(d) x 32(col) transposed accumulator pair (d = 32dt + row) as the 64 values
+// of one [.., 64] 16-bit output row, times `mul`
+template <typename T>
+__device__ __forceinline__ void store_dT(T* row_ptr, const f32x16_t (&acc)[2], int hl, float mul) {
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * dt + 8 * g + 4 * hl;
+      uint2 w;
+      w.x = pack2<T>(acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul);
+      w.y = pack2<T>(acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul);
+      *reinterpret_cast<uint2*>(row_ptr + d) = w;
+    }
+}
+
 struct AttnArgs {
   const void* q;
   const void* k;
   const void* v;
   int64_t qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh;  // element strides
   void* o;           // [B][S][H][64]
-  float* lse;        // [B][H][S]
-  int B, H, S;
+  float* lse;        // [B][H][lse_stride]
+  int B, H, S, lse_stride;
   float scale_log2;  // softmax scale * log2(e)
   uint32_t thr16;    // dropout threshold (p * 65536), 0 = no dropout
   float inv_keep;    // 1 / (1 - p)
@@ -157,7 +175,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
     const int qq = q < a.S ? q : a.S - 1;
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      qf[s] = *reinterpret_cast<const v8*>(Q + qq * a.qss + 16 * s + 8 * hl);
+      qf[s] = *reinterpret_cast<const v8*>(Q + (int64_t)qq * a.qss + 16 * s + 8 * hl);
   }
 
   int nkt = (a.S + kAKT - 1) / kAKT;
@@ -177,8 +195,8 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
       const int kk = key < a.S ? key : a.S - 1;
       const int chk = (swz_rows(row, pch) - row * kARow) >> 4;  // logical chunk at pch
       const int chv = (swz_tr(row, pch) - row * kARow) >> 4;
-      glds16(K + kk * a.kss + chk * 8, Kl + (wid * 2 + i) * 1024);
-      glds16(V + kk * a.vss + chv * 8, Vl + (wid * 2 + i) * 1024);
+      glds16(K + (int64_t)kk * a.kss + chk * 8, Kl + (wid * 2 + i) * 1024);
+      glds16(V + (int64_t)kk * a.vss + chv * 8, Vl + (wid * 2 + i) * 1024);
     }
   };
 
@@ -281,22 +299,350 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   const float lt = l + __shfl_xor(l, 32);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (q < a.S) {
-    T* O = static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * hl;
-        uint2 w;
-        w.x = pack2<T>(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
-        w.y = pack2<T>(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(O + d) = w;
-      }
-    if (hl == 0) a.lse[(int64_t)bh * a.S + q] = m + log2f(lt);
+    store_dT<T>(static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD, o, hl, inv);
+    if (hl == 0) a.lse[(int64_t)bh * a.lse_stride + q] = m + log2f(lt);
   }
 }
 
+// ---------------------------------------------------------------------------- backward
+struct AttnBwdArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  const void* o;
+  const void* dout;
+  int64_t qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, oss, osh, dsb, dss, dsh;
+  void* dq;
+  void* dk;
+  void* dv;
+  int64_t dqsb, dqss, dqsh, dksb, dkss, dksh, dvsb, dvss, dvsh;
+  const float* lse;  // [B][H][lse_stride] log2 units
+  float* D;          // [B][H][lse_stride] rowsum(dO * O)
+  int B, H, S, lse_stride;
+  float scale, scale_log2;
+  uint32_t thr16;
+  float inv_keep;
+  uint32_t seed;
+};
+
+// D[b,h,q] = sum_d dO * O: 8 lanes per (b, q, h) row, one 16-byte load each
+template <typename T>
+__global__ void __launch_bounds__(256) attn_bwd_pre_k(AttnBwdArgs a) {
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
+  const int part = threadIdx.x & 7;
+  const int64_t rows = (int64_t)a.B * a.S * a.H;
+  float acc = 0.f;
+  int b = 0, q = 0, hh = 0;
+  if (row < rows) {
+    hh = (int)(row % a.H);
+    const int64_t bq = row / a.H;
+    q = (int)(bq % a.S);
+    b = (int)(bq / a.S);
+    float ov[8], dv[8];
+    load8(static_cast<const T*>(a.o) + b * a.osb + (int64_t)q * a.oss + hh * a.osh + part * 8, ov);
+    load8(static_cast<const T*>(a.dout) + b * a.dsb + (int64_t)q * a.dss + hh * a.dsh + part * 8,
+          dv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += ov[i] * dv[i];
+  }
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (row < rows && part == 0) a.D[((int64_t)b * a.H + hh) * a.lse_stride + q] = acc;
+}
+
+// dK / dV: a workgroup owns 128 keys (32 per wave, one per lane column), loops
+// over 64-query tiles.  Scores are computed unswapped, S[q][key] = Q . K^T with
+// the wave's K^T / V^T fragments held in registers, so the 16 accumulator
+// registers are 16 queries and dV^T = dO^T . P, dK^T = Q^T . dS consume P / dS
+// straight from the accumulators (the MFMA sums over their register rows).  Q
+// and dO tiles sit in LDS twice: a row image (A operand of S and dP) and a
+// transposed-read image (A operand of dV^T / dK^T); the tile's lse / D values
+// ride the same DMA ring (no plain global loads inside the loop, which would
+// make the compiler's vmcnt waits drain the prefetch).
+template <typename T, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
+  typedef typename Frag<T>::v8 v8;
+  constexpr int IMG = kAKT * kARow;     // 8 KiB
+  constexpr int BUF = 4 * IMG + 1024;   // Q rows, Q tr, dO rows, dO tr, {lse, D}
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hl = lane >> 5, c32 = lane & 31;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+  const int kb0 = blockIdx.x * 128;
+  const int kw0 = kb0 + wid * 32;
+  const int key = kw0 + c32;
+  const int kk = key < a.S ? key : a.S - 1;
+  const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
+  const T* dO = static_cast<const T*>(a.dout) + b * a.dsb + hh * a.dsh;
+  const float* lse = a.lse + (int64_t)bh * a.lse_stride;
+  const float* Dr = a.D + (int64_t)bh * a.lse_stride;
+
+  // K^T / V^T fragments (B operands): key = this lane's column, d = 16s + 8hl + j
+  v8 kf[4], vf[4];
+  {
+    const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh + (int64_t)kk * a.kss;
+    const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh + (int64_t)kk * a.vss;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = *reinterpret_cast<const v8*>(K + 16 * s + 8 * hl);
+      vf[s] = *reinterpret_cast<const v8*>(V + 16 * s + 8 * hl);
+    }
+  }
+
+  const int nqt = (a.S + kAKT - 1) / kAKT;
+  const int qt0 = CAUSAL ? kb0 / kAKT : 0;
+  const int lrow = lane >> 3, pch = lane & 7;
+  auto issue = [&](int qt, int buf) {
+    unsigned char* base = lds + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wid * 2 + i) * 8 + lrow;
+      const int qr = qt * kAKT + row;
+      const int qc = qr < a.S ? qr : a.S - 1;
+      const int chr = (swz_rows(row, pch) - row * kARow) >> 4;
+      const int cht = (swz_tr(row, pch) - row * kARow) >> 4;
+      const T* qrow = Q + (int64_t)qc * a.qss;
+      const T* drow = dO + (int64_t)qc * a.dss;
+      unsigned char* dst = base + (wid * 2 + i) * 1024;
+      glds16(qrow + chr * 8, dst);
+      glds16(qrow + cht * 8, dst + IMG);
+      glds16(drow + chr * 8, dst + 2 * IMG);
+      glds16(drow + cht * 8, dst + 3 * IMG);
+    }
+    if (wid == 0) {  // lanes 0-15: lse[q0 .. q0+63], 16-31: D[...], 32-63: pad (lse again)
+      const int seg = (lane >> 4) & 1, part = lane & 15;
+      const float* src = (seg ? Dr : lse) + qt * kAKT + part * 4;
+      glds16(src, base + 4 * IMG);
+    }
+  };
+
+  f32x16_t dv[2], dk[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dv[0][i] = dv[1][i] = dk[0][i] = dk[1][i] = 0.f;
+
+  int roff[2][4];  // [query half][d step]: row 32h + c32, chunk 2s + hl
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) roff[h][s] = swz_rows(32 * h + c32, 2 * s + hl);
+  int tlo[2][2][2], thi[2][2][2];  // [d tile][query half][k step]
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = 32 * h + 16 * s + 4 * hl;
+        const int c0 = 32 * dt + ((lane >> 4) & 1) * 16;
+        tlo[dt][h][s] = tr_addr(r0, c0, lane);
+        thi[dt][h][s] = tr_addr(r0 + 8, c0, lane);
+      }
+
+  if (qt0 < nqt) issue(qt0, 0);
+  for (int qt = qt0; qt < nqt; ++qt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (qt + 1 < nqt) issue(qt + 1, (qt + 1 - qt0) & 1);
+    const unsigned char* base = lds + ((qt - qt0) & 1) * BUF;
+    const unsigned char* Qr = base;
+    const unsigned char* Qt = base + IMG;
+    const unsigned char* Or = base + 2 * IMG;
+    const unsigned char* Ot = base + 3 * IMG;
+    const float* st_lse = reinterpret_cast<const float*>(base + 4 * IMG);
+    const float* st_D = st_lse + 64;
+    const int q0 = qt * kAKT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qh0 = q0 + 32 * h;
+      if (CAUSAL && qh0 + 31 < kw0) continue;  // every query of this half precedes every key
+      f32x16_t sc, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[i] = dp[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc = mfma32<T>(lds_row8<T>(Qr, roff[h][s]), kf[s], sc);
+        dp = mfma32<T>(lds_row8<T>(Or, roff[h][s]), vf[s], dp);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int li = 32 * h + 8 * g + 4 * hl;  // local query of register 4g
+        const float4 lv = *reinterpret_cast<const float4*>(st_lse + li);
+        const float4 dd = *reinterpret_cast<const float4*>(st_D + li);
+        const float lsev[4] = {lv.x, lv.y, lv.z, lv.w};
+        const float Dv[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const int q = q0 + li + e;
+          const bool live = q < a.S && !(CAUSAL && key > q);
+          float z = 1.f;
+          if (DROP) {
+            const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
+            z = drop_keep(hsh, key, a.thr16) ? a.inv_keep : 0.f;
+          }
+          const float p = live ? exp2f(sc[r] * a.scale_log2 - lsev[e]) : 0.f;
+          const float ds = live ? p * (dp[r] * z - Dv[e]) : 0.f;
+          sc[r] = p * z;
+          dp[r] = ds;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const v8 pf = acc_frag<T>(sc, s);
+        const v8 sf = acc_frag<T>(dp, s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = mfma32<T>(lds_tr8<T>(Ot, tlo[dt][h][s], thi[dt][h][s]), pf, dv[dt]);
+          dk[dt] = mfma32<T>(lds_tr8<T>(Qt, tlo[dt][h][s], thi[dt][h][s]), sf, dk[dt]);
+        }
+      }
+    }
+  }
+
+  if (key < a.S) {
+    store_dT<T>(static_cast<T*>(a.dv) + b * a.dvsb + (int64_t)key * a.dvss + hh * a.dvsh, dv, hl,
+                1.f);
+    store_dT<T>(static_cast<T*>(a.dk) + b * a.dksb + (int64_t)key * a.dkss + hh * a.dksh, dk, hl,
+                a.scale);
+  }
+}
+
+// dQ: a workgroup owns 128 queries (one per lane column), loops over 64-key
+// tiles in the forward's swapped orientation S^T[key][q] = K . Q^T, so a lane's
+// lse / D are scalars and dQ^T = K^T . dS^T consumes dS^T from the accumulator.
+// K sits in LDS as a row image (A of S^T) and a transposed image (A of dQ^T);
+// V as a row image (A of dP^T = V . dO^T).
+template <typename T, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
+  typedef typename Frag<T>::v8 v8;
+  constexpr int IMG = kAKT * kARow;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 3 * IMG];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hl = lane >> 5, c32 = lane & 31;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+  const int qb0 = blockIdx.x * 128;
+  const int q = qb0 + wid * 32 + c32;
+  const int qq = q < a.S ? q : a.S - 1;
+  const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
+  const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
+
+  v8 qf[4], of[4];
+  {
+    const T* Qp = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh + (int64_t)qq * a.qss;
+    const T* Op = static_cast<const T*>(a.dout) + b * a.dsb + hh * a.dsh + (int64_t)qq * a.dss;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const v8*>(Qp + 16 * s + 8 * hl);
+      of[s] = *reinterpret_cast<const v8*>(Op + 16 * s + 8 * hl);
+    }
+  }
+  const float lse_q = a.lse[(int64_t)bh * a.lse_stride + qq];
+  const float D_q = a.D[(int64_t)bh * a.lse_stride + qq];
+
+  int nkt = (a.S + kAKT - 1) / kAKT;
+  if (CAUSAL) {
+    const int last = (qb0 + 127 < a.S ? qb0 + 127 : a.S - 1) / kAKT + 1;
+    nkt = last < nkt ? last : nkt;
+  }
+  const int lrow = lane >> 3, pch = lane & 7;
+  // images per buffer: 0 = K rows, 1 = K transposed, 2 = V rows
+  auto issue = [&](int kt, int buf) {
+    unsigned char* base = lds + buf * 3 * IMG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wid * 2 + i) * 8 + lrow;
+      const int kr = kt * kAKT + row;
+      const int kc = kr < a.S ? kr : a.S - 1;
+      const int chr = (swz_rows(row, pch) - row * kARow) >> 4;
+      const int cht = (swz_tr(row, pch) - row * kARow) >> 4;
+      const T* krow = K + (int64_t)kc * a.kss;
+      unsigned char* dst = base + (wid * 2 + i) * 1024;
+      glds16(krow + chr * 8, dst);
+      glds16(krow + cht * 8, dst + IMG);
+      glds16(V + (int64_t)kc * a.vss + chr * 8, dst + 2 * IMG);
+    }
+  };
+
+  f32x16_t dq[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dq[0][i] = dq[1][i] = 0.f;
+  int koff[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) koff[t][s] = swz_rows(32 * t + c32, 2 * s + hl);
+  int tlo[2][2][2], thi[2][2][2];  // [d tile][key half][k step]
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = 32 * t + 16 * s + 4 * hl;
+        const int c0 = 32 * dt + ((lane >> 4) & 1) * 16;
+        tlo[dt][t][s] = tr_addr(r0, c0, lane);
+        thi[dt][t][s] = tr_addr(r0 + 8, c0, lane);
+      }
+
+  issue(0, 0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nkt) issue(kt + 1, (kt + 1) & 1);
+    const unsigned char* base = lds + (kt & 1) * 3 * IMG;
+    const unsigned char* Kr = base;
+    const unsigned char* Kt = base + IMG;
+    const unsigned char* Vr = base + 2 * IMG;
+    const int k0 = kt * kAKT;
+    if (CAUSAL && k0 > qb0 + wid * 32 + 31) continue;
+    f32x16_t sc[2], dp[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[t][i] = dp[t][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc[t] = mfma32<T>(lds_row8<T>(Kr, koff[t][s]), qf[s], sc[t]);
+        dp[t] = mfma32<T>(lds_row8<T>(Vr, koff[t][s]), of[s], dp[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;  // even
+        const bool live0 = key < a.S && !(CAUSAL && key > q);
+        const bool live1 = key + 1 < a.S && !(CAUSAL && key + 1 > q);
+        float z0 = 1.f, z1 = 1.f;
+        if (DROP) {
+          const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
+          z0 = drop_keep(hsh, key, a.thr16) ? a.inv_keep : 0.f;
+          z1 = drop_keep(hsh, key + 1, a.thr16) ? a.inv_keep : 0.f;
+        }
+        const float p0 = exp2f(sc[t][r] * a.scale_log2 - lse_q);
+        const float p1 = exp2f(sc[t][r + 1] * a.scale_log2 - lse_q);
+        sc[t][r] = live0 ? p0 * (dp[t][r] * z0 - D_q) : 0.f;
+        sc[t][r + 1] = live1 ? p1 * (dp[t][r + 1] * z1 - D_q) : 0.f;
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const v8 sf = acc_frag<T>(sc[t], s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          dq[dt] = mfma32<T>(lds_tr8<T>(Kt, tlo[dt][t][s], thi[dt][t][s]), sf, dq[dt]);
+      }
+  }
+  if (q < a.S)
+    store_dT<T>(static_cast<T*>(a.dq) + b * a.dqsb + (int64_t)q * a.dqss + hh * a.dqsh, dq, hl,
+                a.scale);
+}
+
 }  // namespace
+
+int attn_lse_stride(int S) { return (S + kAKT - 1) / kAKT * kAKT; }
 
 void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   AttnArgs a;
@@ -305,6 +651,7 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   a.ksb = L.ksb; a.kss = L.kss; a.ksh = L.ksh;
   a.vsb = L.vsb; a.vss = L.vss; a.vsh = L.vsh;
   a.o = L.o; a.lse = L.lse; a.B = L.B; a.H = L.H; a.S = L.S;
+  a.lse_stride = L.lse_stride;
   a.scale_log2 = L.scale * 1.4426950408889634f;
   a.thr16 = L.dropout > 0.f ? (uint32_t)(L.dropout * 65536.f + 0.5f) : 0u;
   a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
@@ -325,6 +672,56 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
     ATTN_FWD_LAUNCH(half_t)
   }
 #undef ATTN_FWD_LAUNCH
+}
+
+void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
+  AttnBwdArgs a;
+  a.q = L.q; a.k = L.k; a.v = L.v; a.o = L.o; a.dout = L.dout;
+  a.qsb = L.qsb; a.qss = L.qss; a.qsh = L.qsh;
+  a.ksb = L.ksb; a.kss = L.kss; a.ksh = L.ksh;
+  a.vsb = L.vsb; a.vss = L.vss; a.vsh = L.vsh;
+  a.osb = L.osb; a.oss = L.oss; a.osh = L.osh;
+  a.dsb = L.dsb; a.dss = L.dss; a.dsh = L.dsh;
+  a.dq = L.dq; a.dk = L.dk; a.dv = L.dv;
+  a.dqsb = L.dqsb; a.dqss = L.dqss; a.dqsh = L.dqsh;
+  a.dksb = L.dksb; a.dkss = L.dkss; a.dksh = L.dksh;
+  a.dvsb = L.dvsb; a.dvss = L.dvss; a.dvsh = L.dvsh;
+  a.lse = L.lse; a.D = L.D; a.lse_stride = L.lse_stride;
+  a.B = L.B; a.H = L.H; a.S = L.S;
+  a.scale = L.scale;
+  a.scale_log2 = L.scale * 1.4426950408889634f;
+  a.thr16 = L.dropout > 0.f ? (uint32_t)(L.dropout * 65536.f + 0.5f) : 0u;
+  a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
+  a.seed = L.seed;
+  const int64_t rows = (int64_t)L.B * L.S * L.H;
+  const unsigned pre_blocks = (unsigned)((rows * 8 + 255) / 256);
+  dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
+  const bool drop = a.thr16 != 0;
+#define ATTN_BWD_LAUNCH(T)                                                                     \
+  hipLaunchKernelGGL((attn_bwd_pre_k<T>), dim3(pre_blocks), dim3(256), 0, st, a);               \
+  if (L.causal) {                                                                              \
+    if (drop) {                                                                                \
+      hipLaunchKernelGGL((attn_bwd_dkdv_k<T, true, true>), grid, block, 0, st, a);             \
+      hipLaunchKernelGGL((attn_bwd_dq_k<T, true, true>), grid, block, 0, st, a);               \
+    } else {                                                                                   \
+      hipLaunchKernelGGL((attn_bwd_dkdv_k<T, true, false>), grid, block, 0, st, a);            \
+      hipLaunchKernelGGL((attn_bwd_dq_k<T, true, false>), grid, block, 0, st, a);              \
+    }                                                                                          \
+  } else {                                                                                     \
+    if (drop) {                                                                                \
+      hipLaunchKernelGGL((attn_bwd_dkdv_k<T, false, true>), grid, block, 0, st, a);            \
+      hipLaunchKernelGGL((attn_bwd_dq_k<T, false, true>), grid, block, 0, st, a);              \
+    } else {                                                                                   \
+      hipLaunchKernelGGL((attn_bwd_dkdv_k<T, false, false>), grid, block, 0, st, a);           \
+      hipLaunchKernelGGL((attn_bwd_dq_k<T, false, false>), grid, block, 0, st, a);             \
+    }                                                                                          \
+  }
+  if (L.dtype == DType::BF16) {
+    ATTN_BWD_LAUNCH(bf16_t)
+  } else {
+    ATTN_BWD_LAUNCH(half_t)
+  }
+#undef ATTN_BWD_LAUNCH
 }
 
 }  // namespace amd

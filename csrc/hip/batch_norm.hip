@@ -322,12 +322,12 @@ void bn_combine_stats(const float* means, const float* vars, const float* counts
 }
 
 void bn_apply(const void* x, DType tx, const float* mean, const float* invstd,
-              const void* weight, const void* bias, DType tw, const void* z, void* y,
-              int64_t outer, int64_t C, int64_t inner, int channel_last, int relu,
+              const void* weight, const void* bias, DType tw, const void* z, uint8_t* relu_mask,
+              void* y, int64_t outer, int64_t C, int64_t inner, int channel_last, int relu,
               hipStream_t st) {
   if (outer * inner * C == 0) return;
   if (channel_last)
-    return nhwc_apply(x, tx, mean, invstd, weight, bias, tw, z, y, outer, C, relu, st);
+    return nhwc_apply(x, tx, mean, invstd, weight, bias, tw, z, relu_mask, y, outer, C, relu, st);
   const bool vec = nchw_vec(inner, {x, z, y});
   bn_dispatch(tx, [&](auto t0) {
     bn_dispatch(tw, [&](auto w0) {
@@ -344,13 +344,13 @@ void bn_apply(const void* x, DType tx, const float* mean, const float* invstd,
 
 void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                     const float* invstd, const void* weight, const void* bias, DType tw,
-                    int relu, const void* z, int64_t outer, int64_t C, int64_t inner,
-                    int channel_last, float* sum_dy, float* sum_dy_xmu, void* grad_weight,
-                    void* grad_bias, float* ws, hipStream_t st) {
+                    int relu, const void* z, const uint8_t* relu_mask, int64_t outer, int64_t C,
+                    int64_t inner, int channel_last, float* sum_dy, float* sum_dy_xmu,
+                    void* grad_weight, void* grad_bias, float* ws, hipStream_t st) {
   if (outer * inner * C == 0) return;
   if (channel_last)
-    return nhwc_reduce(dy, x, tx, mean, invstd, weight, bias, tw, relu, z, outer, C, sum_dy,
-                       sum_dy_xmu, grad_weight, grad_bias, ws, st);
+    return nhwc_reduce(dy, x, tx, mean, invstd, weight, bias, tw, relu, z, relu_mask, outer, C,
+                       sum_dy, sum_dy_xmu, grad_weight, grad_bias, ws, st);
   const int splits = nchw_splits(outer, C, inner);
   const int vec = nchw_vec(inner, {dy, x, z}) ? 1 : 0;
   bn_dispatch(tx, [&](auto t0) {
@@ -370,12 +370,13 @@ void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
 void bn_backward_elemt(const void* dy, const void* x, DType tx, const float* mean,
                        const float* invstd, const void* weight, const void* bias, DType tw,
                        const float* sum_dy, const float* sum_dy_xmu, float inv_count,
-                       int relu, const void* z, void* dx, void* dz, int64_t outer, int64_t C,
-                       int64_t inner, int channel_last, hipStream_t st) {
+                       int relu, const void* z, const uint8_t* relu_mask, void* dx, void* dz,
+                       int64_t outer, int64_t C, int64_t inner, int channel_last,
+                       hipStream_t st) {
   if (outer * inner * C == 0) return;
   if (channel_last)
     return nhwc_backward(dy, x, tx, mean, invstd, weight, bias, tw, sum_dy, sum_dy_xmu,
-                         inv_count, relu, z, dx, dz, outer, C, st);
+                         inv_count, relu, z, relu_mask, dx, dz, outer, C, st);
   const bool vec = nchw_vec(inner, {dy, x, z, dx, dz});
   bn_dispatch(tx, [&](auto t0) {
     bn_dispatch(tw, [&](auto w0) {

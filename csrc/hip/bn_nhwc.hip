@@ -9,6 +9,13 @@
 // streams rows.  Every loop keeps 2-4 independent rows (16-B loads) in flight
 // per lane.  Reductions write per-split partial slabs summed by the shared
 // finalize kernel (bn_common.h): deterministic, no atomics.
+//
+// ReLU bitmask: when the forward applies ReLU after a residual add (y =
+// relu(bn(x) + z)) it can also write one bit per element (which outputs were
+// > 0; one byte per lane's 8 channels per row, 1/16 of a bf16 tensor).  The
+// backward passes then read the mask instead of re-reading z to recompute the
+// ReLU condition: two full reads of the residual tensor per layer become two
+// reads of 1/16 of it, and z need not be kept alive for backward.
 #include "bn_common.h"
 
 namespace amd {
@@ -153,10 +160,11 @@ template <typename T, typename TW, bool VEC>
 __global__ void __launch_bounds__(kBNThreads)
     apply_k(const T* __restrict__ x, const float* __restrict__ mean,
             const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
-            const T* __restrict__ z, T* __restrict__ y, int64_t M, int C, int ctile, int rows_iter,
-            int relu) {
+            const T* __restrict__ z, T* __restrict__ y, uint8_t* __restrict__ rmask, int64_t M,
+            int C, int ctile, int rows_iter, int relu) {
   constexpr int W = VEC ? 8 : 1;
   constexpr int U = 2;
+  const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
   if (ri >= rows_iter || c0 >= C) return;
@@ -179,13 +187,18 @@ __global__ void __launch_bounds__(kBNThreads)
     for (int u = 0; u < U; ++u) {
       const int64_t rr = r + (int64_t)u * stride;
       if (rr >= M) continue;
+      uint32_t mb = 0;
 #pragma unroll
       for (int i = 0; i < W; ++i) {
         float o = fmaf(v[u][i], sc[i], sh[i]);
         if (z) o += zz[u][i];
+        mb |= (o > 0.f ? 1u : 0u) << i;
         v[u][i] = relu ? fmaxf(o, 0.f) : o;
       }
       stw<T, W>(y + rr * C + c0, v[u]);
+      if constexpr (W == 8) {
+        if (rmask) rmask[rr * Cb + (c0 >> 3)] = (uint8_t)mb;
+      }
     }
   }
 }
@@ -195,10 +208,11 @@ template <typename T, typename TW, bool VEC>
 __global__ void __launch_bounds__(kBNThreads)
     reduce_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
              const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
-             const T* __restrict__ z, int relu, int64_t M, int C, int ctile, int rows_iter,
-             float* __restrict__ slab) {
+             const T* __restrict__ z, const uint8_t* __restrict__ rmask, int relu, int64_t M,
+             int C, int ctile, int rows_iter, float* __restrict__ slab) {
   constexpr int W = VEC ? 8 : 1;
   constexpr int U = 2;
+  const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
   const bool active = ri < rows_iter && c0 < C;
@@ -217,15 +231,18 @@ __global__ void __launch_bounds__(kBNThreads)
     }
     for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
       float xv[U][W], dv[U][W], zv[U][W];
+      uint32_t mk[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t rr = r + (int64_t)u * rows_iter;
+        mk[u] = 0;
 #pragma unroll
         for (int i = 0; i < W; ++i) xv[u][i] = dv[u][i] = zv[u][i] = 0.f;  // dy = 0: no-op
         if (rr < r1) {
           ldw<T, W>(x + rr * C + c0, xv[u]);
           ldw<T, W>(dy + rr * C + c0, dv[u]);
-          if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
+          if (relu && rmask) mk[u] = rmask[rr * Cb + (c0 >> 3)];
+          else if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
         }
       }
 #pragma unroll
@@ -233,7 +250,9 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
         for (int i = 0; i < W; ++i) {
           float d = dv[u][i];
-          if (relu) {
+          if (relu && rmask) {
+            d = ((mk[u] >> ((c0 + i) & 7)) & 1u) ? d : 0.f;
+          } else if (relu) {
             float o = fmaf(xv[u][i], sc[i], sh[i]);
             if (z) o += zv[u][i];
             d = o > 0.f ? d : 0.f;
@@ -255,10 +274,11 @@ __global__ void __launch_bounds__(kBNThreads)
                const float* __restrict__ invstd, const TW* __restrict__ w,
                const TW* __restrict__ b, const float* __restrict__ sum_dy,
                const float* __restrict__ sum_dy_xmu, float inv_n, int relu,
-               const T* __restrict__ z, T* __restrict__ dx, T* __restrict__ dz, int64_t M, int C,
-               int ctile, int rows_iter) {
+               const T* __restrict__ z, const uint8_t* __restrict__ rmask, T* __restrict__ dx,
+               T* __restrict__ dz, int64_t M, int C, int ctile, int rows_iter) {
   constexpr int W = VEC ? 8 : 1;
   constexpr int U = 2;
+  const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
   if (ri >= rows_iter || c0 >= C) return;
@@ -277,13 +297,16 @@ __global__ void __launch_bounds__(kBNThreads)
   const int64_t stride = (int64_t)gridDim.x * rows_iter;
   for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
     float xv[U][W], dv[U][W], zv[U][W];
+    uint32_t mk[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t rr = r + (int64_t)u * stride;
+      mk[u] = 0;
       if (rr < M) {
         ldw<T, W>(x + rr * C + c0, xv[u]);
         ldw<T, W>(dy + rr * C + c0, dv[u]);
-        if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
+        if (relu && rmask) mk[u] = rmask[rr * Cb + (c0 >> 3)];
+        else if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
       }
     }
 #pragma unroll
@@ -293,7 +316,9 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
       for (int i = 0; i < W; ++i) {
         float d = dv[u][i];
-        if (relu) {
+        if (relu && rmask) {
+          d = ((mk[u] >> ((c0 + i) & 7)) & 1u) ? d : 0.f;
+        } else if (relu) {
           float o = fmaf(xv[u][i], sc[i], sh[i]);
           if (z) o += zv[u][i];
           d = o > 0.f ? d : 0.f;
@@ -351,8 +376,8 @@ void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut&
 }
 
 void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
-                const void* b, DType tw, const void* z, void* y, int64_t M, int64_t C, int relu,
-                hipStream_t st) {
+                const void* b, DType tw, const void* z, uint8_t* rmask, void* y, int64_t M,
+                int64_t C, int relu, hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({x, z, y});
   const NGeom g = ngeom(C, vec);
   const int blocks = elem_blocks(M, g);
@@ -364,17 +389,17 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
         hipLaunchKernelGGL((apply_k<T, TW, decltype(V)::value>), dim3(blocks, g.cblocks),
                            dim3(kBNThreads), 0, st, static_cast<const T*>(x), mean, invstd,
                            static_cast<const TW*>(w), static_cast<const TW*>(b),
-                           static_cast<const T*>(z), static_cast<T*>(y), M, (int)C, g.ctile,
-                           g.rows_iter, relu);
+                           static_cast<const T*>(z), static_cast<T*>(y), vec ? rmask : nullptr,
+                           M, (int)C, g.ctile, g.rows_iter, relu);
       });
     });
   });
 }
 
 void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, const float* invstd,
-                 const void* w, const void* b, DType tw, int relu, const void* z, int64_t M,
-                 int64_t C, float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, float* ws,
-                 hipStream_t st) {
+                 const void* w, const void* b, DType tw, int relu, const void* z,
+                 const uint8_t* rmask, int64_t M, int64_t C, float* sum_dy, float* sum_dy_xmu,
+                 void* gw, void* gb, float* ws, hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({dy, x, z});
   const NGeom g = ngeom(C, vec);
   const int splits = reduce_splits(M, g);
@@ -386,8 +411,8 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
         hipLaunchKernelGGL((reduce_k<T, TW, decltype(V)::value>), dim3(splits, g.cblocks),
                            dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
                            static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
-                           static_cast<const TW*>(b), static_cast<const T*>(z), relu, M, (int)C,
-                           g.ctile, g.rows_iter, ws);
+                           static_cast<const TW*>(b), static_cast<const T*>(z), rmask, relu, M,
+                           (int)C, g.ctile, g.rows_iter, ws);
       });
       launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
                          static_cast<TW*>(gb), st);
@@ -398,7 +423,8 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
 void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
                    const float* invstd, const void* w, const void* b, DType tw,
                    const float* sum_dy, const float* sum_dy_xmu, float inv_count, int relu,
-                   const void* z, void* dx, void* dz, int64_t M, int64_t C, hipStream_t st) {
+                   const void* z, const uint8_t* rmask, void* dx, void* dz, int64_t M, int64_t C,
+                   hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({dy, x, z, dx, dz});
   const NGeom g = ngeom(C, vec);
   const int blocks = elem_blocks(M, g);
@@ -411,8 +437,8 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
                            dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
                            static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
                            static_cast<const TW*>(b), sum_dy, sum_dy_xmu, inv_count, relu,
-                           static_cast<const T*>(z), static_cast<T*>(dx), static_cast<T*>(dz), M,
-                           (int)C, g.ctile, g.rows_iter);
+                           static_cast<const T*>(z), rmask, static_cast<T*>(dx),
+                           static_cast<T*>(dz), M, (int)C, g.ctile, g.rows_iter);
       });
     });
   });

@@ -168,24 +168,27 @@ void bn_combine_stats(const float* means, const float* vars, const float* counts
                       int64_t C, float eps, float momentum, float* mean_out, float* invstd_out,
                       float* running_mean, DType trm, void* running_var_any, float* var_out,
                       hipStream_t st);
-// y = (x - mean) * invstd * w + b  [+ z] [relu]
+// y = (x - mean) * invstd * w + b  [+ z] [relu]; relu_mask (channel-last, C % 8 == 0,
+// 16-B aligned x/z/y; else ignored) receives one bit per element: output > 0
 void bn_apply(const void* x, DType tx, const float* mean, const float* invstd,
-              const void* weight, const void* bias, DType tw, const void* z, void* y,
-              int64_t outer, int64_t C, int64_t inner, int channel_last, int relu,
+              const void* weight, const void* bias, DType tw, const void* z, uint8_t* relu_mask,
+              void* y, int64_t outer, int64_t C, int64_t inner, int channel_last, int relu,
               hipStream_t st);
 // per-channel sum_dy, sum_dy_xmu (fp32) and grad_weight/grad_bias (TW) ; when relu
-// is fused, dy is masked by (y > 0) where y is recomputed from x.
+// is fused, dy is masked by (y > 0), read from relu_mask (channel-last only) or
+// recomputed from x (and z).
 void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                     const float* invstd, const void* weight, const void* bias, DType tw,
-                    int relu, const void* z, int64_t outer, int64_t C, int64_t inner,
+                    int relu, const void* z, const uint8_t* relu_mask, int64_t outer, int64_t C,
+                    int64_t inner,
                     int channel_last, float* sum_dy, float* sum_dy_xmu, void* grad_weight,
                     void* grad_bias, float* ws, hipStream_t st);
 // dx = (dy' - mean_dy - (x-mean)*invstd^2*mean_dy_xmu) * invstd * w ; dz = dy' if z
 void bn_backward_elemt(const void* dy, const void* x, DType tx, const float* mean,
                        const float* invstd, const void* weight, const void* bias, DType tw,
                        const float* sum_dy, const float* sum_dy_xmu, float inv_count,
-                       int relu, const void* z, void* dx, void* dz, int64_t outer, int64_t C,
-                       int64_t inner, int channel_last, hipStream_t st);
+                       int relu, const void* z, const uint8_t* relu_mask, void* dx, void* dz,
+                       int64_t outer, int64_t C, int64_t inner, int channel_last, hipStream_t st);
 
 // ---- NHWC max pooling (pool.hip) -------------------------------------------
 void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, int H, int W, int C,
@@ -222,9 +225,34 @@ struct AttnLaunch {
   int B, H, S;
   float scale, dropout;
   uint32_t seed;
+  int lse_stride;  // row stride of lse, a multiple of 64 (attn_lse_stride(S))
   bool causal;
   DType dtype;  // BF16 or F16
 };
+int attn_lse_stride(int S);
 void attn_fwd(const AttnLaunch& L, hipStream_t st);
+
+// backward: preprocess D = rowsum(dO*O), dK/dV kernel, dQ kernel (no atomics)
+struct AttnBwdLaunch {
+  const void* q;
+  const void* k;
+  const void* v;
+  const void* o;
+  const void* dout;
+  int64_t qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, oss, osh, dsb, dss, dsh;
+  void* dq;     // strided [B,S,H,64] outputs
+  void* dk;
+  void* dv;
+  int64_t dqsb, dqss, dqsh, dksb, dkss, dksh, dvsb, dvss, dvsh;
+  const float* lse;  // [B][H][lse_stride]
+  float* D;          // workspace [B][H][lse_stride]
+  int lse_stride;
+  int B, H, S;
+  float scale, dropout;
+  uint32_t seed;
+  bool causal;
+  DType dtype;
+};
+void attn_bwd(const AttnBwdLaunch& L, hipStream_t st);
 
 }  // namespace amd

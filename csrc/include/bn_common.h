@@ -188,16 +188,19 @@ BNTuning& bn_tuning();
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec);
 void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
                 hipStream_t st);
+// rmask: optional ReLU bitmask [M][C/8] (apply writes it when the VEC path runs,
+// reduce / backward read it instead of recomputing the ReLU condition from z)
 void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
-                const void* b, DType tw, const void* z, void* y, int64_t M, int64_t C, int relu,
-                hipStream_t st);
+                const void* b, DType tw, const void* z, uint8_t* rmask, void* y, int64_t M,
+                int64_t C, int relu, hipStream_t st);
 void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, const float* invstd,
-                 const void* w, const void* b, DType tw, int relu, const void* z, int64_t M,
-                 int64_t C, float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, float* ws,
-                 hipStream_t st);
+                 const void* w, const void* b, DType tw, int relu, const void* z,
+                 const uint8_t* rmask, int64_t M, int64_t C, float* sum_dy, float* sum_dy_xmu,
+                 void* gw, void* gb, float* ws, hipStream_t st);
 void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
                    const float* invstd, const void* w, const void* b, DType tw,
                    const float* sum_dy, const float* sum_dy_xmu, float inv_count, int relu,
-                   const void* z, void* dx, void* dz, int64_t M, int64_t C, hipStream_t st);
+                   const void* z, const uint8_t* rmask, void* dx, void* dz, int64_t M, int64_t C,
+                   hipStream_t st);
 
 }  // namespace amd

@@ -72,6 +72,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   auto attn = m.def_submodule("attn", "fused attention (head dim 64, MFMA, gfx950)");
   attn.def("fwd", &attn_fwd_op);
+  attn.def("bwd", &attn_bwd_op);
 
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
@@ -86,7 +87,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bn.def("local_stats", &bn_local_stats_op);
   bn.def("combine_stats", &bn_combine_stats_op);
   bn.def("apply", &bn_apply_op);
-  bn.def("forward_local", &bn_forward_local_op);
+  bn.def("forward_local", &bn_forward_local_op, py::arg("x"), py::arg("weight"),
+         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("nbt"),
+         py::arg("eps"), py::arg("momentum"), py::arg("z"), py::arg("relu"),
+         py::arg("want_mask") = false);
+  bn.def("apply_mask", &bn_apply_mask_op);
   bn.def("set_tuning", &bn_set_tuning, py::arg("red_rpt") = -1, py::arg("red_cap") = -1,
          py::arg("red_min") = -1, py::arg("elem_rpt") = -1, py::arg("elem_cap") = -1,
          py::arg("elem_min") = -1);
@@ -95,8 +100,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     bn_get_tuning(o);
     return std::vector<int>(o, o + 6);
   });
-  bn.def("reduce_grad", &bn_reduce_grad_op);
-  bn.def("backward_elemt", &bn_backward_elemt_op);
+  bn.def("reduce_grad", &bn_reduce_grad_op, py::arg("dy"), py::arg("x"), py::arg("mean"),
+         py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("z"), py::arg("relu"),
+         py::arg("need_wgrad"), py::arg("mask") = py::none());
+  bn.def("backward_elemt", &bn_backward_elemt_op, py::arg("dy"), py::arg("x"), py::arg("mean"),
+         py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("sum_dy"),
+         py::arg("sum_dy_xmu"), py::arg("count"), py::arg("z"), py::arg("relu"),
+         py::arg("want_dz"), py::arg("mask") = py::none());
 
   auto rd = m.def_submodule("reducer", "DDP bucketed gradient reducer core");
   register_reducer(rd);

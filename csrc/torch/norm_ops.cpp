@@ -117,6 +117,23 @@ at::Tensor conform(const at::Tensor& t, const BNView& v) {
   return v.cl4 ? t.contiguous(at::MemoryFormat::ChannelsLast) : t.contiguous();
 }
 
+bool aligned16(const at::Tensor& t) { return !t.defined() || ((uintptr_t)t.data_ptr() % 16) == 0; }
+
+// mirrors the NHWC launchers' VEC condition, under which apply writes the mask
+bool relu_mask_ok(const BNView& v, bool relu, const at::Tensor& x, const at::Tensor& z,
+                  const at::Tensor& y) {
+  return relu && x.is_cuda() && v.cl == 1 && v.C % 8 == 0 && aligned16(x) && aligned16(z) &&
+         aligned16(y);
+}
+
+const uint8_t* mask_ptr(const OptT& m, const at::Tensor& x, const BNView& v) {
+  if (!has(m)) return nullptr;
+  TORCH_CHECK(x.is_cuda() && v.cl == 1 && m->scalar_type() == at::kByte && m->is_contiguous() &&
+                  m->numel() == v.outer * (v.C / 8),
+              "batch norm: bad ReLU mask");
+  return m->data_ptr<uint8_t>();
+}
+
 std::vector<int64_t> reduce_dims(const at::Tensor& x) {
   std::vector<int64_t> d{0};
   for (int64_t i = 2; i < x.dim(); ++i) d.push_back(i);
@@ -189,9 +206,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
   return {mean, invstd, var};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
     at::Tensor x, OptT weight, OptT bias, OptT running_mean, OptT running_var, OptT nbt,
-    double eps, double momentum, OptT z, bool relu) {
+    double eps, double momentum, OptT z, bool relu, bool want_mask) {
   c10::NoGradGuard no_grad_;
   const bool rs = has(running_mean) && has(running_var);
   auto f32c = [](const OptT& t) {
@@ -207,8 +224,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
     auto cs = bn_combine_stats_op(std::get<0>(st), std::get<1>(st), counts, eps, momentum,
                                   running_mean, running_var);
     if (has(nbt)) nbt->add_(1);
-    at::Tensor y = bn_apply_op(x, std::get<0>(cs), std::get<1>(cs), weight, bias, z, relu);
-    return {y, std::get<0>(cs), std::get<1>(cs)};
+    auto ym = want_mask ? bn_apply_mask_op(x, std::get<0>(cs), std::get<1>(cs), weight, bias, z,
+                                           relu)
+                        : std::make_tuple(bn_apply_op(x, std::get<0>(cs), std::get<1>(cs), weight,
+                                                      bias, z, relu),
+                                          at::Tensor());
+    return {std::get<0>(ym), std::get<0>(cs), std::get<1>(cs), std::get<1>(ym)};
   }
   BNView v = bn_view(x);
   x = conform(x, v);
@@ -221,12 +242,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
                        rs ? running_var->data_ptr<float>() : nullptr,
                        has(nbt) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr,
                        (float)eps, (float)momentum, ws.data_ptr<float>(), cur_stream());
+  if (want_mask) {
+    auto ym = bn_apply_mask_op(x, mean, invstd, weight, bias, z, relu);
+    return {std::get<0>(ym), mean, invstd, std::get<1>(ym)};
+  }
   at::Tensor y = bn_apply_op(x, mean, invstd, weight, bias, z, relu);
-  return {y, mean, invstd};
+  return {y, mean, invstd, at::Tensor()};
 }
 
-at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-                       OptT z, bool relu) {
+static std::tuple<at::Tensor, at::Tensor> bn_apply_impl(at::Tensor x, at::Tensor mean,
+                                                        at::Tensor invstd, OptT weight, OptT bias,
+                                                        OptT z, bool relu, bool want_mask) {
   BNView v = bn_view(x);
   if (!x.is_cuda()) {
     const int64_t d = x.dim();
@@ -235,25 +261,41 @@ at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT we
     at::Tensor y = x.to(at::kFloat) * chan(sc, d) + chan(sh, d);
     if (has(z)) y = y + z->to(at::kFloat);
     if (relu) y = y.clamp_min(0);
-    return y.to(x.scalar_type());
+    return {y.to(x.scalar_type()), at::Tensor()};
   }
   x = conform(x, v);
   at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
   at::Tensor y = at::empty_like(x);
+  at::Tensor mask;
+  if (want_mask && relu_mask_ok(v, relu, x, zc, y))
+    mask = at::empty({v.outer, v.C / 8}, x.options().dtype(at::kByte));
   DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
   at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
   at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
   bn_apply(x.data_ptr(), dtype_of(x), mean.data_ptr<float>(), invstd.data_ptr<float>(),
            w.defined() ? w.data_ptr() : nullptr, b.defined() ? b.data_ptr() : nullptr, tw,
-           zc.defined() ? zc.data_ptr() : nullptr, y.data_ptr(), v.outer, v.C, v.inner, v.cl,
-           relu ? 1 : 0, cur_stream());
-  return y;
+           zc.defined() ? zc.data_ptr() : nullptr,
+           mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, y.data_ptr(), v.outer, v.C,
+           v.inner, v.cl, relu ? 1 : 0, cur_stream());
+  return {y, mask};
+}
+
+at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+                       OptT z, bool relu) {
+  return std::get<0>(bn_apply_impl(x, mean, invstd, weight, bias, z, relu, false));
+}
+
+std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mean,
+                                                    at::Tensor invstd, OptT weight, OptT bias,
+                                                    OptT z, bool relu) {
+  return bn_apply_impl(x, mean, invstd, weight, bias, z, relu, true);
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-    OptT z, bool relu, bool need_wgrad) {
+    OptT z, bool relu, bool need_wgrad, OptT mask) {
   BNView v = bn_view(x);
+  TORCH_CHECK(!has(mask) || x.is_cuda(), "batch norm: ReLU mask is a GPU-path feature");
   if (!x.is_cuda()) {
     const int64_t d = x.dim();
     at::Tensor xf = x.to(at::kFloat), df = dy.to(at::kFloat);
@@ -273,7 +315,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
   }
   x = conform(x, v);
   dy = conform(dy, v);
-  at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
+  const uint8_t* mk = mask_ptr(mask, x, v);
+  at::Tensor zc = (has(z) && !mk) ? conform(*z, v) : at::Tensor();
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor sum_dy = at::empty({v.C}, fopt), sum_dy_xmu = at::empty({v.C}, fopt);
   at::Tensor gw, gb;
@@ -288,7 +331,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
   bn_reduce_grad(dy.data_ptr(), x.data_ptr(), dtype_of(x), mean.data_ptr<float>(),
                  invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
                  b.defined() ? b.data_ptr() : nullptr, tw, relu ? 1 : 0,
-                 zc.defined() ? zc.data_ptr() : nullptr, v.outer, v.C, v.inner, v.cl,
+                 zc.defined() ? zc.data_ptr() : nullptr, mk, v.outer, v.C, v.inner, v.cl,
                  sum_dy.data_ptr<float>(), sum_dy_xmu.data_ptr<float>(),
                  gw.defined() ? gw.data_ptr() : nullptr, gb.defined() ? gb.data_ptr() : nullptr,
                  ws.data_ptr<float>(), cur_stream());
@@ -299,8 +342,10 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
                                                         at::Tensor mean, at::Tensor invstd,
                                                         OptT weight, OptT bias, at::Tensor sum_dy,
                                                         at::Tensor sum_dy_xmu, double count,
-                                                        OptT z, bool relu, bool want_dz) {
+                                                        OptT z, bool relu, bool want_dz,
+                                                        OptT mask) {
   BNView v = bn_view(x);
+  TORCH_CHECK(!has(mask) || x.is_cuda(), "batch norm: ReLU mask is a GPU-path feature");
   if (!x.is_cuda()) {
     const int64_t d = x.dim();
     at::Tensor xf = x.to(at::kFloat), df = dy.to(at::kFloat);
@@ -317,7 +362,8 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
   }
   x = conform(x, v);
   dy = conform(dy, v);
-  at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
+  const uint8_t* mk = mask_ptr(mask, x, v);
+  at::Tensor zc = (has(z) && !mk) ? conform(*z, v) : at::Tensor();
   at::Tensor dx = at::empty_like(x);
   at::Tensor dz = want_dz ? at::empty_like(x) : at::Tensor();
   DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
@@ -327,7 +373,7 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
                     invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
                     b.defined() ? b.data_ptr() : nullptr, tw, sum_dy.data_ptr<float>(),
                     sum_dy_xmu.data_ptr<float>(), (float)(1.0 / count), relu ? 1 : 0,
-                    zc.defined() ? zc.data_ptr() : nullptr, dx.data_ptr(),
+                    zc.defined() ? zc.data_ptr() : nullptr, mk, dx.data_ptr(),
                     dz.defined() ? dz.data_ptr() : nullptr, v.outer, v.C, v.inner, v.cl,
                     cur_stream());
   return {dx, dz};

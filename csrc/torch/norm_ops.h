@@ -26,18 +26,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
                                                                    OptT running_var);
 // Local (per-GPU statistics) training forward: stats + running-stat update +
 // num_batches_tracked += 1 + normalize(+z)(+ReLU).  Returns (y, mean, invstd).
-std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
+// want_mask: also return the ReLU bitmask [M, C/8] uint8 (channels-last GPU input
+// with C % 8 == 0 and relu; otherwise the 4th result is undefined / None).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
     at::Tensor x, OptT weight, OptT bias, OptT running_mean, OptT running_var, OptT nbt,
-    double eps, double momentum, OptT z, bool relu);
+    double eps, double momentum, OptT z, bool relu, bool want_mask);
 at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
                        OptT z, bool relu);
+std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mean,
+                                                    at::Tensor invstd, OptT weight, OptT bias,
+                                                    OptT z, bool relu);
+// mask: the forward's ReLU bitmask; when given, z is not read.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-    OptT z, bool relu, bool need_wgrad);
+    OptT z, bool relu, bool need_wgrad, OptT mask);
 std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tensor x,
                                                         at::Tensor mean, at::Tensor invstd,
                                                         OptT weight, OptT bias, at::Tensor sum_dy,
                                                         at::Tensor sum_dy_xmu, double count,
-                                                        OptT z, bool relu, bool want_dz);
+                                                        OptT z, bool relu, bool want_dz,
+                                                        OptT mask);
 
 }  // namespace amd

@@ -300,6 +300,20 @@ def bench_attn(args):
     """SDPA fwd+bwd at the BERT-large / GPT-2-medium shapes: AOTriton vs CK flash."""
     dev = "cuda"
     shapes = [("bert-large", 32, 16, 512, 64, False), ("gpt2-medium", 8, 16, 1024, 64, True)]
+    from apex_example_amd.ops import fused_attention
+
+    for name, b, h, s_, d, causal in shapes:  # this framework's gfx950 kernels, [B,S,H,D]
+        q, k, v = (torch.randn(b, s_, h, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
+                   for _ in range(3))
+        do = torch.randn(b, s_, h, d, device=dev, dtype=torch.bfloat16)
+        f = lambda: fused_attention(q, k, v, causal=causal)  # noqa: E731
+        tf_ = timeit(f)
+        o = f()
+        tb = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True))
+        fl = 4 * b * h * s_ * s_ * d * (0.5 if causal else 1.0)
+        print("%-8s %-12s fwd %.0f us (%.0f TF)  bwd %.0f us (%.0f TF)" % (
+            "gfx950", name, tf_, fl / (tf_ * 1e-6) / 1e12, tb, 2.5 * fl / (tb * 1e-6) / 1e12),
+            flush=True)
     for lib in ("default", "ck"):
         try:
             torch.backends.cuda.preferred_rocm_fa_library(lib)
