@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import _native
 from ..normalization import FusedLayerNorm
 from ..ops import attention as fused_attn
 
@@ -154,8 +155,17 @@ class BertForPreTraining(nn.Module):
         return logits, self.nsp(pooled)
 
 
-def pretraining_loss(mlm_logits, nsp_logits, mlm_labels, nsp_labels):
-    mlm = F.cross_entropy(mlm_logits.float(), mlm_labels.reshape(-1), ignore_index=-1)
+def pretraining_loss(mlm_logits, nsp_logits, mlm_labels, nsp_labels, fused=True):
+    """Masked-LM (labels -1 = not predicted) + NSP cross entropy.  ``fused``: the
+    MLM term runs the gfx950 softmax-cross-entropy kernel on the 16-bit logits."""
+    labels = mlm_labels.reshape(-1)
+    if fused and mlm_logits.is_cuda and _native.available():
+        from ..contrib.xentropy import SoftmaxCrossEntropyLoss
+
+        losses = SoftmaxCrossEntropyLoss.apply(mlm_logits, labels, 0.0, -1, True)
+        mlm = losses.sum() / (labels != -1).sum().clamp_min(1)
+    else:
+        mlm = F.cross_entropy(mlm_logits.float(), labels, ignore_index=-1)
     nsp = F.cross_entropy(nsp_logits.float(), nsp_labels)
     return mlm + nsp
 

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import _native
 from ..normalization import FusedLayerNorm
 from ..ops import attention as fused_attn
 
@@ -121,8 +122,18 @@ class GPT2LMHeadModel(nn.Module):
         return F.linear(x, self.wte.weight)  # tied LM head
 
 
-def lm_loss(logits, input_ids):
-    """Next-token cross entropy (fp32 softmax)."""
+def lm_loss(logits, input_ids, fused=True):
+    """Next-token cross entropy with an fp32 softmax.  ``fused``: the gfx950
+    softmax-cross-entropy kernel (contrib.xentropy) reads the 16-bit logits
+    directly (the last position's label is padding) instead of materialising a
+    sliced fp32 copy of the [B*S, vocab] logits."""
+    if fused and logits.is_cuda and _native.available():
+        from ..contrib.xentropy import SoftmaxCrossEntropyLoss
+
+        b, s, v = logits.shape
+        labels = torch.cat([input_ids[:, 1:], input_ids.new_full((b, 1), -1)], 1).reshape(-1)
+        losses = SoftmaxCrossEntropyLoss.apply(logits.reshape(b * s, v), labels, 0.0, -1, True)
+        return losses.sum() / (b * (s - 1))
     return F.cross_entropy(logits[:, :-1].reshape(-1, logits.size(-1)).float(),
                            input_ids[:, 1:].reshape(-1))
 

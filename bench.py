@@ -208,7 +208,7 @@ def build_bert(args, device, world):
         def step(b):
             with torch.autocast("cuda", dtype=half):
                 mlm, nsp = model(b[0], b[1], b[2])
-                loss = pretraining_loss(mlm, nsp, b[3], b[4])
+                loss = pretraining_loss(mlm, nsp, b[3], b[4], fused=False)
             opt.zero_grad(set_to_none=True)
             loss.backward()
             opt.step()
@@ -266,7 +266,7 @@ def build_gpt2(args, device, world):
 
         def step(b):
             with torch.autocast("cuda", dtype=half):
-                loss = lm_loss(model(b[0]), b[0])
+                loss = lm_loss(model(b[0]), b[0], fused=False)
             opt.zero_grad(set_to_none=True)
             scaler.scale(loss).backward()
             scaler.step(opt)

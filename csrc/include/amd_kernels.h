@@ -255,4 +255,14 @@ struct AttnBwdLaunch {
 };
 void attn_bwd(const AttnBwdLaunch& L, hipStream_t st);
 
+// ---- fused softmax cross entropy with label smoothing (xentropy.hip) ---------
+// x [rows, V] row-major (T = fp32/fp16/bf16); loss [rows] (TO), lse [rows] fp32
+void xentropy_fwd(const void* x, DType tx, const int64_t* labels, int64_t rows, int V,
+                  float smoothing, int64_t padding_idx, void* loss, DType tloss, float* lse,
+                  hipStream_t st);
+// dx [rows, V] (x's dtype) = dloss * (softmax - (1-eps) onehot - eps/V)
+void xentropy_bwd(const void* dloss, DType tg, const void* x, DType tx, const float* lse,
+                  const int64_t* labels, int64_t rows, int V, float smoothing,
+                  int64_t padding_idx, void* dx, hipStream_t st);
+
 }  // namespace amd

@@ -10,6 +10,7 @@
 #include "attn_ops.h"
 #include "norm_ops.h"
 #include "pool_ops.h"
+#include "xent_ops.h"
 #include "reducer.h"
 
 namespace py = pybind11;
@@ -73,6 +74,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto attn = m.def_submodule("attn", "fused attention (head dim 64, MFMA, gfx950)");
   attn.def("fwd", &attn_fwd_op);
   attn.def("bwd", &attn_bwd_op);
+
+  auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
+  xe.def("forward", &xentropy_fwd_op);
+  xe.def("backward", &xentropy_bwd_op);
 
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);

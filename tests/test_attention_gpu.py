@@ -170,3 +170,23 @@ def test_bert_layer_fused_attention_matches_sdpa():
     yr.backward(dy)
     _close(xa.grad, xr.grad.float(), 3e-2)
     _close(a.attention.qkv.weight.grad, r.attention.qkv.weight.grad.float(), 3e-2)
+
+
+def test_contrib_self_mha_fast_matches_default():
+    from apex_example_amd.contrib.multihead_attn import SelfMultiheadAttn
+
+    torch.manual_seed(0)
+    fast = SelfMultiheadAttn(1024, 16, bias=True, include_norm_add=True).to(DEV).to(
+        torch.bfloat16)
+    ref = SelfMultiheadAttn(1024, 16, bias=True, include_norm_add=True, impl="default").to(
+        DEV).to(torch.bfloat16)
+    ref.load_state_dict(fast.state_dict())
+    x = torch.randn(128, 4, 1024, device=DEV, dtype=torch.bfloat16)
+    xa, xr = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, _ = fast(xa, xa, xa, is_training=False)
+    yr, _ = ref(xr, xr, xr, is_training=False)
+    _close(ya, yr.float(), 2e-2)
+    dy = torch.randn_like(ya)
+    ya.backward(dy)
+    yr.backward(dy)
+    _close(xa.grad, xr.grad.float(), 3e-2)

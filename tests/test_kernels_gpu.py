@@ -467,3 +467,45 @@ def test_rot_weight_and_splitk_reduce():
                                atol=1e-5)
     torch.testing.assert_close(cv.splitk_reduce(part, torch.bfloat16).float(), part.sum(0),
                                rtol=1e-2, atol=5e-2)
+
+
+# ------------------------------------------------------------------ contrib xentropy
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("V", [30522, 50257, 7, 1000])
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_xentropy_kernel(dt, V, smoothing):
+    from apex_example_amd.contrib.xentropy import SoftmaxCrossEntropyLoss
+
+    torch.manual_seed(0)
+    N = 67
+    x = (torch.randn(N, V, device=DEV) * 3).to(dt).requires_grad_(True)
+    y = torch.randint(0, V, (N,), device=DEV)
+    y[3] = -1
+    loss = SoftmaxCrossEntropyLoss.apply(x, y, smoothing, -1, True)
+    assert loss.dtype == torch.float32
+    xr = x.detach().float().clone().requires_grad_(True)
+    ref = F.cross_entropy(xr, y, reduction="none", ignore_index=-1, label_smoothing=smoothing)
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    g = torch.rand(N, device=DEV)
+    loss.backward(g)
+    ref.backward(g)
+    tol = dict(rtol=1e-5, atol=1e-6) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+
+
+def test_xentropy_misaligned_rows_and_half_loss():
+    """Row starts not 16-byte aligned (V odd, storage offset) and 16-bit losses."""
+    from apex_example_amd.contrib.xentropy import SoftmaxCrossEntropyLoss
+
+    base = torch.randn(33 * 1001 + 3, device=DEV, dtype=torch.bfloat16)
+    xs = base[3:].view(33, 1001)  # misaligned view (the forward reads it in place)
+    y = torch.randint(0, 1001, (33,), device=DEV)
+    loss = SoftmaxCrossEntropyLoss.apply(xs, y, 0.0, -1, False)
+    assert loss.dtype == torch.bfloat16
+    ref = F.cross_entropy(xs.float(), y, reduction="none")
+    torch.testing.assert_close(loss.float(), ref, rtol=2e-2, atol=2e-2)
+    x = xs.clone().requires_grad_(True)
+    SoftmaxCrossEntropyLoss.apply(x, y, 0.0, -1, True).sum().backward()
+    xr = xs.float().requires_grad_(True)
+    F.cross_entropy(xr, y, reduction="sum").backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-4)
