@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default=None)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true")
+    ap.add_argument("--no-fused-loss", action="store_true",
+                    help="transformers: torch cross entropy on fp32 logits instead of the fused kernel")
     ap.add_argument("--no-fused-attn", action="store_true",
                     help="transformers: PyTorch SDPA instead of the gfx950 attention kernels")
     ap.add_argument("--syncbn", action="store_true", help="SyncBatchNorm across ranks")
@@ -192,7 +194,7 @@ def build_bert(args, device, world):
 
         def step(b):
             mlm, nsp = model(b[0], b[1], b[2])
-            loss = pretraining_loss(mlm, nsp, b[3], b[4])
+            loss = pretraining_loss(mlm, nsp, b[3], b[4], fused=not args.no_fused_loss)
             opt.zero_grad()
             with amp.scale_loss(loss, opt) as scaled:
                 scaled.backward()
@@ -251,7 +253,7 @@ def build_gpt2(args, device, world):
             model = DistributedDataParallel(model, message_size=args.message_size)
 
         def step(b):
-            loss = lm_loss(model(b[0]), b[0])
+            loss = lm_loss(model(b[0]), b[0], fused=not args.no_fused_loss)
             opt.zero_grad()
             with amp.scale_loss(loss, opt) as scaled:
                 scaled.backward()

@@ -239,3 +239,29 @@ def gpu_ddp_resnet(rank, world, steps=4):
     torch.cuda.synchronize()
     return {"params": [p.detach().float().cpu() for p in m.parameters()], "losses": losses,
             "views": all(getattr(p, "_amd_grad_is_bucket_view", False) for p in m.parameters())}
+
+
+# ---------------------------------------------------------------------- ZeRO Adam
+def dfa_train(rank, world, dtype="fp32", clip=0.0, nb=2, steps=3, scale=1.0):
+    from apex_example_amd.contrib.optimizers import DistributedFusedAdam
+
+    model = _mlp()
+    if rank == 1:  # DistributedFusedAdam broadcasts rank 0's parameters
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(0.5)
+    if dtype == "bf16":
+        model = model.to(torch.bfloat16)
+    opt = DistributedFusedAdam(model.parameters(), lr=1e-2, weight_decay=0.01,
+                               max_grad_norm=clip, dwu_num_blocks=nb, align=8)
+    opt.set_global_scale(scale)
+    x, y = _data(8 * world)
+    xs, ys = x.chunk(world)[rank], y.chunk(world)[rank]
+    for _ in range(steps):
+        opt.zero_grad()
+        out = model(xs.to(next(model.parameters()).dtype)).float()
+        (F.cross_entropy(out, ys) * scale).backward()
+        opt.step()
+    sd = opt.state_dict()
+    return {"params": [p.detach().float().clone() for p in model.parameters()],
+            "step": sd["param_groups"][0]["step"], "shard_numel": sd["shards"][0]["master"].numel()}
