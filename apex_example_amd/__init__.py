@@ -10,7 +10,10 @@ data-parallel training framework with NVIDIA Apex's capabilities and API:
 * ``parallel``       - DistributedDataParallel (flat-bucket all-reduce over RCCL,
                        overlapped with backward), SyncBatchNorm, LARC;
 * ``fp16_utils``     - convert_network, FP16_Optimizer, ...;
-* ``multi_tensor_apply``, ``amp_C``, ``apex_C`` - Apex's low-level surfaces.
+* ``multi_tensor_apply``, ``amp_C``, ``apex_C`` - Apex's low-level surfaces;
+* ``contrib``        - fused softmax cross entropy, fast multi-head attention,
+                       NHWC group BN, ZeRO-style DistributedFusedAdam;
+* ``reparameterization`` (weight norm), ``RNN``, ``mlp``, ``pyprof``.
 
 All kernels are hand-written HIP for gfx950 (csrc/hip), built in-tree by
 ``python tools/build_ext.py``.
@@ -19,3 +22,4 @@ __version__ = "0.1.0"
 
 from . import _native  # noqa: F401
 from . import amp, fp16_utils, multi_tensor_apply, normalization, optimizers, parallel  # noqa: F401
+from . import contrib, reparameterization  # noqa: F401

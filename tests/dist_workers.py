@@ -265,3 +265,37 @@ def dfa_train(rank, world, dtype="fp32", clip=0.0, nb=2, steps=3, scale=1.0):
     sd = opt.state_dict()
     return {"params": [p.detach().float().clone() for p in model.parameters()],
             "step": sd["param_groups"][0]["step"], "shard_numel": sd["shards"][0]["master"].numel()}
+
+
+def gpu_dfa(rank, world, steps=5):
+    """Two ranks sharing cuda:0 over gloo: DistributedFusedAdam's HIP path (fused
+    Adam on shard views, 16-bit param slice written in-kernel, device-side
+    overflow check + step counter under a loss scale) on a bf16 GPT-2 block."""
+    from apex_example_amd.contrib.optimizers import DistributedFusedAdam
+    from apex_example_amd.models.gpt2 import GPT2Block, GPT2Config
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_embd=256, n_head=4, resid_pdrop=0.0, attn_pdrop=0.0)
+    m = GPT2Block(cfg).cuda().to(torch.bfloat16)
+    opt = DistributedFusedAdam(m.parameters(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0,
+                               dwu_num_blocks=3)
+    opt.set_global_scale(torch.tensor([1024.0], device="cuda"))
+    g = torch.Generator().manual_seed(7 + rank)
+    x = torch.randn(2, 128, 256, generator=g).cuda().to(torch.bfloat16)
+    losses = []
+    for it in range(steps):
+        opt.zero_grad()
+        loss = m(x).float().pow(2).mean()
+        (loss * 1024.0).backward()
+        if it == 2 and rank == 1:  # overflow on one rank: every rank must skip
+            next(m.parameters()).grad[0, 0] = float("inf")
+        before = [p.detach().clone() for p in m.parameters()] if it == 2 else None
+        opt.step()
+        if it == 2:
+            torch.cuda.synchronize()
+            skipped = all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
+        losses.append(loss.item())
+    torch.cuda.synchronize()
+    return {"params": [p.detach().float().cpu() for p in m.parameters()], "losses": losses,
+            "skipped": skipped, "step": opt.state_dict()["param_groups"][0]["step"]}

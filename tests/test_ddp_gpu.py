@@ -93,3 +93,13 @@ def test_two_ranks_one_gpu_gloo(tmp_path):
         assert torch.equal(a, b)
     assert res[0]["views"] and res[1]["views"]
     assert res[0]["losses"][-1] < res[0]["losses"][0]
+
+
+def test_distributed_fused_adam_two_ranks_one_gpu(tmp_path):
+    res = W.run("gpu_dfa", 2, str(tmp_path))
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        assert torch.equal(a, b)
+    for r in res:
+        assert r["skipped"]          # the injected overflow skipped the step on both ranks
+        assert r["step"] == 4        # 5 steps, one skipped
+    assert res[0]["losses"][-1] < res[0]["losses"][0]

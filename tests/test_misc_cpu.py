@@ -78,3 +78,58 @@ def test_pyprof_parse_attribution(tmp_path):
     assert per_op["relu(8x32 float32)"][0] == 1  # innermost range wins
     assert per_op["<unattributed>"][0] == 1
     assert "linear" in report(per_op)
+
+
+def test_weight_norm_reparameterization():
+    import torch
+    from apex_example_amd.reparameterization import apply_weight_norm, remove_weight_norm
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    x = torch.randn(5, 8)
+    y0 = m(x)
+    apply_weight_norm(m)
+    names = {n for n, _ in m.named_parameters()}
+    assert "0.weight_g" in names and "0.weight_v" in names and "0.bias" in names
+    torch.testing.assert_close(m(x), y0, rtol=1e-5, atol=1e-6)
+    # grads flow to g and v; scaling v leaves the output unchanged
+    m(x).sum().backward()
+    assert m[0].weight_g.grad is not None and m[0].weight_v.grad is not None
+    with torch.no_grad():
+        m[0].weight_v.mul_(3.0)
+    torch.testing.assert_close(m(x), y0, rtol=1e-5, atol=1e-6)
+    remove_weight_norm(m)
+    assert "0.weight" in {n for n, _ in m.named_parameters()}
+    torch.testing.assert_close(m(x), y0, rtol=1e-5, atol=1e-6)
+
+
+def test_apex_rnn_wrappers():
+    import torch
+    from apex_example_amd import RNN
+
+    x = torch.randn(6, 2, 5)
+    for ctor in (RNN.LSTM, RNN.GRU, RNN.ReLU, RNN.Tanh, RNN.mLSTM):
+        m = ctor(5, 7, 2, output_size=3)
+        out, _ = m(x)
+        assert out.shape == (6, 2, 3)
+        out.sum().backward()
+
+
+def test_multiproc_launcher(tmp_path):
+    import sys
+
+    from apex_example_amd.parallel import multiproc
+
+    script = tmp_path / "child.py"
+    script.write_text(
+        "import os, sys\n"
+        "args = sys.argv[1:]\n"
+        "r = args[args.index('--rank') + 1]; w = args[args.index('--world-size') + 1]\n"
+        "assert os.environ['RANK'] == r and os.environ['WORLD_SIZE'] == w\n"
+        "open(os.path.join(%r, 'rank' + r), 'w').write(w)\n" % str(tmp_path))
+    assert multiproc.main(["--nproc", "3", str(script)]) == 0
+    assert sorted(p.name for p in tmp_path.glob("rank*")) == ["rank0", "rank1", "rank2"]
+    bad = tmp_path / "bad.py"
+    bad.write_text("import sys; sys.exit(3)\n")
+    assert multiproc.main(["--nproc", "2", str(bad)]) == 3
+    del sys
