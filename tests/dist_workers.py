@@ -29,8 +29,8 @@ def _entry(rank, world, port, fn_name, out, kw):
     try:
         res = globals()[fn_name](rank, world, **kw)
         torch.save(res, os.path.join(out, "rank%d.pt" % rank))
+        dist.barrier()  # only on success: a failing rank exits and mp.spawn stops the rest
     finally:
-        dist.barrier()
         dist.destroy_process_group()
 
 
@@ -289,7 +289,7 @@ def gpu_dfa(rank, world, steps=5):
         loss = m(x).float().pow(2).mean()
         (loss * 1024.0).backward()
         if it == 2 and rank == 1:  # overflow on one rank: every rank must skip
-            next(m.parameters()).grad[0, 0] = float("inf")
+            next(m.parameters()).grad.view(-1)[0] = float("inf")
         before = [p.detach().clone() for p in m.parameters()] if it == 2 else None
         opt.step()
         if it == 2:
