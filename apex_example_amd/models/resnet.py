@@ -89,9 +89,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        if self.downsample is None and isinstance(self.conv1, Conv2d1x1):
-            # identity block: the residual-gradient add rides in conv1's dgrad GEMM
-            out, identity = self.conv1.forward_with_skip(x)
+        if isinstance(self.conv1, Conv2d1x1):
+            # the block input feeds conv1 and the residual branch (identity or the
+            # downsample conv): the two input gradients are summed inside conv1's
+            # dgrad GEMM (C += dY @ W into the branch's gradient), not by a separate
+            # add kernel over the block input
+            out, skip = self.conv1.forward_with_skip(x)
+            identity = skip if self.downsample is None else self.downsample(skip)
         else:
             identity = x if self.downsample is None else self.downsample(x)
             out = self.conv1(x)

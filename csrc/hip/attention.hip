@@ -242,20 +242,26 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) x[t] = mfma32<T>(lds_row8<T>(Kl, koff[t][s]), qf[s], x[t]);
     }
-    // scores -> log2 units, mask, running max
+    // mask (boundary / diagonal tiles only: the test is wave-uniform), running
+    // max on the raw scores, then one fma + exp2 per score in log2 units
+    const bool need_mask =
+        (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= a.S || (CAUSAL && key > q)) x[t][r] = -INFINITY;
+        }
+    }
     float tmax = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float sv = x[t][r] * a.scale_log2;
-        const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (key >= a.S || (CAUSAL && key > q)) sv = -INFINITY;
-        x[t][r] = sv;
-        tmax = fmaxf(tmax, sv);
-      }
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, x[t][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-    const float mnew = fmaxf(m, tmax);
+    const float mnew = fmaxf(m, tmax * a.scale_log2);
     const float alpha = exp2f(m - mnew);
     m = mnew;
     float psum = 0.f;
@@ -263,7 +269,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(x[t][r] - mnew);
+        const float p = exp2f(fmaf(x[t][r], a.scale_log2, -mnew));
         psum += p;
         x[t][r] = p;
       }
@@ -464,6 +470,8 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
         sc = mfma32<T>(lds_row8<T>(Qr, roff[h][s]), kf[s], sc);
         dp = mfma32<T>(lds_row8<T>(Or, roff[h][s]), vf[s], dp);
       }
+      // wave-uniform: does any (query, key) of this 32 x 32 block need a mask?
+      const bool need_mask = (qh0 + 31 >= a.S) || (CAUSAL && kw0 + 31 > qh0);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int li = 32 * h + 8 * g + 4 * hl;  // local query of register 4g
@@ -475,15 +483,15 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
           const int q = q0 + li + e;
-          const bool live = q < a.S && !(CAUSAL && key > q);
           float z = 1.f;
           if (DROP) {
             const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
             z = drop_keep(hsh, key, a.thr16) ? a.inv_keep : 0.f;
           }
-          const float p = live ? exp2f(sc[r] * a.scale_log2 - lsev[e]) : 0.f;
-          const float ds = live ? p * (dp[r] * z - Dv[e]) : 0.f;
-          sc[r] = p * z;
+          float p = exp2f(fmaf(sc[r], a.scale_log2, -lsev[e]));
+          float ds = p * fmaf(dp[r], z, -Dv[e]);
+          if (need_mask && !(q < a.S && !(CAUSAL && key > q))) p = ds = 0.f;
+          sc[r] = DROP ? p * z : p;
           dp[r] = ds;
         }
       }
@@ -607,23 +615,26 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
         dp[t] = mfma32<T>(lds_row8<T>(Vr, koff[t][s]), of[s], dp[t]);
       }
     }
+    const bool need_mask = (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;  // even
-        const bool live0 = key < a.S && !(CAUSAL && key > q);
-        const bool live1 = key + 1 < a.S && !(CAUSAL && key + 1 > q);
         float z0 = 1.f, z1 = 1.f;
         if (DROP) {
           const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
           z0 = drop_keep(hsh, key, a.thr16) ? a.inv_keep : 0.f;
           z1 = drop_keep(hsh, key + 1, a.thr16) ? a.inv_keep : 0.f;
         }
-        const float p0 = exp2f(sc[t][r] * a.scale_log2 - lse_q);
-        const float p1 = exp2f(sc[t][r + 1] * a.scale_log2 - lse_q);
-        sc[t][r] = live0 ? p0 * (dp[t][r] * z0 - D_q) : 0.f;
-        sc[t][r + 1] = live1 ? p1 * (dp[t][r + 1] * z1 - D_q) : 0.f;
+        float d0 = exp2f(fmaf(sc[t][r], a.scale_log2, -lse_q)) * fmaf(dp[t][r], z0, -D_q);
+        float d1 = exp2f(fmaf(sc[t][r + 1], a.scale_log2, -lse_q)) * fmaf(dp[t][r + 1], z1, -D_q);
+        if (need_mask) {
+          if (!(key < a.S && !(CAUSAL && key > q))) d0 = 0.f;
+          if (!(key + 1 < a.S && !(CAUSAL && key + 1 > q))) d1 = 0.f;
+        }
+        sc[t][r] = d0;
+        sc[t][r + 1] = d1;
       }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
