@@ -57,7 +57,11 @@ def main(argv=None):
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--md", default=None)
     ap.add_argument("--steps", type=int, default=None, help="divide totals per step")
+    ap.add_argument("--dispatch-filter", default=None,
+                    help="regex: also list every matching dispatch in order (grid, duration)")
+    ap.add_argument("--dispatch-out", default=None)
     a = ap.parse_args(argv)
+    disp = []
 
     files = _find(a.root, "*kernel_trace.csv")
     if not files:
@@ -78,6 +82,10 @@ def main(argv=None):
                 if ranges and not any(r0 <= s <= r1 for r0, r1 in ranges):
                     continue
                 name = row.get("Kernel_Name", "?")
+                if a.dispatch_filter and re.search(a.dispatch_filter, name):
+                    disp.append((s, _short(name, 60), row.get("Grid_Size_X", ""),
+                                 row.get("Grid_Size_Y", ""), row.get("Workgroup_Size_X", ""),
+                                 (e - s) / 1e3))
                 tot[name] += (e - s) / 1e3  # us
                 cnt[name] += 1
                 t_min = s if t_min is None else min(t_min, s)
@@ -101,6 +109,10 @@ def main(argv=None):
     if a.md:
         with open(a.md, "w") as fh:
             fh.write(out)
+    if a.dispatch_out:
+        with open(a.dispatch_out, "w") as fh:
+            for s0, n, gx, gy, wg, us in sorted(disp):
+                fh.write("%s\t%s\t%s\t%s\t%.2f\n" % (n, gx, gy, wg, us))
     return 0
 
 
