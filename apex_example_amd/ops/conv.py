@@ -146,7 +146,9 @@ class Conv2d1x1(nn.Conv2d):
                 and x.dtype == self.weight.dtype and self.groups == 1)
 
 
-_MFMA_WGRAD_MIN_W = 48
+# 3x3 weight gradient: "tap" = per-tap MFMA kernel (default), "nine" = the all-taps
+# strip kernel (W <= 56), "miopen" = MIOpen's convolution_backward
+_WGRAD3 = os.environ.get("APEX_AMD_WGRAD3", "tap")
 # A/B switches for the reduction / rotation kernels (tools, docs/PERF.md)
 _USE_SPLITK_REDUCE = os.environ.get("APEX_AMD_SPLITK_REDUCE", "1") == "1"
 _USE_ROT_KERNEL = os.environ.get("APEX_AMD_ROT_KERNEL", "1") == "1"
@@ -178,10 +180,11 @@ class Conv3x3Function(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _native.require().conv.conv3x3_fwd(dy, _rot_weight(weight))
         if ctx.needs_input_grad[1]:
-            # the all-taps MFMA wgrad kernel beats MIOpen on the 56x56 layers only
-            # (profiles/microbench_conv3x3.txt); its strip is sized for W <= 56
-            if 56 >= x.size(3) >= _MFMA_WGRAD_MIN_W:
-                dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype)
+            n_pix = x.size(0) * x.size(2) * x.size(3)
+            if _WGRAD3 == "tap" and n_pix < (1 << 22):
+                dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype, 0)
+            elif _WGRAD3 == "nine" and x.size(3) <= 56 and n_pix < (1 << 22):
+                dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype, 1)
             else:
                 dw = torch.ops.aten.convolution_backward(
                     dy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,

@@ -400,6 +400,174 @@ __global__ void __launch_bounds__(kCT, 1)
   }
 }
 
+// ----------------------------------------------------------------------------
+// Per-tap weight gradient (the default path): one workgroup = one filter tap
+// (r, s) x a BM(co) x BN(ci) output tile x one pixel range (split-K), so the
+// wave tiles are 64 x 64 (16 MFMA 16x16x32 accumulators per wave, two
+// workgroups per CU) instead of the 9-tap kernel's 32 x 32 x 9:
+//   dW[co, tap, ci] += sum_{p in range} dY[p, co] * X[p + (r-1)*W + (s-1), ci]
+// with the shifted pixel zeroed outside the image.  Both LDS images are pixel
+// rows ([k][channel], 16-byte chunks XOR-swizzled on the DMA source side) read
+// as MFMA fragments with ds_read_b64_tr_b16.  128 x 128 tiles use 2 x 2 waves on
+// BK = 64 pixels; 64-channel layers use 64 x 64 tiles with the 4 waves splitting
+// BK = 128 pixels (an in-workgroup split-K summed in the epilogue), so the LDS
+// bytes per MFMA stay the same.  Workgroups of one pixel range (all taps and
+// tiles: the same dY rows and nearly the same X rows) are packed onto one XCD.
+// Output: fp32 partials [split][tap][co][ci] for wgrad_reduce{1,2}_k.
+template <int BM, int BN, int WM, int WN, int WK, int BK, int NB>
+__global__ void __launch_bounds__(kCT, 2)
+    conv3x3_wgrad_tap_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                        float* __restrict__ part, int H, int W, int Cin, int Cout, int M,
+                        int kps, int total_kt, int gx) {
+  static_assert(WM * WN * WK == 4, "4 waves");
+  constexpr int TM = BM / WM, TN = BN / WN;
+  static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tiles of 32-column blocks");
+  constexpr int FM = TM / 16, FN = TN / 16, HM = TM / 32, HN = TN / 32;
+  constexpr int RBA = BM * 2, RBB = BN * 2;        // LDS row bytes (128 | 256)
+  constexpr int A_BYTES = BK * RBA, B_BYTES = BK * RBB, BUF = A_BYTES + B_BYTES;
+  constexpr int AI = A_BYTES / 4096, BI = B_BYTES / 4096;  // 1 KiB glds per wave per tile
+  constexpr int G = AI + BI;
+  constexpr int LPRA = RBA / 16, LPRB = RBB / 16;  // lanes per LDS row
+  constexpr int KW = BK / WK, KS = KW / 32;        // k rows per wave, 32-k MFMA steps
+  static_assert(AI >= 1 && BI >= 1 && KS >= 1, "tile too small");
+  constexpr int ES = BN + 4;                       // epilogue fp32 row stride
+  constexpr int EPI = WK * BM * ES * 4;
+  constexpr int LDSB = NB * BUF > EPI ? NB * BUF : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDSB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid % WK, wn = (wid / WK) % WN, wm = wid / (WK * WN);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lid / gx, tt = lid - split * gx;
+  const int tap = tt % 9, tile = tt / 9;
+  const int ci_tiles = Cin / BN;
+  const int co0 = (tile / ci_tiles) * BM, ci0 = (tile % ci_tiles) * BN;
+  const int kt_begin = split * kps;
+  const int kt_end = kt_begin + kps < total_kt ? kt_begin + kps : total_kt;
+  const int KT = kt_end - kt_begin;
+  const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+  const int64_t xshift = (int64_t)(dr * W + dc) * Cin;
+  const float invW = 1.f / (float)W, invH = 1.f / (float)H;
+
+  // per DMA row: logical chunk fetched by this lane (source-side swizzle)
+  int achunk[AI], bchunk[BI];
+#pragma unroll
+  for (int q = 0; q < AI; ++q) {
+    const int row = (wid * AI + q) * (1024 / RBA) + lane / LPRA;
+    achunk[q] = (tr_swz<RBA>(row, lane % LPRA) - row * RBA) >> 4;
+  }
+#pragma unroll
+  for (int q = 0; q < BI; ++q) {
+    const int row = (wid * BI + q) * (1024 / RBB) + lane / LPRB;
+    bchunk[q] = (tr_swz<RBB>(row, lane % LPRB) - row * RBB) >> 4;
+  }
+
+#define WGT_ISSUE(i_)                                                                          \
+  {                                                                                            \
+    const int p0_ = (kt_begin + (i_)) * BK;                                                    \
+    unsigned char* A_ = lds + ((i_) % NB) * BUF;                                               \
+    unsigned char* B_ = A_ + A_BYTES;                                                          \
+    _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                           \
+      const int p_ = p0_ + (wid * AI + q) * (1024 / RBA) + lane / LPRA;                        \
+      const void* src_ = p_ < M ? (const void*)(dy + (int64_t)p_ * Cout + co0 + achunk[q] * 8) \
+                                : (const void*)g_zero16;                                       \
+      glds16(src_, A_ + (wid * AI + q) * 1024);                                                \
+    }                                                                                          \
+    _Pragma("unroll") for (int q = 0; q < BI; ++q) {                                           \
+      const int p_ = p0_ + (wid * BI + q) * (1024 / RBB) + lane / LPRB;                        \
+      const int hq_ = fdiv(p_, W, invW);                                                       \
+      const int w_ = p_ - hq_ * W;                                                             \
+      const int h_ = hq_ - fdiv(hq_, H, invH) * H;                                             \
+      const bool ok_ = p_ < M && (unsigned)(h_ + dr) < (unsigned)H &&                          \
+                       (unsigned)(w_ + dc) < (unsigned)W;                                      \
+      const void* src_ = ok_ ? (const void*)(x + (int64_t)p_ * Cin + xshift + ci0 + bchunk[q] * 8) \
+                             : (const void*)g_zero16;                                          \
+      glds16(src_, B_ + (wid * BI + q) * 1024);                                                \
+    }                                                                                          \
+  }
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // loop-invariant transposed-read offsets: per k-step, column blocks c0 and c0+32
+  // (c0+16 / c0+48 are the same offsets with bit 5 flipped)
+  unsigned alo[KS][HM], ahi[KS][HM], blo[KS][HN], bhi[KS][HN];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int kb = wk * KW + ks * 32 + (lane >> 4) * 8;
+#pragma unroll
+    for (int h2 = 0; h2 < HM; ++h2)
+      tr_offsets<RBA>(kb, wm * TM + 32 * h2, lane, alo[ks][h2], ahi[ks][h2]);
+#pragma unroll
+    for (int h2 = 0; h2 < HN; ++h2)
+      tr_offsets<RBB>(kb, wn * TN + 32 * h2, lane, blo[ks][h2], bhi[ks][h2]);
+  }
+
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < KT) WGT_ISSUE(p);
+
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + NB - 2 < KT) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NB - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + NB - 1 < KT) WGT_ISSUE(kt + NB - 1);
+    const unsigned char* A = lds + (kt % NB) * BUF;
+    const unsigned char* B = A + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int h2 = 0; h2 < HM; ++h2) {
+        af[2 * h2] = tr_pair(A, alo[ks][h2], ahi[ks][h2]);
+        af[2 * h2 + 1] = tr_pair(A, alo[ks][h2] ^ 32u, ahi[ks][h2] ^ 32u);
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < HN; ++h2) {
+        bfr[2 * h2] = tr_pair(B, blo[ks][h2], bhi[ks][h2]);
+        bfr[2 * h2 + 1] = tr_pair(B, blo[ks][h2] ^ 32u, bhi[ks][h2] ^ 32u);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef WGT_ISSUE
+  __syncthreads();
+
+  // epilogue: accumulators -> fp32 LDS image [wk][BM][BN] -> (sum over wk) -> float4 rows
+  float* E = reinterpret_cast<float*>(lds);
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        E[(wk * BM + wm * TM + i * 16 + fg * 4 + e) * ES + wn * TN + j * 16 + fr] = acc[i][j][e];
+  __syncthreads();
+  float* out = part + ((int64_t)split * 9 + tap) * Cout * Cin;
+  constexpr int C4 = BN / 4;
+  for (int c = tid; c < BM * C4; c += kCT) {
+    const int row = c / C4, c4 = c - row * C4;
+    float4 v = *reinterpret_cast<const float4*>(E + row * ES + c4 * 4);
+#pragma unroll
+    for (int k = 1; k < WK; ++k) {
+      const float4 u = *reinterpret_cast<const float4*>(E + (k * BM + row) * ES + c4 * 4);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    *reinterpret_cast<float4*>(out + (int64_t)(co0 + row) * Cin + ci0 + c4 * 4) = v;
+  }
+}
+
 // Split-K partial reduction, two stages so that thousands of threads each keep
 // several independent 16-byte loads in flight: stage 1 sums groups of splits
 // (grid.y = group), stage 2 sums the groups and writes dW (KRSC, bf16 / fp32).
@@ -462,35 +630,100 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// per-tap kernel tiling: 128 x 128 when both channel counts allow it, else 64 x 64
+// (algo 2/3: tuning variants - deeper DMA ring with a shorter or equal K-tile)
+struct WgTapCfg {
+  int BM, BN, BK, NB;
+};
+WgTapCfg wg_tap_cfg(int Cin, int Cout, int algo) {
+  if (Cin % 128 == 0 && Cout % 128 == 0) {
+    if (algo == 2) return {128, 128, 32, 4};
+    if (algo == 3) return {128, 128, 64, 3};
+    return {128, 128, 64, 2};
+  }
+  if (algo == 2) return {64, 64, 64, 3};
+  if (algo == 3) return {64, 64, 128, 3};
+  return {64, 64, 128, 2};
+}
+
 }  // namespace
 
 bool conv3x3_nhwc_supported(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
 
-int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout) {
-  const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;  // K-tiles per image
-  const int total = N * kpi;
-  const int tiles = (Cout / 64) * (Cin / 64);
-  int S = (512 + tiles - 1) / tiles;                  // ~2 workgroups per CU
-  const int max_s = total / 8;                         // >= 8 K-tiles per workgroup
-  if (S > max_s) S = max_s;
-  return S < 1 ? 1 : S;
+int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int algo) {
+  if (algo == 1) {
+    const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;  // K-tiles per image
+    const int total = N * kpi;
+    const int tiles = (Cout / 64) * (Cin / 64);
+    int S = (512 + tiles - 1) / tiles;                  // ~2 workgroups per CU
+    const int max_s = total / 8;                         // >= 8 K-tiles per workgroup
+    if (S > max_s) S = max_s;
+    return S < 1 ? 1 : S;
+  }
+  // per-tap kernel: pick the split count minimising (rounds of 512 workgroup slots =
+  // 2 per CU) x (K-tiles per workgroup) x tile time + the fp32 partial traffic
+  const WgTapCfg c = wg_tap_cfg(Cin, Cout, algo);
+  const int64_t M = (int64_t)N * H * W;
+  const int total_kt = (int)((M + c.BK - 1) / c.BK);
+  const int gx = 9 * (Cout / c.BM) * (Cin / c.BN);
+  const int slots = c.BK * c.NB * (c.BM + c.BN) * 2 > 80 * 1024 ? 256 : 512;  // WGs per CU
+  const double t_tile = 2.0 * c.BM * c.BN * c.BK / (4096.0 * 2400.0 * 0.5 / (slots / 256));  // us
+  const double t_split = 9.0 * Cout * Cin * 8.0 / 5.0e6;                           // us
+  int best = 1;
+  double best_cost = 1e30;
+  const int smax = total_kt < 2048 ? total_kt : 2048;
+  for (int S = 1; S <= smax; ++S) {
+    const int kps = (total_kt + S - 1) / S;
+    if (kps < 4 && S > 1) break;
+    const int se = (total_kt + kps - 1) / kps;
+    const int64_t rounds = ((int64_t)gx * se + slots - 1) / slots;
+    const double cost = (double)rounds * kps * t_tile + se * t_split;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = se;
+    }
+  }
+  return best;
 }
 
-bool conv3x3_wgrad_supported(int W) { return W <= kWgMaxW; }
+bool conv3x3_wgrad_supported(int W, int algo) { return algo != 1 || W <= kWgMaxW; }
 
 int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout) {
   return (int64_t)(S + (S + kRedGroup - 1) / kRedGroup) * 9 * Cout * Cin;
 }
 
 void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
-                        int N, int H, int W, int Cin, int Cout, int S, hipStream_t st) {
-  const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;
-  const int total = N * kpi;
-  const int kps = (total + S - 1) / S;
-  const int tiles = (Cout / 64) * (Cin / 64);
-  hipLaunchKernelGGL((conv3x3_wgrad9_k<3>), dim3(tiles, S), dim3(kCT), 0, st,
-                     static_cast<const bf16_t*>(dy), static_cast<const bf16_t*>(x), part, H, W,
-                     Cin, Cout, kpi, kps, total);
+                        int N, int H, int W, int Cin, int Cout, int S, int algo, hipStream_t st) {
+  const auto* dyp = static_cast<const bf16_t*>(dy);
+  const auto* xp = static_cast<const bf16_t*>(x);
+  if (algo == 1) {
+    const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;
+    const int total = N * kpi;
+    const int kps = (total + S - 1) / S;
+    const int tiles = (Cout / 64) * (Cin / 64);
+    hipLaunchKernelGGL((conv3x3_wgrad9_k<3>), dim3(tiles, S), dim3(kCT), 0, st, dyp, xp, part,
+                       H, W, Cin, Cout, kpi, kps, total);
+  } else {
+    const WgTapCfg c = wg_tap_cfg(Cin, Cout, algo);
+    const int M = N * H * W;
+    const int total_kt = (M + c.BK - 1) / c.BK;
+    const int kps = (total_kt + S - 1) / S;
+    const int gx = 9 * (Cout / c.BM) * (Cin / c.BN);
+    const dim3 grid((unsigned)(gx * S));
+#define WGT_LAUNCH(...)                                                                       \
+  hipLaunchKernelGGL((conv3x3_wgrad_tap_k<__VA_ARGS__>), grid, dim3(kCT), 0, st, dyp, xp, part, \
+                     H, W, Cin, Cout, M, kps, total_kt, gx)
+    if (c.BM == 128) {
+      if (c.BK == 32) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 4);
+      else if (c.NB == 3) WGT_LAUNCH(128, 128, 2, 2, 1, 64, 3);
+      else WGT_LAUNCH(128, 128, 2, 2, 1, 64, 2);
+    } else {
+      if (c.BK == 64) WGT_LAUNCH(64, 64, 1, 2, 2, 64, 3);
+      else if (c.NB == 3) WGT_LAUNCH(64, 64, 1, 1, 4, 128, 3);
+      else WGT_LAUNCH(64, 64, 1, 1, 4, 128, 2);
+    }
+#undef WGT_LAUNCH
+  }
   // two-stage reduction; `part` holds S partial slabs followed by ceil(S/16)
   // stage-1 slabs (conv3x3_wgrad_workspace)
   const int64_t nout = (int64_t)9 * Cout * Cin;

@@ -202,8 +202,9 @@ void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W
                       int Cout, hipStream_t st);
 // weight gradient: split-K over pixels into fp32 partials [S][9][Cout][Cin], then a
 // reduce into dW (KRSC, bf16 or fp32)
-int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout);
-bool conv3x3_wgrad_supported(int W);
+// algo 0 = per-tap MFMA kernel (any W), 1 = all-9-taps strip kernel (W <= 56)
+int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int algo);
+bool conv3x3_wgrad_supported(int W, int algo);
 int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout);  // floats
 // generic split-K slab reduction: out[co][ci] = sum_s part[s][co][ci] (n % 4 == 0)
 int64_t splitk_reduce_workspace(int S, int64_t n);
@@ -212,7 +213,7 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
 // 16-bit W'[ci][2-r][2-s][co] = W[co][r][s][ci] (data-gradient filter)
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
 void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
-                        int N, int H, int W, int Cin, int Cout, int S, hipStream_t st);
+                        int N, int H, int W, int Cin, int Cout, int S, int algo, hipStream_t st);
 
 // ---- fused attention, head dim 64 (attention.hip) ---------------------------
 struct AttnLaunch {

@@ -63,7 +63,7 @@ at::Tensor conv3x3_nhwc_fwd_op(at::Tensor x, at::Tensor w) {
   return y;
 }
 
-at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype) {
+at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && dy.dim() == 4, "conv3x3_wgrad: 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16,
@@ -75,14 +75,16 @@ at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv3x3_wgrad: out dtype");
   x = x.contiguous(at::MemoryFormat::ChannelsLast);
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
-  const int S = conv3x3_wgrad_splits((int)N, (int)H, (int)W, (int)Cin, (int)Cout);
-  TORCH_CHECK(conv3x3_wgrad_supported((int)W), "conv3x3_wgrad: width > 56 unsupported");
+  const int S = conv3x3_wgrad_splits((int)N, (int)H, (int)W, (int)Cin, (int)Cout, algo);
+  TORCH_CHECK(conv3x3_wgrad_supported((int)W, algo), "conv3x3_wgrad: width > 56 unsupported for algo 1");
+  // the kernels split pixel indices with a float reciprocal (exact below 2^22)
+  TORCH_CHECK(N * H * W < ((int64_t)1 << 22), "conv3x3_wgrad: too many pixels");
   at::Tensor part = at::empty({conv3x3_wgrad_workspace(S, (int)Cin, (int)Cout)},
                               x.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({Cout, Cin, 3, 3},
                             x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
   conv3x3_nhwc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(),
-                     out_dtype == at::kFloat, (int)N, (int)H, (int)W, (int)Cin, (int)Cout, S,
+                     out_dtype == at::kFloat, (int)N, (int)H, (int)W, (int)Cin, (int)Cout, S, algo,
                      cur_stream());
   return dw;
 }

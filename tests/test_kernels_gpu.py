@@ -509,3 +509,29 @@ def test_xentropy_misaligned_rows_and_half_loss():
     xr = xs.float().requires_grad_(True)
     F.cross_entropy(xr, y, reduction="sum").backward()
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-4)
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(2, 64, 64, 9, 9), (3, 128, 128, 5, 7), (2, 64, 192, 8, 8),
+                                   (1, 256, 128, 14, 14), (4, 128, 256, 7, 7),
+                                   (2, 64, 64, 1, 1), (8, 64, 64, 30, 30)])
+def test_conv3x3_wgrad_kernels(shape, algo):
+    """Per-tap (algo 0: 128x128 and 64x64 tilings) and 9-tap strip (algo 1) MFMA
+    weight gradients vs the fp32 reference, fp32 and bf16 outputs."""
+    from apex_example_amd import _native
+
+    n, ci, co, h, w = shape
+    torch.manual_seed(1)
+    x = torch.randn(n, ci, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    dy = torch.randn(n, co, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    wref = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), torch.zeros(co, ci, 3, 3, device=DEV), None, (1, 1), (1, 1),
+        (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    cv = _native.require().conv
+    got = cv.conv3x3_wgrad(dy, x, torch.float32, algo)
+    assert got.shape == wref.shape
+    torch.testing.assert_close(got, wref, rtol=1e-4, atol=1e-3 * wref.abs().max().item())
+    got16 = cv.conv3x3_wgrad(dy, x, torch.bfloat16, algo)
+    torch.testing.assert_close(got16.float(), wref, rtol=1e-2, atol=1e-2 * wref.abs().max().item())

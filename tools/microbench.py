@@ -261,8 +261,8 @@ def bench_conv3x3(args):
     dev = "cuda"
     torch.backends.cudnn.benchmark = False
     print("| N,C,K,HW | GFLOP | MIOpen fwd | MFMA fwd | MIOpen dgrad | MFMA dgrad (+rot) | "
-          "MIOpen wgrad | MFMA wgrad | max rel err fwd / wgrad |")
-    print("|---|---|---|---|---|---|---|---|---|")
+          "MIOpen wgrad | MFMA wgrad per-tap | MFMA wgrad 9-tap | max rel err fwd / wgrad |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for (n, c, k, hw) in [(256, 64, 64, 56), (256, 128, 128, 28), (256, 256, 256, 14),
                           (256, 512, 512, 7)]:
         x = torch.randn(n, c, hw, hw, device=dev, dtype=torch.bfloat16).to(
@@ -279,21 +279,24 @@ def bench_conv3x3(args):
         t_od = timeit(lambda: cv.conv3x3_fwd(dy, _rot_weight(w)))
         t_mw = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1, (False, True, False)))
-        t_ow = timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16))
+        t_ow = timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16, 0))
+        t_o9 = timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16, 1)) if hw <= 56 else 0.0
+        t_v = [timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16, a)) for a in (2, 3)]
         ref = F.conv2d(x, w, padding=1).float()
         err = float((cv.conv3x3_fwd(x, w).float() - ref).abs().max() / ref.abs().max())
         wref = torch.ops.aten.convolution_backward(
             dy.float(), x.float(), w.float(), None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
             (False, True, False))[1]
-        werr = float((cv.conv3x3_wgrad(dy, x, torch.float32) - wref).abs().max()
+        werr = float((cv.conv3x3_wgrad(dy, x, torch.float32, 0) - wref).abs().max()
                      / wref.abs().max())
 
         def tf(t):
             return "%.0f us (%.0f TF)" % (t, gf / (t * 1e-6) / 1e3)
 
-        print("| %d,%d,%d,%d | %.1f | %s | %s | %s | %s | %s | %s | %.2e / %.2e |" % (
-            n, c, k, hw, gf, tf(t_mf), tf(t_of), tf(t_md), tf(t_od), tf(t_mw), tf(t_ow), err,
-            werr), flush=True)
+        print("| %d,%d,%d,%d | %.1f | %s | %s | %s | %s | %s | %s | %s | %.2e / %.2e |" % (
+            n, c, k, hw, gf, tf(t_mf), tf(t_of), tf(t_md), tf(t_od), tf(t_mw), tf(t_ow),
+            tf(t_o9) if t_o9 else "-", err, werr), "variants 2/3: %.0f / %.0f us" % tuple(t_v),
+            flush=True)
 
 
 def bench_attn(args):
