@@ -2,7 +2,8 @@
 (torchvision is not available).  ResNet-50 = 25,557,032 parameters in 161 tensors.
 
 ``gemm_1x1=True`` runs the stride-1 1x1 convs as hipBLASLt GEMMs and the
-stride-1 3x3 convs on the MFMA implicit-GEMM kernel (ops/conv.py).
+3x3 convs and the stride-2 1x1 projections on the MFMA implicit-GEMM kernels
+(ops/conv.py).
 ``fused_bn=True`` replaces each BatchNorm(+ReLU)(+residual add) with the fused
 gfx950 op ``BatchNorm2dReLU`` (one stats pass + one elementwise pass forward,
 one reduction + one elementwise pass backward, ReLU and the residual add folded
@@ -20,8 +21,8 @@ from ..ops.pool import MaxPool2dNHWC
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1, mfma=False):
-    if mfma and stride == 1 and groups == 1 and dilation == 1:
-        return Conv2d3x3(in_planes, out_planes)
+    if mfma and stride in (1, 2) and groups == 1 and dilation == 1:
+        return Conv2d3x3(in_planes, out_planes, stride)
     return nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation,
                      groups=groups, bias=False, dilation=dilation)
 

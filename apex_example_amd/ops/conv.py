@@ -121,6 +121,33 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         return dx, dw
 
 
+class Conv1x1Stride2Function(torch.autograd.Function):
+    """Stride-2 1x1 convolution (the ResNet downsample projection) on the MFMA
+    implicit-GEMM kernel: forward reads every other pixel in place (no subsample
+    copy), the data gradient is one launch over the 4 input-parity classes (the
+    even-even class is the GEMM dY @ W, the other three a zero store), the weight
+    gradient is the per-tap split-K kernel with one tap."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        ctx.save_for_backward(x, weight)
+        return _native.require().conv.conv_fwd(x, weight, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        cv = _native.require().conv
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        co, ci = weight.shape[0], weight.shape[1]
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            wt = weight.reshape(co, ci).t().contiguous().view(ci, co, 1, 1)
+            dx = cv.conv_dgrad_s2(dy, wt, x.size(2), x.size(3))
+        if ctx.needs_input_grad[1]:
+            dw = cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1)
+        return dx, dw
+
+
 class Conv2d1x1(nn.Conv2d):
     """nn.Conv2d(kernel_size=1) whose stride-1 channels-last GPU path runs as a
     GEMM; every other case falls back to the regular convolution."""
@@ -131,6 +158,8 @@ class Conv2d1x1(nn.Conv2d):
     def forward(self, x):
         if self._gemm_ok(x):
             return Conv1x1GemmFunction.apply(x, self.weight)
+        if self._strided_ok(x):
+            return Conv1x1Stride2Function.apply(x, self.weight)
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
                         self.groups)
 
@@ -139,6 +168,14 @@ class Conv2d1x1(nn.Conv2d):
         if self._gemm_ok(x):
             return Conv1x1SkipFunction.apply(x, self.weight)
         return self.forward(x), x
+
+    def _strided_ok(self, x):
+        return (self.stride == (2, 2) and self.bias is None and x.is_cuda and x.dim() == 4
+                and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last) and self.groups == 1
+                and x.size(2) % 2 == 0 and x.size(3) % 2 == 0
+                and x.size(0) * x.size(2) * x.size(3) < (1 << 22)
+                and self.in_channels % 64 == 0 and self.out_channels % 64 == 0)
 
     def _gemm_ok(self, x):
         return (self.stride == (1, 1) and self.bias is None and x.is_cuda and x.dim() == 4
@@ -163,33 +200,41 @@ def _rot_weight(weight):
 
 
 class Conv3x3Function(torch.autograd.Function):
-    """3x3 / stride 1 / pad 1 NHWC bf16 conv on the MFMA implicit-GEMM kernels
-    (csrc/hip/conv_igemm.hip): forward, data gradient (same kernel, rotated
-    weights) and weight gradient (split-K over pixels, transposed LDS reads)."""
+    """3x3 / pad 1 / stride 1 or 2 NHWC bf16 conv on the MFMA implicit-GEMM
+    kernels (csrc/hip/conv_igemm.hip): forward, data gradient (stride 1: the same
+    kernel with rotated weights; stride 2: one launch over the 4 input-parity
+    classes, each with only its matching filter taps) and weight gradient
+    (per-tap split-K kernel)."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, stride):
         ctx.save_for_backward(x, weight)
-        return _native.require().conv.conv3x3_fwd(x, weight)
+        ctx.stride = stride
+        return _native.require().conv.conv_fwd(x, weight, stride)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
+        stride = ctx.stride
+        cv = _native.require().conv
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = _native.require().conv.conv3x3_fwd(dy, _rot_weight(weight))
+            if stride == 1:
+                dx = cv.conv_fwd(dy, _rot_weight(weight), 1)
+            else:
+                dx = cv.conv_dgrad_s2(dy, _rot_weight(weight), x.size(2), x.size(3))
         if ctx.needs_input_grad[1]:
             n_pix = x.size(0) * x.size(2) * x.size(3)
             if _WGRAD3 == "tap" and n_pix < (1 << 22):
-                dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype, 0)
-            elif _WGRAD3 == "nine" and x.size(3) <= 56 and n_pix < (1 << 22):
-                dw = _native.require().conv.conv3x3_wgrad(dy, x, weight.dtype, 1)
+                dw = cv.conv_wgrad(dy, x, weight.dtype, 0, stride)
+            elif _WGRAD3 == "nine" and stride == 1 and x.size(3) <= 56 and n_pix < (1 << 22):
+                dw = cv.conv_wgrad(dy, x, weight.dtype, 1, 1)
             else:
                 dw = torch.ops.aten.convolution_backward(
-                    dy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                    dy, x, weight, None, (stride, stride), (1, 1), (1, 1), False, (0, 0), 1,
                     (False, True, False))[1]
-        return dx, dw
+        return dx, dw, None
 
 
 class Conv2d3x3(nn.Conv2d):
@@ -201,10 +246,13 @@ class Conv2d3x3(nn.Conv2d):
                          bias=bias)
 
     def forward(self, x):
-        if (self.stride == (1, 1) and self.bias is None and x.is_cuda and x.dim() == 4
+        st = self.stride[0]
+        if (self.stride in ((1, 1), (2, 2)) and self.bias is None and x.is_cuda and x.dim() == 4
+                and (st == 1 or (x.size(2) % 2 == 0 and x.size(3) % 2 == 0))
                 and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
                 and x.is_contiguous(memory_format=torch.channels_last) and self.groups == 1
-                and self.in_channels % 64 == 0 and self.out_channels % 64 == 0):
-            return Conv3x3Function.apply(x, self.weight)
+                and self.in_channels % 64 == 0 and self.out_channels % 64 == 0
+                and self.dilation == (1, 1) and self.padding == (1, 1)):
+            return Conv3x3Function.apply(x, self.weight, st)
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
                         self.groups)

@@ -53,10 +53,54 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + bid / 8;
 }
 
-template <int BN, int WM, int WN, int NB>
+// Tap sets of the implicit-GEMM launches (all wave-uniform integer arithmetic, so
+// the K loop's per-tile offsets stay in scalar registers):
+//   kFwd3 / kFwd1   - 3x3 pad-1 / 1x1 conv forward (stride via ConvGeom::as)
+//   kDgrad3 / kDgrad1 - data gradient of a stride-2 conv, blockIdx.z = input-pixel
+//                       parity class (ph, pw): class pixel (2a+ph, 2b+pw) receives
+//                       dY at (a + dh, b + dw) through the taps of matching parity
+//                       only (3x3: 1, 2, 2 or 4 taps; 1x1: one tap for the even-even
+//                       class, none - a zero store - for the others)
+enum ConvMode { kFwd3 = 0, kFwd1 = 1, kDgrad3 = 2, kDgrad1 = 3 };
+
+template <int MODE>
+__device__ __forceinline__ int conv_ntaps(int z) {
+  if constexpr (MODE == kFwd3) return 9;
+  else if constexpr (MODE == kFwd1) return 1;
+  else if constexpr (MODE == kDgrad3) return ((z >> 1) ? 2 : 1) * ((z & 1) ? 2 : 1);
+  else return z == 0 ? 1 : 0;
+}
+
+// tap t of class z: A-pixel offset (dh, dw) from the row's centre pixel and the
+// filter tap index wt into the B rows
+template <int MODE>
+__device__ __forceinline__ void conv_tap(int z, int t, int& dh, int& dw, int& wt) {
+  if constexpr (MODE == kFwd3) {
+    const int r = t / 3, s = t - r * 3;
+    dh = r - 1; dw = s - 1; wt = t;
+  } else if constexpr (MODE == kDgrad3) {
+    const int ph = z >> 1, pw = z & 1, ns = pw ? 2 : 1;
+    const int ri = t / ns, si = t - ri * ns;
+    const int r = ph ? 2 * ri : 1, s = pw ? 2 * si : 1;
+    dh = (ph + 1 - r) >> 1; dw = (pw + 1 - s) >> 1;
+    wt = 8 - (3 * r + s);  // B = rotated filter: wrot[ci][8-t][co] = W[co][t][ci]
+  } else {
+    dh = 0; dw = 0; wt = 0;
+  }
+}
+
+// GEMM row m -> (img, gh, gw) on a GH x GW grid; A centre pixel (gh*as, gw*as) of an
+// AH x AW image with KC channels; output pixel (gh*ys + yoh, gw*ys + yow) of a
+// YH x YW image with NC channels (dgrad: ys = 2, (yoh, yow) = the parity class);
+// B rows ([NC][taps][KC]) are kb_stride elements long
+struct ConvGeom {
+  int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
+};
+
+template <int MODE, int BN, int WM, int WN, int NB>
 __global__ void __launch_bounds__(kCT, 2)
-    conv3x3_fwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
-                  bf16_t* __restrict__ y, int N, int H, int W, int Cin, int Cout, int M) {
+    conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
+               bf16_t* __restrict__ y, ConvGeom g) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = kBM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -71,14 +115,16 @@ __global__ void __launch_bounds__(kCT, 2)
   const int wm = wid / WN, wn = wid % WN;
   const int mt = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = mt * kBM, n0 = blockIdx.y * BN;
-  const int HW = H * W;
+  const int z = blockIdx.z;
+  const int ntaps = conv_ntaps<MODE>(z);
+  const int KC = g.KC, M = g.M, GHW = g.GH * g.GW;
 
   // DMA lane geometry: wave `wid` fills A rows [wid*32, wid*32+32) as AI
   // instructions of 8 rows; lane -> (row = base + lane/8, physical chunk lane%8)
   // fetching the logical chunk that the swizzle stores at that position.
   const int lrow = lane >> 3, pchunk = lane & 7;
-  // per DMA row: source pointer at tap (1,1) / channel chunk, and a 9-bit mask of
-  // the taps whose shifted pixel is inside the image (so the K loop only adds a
+  // per DMA row: source pointer at the centre pixel / channel chunk, and a bit
+  // mask of the taps whose pixel is inside the A image (so the K loop only adds a
   // wave-uniform offset and tests one bit per row)
   const bf16_t* abase[AI];
   unsigned amask[AI];
@@ -88,15 +134,19 @@ __global__ void __launch_bounds__(kCT, 2)
     const int ch = pchunk ^ ((row >> 1) & 7);
     const int m = m0 + row;
     const int mm = m < M ? m : 0;
-    const int n = mm / HW;
-    const int rem = mm - n * HW;
-    const int h = rem / W, w = rem - (rem / W) * W;
-    abase[q] = x + (int64_t)mm * Cin + ch * 8;
+    const int n = mm / GHW;
+    const int rem = mm - n * GHW;
+    const int gh = rem / g.GW, gw = rem - gh * g.GW;
+    const int h = gh * g.as, w = gw * g.as;
+    abase[q] = x + ((int64_t)(n * g.AH + h) * g.AW + w) * KC + ch * 8;
     unsigned mk = 0;
+    constexpr int TMAX = MODE == kFwd3 ? 9 : (MODE == kDgrad3 ? 4 : 1);
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int hh = h + t / 3 - 1, ww = w + t % 3 - 1;
-      if (m < M && hh >= 0 && hh < H && ww >= 0 && ww < W) mk |= 1u << t;
+    for (int t = 0; t < TMAX; ++t) {
+      int dh, dw, wti;
+      conv_tap<MODE>(z, t, dh, dw, wti);
+      const int hh = h + dh, ww = w + dw;
+      if (t < ntaps && m < M && hh >= 0 && hh < g.AH && ww >= 0 && ww < g.AW) mk |= 1u << t;
     }
     amask[q] = mk;
   }
@@ -104,17 +154,19 @@ __global__ void __launch_bounds__(kCT, 2)
 #pragma unroll
   for (int q = 0; q < BI; ++q) {
     const int row = wid * (BN / 4) + q * 8 + lrow;
-    bbase[q] = wt + (int64_t)(n0 + row) * 9 * Cin + (pchunk ^ ((row >> 1) & 7)) * 8;
+    bbase[q] = wt + (int64_t)(n0 + row) * g.kb_stride + (pchunk ^ ((row >> 1) & 7)) * 8;
   }
-  const int kc_per_tap = Cin / kBK;
-  const int KT = 9 * kc_per_tap;
+  const int kc_per_tap = KC / kBK;
+  const int KT = ntaps * kc_per_tap;
 
 #define CONV_ISSUE(kt_)                                                                     \
   {                                                                                         \
     const int tap_ = (kt_) / kc_per_tap;                                                    \
     const int c0_ = ((kt_) - tap_ * kc_per_tap) * kBK;                                      \
-    const int64_t aoff_ = (int64_t)((tap_ / 3 - 1) * W + (tap_ % 3 - 1)) * Cin + c0_;       \
-    const int boff_ = tap_ * Cin + c0_;                                                     \
+    int dh_, dw_, wt_;                                                                      \
+    conv_tap<MODE>(z, tap_, dh_, dw_, wt_);                                                 \
+    const int64_t aoff_ = (int64_t)(dh_ * g.AW + dw_) * KC + c0_;                           \
+    const int boff_ = wt_ * KC + c0_;                                                       \
     unsigned char* A_ = lds + ((kt_) % NB) * BUF;                                           \
     unsigned char* B_ = A_ + A_BYTES;                                                       \
     _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                        \
@@ -186,15 +238,37 @@ __global__ void __launch_bounds__(kCT, 2)
       }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-byte chunks per output row
+  constexpr bool dense = MODE == kFwd3 || MODE == kFwd1;
   for (int c = tid; c < kBM * CPR; c += kCT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
-    if (m < M)
-      *reinterpret_cast<uint4*>(y + (int64_t)m * Cout + n0 + cc * 8) =
-          *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+    if (m >= M) continue;
+    int64_t opix = m;
+    if (!dense) {
+      const int n = m / GHW;
+      const int rem = m - n * GHW;
+      const int gh = rem / g.GW, gw = rem - gh * g.GW;
+      opix = (int64_t)(n * g.YH + gh * g.ys + (z >> 1)) * g.YW + gw * g.ys + (z & 1);
+    }
+    *reinterpret_cast<uint4*>(y + opix * g.NC + n0 + cc * 8) =
+        *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
   }
 }
 
+template <int MODE>
+void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
+                     hipStream_t st) {
+  if (g.M == 0) return;
+  const int mtiles = (g.M + kBM - 1) / kBM;
+  const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
+  if (g.NC % 128 == 0) {
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 2, 2, 2>), dim3(mtiles, g.NC / 128, nclasses),
+                       dim3(kCT), 0, st, a, w, y, g);
+  } else {
+    hipLaunchKernelGGL((conv_tap_k<MODE, 64, 4, 1, 3>), dim3(mtiles, g.NC / 64, nclasses),
+                       dim3(kCT), 0, st, a, w, y, g);
+  }
+}
 
 // ============================================================================
 // Weight gradient: dW[co, r, s, ci] = sum_p dY[p, co] * x[shift_rs(p), ci].
@@ -414,11 +488,11 @@ __global__ void __launch_bounds__(kCT, 1)
 // bytes per MFMA stay the same.  Workgroups of one pixel range (all taps and
 // tiles: the same dY rows and nearly the same X rows) are packed onto one XCD.
 // Output: fp32 partials [split][tap][co][ci] for wgrad_reduce{1,2}_k.
-template <int BM, int BN, int WM, int WN, int WK, int BK, int NB>
+template <int BM, int BN, int WM, int WN, int WK, int BK, int NB, bool S1>
 __global__ void __launch_bounds__(kCT, 2)
     conv3x3_wgrad_tap_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                        float* __restrict__ part, int H, int W, int Cin, int Cout, int M,
-                        int kps, int total_kt, int gx) {
+                        float* __restrict__ part, int H, int W, int Ho, int Wo, int stride,
+                        int T, int Cin, int Cout, int M, int kps, int total_kt, int gx) {
   static_assert(WM * WN * WK == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;
   static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tiles of 32-column blocks");
@@ -439,15 +513,14 @@ __global__ void __launch_bounds__(kCT, 2)
   const int wk = wid % WK, wn = (wid / WK) % WN, wm = wid / (WK * WN);
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = lid / gx, tt = lid - split * gx;
-  const int tap = tt % 9, tile = tt / 9;
+  const int tap = tt % T, tile = tt / T;
   const int ci_tiles = Cin / BN;
   const int co0 = (tile / ci_tiles) * BM, ci0 = (tile % ci_tiles) * BN;
   const int kt_begin = split * kps;
   const int kt_end = kt_begin + kps < total_kt ? kt_begin + kps : total_kt;
   const int KT = kt_end - kt_begin;
-  const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-  const int64_t xshift = (int64_t)(dr * W + dc) * Cin;
-  const float invW = 1.f / (float)W, invH = 1.f / (float)H;
+  const int dr = T == 9 ? tap / 3 - 1 : 0, dc = T == 9 ? tap % 3 - 1 : 0;
+  const float invWo = 1.f / (float)Wo, invHo = 1.f / (float)Ho;
 
   // per DMA row: logical chunk fetched by this lane (source-side swizzle)
   int achunk[AI], bchunk[BI];
@@ -475,12 +548,15 @@ __global__ void __launch_bounds__(kCT, 2)
     }                                                                                          \
     _Pragma("unroll") for (int q = 0; q < BI; ++q) {                                           \
       const int p_ = p0_ + (wid * BI + q) * (1024 / RBB) + lane / LPRB;                        \
-      const int hq_ = fdiv(p_, W, invW);                                                       \
-      const int w_ = p_ - hq_ * W;                                                             \
-      const int h_ = hq_ - fdiv(hq_, H, invH) * H;                                             \
-      const bool ok_ = p_ < M && (unsigned)(h_ + dr) < (unsigned)H &&                          \
-                       (unsigned)(w_ + dc) < (unsigned)W;                                      \
-      const void* src_ = ok_ ? (const void*)(x + (int64_t)p_ * Cin + xshift + ci0 + bchunk[q] * 8) \
+      const int hq_ = fdiv(p_, Wo, invWo);                                                     \
+      const int n_ = fdiv(hq_, Ho, invHo);                                                     \
+      const int hi_ = (hq_ - n_ * Ho) * (S1 ? 1 : stride) + dr;                                \
+      const int wi_ = (p_ - hq_ * Wo) * (S1 ? 1 : stride) + dc;                                \
+      const bool ok_ = p_ < M && (unsigned)hi_ < (unsigned)H && (unsigned)wi_ < (unsigned)W;   \
+      /* stride 1: the input pixel is the output pixel shifted by (dr, dc) */                  \
+      const int64_t xpix_ = S1 ? (int64_t)p_ + dr * W + dc                                     \
+                               : (int64_t)(n_ * H + hi_) * W + wi_;                            \
+      const void* src_ = ok_ ? (const void*)(x + xpix_ * Cin + ci0 + bchunk[q] * 8)            \
                              : (const void*)g_zero16;                                          \
       glds16(src_, B_ + (wid * BI + q) * 1024);                                                \
     }                                                                                          \
@@ -554,7 +630,7 @@ __global__ void __launch_bounds__(kCT, 2)
       for (int e = 0; e < 4; ++e)
         E[(wk * BM + wm * TM + i * 16 + fg * 4 + e) * ES + wn * TN + j * 16 + fr] = acc[i][j][e];
   __syncthreads();
-  float* out = part + ((int64_t)split * 9 + tap) * Cout * Cin;
+  float* out = part + ((int64_t)split * T + tap) * Cout * Cin;
   constexpr int C4 = BN / 4;
   for (int c = tid; c < BM * C4; c += kCT) {
     const int row = c / C4, c4 = c - row * C4;
@@ -650,7 +726,7 @@ WgTapCfg wg_tap_cfg(int Cin, int Cout, int algo) {
 
 bool conv3x3_nhwc_supported(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
 
-int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int algo) {
+int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int stride, int algo) {
   if (algo == 1) {
     const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;  // K-tiles per image
     const int total = N * kpi;
@@ -662,13 +738,14 @@ int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int algo) {
   }
   // per-tap kernel: pick the split count minimising (rounds of 512 workgroup slots =
   // 2 per CU) x (K-tiles per workgroup) x tile time + the fp32 partial traffic
+  const int T = ksize * ksize;
   const WgTapCfg c = wg_tap_cfg(Cin, Cout, algo);
-  const int64_t M = (int64_t)N * H * W;
+  const int64_t M = (int64_t)N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
   const int total_kt = (int)((M + c.BK - 1) / c.BK);
-  const int gx = 9 * (Cout / c.BM) * (Cin / c.BN);
+  const int gx = T * (Cout / c.BM) * (Cin / c.BN);
   const int slots = c.BK * c.NB * (c.BM + c.BN) * 2 > 80 * 1024 ? 256 : 512;  // WGs per CU
   const double t_tile = 2.0 * c.BM * c.BN * c.BK / (4096.0 * 2400.0 * 0.5 / (slots / 256));  // us
-  const double t_split = 9.0 * Cout * Cin * 8.0 / 5.0e6;                           // us
+  const double t_split = (double)T * Cout * Cin * 8.0 / 5.0e6;                     // us
   int best = 1;
   double best_cost = 1e30;
   const int smax = total_kt < 2048 ? total_kt : 2048;
@@ -688,14 +765,16 @@ int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int algo) {
 
 bool conv3x3_wgrad_supported(int W, int algo) { return algo != 1 || W <= kWgMaxW; }
 
-int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout) {
-  return (int64_t)(S + (S + kRedGroup - 1) / kRedGroup) * 9 * Cout * Cin;
+int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize) {
+  return (int64_t)(S + (S + kRedGroup - 1) / kRedGroup) * ksize * ksize * Cout * Cin;
 }
 
-void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
-                        int N, int H, int W, int Cin, int Cout, int S, int algo, hipStream_t st) {
+void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32, int N,
+                     int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
+                     hipStream_t st) {
   const auto* dyp = static_cast<const bf16_t*>(dy);
   const auto* xp = static_cast<const bf16_t*>(x);
+  const int T = ksize * ksize;
   if (algo == 1) {
     const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;
     const int total = N * kpi;
@@ -705,28 +784,32 @@ void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bo
                        H, W, Cin, Cout, kpi, kps, total);
   } else {
     const WgTapCfg c = wg_tap_cfg(Cin, Cout, algo);
-    const int M = N * H * W;
+    const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+    const int M = N * Ho * Wo;
     const int total_kt = (M + c.BK - 1) / c.BK;
     const int kps = (total_kt + S - 1) / S;
-    const int gx = 9 * (Cout / c.BM) * (Cin / c.BN);
+    const int gx = T * (Cout / c.BM) * (Cin / c.BN);
     const dim3 grid((unsigned)(gx * S));
 #define WGT_LAUNCH(...)                                                                       \
   hipLaunchKernelGGL((conv3x3_wgrad_tap_k<__VA_ARGS__>), grid, dim3(kCT), 0, st, dyp, xp, part, \
-                     H, W, Cin, Cout, M, kps, total_kt, gx)
+                     H, W, Ho, Wo, stride, T, Cin, Cout, M, kps, total_kt, gx)
+    const bool s1 = stride == 1;
     if (c.BM == 128) {
-      if (c.BK == 32) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 4);
-      else if (c.NB == 3) WGT_LAUNCH(128, 128, 2, 2, 1, 64, 3);
-      else WGT_LAUNCH(128, 128, 2, 2, 1, 64, 2);
+      if (c.BK == 32) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 4, false);
+      else if (c.NB == 3) WGT_LAUNCH(128, 128, 2, 2, 1, 64, 3, false);
+      else if (s1) WGT_LAUNCH(128, 128, 2, 2, 1, 64, 2, true);
+      else WGT_LAUNCH(128, 128, 2, 2, 1, 64, 2, false);
     } else {
-      if (c.BK == 64) WGT_LAUNCH(64, 64, 1, 2, 2, 64, 3);
-      else if (c.NB == 3) WGT_LAUNCH(64, 64, 1, 1, 4, 128, 3);
-      else WGT_LAUNCH(64, 64, 1, 1, 4, 128, 2);
+      if (c.BK == 64) WGT_LAUNCH(64, 64, 1, 2, 2, 64, 3, false);
+      else if (c.NB == 3) WGT_LAUNCH(64, 64, 1, 1, 4, 128, 3, false);
+      else if (s1) WGT_LAUNCH(64, 64, 1, 1, 4, 128, 2, true);
+      else WGT_LAUNCH(64, 64, 1, 1, 4, 128, 2, false);
     }
 #undef WGT_LAUNCH
   }
   // two-stage reduction; `part` holds S partial slabs followed by ceil(S/16)
-  // stage-1 slabs (conv3x3_wgrad_workspace)
-  const int64_t nout = (int64_t)9 * Cout * Cin;
+  // stage-1 slabs (conv_wgrad_workspace)
+  const int64_t nout = (int64_t)T * Cout * Cin;
   const int Gn = (S + kRedGroup - 1) / kRedGroup;
   float* stage = part + (int64_t)S * nout;
   const int64_t n4 = nout / 4;
@@ -735,10 +818,10 @@ void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bo
   const unsigned blocks = (unsigned)((nout + 255) / 256);
   if (dw_fp32)
     hipLaunchKernelGGL((wgrad_reduce2_k<float>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<float*>(dw), 9);
+                       Cin, static_cast<float*>(dw), T);
   else
     hipLaunchKernelGGL((wgrad_reduce2_k<bf16_t>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<bf16_t*>(dw), 9);
+                       Cin, static_cast<bf16_t*>(dw), T);
 }
 
 int64_t splitk_reduce_workspace(int S, int64_t n) {
@@ -766,21 +849,30 @@ void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t
                      static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin);
 }
 
-void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin,
-                      int Cout, hipStream_t st) {
-  const int M = N * H * W;
-  if (M == 0) return;
-  const int mtiles = (M + kBM - 1) / kBM;
+void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
+                   int ksize, int stride, hipStream_t st) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const ConvGeom g{Ho, Wo, H, W, stride, Ho, Wo, 1, Cin, Cout, N * Ho * Wo, ksize * ksize * Cin};
   const auto* xp = static_cast<const bf16_t*>(x);
   const auto* wp = static_cast<const bf16_t*>(w);
   auto* yp = static_cast<bf16_t*>(y);
-  if (Cout % 128 == 0) {
-    hipLaunchKernelGGL((conv3x3_fwd_k<128, 2, 2, 2>), dim3(mtiles, Cout / 128), dim3(kCT), 0, st,
-                       xp, wp, yp, N, H, W, Cin, Cout, M);
-  } else {
-    hipLaunchKernelGGL((conv3x3_fwd_k<64, 4, 1, 3>), dim3(mtiles, Cout / 64), dim3(kCT), 0, st,
-                       xp, wp, yp, N, H, W, Cin, Cout, M);
-  }
+  if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st);
+  else launch_conv_tap<kFwd1>(xp, wp, yp, g, st);
+}
+
+// Data gradient of a stride-2 conv (3x3 pad 1 or 1x1 pad 0; H = 2*Ho, W = 2*Wo), one
+// launch over the 4 input-parity classes (kDgrad3 / kDgrad1 above), so no MFMA
+// work is spent on the zeros of the dilated dY.  wt: 3x3 -> conv3x3_rot_weight(W);
+// 1x1 -> W^T ([Cin][Cout]).
+void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, int W, int Cin,
+                        int Cout, int ksize, hipStream_t st) {
+  const int Ho = H / 2, Wo = W / 2;
+  const ConvGeom g{Ho, Wo, Ho, Wo, 1, H, W, 2, Cout, Cin, N * Ho * Wo, ksize * ksize * Cout};
+  const auto* dyp = static_cast<const bf16_t*>(dy);
+  const auto* wp = static_cast<const bf16_t*>(wt);
+  auto* dxp = static_cast<bf16_t*>(dx);
+  if (ksize == 3) launch_conv_tap<kDgrad3>(dyp, wp, dxp, g, st);
+  else launch_conv_tap<kDgrad1>(dyp, wp, dxp, g, st);
 }
 
 }  // namespace amd

@@ -196,24 +196,30 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
 void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
                         int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 
-// ---- implicit-GEMM 3x3 stride-1 pad-1 conv, NHWC bf16, MFMA (conv_igemm.hip) ----
+// ---- implicit-GEMM convolutions, NHWC bf16, MFMA (conv_igemm.hip) ----------
+// 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64
 bool conv3x3_nhwc_supported(int Cin, int Cout);
-void conv3x3_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin,
-                      int Cout, hipStream_t st);
-// weight gradient: split-K over pixels into fp32 partials [S][9][Cout][Cin], then a
-// reduce into dW (KRSC, bf16 or fp32)
-// algo 0 = per-tap MFMA kernel (any W), 1 = all-9-taps strip kernel (W <= 56)
-int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int algo);
+// y is N x Ho x Wo x Cout, Ho = (H-1)/stride + 1; w is [Cout][k*k][Cin]
+void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
+                   int ksize, int stride, hipStream_t st);
+// data gradient of a stride-2 conv (H, W even); wt = rotated 3x3 filter / W^T for 1x1
+void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, int W, int Cin,
+                        int Cout, int ksize, hipStream_t st);
+// weight gradient: split-K over output pixels into fp32 partials [S][k*k][Cout][Cin],
+// then a reduce into dW (KRSC, bf16 or fp32).  algo 0 = per-tap MFMA kernel,
+// 1 = all-9-taps strip kernel (3x3 stride 1, W <= 56)
+int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int stride, int algo);
 bool conv3x3_wgrad_supported(int W, int algo);
-int64_t conv3x3_wgrad_workspace(int S, int Cin, int Cout);  // floats
+int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize);  // floats
 // generic split-K slab reduction: out[co][ci] = sum_s part[s][co][ci] (n % 4 == 0)
 int64_t splitk_reduce_workspace(int S, int64_t n);
 void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, void* out,
                    bool out_fp32, hipStream_t st);
 // 16-bit W'[ci][2-r][2-s][co] = W[co][r][s][ci] (data-gradient filter)
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
-void conv3x3_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32,
-                        int N, int H, int W, int Cin, int Cout, int S, int algo, hipStream_t st);
+void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32, int N,
+                     int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
+                     hipStream_t st);
 
 // ---- fused attention, head dim 64 (attention.hip) ---------------------------
 struct AttnLaunch {

@@ -83,9 +83,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
   pool.def("max_bwd", &maxpool2d_nhwc_bwd_op);
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
-  conv.def("conv3x3_fwd", &conv3x3_nhwc_fwd_op);
-  conv.def("conv3x3_wgrad", &conv3x3_nhwc_wgrad_op, py::arg("dy"), py::arg("x"), py::arg("out_dtype"),
-           py::arg("algo") = 0);
+  conv.def("conv_fwd", &conv_nhwc_fwd_op, py::arg("x"), py::arg("w"), py::arg("stride") = 1);
+  conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);
+  conv.def("conv_wgrad", &conv_nhwc_wgrad_op, py::arg("dy"), py::arg("x"), py::arg("out_dtype"),
+           py::arg("algo") = 0, py::arg("stride") = 1, py::arg("ksize") = 3);
   conv.def("splitk_reduce", &splitk_reduce_op);
   conv.def("rot_weight", &conv3x3_rot_weight_op);
 

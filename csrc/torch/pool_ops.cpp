@@ -45,47 +45,75 @@ at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64
 
 namespace amd {
 
-at::Tensor conv3x3_nhwc_fwd_op(at::Tensor x, at::Tensor w) {
+at::Tensor conv_nhwc_fwd_op(at::Tensor x, at::Tensor w, int64_t stride) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4, "conv3x3: 4-D GPU tensors expected");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4, "conv: 4-D GPU tensors expected");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
-              "conv3x3: bf16 only");
+              "conv: bf16 only");
+  TORCH_CHECK(stride == 1 || stride == 2, "conv: stride 1 or 2");
   const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
-  const int64_t Cout = w.size(0);
-  TORCH_CHECK(w.size(1) == Cin && w.size(2) == 3 && w.size(3) == 3, "conv3x3: weight shape");
-  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv3x3: channels must be x64");
-  TORCH_CHECK(N * H * W < (int64_t)1 << 31, "conv3x3: too many pixels");
+  const int64_t Cout = w.size(0), k = w.size(2);
+  TORCH_CHECK((k == 3 || k == 1) && w.size(3) == k && w.size(1) == Cin, "conv: weight shape");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv: channels must be x64");
+  TORCH_CHECK(N * H * W < (int64_t)1 << 31, "conv: too many pixels");
   x = x.contiguous(at::MemoryFormat::ChannelsLast);
-  w = w.contiguous(at::MemoryFormat::ChannelsLast);  // [Cout][3][3][Cin] in memory
-  at::Tensor y = at::empty({N, Cout, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  conv3x3_nhwc_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)Cin,
-                   (int)Cout, cur_stream());
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);  // [Cout][k][k][Cin] in memory
+  at::Tensor y = at::empty({N, Cout, Ho, Wo},
+                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  conv_nhwc_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)Cin,
+                (int)Cout, (int)k, (int)stride, cur_stream());
   return y;
 }
 
-at::Tensor conv3x3_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo) {
+at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && dy.dim() == 4, "conv3x3_wgrad: 4-D GPU tensors");
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && wt.dim() == 4, "conv_dgrad_s2: 4-D GPU tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && wt.scalar_type() == at::kBFloat16,
+              "conv_dgrad_s2: bf16 only");
+  const int64_t N = dy.size(0), Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  const int64_t Cin = wt.size(0), k = wt.size(2);
+  TORCH_CHECK(wt.size(1) == Cout && (k == 3 || k == 1) && wt.size(3) == k,
+              "conv_dgrad_s2: transposed / rotated weight [Cin, Cout, k, k] expected");
+  TORCH_CHECK(H == 2 * Ho && W == 2 * Wo, "conv_dgrad_s2: even input sizes only");
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cout, (int)Cin), "conv_dgrad_s2: channels x64");
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  wt = wt.contiguous(at::MemoryFormat::ChannelsLast);
+  at::Tensor dx = at::empty({N, Cin, H, W},
+                            dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  conv_nhwc_dgrad_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)N, (int)H, (int)W,
+                     (int)Cin, (int)Cout, (int)k, cur_stream());
+  return dx;
+}
+
+at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
+                              int64_t stride, int64_t ksize) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16,
-              "conv3x3_wgrad: bf16 only");
+              "conv_wgrad: bf16 only");
+  TORCH_CHECK(ksize == 3 || (ksize == 1 && algo != 1), "conv_wgrad: kernel size");
   const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Cout = dy.size(1);
-  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv3x3_wgrad: shapes");
-  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv3x3_wgrad: channels must be x64");
-  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv3x3_wgrad: out dtype");
+  TORCH_CHECK(stride == 1 || (stride == 2 && algo != 1), "conv_wgrad: stride");
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == (H - 1) / stride + 1 &&
+                  dy.size(3) == (W - 1) / stride + 1, "conv_wgrad: shapes");
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv_wgrad: channels must be x64");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv_wgrad: out dtype");
+  TORCH_CHECK(conv3x3_wgrad_supported((int)W, (int)algo), "conv_wgrad: width > 56 unsupported for algo 1");
+  // the kernels split pixel indices with a float reciprocal (exact below 2^22)
+  TORCH_CHECK(N * H * W < ((int64_t)1 << 22), "conv_wgrad: too many pixels");
   x = x.contiguous(at::MemoryFormat::ChannelsLast);
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
-  const int S = conv3x3_wgrad_splits((int)N, (int)H, (int)W, (int)Cin, (int)Cout, algo);
-  TORCH_CHECK(conv3x3_wgrad_supported((int)W, algo), "conv3x3_wgrad: width > 56 unsupported for algo 1");
-  // the kernels split pixel indices with a float reciprocal (exact below 2^22)
-  TORCH_CHECK(N * H * W < ((int64_t)1 << 22), "conv3x3_wgrad: too many pixels");
-  at::Tensor part = at::empty({conv3x3_wgrad_workspace(S, (int)Cin, (int)Cout)},
+  const int S = conv_wgrad_splits((int)N, (int)H, (int)W, (int)Cin, (int)Cout, (int)ksize,
+                                  (int)stride, (int)algo);
+  at::Tensor part = at::empty({conv_wgrad_workspace(S, (int)Cin, (int)Cout, (int)ksize)},
                               x.options().dtype(at::kFloat));
-  at::Tensor dw = at::empty({Cout, Cin, 3, 3},
+  at::Tensor dw = at::empty({Cout, Cin, ksize, ksize},
                             x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
-  conv3x3_nhwc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(),
-                     out_dtype == at::kFloat, (int)N, (int)H, (int)W, (int)Cin, (int)Cout, S, algo,
-                     cur_stream());
+  conv_nhwc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(),
+                  out_dtype == at::kFloat, (int)N, (int)H, (int)W, (int)Cin, (int)Cout, (int)ksize,
+                  (int)stride, S, (int)algo, cur_stream());
   return dw;
 }
 

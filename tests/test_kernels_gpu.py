@@ -530,8 +530,40 @@ def test_conv3x3_wgrad_kernels(shape, algo):
         dy.float(), x.float(), torch.zeros(co, ci, 3, 3, device=DEV), None, (1, 1), (1, 1),
         (1, 1), False, (0, 0), 1, (False, True, False))[1]
     cv = _native.require().conv
-    got = cv.conv3x3_wgrad(dy, x, torch.float32, algo)
+    got = cv.conv_wgrad(dy, x, torch.float32, algo)
     assert got.shape == wref.shape
     torch.testing.assert_close(got, wref, rtol=1e-4, atol=1e-3 * wref.abs().max().item())
-    got16 = cv.conv3x3_wgrad(dy, x, torch.bfloat16, algo)
+    got16 = cv.conv_wgrad(dy, x, torch.bfloat16, algo)
     torch.testing.assert_close(got16.float(), wref, rtol=1e-2, atol=1e-2 * wref.abs().max().item())
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 8, 8), (3, 128, 64, 14, 10), (2, 64, 128, 2, 2),
+                                   (4, 256, 256, 14, 14)])
+@pytest.mark.parametrize("k", [3, 1])
+def test_conv_stride2_mfma(shape, k):
+    """Stride-2 3x3 (pad 1) and 1x1 convs on the MFMA kernels: forward, the
+    parity-class data gradient and the strided per-tap weight gradient vs fp32."""
+    from apex_example_amd.ops.conv import Conv2d1x1, Conv2d3x3
+
+    n, ci, co, h, w = shape
+    torch.manual_seed(2)
+    m = (Conv2d3x3(ci, co, stride=2) if k == 3 else Conv2d1x1(ci, co, stride=2))
+    m = m.to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(n, ci, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    xr = x.detach().float().clone().requires_grad_(True)
+    wr = m.weight.detach().float().clone().requires_grad_(True)
+    y = m(x)
+    if k == 1:
+        assert "Stride2" in type(y.grad_fn).__name__
+    yr = F.conv2d(xr, wr, stride=2, padding=k // 2)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    scale = yr.abs().max().item()
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2 * scale)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy)
+    gs = xr.grad.abs().max().item()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * gs)
+    ws = wr.grad.abs().max().item()
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=2e-2 * ws)

@@ -14,7 +14,7 @@ for (n, c, hw) in [(256, 64, 56), (256, 256, 14)]:
     w = (torch.randn(c, c, 3, 3, device="cuda", dtype=torch.bfloat16) * 0.05).to(
         memory_format=torch.channels_last)
     for _ in range(3):
-        cv.conv3x3_fwd(x, w)
-        cv.conv3x3_wgrad(x, x, torch.bfloat16)
+        cv.conv_fwd(x, w)
+        cv.conv_wgrad(x, x, torch.bfloat16)
 torch.cuda.synchronize()
 print("done")

@@ -273,21 +273,21 @@ def bench_conv3x3(args):
             memory_format=torch.channels_last)
         gf = 2 * n * hw * hw * c * k * 9 / 1e9
         t_mf = timeit(lambda: F.conv2d(x, w, padding=1))
-        t_of = timeit(lambda: cv.conv3x3_fwd(x, w))
+        t_of = timeit(lambda: cv.conv_fwd(x, w))
         t_md = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1, (True, False, False)))
-        t_od = timeit(lambda: cv.conv3x3_fwd(dy, _rot_weight(w)))
+        t_od = timeit(lambda: cv.conv_fwd(dy, _rot_weight(w)))
         t_mw = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1, (False, True, False)))
-        t_ow = timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16, 0))
-        t_o9 = timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16, 1)) if hw <= 56 else 0.0
-        t_v = [timeit(lambda: cv.conv3x3_wgrad(dy, x, torch.bfloat16, a)) for a in (2, 3)]
+        t_ow = timeit(lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0))
+        t_o9 = timeit(lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 1)) if hw <= 56 else 0.0
+        t_v = [timeit(lambda: cv.conv_wgrad(dy, x, torch.bfloat16, a)) for a in (2, 3)]
         ref = F.conv2d(x, w, padding=1).float()
-        err = float((cv.conv3x3_fwd(x, w).float() - ref).abs().max() / ref.abs().max())
+        err = float((cv.conv_fwd(x, w).float() - ref).abs().max() / ref.abs().max())
         wref = torch.ops.aten.convolution_backward(
             dy.float(), x.float(), w.float(), None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
             (False, True, False))[1]
-        werr = float((cv.conv3x3_wgrad(dy, x, torch.float32, 0) - wref).abs().max()
+        werr = float((cv.conv_wgrad(dy, x, torch.float32, 0) - wref).abs().max()
                      / wref.abs().max())
 
         def tf(t):
@@ -296,6 +296,50 @@ def bench_conv3x3(args):
         print("| %d,%d,%d,%d | %.1f | %s | %s | %s | %s | %s | %s | %s | %.2e / %.2e |" % (
             n, c, k, hw, gf, tf(t_mf), tf(t_of), tf(t_md), tf(t_od), tf(t_mw), tf(t_ow),
             tf(t_o9) if t_o9 else "-", err, werr), "variants 2/3: %.0f / %.0f us" % tuple(t_v),
+            flush=True)
+
+
+def bench_conv_s2(args):
+    """Stride-2 convs of ResNet-50 (3x3 in layer2-4's first block, 1x1 downsample
+    projections): MIOpen vs the MFMA kernels, forward / data grad / weight grad."""
+    from apex_example_amd import _native
+    from apex_example_amd.ops.conv import _rot_weight
+
+    cv = _native.require().conv
+    dev = "cuda"
+    print("| k,N,C,K,HW(in) | GFLOP | MIOpen fwd | MFMA fwd | MIOpen dgrad | MFMA dgrad | "
+          "MIOpen wgrad | MFMA wgrad |")
+    print("|---|---|---|---|---|---|---|---|")
+    for (k, n, c, co, hw) in [(3, 256, 128, 128, 56), (3, 256, 256, 256, 28), (3, 256, 512, 512, 14),
+                              (1, 256, 256, 512, 56), (1, 256, 512, 1024, 28),
+                              (1, 256, 1024, 2048, 14)]:
+        x = torch.randn(n, c, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = (torch.randn(co, c, k, k, device=dev, dtype=torch.bfloat16) * 0.05).to(
+            memory_format=torch.channels_last)
+        ho = hw // 2
+        dy = torch.randn(n, co, ho, ho, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        gf = 2 * n * ho * ho * c * co * k * k / 1e9
+        pad = k // 2
+        t_mf = timeit(lambda: F.conv2d(x, w, stride=2, padding=pad))
+        t_of = timeit(lambda: cv.conv_fwd(x, w, 2))
+        t_md = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, (2, 2), (pad, pad), (1, 1), False, (0, 0), 1, (True, False, False)))
+        if k == 3:
+            t_od = timeit(lambda: cv.conv_dgrad_s2(dy, _rot_weight(w), hw, hw))
+        else:
+            t_od = timeit(lambda: cv.conv_dgrad_s2(
+                dy, w.reshape(co, c).t().contiguous().view(c, co, 1, 1), hw, hw))
+        t_mw = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, (2, 2), (pad, pad), (1, 1), False, (0, 0), 1, (False, True, False)))
+        t_ow = timeit(lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0, 2, k))
+
+        def tf(t):
+            return "%.0f us (%.0f TF)" % (t, gf / (t * 1e-6) / 1e3)
+
+        print("| %d,%d,%d,%d,%d | %.1f | %s | %s | %s | %s | %s | %s |" % (
+            k, n, c, co, hw, gf, tf(t_mf), tf(t_of), tf(t_md), tf(t_od), tf(t_mw), tf(t_ow)),
             flush=True)
 
 
@@ -422,12 +466,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     a = ap.parse_args()
     {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
-     "conv3x3": bench_conv3x3, "attn": bench_attn}[a.what](a)
+     "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
 
 if __name__ == "__main__":

@@ -17,6 +17,6 @@ for i in which:
         memory_format=torch.channels_last)
     dy = torch.randn_like(x)
     for _ in range(3):
-        cv.conv3x3_wgrad(dy, x, torch.bfloat16, int(os.environ.get("ALGO", "0")))
+        cv.conv_wgrad(dy, x, torch.bfloat16, int(os.environ.get("ALGO", "0")))
 torch.cuda.synchronize()
 print("ok")
