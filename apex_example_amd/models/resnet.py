@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
-from ..ops.conv import Conv2d1x1, Conv2d3x3
+from ..ops.conv import Conv2d1x1, Conv2d3x3, StemConv2d
 from ..ops.pool import MaxPool2dNHWC
 
 
@@ -122,7 +122,11 @@ class ResNet(nn.Module):
         self.fused_bn = fused_bn
         self.gemm_1x1 = gemm_1x1
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        if gemm_1x1 and self.inplanes == 64:
+            self.conv1 = StemConv2d(3, self.inplanes)  # MFMA stem kernels (ops/conv.py)
+        else:
+            self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3,
+                                   bias=False)
         self.bn1 = _BNAct(self.inplanes, True, fused_bn)
         pool = MaxPool2dNHWC if fused_bn else nn.MaxPool2d
         self.maxpool = pool(kernel_size=3, stride=2, padding=1)

@@ -256,3 +256,56 @@ class Conv2d3x3(nn.Conv2d):
             return Conv3x3Function.apply(x, self.weight, st)
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
                         self.groups)
+
+
+def _pack_stem_weight(weight):
+    """[64, 3, 7, 7] -> [64, 7 (r), 32 (4 s + c)] bf16, zeros at c = 3 and s = 7."""
+    wk = torch.zeros(64, 7, 8, 4, device=weight.device, dtype=torch.bfloat16)
+    wk[:, :, :7, :3] = weight.permute(0, 2, 3, 1)
+    return wk.view(64, 224)
+
+
+class StemConvFunction(torch.autograd.Function):
+    """ResNet stem 7x7/2 conv (3 -> 64 channels) on the gfx950 stem kernels
+    (csrc/hip/stem_conv.hip): the image is zero-padded once to 4 channels, a wave
+    computes whole output rows from an LDS ring of input rows; the weight
+    gradient reads the same padded image.  The image gradient (not needed for
+    training from data) falls back to MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        cv = _native.require().conv
+        xp = cv.stem_pad(x)
+        ctx.save_for_backward(x, xp, weight)
+        return cv.stem_fwd(xp, _pack_stem_weight(weight))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xp, weight = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            part = _native.require().conv.stem_wgrad(xp, dy)  # [64, 256] fp32
+            dw = part.view(64, 8, 8, 4)[:, :7, :7, :3].permute(0, 3, 1, 2).to(weight.dtype)
+            dw = dw.contiguous(memory_format=torch.channels_last) \
+                if weight.is_contiguous(memory_format=torch.channels_last) else dw.contiguous()
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(
+                dy, x, weight, None, (2, 2), (3, 3), (1, 1), False, (0, 0), 1,
+                (True, False, False))[0]
+        return dx, dw
+
+
+class StemConv2d(nn.Conv2d):
+    """nn.Conv2d(3, 64, 7, stride=2, padding=3) whose bf16 GPU path runs the MFMA
+    stem kernels; other dtypes / sizes use the regular convolution."""
+
+    def __init__(self, in_planes=3, out_planes=64):
+        super().__init__(in_planes, out_planes, kernel_size=7, stride=2, padding=3, bias=False)
+
+    def forward(self, x):
+        if (x.is_cuda and x.dim() == 4 and x.size(1) == 3 and self.out_channels == 64
+                and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
+                and x.size(2) % 2 == 0 and x.size(3) % 2 == 0 and x.size(3) <= 250
+                and self.in_channels == 3):
+            return StemConvFunction.apply(x, self.weight)
+        return F.conv2d(x, self.weight, None, self.stride, self.padding)

@@ -221,6 +221,18 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
                      int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
                      hipStream_t st);
 
+// ---- ResNet stem: 7x7 / stride 2 / pad 3, 3 -> 64 channels, NHWC bf16 (stem_conv.hip) ----
+bool stem_conv_supported(int N, int H, int W);
+// x [N][H][W][3] -> xp [N][H+6][W+6][4] (zero border, zero 4th channel)
+void stem_pad(const void* x, void* xp, int N, int H, int W, hipStream_t st);
+// wk: packed filter [64][7][32] (wk[co][r][4s+c] = W[co][c][r][s], zeros elsewhere);
+// y [N][H/2][W/2][64]
+void stem_fwd(const void* xp, const void* wk, void* y, int N, int H, int W, hipStream_t st);
+// fp32 partials [S][64][256] of the packed filter gradient (n = 32 r + 4 s + c)
+int stem_wgrad_splits(int N, int H);
+void stem_wgrad(const void* xp, const void* dy, float* part, int S, int N, int H, int W,
+                hipStream_t st);
+
 // ---- fused attention, head dim 64 (attention.hip) ---------------------------
 struct AttnLaunch {
   const void* q;

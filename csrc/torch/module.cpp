@@ -88,6 +88,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("conv_wgrad", &conv_nhwc_wgrad_op, py::arg("dy"), py::arg("x"), py::arg("out_dtype"),
            py::arg("algo") = 0, py::arg("stride") = 1, py::arg("ksize") = 3);
   conv.def("splitk_reduce", &splitk_reduce_op);
+  conv.def("stem_pad", &stem_pad_op);
+  conv.def("stem_fwd", &stem_fwd_op);
+  conv.def("stem_wgrad", &stem_wgrad_op);
   conv.def("rot_weight", &conv3x3_rot_weight_op);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");

@@ -117,6 +117,53 @@ at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dt
   return dw;
 }
 
+at::Tensor stem_pad_op(at::Tensor x) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) == 3 && x.scalar_type() == at::kBFloat16,
+              "stem_pad: bf16 [N, 3, H, W] expected");
+  x = x.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(stem_conv_supported((int)N, (int)H, (int)W), "stem_pad: unsupported size");
+  at::Tensor xp = at::empty({N, H + 6, W + 6, 4}, x.options());
+  stem_pad(x.data_ptr(), xp.data_ptr(), (int)N, (int)H, (int)W, cur_stream());
+  return xp;
+}
+
+at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(xp.is_cuda() && xp.dim() == 4 && xp.size(3) == 4 && xp.is_contiguous() &&
+                  xp.scalar_type() == at::kBFloat16, "stem_fwd: padded input [N, H+6, W+6, 4]");
+  TORCH_CHECK(wk.is_cuda() && wk.numel() == 64 * 224 && wk.is_contiguous() &&
+                  wk.scalar_type() == at::kBFloat16, "stem_fwd: packed filter [64, 7, 32]");
+  const int64_t N = xp.size(0), H = xp.size(1) - 6, W = xp.size(2) - 6;
+  TORCH_CHECK(stem_conv_supported((int)N, (int)H, (int)W), "stem_fwd: unsupported size");
+  at::Tensor y = at::empty({N, 64, H / 2, W / 2},
+                           xp.options().memory_format(at::MemoryFormat::ChannelsLast));
+  stem_fwd(xp.data_ptr(), wk.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, cur_stream());
+  return y;
+}
+
+at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(xp.is_cuda() && xp.dim() == 4 && xp.size(3) == 4 && xp.is_contiguous() &&
+                  xp.scalar_type() == at::kBFloat16, "stem_wgrad: padded input [N, H+6, W+6, 4]");
+  const int64_t N = xp.size(0), H = xp.size(1) - 6, W = xp.size(2) - 6;
+  TORCH_CHECK(stem_conv_supported((int)N, (int)H, (int)W), "stem_wgrad: unsupported size");
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 64 &&
+                  dy.size(2) == H / 2 && dy.size(3) == W / 2 && dy.scalar_type() == at::kBFloat16,
+              "stem_wgrad: dy [N, 64, H/2, W/2] bf16");
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  const int S = stem_wgrad_splits((int)N, (int)H);
+  at::Tensor part = at::empty({(int64_t)S * 64 * 256 + splitk_reduce_workspace(S, 64 * 256)},
+                              xp.options().dtype(at::kFloat));
+  stem_wgrad(xp.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), S, (int)N, (int)H, (int)W,
+             cur_stream());
+  at::Tensor out = at::empty({64, 256}, xp.options().dtype(at::kFloat));
+  splitk_reduce(part.data_ptr<float>(), S, 64, 256, part.data_ptr<float>() + (int64_t)S * 64 * 256,
+                out.data_ptr(), true, cur_stream());
+  return out;
+}
+
 at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&

@@ -17,6 +17,9 @@ at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_
 at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
                               int64_t stride, int64_t ksize);
 at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype);
+at::Tensor stem_pad_op(at::Tensor x);
+at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk);
+at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy);
 at::Tensor conv3x3_rot_weight_op(at::Tensor w);
 
 }  // namespace amd

@@ -567,3 +567,27 @@ def test_conv_stride2_mfma(shape, k):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * gs)
     ws = wr.grad.abs().max().item()
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=2e-2 * ws)
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 32), (3, 64, 48), (1, 224, 224), (2, 18, 250)])
+def test_stem_conv_mfma(shape):
+    """ResNet stem 7x7/2 (3 -> 64) MFMA kernels: forward and weight gradient vs fp32."""
+    from apex_example_amd.ops.conv import StemConv2d
+
+    n, h, w = shape
+    torch.manual_seed(3)
+    m = StemConv2d().to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(n, 3, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    wr = m.weight.detach().float().clone().requires_grad_(True)
+    y = m(x)
+    assert "StemConv" in type(y.grad_fn).__name__
+    yr = F.conv2d(x.float(), wr, stride=2, padding=3)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    scale = yr.abs().max().item()
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=1e-2 * scale)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy)
+    ws = wr.grad.abs().max().item()
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=1e-2 * ws)
