@@ -22,4 +22,4 @@ __version__ = "0.1.0"
 
 from . import _native  # noqa: F401
 from . import amp, fp16_utils, multi_tensor_apply, normalization, optimizers, parallel  # noqa: F401
-from . import contrib, reparameterization  # noqa: F401
+from . import contrib, fused_dense, reparameterization  # noqa: F401

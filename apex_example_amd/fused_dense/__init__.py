@@ -1,0 +1,158 @@
+"""Fused dense layers (apex.fused_dense API: ``FusedDense``, ``FusedDenseGeluDense``,
+``DenseNoBias`` and the ``fused_dense_function`` / ``fused_dense_gelu_dense_function``
+functionals), MI355X-native.
+
+Forward: hipBLASLt GEMMs with the bias in the GEMM (``addmm``).  Backward: the
+data / weight gradients are hipBLASLt GEMMs; the bias gradients (column sums of
+dY, which PyTorch's generic reduction runs at ~1 TB/s) and the GELU backward of
+the FFN run on ``csrc/hip/bias_grad.hip``: one split-row column-sum pass at HBM
+rate, and for the FFN one pass that forms dpre = dh * gelu'(pre) AND its column
+sums (no extra read of dpre for the first bias).
+
+Under autocast (amp O1) the operands are cast once in forward and the casted
+copies saved, so backward runs plain half-precision GEMMs (no second weight
+cast); bias gradients are reduced in fp32 and written in the bias's dtype.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native
+
+__all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function",
+           "fused_dense_gelu_dense_function", "dense_no_bias_function"]
+
+
+def _compute_dtype(x):
+    if torch.is_autocast_enabled("cuda") and x.is_cuda:
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
+def _cast(t, dt):
+    return t if t is None or t.dtype == dt else t.to(dt)
+
+
+def _bias_grad(g2, dtype):
+    if g2.is_cuda and _native.available():
+        return _native.require().dense.bias_grad(g2, dtype)
+    return g2.float().sum(0).to(dtype)
+
+
+class FusedDenseFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        dt = _compute_dtype(x)
+        with torch.autocast("cuda", enabled=False):
+            xc, wc, bc = _cast(x, dt), _cast(weight, dt), _cast(bias, dt)
+            x2 = xc.reshape(-1, xc.size(-1))
+            y = torch.addmm(bc, x2, wc.t()) if bc is not None else x2 @ wc.t()
+        ctx.save_for_backward(xc, wc)
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        return y.view(*x.shape[:-1], weight.size(0))
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.size(-1)).contiguous()
+        if dy2.dtype != wc.dtype:
+            dy2 = dy2.to(wc.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ wc).view(xc.shape)
+        if ctx.needs_input_grad[1]:
+            dw = dy2.t() @ xc.reshape(-1, xc.size(-1))
+        if ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
+            db = _bias_grad(dy2, ctx.bias_dtype)
+        return dx, dw, db
+
+
+class FusedDenseGeluDenseFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, approximate):
+        dt = _compute_dtype(x)
+        with torch.autocast("cuda", enabled=False):
+            xc = _cast(x, dt)
+            w1c, b1c, w2c, b2c = _cast(w1, dt), _cast(b1, dt), _cast(w2, dt), _cast(b2, dt)
+            x2 = xc.reshape(-1, xc.size(-1))
+            pre = torch.addmm(b1c, x2, w1c.t()) if b1c is not None else x2 @ w1c.t()
+            h = F.gelu(pre, approximate=approximate)
+            y = torch.addmm(b2c, h, w2c.t()) if b2c is not None else h @ w2c.t()
+        ctx.save_for_backward(xc, w1c, pre, h, w2c)
+        ctx.b1_dtype = b1.dtype if b1 is not None else None
+        ctx.b2_dtype = b2.dtype if b2 is not None else None
+        ctx.tanh = approximate == "tanh"
+        return y.view(*x.shape[:-1], w2.size(0))
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w1c, pre, h, w2c = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.size(-1)).contiguous()
+        if dy2.dtype != w2c.dtype:
+            dy2 = dy2.to(w2c.dtype)
+        need = ctx.needs_input_grad
+        dw2 = dy2.t() @ h if need[3] else None
+        db2 = _bias_grad(dy2, ctx.b2_dtype) if ctx.b2_dtype is not None and need[4] else None
+        dh = dy2 @ w2c
+        if dh.is_cuda and _native.available():
+            dpre, db1 = _native.require().dense.gelu_bwd_bias_grad(
+                dh, pre, ctx.tanh, ctx.b1_dtype or dh.dtype)
+        else:
+            with torch.enable_grad():
+                p = pre.detach().float().requires_grad_(True)
+                g, = torch.autograd.grad(F.gelu(p, approximate="tanh" if ctx.tanh else "none"),
+                                         p, dh.float())
+            dpre = g.to(dh.dtype)
+            db1 = dpre.float().sum(0).to(ctx.b1_dtype or dh.dtype)
+        dx = (dpre @ w1c).view(xc.shape) if need[0] else None
+        dw1 = dpre.t() @ xc.reshape(-1, xc.size(-1)) if need[1] else None
+        if ctx.b1_dtype is None or not need[2]:
+            db1 = None
+        return dx, dw1, db1, dw2, db2, None
+
+
+def fused_dense_function(x, weight, bias):
+    return FusedDenseFunc.apply(x, weight, bias)
+
+
+def dense_no_bias_function(x, weight):
+    return FusedDenseFunc.apply(x, weight, None)
+
+
+def fused_dense_gelu_dense_function(x, w1, b1, w2, b2, approximate="none"):
+    return FusedDenseGeluDenseFunc.apply(x, w1, b1, w2, b2, approximate)
+
+
+class FusedDense(nn.Linear):
+    """nn.Linear with the fused backward (same parameters / state dict)."""
+
+    def forward(self, x):
+        return fused_dense_function(x, self.weight, self.bias)
+
+
+class DenseNoBias(nn.Linear):
+    def __init__(self, in_features, out_features, device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=False, device=device, dtype=dtype)
+
+    def forward(self, x):
+        return dense_no_bias_function(x, self.weight)
+
+
+class FusedDenseGeluDense(nn.Module):
+    """Linear -> GELU -> Linear (apex naming: weight1/bias1/weight2/bias2)."""
+
+    def __init__(self, in_features, intermediate_features, out_features, bias=True,
+                 approximate="none"):
+        super().__init__()
+        self.in_features, self.intermediate_features = in_features, intermediate_features
+        self.out_features, self.approximate = out_features, approximate
+        l1 = nn.Linear(in_features, intermediate_features, bias=bias)
+        l2 = nn.Linear(intermediate_features, out_features, bias=bias)
+        self.weight1, self.bias1 = l1.weight, l1.bias
+        self.weight2, self.bias2 = l2.weight, l2.bias
+
+    def forward(self, x):
+        return fused_dense_gelu_dense_function(x, self.weight1, self.bias1, self.weight2,
+                                               self.bias2, self.approximate)

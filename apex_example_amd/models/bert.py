@@ -19,6 +19,7 @@ import torch.nn.functional as F
 
 from .. import _native
 from ..normalization import FusedLayerNorm
+from ..fused_dense import fused_dense_function, fused_dense_gelu_dense_function
 from ..ops import attention as fused_attn
 
 
@@ -37,6 +38,7 @@ class BertConfig:
     layer_norm_eps: float = 1e-12
     fused_layer_norm: bool = True
     fused_attention: bool = True
+    fused_dense: bool = True  # fused bias-grad / GELU-backward dense layers (fused_dense)
 
 
 def _ln(cfg, n):
@@ -71,19 +73,23 @@ class BertSelfAttention(nn.Module):
         self.dense = nn.Linear(cfg.hidden_size, cfg.hidden_size)
         self.p = cfg.attention_probs_dropout_prob
         self.fused = cfg.fused_attention
+        self.fused_dense = cfg.fused_dense
+
+    def _lin(self, m, x):
+        return fused_dense_function(x, m.weight, m.bias) if self.fused_dense else m(x)
 
     def forward(self, x, attn_mask=None):
         b, s, hd = x.shape
-        qkv = self.qkv(x).view(b, s, 3, self.h, self.d)
+        qkv = self._lin(self.qkv, x).view(b, s, 3, self.h, self.d)
         p = self.p if self.training else 0.0
         if self.fused and attn_mask is None and fused_attn.supported(qkv, self.d):
             o = fused_attn.fused_attention_qkv(qkv, causal=False, dropout_p=p)
-            return self.dense(o.view(b, s, hd))
+            return self._lin(self.dense, o.view(b, s, hd))
         qkv = qkv.permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=p)
         o = o.transpose(1, 2).reshape(b, s, hd)
-        return self.dense(o)
+        return self._lin(self.dense, o)
 
 
 class BertLayer(nn.Module):
@@ -96,11 +102,17 @@ class BertLayer(nn.Module):
         self.output = nn.Linear(cfg.intermediate_size, cfg.hidden_size)
         self.out_dropout = nn.Dropout(cfg.hidden_dropout_prob)
         self.out_ln = _ln(cfg, cfg.hidden_size)
+        self.fused_dense = cfg.fused_dense
 
     def forward(self, x, attn_mask=None):
         x = self.attn_ln(x + self.attn_dropout(self.attention(x, attn_mask)))
-        h = F.gelu(self.intermediate(x))
-        return self.out_ln(x + self.out_dropout(self.output(h)))
+        if self.fused_dense:
+            f = fused_dense_gelu_dense_function(x, self.intermediate.weight,
+                                                self.intermediate.bias, self.output.weight,
+                                                self.output.bias)
+        else:
+            f = self.output(F.gelu(self.intermediate(x)))
+        return self.out_ln(x + self.out_dropout(f))
 
 
 class BertModel(nn.Module):

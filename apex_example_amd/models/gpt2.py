@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from .. import _native
 from ..normalization import FusedLayerNorm
+from ..fused_dense import fused_dense_function, fused_dense_gelu_dense_function
 from ..ops import attention as fused_attn
 
 
@@ -33,6 +34,7 @@ class GPT2Config:
     initializer_range: float = 0.02
     fused_layer_norm: bool = True
     fused_attention: bool = True
+    fused_dense: bool = True  # fused bias-grad / GELU-backward dense layers (fused_dense)
 
 
 def _ln(cfg, n):
@@ -51,18 +53,22 @@ class GPT2Attention(nn.Module):
         self.p = cfg.attn_pdrop
         self.resid_dropout = nn.Dropout(cfg.resid_pdrop)
         self.fused = cfg.fused_attention
+        self.fused_dense = cfg.fused_dense
+
+    def _lin(self, m, x):
+        return fused_dense_function(x, m.weight, m.bias) if self.fused_dense else m(x)
 
     def forward(self, x):
         b, s, e = x.shape
-        qkv = self.c_attn(x).view(b, s, 3, self.h, self.d)
+        qkv = self._lin(self.c_attn, x).view(b, s, 3, self.h, self.d)
         p = self.p if self.training else 0.0
         if self.fused and fused_attn.supported(qkv, self.d):
             o = fused_attn.fused_attention_qkv(qkv, causal=True, dropout_p=p).view(b, s, e)
-            return self.resid_dropout(self.c_proj(o))
+            return self.resid_dropout(self._lin(self.c_proj, o))
         qkv = qkv.permute(2, 0, 3, 1, 4)
         o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], is_causal=True, dropout_p=p)
         o = o.transpose(1, 2).reshape(b, s, e)
-        return self.resid_dropout(self.c_proj(o))
+        return self.resid_dropout(self._lin(self.c_proj, o))
 
 
 class GPT2MLP(nn.Module):
@@ -71,8 +77,13 @@ class GPT2MLP(nn.Module):
         self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
         self.dropout = nn.Dropout(cfg.resid_pdrop)
+        self.fused_dense = cfg.fused_dense
 
     def forward(self, x):
+        if self.fused_dense:
+            return self.dropout(fused_dense_gelu_dense_function(
+                x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias,
+                "tanh"))
         return self.dropout(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
 
 

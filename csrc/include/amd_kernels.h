@@ -233,6 +233,14 @@ int stem_wgrad_splits(int N, int H);
 void stem_wgrad(const void* xp, const void* dy, float* part, int S, int N, int H, int W,
                 hipStream_t st);
 
+// ---- dense-layer bias gradients (bias_grad.hip) ------------------------------
+// bias_grad[n] = sum_m g[m, n] for a row-major 16-bit [M, N] (N % 8 == 0, 16-byte
+// aligned); gelu_mode 1 / 2: g = dh * gelu'(pre) (erf / tanh GELU) is computed in
+// the same pass and written to out_dpre.  part: S * N floats (S = colsum_splits).
+int colsum_splits(int64_t M, int N);
+void colsum(const void* x, const void* pre, void* out_dpre, DType t, int64_t M, int N,
+            int gelu_mode, float* part, int S, void* bias_grad, DType tb, hipStream_t st);
+
 // ---- fused attention, head dim 64 (attention.hip) ---------------------------
 struct AttnLaunch {
   const void* q;

@@ -1,0 +1,67 @@
+// Dense-layer bias gradients on the column-sum kernels (csrc/hip/bias_grad.hip);
+// CPU / unsupported layouts use the ATen reference.
+#include "dense_ops.h"
+
+#include "common.h"
+
+namespace amd {
+
+namespace {
+
+bool colsum_ok(const at::Tensor& t) {
+  return t.is_cuda() && t.is_contiguous() && t.dim() >= 1 &&
+         (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf) &&
+         t.size(-1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 &&
+         t.numel() > 0;
+}
+
+at::Tensor gelu_grad_ref(const at::Tensor& pre, bool tanh_approx) {
+  at::Tensor x = pre.to(at::kFloat);
+  if (tanh_approx) {
+    const double k0 = 0.7978845608028654, k1 = 0.044715;
+    at::Tensor t = at::tanh(k0 * (x + k1 * x * x * x));
+    return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x);
+  }
+  return 0.5 * (1 + at::erf(x * 0.7071067811865476)) +
+         x * at::exp(-0.5 * x * x) * 0.3989422804014327;
+}
+
+}  // namespace
+
+at::Tensor bias_grad_op(at::Tensor g, at::ScalarType out_dtype) {
+  c10::NoGradGuard no_grad_;
+  const int64_t N = g.size(-1);
+  if (!colsum_ok(g)) return g.reshape({-1, N}).to(at::kFloat).sum(0).to(out_dtype);
+  const int64_t M = g.numel() / N;
+  const int S = colsum_splits(M, (int)N);
+  at::Tensor part = at::empty({(int64_t)S * N}, g.options().dtype(at::kFloat));
+  at::Tensor out = at::empty({N}, g.options().dtype(out_dtype));
+  colsum(g.data_ptr(), nullptr, nullptr, dtype_of(g), M, (int)N, 0, part.data_ptr<float>(), S,
+         out.data_ptr(), dtype_of(out), cur_stream());
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> gelu_bwd_bias_grad_op(at::Tensor dh, at::Tensor pre,
+                                                         bool tanh_approx,
+                                                         at::ScalarType out_dtype) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(dh.sizes() == pre.sizes(), "gelu_bwd_bias_grad: shape mismatch");
+  const int64_t N = dh.size(-1);
+  dh = dh.contiguous();
+  pre = pre.contiguous();
+  if (!colsum_ok(dh) || !colsum_ok(pre) || dh.scalar_type() != pre.scalar_type()) {
+    at::Tensor dpre = (dh.to(at::kFloat) * gelu_grad_ref(pre, tanh_approx)).to(dh.scalar_type());
+    return {dpre, dpre.reshape({-1, N}).to(at::kFloat).sum(0).to(out_dtype)};
+  }
+  const int64_t M = dh.numel() / N;
+  const int S = colsum_splits(M, (int)N);
+  at::Tensor part = at::empty({(int64_t)S * N}, dh.options().dtype(at::kFloat));
+  at::Tensor dpre = at::empty_like(dh);
+  at::Tensor out = at::empty({N}, dh.options().dtype(out_dtype));
+  colsum(dh.data_ptr(), pre.data_ptr(), dpre.data_ptr(), dtype_of(dh), M, (int)N,
+         tanh_approx ? 2 : 1, part.data_ptr<float>(), S, out.data_ptr(), dtype_of(out),
+         cur_stream());
+  return {dpre, out};
+}
+
+}  // namespace amd

@@ -1,0 +1,16 @@
+// Dense-layer helper operators (bias gradients, fused GELU backward).
+#pragma once
+#include <torch/extension.h>
+
+#include <tuple>
+
+namespace amd {
+
+// sum over rows of a [M, N] tensor (any leading dims) -> [N] in out_dtype
+at::Tensor bias_grad_op(at::Tensor g, at::ScalarType out_dtype);
+// (dpre = dh * gelu'(pre), sum over rows of dpre); approximate: "none" | "tanh"
+std::tuple<at::Tensor, at::Tensor> gelu_bwd_bias_grad_op(at::Tensor dh, at::Tensor pre,
+                                                         bool tanh_approx,
+                                                         at::ScalarType out_dtype);
+
+}  // namespace amd

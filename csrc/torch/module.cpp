@@ -10,6 +10,7 @@
 #include "attn_ops.h"
 #include "norm_ops.h"
 #include "pool_ops.h"
+#include "dense_ops.h"
 #include "xent_ops.h"
 #include "reducer.h"
 
@@ -75,6 +76,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   attn.def("fwd", &attn_fwd_op);
   attn.def("bwd", &attn_bwd_op);
 
+  auto dn = m.def_submodule("dense", "dense-layer bias gradients / fused GELU backward");
+  dn.def("bias_grad", &bias_grad_op);
+  dn.def("gelu_bwd_bias_grad", &gelu_bwd_bias_grad_op);
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);

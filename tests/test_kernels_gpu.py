@@ -591,3 +591,29 @@ def test_stem_conv_mfma(shape):
     yr.backward(dy)
     ws = wr.grad.abs().max().item()
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=1e-2 * ws)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mn", [(16384, 1024), (333, 4096), (7, 24), (1025, 3072)])
+def test_bias_grad_kernels(dt, mn):
+    """Column-sum bias gradient and fused GELU-backward + bias gradient kernels
+    (csrc/hip/bias_grad.hip) vs fp32 references."""
+    from apex_example_amd import _native
+
+    d = _native.require().dense
+    m, n = mn
+    torch.manual_seed(5)
+    g = torch.randn(m, n, device=DEV, dtype=dt)
+    ref = g.float().sum(0)
+    torch.testing.assert_close(d.bias_grad(g, torch.float32), ref, rtol=1e-4,
+                               atol=1e-4 * max(1.0, m ** 0.5))
+    torch.testing.assert_close(d.bias_grad(g, dt).float(), ref, rtol=1e-2, atol=0.05 * m ** 0.5)
+    pre = torch.randn(m, n, device=DEV, dtype=dt) * 2
+    for tanh in (False, True):
+        dpre, db = d.gelu_bwd_bias_grad(g, pre, tanh, torch.float32)
+        p = pre.float().requires_grad_(True)
+        r, = torch.autograd.grad(F.gelu(p, approximate="tanh" if tanh else "none"), p, g.float())
+        torch.testing.assert_close(dpre.float(), r, rtol=2e-2, atol=2e-2)
+        # the kernel sums the fp32 dpre (before its bf16 rounding): compare with the
+        # fp32 reference's column sums
+        torch.testing.assert_close(db, r.sum(0), rtol=1e-3, atol=1e-3 * max(1.0, m ** 0.5))

@@ -1,0 +1,4 @@
+set -e
+cd /root/repo
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+echo ok
