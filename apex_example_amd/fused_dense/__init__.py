@@ -35,6 +35,14 @@ def _cast(t, dt):
     return t if t is None or t.dtype == dt else t.to(dt)
 
 
+def _wgrad(dy2, x2, dtype):
+    """dW = dy2^T x2 written in the parameter's dtype by the GEMM itself (amp O1:
+    fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW)."""
+    if dtype != dy2.dtype and dy2.is_cuda and dtype == torch.float32:
+        return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+    return dy2.t() @ x2
+
+
 def _bias_grad(g2, dtype):
     if g2.is_cuda and _native.available():
         return _native.require().dense.bias_grad(g2, dtype)
@@ -51,6 +59,7 @@ class FusedDenseFunc(torch.autograd.Function):
             y = torch.addmm(bc, x2, wc.t()) if bc is not None else x2 @ wc.t()
         ctx.save_for_backward(xc, wc)
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.w_dtype = weight.dtype
         return y.view(*x.shape[:-1], weight.size(0))
 
     @staticmethod
@@ -63,7 +72,7 @@ class FusedDenseFunc(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ wc).view(xc.shape)
         if ctx.needs_input_grad[1]:
-            dw = dy2.t() @ xc.reshape(-1, xc.size(-1))
+            dw = _wgrad(dy2, xc.reshape(-1, xc.size(-1)), ctx.w_dtype)
         if ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
             db = _bias_grad(dy2, ctx.bias_dtype)
         return dx, dw, db
@@ -84,6 +93,7 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
         ctx.b1_dtype = b1.dtype if b1 is not None else None
         ctx.b2_dtype = b2.dtype if b2 is not None else None
         ctx.tanh = approximate == "tanh"
+        ctx.w_dtypes = (w1.dtype, w2.dtype)
         return y.view(*x.shape[:-1], w2.size(0))
 
     @staticmethod
@@ -93,7 +103,7 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
         if dy2.dtype != w2c.dtype:
             dy2 = dy2.to(w2c.dtype)
         need = ctx.needs_input_grad
-        dw2 = dy2.t() @ h if need[3] else None
+        dw2 = _wgrad(dy2, h, ctx.w_dtypes[1]) if need[3] else None
         db2 = _bias_grad(dy2, ctx.b2_dtype) if ctx.b2_dtype is not None and need[4] else None
         dh = dy2 @ w2c
         if dh.is_cuda and _native.available():
@@ -107,7 +117,7 @@ class FusedDenseGeluDenseFunc(torch.autograd.Function):
             dpre = g.to(dh.dtype)
             db1 = dpre.float().sum(0).to(ctx.b1_dtype or dh.dtype)
         dx = (dpre @ w1c).view(xc.shape) if need[0] else None
-        dw1 = dpre.t() @ xc.reshape(-1, xc.size(-1)) if need[1] else None
+        dw1 = _wgrad(dpre, xc.reshape(-1, xc.size(-1)), ctx.w_dtypes[0]) if need[1] else None
         if ctx.b1_dtype is None or not need[2]:
             db1 = None
         return dx, dw1, db1, dw2, db2, None

@@ -79,6 +79,31 @@ class BatchNormFunction(torch.autograd.Function):
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
                 shape_channel_last
             return y.view(orig_shape) if shape_channel_last else y
+        if world > 1 and xl.is_cuda:
+            # SyncBN: the stats kernels write [mean | var | count] into one buffer -> ONE
+            # all_gather -> one combine kernel (global mean / invstd, running stats,
+            # num_batches_tracked, 1/global count) -> apply.  No host sync, no cat.
+            pg = process_group if process_group is not None else dist.group.WORLD
+            packed = C.local_stats_packed(xl)
+            gathered = torch.empty(world * packed.numel(), dtype=packed.dtype, device=x.device)
+            if dist.get_backend(pg) == "nccl":
+                dist.all_gather_into_tensor(gathered, packed, group=pg)
+            else:  # gloo with GPU tensors (tests): list form into views of `gathered`
+                dist.all_gather(list(gathered.chunk(world)), packed, group=pg)
+            mean_g, invstd, inv_total = C.combine_stats_sync(
+                gathered.view(world, -1), float(eps), float(momentum), running_mean, running_var,
+                num_batches_tracked)
+            if want_mask:
+                y, mask = C.apply_mask(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu))
+            else:
+                y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
+            ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd,
+                                  mask)
+            ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = pg, world, \
+                bool(fuse_relu), inv_total, count
+            ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
+                shape_channel_last
+            return y.view(orig_shape) if shape_channel_last else y
         if num_batches_tracked is not None:
             num_batches_tracked.add_(1)
         mean, var = C.local_stats(xl)
@@ -120,6 +145,24 @@ class BatchNormFunction(torch.autograd.Function):
         xl, zl, weight, bias, mean, invstd, mask = ctx.saved_tensors
         dyl = _to_logical(dy, ctx.shape_channel_last)
         need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        if ctx.world > 1 and xl.is_cuda:
+            # SyncBN: the reduce writes (sum_dy | sum_dy_xmu) / global_count into one [2C]
+            # buffer (the scale is a device scalar from the forward's combine) -> ONE
+            # in-place all_reduce yields the global means -> elementwise pass
+            sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
+                                                       ctx.fuse_relu, need_w, mask=mask,
+                                                       sum_scale=ctx.total)
+            n = sum_dy.numel()
+            packed = sum_dy.as_strided((2 * n,), (1,))  # sum_dy_xmu follows sum_dy in memory
+            dist.all_reduce(packed, group=ctx.pg)
+            dx, dz = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
+                                      1.0, zl, ctx.fuse_relu, ctx.has_z, mask=mask)
+            if ctx.shape_channel_last:
+                dx = dx.view(ctx.orig_shape)
+                if dz is not None:
+                    dz = dz.view(ctx.orig_shape)
+            return (dx, dz if ctx.has_z else None, gw if need_w else None,
+                    gb if need_w else None, None, None, None, None, None, None, None, None)
         sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
                                                    ctx.fuse_relu, need_w, mask=mask)
         if ctx.world > 1:

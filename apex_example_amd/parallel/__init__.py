@@ -32,7 +32,6 @@ def convert_syncbn_model(module, process_group=None, channel_last=False):
     for name, child in module.named_children():
         mod.add_module(name, convert_syncbn_model(child, process_group=process_group,
                                                   channel_last=channel_last))
-    # TODO(jie) should I delete model explicitly?
     del module
     return mod
 

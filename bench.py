@@ -62,7 +62,10 @@ def parse():
                     help="transformers: torch cross entropy on fp32 logits instead of the fused kernel")
     ap.add_argument("--no-fused-attn", action="store_true",
                     help="transformers: PyTorch SDPA instead of the gfx950 attention kernels")
-    ap.add_argument("--syncbn", action="store_true", help="SyncBatchNorm across ranks")
+    ap.add_argument("--syncbn", action="store_true",
+                    help="SyncBatchNorm across ranks (the default for ResNet at N > 1)")
+    ap.add_argument("--no-syncbn", action="store_true",
+                    help="per-GPU BatchNorm statistics at N > 1 (not the BASELINE config)")
     ap.add_argument("--message-size", type=int, default=10_000_000, help="DDP bucket elements")
     ap.add_argument("--materialize-master-grads", action="store_true")
     ap.add_argument("--no-gemm-1x1", action="store_true",
@@ -103,7 +106,9 @@ def build_resnet(args, device, world):
     fused_bn = args.impl == "amd" and not args.no_fused_bn
     gemm_1x1 = args.impl == "amd" and not args.no_gemm_1x1
     model = ctor(fused_bn=fused_bn, gemm_1x1=gemm_1x1).to(device)
-    if args.syncbn and world > 1:
+    # BASELINE.json's multi-GPU ResNet-50 config is DDP + SyncBN: on by default at N > 1
+    args.syncbn = world > 1 and not args.no_syncbn
+    if args.syncbn:
         if args.impl == "amd":
             model = convert_syncbn_model(model)
         else:

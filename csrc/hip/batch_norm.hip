@@ -96,9 +96,18 @@ __global__ void __launch_bounds__(256)
                    const float* __restrict__ counts, int world, int C, float eps, float momentum,
                    float* __restrict__ mean_out, float* __restrict__ invstd_out,
                    float* __restrict__ running_mean, TR* __restrict__ running_var,
-                   float* __restrict__ var_out) {
+                   float* __restrict__ var_out, long long* __restrict__ nbt,
+                   float* __restrict__ inv_total) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  if (c == 0) {
+    if (nbt) *nbt += 1;
+    if (inv_total) {
+      float t = 0.f;
+      for (int w = 0; w < world; ++w) t += counts[w];
+      *inv_total = 1.f / t;
+    }
+  }
   float mean = 0.f, m2 = 0.f, n = 0.f;
   for (int w = 0; w < world; ++w) {
     float nb = counts[w];
@@ -298,8 +307,11 @@ static void local_stats_impl(const void* x, DType tx, int64_t outer, int64_t C, 
 }
 
 void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
-                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st) {
+                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st,
+                    float* count_out) {
   BNStatsOut out{mean, var_biased, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f};
+  out.count_out = count_out;
+  out.count_val = (float)(outer * inner);
   local_stats_impl(x, tx, outer, C, inner, channel_last, out, ws, st);
 }
 
@@ -314,11 +326,11 @@ void bn_local_train_stats(const void* x, DType tx, int64_t outer, int64_t C, int
 void bn_combine_stats(const float* means, const float* vars, const float* counts, int world,
                       int64_t C, float eps, float momentum, float* mean_out, float* invstd_out,
                       float* running_mean, DType trm, void* running_var_any, float* var_out,
-                      hipStream_t st) {
+                      hipStream_t st, long long* nbt, float* inv_total) {
   (void)trm;
   hipLaunchKernelGGL((combine_kernel<float>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st,
                      means, vars, counts, world, (int)C, eps, momentum, mean_out, invstd_out,
-                     running_mean, static_cast<float*>(running_var_any), var_out);
+                     running_mean, static_cast<float*>(running_var_any), var_out, nbt, inv_total);
 }
 
 void bn_apply(const void* x, DType tx, const float* mean, const float* invstd,
@@ -346,11 +358,12 @@ void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                     const float* invstd, const void* weight, const void* bias, DType tw,
                     int relu, const void* z, const uint8_t* relu_mask, int64_t outer, int64_t C,
                     int64_t inner, int channel_last, float* sum_dy, float* sum_dy_xmu,
-                    void* grad_weight, void* grad_bias, float* ws, hipStream_t st) {
+                    void* grad_weight, void* grad_bias, float* ws, hipStream_t st,
+                    const float* sum_scale) {
   if (outer * inner * C == 0) return;
   if (channel_last)
     return nhwc_reduce(dy, x, tx, mean, invstd, weight, bias, tw, relu, z, relu_mask, outer, C,
-                       sum_dy, sum_dy_xmu, grad_weight, grad_bias, ws, st);
+                       sum_dy, sum_dy_xmu, grad_weight, grad_bias, ws, st, sum_scale);
   const int splits = nchw_splits(outer, C, inner);
   const int vec = nchw_vec(inner, {dy, x, z}) ? 1 : 0;
   bn_dispatch(tx, [&](auto t0) {
@@ -362,7 +375,7 @@ void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                          static_cast<const TW*>(weight), static_cast<const TW*>(bias),
                          static_cast<const T*>(z), relu, outer, (int)C, inner, vec, ws);
       launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(grad_weight),
-                         static_cast<TW*>(grad_bias), st);
+                         static_cast<TW*>(grad_bias), st, sum_scale);
     });
   });
 }

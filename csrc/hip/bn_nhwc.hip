@@ -399,7 +399,7 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
 void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, const float* invstd,
                  const void* w, const void* b, DType tw, int relu, const void* z,
                  const uint8_t* rmask, int64_t M, int64_t C, float* sum_dy, float* sum_dy_xmu,
-                 void* gw, void* gb, float* ws, hipStream_t st) {
+                 void* gw, void* gb, float* ws, hipStream_t st, const float* sum_scale) {
   const bool vec = (C % 8 == 0) && all_aligned({dy, x, z});
   const NGeom g = ngeom(C, vec);
   const int splits = reduce_splits(M, g);
@@ -415,7 +415,7 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
                            (int)C, g.ctile, g.rows_iter, ws);
       });
       launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
-                         static_cast<TW*>(gb), st);
+                         static_cast<TW*>(gb), st, sum_scale);
     });
   });
 }

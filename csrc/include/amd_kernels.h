@@ -154,8 +154,10 @@ int64_t bn_stats_workspace(int64_t outer, int64_t C, int64_t inner, int channel_
 // NHWC BN grid-sizing knobs (-1 keeps a value); get returns the 6 current values
 void bn_set_tuning(int red_rpt, int red_cap, int red_min, int elem_rpt, int elem_cap, int elem_min);
 void bn_get_tuning(int* out6);
+// count_out (optional): receives the element count per channel (SyncBN packed stats)
 void bn_local_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
-                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st);
+                    int channel_last, float* mean, float* var_biased, float* ws, hipStream_t st,
+                    float* count_out = nullptr);
 // local (single-GPU) training stats: mean, invstd, running-stat update and
 // num_batches_tracked += 1 in the finalize kernel
 void bn_local_train_stats(const void* x, DType tx, int64_t outer, int64_t C, int64_t inner,
@@ -167,7 +169,7 @@ void bn_local_train_stats(const void* x, DType tx, int64_t outer, int64_t C, int
 void bn_combine_stats(const float* means, const float* vars, const float* counts, int world,
                       int64_t C, float eps, float momentum, float* mean_out, float* invstd_out,
                       float* running_mean, DType trm, void* running_var_any, float* var_out,
-                      hipStream_t st);
+                      hipStream_t st, long long* nbt = nullptr, float* inv_total = nullptr);
 // y = (x - mean) * invstd * w + b  [+ z] [relu]; relu_mask (channel-last, C % 8 == 0,
 // 16-B aligned x/z/y; else ignored) receives one bit per element: output > 0
 void bn_apply(const void* x, DType tx, const float* mean, const float* invstd,
@@ -182,7 +184,8 @@ void bn_reduce_grad(const void* dy, const void* x, DType tx, const float* mean,
                     int relu, const void* z, const uint8_t* relu_mask, int64_t outer, int64_t C,
                     int64_t inner,
                     int channel_last, float* sum_dy, float* sum_dy_xmu, void* grad_weight,
-                    void* grad_bias, float* ws, hipStream_t st);
+                    void* grad_bias, float* ws, hipStream_t st,
+                    const float* sum_scale = nullptr);
 // dx = (dy' - mean_dy - (x-mean)*invstd^2*mean_dy_xmu) * invstd * w ; dz = dy' if z
 void bn_backward_elemt(const void* dy, const void* x, DType tx, const float* mean,
                        const float* invstd, const void* weight, const void* bias, DType tw,

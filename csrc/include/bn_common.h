@@ -88,6 +88,8 @@ struct BNStatsOut {
   float* running_var;     // optional (fp32)
   long long* nbt;         // optional num_batches_tracked (int64)
   float eps, momentum;
+  float* count_out = nullptr;  // optional: receives count_val (SyncBN packed stats)
+  float count_val = 0.f;
 };
 
 // slab of shifted sums -> statistics; the shift is re-read from x
@@ -115,6 +117,7 @@ __global__ void __launch_bounds__(kBNThreads)
       out.running_var[c] = (1.f - out.momentum) * out.running_var[c] + out.momentum * (float)unb;
     }
     if (out.nbt && c == 0) *out.nbt += 1;
+    if (out.count_out && c == 0) *out.count_out = out.count_val;
   }
 }
 
@@ -123,7 +126,8 @@ template <typename TW, int CH>
 __global__ void __launch_bounds__(kBNThreads)
     reduce_finalize(const float* __restrict__ slab, int splits, int C,
                     const float* __restrict__ invstd, float* __restrict__ sum_dy,
-                    float* __restrict__ sum_dy_xmu, TW* __restrict__ gw, TW* __restrict__ gb) {
+                    float* __restrict__ sum_dy_xmu, TW* __restrict__ gw, TW* __restrict__ gb,
+                    const float* __restrict__ sum_scale) {
   __shared__ float sums[2 * CH];
   const int c0 = blockIdx.x * CH;
   slab_sum<CH>(slab, splits, C, c0, sums);
@@ -131,8 +135,11 @@ __global__ void __launch_bounds__(kBNThreads)
   if (k < CH && c0 + k < C) {
     const int c = c0 + k;
     const float s1 = sums[k], s2 = sums[CH + k];
-    sum_dy[c] = s1;
-    sum_dy_xmu[c] = s2;
+    // SyncBN: the sums leave pre-divided by the global count (device scalar), so the
+    // all_reduce of them yields the means directly; dgamma / dbeta stay local sums
+    const float sc = sum_scale ? *sum_scale : 1.f;
+    sum_dy[c] = s1 * sc;
+    sum_dy_xmu[c] = s2 * sc;
     if (gw) gw[c] = from_f32<TW>(s2 * invstd[c]);
     if (gb) gb[c] = from_f32<TW>(s1);
   }
@@ -166,12 +173,13 @@ static inline void launch_stats_finalize(const T* x, const float* slab, int spli
 template <typename TW>
 static inline void launch_reduce_finalize(const float* slab, int splits, int64_t C,
                                           const float* invstd, float* sum_dy, float* sum_dy_xmu,
-                                          TW* gw, TW* gb, hipStream_t st) {
+                                          TW* gw, TW* gb, hipStream_t st,
+                                          const float* sum_scale = nullptr) {
   fin_dispatch(C, [&](auto ch) {
     constexpr int CH = decltype(ch)::value;
     hipLaunchKernelGGL((reduce_finalize<TW, CH>), dim3((unsigned)((C + CH - 1) / CH)),
                        dim3(kBNThreads), 0, st, slab, splits, (int)C, invstd, sum_dy, sum_dy_xmu,
-                       gw, gb);
+                       gw, gb, sum_scale);
   });
 }
 
@@ -196,7 +204,7 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
 void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, const float* invstd,
                  const void* w, const void* b, DType tw, int relu, const void* z,
                  const uint8_t* rmask, int64_t M, int64_t C, float* sum_dy, float* sum_dy_xmu,
-                 void* gw, void* gb, float* ws, hipStream_t st);
+                 void* gw, void* gb, float* ws, hipStream_t st, const float* sum_scale = nullptr);
 void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
                    const float* invstd, const void* w, const void* b, DType tw,
                    const float* sum_dy, const float* sum_dy_xmu, float inv_count, int relu,

@@ -116,7 +116,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   bn.def("reduce_grad", &bn_reduce_grad_op, py::arg("dy"), py::arg("x"), py::arg("mean"),
          py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("z"), py::arg("relu"),
-         py::arg("need_wgrad"), py::arg("mask") = py::none());
+         py::arg("need_wgrad"), py::arg("mask") = py::none(),
+         py::arg("sum_scale") = py::none());
+  bn.def("local_stats_packed", &bn_local_stats_packed_op);
+  bn.def("combine_stats_sync", &bn_combine_stats_sync_op, py::arg("gathered"), py::arg("eps"),
+         py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"),
+         py::arg("nbt") = py::none());
   bn.def("backward_elemt", &bn_backward_elemt_op, py::arg("dy"), py::arg("x"), py::arg("mean"),
          py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("sum_dy"),
          py::arg("sum_dy_xmu"), py::arg("count"), py::arg("z"), py::arg("relu"),

@@ -206,6 +206,66 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
   return {mean, invstd, var};
 }
 
+// SyncBN forward, local part: [mean(C) | var(C) | count] in ONE buffer written by the
+// stats kernels (the count by the finalize kernel), ready for the all_gather
+at::Tensor bn_local_stats_packed_op(at::Tensor x) {
+  c10::NoGradGuard no_grad_;
+  BNView v = bn_view(x);
+  if (!x.is_cuda()) {
+    auto st = bn_local_stats_op(x);
+    return at::cat({std::get<0>(st), std::get<1>(st),
+                    at::full({1}, (double)(v.outer * v.inner), std::get<0>(st).options())});
+  }
+  x = conform(x, v);
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor packed = at::empty({2 * v.C + 1}, fopt);
+  at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
+  float* p = packed.data_ptr<float>();
+  bn_local_stats(x.data_ptr(), dtype_of(x), v.outer, v.C, v.inner, v.cl, p, p + v.C,
+                 ws.data_ptr<float>(), cur_stream(), p + 2 * v.C);
+  return packed;
+}
+
+// SyncBN forward, global part: combine the gathered [world, 2C+1] stats; running stats,
+// num_batches_tracked and 1/global-count (for the backward) in the same kernel
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_sync_op(
+    at::Tensor gathered, double eps, double momentum, OptT running_mean, OptT running_var,
+    OptT nbt) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(gathered.dim() == 2 && (gathered.size(1) - 1) % 2 == 0,
+              "combine_stats_sync: [world, 2C+1] expected");
+  const int64_t world = gathered.size(0), C = (gathered.size(1) - 1) / 2;
+  gathered = gathered.contiguous().to(at::kFloat);
+  const bool rs = has(running_mean) && has(running_var);
+  const bool fast = gathered.is_cuda() &&
+                    (!rs || (running_mean->scalar_type() == at::kFloat &&
+                             running_var->scalar_type() == at::kFloat &&
+                             running_mean->is_contiguous() && running_var->is_contiguous())) &&
+                    (!has(nbt) || nbt->scalar_type() == at::kLong);
+  if (!fast) {
+    at::Tensor means = gathered.narrow(1, 0, C), vars = gathered.narrow(1, C, C);
+    at::Tensor counts = gathered.narrow(1, 2 * C, 1).reshape({world});
+    auto cs = bn_combine_stats_op(means, vars, counts, eps, momentum, running_mean, running_var);
+    if (has(nbt)) nbt->add_(1);
+    return {std::get<0>(cs), std::get<1>(cs), counts.sum().reciprocal().reshape({1})};
+  }
+  // the kernel reads means / vars / counts with row stride C: copy to planar once
+  // (world x (2C+1) floats, tiny)
+  at::Tensor means = gathered.narrow(1, 0, C).contiguous();
+  at::Tensor vars = gathered.narrow(1, C, C).contiguous();
+  at::Tensor counts = gathered.narrow(1, 2 * C, 1).contiguous();
+  auto fopt = gathered.options();
+  at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  at::Tensor inv_total = at::empty({1}, fopt);
+  bn_combine_stats(means.data_ptr<float>(), vars.data_ptr<float>(), counts.data_ptr<float>(),
+                   (int)world, C, (float)eps, (float)momentum, mean.data_ptr<float>(),
+                   invstd.data_ptr<float>(), rs ? running_mean->data_ptr<float>() : nullptr,
+                   DType::F32, rs ? running_var->data_ptr() : nullptr, nullptr, cur_stream(),
+                   has(nbt) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr,
+                   inv_total.data_ptr<float>());
+  return {mean, invstd, inv_total};
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
     at::Tensor x, OptT weight, OptT bias, OptT running_mean, OptT running_var, OptT nbt,
     double eps, double momentum, OptT z, bool relu, bool want_mask) {
@@ -293,7 +353,7 @@ std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mea
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-    OptT z, bool relu, bool need_wgrad, OptT mask) {
+    OptT z, bool relu, bool need_wgrad, OptT mask, OptT sum_scale) {
   BNView v = bn_view(x);
   TORCH_CHECK(!has(mask) || x.is_cuda(), "batch norm: ReLU mask is a GPU-path feature");
   if (!x.is_cuda()) {
@@ -310,6 +370,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     if (need_wgrad && has(weight)) {
       gw = (sum_dy_xmu * invstd).to(weight->scalar_type());
       gb = sum_dy.to(weight->scalar_type());
+    }
+    if (has(sum_scale)) {
+      sum_dy = sum_dy * *sum_scale;
+      sum_dy_xmu = sum_dy_xmu * *sum_scale;
     }
     return {sum_dy, sum_dy_xmu, gw, gb};
   }
@@ -328,13 +392,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
   at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
   at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
   at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
+  const float* scale = nullptr;
+  if (has(sum_scale)) {
+    TORCH_CHECK(sum_scale->is_cuda() && sum_scale->scalar_type() == at::kFloat &&
+                    sum_scale->numel() == 1, "reduce_grad: sum_scale must be a 1-element fp32 GPU tensor");
+    scale = sum_scale->data_ptr<float>();
+    // one [2C] buffer (sum_dy | sum_dy_xmu) for SyncBN's all_reduce
+    at::Tensor packed = at::empty({2 * v.C}, fopt);
+    sum_dy = packed.narrow(0, 0, v.C);
+    sum_dy_xmu = packed.narrow(0, v.C, v.C);
+  }
   bn_reduce_grad(dy.data_ptr(), x.data_ptr(), dtype_of(x), mean.data_ptr<float>(),
                  invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
                  b.defined() ? b.data_ptr() : nullptr, tw, relu ? 1 : 0,
                  zc.defined() ? zc.data_ptr() : nullptr, mk, v.outer, v.C, v.inner, v.cl,
                  sum_dy.data_ptr<float>(), sum_dy_xmu.data_ptr<float>(),
                  gw.defined() ? gw.data_ptr() : nullptr, gb.defined() ? gb.data_ptr() : nullptr,
-                 ws.data_ptr<float>(), cur_stream());
+                 ws.data_ptr<float>(), cur_stream(), scale);
   return {sum_dy, sum_dy_xmu, gw, gb};
 }
 

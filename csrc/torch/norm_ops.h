@@ -28,6 +28,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
 // num_batches_tracked += 1 + normalize(+z)(+ReLU).  Returns (y, mean, invstd).
 // want_mask: also return the ReLU bitmask [M, C/8] uint8 (channels-last GPU input
 // with C % 8 == 0 and relu; otherwise the 4th result is undefined / None).
+// SyncBN: packed local stats [mean | var | count] and the combine of the gathered
+// [world, 2C+1] stats -> (mean, invstd, 1/global count)
+at::Tensor bn_local_stats_packed_op(at::Tensor x);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_sync_op(
+    at::Tensor gathered, double eps, double momentum, OptT running_mean, OptT running_var,
+    OptT nbt);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
     at::Tensor x, OptT weight, OptT bias, OptT running_mean, OptT running_var, OptT nbt,
     double eps, double momentum, OptT z, bool relu, bool want_mask);
@@ -39,7 +45,8 @@ std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mea
 // mask: the forward's ReLU bitmask; when given, z is not read.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-    OptT z, bool relu, bool need_wgrad, OptT mask);
+    OptT z, bool relu, bool need_wgrad, OptT mask,
+    OptT sum_scale);
 std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tensor x,
                                                         at::Tensor mean, at::Tensor invstd,
                                                         OptT weight, OptT bias, at::Tensor sum_dy,

@@ -163,6 +163,38 @@ def syncbn_step(rank, world, sizes=(4, 6), channel_last=False, fuse_relu=False, 
             "rv": bn.running_var.clone()}
 
 
+def gpu_syncbn_step(rank, world, sizes=(4, 6), fuse_relu=True):
+    """The GPU SyncBN path (packed stats, one all_gather, device-scaled backward
+    sums, one all_reduce) with two ranks sharing cuda:0 over gloo, channels-last
+    bf16 with residual + ReLU, vs. BN over the concatenated batch in fp32."""
+    from apex_example_amd.parallel import SyncBatchNorm
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    C = 16
+    full = torch.randn(sum(sizes), C, 6, 6) * 2 + 1
+    zfull = torch.randn(sum(sizes), C, 6, 6)
+    off = sum(sizes[:rank])
+    x = full[off:off + sizes[rank]].cuda().to(torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    z = zfull[off:off + sizes[rank]].cuda().to(torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    bn = SyncBatchNorm(C, fuse_relu=fuse_relu).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+        bn.bias.copy_(torch.linspace(-1, 1, C))
+    y = bn(x, z)
+    g = torch.Generator().manual_seed(99)
+    dy_full = torch.randn(sum(sizes), C, 6, 6, generator=g)
+    dy = dy_full[off:off + sizes[rank]].cuda()
+    (y.float() * dy).sum().backward()
+    torch.cuda.synchronize()
+    return {"y": y.detach().float().cpu(), "dx": x.grad.detach().float().cpu(),
+            "dz": z.grad.detach().float().cpu(), "dw": bn.weight.grad.cpu(),
+            "db": bn.bias.grad.cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
+            "nbt": int(bn.num_batches_tracked)}
+
+
 def syncbn_groups(rank, world):
     from apex_example_amd.parallel import create_syncbn_process_group
 
@@ -208,7 +240,7 @@ def ddp_amp_vs_local(rank, world, opt_level="O2", fused=False, iters=3):
     return {"diffs": diffs}
 
 
-def gpu_ddp_resnet(rank, world, steps=4):
+def gpu_ddp_resnet(rank, world, steps=4, syncbn=False):
     """Two ranks sharing cuda:0 over gloo (RCCL refuses two ranks on one GPU): the
     GPU-side DDP path of bench.py - amp O2 bf16, fused BN, GEMM convs, FusedSGD,
     bucket views - must keep replicas identical and match a one-process run on
@@ -216,12 +248,14 @@ def gpu_ddp_resnet(rank, world, steps=4):
     from apex_example_amd import amp
     from apex_example_amd.models import resnet18
     from apex_example_amd.optimizers import FusedSGD
-    from apex_example_amd.parallel import DistributedDataParallel
+    from apex_example_amd.parallel import DistributedDataParallel, convert_syncbn_model
 
     torch.cuda.set_device(0)
     torch.manual_seed(0)
-    m = resnet18(num_classes=10, fused_bn=True, gemm_1x1=True).cuda().to(
-        memory_format=torch.channels_last)
+    m = resnet18(num_classes=10, fused_bn=True, gemm_1x1=True)
+    if syncbn:  # bench.py's N > 1 default
+        m = convert_syncbn_model(m)
+    m = m.cuda().to(memory_format=torch.channels_last)
     opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, materialize_master_grads=False)
     m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
     ddp = DistributedDataParallel(m, message_size=200_000)

@@ -85,10 +85,11 @@ def test_ddp_resnet_amp_step(pg):
     assert losses[-1] < losses[0]
 
 
-def test_two_ranks_one_gpu_gloo(tmp_path):
+@pytest.mark.parametrize("syncbn", [False, True])
+def test_two_ranks_one_gpu_gloo(tmp_path, syncbn):
     """bench.py's N>1 code path (apex DDP over a process group, bucket views, fused
-    kernels) with two processes on the one test GPU."""
-    res = W.run("gpu_ddp_resnet", 2, str(tmp_path))
+    kernels, SyncBN by default) with two processes on the one test GPU."""
+    res = W.run("gpu_ddp_resnet", 2, str(tmp_path), syncbn=syncbn)
     for a, b in zip(res[0]["params"], res[1]["params"]):
         assert torch.equal(a, b)
     assert res[0]["views"] and res[1]["views"]
@@ -103,3 +104,34 @@ def test_distributed_fused_adam_two_ranks_one_gpu(tmp_path):
         assert r["skipped"]          # the injected overflow skipped the step on both ranks
         assert r["step"] == 4        # 5 steps, one skipped
     assert res[0]["losses"][-1] < res[0]["losses"][0]
+
+
+def test_syncbn_gpu_two_ranks_matches_global_batch(tmp_path):
+    """GPU SyncBN (bench.py's N>1 default) == BN + residual + ReLU over the global batch."""
+    sizes = (4, 6)
+    res = W.run("gpu_syncbn_step", 2, str(tmp_path), sizes=sizes)
+    torch.manual_seed(0)
+    C = 16
+    full = torch.randn(sum(sizes), C, 6, 6) * 2 + 1
+    zfull = torch.randn(sum(sizes), C, 6, 6)
+    x = full.to(torch.bfloat16).float().requires_grad_(True)
+    z = zfull.to(torch.bfloat16).float().requires_grad_(True)
+    bn = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+        bn.bias.copy_(torch.linspace(-1, 1, C))
+    y = torch.relu(bn(x) + z)
+    g = torch.Generator().manual_seed(99)
+    dy = torch.randn(sum(sizes), C, 6, 6, generator=g)
+    (y * dy).sum().backward()
+    ys = torch.cat([r["y"] for r in res])
+    torch.testing.assert_close(ys, y.detach(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(torch.cat([r["dx"] for r in res]), x.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(torch.cat([r["dz"] for r in res]), z.grad, rtol=3e-2, atol=3e-2)
+    # dgamma / dbeta are per-rank partial sums (DDP all-reduces them as gradients)
+    torch.testing.assert_close(res[0]["dw"] + res[1]["dw"], bn.weight.grad, rtol=3e-2, atol=5e-2)
+    torch.testing.assert_close(res[0]["db"] + res[1]["db"], bn.bias.grad, rtol=3e-2, atol=5e-2)
+    for r in res:
+        torch.testing.assert_close(r["rm"], bn.running_mean, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(r["rv"], bn.running_var, rtol=2e-2, atol=2e-2)
+        assert r["nbt"] == 1
