@@ -18,7 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
-from ..normalization import FusedLayerNorm
+from ..normalization import FusedLayerNorm, fused_add_dropout_layer_norm
 from ..fused_dense import fused_dense_function, fused_dense_gelu_dense_function
 from ..ops import attention as fused_attn
 
@@ -105,14 +105,16 @@ class BertLayer(nn.Module):
         self.fused_dense = cfg.fused_dense
 
     def forward(self, x, attn_mask=None):
-        x = self.attn_ln(x + self.attn_dropout(self.attention(x, attn_mask)))
+        x, _ = fused_add_dropout_layer_norm(x, self.attention(x, attn_mask), self.attn_ln,
+                                            self.attn_dropout.p, self.training)
         if self.fused_dense:
             f = fused_dense_gelu_dense_function(x, self.intermediate.weight,
                                                 self.intermediate.bias, self.output.weight,
                                                 self.output.bias)
         else:
             f = self.output(F.gelu(self.intermediate(x)))
-        return self.out_ln(x + self.out_dropout(f))
+        return fused_add_dropout_layer_norm(x, f, self.out_ln, self.out_dropout.p,
+                                            self.training)[0]
 
 
 class BertModel(nn.Module):

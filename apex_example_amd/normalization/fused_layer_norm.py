@@ -8,6 +8,7 @@ either works).  CPU tensors run the C++ CPU path of the same extension.
 from __future__ import annotations
 
 import numbers
+import os
 
 import torch
 from torch.nn import init
@@ -85,6 +86,69 @@ class FusedRMSNormAffineFunction(torch.autograd.Function):
                                                 _n2(ctx.normalized_shape), weight_,
                                                 ctx.needs_input_grad[1], False, True)
         return grad_input, grad_weight, None, None
+
+
+def _dropout_seed() -> int:
+    # per-call seed from torch's CPU generator: no device sync, follows torch.manual_seed
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
+class AddDropoutLayerNormFunction(torch.autograd.Function):
+    """(y, s) = (LN(s), s) with s = x + dropout_p(h), one gfx950 kernel each way.
+
+    Forward reads h and x once and writes s and y (the unfused chain - dropout,
+    residual add, LayerNorm - reads/writes ~7.5 activations; this 4).  The keep
+    mask is a counter hash of (seed, element) regenerated in the backward, which
+    returns ds = LN'(dy) + ds_ext (the residual-stream gradient) and dh = dropout'(ds)
+    in the same pass as dgamma/dbeta partials.
+    """
+
+    @staticmethod
+    def forward(ctx, x, h, weight, bias, normalized_shape, eps, p):
+        C = _native.require().layer_norm
+        n2 = _n2(normalized_shape)
+        seed = _dropout_seed() if p > 0.0 else 0
+        y, s, mean, invvar = C.add_dropout_forward(x, h, n2, weight, bias, eps, p, seed)
+        # an unused output (post-LN callers drop s) gets grad None, not a zero fill + read
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(s, weight, mean, invvar)
+        ctx.cfg = (n2, float(p), seed)
+        return y, s
+
+    @staticmethod
+    def backward(ctx, dy, ds_ext):
+        C = _native.require().layer_norm
+        s, weight, mean, invvar = ctx.saved_tensors
+        n2, p, seed = ctx.cfg
+        if dy is None:
+            dy = torch.zeros_like(s)
+        ds, dh, dw, db = C.add_dropout_backward(dy, s, mean, invvar, n2, weight, ds_ext, p, seed,
+                                                ctx.needs_input_grad[2], ctx.needs_input_grad[3])
+        return ds, dh, dw, db, None, None, None
+
+
+_FUSED_ADD_LN = os.environ.get("APEX_AMD_FUSED_ADD_LN", "1") == "1"
+
+
+def _fused_add_ok(x, h, ln):
+    n2 = _n2(ln.normalized_shape)
+    return (_FUSED_ADD_LN and isinstance(ln, FusedLayerNorm) and x.is_cuda and h.is_cuda and x.dtype == h.dtype and x.shape == h.shape
+            and x.dtype in (torch.float16, torch.bfloat16, torch.float32)
+            and n2 % 8 == 0 and n2 <= 2048 and x.shape[-1] == n2 and ln.elementwise_affine
+            and ln.weight.dtype == ln.bias.dtype and _native.available())
+
+
+def fused_add_dropout_layer_norm(x, h, ln, p=0.0, training=True):
+    """(LN(s), s) for s = x + dropout(h, p): the residual join of a transformer
+    sublayer (post-LN BERT uses y, pre-LN GPT-2 keeps s as the residual stream).
+    ``ln`` is a FusedLayerNorm / nn.LayerNorm module (its weight, bias, eps).
+    Falls back to the unfused PyTorch chain on CPU or unsupported shapes/dtypes."""
+    p = float(p) if training else 0.0
+    if _fused_add_ok(x, h, ln):
+        return AddDropoutLayerNormFunction.apply(x, h, ln.weight, ln.bias, ln.normalized_shape,
+                                                 ln.eps, p)
+    s = x + torch.nn.functional.dropout(h, p, training=p > 0.0)
+    return ln(s), s
 
 
 def fused_layer_norm_affine(input, weight, bias, normalized_shape, eps=1e-6):

@@ -32,12 +32,33 @@ static inline void ln_dispatch(DType a, F&& f) {
   }
 }
 
+// Residual + dropout fused into the LayerNorm (BERT post-LN / GPT-2 pre-LN
+// sublayer joins): forward s = x + keep*h*scale, y = LN(s); backward
+// ds = LN'(dy) + ds_ext, dh = keep*ds*scale.  The keep bits are a counter hash of
+// (seed, flat element index) regenerated in the backward: no mask tensor.
+
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du;
+  x ^= x >> 15; x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+// keep bits of the 8 consecutive elements starting at flat index e (e % 8 == 0)
+__device__ __forceinline__ uint32_t drop_keep8(uint32_t seed, uint32_t thresh, int64_t e) {
+  if (thresh == 0) return 0xFFu;
+  const uint32_t base = drop_mix(seed ^ drop_mix((uint32_t)(e >> 3) ^ ((uint32_t)(e >> 35) * 0x9E3779B1u)));
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bits |= (drop_mix(base + (uint32_t)i * 0x9E3779B9u) >= thresh ? 1u : 0u) << i;
+  return bits;
+}
+
 // ---------------------------------------------------------------- forward (fast)
-template <typename T, typename TW, int VPT>
+template <typename T, typename TW, int VPT, bool FUSE = false>
 __global__ void __launch_bounds__(kLNThreads)
     ln_fwd_fast(const T* __restrict__ x, const TW* __restrict__ gamma, const TW* __restrict__ beta,
                 T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ invvar_out,
-                int64_t n1, int n2, float eps, int rms) {
+                int64_t n1, int n2, float eps, int rms, LnFuse fu = LnFuse{}) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row0 = (int64_t)blockIdx.x * kLNWaves + threadIdx.x / kWave;
   const int64_t wstride = (int64_t)gridDim.x * kLNWaves;
@@ -48,8 +69,22 @@ __global__ void __launch_bounds__(kLNThreads)
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       int col = (k * kWave + lane) * 8;
-      if (col < n2) load8(xr + col, v[k]);
-      else {
+      if (col < n2) {
+        load8(xr + col, v[k]);
+        if constexpr (FUSE) {
+          // s = residual + keep * h / (1 - p); s is the LayerNorm input (and the
+          // new residual stream), written once for the backward / next sublayer
+          float hv[8];
+          load8(static_cast<const T*>(fu.h) + row * n2 + col, hv);
+          const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float t = v[k][i] + (((keep >> i) & 1u) ? hv[i] * fu.scale : 0.f);
+            v[k][i] = to_f32(from_f32<T>(t));  // normalise s as stored, like the backward
+          }
+          store8(static_cast<T*>(fu.s) + row * n2 + col, v[k]);
+        }
+      } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[k][i] = 0.f;
       }
@@ -150,9 +185,15 @@ static inline int ln_grid(int64_t n1) {
   return (int)(blocks > 0 ? blocks : 1);
 }
 
+bool layer_norm_fused_ok(const void* x, const void* h, const void* s, const void* gamma,
+                         const void* beta, const void* y, int64_t n2) {
+  auto al = [](const void* p) { return ((uintptr_t)p % 16) == 0; };
+  return ln_fast_ok(x, gamma, beta, y, n2) && al(h) && al(s);
+}
+
 void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta, DType tw,
                     void* y, float* mean, float* invvar, int64_t n1, int64_t n2, float eps,
-                    int rms, hipStream_t st) {
+                    int rms, hipStream_t st, const LnFuse* fuse) {
   if (n1 == 0 || n2 == 0) return;
   ln_dispatch(tx, [&](auto t0) {
     ln_dispatch(tw, [&](auto w0) {
@@ -162,7 +203,15 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
       const TW* gp = static_cast<const TW*>(gamma);
       const TW* bp = static_cast<const TW*>(beta);
       T* yp = static_cast<T*>(y);
-      if (ln_fast_ok(x, gamma, beta, y, n2)) {
+      if (fuse) {  // caller checked layer_norm_fused_ok
+        dim3 grid(ln_grid(n1)), block(kLNThreads);
+        switch (ln_vpt(n2)) {
+          case 1: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 1, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+          case 2: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 2, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+          case 3: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 3, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+          default: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 4, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+        }
+      } else if (ln_fast_ok(x, gamma, beta, y, n2)) {
         int vpt = ln_vpt(n2);
         dim3 grid(ln_grid(n1)), block(kLNThreads);
         switch (vpt) {
@@ -181,11 +230,12 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 
 // ---------------------------------------------------------------- backward (fast, fused)
 // part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
-template <typename T, typename TW, int VPT>
+template <typename T, typename TW, int VPT, bool FUSE = false>
 __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
                 const float* __restrict__ mean, const float* __restrict__ invvar,
-                T* __restrict__ dx, float* __restrict__ part, int64_t n1, int n2, int rms) {
+                T* __restrict__ dx, float* __restrict__ part, int64_t n1, int n2, int rms,
+                LnFuse fu = LnFuse{}) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [kLNWaves][2][n2]
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
@@ -249,6 +299,19 @@ __global__ void __launch_bounds__(kLNThreads)
         float dg = dv[k][i] * g[k][i];
         float t = rms ? (dg - xv[k][i] * s2) : (dg - s1 - xv[k][i] * s2);
         o[i] = t * iv;
+      }
+      if constexpr (FUSE) {
+        if (fu.dres) {
+          float e[8];
+          load8(static_cast<const T*>(fu.dres) + row * n2 + col, e);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += e[i];
+        }
+        const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
+        float hd[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hd[i] = ((keep >> i) & 1u) ? o[i] * fu.scale : 0.f;
+        store8(static_cast<T*>(fu.dh) + row * n2 + col, hd);
       }
       store8(dxr + col, o);
     }
@@ -415,7 +478,8 @@ int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2) {
 
 void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, DType tw,
                     const float* mean, const float* invvar, void* dx, void* dgamma, void* dbeta,
-                    float* part, int64_t n1, int64_t n2, int rms, hipStream_t st) {
+                    float* part, int64_t n1, int64_t n2, int rms, hipStream_t st,
+                    const LnFuse* fuse) {
   if (n1 == 0 || n2 == 0) return;
   const bool want_wb = dgamma != nullptr || dbeta != nullptr;
   ln_dispatch(tx, [&](auto t0) {
@@ -427,7 +491,19 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
       const TW* gp = static_cast<const TW*>(gamma);
       T* dxp = static_cast<T*>(dx);
       int nparts;
-      if (ln_fast_ok(x, gamma, nullptr, dx, n2) && ((uintptr_t)dy % 16) == 0) {
+      if (fuse) {  // caller checked alignment / width (layer_norm_fused_ok + dy, dres, dh)
+        int blocks = ln_bwd_blocks(n1);
+        size_t lds = want_wb ? (size_t)kLNWaves * 2 * n2 * sizeof(float) : 0;
+        float* pp = want_wb ? part : nullptr;
+        dim3 grid(blocks), block(kLNThreads);
+        switch (ln_vpt(n2)) {
+          case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+          case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+          case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+          default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+        }
+        nparts = blocks;
+      } else if (ln_fast_ok(x, gamma, nullptr, dx, n2) && ((uintptr_t)dy % 16) == 0) {
         int vpt = ln_vpt(n2);
         int blocks = ln_bwd_blocks(n1);
         size_t lds = want_wb ? (size_t)kLNWaves * 2 * n2 * sizeof(float) : 0;

@@ -135,16 +135,28 @@ void flat_scale(const void* in, DType tin, void* out, DType tout, int64_t n, Sca
                 int* noop, hipStream_t st);
 
 // ----- LayerNorm (apex fused_layer_norm_cuda) --------------------------------
+struct LnFuse {
+  const void* h = nullptr;     // fwd: sublayer output
+  void* s = nullptr;           // fwd: residual sum out (LN input)
+  const void* dres = nullptr;  // bwd: extra gradient of s (pre-LN residual stream), nullable
+  void* dh = nullptr;          // bwd: gradient of h
+  uint32_t seed = 0, thresh = 0;  // keep iff hash >= thresh (thresh = p * 2^32)
+  float scale = 1.f;              // 1 / (1 - p)
+};
+// fast-path requirements of the fused residual+dropout LayerNorm (16-B aligned, n2 % 8 == 0, <= 2048)
+bool layer_norm_fused_ok(const void* x, const void* h, const void* s, const void* gamma,
+                         const void* beta, const void* y, int64_t n2);
 // x[n1, n2] (T), gamma/beta [n2] (TW, nullable), y [n1,n2] (T), mean/invvar [n1] fp32
 void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta, DType tw,
                     void* y, float* mean, float* invvar, int64_t n1, int64_t n2, float eps,
-                    int rms, hipStream_t st);
+                    int rms, hipStream_t st, const LnFuse* fuse = nullptr);
 // dx [n1,n2]; dgamma/dbeta [n2] (TW) computed if non-null. `part` workspace
 // must hold layer_norm_bwd_workspace(n1, n2) floats.
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2);
 void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, DType tw,
                     const float* mean, const float* invvar, void* dx, void* dgamma, void* dbeta,
-                    float* part, int64_t n1, int64_t n2, int rms, hipStream_t st);
+                    float* part, int64_t n1, int64_t n2, int rms, hipStream_t st,
+                    const LnFuse* fuse = nullptr);
 
 // ----- BatchNorm / SyncBN (apex syncbn) --------------------------------------
 // Layout: NCHW  -> x viewed as [N, C, HW]; NHWC (channel-last) -> [M, C] with M = N*H*W.

@@ -71,6 +71,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto ln = m.def_submodule("layer_norm", "fused LayerNorm / RMSNorm (wave64 row kernels)");
   ln.def("forward", &layer_norm_forward_op);
   ln.def("backward", &layer_norm_backward_op);
+  ln.def("add_dropout_forward", &add_dropout_layer_norm_forward_op);
+  ln.def("add_dropout_backward", &add_dropout_layer_norm_backward_op);
 
   auto attn = m.def_submodule("attn", "fused attention (head dim 64, MFMA, gfx950)");
   attn.def("fwd", &attn_fwd_op);

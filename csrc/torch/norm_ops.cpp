@@ -79,6 +79,79 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_backward_op(
   return {dx, dgam, dbet};
 }
 
+// ----------------------------------------------- residual + dropout + LayerNorm (GPU)
+namespace {
+LnFuse make_fuse(double p, int64_t seed) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  LnFuse f;
+  f.seed = (uint32_t)(seed & 0xFFFFFFFF) ^ (uint32_t)((uint64_t)seed >> 32);
+  const double t = p * 4294967296.0;
+  f.thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
+  f.scale = (float)(1.0 / (1.0 - p));
+  return f;
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_forward_op(
+    at::Tensor x, at::Tensor h, int64_t n2, OptT gamma, OptT beta, double eps, double p,
+    int64_t seed) {
+  TORCH_CHECK(x.is_cuda() && h.is_cuda(), "add_dropout_layer_norm: GPU tensors only");
+  TORCH_CHECK(x.sizes() == h.sizes() && x.scalar_type() == h.scalar_type(),
+              "add_dropout_layer_norm: residual / sublayer output mismatch");
+  x = x.contiguous();
+  h = h.contiguous();
+  const int64_t n1 = x.numel() / n2;
+  at::Tensor g = has(gamma) ? gamma->contiguous() : at::Tensor();
+  at::Tensor b = has(beta) ? beta->contiguous() : at::Tensor();
+  at::Tensor y = at::empty_like(x), s = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({n1}, fopt), invvar = at::empty({n1}, fopt);
+  TORCH_CHECK(layer_norm_fused_ok(x.data_ptr(), h.data_ptr(), s.data_ptr(),
+                                  g.defined() ? g.data_ptr() : nullptr,
+                                  b.defined() ? b.data_ptr() : nullptr, y.data_ptr(), n2),
+              "add_dropout_layer_norm: needs n2 % 8 == 0, n2 <= 2048 and 16-byte aligned rows");
+  LnFuse f = make_fuse(p, seed);
+  f.h = h.data_ptr();
+  f.s = s.data_ptr();
+  DType tw = g.defined() ? dtype_of(g) : (b.defined() ? dtype_of(b) : DType::F32);
+  layer_norm_fwd(x.data_ptr(), dtype_of(x), g.defined() ? g.data_ptr() : nullptr,
+                 b.defined() ? b.data_ptr() : nullptr, tw, y.data_ptr(), mean.data_ptr<float>(),
+                 invvar.data_ptr<float>(), n1, n2, (float)eps, 0, cur_stream(), &f);
+  return {y, s, mean, invvar};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
+    at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
+    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad) {
+  TORCH_CHECK(s.is_cuda(), "add_dropout_layer_norm: GPU tensors only");
+  s = s.contiguous();
+  dy = dy.contiguous();
+  at::Tensor e = has(dres) ? dres->contiguous() : at::Tensor();
+  const int64_t n1 = s.numel() / n2;
+  at::Tensor g = has(gamma) ? gamma->contiguous() : at::Tensor();
+  at::Tensor ds = at::empty_like(s), dh = at::empty_like(s);
+  auto al = [](const at::Tensor& t) { return !t.defined() || ((uintptr_t)t.data_ptr() % 16) == 0; };
+  TORCH_CHECK(layer_norm_fused_ok(s.data_ptr(), dh.data_ptr(), ds.data_ptr(),
+                                  g.defined() ? g.data_ptr() : nullptr, nullptr, dy.data_ptr(),
+                                  n2) && al(e),
+              "add_dropout_layer_norm: needs n2 % 8 == 0, n2 <= 2048 and 16-byte aligned rows");
+  at::Tensor dgam, dbet, part;
+  DType tw = g.defined() ? dtype_of(g) : DType::F32;
+  if (need_wgrad && g.defined()) dgam = at::empty_like(g);
+  if (need_bgrad && g.defined()) dbet = at::empty_like(g);
+  if (dgam.defined() || dbet.defined())
+    part = at::empty({layer_norm_bwd_workspace(n1, n2)}, s.options().dtype(at::kFloat));
+  LnFuse f = make_fuse(p, seed);
+  f.dres = e.defined() ? e.data_ptr() : nullptr;
+  f.dh = dh.data_ptr();
+  layer_norm_bwd(dy.data_ptr(), s.data_ptr(), dtype_of(s), g.defined() ? g.data_ptr() : nullptr,
+                 tw, mean.data_ptr<float>(), invvar.data_ptr<float>(), ds.data_ptr(),
+                 dgam.defined() ? dgam.data_ptr() : nullptr,
+                 dbet.defined() ? dbet.data_ptr() : nullptr,
+                 part.defined() ? part.data_ptr<float>() : nullptr, n1, n2, 0, cur_stream(), &f);
+  return {ds, dh, dgam, dbet};
+}
+
 // ============================================================================ BatchNorm
 namespace {
 struct BNView {

@@ -16,6 +16,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_backward_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
     bool need_wgrad, bool need_bgrad, bool rms);
 
+// Residual + dropout + LayerNorm (GPU): s = x + dropout_p(h) with counter-hash keep
+// bits from `seed`, y = LN(s).  Returns (y, s, mean, invvar).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_forward_op(
+    at::Tensor x, at::Tensor h, int64_t n2, OptT gamma, OptT beta, double eps, double p,
+    int64_t seed);
+// -> (ds = LN'(dy) + dres, dh = dropout'(ds), dgamma, dbeta)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
+    at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
+    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad);
+
 // BatchNorm building blocks (local / synchronized).
 std::tuple<at::Tensor, at::Tensor> bn_local_stats_op(at::Tensor x);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor means,

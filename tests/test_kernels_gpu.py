@@ -244,6 +244,79 @@ def test_layer_norm_fwd_bwd(shape, dt):
     torch.testing.assert_close(ln.bias.grad.float(), ref.bias.grad, **gtol)
 
 
+@pytest.mark.parametrize("shape", [(64, 1024), (4096, 1024), (3, 5, 768), (7, 2048), (9, 64)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
+@pytest.mark.parametrize("use_s", [False, True])
+def test_add_dropout_layer_norm(shape, dt, p, use_s):
+    """fused residual + dropout + LayerNorm kernel vs an fp32 PyTorch chain with the
+    same keep mask (recovered by replaying the seed on x = 0, h = 1)."""
+    from apex_example_amd.normalization import FusedLayerNorm, fused_add_dropout_layer_norm
+
+    torch.manual_seed(0)
+    n2 = shape[-1]
+    x = (torch.randn(*shape, device=DEV) * 0.7 + 0.3).to(dt)
+    h = torch.randn(*shape, device=DEV).to(dt)
+    ln = FusedLayerNorm(n2).to(DEV).to(dt)
+    with torch.no_grad():
+        ln.weight.normal_()
+        ln.bias.normal_()
+    xa = x.clone().requires_grad_(True)
+    ha = h.clone().requires_grad_(True)
+    torch.manual_seed(77)
+    ya, sa = fused_add_dropout_layer_norm(xa, ha, ln, p, training=True)
+    with torch.no_grad():
+        torch.manual_seed(77)
+        _, m = fused_add_dropout_layer_norm(torch.zeros_like(x), torch.ones_like(h), ln, p)
+    keep = (m.float() != 0).float()
+    if p == 0.0:
+        assert bool((keep == 1).all())
+    else:
+        frac = keep.mean().item()
+        assert abs(frac - (1 - p)) < 0.02 + 3 / math.sqrt(keep.numel()), frac
+        torch.testing.assert_close(m.float()[keep.bool()],
+                                   torch.full_like(m.float()[keep.bool()], 1 / (1 - p)),
+                                   rtol=1e-2, atol=0)
+    ref = torch.nn.LayerNorm(n2).to(DEV)
+    ref.load_state_dict({k: v.float() for k, v in ln.state_dict().items()})
+    xb = x.float().clone().requires_grad_(True)
+    hb = h.float().clone().requires_grad_(True)
+    sb = xb + hb * keep / (1 - p)
+    yb = ref(sb)
+    tol = dict(rtol=1e-5, atol=1e-4) if dt == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(sa.float(), sb, **tol)
+    torch.testing.assert_close(ya.float(), yb, **tol)
+    dy = torch.randn_like(yb)
+    de = torch.randn_like(yb)
+    la = (ya.float() * dy).sum() + ((sa.float() * de).sum() if use_s else 0.0)
+    lb = (yb * dy).sum() + ((sb * de).sum() if use_s else 0.0)
+    la.backward()
+    lb.backward()
+    gt = dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=3e-2, atol=6e-2)
+    torch.testing.assert_close(xa.grad.float(), xb.grad, **gt)
+    torch.testing.assert_close(ha.grad.float(), hb.grad, **gt)
+    wt = dict(rtol=1e-4, atol=1e-3) if dt == torch.float32 else dict(rtol=5e-2, atol=5e-1)
+    torch.testing.assert_close(ln.weight.grad.float(), ref.weight.grad, **wt)
+    torch.testing.assert_close(ln.bias.grad.float(), ref.bias.grad, **wt)
+
+
+def test_add_dropout_layer_norm_deterministic_and_seeded():
+    from apex_example_amd.normalization import FusedLayerNorm, fused_add_dropout_layer_norm
+
+    x = torch.randn(256, 1024, device=DEV, dtype=torch.bfloat16)
+    h = torch.randn_like(x)
+    ln = FusedLayerNorm(1024).to(DEV).to(torch.bfloat16)
+    torch.manual_seed(5)
+    y1, s1 = fused_add_dropout_layer_norm(x, h, ln, 0.1)
+    torch.manual_seed(5)
+    y2, s2 = fused_add_dropout_layer_norm(x, h, ln, 0.1)
+    y3, s3 = fused_add_dropout_layer_norm(x, h, ln, 0.1)
+    assert torch.equal(y1, y2) and torch.equal(s1, s2)
+    assert not torch.equal(s1, s3)
+    _, s4 = fused_add_dropout_layer_norm(x, h, ln, 0.1, training=False)
+    torch.testing.assert_close(s4.float(), (x.float() + h.float()), rtol=1e-2, atol=1e-2)
+
+
 def test_rms_norm():
     from apex_example_amd.normalization import FusedRMSNorm
 
