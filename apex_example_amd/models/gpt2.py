@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
-from ..normalization import FusedLayerNorm
+from ..normalization import FusedLayerNorm, fused_add_dropout_layer_norm
 from ..fused_dense import fused_dense_function, fused_dense_gelu_dense_function
 from ..ops import attention as fused_attn
 
@@ -35,6 +35,9 @@ class GPT2Config:
     fused_layer_norm: bool = True
     fused_attention: bool = True
     fused_dense: bool = True  # fused bias-grad / GELU-backward dense layers (fused_dense)
+    # residual add + dropout + the next LayerNorm as one kernel per sublayer join
+    # (fp32 residual stream, 16-bit sublayer output under O1)
+    fused_residual_ln: bool = True
 
 
 def _ln(cfg, n):
@@ -58,17 +61,18 @@ class GPT2Attention(nn.Module):
     def _lin(self, m, x):
         return fused_dense_function(x, m.weight, m.bias) if self.fused_dense else m(x)
 
-    def forward(self, x):
+    def forward(self, x, resid_dropout=True):
         b, s, e = x.shape
+        drop = self.resid_dropout if resid_dropout else (lambda t: t)
         qkv = self._lin(self.c_attn, x).view(b, s, 3, self.h, self.d)
         p = self.p if self.training else 0.0
         if self.fused and fused_attn.supported(qkv, self.d):
             o = fused_attn.fused_attention_qkv(qkv, causal=True, dropout_p=p).view(b, s, e)
-            return self.resid_dropout(self._lin(self.c_proj, o))
+            return drop(self._lin(self.c_proj, o))
         qkv = qkv.permute(2, 0, 3, 1, 4)
         o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], is_causal=True, dropout_p=p)
         o = o.transpose(1, 2).reshape(b, s, e)
-        return self.resid_dropout(self._lin(self.c_proj, o))
+        return drop(self._lin(self.c_proj, o))
 
 
 class GPT2MLP(nn.Module):
@@ -79,12 +83,13 @@ class GPT2MLP(nn.Module):
         self.dropout = nn.Dropout(cfg.resid_pdrop)
         self.fused_dense = cfg.fused_dense
 
-    def forward(self, x):
+    def forward(self, x, dropout=True):
+        drop = self.dropout if dropout else (lambda t: t)
         if self.fused_dense:
-            return self.dropout(fused_dense_gelu_dense_function(
+            return drop(fused_dense_gelu_dense_function(
                 x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias,
                 "tanh"))
-        return self.dropout(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+        return drop(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
 
 
 class GPT2Block(nn.Module):
@@ -98,6 +103,15 @@ class GPT2Block(nn.Module):
     def forward(self, x):
         x = x + self.attn(self.ln_1(x))
         return x + self.mlp(self.ln_2(x))
+
+    def forward_joined(self, x, y, next_ln):
+        """Same block with the sublayer joins fused: ``y`` = ln_1(x) is given,
+        returns (next_ln(x'), x') for the block output x'.  Each join (dropout,
+        residual add, the following LayerNorm) is one kernel each way."""
+        y, x = fused_add_dropout_layer_norm(x, self.attn(y, resid_dropout=False), self.ln_2,
+                                            self.attn.resid_dropout.p, self.training)
+        return fused_add_dropout_layer_norm(x, self.mlp(y, dropout=False), next_ln,
+                                            self.mlp.dropout.p, self.training)
 
 
 class GPT2LMHeadModel(nn.Module):
@@ -127,6 +141,12 @@ class GPT2LMHeadModel(nn.Module):
         s = input_ids.size(1)
         pos = torch.arange(s, device=input_ids.device).unsqueeze(0)
         x = self.drop(self.wte(input_ids) + self.wpe(pos))
+        if self.config.fused_residual_ln:
+            y = self.h[0].ln_1(x)
+            for i, block in enumerate(self.h):
+                nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f
+                y, x = block.forward_joined(x, y, nxt)
+            return F.linear(y, self.wte.weight)  # tied LM head
         for block in self.h:
             x = block(x)
         x = self.ln_f(x)

@@ -112,18 +112,19 @@ class AddDropoutLayerNormFunction(torch.autograd.Function):
         # an unused output (post-LN callers drop s) gets grad None, not a zero fill + read
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(s, weight, mean, invvar)
-        ctx.cfg = (n2, float(p), seed)
+        ctx.cfg = (n2, float(p), seed, h.dtype if h.dtype != x.dtype else None)
         return y, s
 
     @staticmethod
     def backward(ctx, dy, ds_ext):
         C = _native.require().layer_norm
         s, weight, mean, invvar = ctx.saved_tensors
-        n2, p, seed = ctx.cfg
+        n2, p, seed, h_dtype = ctx.cfg
         if dy is None:
             dy = torch.zeros_like(s)
         ds, dh, dw, db = C.add_dropout_backward(dy, s, mean, invvar, n2, weight, ds_ext, p, seed,
-                                                ctx.needs_input_grad[2], ctx.needs_input_grad[3])
+                                                ctx.needs_input_grad[2], ctx.needs_input_grad[3],
+                                                h_dtype)
         return ds, dh, dw, db, None, None, None
 
 
@@ -132,7 +133,10 @@ _FUSED_ADD_LN = os.environ.get("APEX_AMD_FUSED_ADD_LN", "1") == "1"
 
 def _fused_add_ok(x, h, ln):
     n2 = _n2(ln.normalized_shape)
-    return (_FUSED_ADD_LN and isinstance(ln, FusedLayerNorm) and x.is_cuda and h.is_cuda and x.dtype == h.dtype and x.shape == h.shape
+    # h may be 16-bit under an fp32 residual stream (amp O1): read / written as is
+    mixed = x.dtype == torch.float32 and h.dtype in (torch.float16, torch.bfloat16)
+    return (_FUSED_ADD_LN and isinstance(ln, FusedLayerNorm) and x.is_cuda and h.is_cuda
+            and (x.dtype == h.dtype or mixed) and x.shape == h.shape
             and x.dtype in (torch.float16, torch.bfloat16, torch.float32)
             and n2 % 8 == 0 and n2 <= 2048 and x.shape[-1] == n2 and ln.elementwise_affine
             and ln.weight.dtype == ln.bias.dtype and _native.available())

@@ -62,6 +62,8 @@ def parse():
                     help="transformers: torch cross entropy on fp32 logits instead of the fused kernel")
     ap.add_argument("--no-fused-attn", action="store_true",
                     help="transformers: PyTorch SDPA instead of the gfx950 attention kernels")
+    ap.add_argument("--no-fused-residual-ln", action="store_true",
+                    help="GPT-2: unfused residual add / dropout / LayerNorm sublayer joins")
     ap.add_argument("--syncbn", action="store_true",
                     help="SyncBatchNorm across ranks (the default for ResNet at N > 1)")
     ap.add_argument("--no-syncbn", action="store_true",
@@ -246,7 +248,8 @@ def build_gpt2(args, device, world):
     seq = args.seq_len or 1024
     opt_level = args.opt_level or "O1"
     cfg = GPT2Config(fused_layer_norm=(args.impl == "amd"),
-                     fused_attention=(args.impl == "amd" and not args.no_fused_attn))
+                     fused_attention=(args.impl == "amd" and not args.no_fused_attn),
+                     fused_residual_ln=(args.impl == "amd" and not args.no_fused_residual_ln))
     model = GPT2LMHeadModel(cfg).to(device)
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(0, cfg.vocab_size, (bs, seq), generator=g).to(device)

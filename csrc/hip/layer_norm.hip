@@ -14,6 +14,8 @@
 //    visits, so the column sums stay in registers across rows; one LDS combine
 //    per block then a deterministic column-sum kernel (no float atomics);
 //  * a generic block-per-row path covers odd widths / unaligned rows.
+#include <type_traits>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -30,6 +32,18 @@ static inline void ln_dispatch(DType a, F&& f) {
     case DType::BF16: f(bf16_t{}); break;
     default: break;
   }
+}
+
+// Sublayer-output type of the fused residual LayerNorm: the LN input's own type,
+// or (fp32 residual stream under amp O1) the F16 / BF16 type the GEMM produced,
+// read and written directly so no cast kernel runs either way.
+template <typename T, typename F>
+static inline void ln_fuse_h_dispatch(int th, F&& f) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (th == (int)DType::F16) return f(half_t{});
+    if (th == (int)DType::BF16) return f(bf16_t{});
+  }
+  f(T{});
 }
 
 // Residual + dropout fused into the LayerNorm (BERT post-LN / GPT-2 pre-LN
@@ -54,7 +68,7 @@ __device__ __forceinline__ uint32_t drop_keep8(uint32_t seed, uint32_t thresh, i
 }
 
 // ---------------------------------------------------------------- forward (fast)
-template <typename T, typename TW, int VPT, bool FUSE = false>
+template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_fwd_fast(const T* __restrict__ x, const TW* __restrict__ gamma, const TW* __restrict__ beta,
                 T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ invvar_out,
@@ -75,7 +89,7 @@ __global__ void __launch_bounds__(kLNThreads)
           // s = residual + keep * h / (1 - p); s is the LayerNorm input (and the
           // new residual stream), written once for the backward / next sublayer
           float hv[8];
-          load8(static_cast<const T*>(fu.h) + row * n2 + col, hv);
+          load8(static_cast<const TH*>(fu.h) + row * n2 + col, hv);
           const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
@@ -205,12 +219,16 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
       T* yp = static_cast<T*>(y);
       if (fuse) {  // caller checked layer_norm_fused_ok
         dim3 grid(ln_grid(n1)), block(kLNThreads);
-        switch (ln_vpt(n2)) {
-          case 1: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 1, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-          case 2: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 2, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-          case 3: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 3, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-          default: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 4, true>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-        }
+        auto launch = [&](auto h0) {
+          using TH = decltype(h0);
+          switch (ln_vpt(n2)) {
+            case 1: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 1, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            case 2: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 2, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            case 3: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 3, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            default: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 4, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+          }
+        };
+        ln_fuse_h_dispatch<T>(fuse->th, launch);
       } else if (ln_fast_ok(x, gamma, beta, y, n2)) {
         int vpt = ln_vpt(n2);
         dim3 grid(ln_grid(n1)), block(kLNThreads);
@@ -230,7 +248,7 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 
 // ---------------------------------------------------------------- backward (fast, fused)
 // part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
-template <typename T, typename TW, int VPT, bool FUSE = false>
+template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
                 const float* __restrict__ mean, const float* __restrict__ invvar,
@@ -311,7 +329,7 @@ __global__ void __launch_bounds__(kLNThreads)
         float hd[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) hd[i] = ((keep >> i) & 1u) ? o[i] * fu.scale : 0.f;
-        store8(static_cast<T*>(fu.dh) + row * n2 + col, hd);
+        store8(static_cast<TH*>(fu.dh) + row * n2 + col, hd);
       }
       store8(dxr + col, o);
     }
@@ -496,12 +514,16 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
         size_t lds = want_wb ? (size_t)kLNWaves * 2 * n2 * sizeof(float) : 0;
         float* pp = want_wb ? part : nullptr;
         dim3 grid(blocks), block(kLNThreads);
-        switch (ln_vpt(n2)) {
-          case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-          case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-          case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-          default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-        }
+        auto launch = [&](auto h0) {
+          using TH = decltype(h0);
+          switch (ln_vpt(n2)) {
+            case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+          }
+        };
+        ln_fuse_h_dispatch<T>(fuse->th, launch);
         nparts = blocks;
       } else if (ln_fast_ok(x, gamma, nullptr, dx, n2) && ((uintptr_t)dy % 16) == 0) {
         int vpt = ln_vpt(n2);

@@ -142,6 +142,8 @@ struct LnFuse {
   void* dh = nullptr;          // bwd: gradient of h
   uint32_t seed = 0, thresh = 0;  // keep iff hash >= thresh (thresh = p * 2^32)
   float scale = 1.f;              // 1 / (1 - p)
+  int th = -1;                    // DType of h / dh: -1 = the LN input's; an fp32 residual
+                                  // stream may take an F16 / BF16 sublayer output (amp O1)
 };
 // fast-path requirements of the fused residual+dropout LayerNorm (16-B aligned, n2 % 8 == 0, <= 2048)
 bool layer_norm_fused_ok(const void* x, const void* h, const void* s, const void* gamma,

@@ -96,7 +96,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
     at::Tensor x, at::Tensor h, int64_t n2, OptT gamma, OptT beta, double eps, double p,
     int64_t seed) {
   TORCH_CHECK(x.is_cuda() && h.is_cuda(), "add_dropout_layer_norm: GPU tensors only");
-  TORCH_CHECK(x.sizes() == h.sizes() && x.scalar_type() == h.scalar_type(),
+  // h is x's type, or 16-bit under an fp32 residual stream (amp O1)
+  const bool mixed = x.scalar_type() == at::kFloat &&
+                     (h.scalar_type() == at::kHalf || h.scalar_type() == at::kBFloat16);
+  TORCH_CHECK(x.sizes() == h.sizes() && (x.scalar_type() == h.scalar_type() || mixed),
               "add_dropout_layer_norm: residual / sublayer output mismatch");
   x = x.contiguous();
   h = h.contiguous();
@@ -113,6 +116,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   LnFuse f = make_fuse(p, seed);
   f.h = h.data_ptr();
   f.s = s.data_ptr();
+  if (mixed) f.th = (int)dtype_of(h);
   DType tw = g.defined() ? dtype_of(g) : (b.defined() ? dtype_of(b) : DType::F32);
   layer_norm_fwd(x.data_ptr(), dtype_of(x), g.defined() ? g.data_ptr() : nullptr,
                  b.defined() ? b.data_ptr() : nullptr, tw, y.data_ptr(), mean.data_ptr<float>(),
@@ -122,14 +126,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
     at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
-    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad) {
+    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad,
+    c10::optional<at::ScalarType> h_dtype) {
   TORCH_CHECK(s.is_cuda(), "add_dropout_layer_norm: GPU tensors only");
   s = s.contiguous();
   dy = dy.contiguous();
   at::Tensor e = has(dres) ? dres->contiguous() : at::Tensor();
   const int64_t n1 = s.numel() / n2;
   at::Tensor g = has(gamma) ? gamma->contiguous() : at::Tensor();
-  at::Tensor ds = at::empty_like(s), dh = at::empty_like(s);
+  const bool mixed = h_dtype.has_value() && *h_dtype != s.scalar_type();
+  TORCH_CHECK(!mixed || (s.scalar_type() == at::kFloat &&
+                         (*h_dtype == at::kHalf || *h_dtype == at::kBFloat16)),
+              "add_dropout_layer_norm: 16-bit sublayer output needs an fp32 residual");
+  at::Tensor ds = at::empty_like(s);
+  at::Tensor dh = mixed ? at::empty_like(s, s.options().dtype(*h_dtype)) : at::empty_like(s);
   auto al = [](const at::Tensor& t) { return !t.defined() || ((uintptr_t)t.data_ptr() % 16) == 0; };
   TORCH_CHECK(layer_norm_fused_ok(s.data_ptr(), dh.data_ptr(), ds.data_ptr(),
                                   g.defined() ? g.data_ptr() : nullptr, nullptr, dy.data_ptr(),
@@ -144,6 +154,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   LnFuse f = make_fuse(p, seed);
   f.dres = e.defined() ? e.data_ptr() : nullptr;
   f.dh = dh.data_ptr();
+  if (mixed) f.th = (int)dtype_of(dh);
   layer_norm_bwd(dy.data_ptr(), s.data_ptr(), dtype_of(s), g.defined() ? g.data_ptr() : nullptr,
                  tw, mean.data_ptr<float>(), invvar.data_ptr<float>(), ds.data_ptr(),
                  dgam.defined() ? dgam.data_ptr() : nullptr,

@@ -24,7 +24,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
 // -> (ds = LN'(dy) + dres, dh = dropout'(ds), dgamma, dbeta)
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
     at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
-    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad);
+    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad,
+    c10::optional<at::ScalarType> h_dtype);
 
 // BatchNorm building blocks (local / synchronized).
 std::tuple<at::Tensor, at::Tensor> bn_local_stats_op(at::Tensor x);

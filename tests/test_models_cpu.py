@@ -69,6 +69,20 @@ def test_gpt2_causal():
     assert not torch.allclose(out[:, 8:], out2[:, 8:])
 
 
+def test_gpt2_joined_residual_ln_matches_blockwise():
+    """fused_residual_ln (joins feed the next block's ln_1 / ln_f) computes the
+    same function as the plain pre-LN block loop, same state dict."""
+    cfg = _tiny_gpt()
+    torch.manual_seed(0)
+    m = GPT2LMHeadModel(cfg).eval()
+    cfg2 = _tiny_gpt()
+    cfg2.fused_residual_ln = False
+    m2 = GPT2LMHeadModel(cfg2).eval()
+    m2.load_state_dict(m.state_dict())
+    ids = torch.randint(0, 96, (2, 12))
+    torch.testing.assert_close(m(ids), m2(ids), rtol=1e-5, atol=1e-5)
+
+
 def _train(model, opt, batch_fn, loss_fn, opt_level, steps=12):
     from apex_example_amd import amp
 
