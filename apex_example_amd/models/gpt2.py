@@ -108,10 +108,13 @@ class GPT2Block(nn.Module):
         """Same block with the sublayer joins fused: ``y`` = ln_1(x) is given,
         returns (next_ln(x'), x') for the block output x'.  Each join (dropout,
         residual add, the following LayerNorm) is one kernel each way."""
+        # y only feeds autocast GEMMs (c_attn / c_fc / the tied LM head): under O1 it
+        # leaves the join in the GEMM dtype instead of fp32 + a cast kernel
+        y16 = torch.is_autocast_enabled("cuda")
         y, x = fused_add_dropout_layer_norm(x, self.attn(y, resid_dropout=False), self.ln_2,
-                                            self.attn.resid_dropout.p, self.training)
+                                            self.attn.resid_dropout.p, self.training, y16)
         return fused_add_dropout_layer_norm(x, self.mlp(y, dropout=False), next_ln,
-                                            self.mlp.dropout.p, self.training)
+                                            self.mlp.dropout.p, self.training, y16)
 
 
 class GPT2LMHeadModel(nn.Module):

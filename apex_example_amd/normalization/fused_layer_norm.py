@@ -104,11 +104,12 @@ class AddDropoutLayerNormFunction(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, h, weight, bias, normalized_shape, eps, p):
+    def forward(ctx, x, h, weight, bias, normalized_shape, eps, p, y_as_h=False):
         C = _native.require().layer_norm
         n2 = _n2(normalized_shape)
         seed = _dropout_seed() if p > 0.0 else 0
-        y, s, mean, invvar = C.add_dropout_forward(x, h, n2, weight, bias, eps, p, seed)
+        y, s, mean, invvar = C.add_dropout_forward(x, h, n2, weight, bias, eps, p, seed,
+                                                   bool(y_as_h))
         # an unused output (post-LN callers drop s) gets grad None, not a zero fill + read
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(s, weight, mean, invvar)
@@ -125,7 +126,7 @@ class AddDropoutLayerNormFunction(torch.autograd.Function):
         ds, dh, dw, db = C.add_dropout_backward(dy, s, mean, invvar, n2, weight, ds_ext, p, seed,
                                                 ctx.needs_input_grad[2], ctx.needs_input_grad[3],
                                                 h_dtype)
-        return ds, dh, dw, db, None, None, None
+        return ds, dh, dw, db, None, None, None, None
 
 
 _FUSED_ADD_LN = os.environ.get("APEX_AMD_FUSED_ADD_LN", "1") == "1"
@@ -142,15 +143,17 @@ def _fused_add_ok(x, h, ln):
             and ln.weight.dtype == ln.bias.dtype and _native.available())
 
 
-def fused_add_dropout_layer_norm(x, h, ln, p=0.0, training=True):
+def fused_add_dropout_layer_norm(x, h, ln, p=0.0, training=True, y_as_h=False):
     """(LN(s), s) for s = x + dropout(h, p): the residual join of a transformer
     sublayer (post-LN BERT uses y, pre-LN GPT-2 keeps s as the residual stream).
     ``ln`` is a FusedLayerNorm / nn.LayerNorm module (its weight, bias, eps).
-    Falls back to the unfused PyTorch chain on CPU or unsupported shapes/dtypes."""
+    Falls back to the unfused PyTorch chain on CPU or unsupported shapes/dtypes.
+    ``y_as_h``: with an fp32 residual and a 16-bit ``h`` (amp O1) return y in h's
+    dtype - for a consumer that is an autocast GEMM, which would cast it anyway."""
     p = float(p) if training else 0.0
     if _fused_add_ok(x, h, ln):
         return AddDropoutLayerNormFunction.apply(x, h, ln.weight, ln.bias, ln.normalized_shape,
-                                                 ln.eps, p)
+                                                 ln.eps, p, y_as_h and h.dtype != x.dtype)
     s = x + torch.nn.functional.dropout(h, p, training=p > 0.0)
     return ln(s), s
 

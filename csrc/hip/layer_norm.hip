@@ -45,6 +45,14 @@ static inline void ln_fuse_h_dispatch(int th, F&& f) {
   }
   f(T{});
 }
+// LN output / its gradient: T, or the 16-bit sublayer type when fu.ty is set
+template <typename T, typename TH, typename F>
+static inline void ln_fuse_y_dispatch(int ty, F&& f) {
+  if constexpr (!std::is_same<T, TH>::value) {
+    if (ty >= 0) return f(TH{});
+  }
+  f(T{});
+}
 
 // Residual + dropout fused into the LayerNorm (BERT post-LN / GPT-2 pre-LN
 // sublayer joins): forward s = x + keep*h*scale, y = LN(s); backward
@@ -68,7 +76,7 @@ __device__ __forceinline__ uint32_t drop_keep8(uint32_t seed, uint32_t thresh, i
 }
 
 // ---------------------------------------------------------------- forward (fast)
-template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T>
+template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_fwd_fast(const T* __restrict__ x, const TW* __restrict__ gamma, const TW* __restrict__ beta,
                 T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ invvar_out,
@@ -130,7 +138,7 @@ __global__ void __launch_bounds__(kLNThreads)
       if (mean_out) mean_out[row] = mu;
       invvar_out[row] = iv;
     }
-    T* yr = y + row * n2;
+    TY* yr = reinterpret_cast<TY*>(y) + row * n2;
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       int col = (k * kWave + lane) * 8;
@@ -221,12 +229,15 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
         dim3 grid(ln_grid(n1)), block(kLNThreads);
         auto launch = [&](auto h0) {
           using TH = decltype(h0);
+          ln_fuse_y_dispatch<T, TH>(fuse->ty, [&](auto y0) {
+          using TY = decltype(y0);
           switch (ln_vpt(n2)) {
-            case 1: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 1, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-            case 2: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 2, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-            case 3: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 3, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
-            default: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 4, true, TH>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            case 1: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 1, true, TH, TY>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            case 2: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 2, true, TH, TY>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            case 3: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 3, true, TH, TY>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
+            default: hipLaunchKernelGGL((ln_fwd_fast<T, TW, 4, true, TH, TY>), grid, block, 0, st, xp, gp, bp, yp, mean, invvar, n1, (int)n2, eps, rms, *fuse); break;
           }
+          });
         };
         ln_fuse_h_dispatch<T>(fuse->th, launch);
       } else if (ln_fast_ok(x, gamma, beta, y, n2)) {
@@ -248,7 +259,7 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 
 // ---------------------------------------------------------------- backward (fast, fused)
 // part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
-template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T>
+template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
                 const float* __restrict__ mean, const float* __restrict__ invvar,
@@ -286,7 +297,7 @@ __global__ void __launch_bounds__(kLNThreads)
       int col = (k * kWave + lane) * 8;
       if (col < n2) {
         load8(x + row * n2 + col, xv[k]);
-        load8(dy + row * n2 + col, dv[k]);
+        load8(reinterpret_cast<const TY*>(dy) + row * n2 + col, dv[k]);
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) xv[k][i] = dv[k][i] = 0.f;
@@ -516,12 +527,15 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
         dim3 grid(blocks), block(kLNThreads);
         auto launch = [&](auto h0) {
           using TH = decltype(h0);
+          ln_fuse_y_dispatch<T, TH>(fuse->ty, [&](auto y0) {
+          using TY = decltype(y0);
           switch (ln_vpt(n2)) {
-            case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-            case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-            case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-            default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
           }
+          });
         };
         ln_fuse_h_dispatch<T>(fuse->th, launch);
         nparts = blocks;

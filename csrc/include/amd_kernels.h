@@ -144,6 +144,8 @@ struct LnFuse {
   float scale = 1.f;              // 1 / (1 - p)
   int th = -1;                    // DType of h / dh: -1 = the LN input's; an fp32 residual
                                   // stream may take an F16 / BF16 sublayer output (amp O1)
+  int ty = -1;                    // >= 0 (mixed only): y / dy are in h's 16-bit type, the
+                                  // dtype the consuming autocast GEMM reads (no cast kernel)
 };
 // fast-path requirements of the fused residual+dropout LayerNorm (16-B aligned, n2 % 8 == 0, <= 2048)
 bool layer_norm_fused_ok(const void* x, const void* h, const void* s, const void* gamma,

@@ -94,7 +94,7 @@ LnFuse make_fuse(double p, int64_t seed) {
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_forward_op(
     at::Tensor x, at::Tensor h, int64_t n2, OptT gamma, OptT beta, double eps, double p,
-    int64_t seed) {
+    int64_t seed, bool y_as_h) {
   TORCH_CHECK(x.is_cuda() && h.is_cuda(), "add_dropout_layer_norm: GPU tensors only");
   // h is x's type, or 16-bit under an fp32 residual stream (amp O1)
   const bool mixed = x.scalar_type() == at::kFloat &&
@@ -106,7 +106,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   const int64_t n1 = x.numel() / n2;
   at::Tensor g = has(gamma) ? gamma->contiguous() : at::Tensor();
   at::Tensor b = has(beta) ? beta->contiguous() : at::Tensor();
-  at::Tensor y = at::empty_like(x), s = at::empty_like(x);
+  // y_as_h (mixed only): emit y in h's 16-bit type for an autocast GEMM consumer
+  const bool y16 = mixed && y_as_h;
+  at::Tensor y = y16 ? at::empty_like(x, x.options().dtype(h.scalar_type())) : at::empty_like(x);
+  at::Tensor s = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor mean = at::empty({n1}, fopt), invvar = at::empty({n1}, fopt);
   TORCH_CHECK(layer_norm_fused_ok(x.data_ptr(), h.data_ptr(), s.data_ptr(),
@@ -117,6 +120,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   f.h = h.data_ptr();
   f.s = s.data_ptr();
   if (mixed) f.th = (int)dtype_of(h);
+  if (y16) f.ty = f.th;
   DType tw = g.defined() ? dtype_of(g) : (b.defined() ? dtype_of(b) : DType::F32);
   layer_norm_fwd(x.data_ptr(), dtype_of(x), g.defined() ? g.data_ptr() : nullptr,
                  b.defined() ? b.data_ptr() : nullptr, tw, y.data_ptr(), mean.data_ptr<float>(),
@@ -155,6 +159,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   f.dres = e.defined() ? e.data_ptr() : nullptr;
   f.dh = dh.data_ptr();
   if (mixed) f.th = (int)dtype_of(dh);
+  if (mixed && dy.scalar_type() == dh.scalar_type()) f.ty = f.th;  // 16-bit y's gradient
+  TORCH_CHECK(dy.scalar_type() == s.scalar_type() || f.ty >= 0,
+              "add_dropout_layer_norm: dy dtype matches neither s nor h");
   layer_norm_bwd(dy.data_ptr(), s.data_ptr(), dtype_of(s), g.defined() ? g.data_ptr() : nullptr,
                  tw, mean.data_ptr<float>(), invvar.data_ptr<float>(), ds.data_ptr(),
                  dgam.defined() ? dgam.data_ptr() : nullptr,

@@ -20,7 +20,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_backward_op(
 // bits from `seed`, y = LN(s).  Returns (y, s, mean, invvar).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_forward_op(
     at::Tensor x, at::Tensor h, int64_t n2, OptT gamma, OptT beta, double eps, double p,
-    int64_t seed);
+    int64_t seed, bool y_as_h);
 // -> (ds = LN'(dy) + dres, dh = dropout'(ds), dgamma, dbeta)
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
     at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
