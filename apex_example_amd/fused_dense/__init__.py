@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-__all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function",
+__all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function", "cast_params_once",
            "fused_dense_gelu_dense_function", "dense_no_bias_function"]
 
 
@@ -31,8 +31,53 @@ def _compute_dtype(x):
     return x.dtype
 
 
+# {id(param): 16-bit copy} while a cast_params_once() block runs
+_CAST_CACHE = None
+
+
 def _cast(t, dt):
-    return t if t is None or t.dtype == dt else t.to(dt)
+    if t is None or t.dtype == dt:
+        return t
+    if _CAST_CACHE is not None:
+        c = _CAST_CACHE.get(id(t))
+        if c is not None and c.dtype == dt:
+            return c
+    return t.to(dt)
+
+
+class cast_params_once:
+    """amp O1 weight casts for a whole forward in ONE multi-tensor launch: the fp32
+    parameters are written as 16-bit copies into one flat buffer (``mt.scale``
+    with factor 1: plain round-to-nearest casts, the same values ``.to()`` gives),
+    and the dense layers' ``_cast`` picks them up instead of launching one cast
+    kernel per weight and bias (~200 small launches per GPT-2-medium step).
+    Re-cast on every entry, so an optimizer step between forwards is seen."""
+
+    def __init__(self, params, dtype):
+        self.params, self.dtype, self.prev = params, dtype, None
+
+    def __enter__(self):
+        global _CAST_CACHE
+        self.prev = _CAST_CACHE
+        ps = [p for p in self.params if p.is_cuda and p.dtype == torch.float32]
+        if not ps or not _native.available():
+            return self
+        # each copy starts 16-byte aligned (8 halves): the kernel's vector path
+        pad = [(p.numel() + 7) // 8 * 8 for p in ps]
+        flat = torch.empty(sum(pad), dtype=self.dtype, device=ps[0].device)
+        outs, off = [], 0
+        for p, n in zip(ps, pad):
+            outs.append(flat[off:off + p.numel()].view(p.shape))
+            off += n
+        noop = torch.zeros(1, dtype=torch.int32, device=ps[0].device)
+        _native.require().mt.scale(noop, [[p.detach() for p in ps], outs], 1.0)
+        _CAST_CACHE = {id(p): o for p, o in zip(ps, outs)}
+        return self
+
+    def __exit__(self, *exc):
+        global _CAST_CACHE
+        _CAST_CACHE = self.prev
+        return False
 
 
 def _wgrad(dy2, x2, dtype):

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from .. import _native
 from ..normalization import FusedLayerNorm, fused_add_dropout_layer_norm
-from ..fused_dense import fused_dense_function, fused_dense_gelu_dense_function
+from ..fused_dense import cast_params_once, fused_dense_function, fused_dense_gelu_dense_function
 from ..ops import attention as fused_attn
 
 
@@ -144,6 +144,16 @@ class GPT2LMHeadModel(nn.Module):
         s = input_ids.size(1)
         pos = torch.arange(s, device=input_ids.device).unsqueeze(0)
         x = self.drop(self.wte(input_ids) + self.wpe(pos))
+        if self.config.fused_dense and x.is_cuda and torch.is_autocast_enabled("cuda"):
+            # O1: every dense weight / bias cast to the GEMM dtype in one launch
+            dense = [p for blk in self.h for m in (blk.attn.c_attn, blk.attn.c_proj,
+                                                   blk.mlp.c_fc, blk.mlp.c_proj)
+                     for p in (m.weight, m.bias)]
+            with cast_params_once(dense, torch.get_autocast_dtype("cuda")):
+                return self._blocks(x)
+        return self._blocks(x)
+
+    def _blocks(self, x):
         if self.config.fused_residual_ln:
             y = self.h[0].ln_1(x)
             for i, block in enumerate(self.h):
