@@ -1,12 +1,16 @@
 """O1 ("patch torch functions") on top of ``torch.autocast``, plus the user cast
 registries (apex@f3a960f8 apex/amp/amp.py + wrap.py + utils.py).
 
-Apex O1 monkey-patches every function in its FP16/FP32/promote tables.  On
-PyTorch 2.10 the same policy is implemented natively by the autocast dispatch
-key, whose op lists match Apex's (see amp/lists/ for the Apex tables and the
-mapping notes).  ``init()`` enables autocast for the calling thread globally -
-exactly the scope of Apex's global patching - and ``disable_casts()`` turns it
-off for a region.  The user registries keep Apex's decorator API.
+Apex O1 monkey-patches every function in its FP16/FP32/promote tables
+(amp/lists/).  On PyTorch 2.10 nearly all of that policy is implemented
+natively (in C++, no Python per call) by the autocast dispatch key, so
+``init()`` enables autocast for the calling thread - the scope of Apex's global
+patching - and ``disable_casts()`` turns it off for a region.  The entries of
+Apex's tables on which autocast decides differently are found by
+``amp.lists.audit`` (every table entry is called and its output dtype checked;
+tests/test_amp_o1_tables.py) and patched here with Apex's decision
+(``APEX_POLICY_OVERRIDES``), active only while autocast is on in the calling
+thread.  The user registries keep Apex's decorator API.
 """
 from __future__ import annotations
 
@@ -50,13 +54,14 @@ def _widest(args):
 
 
 def _no_autocast(fn_call):
-    dev = "cuda" if torch.cuda.is_available() else "cpu"
-    prev = torch.is_autocast_enabled(dev)
-    torch.set_autocast_enabled(dev, False)
+    prev = {d: torch.is_autocast_enabled(d) for d in ("cuda", "cpu")}
+    for d in prev:
+        torch.set_autocast_enabled(d, False)
     try:
         return fn_call()
     finally:
-        torch.set_autocast_enabled(dev, prev)
+        for d, v in prev.items():
+            torch.set_autocast_enabled(d, v)
 
 
 def half_function(fn):
@@ -85,6 +90,54 @@ def promote_function(fn):
             return fn(*args, **kwargs)
         return _no_autocast(lambda: fn(*_cast(args, dt), **_cast(kwargs, dt)))
     return wrapper
+
+
+def _autocast_on():
+    return torch.is_autocast_enabled("cuda") or torch.is_autocast_enabled("cpu")
+
+
+def _policy_float(fn):
+    """Apex FP32_FUNCS entry that autocast leaves in the input dtype: under
+    autocast, run it in fp32 (floating args cast, autocast off inside)."""
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        if not _autocast_on():
+            return fn(*args, **kwargs)
+        return _no_autocast(lambda: fn(*_cast(args, torch.float32),
+                                       **_cast(kwargs, torch.float32)))
+    wrapper._amp_policy_original = fn
+    return wrapper
+
+
+# Apex FP32_FUNCS entries whose autocast (CUDA, fp16 and bf16) policy differs:
+# autocast runs them in the input dtype.  Found by amp.lists.audit.
+APEX_POLICY_OVERRIDES = (
+    ("torch", "std"), ("torch", "var"),
+    ("tensor", "std"), ("tensor", "var"),
+    ("F", "gelu"), ("F", "grid_sample"),
+)
+_POLICY_APPLIED = []
+
+
+def _ns(name):
+    import torch.nn.functional as F
+    return {"torch": torch, "tensor": torch.Tensor, "F": F}[name]
+
+
+def _apply_policy_overrides():
+    if _POLICY_APPLIED:
+        return
+    for ns, name in APEX_POLICY_OVERRIDES:
+        mod = _ns(ns)
+        orig = getattr(mod, name)
+        setattr(mod, name, _policy_float(orig))
+        _POLICY_APPLIED.append((mod, name, orig))
+
+
+def _restore_policy_overrides():
+    while _POLICY_APPLIED:
+        mod, name, orig = _POLICY_APPLIED.pop()
+        setattr(mod, name, orig)
 
 
 def _register(module, name, kind):
@@ -154,6 +207,7 @@ def init(enabled=True, loss_scale="dynamic", enable_caching=True, verbose=False,
 
         register_float_function(F, "binary_cross_entropy")
     _amp_state.handle = handle
+    _apply_policy_overrides()
     _apply_registries()
     _DECORATOR_HANDLE = handle
     return handle
@@ -164,4 +218,5 @@ def deinit():
     h = getattr(_amp_state, "handle", None)
     if h is not None:
         h._deactivate()
+    _restore_policy_overrides()
     _restore_registries()

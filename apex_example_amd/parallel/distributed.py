@@ -18,6 +18,19 @@ Bucket size (``message_size``, elements): Apex's default 1e7 elements.  On an
 (~153 GB/s each); RCCL's ring/tree channels spread one collective over those
 links, so a bucket only needs to be large enough to amortise RCCL's per-call
 latency (tens of us) - see docs/DDP_TUNING.md and tools/allreduce_sweep.py.
+
+Communicators (RCCL): the buckets go to a DEDICATED process group whose HIP
+streams are created high-priority (``ProcessGroupNCCL.Options
+(is_high_priority_stream=True)``), not to the default group: bucket
+all-reduces are then scheduled ahead of the backward kernels they overlap, and
+they never queue behind (or interleave with) collectives other code issues on
+the default group - SyncBatchNorm uses its own communicator as well
+(``parallel.sync_batchnorm``).
+
+Precision: bf16 buckets are all-reduced in fp32 by default (RCCL rounds the
+running sum to the wire dtype at every ring hop; with an 8-bit mantissa that
+costs ~3 bits over 8 ranks) - ``allreduce_always_fp32=None`` means "fp32 for
+bf16 buckets, native for fp16" (Apex's fp16 behaviour); True / False force it.
 """
 from __future__ import annotations
 
@@ -124,15 +137,20 @@ class DistributedDataParallel(Module):
 
     Extensions: ``process_group``, ``allow_unused`` (tolerate params without
     grads), ``bucket_align`` (elements; views 16-B aligned for vector kernels),
-    ``use_avg_op`` (ReduceOp.AVG instead of SUM + scale; default on for RCCL).
+    ``use_avg_op`` (ReduceOp.AVG instead of SUM + scale; default on for RCCL),
+    ``high_priority_streams`` (RCCL: a dedicated bucket communicator on
+    high-priority streams; default on), ``force_collectives`` (issue the bucket
+    all-reduces even at world size 1 - test hook for 1-GPU boxes),
+    ``allreduce_always_fp32=None`` (auto: fp32 accumulation for bf16 buckets).
     """
 
     def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,
                  allreduce_trigger_params=None, retain_allreduce_buffers=False,
-                 allreduce_always_fp32=False, num_allreduce_streams=1,
+                 allreduce_always_fp32=None, num_allreduce_streams=1,
                  allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
-                 process_group=None, allow_unused=False, bucket_align=64, use_avg_op=None):
+                 process_group=None, allow_unused=False, bucket_align=64, use_avg_op=None,
+                 high_priority_streams=True, force_collectives=False):
         super().__init__()
         if not dist.is_initialized():
             raise RuntimeError("DistributedDataParallel requires torch.distributed to be "
@@ -166,17 +184,23 @@ class DistributedDataParallel(Module):
         if use_avg_op is None:
             use_avg_op = self.backend == "nccl"
         self.use_avg_op = bool(use_avg_op)
+        self.force_collectives = bool(force_collectives)
         self._trigger_params = allreduce_trigger_params
         self.custom_allreduce_triggers = allreduce_trigger_params is not None
 
+        self.high_priority_streams = bool(high_priority_streams) and self.backend == "nccl"
         self._bucket_pgs = None
+        self._comm_pg = process_group
         if allreduce_communicators is not None:
             self._bucket_pgs = list(allreduce_communicators[0] if isinstance(
                 allreduce_communicators, tuple) else allreduce_communicators)
             self.num_allreduce_streams = len(self._bucket_pgs)
         elif num_allreduce_streams > 1:
-            ranks = list(range(self.world_size))
-            self._bucket_pgs = [dist.new_group(ranks=ranks) for _ in range(num_allreduce_streams)]
+            self._bucket_pgs = [self._new_comm_group() for _ in range(num_allreduce_streams)]
+        elif self.high_priority_streams and (self.world_size > 1 or self.force_collectives):
+            # every rank constructs DDP in the same order, so this collective
+            # group creation lines up across ranks
+            self._comm_pg = self._new_comm_group()
 
         self.active_params = self._collect_params()
         if self.backend == "nccl":
@@ -190,6 +214,20 @@ class DistributedDataParallel(Module):
         self._build_reducer()
 
     # ------------------------------------------------------------------ internals
+    def _new_comm_group(self):
+        ranks = (list(range(dist.get_world_size())) if self.process_group is None
+                 else dist.get_process_group_ranks(self.process_group))
+        if self.backend == "nccl" and self.high_priority_streams:
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            return dist.new_group(ranks=ranks, pg_options=opts)
+        return dist.new_group(ranks=ranks)
+
+    def _fp32_mode(self):
+        if self.allreduce_always_fp32 is None:
+            return 2  # bf16 buckets in fp32, fp16 / fp32 native
+        return 1 if self.allreduce_always_fp32 else 0
+
     def _collect_params(self):
         seen = set()
         params = []
@@ -201,17 +239,18 @@ class DistributedDataParallel(Module):
 
     def _build_reducer(self):
         C = _native.require()
-        pg = self.process_group if self.process_group is not None else dist.group.WORLD
+        pg = self._comm_pg if self._comm_pg is not None else dist.group.WORLD
         triggers = []
         if self._trigger_params is not None:
             ids = {id(p) for p in self._trigger_params}
             triggers = [i for i, p in enumerate(self.active_params) if id(p) in ids]
         self.reducer = C.reducer.Reducer(self.active_params, pg, self.message_size,
-                                         self.allreduce_always_fp32,
+                                         self._fp32_mode(),
                                          float(self.gradient_predivide_factor),
                                          self.gradient_average, self.delay_allreduce,
                                          self.use_avg_op, triggers, int(self.bucket_align))
         self.reducer.set_allow_unused(self.allow_unused)
+        self.reducer.set_force_collectives(self.force_collectives)
         if self._bucket_pgs:
             self.reducer.set_bucket_process_groups(self._bucket_pgs)
         for p in self.active_params:
@@ -254,6 +293,24 @@ class DistributedDataParallel(Module):
     def bucket_layout(self):
         """List of buckets, each a list of indices into ``active_params``."""
         return [list(b) for b in self.reducer.layout()]
+
+    def enable_bucket_timing(self, on=True):
+        """Record HIP events around every bucket (see ``bucket_timing``)."""
+        self.reducer.set_timing(bool(on))
+
+    def bucket_timing(self):
+        """Timing of the last backward (needs ``enable_bucket_timing()``), in ms
+        from the first gradient: ``{"backward_ms", "exposed_tail_ms",
+        "launch_ms": [...], "joined_ms": [...], "bucket_numel": [...]}``.
+        ``exposed_tail_ms`` is the time between the end of backward and the
+        compute stream having joined every bucket's all-reduce - the part of
+        the communication that overlap did not hide.  None if nothing timed."""
+        t = list(self.reducer.timing())
+        if not t:
+            return None
+        nb = (len(t) - 2) // 2
+        return {"backward_ms": t[0], "exposed_tail_ms": t[1], "launch_ms": t[2:2 + nb],
+                "joined_ms": t[2 + nb:], "bucket_numel": list(self.reducer.bucket_numels())}
 
     def zero_grad_buckets(self):
         """Zero every gradient with one memset per bucket (grads stay views)."""

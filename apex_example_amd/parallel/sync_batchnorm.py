@@ -8,6 +8,14 @@ running-stat momentum update with the unbiased global variance, fused
 normalise (+z)(+ReLU).  Backward: local reduction, ONE packed all_reduce of
 [sum_dy, sum_dy_xmu], fused elementwise dx (+dz).  Collectives run over RCCL
 (nccl backend) on MI355X or gloo on CPU.
+
+Communicator: with ``process_group=None`` the layers share ONE dedicated
+process group over all ranks (created on first use - every rank reaches its
+first SyncBN forward in the same order, so the collective creation lines up),
+with high-priority HIP streams under RCCL.  These per-layer collectives are
+latency-bound and sit on the critical path (the compute stream waits on them at
+once), so they must not queue behind DDP's multi-MB bucket all-reduces, which
+run on their own communicator (``parallel.distributed``).
 """
 from __future__ import annotations
 
@@ -18,6 +26,32 @@ from torch.nn.modules.batchnorm import _BatchNorm
 
 from .. import _native
 from ..ops.batch_norm import BatchNormFunction
+
+
+_COMM_GROUPS = {}
+
+
+def syncbn_comm_group():
+    """The dedicated SyncBN process group for the current world (see module doc)."""
+    key = id(dist.group.WORLD)
+    g = _COMM_GROUPS.get(key)
+    if g is not None:
+        try:  # destroyed by destroy_process_group() (a new world may reuse the id)
+            alive = g in dist.distributed_c10d._world.pg_map
+        except AttributeError:
+            alive = True
+        if not alive:
+            g = None
+    if g is None:
+        if dist.get_backend() == "nccl":
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            g = dist.new_group(ranks=list(range(dist.get_world_size())), pg_options=opts)
+        else:
+            g = dist.new_group(ranks=list(range(dist.get_world_size())))
+        _COMM_GROUPS.clear()
+        _COMM_GROUPS[key] = g
+    return g
 
 
 class SyncBatchNorm(_BatchNorm):
@@ -83,6 +117,8 @@ class SyncBatchNorm(_BatchNorm):
         pg = self.process_group
         if not (dist.is_available() and dist.is_initialized()):
             pg = False
+        elif pg is None and dist.get_world_size() > 1:
+            pg = syncbn_comm_group()
         return BatchNormFunction.apply(input, z, self.weight, self.bias,
                                        self.running_mean if self.track_running_stats else None,
                                        self.running_var if self.track_running_stats else None,

@@ -5,6 +5,13 @@ for the whole job (BASELINE.json metric), 1..8 MI355X, one process per GPU.
     python bench.py [--gpus N] [--steps K] [--warmup W] [...]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Without torchrun (WORLD_SIZE unset) and --gpus N > 1, bench.py starts the N
+rank processes itself (one per GPU, child processes started BEFORE anything
+touches the GPU in the parent, 127.0.0.1 rendezvous) and exits with the worst
+child status.  Every rank checks that the world it joined has exactly --gpus
+ranks and exits non-zero otherwise (the reference derives its process count
+from --gpus the same way: test_apex_distributed_spawn.py:42,53-57).
+
 Step = forward + loss + amp.scale_loss backward (+ bucketed RCCL all-reduce
 overlapped with backward when N > 1) + FusedSGD step (momentum 0.9, wd 5e-5,
 fp32 master weights, bf16 model copy written in-kernel).  Synthetic ImageNet
@@ -81,8 +88,65 @@ def parse():
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="MIOpen find (solver search) instead of immediate mode")
     ap.add_argument("--opt-step-iters", type=int, default=20)
+    ap.add_argument("--bucket-timing-steps", type=int, default=5,
+                    help="N > 1: extra untimed steps with per-bucket DDP timing (0 = off)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--loss-trace", action="store_true",
+                    help="keep every step's loss (device scalars, read after timing) in the JSON")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + rendezvous + world-size check only (launcher tests)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """Start ranks 0..n-1 of this same command as child processes and wait.
+
+    Runs before any GPU call in this (parent) process: counting devices does not
+    initialise HIP.  A child that fails takes the others down (they would block
+    in a collective otherwise).  Returns the exit code for the parent."""
+    import subprocess
+
+    ndev = torch.cuda.device_count()
+    if (ndev < n and os.environ.get("APEX_AMD_SINGLE_DEVICE") != "1"
+            and os.environ.get("APEX_AMD_FORCE_CPU") != "1"):
+        print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, ndev), file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   APEX_AMD_BENCH_LAUNCHER="self-spawn")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 128 - code)
+                for q in alive:
+                    q.terminate()
+        if alive:
+            time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
 
 
 def log(rank, *a):
@@ -127,6 +191,7 @@ def build_resnet(args, device, world):
                                     verbosity=0)
         if world > 1:
             model = DistributedDataParallel(model, message_size=args.message_size)
+            w.ddp = model
 
         def step(b):
             out = model(b[0])
@@ -198,6 +263,7 @@ def build_bert(args, device, world):
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
         if world > 1:
             model = DistributedDataParallel(model, message_size=args.message_size)
+            w.ddp = model
 
         def step(b):
             mlm, nsp = model(b[0], b[1], b[2])
@@ -259,6 +325,7 @@ def build_gpt2(args, device, world):
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
         if world > 1:
             model = DistributedDataParallel(model, message_size=args.message_size)
+            w.ddp = model
 
         def step(b):
             loss = lm_loss(model(b[0]), b[0], fused=not args.no_fused_loss)
@@ -298,14 +365,83 @@ def build_gpt2(args, device, world):
     return w
 
 
+def ddp_timing(ddp, step, batch, steps, device):
+    """Per-bucket DDP timing over a few extra (untimed) steps: when each bucket's
+    all-reduce was launched during backward, the exposed post-backward tail
+    (end of backward -> every collective joined), and the same buckets
+    all-reduced back to back with nothing else running (the comm-only cost the
+    overlap has to hide).  Max over ranks."""
+    ddp.enable_bucket_timing(True)
+    tails, bwd, launches = [], [], None
+    for _ in range(steps):
+        step(batch)
+        t = ddp.bucket_timing()
+        if t is None:
+            continue
+        tails.append(t["exposed_tail_ms"])
+        bwd.append(t["backward_ms"])
+        launches = t["launch_ms"]
+        numels = t["bucket_numel"]
+    ddp.enable_bucket_timing(False)
+    if not tails:
+        return None
+    bufs = ddp.allreduce_buffers
+    pg = ddp._comm_pg
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    for i in range(reps + 1):
+        if i == 1:
+            e0.record()
+        for b in bufs:
+            cb = b.float() if (b.dtype == torch.bfloat16 and ddp._fp32_mode() == 2) else b
+            dist.all_reduce(cb, group=pg)
+    e1.record()
+    torch.cuda.synchronize()
+    comm_ms = e0.elapsed_time(e1) / reps
+    ddp.zero_grad_buckets()  # the buckets above were summed, not averaged
+    v = torch.tensor([sum(tails) / len(tails), sum(bwd) / len(bwd), comm_ms],
+                     dtype=torch.float64, device=device)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    tail, bw, comm = [float(x) for x in v.tolist()]
+    return {
+        "buckets": len(numels),
+        "bucket_mb": [round(n * bufs[i].element_size() / 2**20, 2) for i, n in enumerate(numels)],
+        "message_size": ddp.message_size,
+        "allreduce_fp32_accumulate_bf16": ddp._fp32_mode() == 2,
+        "high_priority_streams": ddp.high_priority_streams,
+        "backward_ms": round(bw, 3),
+        "exposed_tail_ms": round(tail, 3),
+        "comm_only_ms": round(comm, 3),
+        "launch_ms": [round(x, 3) for x in launches],
+        "timing_steps": len(tails),
+    }
+
+
 def main():
     args = parse()
     from apex_example_amd.utils.dist import barrier, init_distributed
 
-    env_world = int(os.environ.get("WORLD_SIZE", "1"))
-    if env_world != args.gpus and env_world > 1:
-        print("warning: --gpus %d but WORLD_SIZE=%d" % (args.gpus, env_world), file=sys.stderr)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     rank, world, device = init_distributed()
+    if world != args.gpus:
+        print("bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s); refusing to "
+              "report a number for the wrong world size" % (args.gpus, world,
+                                                           os.environ.get("WORLD_SIZE")),
+              file=sys.stderr)
+        sys.exit(3)
+    if args.dry_run:
+        if world > 1:
+            barrier()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "backend":
+                              dist.get_backend() if world > 1 else None,
+                              "launcher": os.environ.get("APEX_AMD_BENCH_LAUNCHER", "single")}),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.backends.cudnn.benchmark = (not args.deterministic) and args.cudnn_benchmark
     torch.backends.cudnn.deterministic = args.deterministic
     torch.manual_seed(1234 + rank)
@@ -322,8 +458,11 @@ def main():
         args.impl, args.model, w.units, world, args.warmup, args.steps))
     t0 = time.time()
     loss = None
+    trace = [] if args.loss_trace else None
     for i in range(args.warmup):
         loss = step(batch)
+        if trace is not None:
+            trace.append(loss.detach())
         if i == 0 or (i + 1) % 5 == 0:
             torch.cuda.synchronize()
             log(rank, "[bench] warmup %d/%d loss %.4f (%.1fs)" % (i + 1, args.warmup, loss.item(),
@@ -367,6 +506,8 @@ def main():
     t_start = time.perf_counter()
     for _ in range(args.steps):
         loss = step(batch)
+        if trace is not None:
+            trace.append(loss.detach().clone())
     sync_all()
     torch.cuda.nvtx.range_pop()
     elapsed = time.perf_counter() - t_start
@@ -385,6 +526,11 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     opt_ms = e0.elapsed_time(e1) / args.opt_step_iters
+
+    ddp_stats = None
+    ddp = getattr(w, "ddp", None)
+    if world > 1 and ddp is not None and args.bucket_timing_steps > 0:
+        ddp_stats = ddp_timing(ddp, step, batch, args.bucket_timing_steps, device)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = w.units * world * args.steps / elapsed
@@ -408,7 +554,13 @@ def main():
         "config": w.config,
         "optimizer_step_ms": round(opt_ms, 4),
         "final_loss": round(final_loss, 4),
+        "launcher": os.environ.get("APEX_AMD_BENCH_LAUNCHER",
+                                   "torchrun" if world > 1 else "single"),
     }
+    if ddp_stats is not None:
+        rec["ddp"] = ddp_stats
+    if trace is not None:
+        rec["loss_trace"] = [round(float(v), 4) for v in trace]
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)

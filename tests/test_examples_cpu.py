@@ -108,3 +108,24 @@ def test_metrics_logger(tmp_path):
     assert [r["step"] for r in recs] == [3, 6]
     assert recs[0]["unit"] == "images/s" and recs[0]["throughput"] > 0
     assert recs[1]["model"] == "x" and abs(recs[1]["loss"] - 1 / 6) < 1e-6
+
+
+def test_bench_self_spawns_gpus_ranks():
+    """`python bench.py --gpus N` without torchrun starts N rank processes itself
+    (gloo on this CPU host) and every rank sees world size N."""
+    env = dict(os.environ, APEX_AMD_FORCE_CPU="1", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec == {"dry_run": True, "n_gpus": 3, "backend": "gloo", "launcher": "self-spawn"}
+
+
+def test_bench_refuses_world_mismatch():
+    env = dict(os.environ, APEX_AMD_FORCE_CPU="1", WORLD_SIZE="1", RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 3
+    assert "refusing" in p.stderr

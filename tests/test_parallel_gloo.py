@@ -150,3 +150,23 @@ def test_ddp_amp_stashed_fp32_grads(tmp_path, opt_level, fused):
     res = W.run("ddp_amp_vs_local", 2, str(tmp_path), opt_level=opt_level, fused=fused)
     for r in res:
         assert max(r["diffs"]) < 2e-2, r["diffs"]
+
+
+def test_ddp_bf16_buckets_reduce_in_fp32(tmp_path):
+    """Default (allreduce_always_fp32=None): bf16 buckets are reduced in fp32 and
+    rounded once - the result is the correctly rounded exact average.  Forcing
+    native bf16 accumulation is measurably worse (rounding at every add)."""
+    (tmp_path / "auto").mkdir()
+    (tmp_path / "native").mkdir()
+    auto = W.run("ddp_bf16_precision", 4, str(tmp_path / "auto"), fp32=None)
+    native = W.run("ddp_bf16_precision", 4, str(tmp_path / "native"), fp32=False)
+    exact = auto[0]["exact"]
+    rounded = exact.to(torch.bfloat16).float()
+    for r in auto:
+        assert torch.equal(r["grad"], rounded)
+    err_auto = (auto[0]["grad"] - exact).abs().max().item()
+    err_native = (native[0]["grad"] - exact).abs().max().item()
+    assert err_native >= err_auto
+    # relative error bound of ONE bf16 rounding (2^-9) for the fp32 path
+    rel = ((auto[0]["grad"] - exact).abs() / exact.abs().clamp_min(1e-3)).max().item()
+    assert rel <= 2 ** -8
