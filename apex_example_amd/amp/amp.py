@@ -114,7 +114,7 @@ def _policy_float(fn):
 APEX_POLICY_OVERRIDES = (
     ("torch", "std"), ("torch", "var"),
     ("tensor", "std"), ("tensor", "var"),
-    ("F", "gelu"), ("F", "grid_sample"),
+    ("F", "gelu"), ("F", "grid_sample"), ("F", "ctc_loss"),
 )
 _POLICY_APPLIED = []
 

@@ -92,19 +92,17 @@ def multi_tensor_adam(chunk_size, noop_flag, tensor_lists, lr, beta1, beta2, eps
               step_t, int(mode), bool(bias_correction), float(weight_decay), sv, st, scale_inv)
 
 
-def _lamb_workspace(params):
-    return [torch.empty_like(p, dtype=torch.float32) for p in params]
-
-
 def multi_tensor_lamb(chunk_size, noop_flag, tensor_lists, lr, beta1, beta2, epsilon, step,
                       bias_correction, weight_decay, grad_averaging, mode, global_grad_norm,
                       max_grad_norm, use_nvlamb=False, *, update_buffers=None, model_copies=None,
                       scale=1.0, scale_inv=False):
-    """tensor_lists = [grads, params, exp_avg, exp_avg_sq] (Apex).  The fp32 update
-    workspace is allocated here unless ``update_buffers`` is given."""
+    """tensor_lists = [grads, params, exp_avg, exp_avg_sq] (Apex).  The update
+    direction is recomputed from (p, m, v) in the second stage on the device, so
+    no fp32 workspace exists; ``update_buffers`` is accepted for API
+    compatibility and ignored."""
+    del update_buffers
     g, p, m, v = tensor_lists[:4]
-    u = update_buffers if update_buffers is not None else _lamb_workspace(p)
-    lists = [list(g), list(p), list(m), list(v), list(u)]
+    lists = [list(g), list(p), list(m), list(v)]
     if model_copies is not None:
         lists.append(list(model_copies))
     lv, lt = _split(lr)

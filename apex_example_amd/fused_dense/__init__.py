@@ -15,6 +15,9 @@ cast); bias gradients are reduced in fp32 and written in the bias's dtype.
 """
 from __future__ import annotations
 
+import collections
+import threading
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -31,17 +34,28 @@ def _compute_dtype(x):
     return x.dtype
 
 
-# {id(param): 16-bit copy} while a cast_params_once() block runs
-_CAST_CACHE = None
+# Per-thread state (nn.DataParallel runs replica forwards in threads):
+#   active: {id(param): (param, 16-bit copy)} while a cast_params_once() block runs
+#   bufs:   persistent flat buffers, one per parameter list (LRU of _MAX_BUFS)
+_TLS = threading.local()
+_MAX_BUFS = 4
+
+
+def _tls():
+    if not hasattr(_TLS, "active"):
+        _TLS.active, _TLS.bufs = None, collections.OrderedDict()
+    return _TLS
 
 
 def _cast(t, dt):
     if t is None or t.dtype == dt:
         return t
-    if _CAST_CACHE is not None:
-        c = _CAST_CACHE.get(id(t))
-        if c is not None and c.dtype == dt:
-            return c
+    active = _tls().active
+    if active is not None:
+        e = active.get(id(t))
+        # identity + shape check: a recycled id() never matches a stale copy
+        if e is not None and e[0] is t and e[1].dtype == dt and e[1].shape == t.shape:
+            return e[1]
     return t.to(dt)
 
 
@@ -51,32 +65,51 @@ class cast_params_once:
     with factor 1: plain round-to-nearest casts, the same values ``.to()`` gives),
     and the dense layers' ``_cast`` picks them up instead of launching one cast
     kernel per weight and bias (~200 small launches per GPT-2-medium step).
-    Re-cast on every entry, so an optimizer step between forwards is seen."""
+    Re-cast on every entry, so an optimizer step between forwards is seen.
+
+    The flat buffer (and the zeroed no-op flag) persist per parameter list, so
+    the data pointers - and with them the cached multi-tensor launch plan - are
+    the same every step.  Contract that follows: the copies a graph saved for
+    backward are refreshed by the next forward of the same parameter list, so
+    run a graph's backward before changing the weights and re-running forward
+    (every ordinary training loop does).  With grad disabled (eval / no_grad)
+    nothing is batched: per-layer casts are freed right after their GEMM
+    instead of keeping every 16-bit copy live for the whole forward."""
 
     def __init__(self, params, dtype):
         self.params, self.dtype, self.prev = params, dtype, None
 
     def __enter__(self):
-        global _CAST_CACHE
-        self.prev = _CAST_CACHE
+        st = _tls()
+        self.prev = st.active
+        if not torch.is_grad_enabled():
+            return self
         ps = [p for p in self.params if p.is_cuda and p.dtype == torch.float32]
         if not ps or not _native.available():
             return self
-        # each copy starts 16-byte aligned (8 halves): the kernel's vector path
-        pad = [(p.numel() + 7) // 8 * 8 for p in ps]
-        flat = torch.empty(sum(pad), dtype=self.dtype, device=ps[0].device)
-        outs, off = [], 0
-        for p, n in zip(ps, pad):
-            outs.append(flat[off:off + p.numel()].view(p.shape))
-            off += n
-        noop = torch.zeros(1, dtype=torch.int32, device=ps[0].device)
-        _native.require().mt.scale(noop, [[p.detach() for p in ps], outs], 1.0)
-        _CAST_CACHE = {id(p): o for p, o in zip(ps, outs)}
+        key = (self.dtype, ps[0].device, tuple(id(p) for p in ps))
+        ent = st.bufs.get(key)
+        if ent is None or any(a is not b or o.shape != b.shape
+                              for a, b, o in zip(ent[0], ps, ent[1])):
+            # each copy starts 16-byte aligned (8 halves): the kernel's vector path
+            pad = [(p.numel() + 7) // 8 * 8 for p in ps]
+            flat = torch.empty(sum(pad), dtype=self.dtype, device=ps[0].device)
+            outs, off = [], 0
+            for p, n in zip(ps, pad):
+                outs.append(flat[off:off + p.numel()].view(p.shape))
+                off += n
+            noop = torch.zeros(1, dtype=torch.int32, device=ps[0].device)
+            ent = (list(ps), outs, noop)
+            st.bufs[key] = ent
+            while len(st.bufs) > _MAX_BUFS:
+                st.bufs.popitem(last=False)
+        st.bufs.move_to_end(key)
+        _native.require().mt.scale(ent[2], [[p.detach() for p in ps], ent[1]], 1.0)
+        st.active = {id(p): (p, o) for p, o in zip(ps, ent[1])}
         return self
 
     def __exit__(self, *exc):
-        global _CAST_CACHE
-        _CAST_CACHE = self.prev
+        _tls().active = self.prev
         return False
 
 

@@ -28,12 +28,7 @@ class FusedAdagrad(FusedOptimizerBase):
         for gid, group in enumerate(self.param_groups):
             for key, s in self._launch_sets(gid, group).items():
                 dev = s["params"][0].device
-                h = []
-                for p in s["params"]:
-                    state = self.state[p]
-                    if len(state) == 0:
-                        state["sum"] = torch.zeros_like(p)
-                    h.append(state["sum"])
+                h, = self._state_lists(s, ("sum",))
                 scale_v, inv = self._scale_args(s["scaled"])
                 noop = self._noop(dev)
                 amp_C.multi_tensor_adagrad(65536, noop, [s["grads"], s["params"], h], group["lr"],

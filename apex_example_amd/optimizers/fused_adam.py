@@ -47,17 +47,8 @@ class FusedAdam(FusedOptimizerBase):
             step, step_t = self._step_value(gid, group, dev)
             noop = self._noop(dev)
             for key, s in sets.items():
-                m, v = [], []
-                for p in s["params"]:
-                    state = self.state[p]
-                    # State initialization
-                    if len(state) == 0:
-                        # Exponential moving average of gradient values
-                        state["exp_avg"] = torch.zeros_like(p)
-                        # Exponential moving average of squared gradient values
-                        state["exp_avg_sq"] = torch.zeros_like(p)
-                    m.append(state["exp_avg"])
-                    v.append(state["exp_avg_sq"])
+                # exponential moving averages of the gradient and its square
+                m, v = self._state_lists(s, ("exp_avg", "exp_avg_sq"))
                 lists = [s["grads"], s["params"], m, v]
                 if s["copies"] is not None:
                     lists.append(s["copies"])

@@ -5,10 +5,15 @@ Per step:
      deterministic multi-tensor l2norm (no host sync), divided by the loss scale
      when the grads are still scaled;
   2. one fused launch per dtype set: stage 1 (clip by global_norm/max_grad_norm,
-     Adam(W) moments, update into an fp32 workspace, per-chunk ||p||^2 and
-     ||u||^2 partials in the same pass) -> per-tensor norm finalize -> stage 2
-     (trust ratio ||p||/||u||, p -= lr*ratio*u, 16-bit model copy written in-pass
-     under amp O2).
+     Adam(W) moments, per-chunk ||p||^2 and ||u||^2 partials in the same pass;
+     u itself is not stored) -> per-tensor norm finalize -> stage 2 (u
+     recomputed from p, m, v; trust ratio ||p||/||u||, p -= lr*ratio*u, 16-bit
+     model copy written in-pass under amp O2).  No fp32 update workspace: the
+     optimizer's persistent memory is exactly m and v.
+
+``max_grad_norm`` is honoured per param group (Apex reads only the constructor
+default; a group without its own value gets that default, so Apex behaviour is
+unchanged).  The clip factor comes from the global norm over every group.
 """
 from __future__ import annotations
 
@@ -32,14 +37,6 @@ class FusedLAMB(FusedOptimizerBase):
                          materialize_master_grads=materialize_master_grads)
         self.adam_w_mode = 1 if adam_w_mode else 0
         self.use_nvlamb = use_nvlamb
-        self._workspaces = {}
-
-    def _workspace(self, p):
-        w = self._workspaces.get(id(p))
-        if w is None or w.shape != p.shape or w.device != p.device:
-            w = torch.empty_like(p, dtype=torch.float32)
-            self._workspaces[id(p)] = w
-        return w
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -73,7 +70,6 @@ class FusedLAMB(FusedOptimizerBase):
                 n = n * sv
             parts.append(n)
         global_grad_norm = parts[0] if len(parts) == 1 else torch.stack(parts).norm().reshape(1)
-        max_grad_norm = self.defaults["max_grad_norm"]
 
         for gid, group in enumerate(self.param_groups):
             sets = all_sets[gid]
@@ -84,22 +80,15 @@ class FusedLAMB(FusedOptimizerBase):
             grad_averaging = 1 if group["grad_averaging"] else 0
             step, step_t = self._step_value(gid, group, dev)
             for key, s in sets.items():
-                m, v = [], []
-                for p in s["params"]:
-                    state = self.state[p]
-                    if len(state) == 0:
-                        state["exp_avg"] = torch.zeros_like(p)
-                        state["exp_avg_sq"] = torch.zeros_like(p)
-                    m.append(state["exp_avg"])
-                    v.append(state["exp_avg_sq"])
-                u = [self._workspace(p) for p in s["params"]]
+                m, v = self._state_lists(s, ("exp_avg", "exp_avg_sq"))
                 scale_v, inv = self._scale_args(s["scaled"])
                 amp_C.multi_tensor_lamb(65536, noop, [s["grads"], s["params"], m, v], group["lr"],
                                         beta1, beta2, group["eps"],
                                         step_t if step_t is not None else step, bias_correction,
                                         group["weight_decay"], grad_averaging, self.adam_w_mode,
-                                        global_grad_norm, max_grad_norm, self.use_nvlamb,
-                                        update_buffers=u, model_copies=s["copies"], scale=scale_v,
+                                        global_grad_norm,
+                                        group.get("max_grad_norm", self.defaults["max_grad_norm"]),
+                                        self.use_nvlamb, model_copies=s["copies"], scale=scale_v,
                                         scale_inv=inv)
             self._after_step(gid, dev, step_t, noop)
         return loss

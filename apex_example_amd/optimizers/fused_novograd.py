@@ -55,12 +55,7 @@ class FusedNovoGrad(FusedOptimizerBase):
             if first:
                 group["exp_avg_sq"] = []
             for k, (key, s) in enumerate(sets.items()):
-                m = []
-                for p in s["params"]:
-                    state = self.state[p]
-                    if len(state) == 0:
-                        state["exp_avg"] = torch.zeros_like(p)
-                    m.append(state["exp_avg"])
+                m, = self._state_lists(s, ("exp_avg",))
                 _, gnorms = C.norm(scratch, s["grads"], True, group["norm_type"] == 0)
                 scale_v, inv = self._scale_args(s["scaled"])
                 if s["scaled"]:

@@ -83,7 +83,12 @@ class FusedSGD(FusedOptimizerBase):
             for key, s in self._launch_sets(gid, group).items():
                 params = s["params"]
                 dev = params[0].device
-                moms, first_run = self.get_momentums(params)
+                cached = s.get("_moms")
+                if cached is None:
+                    moms, first_run = self.get_momentums(params)
+                    s["_moms"] = moms
+                else:
+                    moms, first_run = cached, False
                 lists = [s["grads"], params, moms]
                 if s["copies"] is not None:
                     lists.append(s["copies"])

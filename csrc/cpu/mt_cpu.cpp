@@ -196,7 +196,7 @@ void lamb(at::Tensor& noop, const TensorLists& l, const Lamb& a) {
     at::Tensor p = f32(l[1][i]).contiguous();
     at::Tensor m = f32(l[2][i]).contiguous();
     at::Tensor v = f32(l[3][i]).contiguous();
-    at::Tensor u = l[4][i];
+    at::Tensor u = at::empty_like(p);
     const float* pg = g.data_ptr<float>();
     float* pp = p.data_ptr<float>();
     float* pm = m.data_ptr<float>();
@@ -223,8 +223,8 @@ void lamb(at::Tensor& noop, const TensorLists& l, const Lamb& a) {
     put(d1, p);
     put(d2, m);
     put(d3, v);
-    if (l.size() == 6) {
-      at::Tensor c = l[5][i];
+    if (l.size() == 5) {
+      at::Tensor c = l[4][i];
       c.copy_(p);
     }
   }

@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(kMTThreads) scale_kernel(MTLaunch L, ScaleArg 
     }
     st<TO>(c.t->ptr[1], c.start + off, cnt, al && cnt >= 8, v[u]);
   }
-  if (!finite) *noop = 1;
+  if (noop && !finite) *noop = 1;
 }
 
 template <typename TI>
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(kMTThreads) check_finite_kernel(MTLaunch L, in
 #pragma unroll
     for (int i = 0; i < 8; ++i) finite &= finite_f32(v[i]);
   }
-  if (!finite) *noop = 1;
+  if (noop && !finite) *noop = 1;
 }
 
 template <typename TX, typename TY, typename TO>
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(kMTThreads)
     }
     st<TO>(c.t->ptr[2], c.start + off, cnt, vec, o);
   }
-  if (!finite) *noop = 1;
+  if (noop && !finite) *noop = 1;
 }
 
 template <typename T>

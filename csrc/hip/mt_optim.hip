@@ -14,8 +14,17 @@
 //  * the loss-scale reciprocal, the lr and the step counter may come from device
 //    scalars, so the whole optimizer step is hipGraph-capturable;
 //  * LAMB stage 1 emits the per-chunk ||p||^2 and ||u||^2 partials in the same
-//    pass that produces u (saves two extra reads of p and u vs apex's
-//    stage1 -> l2norm -> l2norm -> stage2 sequence).
+//    pass that updates the moments, and stage 2 RECOMPUTES u from (p, m, v)
+//    instead of reading an fp32 update workspace: no 4 B/param persistent
+//    buffer (1.3 GB for BERT-large) and the same 42 B/param of traffic as
+//    apex's stage1 -> l2norm -> l2norm -> stage2 sequence minus its two norm
+//    passes;
+//  * every kernel is persistent (mt_pgrid: min(#chunks, CUs x k) workgroups
+//    walking the chunk list) and issues all of a tile's loads before any
+//    arithmetic: the stores of one 8-vector can no longer serialise the loads
+//    of the next (the table pointers may alias as far as the compiler knows).
+#include <cstdlib>
+
 #include "mt_device.h"
 
 namespace amd {
@@ -28,37 +37,46 @@ __device__ __forceinline__ float lr_of(const float* p, float v) { return p ? *p 
 template <typename TG, typename TP, typename TM, typename TC, int DEPTH>
 __global__ void __launch_bounds__(kMTThreads) sgd_kernel(MTLaunch L, SgdArgs a, const int* noop) {
   if (skip_step(noop)) return;
-  TileCtx c = tile_ctx(L);
-  const bool al = c.t->aligned;
   const float sc = get_scale(a.scale);
   const float lr = lr_of(a.lr_ptr, a.lr);
   const bool first = a.first_run_flag ? (*a.first_run_flag == 0) : (a.first_run != 0);
   const bool has_mom = a.momentum != 0.f;
+  const bool load_m = has_mom && !first;
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+    float g[kMTUnroll][8], p[kMTUnroll][8], m[kMTUnroll][8];
 #pragma unroll
-  for (int u = 0; u < kMTUnroll; ++u) {
-    int off = lane_off(u);
-    int cnt = c.n - off;
-    if (cnt <= 0) continue;
-    bool vec = al && cnt >= 8;
-    int64_t idx = c.start + off;
-    float g[8], p[8], m[8];
-    ld<TG>(c.t->ptr[0], idx, cnt, vec, g);
-    ld<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    if (has_mom && !first) ld<TM>(c.t->ptr[2], idx, cnt, vec, m);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float gi = g[i] * sc;
-      if (a.wd != 0.f && !a.wd_after_momentum) gi = fmaf(a.wd, p[i], gi);
-      if (has_mom) {
-        m[i] = first ? gi : fmaf(m[i], a.momentum, (1.f - a.dampening) * gi);
-        gi = a.nesterov ? fmaf(a.momentum, m[i], gi) : m[i];
-      }
-      if (a.wd != 0.f && a.wd_after_momentum) gi = fmaf(a.wd, p[i], gi);
-      p[i] = fmaf(-lr, gi, p[i]);
+    for (int u = 0; u < kMTUnroll; ++u) {
+      const int off = lane_off(u), cnt = c.n - off;
+      if (cnt <= 0) continue;
+      const bool vec = al && cnt >= 8;
+      const int64_t idx = c.start + off;
+      ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+      ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+      if (load_m) ld<TM>(c.t->ptr[2], idx, cnt, vec, m[u]);
     }
-    st<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    if (has_mom) st<TM>(c.t->ptr[2], idx, cnt, vec, m);
-    if (DEPTH == 4) st<TC>(c.t->ptr[3], idx, cnt, vec, p);
+#pragma unroll
+    for (int u = 0; u < kMTUnroll; ++u) {
+      const int off = lane_off(u), cnt = c.n - off;
+      if (cnt <= 0) continue;
+      const bool vec = al && cnt >= 8;
+      const int64_t idx = c.start + off;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float gi = g[u][i] * sc;
+        if (a.wd != 0.f && !a.wd_after_momentum) gi = fmaf(a.wd, p[u][i], gi);
+        if (has_mom) {
+          m[u][i] = first ? gi : fmaf(m[u][i], a.momentum, (1.f - a.dampening) * gi);
+          gi = a.nesterov ? fmaf(a.momentum, m[u][i], gi) : m[u][i];
+        }
+        if (a.wd != 0.f && a.wd_after_momentum) gi = fmaf(a.wd, p[u][i], gi);
+        p[u][i] = fmaf(-lr, gi, p[u][i]);
+      }
+      st<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+      if (has_mom) st<TM>(c.t->ptr[2], idx, cnt, vec, m[u]);
+      if (DEPTH == 4) st<TC>(c.t->ptr[3], idx, cnt, vec, p[u]);
+    }
   }
 }
 
@@ -72,18 +90,22 @@ void mt_sgd(const MTLaunch& L, int depth, DType g, DType p, DType m, DType copy,
       using TG = decltype(tg);
       using TP = decltype(tp);
       if (depth == 3) {
-        hipLaunchKernelGGL((sgd_kernel<TG, TP, TP, TP, 3>), mt_grid(L), dim3(kMTThreads), 0, st,
+        hipLaunchKernelGGL((sgd_kernel<TG, TP, TP, TP, 3>), mt_pgrid(L), dim3(kMTThreads), 0, st,
                            L, a, noop);
       } else {
         dispatch1(copy, [&](auto tc) {
           using TC = decltype(tc);
-          hipLaunchKernelGGL((sgd_kernel<TG, TP, TP, TC, 4>), mt_grid(L), dim3(kMTThreads), 0, st,
-                             L, a, noop);
+          hipLaunchKernelGGL((sgd_kernel<TG, TP, TP, TC, 4>), mt_pgrid(L), dim3(kMTThreads), 0,
+                             st, L, a, noop);
         });
       }
     });
   });
 }
+
+// Adam / LAMB keep 4 state arrays per 8-vector: half a tile's vectors per pass
+// (64 instead of 128 data VGPRs) doubles the resident waves per SIMD.
+constexpr int UA = 2;
 
 // --------------------------------------------------------------------------
 // Adam / AdamW
@@ -101,8 +123,6 @@ __device__ __forceinline__ void bias_corrections(int bias_correction, float b1, 
 template <typename TG, typename TP, typename TC, int DEPTH>
 __global__ void __launch_bounds__(kMTThreads) adam_kernel(MTLaunch L, AdamArgs a, const int* noop) {
   if (skip_step(noop)) return;
-  TileCtx c = tile_ctx(L);
-  const bool al = c.t->aligned;
   const float sc = get_scale(a.scale);
   const float lr = lr_of(a.lr_ptr, a.lr);
   const int step = a.step_ptr ? (*a.step_ptr + 1) : a.step;
@@ -110,33 +130,46 @@ __global__ void __launch_bounds__(kMTThreads) adam_kernel(MTLaunch L, AdamArgs a
   bias_corrections(a.bias_correction, a.beta1, a.beta2, step, bc1, bc2);
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = rsqrtf(bc2);
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+#pragma unroll 1
+    for (int h = 0; h < kMTUnroll / UA; ++h) {
+      float g[UA][8], p[UA][8], m[UA][8], v[UA][8];
 #pragma unroll
-  for (int u = 0; u < kMTUnroll; ++u) {
-    int off = lane_off(u);
-    int cnt = c.n - off;
-    if (cnt <= 0) continue;
-    bool vec = al && cnt >= 8;
-    int64_t idx = c.start + off;
-    float g[8], p[8], m[8], v[8];
-    ld<TG>(c.t->ptr[0], idx, cnt, vec, g);
-    ld<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    ld<TP>(c.t->ptr[2], idx, cnt, vec, m);
-    ld<TP>(c.t->ptr[3], idx, cnt, vec, v);
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+        ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+        ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+        ld<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+        ld<TP>(c.t->ptr[3], idx, cnt, vec, v[u]);
+      }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float gi = g[i] * sc;
-      if (a.mode == 0) gi = fmaf(a.wd, p[i], gi);
-      m[i] = fmaf(a.beta1, m[i], (1.f - a.beta1) * gi);
-      v[i] = fmaf(a.beta2, v[i], (1.f - a.beta2) * gi * gi);
-      float denom = sqrtf(v[i]) * inv_sqrt_bc2 + a.eps;
-      float upd = (m[i] / denom) * step_size;
-      if (a.mode == 1) upd = fmaf(lr * a.wd, p[i], upd);
-      p[i] -= upd;
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float gi = g[u][i] * sc;
+          if (a.mode == 0) gi = fmaf(a.wd, p[u][i], gi);
+          m[u][i] = fmaf(a.beta1, m[u][i], (1.f - a.beta1) * gi);
+          v[u][i] = fmaf(a.beta2, v[u][i], (1.f - a.beta2) * gi * gi);
+          const float denom = sqrtf(v[u][i]) * inv_sqrt_bc2 + a.eps;
+          float upd = (m[u][i] / denom) * step_size;
+          if (a.mode == 1) upd = fmaf(lr * a.wd, p[u][i], upd);
+          p[u][i] -= upd;
+        }
+        st<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+        st<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+        st<TP>(c.t->ptr[3], idx, cnt, vec, v[u]);
+        if (DEPTH == 5) st<TC>(c.t->ptr[4], idx, cnt, vec, p[u]);
+      }
     }
-    st<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    st<TP>(c.t->ptr[2], idx, cnt, vec, m);
-    st<TP>(c.t->ptr[3], idx, cnt, vec, v);
-    if (DEPTH == 5) st<TC>(c.t->ptr[4], idx, cnt, vec, p);
   }
 }
 
@@ -148,13 +181,13 @@ void mt_adam(const MTLaunch& L, int depth, DType g, DType p, DType copy, const A
       using TG = decltype(tg);
       using TP = decltype(tp);
       if (depth == 4) {
-        hipLaunchKernelGGL((adam_kernel<TG, TP, TP, 4>), mt_grid(L), dim3(kMTThreads), 0, st, L, a,
-                           noop);
+        hipLaunchKernelGGL((adam_kernel<TG, TP, TP, 4>), mt_pgrid(L), dim3(kMTThreads), 0, st, L,
+                           a, noop);
       } else {
         dispatch1(copy, [&](auto tc) {
           using TC = decltype(tc);
-          hipLaunchKernelGGL((adam_kernel<TG, TP, TC, 5>), mt_grid(L), dim3(kMTThreads), 0, st, L,
-                             a, noop);
+          hipLaunchKernelGGL((adam_kernel<TG, TP, TC, 5>), mt_pgrid(L), dim3(kMTThreads), 0, st,
+                             L, a, noop);
         });
       }
     });
@@ -163,89 +196,132 @@ void mt_adam(const MTLaunch& L, int depth, DType g, DType p, DType copy, const A
 
 // --------------------------------------------------------------------------
 // LAMB
+struct LambConsts {
+  float bc1, bc2, beta3, gmul;
+};
+
+__device__ __forceinline__ LambConsts lamb_consts(const LambArgs& a) {
+  LambConsts k;
+  const int step = a.step_ptr ? (*a.step_ptr + 1) : a.step;
+  bias_corrections(a.bias_correction, a.beta1, a.beta2, step, k.bc1, k.bc2);
+  k.beta3 = a.grad_averaging ? (1.f - a.beta1) : 1.f;
+  const float gn = a.global_grad_norm ? *a.global_grad_norm : 0.f;
+  const float clip = (a.max_grad_norm > 0.f && gn > a.max_grad_norm) ? gn / a.max_grad_norm : 1.f;
+  k.gmul = get_scale(a.scale) / clip;
+  return k;
+}
+
+// the update direction from the (already updated) moments: stage 1 uses it for
+// ||u||, stage 2 recomputes it bit-identically for the parameter update
+__device__ __forceinline__ float lamb_update(const LambArgs& a, const LambConsts& k, float m,
+                                             float v, float p) {
+  const float mh = m / k.bc1;
+  const float vh = v / k.bc2;
+  float uu = mh / (sqrtf(vh) + a.eps);
+  if (a.mode == 1) uu = fmaf(a.wd, p, uu);
+  return uu;
+}
+
 template <typename TG, typename TP>
 __global__ void __launch_bounds__(kMTThreads)
     lamb_stage1_kernel(MTLaunch L, LambArgs a, float* partials, const int* noop) {
   __shared__ float scratch[kMTThreads / kWave];
   if (skip_step(noop)) return;
-  TileCtx c = tile_ctx(L);
-  const bool al = c.t->aligned;
-  const float sc = get_scale(a.scale);
-  const int step = a.step_ptr ? (*a.step_ptr + 1) : a.step;
-  float bc1, bc2;
-  bias_corrections(a.bias_correction, a.beta1, a.beta2, step, bc1, bc2);
-  const float beta3 = a.grad_averaging ? (1.f - a.beta1) : 1.f;
-  float gn = a.global_grad_norm ? *a.global_grad_norm : 0.f;
-  const float clip = (a.max_grad_norm > 0.f && gn > a.max_grad_norm) ? gn / a.max_grad_norm : 1.f;
-  const float gmul = sc / clip;
-  float pn2 = 0.f, un2 = 0.f;
+  const LambConsts k = lamb_consts(a);
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+    float pn2 = 0.f, un2 = 0.f;
+#pragma unroll 1
+    for (int h = 0; h < kMTUnroll / UA; ++h) {
+      float g[UA][8], p[UA][8], m[UA][8], v[UA][8];
 #pragma unroll
-  for (int u = 0; u < kMTUnroll; ++u) {
-    int off = lane_off(u);
-    int cnt = c.n - off;
-    if (cnt <= 0) continue;
-    bool vec = al && cnt >= 8;
-    int64_t idx = c.start + off;
-    float g[8], p[8], m[8], v[8], up[8];
-    ld<TG>(c.t->ptr[0], idx, cnt, vec, g);
-    ld<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    ld<TP>(c.t->ptr[2], idx, cnt, vec, m);
-    ld<TP>(c.t->ptr[3], idx, cnt, vec, v);
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+        ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+        ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+        ld<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+        ld<TP>(c.t->ptr[3], idx, cnt, vec, v[u]);
+      }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float gi = g[i] * gmul;
-      if (a.mode == 0) gi = fmaf(a.wd, p[i], gi);
-      m[i] = fmaf(a.beta1, m[i], beta3 * gi);
-      v[i] = fmaf(a.beta2, v[i], (1.f - a.beta2) * gi * gi);
-      float mh = m[i] / bc1;
-      float vh = v[i] / bc2;
-      float uu = mh / (sqrtf(vh) + a.eps);
-      if (a.mode == 1) uu = fmaf(a.wd, p[i], uu);
-      up[i] = (i < cnt) ? uu : 0.f;
-      float pi = (i < cnt) ? p[i] : 0.f;
-      pn2 = fmaf(pi, pi, pn2);
-      un2 = fmaf(up[i], up[i], un2);
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float gi = g[u][i] * k.gmul;
+          if (a.mode == 0) gi = fmaf(a.wd, p[u][i], gi);
+          m[u][i] = fmaf(a.beta1, m[u][i], k.beta3 * gi);
+          v[u][i] = fmaf(a.beta2, v[u][i], (1.f - a.beta2) * gi * gi);
+          // m / v are stored in TP: recompute u from the ROUNDED values stage 2 reads
+          m[u][i] = to_f32(from_f32<TP>(m[u][i]));
+          v[u][i] = to_f32(from_f32<TP>(v[u][i]));
+          const float uu = (i < cnt) ? lamb_update(a, k, m[u][i], v[u][i], p[u][i]) : 0.f;
+          const float pi = (i < cnt) ? p[u][i] : 0.f;
+          pn2 = fmaf(pi, pi, pn2);
+          un2 = fmaf(uu, uu, un2);
+        }
+        st<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+        st<TP>(c.t->ptr[3], idx, cnt, vec, v[u]);
+      }
     }
-    st<TP>(c.t->ptr[2], idx, cnt, vec, m);
-    st<TP>(c.t->ptr[3], idx, cnt, vec, v);
-    st<float>(c.t->ptr[4], idx, cnt, vec, up);
-  }
-  float rp = block_sum(pn2, scratch);
-  float ru = block_sum(un2, scratch);
-  if (threadIdx.x == 0) {
-    partials[blockIdx.x] = rp;
-    partials[L.nchunks + blockIdx.x] = ru;
+    const float rp = block_sum(pn2, scratch);
+    const float ru = block_sum(un2, scratch);
+    if (threadIdx.x == 0) {
+      partials[ch] = rp;
+      partials[L.nchunks + ch] = ru;
+    }
   }
 }
 
+// stage 2 lists: [p, m, v] or [p, m, v, p_copy]
 template <typename TP, typename TC, int DEPTH>
 __global__ void __launch_bounds__(kMTThreads)
     lamb_stage2_kernel(MTLaunch L, LambArgs a, const float* pnorm, const float* unorm,
                        const int* noop) {
   if (skip_step(noop)) return;
-  const int tensor = L.chunks[blockIdx.x].tensor;
-  TileCtx c = tile_ctx(L);
-  const bool al = c.t->aligned;
+  const LambConsts k = lamb_consts(a);
   const float lr = lr_of(a.lr_ptr, a.lr);
-  float ratio = lr;
-  if (a.use_nvlamb || a.wd != 0.f) {
-    float pn = pnorm[tensor], un = unorm[tensor];
-    ratio = (pn != 0.f && un != 0.f) ? lr * (pn / un) : lr;
-  }
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const int tensor = L.chunks[ch].tensor;
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+#pragma unroll 1
+    for (int h = 0; h < kMTUnroll / UA; ++h) {
+      float ratio = lr;
+      if (a.use_nvlamb || a.wd != 0.f) {
+        const float pn = pnorm[tensor], un = unorm[tensor];
+        ratio = (pn != 0.f && un != 0.f) ? lr * (pn / un) : lr;
+      }
+      float p[UA][8], m[UA][8], v[UA][8];
 #pragma unroll
-  for (int u = 0; u < kMTUnroll; ++u) {
-    int off = lane_off(u);
-    int cnt = c.n - off;
-    if (cnt <= 0) continue;
-    bool vec = al && cnt >= 8;
-    int64_t idx = c.start + off;
-    float p[8], up[8];
-    ld<TP>(c.t->ptr[0], idx, cnt, vec, p);
-    ld<float>(c.t->ptr[1], idx, cnt, vec, up);
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+        ld<TP>(c.t->ptr[0], idx, cnt, vec, p[u]);
+        ld<TP>(c.t->ptr[1], idx, cnt, vec, m[u]);
+        ld<TP>(c.t->ptr[2], idx, cnt, vec, v[u]);
+      }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) p[i] = fmaf(-ratio, up[i], p[i]);
-    st<TP>(c.t->ptr[0], idx, cnt, vec, p);
-    if (DEPTH == 3) st<TC>(c.t->ptr[2], idx, cnt, vec, p);
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          p[u][i] = fmaf(-ratio, lamb_update(a, k, m[u][i], v[u][i], p[u][i]), p[u][i]);
+        st<TP>(c.t->ptr[0], idx, cnt, vec, p[u]);
+        if (DEPTH == 4) st<TC>(c.t->ptr[3], idx, cnt, vec, p[u]);
+      }
+    }
   }
 }
 
@@ -256,7 +332,7 @@ void mt_lamb_stage1(const MTLaunch& L, DType g, DType p, const LambArgs& a, floa
     dispatch1(p, [&](auto tp) {
       using TG = decltype(tg);
       using TP = decltype(tp);
-      hipLaunchKernelGGL((lamb_stage1_kernel<TG, TP>), mt_grid(L), dim3(kMTThreads), 0, st, L, a,
+      hipLaunchKernelGGL((lamb_stage1_kernel<TG, TP>), mt_pgrid(L), dim3(kMTThreads), 0, st, L, a,
                          partials, noop);
     });
   });
@@ -268,13 +344,13 @@ void mt_lamb_stage2(const MTLaunch& L, int depth, DType p, DType copy, const Lam
   if (L.nchunks == 0) return;
   dispatch1(p, [&](auto tp) {
     using TP = decltype(tp);
-    if (depth == 2) {
-      hipLaunchKernelGGL((lamb_stage2_kernel<TP, TP, 2>), mt_grid(L), dim3(kMTThreads), 0, st, L,
+    if (depth == 3) {
+      hipLaunchKernelGGL((lamb_stage2_kernel<TP, TP, 3>), mt_pgrid(L), dim3(kMTThreads), 0, st, L,
                          a, param_norms, update_norms, noop);
     } else {
       dispatch1(copy, [&](auto tc) {
         using TC = decltype(tc);
-        hipLaunchKernelGGL((lamb_stage2_kernel<TP, TC, 3>), mt_grid(L), dim3(kMTThreads), 0, st,
+        hipLaunchKernelGGL((lamb_stage2_kernel<TP, TC, 4>), mt_pgrid(L), dim3(kMTThreads), 0, st,
                            L, a, param_norms, update_norms, noop);
       });
     }
@@ -309,39 +385,46 @@ template <typename TG, typename TP>
 __global__ void __launch_bounds__(kMTThreads)
     novograd_kernel(MTLaunch L, NovoArgs a, const float* vnorm, const int* noop) {
   if (skip_step(noop)) return;
-  const int tensor = L.chunks[blockIdx.x].tensor;
-  TileCtx c = tile_ctx(L);
-  const bool al = c.t->aligned;
   const float sc = get_scale(a.scale);
   const float lr = lr_of(a.lr_ptr, a.lr);
   const int step = a.step_ptr ? (*a.step_ptr + 1) : a.step;
   float bc1, bc2;
   bias_corrections(a.bias_correction, a.beta1, a.beta2, step, bc1, bc2);
   const float beta3 = a.grad_averaging ? (1.f - a.beta1) : 1.f;
-  const float denom = vnorm[tensor] / sqrtf(bc2) + a.eps;
-  const float inv_denom = 1.f / denom;
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const int tensor = L.chunks[ch].tensor;
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+    const float inv_denom = 1.f / (vnorm[tensor] / sqrtf(bc2) + a.eps);
+    float g[kMTUnroll][8], p[kMTUnroll][8], m[kMTUnroll][8];
 #pragma unroll
-  for (int u = 0; u < kMTUnroll; ++u) {
-    int off = lane_off(u);
-    int cnt = c.n - off;
-    if (cnt <= 0) continue;
-    bool vec = al && cnt >= 8;
-    int64_t idx = c.start + off;
-    float g[8], p[8], m[8];
-    ld<TG>(c.t->ptr[0], idx, cnt, vec, g);
-    ld<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    ld<TP>(c.t->ptr[2], idx, cnt, vec, m);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float gi = g[i] * sc * inv_denom;
-      if (a.mode == 0) gi = fmaf(a.wd, p[i], gi);
-      m[i] = fmaf(a.beta1, m[i], beta3 * gi);
-      float upd = m[i] / bc1;
-      if (a.mode == 1) upd = fmaf(a.wd, p[i], upd);
-      p[i] = fmaf(-lr, upd, p[i]);
+    for (int u = 0; u < kMTUnroll; ++u) {
+      const int off = lane_off(u), cnt = c.n - off;
+      if (cnt <= 0) continue;
+      const bool vec = al && cnt >= 8;
+      const int64_t idx = c.start + off;
+      ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+      ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+      ld<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
     }
-    st<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    st<TP>(c.t->ptr[2], idx, cnt, vec, m);
+#pragma unroll
+    for (int u = 0; u < kMTUnroll; ++u) {
+      const int off = lane_off(u), cnt = c.n - off;
+      if (cnt <= 0) continue;
+      const bool vec = al && cnt >= 8;
+      const int64_t idx = c.start + off;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float gi = g[u][i] * sc * inv_denom;
+        if (a.mode == 0) gi = fmaf(a.wd, p[u][i], gi);
+        m[u][i] = fmaf(a.beta1, m[u][i], beta3 * gi);
+        float upd = m[u][i] / bc1;
+        if (a.mode == 1) upd = fmaf(a.wd, p[u][i], upd);
+        p[u][i] = fmaf(-lr, upd, p[u][i]);
+      }
+      st<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+      st<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+    }
   }
 }
 
@@ -352,7 +435,7 @@ void mt_novograd(const MTLaunch& L, DType g, DType p, const NovoArgs& a, const f
     dispatch1(p, [&](auto tp) {
       using TG = decltype(tg);
       using TP = decltype(tp);
-      hipLaunchKernelGGL((novograd_kernel<TG, TP>), mt_grid(L), dim3(kMTThreads), 0, st, L, a, v,
+      hipLaunchKernelGGL((novograd_kernel<TG, TP>), mt_pgrid(L), dim3(kMTThreads), 0, st, L, a, v,
                          noop);
     });
   });
@@ -364,32 +447,40 @@ template <typename TG, typename TP>
 __global__ void __launch_bounds__(kMTThreads)
     adagrad_kernel(MTLaunch L, AdagradArgs a, const int* noop) {
   if (skip_step(noop)) return;
-  TileCtx c = tile_ctx(L);
-  const bool al = c.t->aligned;
   const float sc = get_scale(a.scale);
   const float lr = lr_of(a.lr_ptr, a.lr);
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+    float g[kMTUnroll][8], p[kMTUnroll][8], h[kMTUnroll][8];
 #pragma unroll
-  for (int u = 0; u < kMTUnroll; ++u) {
-    int off = lane_off(u);
-    int cnt = c.n - off;
-    if (cnt <= 0) continue;
-    bool vec = al && cnt >= 8;
-    int64_t idx = c.start + off;
-    float g[8], p[8], h[8];
-    ld<TG>(c.t->ptr[0], idx, cnt, vec, g);
-    ld<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    ld<TP>(c.t->ptr[2], idx, cnt, vec, h);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float gi = g[i] * sc;
-      if (a.mode == 0) gi = fmaf(a.wd, p[i], gi);
-      h[i] = fmaf(gi, gi, h[i]);
-      float upd = gi / (sqrtf(h[i]) + a.eps);
-      if (a.mode == 1) upd = fmaf(a.wd, p[i], upd);
-      p[i] = fmaf(-lr, upd, p[i]);
+    for (int u = 0; u < kMTUnroll; ++u) {
+      const int off = lane_off(u), cnt = c.n - off;
+      if (cnt <= 0) continue;
+      const bool vec = al && cnt >= 8;
+      const int64_t idx = c.start + off;
+      ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+      ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+      ld<TP>(c.t->ptr[2], idx, cnt, vec, h[u]);
     }
-    st<TP>(c.t->ptr[1], idx, cnt, vec, p);
-    st<TP>(c.t->ptr[2], idx, cnt, vec, h);
+#pragma unroll
+    for (int u = 0; u < kMTUnroll; ++u) {
+      const int off = lane_off(u), cnt = c.n - off;
+      if (cnt <= 0) continue;
+      const bool vec = al && cnt >= 8;
+      const int64_t idx = c.start + off;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float gi = g[u][i] * sc;
+        if (a.mode == 0) gi = fmaf(a.wd, p[u][i], gi);
+        h[u][i] = fmaf(gi, gi, h[u][i]);
+        float upd = gi / (sqrtf(h[u][i]) + a.eps);
+        if (a.mode == 1) upd = fmaf(a.wd, p[u][i], upd);
+        p[u][i] = fmaf(-lr, upd, p[u][i]);
+      }
+      st<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+      st<TP>(c.t->ptr[2], idx, cnt, vec, h[u]);
+    }
   }
 }
 
@@ -400,10 +491,29 @@ void mt_adagrad(const MTLaunch& L, DType g, DType p, const AdagradArgs& a, const
     dispatch1(p, [&](auto tp) {
       using TG = decltype(tg);
       using TP = decltype(tp);
-      hipLaunchKernelGGL((adagrad_kernel<TG, TP>), mt_grid(L), dim3(kMTThreads), 0, st, L, a,
+      hipLaunchKernelGGL((adagrad_kernel<TG, TP>), mt_pgrid(L), dim3(kMTThreads), 0, st, L, a,
                          noop);
     });
   });
 }
 
+// --------------------------------------------------------------------------
+int device_cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cus[dev] = n > 0 ? n : 256;
+  }
+  return cus[dev];
+}
+
+int mt_persistent_wgs_per_cu() {
+  const char* e = std::getenv("APEX_AMD_MT_WGS_PER_CU");
+  return e ? std::atoi(e) : 0;  // measured: one WG per chunk is best for SGD / Adam
+}
+
 }  // namespace amd
+

@@ -80,10 +80,11 @@ struct LambArgs {
   ScaleArg scale;
   const float* lr_ptr;
 };
-// stage 1: [g, p, m, v, u] -> u (fp32 update) + partials (||p||^2, ||u||^2 per chunk)
+// stage 1: [g, p, m, v] -> updated m, v + partials (||p||^2, ||u||^2 per chunk)
 void mt_lamb_stage1(const MTLaunch& L, DType g, DType p, const LambArgs& a, float* partials,
                     const int* noop, hipStream_t st);
-// stage 2: [p, u] or [p, u, p_copy]; per-tensor norms from mt_norm_finalize
+// stage 2: [p, m, v] or [p, m, v, p_copy] (u recomputed); per-tensor norms from
+// mt_norm_finalize
 void mt_lamb_stage2(const MTLaunch& L, int depth, DType p, DType copy, const LambArgs& a,
                     const float* param_norms, const float* update_norms, const int* noop,
                     hipStream_t st);

@@ -33,8 +33,8 @@ struct TileCtx {
   int n;
 };
 
-__device__ __forceinline__ TileCtx tile_ctx(const MTLaunch& L) {
-  const ChunkDesc c = L.chunks[blockIdx.x];
+__device__ __forceinline__ TileCtx tile_ctx(const MTLaunch& L, int chunk) {
+  const ChunkDesc c = L.chunks[chunk];
   TileCtx ctx;
   ctx.t = L.tensors + c.tensor;
   ctx.start = (int64_t)c.chunk * kTile;
@@ -42,6 +42,7 @@ __device__ __forceinline__ TileCtx tile_ctx(const MTLaunch& L) {
   ctx.n = rem > kTile ? kTile : (int)rem;
   return ctx;
 }
+__device__ __forceinline__ TileCtx tile_ctx(const MTLaunch& L) { return tile_ctx(L, blockIdx.x); }
 
 template <typename F>
 static inline void dispatch1(DType a, F&& f) {
@@ -55,5 +56,20 @@ static inline void dispatch1(DType a, F&& f) {
 
 
 static inline dim3 mt_grid(const MTLaunch& L) { return dim3((unsigned)L.nchunks); }
+
+// Persistent grid for the optimizer kernels: min(#chunks, CUs x WGs-per-CU)
+// workgroups walk the chunk list with a grid stride, so a 3,000-chunk step is
+// not a full wave of workgroups plus a half-empty second one (the tail of a
+// non-persistent launch), and each workgroup's descriptor fetch is paid once
+// per several tiles of streaming.  APEX_AMD_MT_WGS_PER_CU overrides (0 = one
+// workgroup per chunk).
+int mt_persistent_wgs_per_cu();
+int device_cu_count();
+static inline dim3 mt_pgrid(const MTLaunch& L) {
+  const int per = mt_persistent_wgs_per_cu();
+  if (per <= 0) return mt_grid(L);
+  const long cap = (long)device_cu_count() * per;
+  return dim3((unsigned)(L.nchunks < cap ? L.nchunks : cap));
+}
 
 }  // namespace amd

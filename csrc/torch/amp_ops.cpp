@@ -227,8 +227,9 @@ void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optio
                 c10::optional<at::Tensor> scale_t, bool scale_inv) {
   c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   if (lists.empty() || lists[0].empty()) return;
-  // lists: [g, p, m, v, u] or [g, p, m, v, u, p_copy]; u is an fp32 workspace
-  bool gpu = mt_validate(lists, 5, 6);
+  // lists: [g, p, m, v] or [g, p, m, v, p_copy]; the update u is recomputed in
+  // stage 2 from (p, m, v) - no fp32 workspace
+  bool gpu = mt_validate(lists, 4, 5);
   if (!gpu) {
     cpu::Lamb a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (int)step,
                 optp(step_t), (int)mode, bias_correction ? 1 : 0, grad_averaging ? 1 : 0,
@@ -254,9 +255,10 @@ void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optio
   a.lr_ptr = opt_fptr(lr_t);
   auto fopt = at::TensorOptions().dtype(at::kFloat).device(lists[0][0].device());
   by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
-    for (size_t i = 0; i < g[4].size(); ++i)
-      TORCH_CHECK(g[4][i].scalar_type() == at::kFloat, "lamb: update workspace must be fp32");
-    TensorLists s1 = sub(g, {0, 1, 2, 3, 4});
+    TORCH_CHECK(g[2][0].scalar_type() == g[1][0].scalar_type() &&
+                    g[3][0].scalar_type() == g[1][0].scalar_type(),
+                "lamb: exp_avg / exp_avg_sq must match the parameter dtype");
+    TensorLists s1 = sub(g, {0, 1, 2, 3});
     const MTPlan& P1 = mt_plan(s1);
     at::Tensor partials = at::empty({2 * (int64_t)P1.L.nchunks}, fopt);
     at::Tensor norms = at::empty({2 * (int64_t)P1.L.ntensors}, fopt);
@@ -264,9 +266,9 @@ void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optio
                    noop_ptr(noop), cur_stream());
     mt_norm_finalize(P1.L, partials.data_ptr<float>(), 2, 0, nullptr, norms.data_ptr<float>(),
                      cur_stream());
-    TensorLists s2 = g.size() == 6 ? sub(g, {1, 4, 5}) : sub(g, {1, 4});
+    TensorLists s2 = g.size() == 5 ? sub(g, {1, 2, 3, 4}) : sub(g, {1, 2, 3});
     const MTPlan& P2 = mt_plan(s2);
-    DType copy = g.size() == 6 ? dtype_of(g[5][0]) : dtype_of(g[1][0]);
+    DType copy = g.size() == 5 ? dtype_of(g[4][0]) : dtype_of(g[1][0]);
     mt_lamb_stage2(P2.L, (int)s2.size(), dtype_of(g[1][0]), copy, a, norms.data_ptr<float>(),
                    norms.data_ptr<float>() + P1.L.ntensors, noop_ptr(noop), cur_stream());
   });

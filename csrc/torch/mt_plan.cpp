@@ -11,6 +11,7 @@
 
 #include <c10/hip/HIPException.h>
 #include <c10/hip/HIPGraphsC10Utils.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "common.h"
 
@@ -179,7 +180,9 @@ const MTPlan& mt_plan(const TensorLists& lists) {
       --it2;
       auto oit = c.map.find(*it2);
       if (oit == c.map.end() || oit->second.plan.captured) continue;
-      oit->second.plan.table.record_stream(c10::hip::getCurrentHIPStream());
+      // (the allocator files HIP streams under the CUDA device type: a plain
+      // c10::hip stream here is rejected by Tensor::record_stream)
+      oit->second.plan.table.record_stream(at::hip::getCurrentHIPStreamMasqueradingAsCUDA());
       c.map.erase(oit);
       c.lru.erase(it2);
       break;

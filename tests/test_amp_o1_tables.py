@@ -47,7 +47,8 @@ def test_override_list_is_exactly_the_autocast_difference(dtype):
         bad = A.audit("cuda", dtype, fake=True)
     finally:
         torch.set_autocast_enabled("cuda", False)
-    assert sorted((ns, n) for ns, n, *_ in bad) == sorted(amp_mod.APEX_POLICY_OVERRIDES)
+    want = [e for e in amp_mod.APEX_POLICY_OVERRIDES if e not in A.FAKE_UNVERIFIABLE]
+    assert sorted((ns, n) for ns, n, *_ in bad) == sorted(want)
 
 
 def test_every_table_entry_has_a_recipe():

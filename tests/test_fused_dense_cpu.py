@@ -73,3 +73,30 @@ def test_functional_models_use_fused_dense():
     (a2.sum() + n2.sum()).backward()
     for (k, p), q in zip(m.named_parameters(), r.parameters()):
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-3, atol=1e-4, msg=k)
+
+
+def test_cast_cache_is_thread_local_and_identity_checked():
+    """the O1 cast cache must not hand a recycled id() a stale copy, and
+    one thread's active block must not leak into another thread."""
+    import threading
+
+    from apex_example_amd import fused_dense as fd
+
+    w = torch.randn(4, 3)
+    stale = torch.zeros(4, 3, dtype=torch.float16)
+    other = torch.randn(5, 2)
+    st = fd._tls()
+    # an entry keyed by other's id but holding a different tensor object: ignored
+    st.active = {id(w): (other, stale)}
+    try:
+        got = fd._cast(w, torch.float16)
+        assert torch.equal(got, w.half())
+        st.active = {id(w): (w, stale)}
+        assert fd._cast(w, torch.float16) is stale
+        seen = []
+        t = threading.Thread(target=lambda: seen.append(fd._cast(w, torch.float16)))
+        t.start()
+        t.join()
+        assert seen[0] is not stale and torch.equal(seen[0], w.half())
+    finally:
+        st.active = None

@@ -26,6 +26,26 @@ def _tensors(sizes, dtype, dev=DEV, seed=0):
 SIZES = [1, 7, 8, 63, 64, 1000, 8191, 8192, 8193, 65536 * 2 + 5, 333333]
 
 
+def test_mt_plan_cache_eviction():
+    """More distinct tensor sets than the 512-entry launch-plan cache holds: the
+    LRU eviction path (stream-recorded table release) runs on the device and
+    every launch stays correct."""
+    mt = C().mt
+    mt.plan_cache_clear()
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for k in range(600):
+        x = torch.full((100 + k,), float(k), device=DEV)
+        y = torch.empty_like(x)
+        mt.scale(noop, [[x], [y]], 0.5)
+        if k % 97 == 0:
+            torch.cuda.synchronize()
+            assert torch.equal(y, x * 0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(y, x * 0.5)
+    assert mt.plan_cache_size() <= 512
+    mt.plan_cache_clear()
+
+
 @pytest.mark.parametrize("tin", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("tout", [torch.float32, torch.float16, torch.bfloat16])
 def test_mt_scale(tin, tout):

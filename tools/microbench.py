@@ -386,33 +386,61 @@ def bench_attn(args):
 
 
 def bench_optim(args):
-    from apex_example_amd.optimizers import FusedAdam, FusedSGD
+    """Optimizer-kernel bandwidth on ResNet-50's 161 tensors, straight through
+    amp_C (no Python optimizer bookkeeping in the loop), swept over the
+    persistent-grid size APEX_AMD_MT_WGS_PER_CU (0 = one workgroup per chunk)."""
+    import os
+
+    from apex_example_amd import amp_C
     from apex_example_amd.models import resnet50
+    from apex_example_amd.optimizers import FusedAdam, FusedSGD
 
     dev = "cuda"
     m = resnet50().to(dev)
-    ps = [p for p in m.parameters()]
+    ps = [p.detach() for p in m.parameters()]
     n = sum(p.numel() for p in ps)
-    for p in ps:
-        p.grad = torch.randn_like(p)
+    g32 = [torch.randn_like(p) for p in ps]
+    g16 = [g.to(torch.bfloat16) for g in g32]
+    mom = [torch.zeros_like(p) for p in ps]
+    v = [torch.zeros_like(p) for p in ps]
+    cp = [p.to(torch.bfloat16) for p in ps]
+    noop = torch.zeros(1, dtype=torch.int32, device=dev)
+    cases = [
+        ("SGD fp32 [g,p,m]", 16, lambda: amp_C.multi_tensor_sgd(
+            0, noop, [g32, ps, mom], 1e-4, 0.9, 0.0, 0.1, False, False, False, 1.0)),
+        ("SGD O2 [g16,p,m,copy16]", 20, lambda: amp_C.multi_tensor_sgd(
+            0, noop, [g16, ps, mom, cp], 1e-4, 0.9, 0.0, 0.1, False, False, False, 1 / 1024.)),
+        ("Adam fp32 [g,p,m,v]", 28, lambda: amp_C.multi_tensor_adam(
+            0, noop, [g32, ps, mom, v], 1e-3, 0.9, 0.999, 1e-8, 1, 1, True, 0.0)),
+        ("LAMB fp32 [g,p,m,v]", 40, lambda: amp_C.multi_tensor_lamb(
+            0, noop, [g32, ps, mom, v], 1e-3, 0.9, 0.999, 1e-6, 1, True, 0.01, True, 1,
+            torch.ones(1, device=dev), 1.0)),
+    ]
+    print("| kernel | B/param | " + " | ".join("wgs/CU=%s" % w for w in args.wgs) + " |")
+    print("|---|---|" + "---|" * len(args.wgs))
+    for name, bpp, fn in cases:
+        row = []
+        for w in args.wgs:
+            os.environ["APEX_AMD_MT_WGS_PER_CU"] = str(w)
+            t = timeit(fn, iters=50, warmup=5)
+            row.append("%.1f us %.2f TB/s" % (t, bpp * n / (t * 1e-6) / 1e12))
+        print("| %s | %d | %s |" % (name, bpp, " | ".join(row)), flush=True)
+    os.environ.pop("APEX_AMD_MT_WGS_PER_CU", None)
+    # whole optimizer.step() (Python bookkeeping included) vs torch's fused optimizers
+    for p_, g_ in zip(ps, g32):
+        p_.grad = g_
     o = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4)
     o.step()
-    t = timeit(lambda: o.step())
-    print("FusedSGD fp32 ResNet-50 (%d params, 161 tensors): %.1f us, %.2f TB/s (16 B/param)" % (
-        n, t, 16 * n / (t * 1e-6) / 1e12))
+    print("FusedSGD.step() fp32: %.1f us" % timeit(lambda: o.step()))
     ref = torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
     ref.step()
-    t2 = timeit(lambda: ref.step())
-    print("torch.optim.SGD(fused) same: %.1f us" % t2)
+    print("torch.optim.SGD(fused).step(): %.1f us" % timeit(lambda: ref.step()))
     oa = FusedAdam(ps, lr=1e-3)
     oa.step()
-    t3 = timeit(lambda: oa.step())
-    print("FusedAdam fp32 ResNet-50: %.1f us, %.2f TB/s (28 B/param)" % (
-        t3, 28 * n / (t3 * 1e-6) / 1e12))
+    print("FusedAdam.step() fp32: %.1f us" % timeit(lambda: oa.step()))
     ra = torch.optim.AdamW(ps, lr=1e-3, fused=True)
     ra.step()
-    t4 = timeit(lambda: ra.step())
-    print("torch.optim.AdamW(fused) same: %.1f us" % t4)
+    print("torch.optim.AdamW(fused).step(): %.1f us" % timeit(lambda: ra.step()))
 
 
 def bench_ln(args):
@@ -468,6 +496,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
+    ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
+                    help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
     {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
