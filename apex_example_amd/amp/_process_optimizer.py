@@ -252,9 +252,31 @@ def lazy_init_no_master_weights(self):
     stash.all_fp32_grad_stash = [None for _ in stash.all_fp32_params]
 
 
+def _unscale_pending(opt):
+    """Grads left loss-scaled by a folded-unscale backward (see
+    post_backward_no_master_weights) meet another backward before a step:
+    unscale them in place by the scale they carry, so stashing / accumulation
+    sees unscaled values as in Apex."""
+    stash = opt._amp_stash
+    stash.grads_scaled = False
+    grads = [p.grad for p in stash.all_fp16_params + stash.all_fp32_params if p.grad is not None]
+    if not grads or stash.last_scaler is None:
+        return
+    from .. import amp_C
+
+    s = stash.last_scaler.grads_scale()
+    dummy = torch.zeros(1, dtype=torch.int32, device=grads[0].device)
+    if isinstance(s, torch.Tensor):
+        amp_C.multi_tensor_scale(65536, dummy, [grads, grads], s, scale_inv=True)
+    else:
+        amp_C.multi_tensor_scale(65536, dummy, [grads, grads], 1.0 / s)
+
+
 def prepare_backward_no_master_weights(self):
     stash = self._amp_stash
     self._amp_lazy_init()
+    if getattr(stash, "grads_scaled", False):
+        _unscale_pending(self)
     for i, param in enumerate(stash.all_fp16_params):
         stash.all_fp16_grad_stash[i] = _stash_grad(stash, param)
     for i, param in enumerate(stash.all_fp32_params):
@@ -265,6 +287,21 @@ def post_backward_no_master_weights(self, scaler):
     stash = self._amp_stash
     self._amp_lazy_init()
     stash.model_grads_zeroed = False
+    if (_folds_unscale(self) and multi_tensor_applier.available
+            and not any(g is not None for g in stash.all_fp16_grad_stash)
+            and not any(g is not None for g in stash.all_fp32_grad_stash)):
+        # amp O1 with a fused optimizer and materialize_master_grads=False: the
+        # optimizer kernel multiplies by 1/scale itself (as under O2), so the
+        # separate in-place unscale pass over every fp32 grad becomes a read-only
+        # overflow check.  The grads stay scaled until the step (or the next
+        # backward, which unscales them first).
+        grads = [p.grad for p in stash.all_fp16_params + stash.all_fp32_params
+                 if p.grad is not None]
+        if grads:
+            scaler.check_overflow(grads)
+        stash.grads_scaled = True
+        return
+    stash.grads_scaled = False
     split_types = ((stash.all_fp16_params, stash.all_fp16_grad_stash),
                    (stash.all_fp32_params, stash.all_fp32_grad_stash))
     for params, stashed_grads in split_types:

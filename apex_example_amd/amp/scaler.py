@@ -63,6 +63,11 @@ class LossScaler(object):
         d = self._device
         self._scale_dev = torch.tensor([self._loss_scale], dtype=torch.float32, device=d)
         self._scale_view = self._scale_dev[0]
+        # the scale the latest backward's grads carry (the update kernel writes the
+        # pre-update value here): what a fused optimizer that unscales in-kernel
+        # after update_scale() must divide by
+        self._scale_applied = (torch.tensor([self._loss_scale], dtype=torch.float32, device=d)
+                               if self.dynamic else self._scale_dev)
         self._unskipped_dev = torch.tensor([self._unskipped], dtype=torch.int32, device=d)
         self._skipped_dev = torch.zeros(1, dtype=torch.int32, device=d)
         self._skipped_seen = 0
@@ -85,6 +90,14 @@ class LossScaler(object):
     def loss_scale_tensor(self):
         """Device scalar (0-dim view) of the current scale (sync-free mode)."""
         return self._scale_view
+
+    def grads_scale(self):
+        """The loss scale the latest backward's gradients carry, for in-kernel
+        unscaling that runs after ``update_scale()`` (a growth step must still
+        divide by the pre-growth value): a device scalar in sync-free mode."""
+        if self.sync_free:
+            return self._scale_applied
+        return getattr(self, "_applied_scale", self._loss_scale)
 
     def scale_for_kernels(self):
         """(value, tensor) pair understood by amp_C functions with scale_inv=True."""
@@ -200,13 +213,15 @@ class LossScaler(object):
                 _native.require().mt.update_loss_scale(
                     self._scale_dev, self._unskipped_dev, self._skipped_dev, self._overflow_buf,
                     float(self._scale_factor), int(self._scale_seq_len),
-                    float(self._min_loss_scale or 0.0), float(self._max_loss_scale), True)
+                    float(self._min_loss_scale or 0.0), float(self._max_loss_scale), True,
+                    self._scale_applied)
                 if not (self._device.type == "cuda"
                         and torch.cuda.is_current_stream_capturing()):
                     self._post_report()  # (inside a hipGraph capture: poll via skipped_steps())
             else:
                 self._unskipped_dev.add_(1)
             return False
+        self._applied_scale = self._loss_scale  # the scale this step's grads carry
         # If the fused kernel is available, we only need one D2H memcopy and sync.
         if LossScaler.has_fused_kernel and self.dynamic and not self._has_overflow:
             self._has_overflow = bool(self._overflow_buf.item())
@@ -269,4 +284,5 @@ class LossScaler(object):
         self._unskipped = int(unskipped)
         if self.sync_free:
             self._scale_dev.fill_(self._loss_scale)
+            self._scale_applied.fill_(self._loss_scale)
             self._unskipped_dev.fill_(self._unskipped)

@@ -12,10 +12,18 @@ sums (no extra read of dpre for the first bias).
 Under autocast (amp O1) the operands are cast once in forward and the casted
 copies saved, so backward runs plain half-precision GEMMs (no second weight
 cast); bias gradients are reduced in fp32 and written in the bias's dtype.
+
+``FusedDenseGeluDense(approximate="tanh")`` - apex's semantics: its cuBLASLt GELU
+epilogues are the tanh approximation - runs the GELU inside hipBLASLt epilogues
+both ways (csrc/torch/lt_ops.cpp): forward GELU_AUX_BIAS (h and the
+pre-activation from one GEMM), backward DGELU_BGRAD (dpre and the first bias
+gradient from the dh GEMM).  Shapes / dtypes the library has no algorithm for
+fall back to GEMM + the kernels above.
 """
 from __future__ import annotations
 
 import collections
+import os
 import threading
 
 import torch
@@ -25,7 +33,8 @@ import torch.nn.functional as F
 from .. import _native
 
 __all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function", "cast_params_once",
-           "fused_dense_gelu_dense_function", "dense_no_bias_function"]
+           "fused_dense_gelu_dense_function", "dense_no_bias_function", "fused_dense_skip_function",
+           "fused_dense_gelu_dense_skip_function"]
 
 
 def _compute_dtype(x):
@@ -124,85 +133,180 @@ def _wgrad(dy2, x2, dtype):
 def _bias_grad(g2, dtype):
     if g2.is_cuda and _native.available():
         return _native.require().dense.bias_grad(g2, dtype)
-    return g2.float().sum(0).to(dtype)
+    return g2.to(torch.promote_types(g2.dtype, torch.float32)).sum(0).to(dtype)
+
+
+def _dgrad(g2, w, xshape, dskip):
+    """dX = g2 @ W, accumulated IN PLACE into the residual-branch gradient ``dskip``
+    (C += A @ B, hipBLASLt beta = 1) when the input also fed a residual: the sum
+    autograd would otherwise launch over the input gradient disappears.  ``dskip``
+    is the fresh gradient buffer the residual consumer's backward produced."""
+    if dskip is not None:
+        if dskip.dtype == g2.dtype and dskip.is_contiguous():
+            return dskip.view(-1, w.size(1)).addmm_(g2, w).view(xshape)
+        return (dskip.float() + (g2 @ w).view(xshape).float()).to(dskip.dtype)
+    return (g2 @ w).view(xshape)
+
+
+def _dense_fwd(ctx, x, weight, bias):
+    dt = _compute_dtype(x)
+    with torch.autocast("cuda", enabled=False):
+        xc, wc, bc = _cast(x, dt), _cast(weight, dt), _cast(bias, dt)
+        x2 = xc.reshape(-1, xc.size(-1))
+        y = torch.addmm(bc, x2, wc.t()) if bc is not None else x2 @ wc.t()
+    ctx.save_for_backward(xc, wc)
+    ctx.bias_dtype = bias.dtype if bias is not None else None
+    ctx.w_dtype = weight.dtype
+    return y.view(*x.shape[:-1], weight.size(0))
+
+
+def _dense_bwd(ctx, dy, dskip=None):
+    xc, wc = ctx.saved_tensors
+    dx = dw = db = None
+    if dy is None:
+        return dskip, None, None
+    dy2 = dy.reshape(-1, dy.size(-1)).contiguous()
+    if dy2.dtype != wc.dtype:
+        dy2 = dy2.to(wc.dtype)
+    if ctx.needs_input_grad[0]:
+        dx = _dgrad(dy2, wc, xc.shape, dskip)
+    if ctx.needs_input_grad[1]:
+        dw = _wgrad(dy2, xc.reshape(-1, xc.size(-1)), ctx.w_dtype)
+    if ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
+        db = _bias_grad(dy2, ctx.bias_dtype)
+    return dx, dw, db
 
 
 class FusedDenseFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
-        dt = _compute_dtype(x)
-        with torch.autocast("cuda", enabled=False):
-            xc, wc, bc = _cast(x, dt), _cast(weight, dt), _cast(bias, dt)
-            x2 = xc.reshape(-1, xc.size(-1))
-            y = torch.addmm(bc, x2, wc.t()) if bc is not None else x2 @ wc.t()
-        ctx.save_for_backward(xc, wc)
-        ctx.bias_dtype = bias.dtype if bias is not None else None
-        ctx.w_dtype = weight.dtype
-        return y.view(*x.shape[:-1], weight.size(0))
+        return _dense_fwd(ctx, x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
-        xc, wc = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.size(-1)).contiguous()
-        if dy2.dtype != wc.dtype:
-            dy2 = dy2.to(wc.dtype)
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = (dy2 @ wc).view(xc.shape)
-        if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy2, xc.reshape(-1, xc.size(-1)), ctx.w_dtype)
-        if ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
-            db = _bias_grad(dy2, ctx.bias_dtype)
-        return dx, dw, db
+        return _dense_bwd(ctx, dy)
+
+
+class FusedDenseSkipFunc(torch.autograd.Function):
+    """(dense(x), x): the dense layer whose input also feeds a residual branch
+    (BERT's QKV projection and FFN input).  Backward receives both gradients and
+    forms dx = dskip + dy @ W as one accumulating GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        return _dense_fwd(ctx, x, weight, bias), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        return _dense_bwd(ctx, dy, dskip)
+
+
+# hipBLASLt GELU epilogues (csrc/torch/lt_ops.cpp) for the tanh-GELU FFN; set
+# APEX_AMD_LT_GELU=0 to run GEMM + separate GELU / column-sum kernels instead
+_LT_GELU = os.environ.get("APEX_AMD_LT_GELU", "1") == "1"
+
+
+def _lt_ok(*ts):
+    return (_LT_GELU and all(t is not None and t.is_cuda for t in ts)
+            and ts[0].dtype in (torch.bfloat16, torch.float16)
+            and all(t.dtype == ts[0].dtype for t in ts) and _native.available())
+
+
+def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
+    dt = _compute_dtype(x)
+    with torch.autocast("cuda", enabled=False):
+        xc = _cast(x, dt)
+        w1c, b1c, w2c, b2c = _cast(w1, dt), _cast(b1, dt), _cast(w2, dt), _cast(b2, dt)
+        x2 = xc.reshape(-1, xc.size(-1))
+        res = None
+        if approximate == "tanh" and _lt_ok(x2, w1c, b1c):
+            # one GEMM: h = gelu(x W1^T + b1) with pre as the epilogue's aux output
+            res = _native.require().dense.gelu_fwd_lt(x2, w1c, b1c) or None
+        if res is not None:
+            h, pre = res
+        else:
+            pre = torch.addmm(b1c, x2, w1c.t()) if b1c is not None else x2 @ w1c.t()
+            h = F.gelu(pre, approximate=approximate)
+        y = torch.addmm(b2c, h, w2c.t()) if b2c is not None else h @ w2c.t()
+    ctx.save_for_backward(xc, w1c, pre, h, w2c)
+    ctx.b1_dtype = b1.dtype if b1 is not None else None
+    ctx.b2_dtype = b2.dtype if b2 is not None else None
+    ctx.tanh = approximate == "tanh"
+    ctx.w_dtypes = (w1.dtype, w2.dtype)
+    return y.view(*x.shape[:-1], w2.size(0))
+
+
+def _gelu_dense_bwd(ctx, dy, dskip=None):
+    if dy is None:
+        return dskip, None, None, None, None, None
+    xc, w1c, pre, h, w2c = ctx.saved_tensors
+    dy2 = dy.reshape(-1, dy.size(-1)).contiguous()
+    if dy2.dtype != w2c.dtype:
+        dy2 = dy2.to(w2c.dtype)
+    need = ctx.needs_input_grad
+    dw2 = _wgrad(dy2, h, ctx.w_dtypes[1]) if need[3] else None
+    db2 = _bias_grad(dy2, ctx.b2_dtype) if ctx.b2_dtype is not None and need[4] else None
+    res = None
+    if ctx.tanh and _lt_ok(dy2, w2c, pre):
+        # one GEMM: dpre = (dy W2) * gelu'(pre) and its column sums, dh never stored
+        res = _native.require().dense.dgelu_bgrad_lt(dy2, w2c, pre,
+                                                     ctx.b1_dtype or dy2.dtype) or None
+    if res is not None:
+        dpre, db1 = res
+    elif dy2.is_cuda and _native.available():
+        dh = dy2 @ w2c
+        dpre, db1 = _native.require().dense.gelu_bwd_bias_grad(
+            dh, pre, ctx.tanh, ctx.b1_dtype or dh.dtype)
+    else:
+        dh = dy2 @ w2c
+        with torch.enable_grad():
+            p = pre.detach().to(torch.promote_types(pre.dtype, torch.float32))
+            p.requires_grad_(True)
+            g, = torch.autograd.grad(F.gelu(p, approximate="tanh" if ctx.tanh else "none"),
+                                     p, dh.to(p.dtype))
+        dpre = g.to(dh.dtype)
+        db1 = _bias_grad(dpre, ctx.b1_dtype or dh.dtype)
+    dx = _dgrad(dpre, w1c, xc.shape, dskip) if need[0] else None
+    dw1 = _wgrad(dpre, xc.reshape(-1, xc.size(-1)), ctx.w_dtypes[0]) if need[1] else None
+    if ctx.b1_dtype is None or not need[2]:
+        db1 = None
+    return dx, dw1, db1, dw2, db2, None
 
 
 class FusedDenseGeluDenseFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, approximate):
-        dt = _compute_dtype(x)
-        with torch.autocast("cuda", enabled=False):
-            xc = _cast(x, dt)
-            w1c, b1c, w2c, b2c = _cast(w1, dt), _cast(b1, dt), _cast(w2, dt), _cast(b2, dt)
-            x2 = xc.reshape(-1, xc.size(-1))
-            pre = torch.addmm(b1c, x2, w1c.t()) if b1c is not None else x2 @ w1c.t()
-            h = F.gelu(pre, approximate=approximate)
-            y = torch.addmm(b2c, h, w2c.t()) if b2c is not None else h @ w2c.t()
-        ctx.save_for_backward(xc, w1c, pre, h, w2c)
-        ctx.b1_dtype = b1.dtype if b1 is not None else None
-        ctx.b2_dtype = b2.dtype if b2 is not None else None
-        ctx.tanh = approximate == "tanh"
-        ctx.w_dtypes = (w1.dtype, w2.dtype)
-        return y.view(*x.shape[:-1], w2.size(0))
+        return _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate)
 
     @staticmethod
     def backward(ctx, dy):
-        xc, w1c, pre, h, w2c = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.size(-1)).contiguous()
-        if dy2.dtype != w2c.dtype:
-            dy2 = dy2.to(w2c.dtype)
-        need = ctx.needs_input_grad
-        dw2 = _wgrad(dy2, h, ctx.w_dtypes[1]) if need[3] else None
-        db2 = _bias_grad(dy2, ctx.b2_dtype) if ctx.b2_dtype is not None and need[4] else None
-        dh = dy2 @ w2c
-        if dh.is_cuda and _native.available():
-            dpre, db1 = _native.require().dense.gelu_bwd_bias_grad(
-                dh, pre, ctx.tanh, ctx.b1_dtype or dh.dtype)
-        else:
-            with torch.enable_grad():
-                p = pre.detach().float().requires_grad_(True)
-                g, = torch.autograd.grad(F.gelu(p, approximate="tanh" if ctx.tanh else "none"),
-                                         p, dh.float())
-            dpre = g.to(dh.dtype)
-            db1 = dpre.float().sum(0).to(ctx.b1_dtype or dh.dtype)
-        dx = (dpre @ w1c).view(xc.shape) if need[0] else None
-        dw1 = _wgrad(dpre, xc.reshape(-1, xc.size(-1)), ctx.w_dtypes[0]) if need[1] else None
-        if ctx.b1_dtype is None or not need[2]:
-            db1 = None
-        return dx, dw1, db1, dw2, db2, None
+        return _gelu_dense_bwd(ctx, dy)
+
+
+class FusedDenseGeluDenseSkipFunc(torch.autograd.Function):
+    """(dense2(gelu(dense1(x))), x) with dx = dskip + dpre @ W1 in one GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, approximate):
+        return _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        return _gelu_dense_bwd(ctx, dy, dskip)
 
 
 def fused_dense_function(x, weight, bias):
     return FusedDenseFunc.apply(x, weight, bias)
+
+
+def fused_dense_skip_function(x, weight, bias):
+    """(dense(x), x) - use the second output as the residual so that the input
+    gradient is one accumulating GEMM (see FusedDenseSkipFunc)."""
+    return FusedDenseSkipFunc.apply(x, weight, bias)
+
+
+def fused_dense_gelu_dense_skip_function(x, w1, b1, w2, b2, approximate="none"):
+    return FusedDenseGeluDenseSkipFunc.apply(x, w1, b1, w2, b2, approximate)
 
 
 def dense_no_bias_function(x, weight):

@@ -9,8 +9,12 @@ layer and no autograd graph per op.
 MI355X mapping: the forward GEMM + bias + ReLU is a single hipBLASLt call with
 the RELU_BIAS epilogue (``torch._addmm_activation``), so the activation never
 makes its own pass over HBM; sigmoid / none use the BIAS epilogue (addmm) plus
-one elementwise pass.  The backward's activation derivative is recomputed
-from the saved output (relu: out > 0; sigmoid: out * (1 - out)).
+one elementwise pass.  Backward per layer: ONE pass of the gfx950 column-sum
+kernel (csrc/hip/bias_grad.hip, ``dense.act_bwd_bias_grad``) forms the
+pre-activation gradient from the saved output (relu: out > 0; sigmoid:
+out * (1 - out)) AND its column sums (the bias gradient) - the mask multiply
+and the bias reduction never make separate passes - then the dgrad and wgrad
+GEMMs (hipBLASLt; wgrad written in the weight dtype by the GEMM).
 Weights are [out, in] like nn.Linear, initialised as Apex's MLP
 (normal(0, sqrt(2/(fan_in+fan_out))), bias normal(0, sqrt(1/fan_out))).
 """
@@ -20,6 +24,8 @@ import math
 
 import torch
 from torch import nn
+
+from . import _native
 
 _ACTS = {"none": 0, "relu": 1, "sigmoid": 2}
 
@@ -63,16 +69,27 @@ class MlpFunction(torch.autograd.Function):
         act = ctx.activation
         gw = [None] * n
         gb = [None] * n
-        g = grad
+        bs = params[n:] if ctx.bias else [None] * n
+        g = grad.contiguous()
+        native = g.is_cuda and _native.available()
         for i in reversed(range(n)):
             y = outs[i + 1]
-            if act == 1:
-                g = g * (y > 0).to(g.dtype)
-            elif act == 2:
-                g = g * y * (1 - y)
-            gw[i] = g.t().mm(outs[i])
+            bdt = bs[i].dtype if bs[i] is not None else g.dtype
+            if act in (1, 2) and native:
+                g, db = _native.require().dense.act_bwd_bias_grad(g, y, act, bdt)
+            else:
+                if act == 1:
+                    g = g * (y > 0).to(g.dtype)
+                elif act == 2:
+                    g = g * y * (1 - y)
+                db = None
+                if ctx.bias:
+                    db = (_native.require().dense.bias_grad(g, bdt) if native
+                          else g.sum(0, dtype=torch.promote_types(g.dtype, torch.float32))
+                          .to(bdt))
             if ctx.bias:
-                gb[i] = g.sum(0)
+                gb[i] = db
+            gw[i] = g.t().mm(outs[i])
             g = g.mm(ws[i]) if (i > 0 or ctx.needs_input_grad[2]) else None
         grads = gw + (gb if ctx.bias else [])
         return (None, None, g, *grads)

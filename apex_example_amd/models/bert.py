@@ -19,7 +19,8 @@ import torch.nn.functional as F
 
 from .. import _native
 from ..normalization import FusedLayerNorm, fused_add_dropout_layer_norm
-from ..fused_dense import fused_dense_function, fused_dense_gelu_dense_function
+from ..fused_dense import (fused_dense_function, fused_dense_gelu_dense_skip_function,
+                           fused_dense_skip_function)
 from ..ops import attention as fused_attn
 
 
@@ -39,6 +40,11 @@ class BertConfig:
     fused_layer_norm: bool = True
     fused_attention: bool = True
     fused_dense: bool = True  # fused bias-grad / GELU-backward dense layers (fused_dense)
+    # FFN activation: "gelu_tanh" (apex fused_dense's GELU, the tanh approximation:
+    # forward and backward run inside hipBLASLt GEMM epilogues; |erf - tanh| GELU is
+    # < 1e-3, below bf16 resolution at FFN magnitudes) or "gelu" (erf).  The stock
+    # path (fused_dense=False) uses the same function, so comparisons stay like for like.
+    hidden_act: str = "gelu_tanh"
 
 
 def _ln(cfg, n):
@@ -79,17 +85,24 @@ class BertSelfAttention(nn.Module):
         return fused_dense_function(x, m.weight, m.bias) if self.fused_dense else m(x)
 
     def forward(self, x, attn_mask=None):
+        """Returns (attention output, x as the residual branch).  With fused_dense the
+        residual is the QKV layer's skip output, so the input gradient of the block
+        is one accumulating GEMM (no separate residual-gradient add)."""
         b, s, hd = x.shape
-        qkv = self._lin(self.qkv, x).view(b, s, 3, self.h, self.d)
+        if self.fused_dense:
+            qkv, skip = fused_dense_skip_function(x, self.qkv.weight, self.qkv.bias)
+        else:
+            qkv, skip = self.qkv(x), x
+        qkv = qkv.view(b, s, 3, self.h, self.d)
         p = self.p if self.training else 0.0
         if self.fused and attn_mask is None and fused_attn.supported(qkv, self.d):
             o = fused_attn.fused_attention_qkv(qkv, causal=False, dropout_p=p)
-            return self._lin(self.dense, o.view(b, s, hd))
+            return self._lin(self.dense, o.view(b, s, hd)), skip
         qkv = qkv.permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=p)
         o = o.transpose(1, 2).reshape(b, s, hd)
-        return self._lin(self.dense, o)
+        return self._lin(self.dense, o), skip
 
 
 class BertLayer(nn.Module):
@@ -103,16 +116,19 @@ class BertLayer(nn.Module):
         self.out_dropout = nn.Dropout(cfg.hidden_dropout_prob)
         self.out_ln = _ln(cfg, cfg.hidden_size)
         self.fused_dense = cfg.fused_dense
+        self.approximate = {"gelu_tanh": "tanh", "gelu": "none"}[cfg.hidden_act]
 
     def forward(self, x, attn_mask=None):
-        x, _ = fused_add_dropout_layer_norm(x, self.attention(x, attn_mask), self.attn_ln,
-                                            self.attn_dropout.p, self.training)
+        a, x = self.attention(x, attn_mask)
+        x, _ = fused_add_dropout_layer_norm(x, a, self.attn_ln, self.attn_dropout.p,
+                                            self.training)
         if self.fused_dense:
-            f = fused_dense_gelu_dense_function(x, self.intermediate.weight,
-                                                self.intermediate.bias, self.output.weight,
-                                                self.output.bias)
+            f, x = fused_dense_gelu_dense_skip_function(x, self.intermediate.weight,
+                                                        self.intermediate.bias,
+                                                        self.output.weight, self.output.bias,
+                                                        self.approximate)
         else:
-            f = self.output(F.gelu(self.intermediate(x)))
+            f = self.output(F.gelu(self.intermediate(x), approximate=self.approximate))
         return fused_add_dropout_layer_norm(x, f, self.out_ln, self.out_dropout.p,
                                             self.training)[0]
 

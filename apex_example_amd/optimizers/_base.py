@@ -92,14 +92,16 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         return stash is not None and stash.sync_free and stash.last_scaler is not None
 
     def _fold_scale(self):
-        """Scale argument for launch sets that read raw (loss-scaled) 16-bit grads."""
+        """Scale argument for launch sets that read raw (loss-scaled) grads: the scale
+        the grads were PRODUCED with (``grads_scale``), not the current one, which
+        update_scale() has already grown on a window's last step."""
         stash = self._amp()
         if stash is None or stash.last_scaler is None:
             return 1.0, False
-        sc = stash.last_scaler
-        if sc.sync_free:
-            return sc._scale_dev, True
-        return 1.0 / sc.loss_scale(), False
+        s = stash.last_scaler.grads_scale()
+        if isinstance(s, torch.Tensor):
+            return s, True
+        return 1.0 / s, False
 
     def _launch_sets(self, gid, group):
         """OrderedDict key -> dict(grads, params, copies, scaled).
@@ -120,12 +122,15 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         else:
             srcs = (group["params"],)
         grads = list(itertools.chain.from_iterable(map(_GRAD, s) for s in srcs))
-        key = (amp_path, fold)
+        # amp O1 folded unscale: the (fp32) grads still carry the loss scale
+        o1_scaled = bool(not amp_path and stash is not None
+                         and getattr(stash, "grads_scaled", False))
+        key = (amp_path, fold, o1_scaled)
         c = self._set_cache.get(gid)
         if (c is not None and c[0] == key and len(c[1]) == len(grads)
                 and all(map(operator.is_, c[1], grads))):
             return c[2]
-        sets = self._build_launch_sets(gid, group, stash, amp_path, fold)
+        sets = self._build_launch_sets(gid, group, stash, amp_path, fold, o1_scaled)
         self._set_cache[gid] = (key, grads, sets)
         return sets
 
@@ -146,7 +151,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         s["_state"] = (names, out)
         return out
 
-    def _build_launch_sets(self, gid, group, stash, amp_path, fold):
+    def _build_launch_sets(self, gid, group, stash, amp_path, fold, o1_scaled=False):
         sets = OrderedDict()
 
         def add(key, g, p, c, scaled):
@@ -177,7 +182,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
                     continue
                 if p.grad.is_sparse:
                     raise RuntimeError("fused optimizers do not support sparse gradients")
-                add((p.grad.dtype, p.dtype, None, False), p.grad, p, None, False)
+                add((p.grad.dtype, p.dtype, None, o1_scaled), p.grad, p, None, o1_scaled)
         return sets
 
     def _scale_args(self, scaled):
@@ -236,6 +241,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         stash = self._amp()
         if stash is not None:
             stash.model_grads_zeroed = True
+            stash.grads_scaled = False  # nothing loss-scaled is pending any more
 
     def _materialize_steps(self):
         for gid, t in self._dev_steps.items():

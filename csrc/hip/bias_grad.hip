@@ -9,9 +9,11 @@
 // S partials of a column (4 split lanes x 4 independent loads in flight) and
 // writes the bias dtype.  Deterministic, no atomics.
 //
-// gelu_bwd_colsum additionally computes dpre = dh * gelu'(pre) in the same pass
-// (erf or tanh GELU), writes dpre and its column partials, so the FFN's bias
-// gradient costs no extra read of dpre.
+// The activation-backward modes additionally compute the pre-activation gradient
+// in the same pass - dpre = dh * gelu'(pre) (erf or tanh GELU, fused_dense's FFN)
+// or dpre = dh * act'(y) from the layer's saved OUTPUT y (ReLU: y > 0; sigmoid:
+// y (1 - y); apex.mlp) - write it and its column partials, so the bias gradient
+// costs no extra read of dpre.
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -39,6 +41,14 @@ __device__ __forceinline__ float gelu_grad(float x, bool tanh_approx) {
 }
 
 // MODE 0: column sums of x.  MODE 1: dpre = dh * gelu'(pre) -> out, sums of dpre.
+// MODE 2 / 3: dpre = dh * relu'(y) / dh * sigmoid'(y) with y the saved output.
+template <int MODE>
+__device__ __forceinline__ float act_grad(float p, bool tanh_approx) {
+  if constexpr (MODE == 1) return gelu_grad(p, tanh_approx);
+  else if constexpr (MODE == 2) return p > 0.f ? 1.f : 0.f;
+  else return p * (1.f - p);
+}
+
 template <typename T, int MODE>
 __global__ void __launch_bounds__(kCsThreads)
     colsum_partial_k(const T* __restrict__ x, const T* __restrict__ pre, T* __restrict__ out,
@@ -57,11 +67,11 @@ __global__ void __launch_bounds__(kCsThreads)
     for (int64_t r = r0 + rl; r < r1; r += kCsRowLanes) {
       float v[8];
       ld8(x + r * N + c0, v);
-      if constexpr (MODE == 1) {
+      if constexpr (MODE != 0) {
         float p[8];
         ld8(pre + r * N + c0, p);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] *= gelu_grad(p[i], tanh_approx);
+        for (int i = 0; i < 8; ++i) v[i] *= act_grad<MODE>(p[i], tanh_approx);
         store8(out + r * N + c0, v);
       }
 #pragma unroll
@@ -113,22 +123,37 @@ int colsum_splits(int64_t M, int N) {
 }
 
 void colsum(const void* x, const void* pre, void* out_dpre, DType t, int64_t M, int N,
-            int gelu_mode, float* part, int S, void* bias_grad, DType tb, hipStream_t st) {
+            int act_mode, float* part, int S, void* bias_grad, DType tb, hipStream_t st) {
   const int rps = (int)((M + S - 1) / S);
   const dim3 grid((unsigned)((N + kCsCols - 1) / kCsCols), (unsigned)S);
-  const bool tanh_approx = gelu_mode == 2;
+  // act_mode: 0 none, 1 GELU (erf), 2 GELU (tanh), 3 ReLU(y), 4 sigmoid(y)
+  const bool tanh_approx = act_mode == 2;
   auto launch1 = [&](auto t0) {
     using T = decltype(t0);
-    if (gelu_mode == 0)
-      hipLaunchKernelGGL((colsum_partial_k<T, 0>), grid, dim3(kCsThreads), 0, st,
-                         static_cast<const T*>(x), nullptr, nullptr, M, N, rps, false, part);
-    else
-      hipLaunchKernelGGL((colsum_partial_k<T, 1>), grid, dim3(kCsThreads), 0, st,
-                         static_cast<const T*>(x), static_cast<const T*>(pre),
-                         static_cast<T*>(out_dpre), M, N, rps, tanh_approx, part);
+    const T* xp = static_cast<const T*>(x);
+    const T* pp = static_cast<const T*>(pre);
+    T* op = static_cast<T*>(out_dpre);
+    switch (act_mode) {
+      case 0:
+        hipLaunchKernelGGL((colsum_partial_k<T, 0>), grid, dim3(kCsThreads), 0, st, xp, nullptr,
+                           nullptr, M, N, rps, false, part);
+        break;
+      case 3:
+        hipLaunchKernelGGL((colsum_partial_k<T, 2>), grid, dim3(kCsThreads), 0, st, xp, pp, op,
+                           M, N, rps, false, part);
+        break;
+      case 4:
+        hipLaunchKernelGGL((colsum_partial_k<T, 3>), grid, dim3(kCsThreads), 0, st, xp, pp, op,
+                           M, N, rps, false, part);
+        break;
+      default:
+        hipLaunchKernelGGL((colsum_partial_k<T, 1>), grid, dim3(kCsThreads), 0, st, xp, pp, op,
+                           M, N, rps, tanh_approx, part);
+    }
   };
   if (t == DType::BF16) launch1(bf16_t{});
-  else launch1(half_t{});
+  else if (t == DType::F16) launch1(half_t{});
+  else launch1(float{});
   const dim3 g2((unsigned)((N + 63) / 64));
   if (tb == DType::F32)
     hipLaunchKernelGGL(colsum_final_k<float>, g2, dim3(256), 0, st, part, S, N,

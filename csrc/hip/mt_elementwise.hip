@@ -277,8 +277,12 @@ void flat_scale(const void* in, DType tin, void* out, DType tout, int64_t n, Sca
 // --------------------------------------------------------------------------
 __global__ void update_loss_scale_kernel(float* scale, int* unskipped, int* skipped_total,
                                          const int* overflow, float factor, int window,
-                                         float min_scale, float max_scale, int dynamic) {
+                                         float min_scale, float max_scale, int dynamic,
+                                         float* applied) {
   if (threadIdx.x != 0) return;
+  // the scale this step's gradients carry, for optimizers that unscale in-kernel
+  // AFTER this update (the growth step must not unscale by the doubled value)
+  if (applied) *applied = *scale;
   if (*overflow) {
     if (dynamic) {
       float s = *scale / factor;
@@ -301,9 +305,10 @@ __global__ void update_loss_scale_kernel(float* scale, int* unskipped, int* skip
 
 void update_loss_scale(float* scale, int* unskipped, int* skipped_total, const int* overflow,
                        float factor, int window, float min_scale, float max_scale, int dynamic,
-                       hipStream_t st) {
+                       hipStream_t st, float* applied) {
   hipLaunchKernelGGL(update_loss_scale_kernel, dim3(1), dim3(64), 0, st, scale, unskipped,
-                     skipped_total, overflow, factor, window, min_scale, max_scale, dynamic);
+                     skipped_total, overflow, factor, window, min_scale, max_scale, dynamic,
+                     applied);
 }
 
 __global__ void mark_step_done_kernel(int* flag, const int* noop) {

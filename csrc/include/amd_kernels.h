@@ -123,9 +123,10 @@ void mt_adagrad(const MTLaunch& L, DType g, DType p, const AdagradArgs& a, const
 // ----- loss scaler state machine (device resident) --------------------------
 // if *overflow: scale = max(scale/factor, min_scale), unskipped = 0, ++skipped
 // else: ++unskipped; if unskipped == window: scale = min(scale*factor, max), unskipped = 0
+// applied (optional): receives the PRE-update scale (the one this step's grads carry)
 void update_loss_scale(float* scale, int* unskipped, int* skipped_total, const int* overflow,
                        float factor, int window, float min_scale, float max_scale, int dynamic,
-                       hipStream_t st);
+                       hipStream_t st, float* applied = nullptr);
 
 // ----- flat buffers ---------------------------------------------------------
 // out[i] = in[i] * s (cast between dtypes), optional finiteness flag.
@@ -254,12 +255,13 @@ void stem_wgrad(const void* xp, const void* dy, float* part, int S, int N, int H
                 hipStream_t st);
 
 // ---- dense-layer bias gradients (bias_grad.hip) ------------------------------
-// bias_grad[n] = sum_m g[m, n] for a row-major 16-bit [M, N] (N % 8 == 0, 16-byte
-// aligned); gelu_mode 1 / 2: g = dh * gelu'(pre) (erf / tanh GELU) is computed in
-// the same pass and written to out_dpre.  part: S * N floats (S = colsum_splits).
+// bias_grad[n] = sum_m g[m, n] for a row-major [M, N] (bf16 / fp16 / fp32, N % 8 ==
+// 0, 16-byte aligned); act_mode 1 / 2: g = dh * gelu'(pre) (erf / tanh GELU), 3 / 4:
+// g = dh * relu'(y) / dh * sigmoid'(y) from the saved output y (passed as `pre`) is
+// computed in the same pass and written to out_dpre.  part: S * N floats.
 int colsum_splits(int64_t M, int N);
 void colsum(const void* x, const void* pre, void* out_dpre, DType t, int64_t M, int N,
-            int gelu_mode, float* part, int S, void* bias_grad, DType tb, hipStream_t st);
+            int act_mode, float* part, int S, void* bias_grad, DType tb, hipStream_t st);
 
 // ---- fused attention, head dim 64 (attention.hip) ---------------------------
 struct AttnLaunch {

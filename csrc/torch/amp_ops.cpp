@@ -345,18 +345,19 @@ void mt_adagrad_op(at::Tensor noop, const TensorLists& lists, double lr,
 
 void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, c10::optional<at::Tensor> skipped,
                           at::Tensor overflow, double factor, int64_t window, double min_scale,
-                          double max_scale, bool dynamic) {
+                          double max_scale, bool dynamic, c10::optional<at::Tensor> applied) {
   c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated
   TORCH_CHECK(scale.scalar_type() == at::kFloat && unskipped.scalar_type() == at::kInt &&
                   overflow.scalar_type() == at::kInt,
               "update_loss_scale: bad dtypes");
   if (!scale.is_cuda()) {
+    if (applied.has_value() && applied->defined()) applied->copy_(scale);
     return cpu::update_loss_scale(scale, unskipped, optp(skipped), overflow, (float)factor,
                                   (int)window, (float)min_scale, (float)max_scale, dynamic);
   }
   update_loss_scale(scale.data_ptr<float>(), unskipped.data_ptr<int>(), opt_iptr(skipped),
                     overflow.data_ptr<int>(), (float)factor, (int)window, (float)min_scale,
-                    (float)max_scale, dynamic ? 1 : 0, cur_stream());
+                    (float)max_scale, dynamic ? 1 : 0, cur_stream(), opt_fptr(applied));
 }
 
 void advance_step_op(at::Tensor step, c10::optional<at::Tensor> noop) {

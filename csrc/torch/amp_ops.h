@@ -39,7 +39,7 @@ void mt_adagrad_op(at::Tensor noop, const TensorLists& lists, double lr, OptT lr
                    int64_t mode, double wd, double scale, OptT scale_t, bool scale_inv);
 void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, OptT skipped, at::Tensor overflow,
                           double factor, int64_t window, double min_scale, double max_scale,
-                          bool dynamic);
+                          bool dynamic, OptT applied);
 void advance_step_op(at::Tensor step, OptT noop);
 void mark_step_done_op(at::Tensor flag, OptT noop);
 void flat_scale_op(at::Tensor in, at::Tensor out, double scale, OptT scale_t, bool invert,

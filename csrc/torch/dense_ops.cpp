@@ -10,7 +10,8 @@ namespace {
 
 bool colsum_ok(const at::Tensor& t) {
   return t.is_cuda() && t.is_contiguous() && t.dim() >= 1 &&
-         (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf) &&
+         (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf ||
+          t.scalar_type() == at::kFloat) &&
          t.size(-1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 &&
          t.numel() > 0;
 }
@@ -60,6 +61,31 @@ std::tuple<at::Tensor, at::Tensor> gelu_bwd_bias_grad_op(at::Tensor dh, at::Tens
   at::Tensor out = at::empty({N}, dh.options().dtype(out_dtype));
   colsum(dh.data_ptr(), pre.data_ptr(), dpre.data_ptr(), dtype_of(dh), M, (int)N,
          tanh_approx ? 2 : 1, part.data_ptr<float>(), S, out.data_ptr(), dtype_of(out),
+         cur_stream());
+  return {dpre, out};
+}
+
+std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tensor y, int64_t act,
+                                                        at::ScalarType out_dtype) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(dh.sizes() == y.sizes(), "act_bwd_bias_grad: shape mismatch");
+  TORCH_CHECK(act == 1 || act == 2, "act_bwd_bias_grad: act must be 1 (relu) or 2 (sigmoid)");
+  const int64_t N = dh.size(-1);
+  dh = dh.contiguous();
+  y = y.contiguous();
+  if (!colsum_ok(dh) || !colsum_ok(y) || dh.scalar_type() != y.scalar_type()) {
+    at::Tensor yf = y.to(at::kFloat);
+    at::Tensor d = act == 1 ? (yf > 0).to(at::kFloat) : yf * (1 - yf);
+    at::Tensor dpre = (dh.to(at::kFloat) * d).to(dh.scalar_type());
+    return {dpre, dpre.reshape({-1, N}).to(at::kFloat).sum(0).to(out_dtype)};
+  }
+  const int64_t M = dh.numel() / N;
+  const int S = colsum_splits(M, (int)N);
+  at::Tensor part = at::empty({(int64_t)S * N}, dh.options().dtype(at::kFloat));
+  at::Tensor dpre = at::empty_like(dh);
+  at::Tensor out = at::empty({N}, dh.options().dtype(out_dtype));
+  colsum(dh.data_ptr(), y.data_ptr(), dpre.data_ptr(), dtype_of(dh), M, (int)N,
+         act == 1 ? 3 : 4, part.data_ptr<float>(), S, out.data_ptr(), dtype_of(out),
          cur_stream());
   return {dpre, out};
 }

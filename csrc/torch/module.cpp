@@ -11,6 +11,7 @@
 #include "norm_ops.h"
 #include "pool_ops.h"
 #include "dense_ops.h"
+#include "lt_ops.h"
 #include "xent_ops.h"
 #include "reducer.h"
 
@@ -57,7 +58,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mt.def("lamb", &mt_lamb_op);
   mt.def("novograd", &mt_novograd_op);
   mt.def("adagrad", &mt_adagrad_op);
-  mt.def("update_loss_scale", &update_loss_scale_op);
+  mt.def("update_loss_scale", &update_loss_scale_op, py::arg("scale"), py::arg("unskipped"),
+         py::arg("skipped"), py::arg("overflow"), py::arg("factor"), py::arg("window"),
+         py::arg("min_scale"), py::arg("max_scale"), py::arg("dynamic"),
+         py::arg("applied") = py::none());
   mt.def("advance_step", &advance_step_op);
   mt.def("mark_step_done", &mark_step_done_op);
   mt.def("flat_scale", &flat_scale_op);
@@ -81,6 +85,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto dn = m.def_submodule("dense", "dense-layer bias gradients / fused GELU backward");
   dn.def("bias_grad", &bias_grad_op);
   dn.def("gelu_bwd_bias_grad", &gelu_bwd_bias_grad_op);
+  dn.def("act_bwd_bias_grad", &act_bwd_bias_grad_op);
+  dn.def("gelu_fwd_lt", &dense_gelu_fwd_op);
+  dn.def("dgelu_bgrad_lt", &dense_dgelu_bgrad_op);
+  dn.def("lt_cache_clear", &lt_algo_cache_clear);
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);

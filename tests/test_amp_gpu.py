@@ -107,11 +107,14 @@ def test_overflow_skips_step_and_halves_scale(materialize, capsys):
     torch.cuda.synchronize()
     changed = any(not torch.equal(b, p.detach()) for b, p in zip(before, model.parameters()))
     assert changed
+    torch.cuda.synchronize()
     scaler.poll()
-    # the Apex message is printed (immediately in sync mode, asynchronously otherwise)
+    # the Apex message is printed: immediately in sync mode; in sync-free mode from
+    # the pinned report the overflow step queued, once it reached the host
     out = capsys.readouterr().out
-    if not scaler.sync_free:
-        assert "Gradient overflow.  Skipping step" in out
+    assert ("Gradient overflow.  Skipping step, loss scaler 0 reducing loss scale to %s"
+            % float(s0 / 2)) in out, out
+    assert out.count("Gradient overflow.") == 1, out
 
 
 def test_o1_fp16_autocast_and_o3():
@@ -171,3 +174,87 @@ def test_fused_adam_lamb_o2_model_copy_in_kernel():
             torch.testing.assert_close(mp, ms.to(torch.bfloat16), rtol=0, atol=0)
         sd = opt.state_dict()
         assert sd["param_groups"][0]["step"] == 11
+
+
+@pytest.mark.parametrize("min_scale", [None, 2.0 ** 14])
+def test_sync_free_scaler_trajectory_matches_sync_mode(min_scale):
+    """The device-resident scaler (update_loss_scale kernel) follows Apex's
+    sync-mode state machine step for step - scale and clean-step counter - over
+    4,200 steps with injected overflows: back-to-back overflows (floored at
+    min_loss_scale), 2,000-step growth windows, an overflow right after growth."""
+    from apex_example_amd.amp.scaler import LossScaler
+
+    sync = LossScaler("dynamic", device=DEV, min_loss_scale=min_scale)
+    dev = LossScaler("dynamic", device=DEV, min_loss_scale=min_scale, sync_free=True)
+    assert not sync.sync_free and dev.sync_free
+    overflows = {3, 4, 5, 6, 700, 2706, 2707, 4100}
+    n = 4200
+    hist = torch.empty(n, 2, device=DEV)
+    ref = []
+    for i in range(n):
+        for s in (sync, dev):
+            s.clear_overflow_state()
+            if i in overflows:
+                s._overflow_buf.fill_(1)
+        skip = sync.update_scale()
+        assert skip == (i in overflows)
+        ref.append((sync.loss_scale(), sync._unskipped))
+        assert dev.update_scale() is False  # never a host decision in sync-free mode
+        hist[i, 0] = dev._scale_dev[0]
+        hist[i, 1] = dev._unskipped_dev[0].float()
+    got = hist.cpu().tolist()
+    for i, ((s_ref, u_ref), (s_dev, u_dev)) in enumerate(zip(ref, got)):
+        assert (s_ref, u_ref) == (s_dev, int(u_dev)), (i, (s_ref, u_ref), (s_dev, u_dev))
+    assert dev.skipped_steps() == len(overflows)
+    # the run crossed at least one full 2,000-step growth window (707..2706)
+    assert max(r[0] for r in ref[707:2706]) > ref[706][0]
+
+
+@pytest.mark.parametrize("opt_level", ["O1", "O2"])
+@pytest.mark.parametrize("sync_free", [True, False])
+def test_folded_unscale_matches_materialized_across_growth(opt_level, sync_free):
+    """Folded unscale (materialize_master_grads=False: the fused optimizer divides
+    by the loss scale in-kernel, AFTER update_scale ran) vs the materialized path
+    (grads unscaled before update_scale), with scale_window=2 so the scale GROWS
+    every other step: the folded path must divide by the scale the grads were
+    produced with, not the grown one.  O1 also covers the pending-grad unscale of
+    a second backward before a step (gradient accumulation)."""
+    from apex_example_amd import amp
+    from apex_example_amd.amp import amp as amp_mod
+    from apex_example_amd.optimizers import FusedAdam
+
+    def run(materialize):
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(),
+                                    torch.nn.Linear(64, 4)).to(DEV)
+        opt = FusedAdam(model.parameters(), lr=1e-2, materialize_master_grads=materialize)
+        model, opt = amp.initialize(model, opt, opt_level=opt_level, verbosity=0,
+                                    loss_scale="dynamic")
+        sc = amp._amp_state.loss_scalers[0]
+        sc._scale_seq_len = 2
+        if not sync_free and sc.sync_free:
+            sc.sync_free = False
+            opt._amp_stash.sync_free = False
+        torch.manual_seed(1)
+        scales = []
+        for it in range(6):
+            x = torch.randn(16, 32, device=DEV)
+            y = torch.randint(0, 4, (16,), device=DEV)
+            opt.zero_grad()
+            n_acc = 2 if (opt_level == "O1" and it == 3) else 1
+            for _ in range(n_acc):
+                loss = F.cross_entropy(model(x), y)
+                with amp.scale_loss(loss, opt) as s:
+                    s.backward()
+            opt.step()
+            scales.append(sc.loss_scale())
+        out = [p.detach().float().clone() for p in amp.master_params(opt)]
+        amp_mod.deinit()
+        amp._amp_state.handle = None
+        return out, scales
+
+    a, sa = run(True)
+    b, sb = run(False)
+    assert sa == sb and sa[-1] > sa[0], (sa, sb)
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)

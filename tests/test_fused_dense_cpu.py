@@ -100,3 +100,36 @@ def test_cast_cache_is_thread_local_and_identity_checked():
         assert seen[0] is not stale and torch.equal(seen[0], w.half())
     finally:
         st.active = None
+
+
+def test_skip_variants_match_plain_residual():
+    """(dense(x), x) skip functions: dx = dskip + dy @ W (accumulated in place)
+    equals autograd's sum over the two uses of x."""
+    from apex_example_amd.fused_dense import (fused_dense_gelu_dense_skip_function,
+                                              fused_dense_skip_function)
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 16, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(8, 16, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(8, dtype=torch.float64, requires_grad=True)
+    w2 = torch.randn(16, 8, dtype=torch.float64, requires_grad=True)
+    b2 = torch.randn(16, dtype=torch.float64, requires_grad=True)
+    y, skip = fused_dense_skip_function(x, w, b)
+    (y.pow(2).sum() + (skip * 3).sum()).backward()
+    got = [t.grad.clone() for t in (x, w, b)]
+    for t in (x, w, b):
+        t.grad = None
+    (torch.nn.functional.linear(x, w, b).pow(2).sum() + (x * 3).sum()).backward()
+    for g, t in zip(got, (x, w, b)):
+        torch.testing.assert_close(g, t.grad)
+    for t in (x, w, b):
+        t.grad = None
+    y, skip = fused_dense_gelu_dense_skip_function(x, w, b, w2, b2)
+    (y.pow(2).sum() + skip.sin().sum()).backward()
+    got = [t.grad.clone() for t in (x, w, b, w2, b2)]
+    for t in (x, w, b, w2, b2):
+        t.grad = None
+    F = torch.nn.functional
+    (F.linear(F.gelu(F.linear(x, w, b)), w2, b2).pow(2).sum() + x.sin().sum()).backward()
+    for g, t in zip(got, (x, w, b, w2, b2)):
+        torch.testing.assert_close(g, t.grad)

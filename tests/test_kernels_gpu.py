@@ -18,6 +18,15 @@ def C():
     return _native.require()
 
 
+def _assert_max_scaled(got, ref, rel):
+    """max |got - ref| <= rel * max |ref| (a bound that scales with the data, unlike
+    a fixed atol on sums of hundreds of terms)."""
+    got, ref = got.double(), ref.double()
+    err = float((got - ref).abs().max())
+    scale = float(ref.abs().max())
+    assert err <= rel * scale + 1e-12, (err, scale, err / max(scale, 1e-30))
+
+
 def _tensors(sizes, dtype, dev=DEV, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return [torch.randn(n, generator=g).to(dev, dtype) for n in sizes]
@@ -255,13 +264,14 @@ def test_layer_norm_fwd_bwd(shape, dt):
     yb = ref(xb)
     tol = dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(ya.float(), yb, **tol)
-    dy = torch.randn_like(yb)
-    ya.backward(dy.to(dt))
-    yb.backward(dy)
+    dy = torch.randn_like(yb).to(dt)  # the reference sees the same rounded dy
+    ya.backward(dy)
+    yb.backward(dy.float())
     torch.testing.assert_close(xa.grad.float(), xb.grad, **tol)
-    gtol = dict(rtol=1e-4, atol=1e-3) if dt == torch.float32 else dict(rtol=5e-2, atol=5e-1)
-    torch.testing.assert_close(ln.weight.grad.float(), ref.weight.grad, **gtol)
-    torch.testing.assert_close(ln.bias.grad.float(), ref.bias.grad, **gtol)
+    # dgamma / dbeta are sums over all rows: fp32 accumulation, one rounding to dt
+    rel = 1e-5 if dt == torch.float32 else 8e-3
+    _assert_max_scaled(ln.weight.grad.float(), ref.weight.grad, rel)
+    _assert_max_scaled(ln.bias.grad.float(), ref.bias.grad, rel)
 
 
 @pytest.mark.parametrize("shape", [(64, 1024), (4096, 1024), (3, 5, 768), (7, 2048), (9, 64)])
@@ -306,8 +316,8 @@ def test_add_dropout_layer_norm(shape, dt, p, use_s):
     tol = dict(rtol=1e-5, atol=1e-4) if dt == torch.float32 else dict(rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(sa.float(), sb, **tol)
     torch.testing.assert_close(ya.float(), yb, **tol)
-    dy = torch.randn_like(yb)
-    de = torch.randn_like(yb)
+    dy = torch.randn_like(yb).to(dt).float()
+    de = torch.randn_like(yb).to(dt).float()
     la = (ya.float() * dy).sum() + ((sa.float() * de).sum() if use_s else 0.0)
     lb = (yb * dy).sum() + ((sb * de).sum() if use_s else 0.0)
     la.backward()
@@ -315,9 +325,11 @@ def test_add_dropout_layer_norm(shape, dt, p, use_s):
     gt = dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=3e-2, atol=6e-2)
     torch.testing.assert_close(xa.grad.float(), xb.grad, **gt)
     torch.testing.assert_close(ha.grad.float(), hb.grad, **gt)
-    wt = dict(rtol=1e-4, atol=1e-3) if dt == torch.float32 else dict(rtol=5e-2, atol=5e-1)
-    torch.testing.assert_close(ln.weight.grad.float(), ref.weight.grad, **wt)
-    torch.testing.assert_close(ln.bias.grad.float(), ref.bias.grad, **wt)
+    # 16-bit: x and h are rounded inputs of the reference too, but s = x + h*keep/(1-p)
+    # is rounded to dt in the kernel's saved residual stream -> a few ulp of dt
+    rel = 1e-5 if dt == torch.float32 else 1.5e-2
+    _assert_max_scaled(ln.weight.grad.float(), ref.weight.grad, rel)
+    _assert_max_scaled(ln.bias.grad.float(), ref.bias.grad, rel)
 
 
 @pytest.mark.parametrize("hdt", [torch.float16, torch.bfloat16])
@@ -436,16 +448,18 @@ def test_fused_bn(fmt, dt, relu, res, shape):
     assert ya.is_contiguous(memory_format=mf)
     torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
-    dy = torch.randn_like(yb)
-    ya.backward(dy.to(dt))
-    yb.backward(dy)
+    dy = torch.randn_like(yb).to(dt)  # the reference sees the same rounded dy
+    ya.backward(dy)
+    yb.backward(dy.float())
     gt = dict(rtol=1e-3, atol=1e-3) if dt == torch.float32 else dict(rtol=5e-2, atol=6e-2)
     torch.testing.assert_close(xa.grad.float(), xb.grad, **gt)
     if res:
         torch.testing.assert_close(za.grad.float(), zb.grad, **gt)
-    wt = dict(rtol=1e-3, atol=1e-2) if dt == torch.float32 else dict(rtol=5e-2, atol=1.0)
-    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, **wt)
-    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, **wt)
+    # fp32 dgamma / dbeta from fp32 accumulation; with 16-bit x the relu mask and
+    # x_hat are formed from the same rounded x as the reference: max-scaled bounds
+    rel = 1e-5 if dt == torch.float32 else 2e-3
+    _assert_max_scaled(bn.weight.grad, ref.weight.grad, rel)
+    _assert_max_scaled(bn.bias.grad, ref.bias.grad, rel)
 
 
 def test_bn_stats_large_mean_no_cancellation():
@@ -474,11 +488,12 @@ def test_conv1x1_gemm_matches_conv(shape):
     yr = F.conv2d(xr, wr)
     assert y.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2)
-    dy = torch.randn_like(yr)
-    y.backward(dy.to(torch.bfloat16))
-    yr.backward(dy)
-    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=1e-1)
-    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=5e-1)
+    dy = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    # bf16 outputs of fp32-accumulated GEMMs: one rounding (2^-8 relative) each
+    _assert_max_scaled(x.grad.float(), xr.grad, 8e-3)
+    _assert_max_scaled(m.weight.grad.float(), wr.grad, 8e-3)
 
 
 @pytest.mark.parametrize("cl", [False, True])
@@ -519,34 +534,50 @@ def test_conv1x1_skip_fused_residual_grad():
     wr = m.weight.detach().float().clone().requires_grad_(True)
     outr = (F.conv2d(xr, wr) ** 2).sum() + (xr * 3).sum()
     outr.backward()
-    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=2e-1)
-    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=3e-2, atol=1.0)
+    # the upstream gradient 2*y is formed from the bf16 y: bounds scale with the data
+    _assert_max_scaled(x.grad.float(), xr.grad, 2e-2)
+    _assert_max_scaled(m.weight.grad.float(), wr.grad, 2e-2)
 
 
 def test_resnet50_fused_vs_plain_forward_backward():
-    """ResNet-50 with the fused BN / GEMM-1x1 / skip-GEMM paths vs a CPU float64
-    reference (same weights): loss and every parameter grad.  A 50-layer net at
-    random init with 4-sample BatchNorm is ill-conditioned: plain torch fp32 -
-    on the CPU as on the GPU - is itself 1.5-3 % off fp64 (median over tensors,
-    worst ~4 %; tools/diag/resnet_grad_parity.py), so the bounds are ~3x that;
-    a wrong kernel shows up as O(1) errors."""
+    """ResNet-50 with the fused BN / GEMM-1x1 / skip-GEMM / MFMA-conv paths (fp32)
+    vs stock PyTorch fp32 on the same GPU, both measured against a CPU float64
+    run of the same weights and batch.  A 50-layer net at random init with a
+    4-sample BatchNorm is ill-conditioned (stock fp32 itself is a few % off fp64,
+    tools/diag/resnet_grad_parity.py), so the bound is relative to stock: every
+    parameter gradient of the fused path must be within 2.5x stock's own fp64
+    error (+0.5 %) - measured worst 2.1x, on 2 of 161 tensors - and its median
+    no worse than stock's median + 0.5 %.  A wrong kernel shows up as O(1)
+    errors."""
     from apex_example_amd.models import resnet50
 
     torch.manual_seed(0)
     a = resnet50(num_classes=10, fused_bn=True, gemm_1x1=True)
+    stock = resnet50(num_classes=10)
     ref = resnet50(num_classes=10).double()
+    stock.load_state_dict(a.state_dict())
     ref.load_state_dict(a.state_dict())
     a = a.to(DEV).to(memory_format=torch.channels_last)
+    stock = stock.to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(4, 3, 64, 64)
     y = torch.randint(0, 10, (4,))
-    la = F.cross_entropy(a(x.to(DEV).to(memory_format=torch.channels_last)), y.to(DEV))
+    xd = x.to(DEV).to(memory_format=torch.channels_last)
+    la = F.cross_entropy(a(xd), y.to(DEV))
+    ls = F.cross_entropy(stock(xd), y.to(DEV))
     lr = F.cross_entropy(ref(x.double()), y)
-    assert abs(la.item() - lr.item()) < 1e-4
+    assert abs(la.item() - lr.item()) < 1e-4 and abs(ls.item() - lr.item()) < 1e-4
     la.backward()
+    ls.backward()
     lr.backward()
-    errs = sorted(float((pa.grad.double().cpu() - pb.grad).norm() / pb.grad.norm())
-                  for pa, pb in zip(a.parameters(), ref.parameters()))
-    assert errs[-1] < 1.5e-1 and errs[len(errs) // 2] < 8e-2, (errs[-3:], errs[len(errs) // 2])
+
+    def rel(p, q):
+        return float((p.grad.double().cpu() - q.grad).norm() / q.grad.norm())
+    ea = [rel(pa, pr) for pa, pr in zip(a.parameters(), ref.parameters())]
+    es = [rel(ps, pr) for ps, pr in zip(stock.parameters(), ref.parameters())]
+    worst = [(i, e, f) for i, (e, f) in enumerate(zip(ea, es)) if e > 2.5 * f + 5e-3]
+    assert not worst, worst[:5]
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    assert med(ea) <= med(es) + 5e-3, (med(ea), med(es))
 
 
 @pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 24, 9, 11), 3, 2, 1),
@@ -760,3 +791,68 @@ def test_bias_grad_kernels(dt, mn):
         # the kernel sums the fp32 dpre (before its bf16 rounding): compare with the
         # fp32 reference's column sums
         torch.testing.assert_close(db, r.sum(0), rtol=1e-3, atol=1e-3 * max(1.0, m ** 0.5))
+
+
+# ------------------------------------------------------------------ apex.mlp
+@pytest.mark.parametrize("activation", ["relu", "sigmoid", "none"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_mlp_native_backward(activation, dt):
+    """MLP backward on dense.act_bwd_bias_grad (activation derivative from the saved
+    output + bias column sums in one pass).  fp32: vs an nn.Sequential chain with
+    tight bounds.  bf16: both our MLP and a stock bf16 nn.Sequential are measured
+    against the fp32 chain; ours must be within 1.5x stock's error (+1 %) - the
+    error is bf16 rounding of the per-layer activations / ReLU-mask flips, which
+    both paths share."""
+    from apex_example_amd import _native
+    from apex_example_amd.mlp import MLP
+
+    torch.manual_seed(0)
+    sizes = [480, 1024, 512, 256, 8]
+    mlp = MLP(sizes, activation=activation).to(DEV).to(dt)
+
+    def chain(dtype):
+        layers = []
+        for i, (w, b) in enumerate(zip(mlp.weights, mlp.biases)):
+            lin = torch.nn.Linear(sizes[i], sizes[i + 1]).to(DEV).to(dtype)
+            with torch.no_grad():
+                lin.weight.copy_(w)
+                lin.bias.copy_(b)
+            layers.append(lin)
+            if activation == "relu":
+                layers.append(torch.nn.ReLU())
+            elif activation == "sigmoid":
+                layers.append(torch.nn.Sigmoid())
+        return torch.nn.Sequential(*layers)
+
+    ref, stock = chain(torch.float32), chain(dt)
+    x = torch.randn(257, 480, device=DEV).to(dt).requires_grad_(True)
+    xr = x.detach().float().clone().requires_grad_(True)
+    xs = x.detach().clone().requires_grad_(True)
+    y, yr, ys = mlp(x), ref(xr), stock(xs)
+    dy = torch.randn_like(yr).to(dt)
+    y.backward(dy)
+    yr.backward(dy.float())
+    ys.backward(dy)
+    lins = [m for m in ref if isinstance(m, torch.nn.Linear)]
+    slins = [m for m in stock if isinstance(m, torch.nn.Linear)]
+    pairs = [(y, yr, ys), (x.grad, xr.grad, xs.grad)]
+    pairs += [(w.grad, lr.weight.grad, ls.weight.grad) for w, lr, ls in zip(mlp.weights, lins, slins)]
+    pairs += [(b.grad, lr.bias.grad, ls.bias.grad) for b, lr, ls in zip(mlp.biases, lins, slins)]
+    for k, (ours, want, st) in enumerate(pairs):
+        if dt == torch.float32:
+            _assert_max_scaled(ours.float(), want, 1e-4)
+        else:
+            sc = float(want.abs().max())
+            e_ours = float((ours.float() - want).abs().max()) / sc
+            e_stock = float((st.float() - want).abs().max()) / sc
+            assert e_ours <= 1.5 * e_stock + 1e-2, (k, e_ours, e_stock)
+    # the kernel itself: one pass gives dpre and the fp32 column sums of g * act'(y)
+    if activation in ("relu", "sigmoid"):
+        g = torch.randn(300, 1024, device=DEV).to(dt)
+        yy = torch.rand(300, 1024, device=DEV).sub(0.3).to(dt)
+        a = 1 if activation == "relu" else 2
+        dpre, db = _native.require().dense.act_bwd_bias_grad(g, yy, a, torch.float32)
+        d = (yy.float() > 0).float() if a == 1 else yy.float() * (1 - yy.float())
+        want = g.float() * d
+        _assert_max_scaled(dpre.float(), want, 1e-6 if dt == torch.float32 else 8e-3)
+        _assert_max_scaled(db, want.sum(0), 1e-5)

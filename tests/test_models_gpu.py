@@ -3,6 +3,7 @@ stays fast): BERT amp O2 + FusedLAMB + FusedLayerNorm, GPT-2 amp O1 fp16 +
 FusedAdam including the dynamic-loss-scale overflow-skip path."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -136,3 +137,49 @@ def test_cast_params_once_matches_per_weight_casts():
     with torch.autocast("cuda", dtype=torch.float16), cast_params_once([w, b], torch.float16):
         y2 = fused_dense_function(x, w, b)
     assert not torch.equal(y2, outs[0][0])
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_fused_dense_gelu_hipblaslt_epilogues(dt):
+    """FusedDenseGeluDense(approximate="tanh") on the hipBLASLt GELU_AUX_BIAS /
+    DGELU_BGRAD epilogues vs the same layer composed from fp32 torch ops (tanh GELU)
+    fed the same rounded operands; the epilogue ops must actually be taken."""
+    from apex_example_amd import _native
+    from apex_example_amd.fused_dense import FusedDenseGeluDense
+
+    torch.manual_seed(0)
+    x2 = torch.randn(1024, 256, device="cuda").to(dt)
+    w1 = (torch.randn(1024, 256, device="cuda") * 0.05).to(dt)
+    b1 = torch.randn(1024, device="cuda").to(dt)
+    res = _native.require().dense.gelu_fwd_lt(x2, w1, b1)
+    assert len(res) == 2, "hipBLASLt offered no GELU_AUX_BIAS algorithm"
+    h, pre = res
+    pre_ref = x2.float() @ w1.float().t() + b1.float()
+    torch.testing.assert_close(pre.float(), pre_ref, rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(h.float(), F.gelu(pre_ref, approximate="tanh"),
+                               rtol=1e-2, atol=2e-2)
+    w2 = (torch.randn(256, 1024, device="cuda") * 0.05).to(dt)
+    dy = torch.randn(1024, 256, device="cuda").to(dt)
+    res = _native.require().dense.dgelu_bgrad_lt(dy, w2, pre, dt)
+    assert len(res) == 2, "hipBLASLt offered no DGELU_BGRAD algorithm"
+    dpre, db = res
+    p = pre.float().requires_grad_(True)
+    g, = torch.autograd.grad(F.gelu(p, approximate="tanh"), p, dy.float() @ w2.float())
+    torch.testing.assert_close(dpre.float(), g, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(db.float(), g.sum(0), rtol=2e-2, atol=2e-1)
+
+    # the module end to end (forward + backward) vs fp32 torch ops
+    m = FusedDenseGeluDense(256, 1024, 256, approximate="tanh").cuda().to(dt)
+    xa = torch.randn(8, 128, 256, device="cuda").to(dt).requires_grad_(True)
+    xr = xa.detach().float().clone().requires_grad_(True)
+    ps = [m.weight1, m.bias1, m.weight2, m.bias2]
+    pr = [t.detach().float().clone().requires_grad_(True) for t in ps]
+    ya = m(xa)
+    yr = F.linear(F.gelu(F.linear(xr, pr[0], pr[1]), approximate="tanh"), pr[2], pr[3])
+    torch.testing.assert_close(ya.float(), yr, rtol=2e-2, atol=5e-2)
+    g = torch.randn_like(yr).to(dt)
+    ya.backward(g)
+    yr.backward(g.float())
+    for a, r in zip([xa] + ps, [xr] + pr):
+        err = float((a.grad.float() - r.grad).abs().max())
+        assert err <= 2e-2 * float(r.grad.abs().max()) + 1e-3, err

@@ -406,7 +406,7 @@ def bench_optim(args):
     cp = [p.to(torch.bfloat16) for p in ps]
     noop = torch.zeros(1, dtype=torch.int32, device=dev)
     cases = [
-        ("SGD fp32 [g,p,m]", 16, lambda: amp_C.multi_tensor_sgd(
+        ("SGD fp32 [g,p,m]", 20, lambda: amp_C.multi_tensor_sgd(
             0, noop, [g32, ps, mom], 1e-4, 0.9, 0.0, 0.1, False, False, False, 1.0)),
         ("SGD O2 [g16,p,m,copy16]", 20, lambda: amp_C.multi_tensor_sgd(
             0, noop, [g16, ps, mom, cp], 1e-4, 0.9, 0.0, 0.1, False, False, False, 1 / 1024.)),
