@@ -120,40 +120,64 @@ def multi_tensor_lamb(chunk_size, noop_flag, tensor_lists, lr, beta1, beta2, eps
               float(max_grad_norm), bool(use_nvlamb), sv, st, scale_inv)
 
 
+def _dev_scalar(v, device):
+    """A python number or 1-element tensor as a 0-dim fp32 device tensor (no sync)."""
+    if isinstance(v, torch.Tensor):
+        return v.reshape(()).to(device=device, dtype=torch.float32)
+    return torch.tensor(float(v), dtype=torch.float32, device=device)
+
+
 def multi_tensor_lamb_stage1_cuda(chunk_size, noop_flag, tensor_lists, per_tensor_decay, step,
                                   beta1, beta2, epsilon, global_grad_norm, max_global_grad_norm):
-    """Legacy two-stage LAMB, stage 1 (writes the update into tensor_lists[4]).
-    Composed from torch ops (reference semantics; the fused path is multi_tensor_lamb)."""
+    """Legacy two-stage LAMB, stage 1 (apex csrc/multi_tensor_lamb_stage_1.cu): Adam
+    moments of the clipped grad and the update u = m^/(sqrt(v^)+eps) + decay_i * p
+    written into tensor_lists[4].  API parity for callers of the old interface (the
+    fused path is multi_tensor_lamb): composed from device tensor ops with the
+    overflow flag and the global norm kept on the device - no host sync."""
     g, p, m, v, u = tensor_lists
-    if noop_flag.item() != 0:
+    if not g:
         return
-    gn = float(global_grad_norm)
-    clip = gn / max_global_grad_norm if gn > max_global_grad_norm else 1.0
+    dev = p[0].device
+    keep = noop_flag.reshape(()).to(dev).eq(0)
+    gn = _dev_scalar(global_grad_norm, dev)
+    mx = float(max_global_grad_norm)
+    clip = torch.where(gn > mx, gn / mx, torch.ones_like(gn))
     bc1 = 1 - beta1 ** step
     bc2 = 1 - beta2 ** step
     with torch.no_grad():
         for i in range(len(g)):
+            d = per_tensor_decay[i]
+            d = d.reshape(()).to(dev, torch.float32) if isinstance(d, torch.Tensor) else float(d)
             gi = g[i].float() / clip
-            m[i].mul_(beta1).add_(gi.to(m[i].dtype), alpha=1 - beta1)
-            v[i].mul_(beta2).addcmul_(gi.to(v[i].dtype), gi.to(v[i].dtype), value=1 - beta2)
-            upd = (m[i].float() / bc1) / ((v[i].float() / bc2).sqrt() + epsilon)
-            upd = upd + float(per_tensor_decay[i]) * p[i].float()
-            u[i].copy_(upd)
+            mn = m[i].float() * beta1 + gi * (1 - beta1)
+            vn = v[i].float() * beta2 + gi * gi * (1 - beta2)
+            upd = (mn / bc1) / ((vn / bc2).sqrt() + epsilon) + d * p[i].float()
+            m[i].copy_(torch.where(keep, mn, m[i].float()))
+            v[i].copy_(torch.where(keep, vn, v[i].float()))
+            u[i].copy_(torch.where(keep, upd, u[i].float()))
 
 
 def multi_tensor_lamb_stage2_cuda(chunk_size, noop_flag, tensor_lists, per_tensor_param_norm,
                                   per_tensor_update_norm, lr, weight_decay=0.0, use_nvlamb=False):
+    """Legacy LAMB stage 2: p -= lr * (||p|| / ||u||) * u per tensor (trust ratio 1
+    when a norm is zero, plain lr when neither weight decay nor nvlamb applies).
+    Device-side like stage 1: no host sync."""
     p, u = tensor_lists[:2]
-    if noop_flag.item() != 0:
+    if not p:
         return
+    dev = p[0].device
+    keep = noop_flag.reshape(()).to(dev).eq(0)
     with torch.no_grad():
         for i in range(len(p)):
-            pn = float(per_tensor_param_norm[i])
-            un = float(per_tensor_update_norm[i])
-            ratio = lr
             if use_nvlamb or weight_decay != 0.0:
-                ratio = lr * (pn / un) if (pn != 0.0 and un != 0.0) else lr
-            p[i].add_(u[i].to(p[i].dtype), alpha=-ratio)
+                pn = _dev_scalar(per_tensor_param_norm[i], dev)
+                un = _dev_scalar(per_tensor_update_norm[i], dev)
+                ratio = torch.where((pn != 0) & (un != 0), lr * pn / un,
+                                    torch.full_like(pn, float(lr)))
+            else:
+                ratio = _dev_scalar(lr, dev)
+            step_i = u[i].float() * (ratio * keep)
+            p[i].sub_(step_i.to(p[i].dtype))
 
 
 def multi_tensor_novograd(chunk_size, noop_flag, tensor_lists, grad_norms, lr, beta1, beta2,

@@ -170,9 +170,12 @@ def _dense_bwd(ctx, dy, dskip=None):
         dy2 = dy2.to(wc.dtype)
     if ctx.needs_input_grad[0]:
         dx = _dgrad(dy2, wc, xc.shape, dskip)
-    if ctx.needs_input_grad[1]:
+    need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[2]
+    if ctx.needs_input_grad[1] and need_b:
+        dw, db = _wgrad_bgrad(dy2, xc.reshape(-1, xc.size(-1)), ctx.w_dtype, ctx.bias_dtype)
+    elif ctx.needs_input_grad[1]:
         dw = _wgrad(dy2, xc.reshape(-1, xc.size(-1)), ctx.w_dtype)
-    if ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
+    elif need_b:
         db = _bias_grad(dy2, ctx.bias_dtype)
     return dx, dw, db
 
@@ -212,6 +215,35 @@ def _lt_ok(*ts):
             and all(t.dtype == ts[0].dtype for t in ts) and _native.available())
 
 
+# (op, shapes, dtypes) the library offered no algorithm for: not asked again
+_LT_MISSING = set()
+
+
+def _lt_call(name, *args):
+    """Run a hipBLASLt epilogue op of csrc/torch/lt_ops.cpp; None when the library
+    has no algorithm for this problem (remembered, so the fallback is direct)."""
+    key = (name,) + tuple((tuple(a.shape), a.dtype) if isinstance(a, torch.Tensor) else a
+                          for a in args)
+    if key in _LT_MISSING:
+        return None
+    res = getattr(_native.require().dense, name)(*args)
+    if not res:
+        _LT_MISSING.add(key)
+        return None
+    return res
+
+
+def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype):
+    """(dW, db): one hipBLASLt GEMM with the BGRADB epilogue when available (the
+    bias gradient rides on the weight-gradient GEMM's read of dy), else the GEMM +
+    the column-sum kernel."""
+    if _lt_ok(dy2, x2):
+        res = _lt_call("wgrad_bgrad_lt", dy2, x2, w_dtype, b_dtype)
+        if res is not None:
+            return res
+    return _wgrad(dy2, x2, w_dtype), _bias_grad(dy2, b_dtype)
+
+
 def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
     dt = _compute_dtype(x)
     with torch.autocast("cuda", enabled=False):
@@ -221,7 +253,7 @@ def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
         res = None
         if approximate == "tanh" and _lt_ok(x2, w1c, b1c):
             # one GEMM: h = gelu(x W1^T + b1) with pre as the epilogue's aux output
-            res = _native.require().dense.gelu_fwd_lt(x2, w1c, b1c) or None
+            res = _lt_call("gelu_fwd_lt", x2, w1c, b1c)
         if res is not None:
             h, pre = res
         else:
@@ -244,13 +276,18 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
     if dy2.dtype != w2c.dtype:
         dy2 = dy2.to(w2c.dtype)
     need = ctx.needs_input_grad
-    dw2 = _wgrad(dy2, h, ctx.w_dtypes[1]) if need[3] else None
-    db2 = _bias_grad(dy2, ctx.b2_dtype) if ctx.b2_dtype is not None and need[4] else None
+    dw2 = db2 = None
+    need_b2 = ctx.b2_dtype is not None and need[4]
+    if need[3] and need_b2:
+        dw2, db2 = _wgrad_bgrad(dy2, h, ctx.w_dtypes[1], ctx.b2_dtype)
+    elif need[3]:
+        dw2 = _wgrad(dy2, h, ctx.w_dtypes[1])
+    elif need_b2:
+        db2 = _bias_grad(dy2, ctx.b2_dtype)
     res = None
     if ctx.tanh and _lt_ok(dy2, w2c, pre):
         # one GEMM: dpre = (dy W2) * gelu'(pre) and its column sums, dh never stored
-        res = _native.require().dense.dgelu_bgrad_lt(dy2, w2c, pre,
-                                                     ctx.b1_dtype or dy2.dtype) or None
+        res = _lt_call("dgelu_bgrad_lt", dy2, w2c, pre, ctx.b1_dtype or dy2.dtype)
     if res is not None:
         dpre, db1 = res
     elif dy2.is_cuda and _native.available():

@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
 from ..ops.conv import Conv2d1x1, Conv2d3x3, StemConv2d
-from ..ops.pool import MaxPool2dNHWC
+from ..ops.pool import MaxPool2dNHWC, bn_relu_maxpool, bn_relu_maxpool_fusable
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1, mfma=False):
@@ -154,8 +154,13 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.bn1(self.conv1(x))
-        x = self.maxpool(x)
+        x = self.conv1(x)
+        if (self.fused_bn and isinstance(self.maxpool, MaxPool2dNHWC)
+                and bn_relu_maxpool_fusable(x, self.bn1.bn, self.maxpool)):
+            # stem BN + ReLU applied inside the max-pool's loads (never materialised)
+            x = bn_relu_maxpool(x, self.bn1.bn, self.maxpool)
+        else:
+            x = self.maxpool(self.bn1(x))
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -7,11 +7,16 @@ element written once), replacing ATen's NHWC max_pool2d kernels, which cost
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+
+# A/B switch for the fused stem (tools, docs/PERF.md)
+_FUSE_STEM = os.environ.get("APEX_AMD_FUSE_STEM", "1") == "1"
 
 
 class MaxPool2dNHWCFunction(torch.autograd.Function):
@@ -27,6 +32,62 @@ class MaxPool2dNHWCFunction(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         H, W, k, s, p = ctx.geom
         return _native.require().pool.max_bwd(dy, idx, H, W, k, s, p), None, None, None
+
+
+class BNReLUMaxPoolFunction(torch.autograd.Function):
+    """maxpool(relu(batchnorm(x))) in training mode without materialising the
+    BatchNorm output (the ResNet stem: conv 7x7 -> BN -> ReLU -> max-pool 3x3/2).
+
+    Forward: the BN statistics pass (running stats and num_batches_tracked
+    updated on the device), then ONE pooling pass that applies the BN affine +
+    ReLU to x as it loads the window (csrc/hip/pool.hip) - the separate BN
+    apply (read x, write y: 2 x 411 MB per step at ResNet-50 bs 256) disappears.
+    Backward: the pooling gather yields the gradient of the BN+ReLU output, then
+    the BN reduce + elementwise kernels (ReLU condition recomputed from x)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, eps, momentum, k, s, p):
+        C = _native.require()
+        mean, invstd = C.bn.train_stats(x, running_mean, running_var, nbt, float(eps),
+                                        float(momentum))
+        y, idx = C.pool.max_fwd_bn(x, mean, invstd, weight, bias, k, s, p)
+        ctx.save_for_backward(x, weight, bias, mean, invstd, idx)
+        ctx.geom = (x.size(2), x.size(3), k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, invstd, idx = ctx.saved_tensors
+        H, W, k, s, p = ctx.geom
+        C = _native.require()
+        dbn = C.pool.max_bwd(dy, idx, H, W, k, s, p)
+        need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        sum_dy, sum_dy_xmu, gw, gb = C.bn.reduce_grad(dbn, x, mean, invstd, weight, bias, None,
+                                                      True, need_w)
+        count = x.numel() // x.size(1)
+        dx, _ = C.bn.backward_elemt(dbn, x, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
+                                    float(count), None, True, False)
+        return (dx, gw if need_w else None, gb if need_w else None,
+                None, None, None, None, None, None, None, None)
+
+
+def bn_relu_maxpool_fusable(x, bn, pool):
+    """True when ``pool(relu(bn(x)))`` can run as BNReLUMaxPoolFunction."""
+    k, s, p = pool.kernel_size, pool.stride, pool.padding
+    return (_FUSE_STEM and bn.training and bn.track_running_stats and bn.momentum is not None
+            and x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.size(1) % 8 == 0 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and bn.weight is not None and bn.weight.dtype == torch.float32
+            and bn.bias.dtype == torch.float32 and bn.running_mean.dtype == torch.float32
+            and isinstance(k, int) and isinstance(s, int) and isinstance(p, int)
+            and pool.dilation == 1 and not pool.ceil_mode and not pool.return_indices
+            and p <= k // 2 and k <= 15 and _native.available())
+
+
+def bn_relu_maxpool(x, bn, pool):
+    return BNReLUMaxPoolFunction.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                       bn.num_batches_tracked, bn.eps, bn.momentum,
+                                       pool.kernel_size, pool.stride, pool.padding)
 
 
 class MaxPool2dNHWC(nn.MaxPool2d):

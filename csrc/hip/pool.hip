@@ -4,6 +4,11 @@
 // tap, VEC path; scalar path for C % 8 != 0) of one output pixel, scans the
 // window in (kh, kw) order keeping the FIRST maximum (NaN propagates, as torch),
 // writes y and the winning tap index as one byte per element (kh*k + kw).
+// BN variant (ResNet stem): the window values are relu(x * scale + shift) with the
+// BatchNorm's per-channel affine applied on load - the BN + ReLU output is never
+// written to HBM (saves one write + one read of the largest activation of the
+// network); values are rounded to T before the comparison so ties and the
+// chosen taps match pooling the materialised bf16 tensor.
 // Backward is a gather, not a scatter: a thread owns 8 channels of one INPUT
 // pixel and sums dy over the <= ceil(k/s)^2 output windows that cover it and
 // picked it, so there are no atomics and every dx element is written once.
@@ -16,10 +21,14 @@ namespace {
 
 constexpr int kPoolThreads = 256;
 
-template <typename T, bool VEC>
+struct PoolBN {
+  const float *mean, *invstd, *w, *b;  // fp32 [C]; w / b optional
+};
+
+template <typename T, bool VEC, bool BN>
 __global__ void __launch_bounds__(kPoolThreads)
     maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx,
-                  int N, int H, int W, int C, int OH, int OW, int k, int s, int p) {
+                  int N, int H, int W, int C, int OH, int OW, int k, int s, int p, PoolBN bn) {
   constexpr int V = VEC ? 8 : 1;
   const int CV = C / V;
   const int64_t total = (int64_t)N * OH * OW * CV;
@@ -38,6 +47,15 @@ __global__ void __launch_bounds__(kPoolThreads)
       best[i] = -INFINITY;
       arg[i] = 0;
     }
+    float sc[V], sh[V];
+    if constexpr (BN) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = cv * V + i;
+        sc[i] = bn.invstd[c] * (bn.w ? bn.w[c] : 1.f);
+        sh[i] = (bn.b ? bn.b[c] : 0.f) - bn.mean[c] * sc[i];
+      }
+    }
     const int h0 = oh * s - p, w0 = ow * s - p;
     for (int kh = 0; kh < k; ++kh) {
       const int h = h0 + kh;
@@ -49,6 +67,10 @@ __global__ void __launch_bounds__(kPoolThreads)
         float v[V];
         if constexpr (VEC) load8(src, v);
         else v[0] = to_f32(src[0]);
+        if constexpr (BN) {
+#pragma unroll
+          for (int i = 0; i < V; ++i) v[i] = to_f32(from_f32<T>(fmaxf(fmaf(v[i], sc[i], sh[i]), 0.f)));
+        }
         const int tap = kh * k + kw;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -148,21 +170,31 @@ int pool_grid(int64_t items) {
 }  // namespace
 
 void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, int H, int W, int C,
-                        int OH, int OW, int k, int s, int p, hipStream_t st) {
+                        int OH, int OW, int k, int s, int p, hipStream_t st, const float* mean,
+                        const float* invstd, const float* bw, const float* bb) {
   const bool vec = C % 8 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 &&
                    ((uintptr_t)idx % 8) == 0;
   const int64_t items = (int64_t)N * OH * OW * (vec ? C / 8 : C);
   if (items == 0) return;
+  const PoolBN bn{mean, invstd, bw, bb};
+  const bool with_bn = mean != nullptr;
   pool_dispatch(t, [&](auto t0) {
     using T = decltype(t0);
-    if (vec)
-      hipLaunchKernelGGL((maxpool_fwd_k<T, true>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
-                         st, static_cast<const T*>(x), static_cast<T*>(y), idx, N, H, W, C, OH,
-                         OW, k, s, p);
+    const dim3 g(pool_grid(items)), b(kPoolThreads);
+    const T* xp = static_cast<const T*>(x);
+    T* yp = static_cast<T*>(y);
+    if (vec && with_bn)
+      hipLaunchKernelGGL((maxpool_fwd_k<T, true, true>), g, b, 0, st, xp, yp, idx, N, H, W, C,
+                         OH, OW, k, s, p, bn);
+    else if (vec)
+      hipLaunchKernelGGL((maxpool_fwd_k<T, true, false>), g, b, 0, st, xp, yp, idx, N, H, W, C,
+                         OH, OW, k, s, p, bn);
+    else if (with_bn)
+      hipLaunchKernelGGL((maxpool_fwd_k<T, false, true>), g, b, 0, st, xp, yp, idx, N, H, W, C,
+                         OH, OW, k, s, p, bn);
     else
-      hipLaunchKernelGGL((maxpool_fwd_k<T, false>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
-                         st, static_cast<const T*>(x), static_cast<T*>(y), idx, N, H, W, C, OH,
-                         OW, k, s, p);
+      hipLaunchKernelGGL((maxpool_fwd_k<T, false, false>), g, b, 0, st, xp, yp, idx, N, H, W, C,
+                         OH, OW, k, s, p, bn);
   });
 }
 

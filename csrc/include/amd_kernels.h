@@ -212,8 +212,12 @@ void bn_backward_elemt(const void* dy, const void* x, DType tx, const float* mea
                        int64_t outer, int64_t C, int64_t inner, int channel_last, hipStream_t st);
 
 // ---- NHWC max pooling (pool.hip) -------------------------------------------
+// mean != nullptr: pool relu(x * invstd*w + (b - mean*invstd*w)) (BatchNorm + ReLU
+// applied on load; w / b optional, all fp32 [C])
 void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, int H, int W, int C,
-                        int OH, int OW, int k, int s, int p, hipStream_t st);
+                        int OH, int OW, int k, int s, int p, hipStream_t st,
+                        const float* mean = nullptr, const float* invstd = nullptr,
+                        const float* bw = nullptr, const float* bb = nullptr);
 void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
                         int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 

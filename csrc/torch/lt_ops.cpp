@@ -209,6 +209,78 @@ std::vector<at::Tensor> dense_dgelu_bgrad_op(at::Tensor dy2, at::Tensor w2, at::
   return {dpre, db};
 }
 
+std::vector<at::Tensor> dense_wgrad_bgrad_op(at::Tensor dy2, at::Tensor x2,
+                                             at::ScalarType w_dtype, at::ScalarType bias_dtype) {
+  // dW[N, K] = dy2[M, N]^T x2[M, K] with db[N] = column sums of dy2 from the SAME
+  // GEMM (HIPBLASLT_EPILOGUE_BGRADB): the GEMM streams dy anyway, so the bias
+  // gradient costs no extra pass over it.  Column-major: dW'[K, N] = X'[K, M] op(DY')
+  // with DY' stored [N, M] and op = T; BGRADB reduces op(B) over the k (= M) axis.
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(dy2.is_cuda() && dy2.dim() == 2 && x2.dim() == 2 && dy2.size(0) == x2.size(0),
+              "dense_wgrad_bgrad: dy [M, N], x [M, K] on the GPU");
+  TORCH_CHECK(dy2.scalar_type() == x2.scalar_type(), "dense_wgrad_bgrad: dy / x dtype mismatch");
+  dy2 = dy2.contiguous();
+  x2 = x2.contiguous();
+  const int64_t M = dy2.size(0), N = dy2.size(1), K = x2.size(1);
+  const hipDataType dt = hip_type(dy2.scalar_type()), ot = hip_type(w_dtype);
+  at::Tensor dw = at::empty({N, K}, dy2.options().dtype(w_dtype));
+  at::Tensor db = at::empty({N}, dy2.options().dtype(bias_dtype));
+  Desc d;
+  LT_CHECK(hipblasLtMatmulDescCreate(&d.op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  const int32_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  const uint32_t epi = HIPBLASLT_EPILOGUE_BGRADB;
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
+  void* bp = db.data_ptr();
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp));
+  const int32_t bdt = hip_type(bias_dtype);
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bdt, sizeof(bdt));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&d.a, dt, K, M, K));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&d.b, dt, N, M, N));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&d.c, ot, K, N, K));
+  const AlgoKey key{(int)epi, M, N, K, (int)dt, (int)ot, 1, (int)bdt};
+  if (!run(d, key, x2.data_ptr(), dy2.data_ptr(), dw.data_ptr(), K, N, dt)) return {};
+  return {dw, db};
+}
+
+int64_t lt_probe_op(int64_t m, int64_t n, int64_t k, int64_t epilogue, int64_t ta, int64_t tb,
+                    at::ScalarType dtype, int64_t aux_type, int64_t bias_type) {
+  // diagnostics: how many algorithms the heuristic offers for an epilogue / layout
+  Desc d;
+  const hipDataType dt = hip_type(dtype);
+  LT_CHECK(hipblasLtMatmulDescCreate(&d.op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  const int32_t a = ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, b = tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_TRANSA, &a, sizeof(a));
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_TRANSB, &b, sizeof(b));
+  const uint32_t epi = (uint32_t)epilogue;
+  set_attr(d.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
+  if (bias_type >= 0) {
+    const int32_t bt = (int32_t)bias_type;
+    set_attr(d.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
+  if (aux_type >= 0) {
+    const int32_t at_ = (int32_t)aux_type;
+    set_attr(d.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at_, sizeof(at_));
+    const int64_t ld = m;
+    set_attr(d.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld));
+  }
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&d.a, dt, ta ? k : m, ta ? m : k, ta ? k : m));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&d.b, dt, tb ? n : k, tb ? k : n, tb ? n : k));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&d.c, dt, m, n, m));
+  hipblasLtMatmulPreference_t pref;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  uint64_t ws = kWorkspace;
+  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
+                                                 &ws, sizeof(ws)));
+  hipblasLtMatmulHeuristicResult_t res[8];
+  int got = 0;
+  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(handle_for_device(), d.op, d.a, d.b, d.c,
+                                                       d.c, pref, 8, res, &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  return st == HIPBLAS_STATUS_SUCCESS ? got : -(int64_t)st;
+}
+
 void lt_algo_cache_clear() {
   AlgoCache& c = algo_cache();
   std::lock_guard<std::mutex> g(c.mu);

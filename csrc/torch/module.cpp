@@ -89,6 +89,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   dn.def("gelu_fwd_lt", &dense_gelu_fwd_op);
   dn.def("dgelu_bgrad_lt", &dense_dgelu_bgrad_op);
   dn.def("lt_cache_clear", &lt_algo_cache_clear);
+  dn.def("lt_probe", &lt_probe_op);
+  dn.def("wgrad_bgrad_lt", &dense_wgrad_bgrad_op);
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);
@@ -96,6 +98,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
   pool.def("max_bwd", &maxpool2d_nhwc_bwd_op);
+  pool.def("max_fwd_bn", &maxpool2d_nhwc_bn_fwd_op);
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
   conv.def("conv_fwd", &conv_nhwc_fwd_op, py::arg("x"), py::arg("w"), py::arg("stride") = 1);
   conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);
@@ -109,6 +112,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);
+  bn.def("train_stats", &bn_train_stats_op);
   bn.def("combine_stats", &bn_combine_stats_op);
   bn.def("apply", &bn_apply_op);
   bn.def("forward_local", &bn_forward_local_op, py::arg("x"), py::arg("weight"),

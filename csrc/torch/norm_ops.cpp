@@ -401,6 +401,34 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
   return {y, mean, invstd, at::Tensor()};
 }
 
+std::tuple<at::Tensor, at::Tensor> bn_train_stats_op(at::Tensor x, OptT running_mean,
+                                                      OptT running_var, OptT nbt, double eps,
+                                                      double momentum) {
+  // training statistics only (mean, invstd; running stats + num_batches_tracked
+  // updated in the finalize kernel) for consumers that apply the BatchNorm
+  // themselves (the ResNet stem's fused BN + ReLU + max-pool)
+  c10::NoGradGuard no_grad_;
+  const bool rs = has(running_mean) && has(running_var);
+  TORCH_CHECK(x.is_cuda() && (!rs || (running_mean->scalar_type() == at::kFloat &&
+                                      running_var->scalar_type() == at::kFloat &&
+                                      running_mean->is_contiguous() &&
+                                      running_var->is_contiguous())) &&
+                  (!has(nbt) || nbt->scalar_type() == at::kLong),
+              "bn.train_stats: GPU tensor, fp32 contiguous running stats, int64 counter");
+  BNView v = bn_view(x);
+  x = conform(x, v);
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({v.C}, fopt), invstd = at::empty({v.C}, fopt);
+  at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
+  bn_local_train_stats(x.data_ptr(), dtype_of(x), v.outer, v.C, v.inner, v.cl,
+                       mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                       rs ? running_mean->data_ptr<float>() : nullptr,
+                       rs ? running_var->data_ptr<float>() : nullptr,
+                       has(nbt) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr,
+                       (float)eps, (float)momentum, ws.data_ptr<float>(), cur_stream());
+  return {mean, invstd};
+}
+
 static std::tuple<at::Tensor, at::Tensor> bn_apply_impl(at::Tensor x, at::Tensor mean,
                                                         at::Tensor invstd, OptT weight, OptT bias,
                                                         OptT z, bool relu, bool want_mask) {

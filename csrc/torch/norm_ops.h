@@ -50,6 +50,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
     double eps, double momentum, OptT z, bool relu, bool want_mask);
 at::Tensor bn_apply_op(at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
                        OptT z, bool relu);
+// (mean, invstd) of a training batch; running stats / counter updated on the device
+std::tuple<at::Tensor, at::Tensor> bn_train_stats_op(at::Tensor x, OptT running_mean,
+                                                      OptT running_var, OptT nbt, double eps,
+                                                      double momentum);
 std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mean,
                                                     at::Tensor invstd, OptT weight, OptT bias,
                                                     OptT z, bool relu);

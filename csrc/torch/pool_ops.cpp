@@ -11,7 +11,24 @@ int64_t out_size(int64_t in, int64_t k, int64_t s, int64_t p) { return (in + 2 *
 
 std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_fwd_op(at::Tensor x, int64_t k, int64_t s,
                                                          int64_t p) {
+  return maxpool2d_nhwc_bn_fwd_op(x, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, k, s,
+                                  p);
+}
+
+std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_bn_fwd_op(
+    at::Tensor x, c10::optional<at::Tensor> mean, c10::optional<at::Tensor> invstd,
+    c10::optional<at::Tensor> w, c10::optional<at::Tensor> b, int64_t k, int64_t s, int64_t p) {
   c10::NoGradGuard no_grad_;
+  auto f32 = [&](const c10::optional<at::Tensor>& t) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->is_cuda() &&
+                    t->numel() == x.size(1),
+                "maxpool BN operands: contiguous fp32 [C] GPU tensors");
+    return t->data_ptr<float>();
+  };
+  const float* mp = f32(mean);
+  const float* ip = f32(invstd);
+  TORCH_CHECK((mp == nullptr) == (ip == nullptr), "maxpool BN: mean and invstd go together");
   TORCH_CHECK(x.is_cuda() && x.dim() == 4, "maxpool2d_nhwc: 4-D GPU tensor expected");
   TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && p <= k / 2, "unsupported pool geometry");
   x = x.contiguous(at::MemoryFormat::ChannelsLast);
@@ -23,7 +40,7 @@ std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_fwd_op(at::Tensor x, int64_t k
   at::Tensor idx = at::empty({N, C, OH, OW}, opt.dtype(at::kByte));
   maxpool2d_nhwc_fwd(x.data_ptr(), dtype_of(x), y.data_ptr(), idx.data_ptr<uint8_t>(), (int)N,
                      (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p,
-                     cur_stream());
+                     cur_stream(), mp, ip, f32(w), f32(b));
   return {y, idx};
 }
 

@@ -1,5 +1,6 @@
 #pragma once
 #include <ATen/ATen.h>
+#include <c10/util/Optional.h>
 
 #include <tuple>
 
@@ -8,6 +9,10 @@ namespace amd {
 // NHWC (channels_last) max pooling: forward returns (y, tap index per element).
 std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_fwd_op(at::Tensor x, int64_t k, int64_t s,
                                                          int64_t p);
+// the same with a BatchNorm affine + ReLU applied to x on load (ResNet stem)
+std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_bn_fwd_op(
+    at::Tensor x, c10::optional<at::Tensor> mean, c10::optional<at::Tensor> invstd,
+    c10::optional<at::Tensor> w, c10::optional<at::Tensor> b, int64_t k, int64_t s, int64_t p);
 at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W, int64_t k,
                                  int64_t s, int64_t p);
 

@@ -165,3 +165,43 @@ def test_channels_last_tensors_accepted():
     noop = torch.zeros(1, dtype=torch.int32)
     amp_C.multi_tensor_scale(65536, noop, [[a], [b]], 3.0)
     torch.testing.assert_close(b, a * 3)
+
+
+def test_legacy_lamb_stages_match_formula_and_honour_noop():
+    """amp_C.multi_tensor_lamb_stage{1,2}_cuda (legacy two-stage LAMB API): values
+    vs the textbook formula, and a set noop flag leaves every tensor untouched."""
+    import torch
+
+    from apex_example_amd import amp_C
+
+    torch.manual_seed(0)
+    shapes = [(7,), (3, 5)]
+    g = [torch.randn(s) for s in shapes]
+    p = [torch.randn(s) for s in shapes]
+    m = [torch.randn(s) * 0.1 for s in shapes]
+    v = [torch.rand(s) * 0.1 for s in shapes]
+    u = [torch.zeros(s) for s in shapes]
+    decay = [0.01, 0.0]
+    b1, b2, eps, step, gn, mx, lr = 0.9, 0.999, 1e-6, 3, 4.0, 1.0, 0.1
+    ref_m = [mi * b1 + (gi / 4.0) * (1 - b1) for gi, mi in zip(g, m)]
+    ref_v = [vi * b2 + (gi / 4.0) ** 2 * (1 - b2) for gi, vi in zip(g, v)]
+    ref_u = [(rm / (1 - b1 ** step)) / ((rv / (1 - b2 ** step)).sqrt() + eps) + d * pi
+             for rm, rv, d, pi in zip(ref_m, ref_v, decay, p)]
+    noop = torch.zeros(1, dtype=torch.int32)
+    # noop set: nothing changes
+    before = [t.clone() for t in m + v + u + p]
+    amp_C.multi_tensor_lamb_stage1_cuda(0, noop + 1, [g, p, m, v, u], decay, step, b1, b2, eps,
+                                        gn, mx)
+    pn = [pi.norm() for pi in p]
+    amp_C.multi_tensor_lamb_stage2_cuda(0, noop + 1, [p, u], pn, [torch.ones(())] * 2, lr, 0.01)
+    for a, b in zip(before, m + v + u + p):
+        assert torch.equal(a, b)
+    amp_C.multi_tensor_lamb_stage1_cuda(0, noop, [g, p, m, v, u], decay, step, b1, b2, eps,
+                                        torch.tensor([gn]), mx)
+    for a, b in zip(m + v + u, ref_m + ref_v + ref_u):
+        torch.testing.assert_close(a, b)
+    un = [ui.norm() for ui in u]
+    p0 = [pi.clone() for pi in p]
+    amp_C.multi_tensor_lamb_stage2_cuda(0, noop, [p, u], pn, un, lr, 0.01)
+    for a, b, ui, pni, uni in zip(p, p0, u, pn, un):
+        torch.testing.assert_close(a, b - lr * (pni / uni) * ui)
