@@ -72,9 +72,12 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
 
 
 def bn_relu_maxpool_fusable(x, bn, pool):
-    """True when ``pool(relu(bn(x)))`` can run as BNReLUMaxPoolFunction."""
+    """True when ``pool(relu(bn(x)))`` can run as BNReLUMaxPoolFunction: a LOCAL
+    BatchNorm2dReLU only (a SyncBatchNorm needs the cross-rank statistics)."""
+    from .batch_norm import BatchNorm2dReLU
+
     k, s, p = pool.kernel_size, pool.stride, pool.padding
-    return (_FUSE_STEM and bn.training and bn.track_running_stats and bn.momentum is not None
+    return (_FUSE_STEM and type(bn) is BatchNorm2dReLU and bn.fuse_relu and bn.training and bn.track_running_stats and bn.momentum is not None
             and x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
             and x.size(1) % 8 == 0 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and bn.weight is not None and bn.weight.dtype == torch.float32

@@ -112,7 +112,52 @@ __global__ void __launch_bounds__(256)
   if (sl == 0 && c < N) out[c] = from_f32<TO>((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]));
 }
 
+__device__ __forceinline__ float gelu_f(float x, bool tanh_approx) {
+  if (tanh_approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+
+// h = gelu(pre): a streaming pass with 4 independent 16-byte loads in flight per
+// lane (the FFN forward's [tokens x 4h] activation; ATen's GELU ran it at ~4.3 TB/s)
+template <typename T>
+__global__ void __launch_bounds__(256)
+    gelu_fwd_k(const T* __restrict__ x, T* __restrict__ y, int64_t n8, bool tanh_approx) {
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride * U) {
+    float v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u * stride < n8) load8(x + (i + u * stride) * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i + u * stride >= n8) continue;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[u][k] = gelu_f(v[u][k], tanh_approx);
+      store8(y + (i + u * stride) * 8, v[u]);
+    }
+  }
+}
+
 }  // namespace
+
+void gelu_fwd(const void* x, void* y, DType t, int64_t n, bool tanh_approx, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return;
+  int64_t blocks = (n8 + 256 * 4 - 1) / (256 * 4);
+  if (blocks > 8192) blocks = 8192;
+  auto go = [&](auto t0) {
+    using T = decltype(t0);
+    hipLaunchKernelGGL((gelu_fwd_k<T>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       static_cast<const T*>(x), static_cast<T*>(y), n8, tanh_approx);
+  };
+  if (t == DType::BF16) go(bf16_t{});
+  else if (t == DType::F16) go(half_t{});
+  else go(float{});
+}
 
 int colsum_splits(int64_t M, int N) {
   const int cb = (N + kCsCols - 1) / kCsCols;

@@ -264,6 +264,8 @@ void stem_wgrad(const void* xp, const void* dy, float* part, int S, int N, int H
 // g = dh * relu'(y) / dh * sigmoid'(y) from the saved output y (passed as `pre`) is
 // computed in the same pass and written to out_dpre.  part: S * N floats.
 int colsum_splits(int64_t M, int N);
+// y = gelu(x) (erf or tanh), n % 8 == 0, 16-byte aligned
+void gelu_fwd(const void* x, void* y, DType t, int64_t n, bool tanh_approx, hipStream_t st);
 void colsum(const void* x, const void* pre, void* out_dpre, DType t, int64_t M, int N,
             int act_mode, float* part, int S, void* bias_grad, DType tb, hipStream_t st);
 

@@ -65,6 +65,16 @@ std::tuple<at::Tensor, at::Tensor> gelu_bwd_bias_grad_op(at::Tensor dh, at::Tens
   return {dpre, out};
 }
 
+at::Tensor gelu_fwd_op(at::Tensor x, bool tanh_approx) {
+  c10::NoGradGuard no_grad_;
+  x = x.contiguous();
+  if (!colsum_ok(x) || x.numel() % 8 != 0)
+    return at::gelu(x, tanh_approx ? "tanh" : "none");
+  at::Tensor y = at::empty_like(x);
+  gelu_fwd(x.data_ptr(), y.data_ptr(), dtype_of(x), x.numel(), tanh_approx, cur_stream());
+  return y;
+}
+
 std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tensor y, int64_t act,
                                                         at::ScalarType out_dtype) {
   c10::NoGradGuard no_grad_;

@@ -12,6 +12,8 @@ at::Tensor bias_grad_op(at::Tensor g, at::ScalarType out_dtype);
 std::tuple<at::Tensor, at::Tensor> gelu_bwd_bias_grad_op(at::Tensor dh, at::Tensor pre,
                                                          bool tanh_approx,
                                                          at::ScalarType out_dtype);
+// h = gelu(pre) (erf, or tanh when tanh_approx) on the streaming kernel
+at::Tensor gelu_fwd_op(at::Tensor x, bool tanh_approx);
 // (dpre = dh * act'(y), sum over rows of dpre) from the layer OUTPUT y;
 // act: 1 = ReLU (y > 0), 2 = sigmoid (y (1 - y))  [apex.mlp backward]
 std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tensor y, int64_t act,

@@ -86,6 +86,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   dn.def("bias_grad", &bias_grad_op);
   dn.def("gelu_bwd_bias_grad", &gelu_bwd_bias_grad_op);
   dn.def("act_bwd_bias_grad", &act_bwd_bias_grad_op);
+  dn.def("gelu", &gelu_fwd_op);
   dn.def("gelu_fwd_lt", &dense_gelu_fwd_op);
   dn.def("dgelu_bgrad_lt", &dense_dgelu_bgrad_op);
   dn.def("lt_cache_clear", &lt_algo_cache_clear);

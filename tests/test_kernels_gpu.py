@@ -891,3 +891,21 @@ def test_bn_relu_maxpool_fused_matches_unfused(dt):
     torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(bn_a.weight.grad, bn_b.weight.grad, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(bn_a.bias.grad, bn_b.bias.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("tanh", [False, True])
+def test_dense_gelu_kernel(dt, tanh):
+    """dense.gelu (streaming GELU of the FFN forward) vs F.gelu in fp32, rounded once."""
+    from apex_example_amd import _native
+
+    torch.manual_seed(0)
+    x = (torch.randn(1037, 4096, device=DEV) * 3).to(dt)
+    y = _native.require().dense.gelu(x, tanh)
+    ref = F.gelu(x.float(), approximate="tanh" if tanh else "none")
+    tol = 1e-6 if dt == torch.float32 else (4e-3 if dt == torch.float16 else 8e-3)
+    _assert_max_scaled(y.float(), ref, tol)
+    # odd sizes take the ATen fallback
+    z = torch.randn(5, 7, device=DEV).to(dt)
+    torch.testing.assert_close(_native.require().dense.gelu(z, tanh),
+                               F.gelu(z, approximate="tanh" if tanh else "none"))

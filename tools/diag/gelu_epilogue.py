@@ -29,3 +29,10 @@ got = torch._addmm_activation(b, x, w.t(), use_gelu=True).float()
 print("epilogue vs tanh-gelu max err %.3e (max |ref| %.2f)" % ((got - ref).abs().max(), ref.abs().max()))
 ref2 = F.gelu(torch.addmm(b, x, w.t()).float())
 print("epilogue vs erf-gelu max err %.3e" % (got - ref2).abs().max())
+from apex_example_amd import _native  # noqa: E402
+
+pre = torch.addmm(b, x, w.t())
+print("ATen gelu(erf)         %.1f us" % t(lambda: F.gelu(pre)))
+print("dense.gelu(erf)        %.1f us" % t(lambda: _native.require().dense.gelu(pre, False)))
+print("ATen gelu(tanh)        %.1f us" % t(lambda: F.gelu(pre, approximate="tanh")))
+print("dense.gelu(tanh)       %.1f us" % t(lambda: _native.require().dense.gelu(pre, True)))
