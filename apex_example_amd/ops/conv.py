@@ -49,6 +49,44 @@ def wgrad_1x1(dy_rows, x_rows, out_dtype):
     return part.sum(0).to(out_dtype)
 
 
+# Stride-1 1x1 convs on the own MFMA implicit-GEMM kernel (conv_tap_k, kFwd1) where
+# it measured faster than hipBLASLt (tools/microbench.py conv1x1-own,
+# profiles/microbench_conv1x1_own.txt; bit-identical results): the channel-
+# reducing ResNet-50 shapes 256->64 @ 56x56 (97 vs 156 us) and 512->128 @ 28x28
+# (50 vs 61 us), and 512->2048 @ 7x7 (46 vs 53 us).  A data gradient is the same
+# 1x1 conv of dY with the transposed weight, so conv3's dgrads (256->64, 512->128)
+# take it too.  (cin, cout) -> minimum rows M = N*H*W; APEX_AMD_OWN1X1=0 disables.
+_OWN1X1 = {(256, 64): 200_000, (512, 128): 100_000, (512, 2048): 0}
+_USE_OWN1X1 = os.environ.get("APEX_AMD_OWN1X1", "1") == "1"
+
+
+def _own_1x1(x_rows_dtype, cin, cout, m):
+    lim = _OWN1X1.get((cin, cout))
+    return (_USE_OWN1X1 and lim is not None and m >= lim and m < (1 << 31)
+            and x_rows_dtype == torch.bfloat16 and _native.available())
+
+
+def _conv1x1_fwd(x, weight):
+    """y = conv1x1(x) for a channels-last bf16 x: own MFMA kernel or hipBLASLt GEMM."""
+    n, ci, h, w = x.shape
+    co = weight.shape[0]
+    if _own_1x1(x.dtype, ci, co, n * h * w) and weight.dtype == torch.bfloat16:
+        return _native.require().conv.conv_fwd(x, weight, 1)
+    y2 = torch.mm(_as_rows(x), weight.reshape(co, ci).t())
+    return y2.view(n, h, w, co).permute(0, 3, 1, 2)
+
+
+def _conv1x1_dgrad(dy, weight, xshape):
+    """dX = dY @ W (a 1x1 conv of dY with W^T)."""
+    n, ci, h, w = xshape
+    co = weight.shape[0]
+    if _own_1x1(dy.dtype, co, ci, n * h * w) and weight.dtype == torch.bfloat16:
+        wt = weight.reshape(co, ci).t().contiguous().view(ci, co, 1, 1)
+        return _native.require().conv.conv_fwd(dy, wt, 1)
+    dx2 = torch.mm(_as_rows(dy), weight.reshape(co, ci))
+    return dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
+
+
 def _as_rows(t):
     n, c, h, w = t.shape
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
@@ -57,23 +95,16 @@ def _as_rows(t):
 class Conv1x1GemmFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
-        n, ci, h, w = x.shape
-        co = weight.shape[0]
-        w2 = weight.reshape(co, ci)
-        y2 = torch.mm(_as_rows(x), w2.t())
         ctx.save_for_backward(x, weight)
-        return y2.view(n, h, w, co).permute(0, 3, 1, 2)
+        return _conv1x1_fwd(x, weight)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        n, ci, h, w = x.shape
-        co = weight.shape[0]
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx2 = torch.mm(_as_rows(dy), weight.reshape(co, ci))
-            dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
+            dx = _conv1x1_dgrad(dy, weight, x.shape)
         if ctx.needs_input_grad[1]:
             dw = wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype).view(weight.shape)
         return dx, dw
@@ -89,11 +120,8 @@ class Conv1x1SkipFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight):
-        n, ci, h, w = x.shape
-        co = weight.shape[0]
-        y2 = torch.mm(_as_rows(x), weight.reshape(co, ci).t())
         ctx.save_for_backward(x, weight)
-        return y2.view(n, h, w, co).permute(0, 3, 1, 2), x.view_as(x)
+        return _conv1x1_fwd(x, weight), x.view_as(x)
 
     @staticmethod
     def backward(ctx, dy, dskip):

@@ -16,6 +16,9 @@
 // backward passes then read the mask instead of re-reading z to recompute the
 // ReLU condition: two full reads of the residual tensor per layer become two
 // reads of 1/16 of it, and z need not be kept alive for backward.
+#include <cstdio>
+#include <cstdlib>
+
 #include "bn_common.h"
 
 namespace amd {
@@ -42,6 +45,25 @@ BNTuning& bn_tuning() {
   static BNTuning t;
   return t;
 }
+
+namespace {
+// rows in flight per lane of the read-only reductions; APEX_AMD_BN_U="stats,reduce"
+// (A/B switch for tools/microbench.py bn-u, read per launch)
+struct BNUnroll {
+  int stats = 4, reduce = 2;
+};
+BNUnroll bn_unroll() {
+  BNUnroll u;
+  if (const char* e = std::getenv("APEX_AMD_BN_U")) {
+    int a = 0, b = 0;
+    if (std::sscanf(e, "%d,%d", &a, &b) == 2) {
+      u.stats = a;
+      u.reduce = b;
+    }
+  }
+  return u;
+}
+}  // namespace
 
 namespace {
 
@@ -116,12 +138,11 @@ __device__ __forceinline__ void block_slab_write(float (&s1)[W], float (&s2)[W],
 }
 
 // ---------------------------------------------------------------- statistics
-template <typename T, bool VEC>
+template <typename T, bool VEC, int U>
 __global__ void __launch_bounds__(kBNThreads)
     stats_k(const T* __restrict__ x, int64_t M, int C, int ctile, int rows_iter,
             float* __restrict__ slab) {
   constexpr int W = VEC ? 8 : 1;
-  constexpr int U = 4;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
   const bool active = ri < rows_iter && c0 < C;
@@ -204,14 +225,13 @@ __global__ void __launch_bounds__(kBNThreads)
 }
 
 // ---------------------------------------------------------------- backward reduce
-template <typename T, typename TW, bool VEC>
+template <typename T, typename TW, bool VEC, int U>
 __global__ void __launch_bounds__(kBNThreads)
     reduce_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
              const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
              const T* __restrict__ z, const uint8_t* __restrict__ rmask, int relu, int64_t M,
              int C, int ctile, int rows_iter, float* __restrict__ slab) {
   constexpr int W = VEC ? 8 : 1;
-  constexpr int U = 2;
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
@@ -368,8 +388,13 @@ void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut&
     using T = decltype(t0);
     const T* xp = static_cast<const T*>(x);
     vec_dispatch(vec, [&](auto V) {
-      hipLaunchKernelGGL((stats_k<T, decltype(V)::value>), dim3(splits, g.cblocks),
-                         dim3(kBNThreads), 0, st, xp, M, (int)C, g.ctile, g.rows_iter, ws);
+      constexpr bool VV = decltype(V)::value;
+      if (bn_unroll().stats == 8)
+        hipLaunchKernelGGL((stats_k<T, VV, 8>), dim3(splits, g.cblocks), dim3(kBNThreads), 0, st,
+                           xp, M, (int)C, g.ctile, g.rows_iter, ws);
+      else
+        hipLaunchKernelGGL((stats_k<T, VV, 4>), dim3(splits, g.cblocks), dim3(kBNThreads), 0, st,
+                           xp, M, (int)C, g.ctile, g.rows_iter, ws);
     });
     launch_stats_finalize<T>(xp, ws, splits, C, M, (int64_t)1, out, st);
   });
@@ -408,11 +433,16 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
       using T = decltype(t0);
       using TW = decltype(w0);
       vec_dispatch(vec, [&](auto V) {
-        hipLaunchKernelGGL((reduce_k<T, TW, decltype(V)::value>), dim3(splits, g.cblocks),
-                           dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
-                           static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
-                           static_cast<const TW*>(b), static_cast<const T*>(z), rmask, relu, M,
-                           (int)C, g.ctile, g.rows_iter, ws);
+        constexpr bool VV = decltype(V)::value;
+        auto go = [&](auto u) {
+          hipLaunchKernelGGL((reduce_k<T, TW, VV, decltype(u)::value>), dim3(splits, g.cblocks),
+                             dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
+                             static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
+                             static_cast<const TW*>(b), static_cast<const T*>(z), rmask, relu, M,
+                             (int)C, g.ctile, g.rows_iter, ws);
+        };
+        if (bn_unroll().reduce == 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 2>{});
       });
       launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
                          static_cast<TW*>(gb), st, sum_scale);

@@ -909,3 +909,33 @@ def test_dense_gelu_kernel(dt, tanh):
     z = torch.randn(5, 7, device=DEV).to(dt)
     torch.testing.assert_close(_native.require().dense.gelu(z, tanh),
                                F.gelu(z, approximate="tanh" if tanh else "none"))
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 64, 30), (2, 512, 128, 28), (3, 512, 2048, 7)])
+def test_conv1x1_own_kernel_matches_gemm(shape, monkeypatch):
+    """Stride-1 1x1 conv on the own MFMA kernel (the measured-faster ResNet shapes,
+    forward and data gradient) vs the hipBLASLt GEMM path: bit-identical outputs
+    (both accumulate in fp32 and round once) and matching gradients."""
+    from apex_example_amd.ops import conv as convmod
+
+    n, ci, co, hw = shape
+    monkeypatch.setitem(convmod._OWN1X1, (ci, co), 0)
+    monkeypatch.setitem(convmod._OWN1X1, (co, ci), 0)
+    torch.manual_seed(0)
+    m = convmod.Conv2d1x1(ci, co).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(n, ci, hw, hw, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    dy = torch.randn(n, co, hw, hw, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    outs = []
+    for own in (True, False):
+        monkeypatch.setattr(convmod, "_USE_OWN1X1", own)
+        xa = x.clone().requires_grad_(True)
+        m.weight.grad = None
+        y = m(xa)
+        y.backward(dy)
+        outs.append((y.detach(), xa.grad, m.weight.grad.clone()))
+    assert outs[0][0].is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=0, atol=0)

@@ -93,6 +93,40 @@ R50_BN = {(256, 64, 112, 112): 1, (256, 64, 56, 56): 6, (256, 256, 56, 56): 4,
           (256, 512, 14, 14): 1, (256, 512, 7, 7): 5, (256, 2048, 7, 7): 4}
 
 
+def bench_bn_u(args):
+    """A/B of the rows-in-flight unroll of the read-only BN reductions (stats_k,
+    reduce_k) via APEX_AMD_BN_U: per-shape us and the ResNet-50-weighted total."""
+    import os
+
+    from apex_example_amd import _native
+
+    C_ = _native.require().bn
+    dev = "cuda"
+    variants = ["4,2", "8,2", "4,4", "8,4"]
+    tot = {v: [0.0, 0.0] for v in variants}
+    print("| shape | count | " + " | ".join("stats/reduce U=%s" % v for v in variants) + " |")
+    print("|---|---|" + "---|" * len(variants))
+    for (n, c, h, w), cnt in R50_BN.items():
+        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy, z = torch.randn_like(x), torch.randn_like(x)
+        wt, bs = torch.ones(c, device=dev), torch.zeros(c, device=dev)
+        mean, var = C_.local_stats(x)
+        invstd = (var + 1e-5).rsqrt()
+        row = []
+        for v in variants:
+            os.environ["APEX_AMD_BN_U"] = v
+            ts = timeit(lambda: C_.local_stats(x))
+            tr = timeit(lambda: C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True))
+            tot[v][0] += cnt * ts
+            tot[v][1] += cnt * tr
+            row.append("%.0f / %.0f" % (ts, tr))
+        print("| %s | %d | %s |" % ((n, c, h, w), cnt, " | ".join(row)), flush=True)
+    os.environ.pop("APEX_AMD_BN_U", None)
+    print("| R50-weighted total us | | " + " | ".join(
+        "%.0f / %.0f" % tuple(tot[v]) for v in variants) + " |")
+
+
 def bench_bn_tune(args):
     """Sweep the NHWC BN grid-sizing knobs; report the ResNet-50-weighted total
     (forward stats+finalize+apply, backward reduce+finalize+elementwise) per config."""
@@ -202,6 +236,62 @@ def bench_conv1x1(args):
 
         print("| %d,%d,%d,%d | %.1f | %s | %s | %s | %s | %s | %s |" % (
             n, ci, co, hw, gf, tf(t_cf), tf(t_gf), tf(t_cd), tf(t_gd), tf(t_cw), tf(t_gw)))
+
+
+def bench_conv1x1_own(args):
+    """Stride-1 1x1 conv forward: hipBLASLt GEMM (torch.mm on the NHWC rows) vs the
+    own MFMA implicit-GEMM kernel (conv_tap_k kFwd1), with bandwidth - the base a
+    fused BN prologue / statistics epilogue would be built on."""
+    from apex_example_amd import _native
+
+    cv = _native.require().conv
+    dev = "cuda"
+    shapes = [(256, 64, 256, 56), (256, 256, 64, 56), (256, 128, 512, 28), (256, 512, 128, 28),
+              (256, 256, 1024, 14), (256, 1024, 256, 14), (256, 512, 2048, 7),
+              (256, 2048, 512, 7)]
+    print("| N,Cin,Cout,HW | MB moved | hipBLASLt | own MFMA | max abs diff |")
+    print("|---|---|---|---|---|")
+    for (n, ci, co, hw) in shapes:
+        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = (torch.randn(co, ci, 1, 1, device=dev) * 0.05).to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        M = n * hw * hw
+        x2 = x.permute(0, 2, 3, 1).reshape(M, ci)
+        w2 = w.reshape(co, ci)
+        mb = (M * ci + M * co) * 2 / 1e6
+        t_g = timeit(lambda: torch.mm(x2, w2.t()))
+        t_o = timeit(lambda: cv.conv_fwd(x, w, 1))
+        y_g = torch.mm(x2, w2.t())
+        y_o = cv.conv_fwd(x, w, 1).permute(0, 2, 3, 1).reshape(M, co)
+        d = float((y_g.float() - y_o.float()).abs().max())
+
+        def bw(t):
+            return "%.0f us (%.2f TB/s)" % (t, mb / 1e6 / (t * 1e-6))
+
+        print("| %d,%d,%d,%d | %.0f | %s | %s | %.3g |" % (n, ci, co, hw, mb, bw(t_g), bw(t_o), d),
+              flush=True)
+    # weight gradient dW = dY^T X: split-K hipBLASLt (ops/conv.py wgrad_1x1) vs the
+    # own per-tap MFMA wgrad kernel with one tap
+    from apex_example_amd.ops.conv import wgrad_1x1
+
+    print("\n| N,Cin,Cout,HW | split-K hipBLASLt wgrad | own MFMA wgrad | rel diff |")
+    print("|---|---|---|---|")
+    for (n, ci, co, hw) in shapes:
+        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy = torch.randn(n, co, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        M = n * hw * hw
+        x2 = x.permute(0, 2, 3, 1).reshape(M, ci)
+        dy2 = dy.permute(0, 2, 3, 1).reshape(M, co)
+        t_g = timeit(lambda: wgrad_1x1(dy2, x2, torch.bfloat16))
+        t_o = timeit(lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0, 1, 1))
+        a = wgrad_1x1(dy2, x2, torch.float32)
+        b = cv.conv_wgrad(dy, x, torch.float32, 0, 1, 1).reshape(co, ci)
+        rd = float((a - b).abs().max() / a.abs().max())
+        print("| %d,%d,%d,%d | %.0f us | %.0f us | %.2g |" % (n, ci, co, hw, t_g, t_o, rd),
+              flush=True)
 
 
 def bench_wgrad(args):
@@ -494,12 +584,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-tune", "bn-u", "conv1x1", "conv1x1-own", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "optim": bench_optim,
+    {"bn": bench_bn, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
