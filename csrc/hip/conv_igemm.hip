@@ -21,6 +21,9 @@
 // writes lane-linearly), so the 16 rows a ds_read_b128 lane group touches land
 // in distinct bank slots.  Workgroups are remapped so consecutive M tiles
 // (which share input rows through the 3x3 halo) run on one XCD's L2.
+#include <cstdlib>
+#include <cstring>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -97,16 +100,16 @@ struct ConvGeom {
   int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
 };
 
-template <int MODE, int BN, int WM, int WN, int NB>
-__global__ void __launch_bounds__(kCT, 2)
+template <int MODE, int BM, int BN, int WM, int WN, int NB>
+__global__ void __launch_bounds__(kCT, BM == 256 ? 1 : 2)
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g) {
   static_assert(WM * WN == 4, "4 waves");
-  constexpr int TM = kBM / WM, TN = BN / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = kBM * kRowBytes, B_BYTES = BN * kRowBytes;
+  constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
   constexpr int BUF = A_BYTES + B_BYTES;
-  constexpr int AI = kBM / 32;      // A wave-instructions (8 rows each) per wave per tile
+  constexpr int AI = BM / 32;      // A wave-instructions (8 rows each) per wave per tile
   constexpr int BI = BN / 32;       // B wave-instructions per wave per tile
   constexpr int G = AI + BI;        // glds per wave per tile (vmcnt units)
   __shared__ __attribute__((aligned(1024))) unsigned char lds[NB * BUF];
@@ -114,7 +117,7 @@ __global__ void __launch_bounds__(kCT, 2)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int mt = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = mt * kBM, n0 = blockIdx.y * BN;
+  const int m0 = mt * BM, n0 = blockIdx.y * BN;
   const int z = blockIdx.z;
   const int ntaps = conv_ntaps<MODE>(z);
   const int KC = g.KC, M = g.M, GHW = g.GH * g.GW;
@@ -130,7 +133,7 @@ __global__ void __launch_bounds__(kCT, 2)
   unsigned amask[AI];
 #pragma unroll
   for (int q = 0; q < AI; ++q) {
-    const int row = wid * (kBM / 4) + q * 8 + lrow;
+    const int row = wid * (BM / 4) + q * 8 + lrow;
     const int ch = pchunk ^ ((row >> 1) & 7);
     const int m = m0 + row;
     const int mm = m < M ? m : 0;
@@ -172,7 +175,7 @@ __global__ void __launch_bounds__(kCT, 2)
     _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                        \
       const bool ok = (amask[q] >> tap_) & 1u;                                              \
       glds16(ok ? (const void*)(abase[q] + aoff_) : (const void*)g_zero16,                  \
-             A_ + (wid * (kBM / 4) + q * 8) * kRowBytes);                                   \
+             A_ + (wid * (BM / 4) + q * 8) * kRowBytes);                                   \
     }                                                                                       \
     _Pragma("unroll") for (int q = 0; q < BI; ++q)                                          \
       glds16(bbase[q] + boff_, B_ + (wid * (BN / 4) + q * 8) * kRowBytes);                  \
@@ -239,7 +242,7 @@ __global__ void __launch_bounds__(kCT, 2)
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-byte chunks per output row
   constexpr bool dense = MODE == kFwd3 || MODE == kFwd1;
-  for (int c = tid; c < kBM * CPR; c += kCT) {
+  for (int c = tid; c < BM * CPR; c += kCT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
     if (m >= M) continue;
@@ -255,18 +258,35 @@ __global__ void __launch_bounds__(kCT, 2)
   }
 }
 
+// M-tile choice: 128 (2 workgroups / CU, 64x64 per wave) or 256 (1 workgroup / CU,
+// 128x64 per wave: 1/3 less LDS read traffic per MFMA; 2- or 3-deep DMA ring).
+// APEX_AMD_CONV_BM = 128 | 256 | 256x3 for A/B runs (tools/microbench.py conv3x3).
+static int conv_bm_choice() {
+  const char* e = std::getenv("APEX_AMD_CONV_BM");
+  if (!e) return 0;
+  if (std::strcmp(e, "256") == 0) return 1;
+  if (std::strcmp(e, "256x3") == 0) return 2;
+  return 0;
+}
+
 template <int MODE>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st) {
   if (g.M == 0) return;
-  const int mtiles = (g.M + kBM - 1) / kBM;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
-  if (g.NC % 128 == 0) {
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 2, 2, 2>), dim3(mtiles, g.NC / 128, nclasses),
-                       dim3(kCT), 0, st, a, w, y, g);
+  const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
+  if (big) {
+    const dim3 grid((g.M + 255) / 256, g.NC / 128, nclasses);
+    if (big == 2)
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
+    else
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g);
+  } else if (g.NC % 128 == 0) {
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g);
   } else {
-    hipLaunchKernelGGL((conv_tap_k<MODE, 64, 4, 1, 3>), dim3(mtiles, g.NC / 64, nclasses),
-                       dim3(kCT), 0, st, a, w, y, g);
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
   }
 }
 

@@ -149,7 +149,10 @@ def test_two_ranks_match_concatenated_batch(tmp_path, opt_level):
     """With SyncBN the two ranks compute exactly the math of ONE process on the
     concatenated batch (global BN statistics, averaged gradients).  In fp32 (O0)
     the loss curve and the parameter updates must agree to rounding-order noise
-    (measured: identical to 4 decimals over 6 steps, tools/diag/ddp_parity.py).
+    (measured: identical to 4 decimals over 6 steps on one box, tools/diag/ddp_parity.py;
+    on another the 4th loss, 0.099, differed by 9e-4 - the fp32 convolutions are
+    MIOpen's, whose algorithm choice varies by box - hence 2e-3 relative + 1e-3
+    absolute).
     In bf16 (O2) the two runs round differently and this tiny memorisation task
     amplifies that (measured 0.2 % at step 1, 2.6 % at step 2, tens of % by step
     4), so only the first two losses are pinned."""
@@ -159,9 +162,9 @@ def test_two_ranks_match_concatenated_batch(tmp_path, opt_level):
     ref = W.gpu_resnet_reference(world=2, lr=0.01, opt_level=opt_level, steps=steps)
     # the rank losses are per-half means; the global loss is their average
     ddp_loss = [(a + b) / 2 for a, b in zip(res[0]["losses"], res[1]["losses"])]
-    tol = 2e-3 if opt_level == "O0" else 5e-2
+    tol, atol = (2e-3, 1e-3) if opt_level == "O0" else (5e-2, 0.0)
     for a, b in zip(ddp_loss, ref["losses"]):
-        assert abs(a - b) <= tol * abs(b), (ddp_loss, ref["losses"])
+        assert abs(a - b) <= tol * abs(b) + atol, (ddp_loss, ref["losses"])
     if opt_level != "O0":
         return
     worst = 0.0

@@ -342,6 +342,54 @@ def bench_wgrad(args):
             n, ci, co, hw, gf, t_cw, gf / (t_cw * 1e-6) / 1e3, " | ".join(cells)), flush=True)
 
 
+def bench_conv_bm(args):
+    """M-tile A/B of the MFMA implicit-GEMM conv (APEX_AMD_CONV_BM = 128 | 256 | 256x3):
+    3x3 forward and stride-1 data gradient at ResNet-50's 128+ channel shapes, plus
+    the 1x1 forward shapes that run on the own kernel."""
+    import os
+
+    from apex_example_amd import _native
+    from apex_example_amd.ops.conv import _rot_weight
+
+    cv = _native.require().conv
+    dev = "cuda"
+    variants = ["128", "256", "256x3"]
+    print("| conv | GFLOP | " + " | ".join("BM=%s" % v for v in variants) + " | max diff |")
+    print("|---|---|" + "---|" * len(variants) + "---|")
+    cases = []
+    for (n, c, k, hw) in [(256, 128, 128, 28), (256, 256, 256, 14), (256, 512, 512, 7)]:
+        x = torch.randn(n, c, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = (torch.randn(k, c, 3, 3, device=dev) * 0.05).to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy = torch.randn(n, k, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        wr = _rot_weight(w)
+        gf = 2 * n * hw * hw * c * k * 9 / 1e9
+        cases.append(("3x3 fwd %d,%d,%d,%d" % (n, c, k, hw), gf, lambda x=x, w=w: cv.conv_fwd(x, w)))
+        cases.append(("3x3 dgrad %d,%d,%d,%d" % (n, k, c, hw), gf,
+                      lambda dy=dy, wr=wr: cv.conv_fwd(dy, wr)))
+    for (n, ci, co, hw) in [(256, 256, 128, 28), (256, 512, 128, 28), (256, 512, 2048, 7),
+                            (256, 1024, 256, 14)]:
+        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = (torch.randn(co, ci, 1, 1, device=dev) * 0.05).to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        gf = 2 * n * hw * hw * ci * co / 1e9
+        cases.append(("1x1 fwd %d,%d,%d,%d" % (n, ci, co, hw), gf,
+                      lambda x=x, w=w: cv.conv_fwd(x, w, 1)))
+    for name, gf, fn in cases:
+        row, outs = [], []
+        for v in variants:
+            os.environ["APEX_AMD_CONV_BM"] = v
+            t = timeit(fn)
+            outs.append(fn().float())
+            row.append("%.0f us (%.0f TF)" % (t, gf / (t * 1e-6) / 1e3))
+        d = max(float((o - outs[0]).abs().max()) for o in outs[1:])
+        print("| %s | %.1f | %s | %.3g |" % (name, gf, " | ".join(row), d), flush=True)
+    os.environ.pop("APEX_AMD_CONV_BM", None)
+
+
 def bench_conv3x3(args):
     """3x3 stride-1 convs of ResNet-50: MIOpen vs the MFMA implicit-GEMM kernel."""
     from apex_example_amd import _native
@@ -584,12 +632,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "bn-u", "conv1x1", "conv1x1-own", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "optim": bench_optim,
+    {"bn": bench_bn, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv-bm": bench_conv_bm, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
