@@ -26,6 +26,8 @@
 // dK = dS^T.Q sum over the register rows) and a dQ kernel (workgroup owns 128
 // queries, swapped orientation so dQ = dS.K sums over register rows) - no
 // atomics (bitwise reproducible), no LDS transposes of score tiles.
+#include <cstdlib>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -153,7 +155,13 @@ struct AttnArgs {
   uint32_t thr16;    // dropout threshold (p * 65536), 0 = no dropout
   float inv_keep;    // 1 / (1 - p)
   uint32_t seed;
+  int base;  // APEX_AMD_ATTN_BASE=1: round-1 behaviour (eager rescale / per-lane hashes), A/B only
 };
+
+int attn_base_flag() {
+  const char* e = std::getenv("APEX_AMD_ATTN_BASE");
+  return (e && e[0] == '1') ? 1 : 0;
+}
 
 // ---------------------------------------------------------------------------- forward
 template <typename T, bool CAUSAL, bool DROP>
@@ -262,7 +270,11 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, x[t][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
     const float mnew = fmaxf(m, tmax * a.scale_log2);
-    const float alpha = exp2f(m - mnew);
+    // the O / l rescale by exp2(m - mnew) is skipped while no query of the wave
+    // raised its running max (alpha == 1 exactly: same math, 32 fewer multiplies
+    // per tile - the common case once the first tiles have set the max)
+    const bool grow = a.base || __any(mnew != m);
+    const float alpha = grow ? exp2f(m - mnew) : 1.f;
     m = mnew;
     float psum = 0.f;
 #pragma unroll
@@ -274,10 +286,12 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
         x[t][r] = p;
       }
     l = l * alpha + psum;
+    if (grow) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[0][i] *= alpha;
-      o[1][i] *= alpha;
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+      }
     }
     if (DROP) {
 #pragma unroll
@@ -329,6 +343,7 @@ struct AttnBwdArgs {
   uint32_t thr16;
   float inv_keep;
   uint32_t seed;
+  int base;  // APEX_AMD_ATTN_BASE=1: round-1 behaviour (eager rescale / per-lane hashes), A/B only
 };
 
 // D[b,h,q] = sum_d dO * O: 8 lanes per (b, q, h) row, one 16-byte load each
@@ -479,15 +494,31 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
         const float4 dd = *reinterpret_cast<const float4*>(st_D + li);
         const float lsev[4] = {lv.x, lv.y, lv.z, lv.w};
         const float Dv[4] = {dd.x, dd.y, dd.z, dd.w};
+        // keep bits: one hash covers a (query, key pair); the lanes of a key pair
+        // (lane ^ 1) each hash every other query and swap the results over DPP
+        // (quad_perm [1,0,3,2]), so a lane computes 2 hashes per 4 queries, not 4
+        uint32_t hq[4];
+        if (DROP && a.base) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            hq[e] = drop_hash(a.seed, (uint32_t)bh, (uint32_t)(q0 + li + e), (uint32_t)(key >> 1));
+        } else if (DROP) {
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const uint32_t v = drop_hash(a.seed, (uint32_t)bh,
+                                         (uint32_t)(q0 + li + 2 * pr + (key & 1)),
+                                         (uint32_t)(key >> 1));
+            const uint32_t w = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+            hq[2 * pr] = (key & 1) ? w : v;
+            hq[2 * pr + 1] = (key & 1) ? v : w;
+          }
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
           const int q = q0 + li + e;
           float z = 1.f;
-          if (DROP) {
-            const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
-            z = drop_keep(hsh, key, a.thr16) ? a.inv_keep : 0.f;
-          }
+          if (DROP) z = drop_keep(hq[e], key, a.thr16) ? a.inv_keep : 0.f;
           float p = exp2f(fmaf(sc[r], a.scale_log2, -lsev[e]));
           float ds = p * fmaf(dp[r], z, -Dv[e]);
           if (need_mask && !(q < a.S && !(CAUSAL && key > q))) p = ds = 0.f;
@@ -667,6 +698,7 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   a.thr16 = L.dropout > 0.f ? (uint32_t)(L.dropout * 65536.f + 0.5f) : 0u;
   a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
   a.seed = L.seed;
+  a.base = attn_base_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr16 != 0;
 #define ATTN_FWD_LAUNCH(T)                                                                     \
@@ -704,6 +736,7 @@ void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
   a.thr16 = L.dropout > 0.f ? (uint32_t)(L.dropout * 65536.f + 0.5f) : 0u;
   a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
   a.seed = L.seed;
+  a.base = attn_base_flag();
   const int64_t rows = (int64_t)L.B * L.S * L.H;
   const unsigned pre_blocks = (unsigned)((rows * 8 + 255) / 256);
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);

@@ -101,7 +101,7 @@ struct ConvGeom {
 };
 
 template <int MODE, int BM, int BN, int WM, int WN, int NB>
-__global__ void __launch_bounds__(kCT, BM == 256 ? 1 : 2)
+__global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024) ? 1 : 2)
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g) {
   static_assert(WM * WN == 4, "4 waves");
@@ -266,6 +266,7 @@ static int conv_bm_choice() {
   if (!e) return 0;
   if (std::strcmp(e, "256") == 0) return 1;
   if (std::strcmp(e, "256x3") == 0) return 2;
+  if (std::strcmp(e, "128x3") == 0) return 3;
   return 0;
 }
 
@@ -275,7 +276,10 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
-  if (big) {
+  if (big == 3) {
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
+  } else if (big) {
     const dim3 grid((g.M + 255) / 256, g.NC / 128, nclasses);
     if (big == 2)
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
