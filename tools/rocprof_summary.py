@@ -60,6 +60,8 @@ def main(argv=None):
     ap.add_argument("--dispatch-filter", default=None,
                     help="regex: also list every matching dispatch in order (grid, duration)")
     ap.add_argument("--dispatch-out", default=None)
+    ap.add_argument("--names-out", default=None,
+                    help="write every kernel's FULL name with calls / total us (untruncated)")
     a = ap.parse_args(argv)
     disp = []
 
@@ -109,6 +111,10 @@ def main(argv=None):
     if a.md:
         with open(a.md, "w") as fh:
             fh.write(out)
+    if a.names_out:
+        with open(a.names_out, "w") as fh:
+            for k, v in rows:
+                fh.write("%d\t%.1f\t%s\n" % (cnt[k] // div, v / div, re.sub(r"\s+", " ", k)))
     if a.dispatch_out:
         with open(a.dispatch_out, "w") as fh:
             for s0, n, gx, gy, wg, us in sorted(disp):
