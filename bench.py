@@ -81,6 +81,9 @@ def parse():
                     help="keep MIOpen for the stride-1 1x1 convs (default: hipBLASLt GEMM)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step in a hipGraph and replay it")
+    ap.add_argument("--gemm-tuning", choices=["auto", "off"], default="auto",
+                    help="auto: library GEMMs use the TunableOp selections in tuning/<model>.csv "
+                         "(read-only, validator-checked; tools/tune_gemms.sh makes them)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--deterministic", action="store_true")
     # MIOpen immediate mode measured as fast as exhaustive find for ResNet-50 on
@@ -453,6 +456,10 @@ def main():
     torch.backends.cudnn.benchmark = (not args.deterministic) and args.cudnn_benchmark
     torch.backends.cudnn.deterministic = args.deterministic
     torch.manual_seed(1234 + rank)
+    gemm_table = None
+    if args.gemm_tuning == "auto" and not os.environ.get("PYTORCH_TUNABLEOP_ENABLED"):
+        from apex_example_amd.utils.gemm_tuning import use_tuned_gemms
+        gemm_table = use_tuned_gemms(args.model)
 
     if args.model.startswith("resnet"):
         w = build_resnet(args, device, world)
@@ -480,6 +487,10 @@ def main():
     if args.graph:
         if world > 1:
             raise SystemExit("--graph is single-GPU only in this version")
+        if not args.model.startswith("resnet"):
+            # BERT-large's captured step hung on its first replay (MI355X, round 2,
+            # docs/PERF.md); capture is validated for the ResNet models only
+            raise SystemExit("--graph is validated for the ResNet models only")
         # drop every reference to an eager autograd graph (its AccumulateGrad
         # nodes would pin the default stream), then warm the capture path on a
         # side stream (allocator pools, multi-tensor plan caches)
@@ -548,6 +559,8 @@ def main():
     if args.model.startswith("resnet") and (w.config.get("per_gpu_batch") != 256
                                             or args.image_size != 224):
         base = None
+    w.config["gemm_tuning"] = (os.path.relpath(gemm_table, ROOT) if gemm_table else
+                               "env" if os.environ.get("PYTORCH_TUNABLEOP_ENABLED") else None)
     rec = {
         "metric": w.metric,
         "value": round(value, 2),

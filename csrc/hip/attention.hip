@@ -164,14 +164,37 @@ int attn_base_flag() {
 }
 
 // ---------------------------------------------------------------------------- forward
+// Block -> (tile, b*H+h).  Dispatch order is the flattened block id (x fastest) and
+// consecutive ids go to consecutive XCDs, so: (1) the tiles of one head are gridDim.y
+// ids apart - the same XCD whenever B*H % 8 == 0, so that head's K/V (fwd, dQ) or
+// Q/dO (dK/dV) stream through one L2 instead of up to 8; (2) under a causal mask the
+// tiles with the most work are dispatched first (longest-processing-time order: the
+// last query tiles in fwd / dQ, the first key tiles in dK/dV), so the light diagonal
+// tiles fill the tail instead of a few heavy ones.  `base`: the round-1 mapping (A/B).
+__device__ __forceinline__ void tile_of_block(bool causal, bool heavy_high, int base, int& tile,
+                                              int& bh) {
+  if (base) {
+    tile = blockIdx.x;
+    bh = blockIdx.y;
+    return;
+  }
+  const int nt = gridDim.x, nbh = gridDim.y;
+  const int id = blockIdx.x + blockIdx.y * nt;
+  const int t = id / nbh;
+  bh = id - t * nbh;
+  tile = (causal && heavy_high) ? nt - 1 - t : t;
+}
+
 template <typename T, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   typedef typename Frag<T>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * kAKT * kARow];  // 2 x (K, V)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hl = lane >> 5, c32 = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
-  const int qb0 = blockIdx.x * 128;
+  int tile, bh;
+  tile_of_block(CAUSAL, true, a.base, tile, bh);
+  const int b = bh / a.H, hh = bh - b * a.H;
+  const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;  // this lane's query
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
@@ -389,8 +412,10 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hl = lane >> 5, c32 = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
-  const int kb0 = blockIdx.x * 128;
+  int tile, bh;
+  tile_of_block(CAUSAL, false, a.base, tile, bh);
+  const int b = bh / a.H, hh = bh - b * a.H;
+  const int kb0 = tile * 128;
   const int kw0 = kb0 + wid * 32;
   const int key = kw0 + c32;
   const int kk = key < a.S ? key : a.S - 1;
@@ -559,8 +584,10 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 3 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hl = lane >> 5, c32 = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
-  const int qb0 = blockIdx.x * 128;
+  int tile, bh;
+  tile_of_block(CAUSAL, true, a.base, tile, bh);
+  const int b = bh / a.H, hh = bh - b * a.H;
+  const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;
   const int qq = q < a.S ? q : a.S - 1;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
