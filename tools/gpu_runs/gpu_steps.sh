@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Run GPU steps in sequence on the gpurun box; stop at the first step that ends
 # in a fault / abort / timeout (rc not in {0,1}).  Each step has its own limit.
-#   tools/gpu_steps.sh "<secs>|<name>|<command>" ...
+#   tools/gpu_runs/gpu_steps.sh "<secs>|<name>|<command>" ...
 set -u
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
