@@ -50,10 +50,13 @@ namespace {
 // rows in flight per lane of the read-only reductions; APEX_AMD_BN_U="stats,reduce"
 // (A/B switch for tools/microbench.py bn-u, read per launch)
 struct BNUnroll {
-  int stats = 4, reduce = 2;
+  int stats = 4, reduce = 2, elem = 2;
 };
 BNUnroll bn_unroll() {
   BNUnroll u;
+  // rows in flight per lane of the elementwise passes (apply_k, backward_k):
+  // APEX_AMD_BN_EU=2|4 (A/B switch for tools/microbench.py bn-eu)
+  if (const char* e = std::getenv("APEX_AMD_BN_EU")) u.elem = std::atoi(e) == 4 ? 4 : 2;
   if (const char* e = std::getenv("APEX_AMD_BN_U")) {
     int a = 0, b = 0;
     if (std::sscanf(e, "%d,%d", &a, &b) == 2) {
@@ -177,14 +180,13 @@ __global__ void __launch_bounds__(kBNThreads)
 }
 
 // ---------------------------------------------------------------- apply
-template <typename T, typename TW, bool VEC>
+template <typename T, typename TW, bool VEC, int U>
 __global__ void __launch_bounds__(kBNThreads)
     apply_k(const T* __restrict__ x, const float* __restrict__ mean,
             const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
             const T* __restrict__ z, T* __restrict__ y, uint8_t* __restrict__ rmask, int64_t M,
             int C, int ctile, int rows_iter, int relu) {
   constexpr int W = VEC ? 8 : 1;
-  constexpr int U = 2;
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
@@ -288,7 +290,7 @@ __global__ void __launch_bounds__(kBNThreads)
 // ---------------------------------------------------------------- backward elementwise
 // dx = dy'*k1 + x*k2 + k3  with  k1 = invstd*w, k2 = -invstd^3*w*mean(dy'(x-mu)),
 //                                 k3 = -invstd*w*mean(dy') - k2*mu ;  dz = dy'
-template <typename T, typename TW, bool VEC>
+template <typename T, typename TW, bool VEC, int U>
 __global__ void __launch_bounds__(kBNThreads)
     backward_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
                const float* __restrict__ invstd, const TW* __restrict__ w,
@@ -297,7 +299,6 @@ __global__ void __launch_bounds__(kBNThreads)
                const T* __restrict__ z, const uint8_t* __restrict__ rmask, T* __restrict__ dx,
                T* __restrict__ dz, int64_t M, int C, int ctile, int rows_iter) {
   constexpr int W = VEC ? 8 : 1;
-  constexpr int U = 2;
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
@@ -411,11 +412,16 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
       using T = decltype(t0);
       using TW = decltype(w0);
       vec_dispatch(vec, [&](auto V) {
-        hipLaunchKernelGGL((apply_k<T, TW, decltype(V)::value>), dim3(blocks, g.cblocks),
-                           dim3(kBNThreads), 0, st, static_cast<const T*>(x), mean, invstd,
-                           static_cast<const TW*>(w), static_cast<const TW*>(b),
-                           static_cast<const T*>(z), static_cast<T*>(y), vec ? rmask : nullptr,
-                           M, (int)C, g.ctile, g.rows_iter, relu);
+        auto go = [&](auto u) {
+          hipLaunchKernelGGL((apply_k<T, TW, decltype(V)::value, decltype(u)::value>),
+                             dim3(blocks, g.cblocks), dim3(kBNThreads), 0, st,
+                             static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
+                             static_cast<const TW*>(b), static_cast<const T*>(z),
+                             static_cast<T*>(y), vec ? rmask : nullptr, M, (int)C, g.ctile,
+                             g.rows_iter, relu);
+        };
+        if (bn_unroll().elem == 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 2>{});
       });
     });
   });
@@ -463,12 +469,17 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
       using T = decltype(t0);
       using TW = decltype(w0);
       vec_dispatch(vec, [&](auto V) {
-        hipLaunchKernelGGL((backward_k<T, TW, decltype(V)::value>), dim3(blocks, g.cblocks),
-                           dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
-                           static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
-                           static_cast<const TW*>(b), sum_dy, sum_dy_xmu, inv_count, relu,
-                           static_cast<const T*>(z), rmask, static_cast<T*>(dx),
-                           static_cast<T*>(dz), M, (int)C, g.ctile, g.rows_iter);
+        auto go = [&](auto u) {
+          hipLaunchKernelGGL((backward_k<T, TW, decltype(V)::value, decltype(u)::value>),
+                             dim3(blocks, g.cblocks), dim3(kBNThreads), 0, st,
+                             static_cast<const T*>(dy), static_cast<const T*>(x), mean, invstd,
+                             static_cast<const TW*>(w), static_cast<const TW*>(b), sum_dy,
+                             sum_dy_xmu, inv_count, relu, static_cast<const T*>(z), rmask,
+                             static_cast<T*>(dx), static_cast<T*>(dz), M, (int)C, g.ctile,
+                             g.rows_iter);
+        };
+        if (bn_unroll().elem == 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 2>{});
       });
     });
   });

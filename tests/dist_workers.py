@@ -278,17 +278,20 @@ def gpu_ddp_resnet(rank, world, steps=4, syncbn=False, lr=0.05, opt_level="O2"):
     m, opt = amp.initialize(m, opt, opt_level=opt_level, half_dtype=torch.bfloat16, verbosity=0)
     ddp = DistributedDataParallel(m, message_size=200_000)
     x, y = _resnet_batch(rank)
-    losses = []
-    for _ in range(steps):
+    losses, masters1 = [], None
+    for i in range(steps):
         loss = F.cross_entropy(ddp(x), y)
         opt.zero_grad()
         with amp.scale_loss(loss, opt) as s:
             s.backward()
         opt.step()
         losses.append(loss.item())
+        if i == 0:
+            masters1 = [p.detach().float().cpu() for p in amp.master_params(opt)]
     torch.cuda.synchronize()
     return {"params": [p.detach().float().cpu() for p in m.parameters()], "losses": losses,
             "masters": [p.detach().float().cpu() for p in amp.master_params(opt)],
+            "masters1": masters1,
             "views": all(getattr(p, "_amd_grad_is_bucket_view", False) for p in m.parameters())}
 
 
@@ -316,17 +319,19 @@ def gpu_resnet_reference(world=2, steps=4, lr=0.05, opt_level="O2"):
     batches = [_resnet_batch(r) for r in range(world)]
     x = torch.cat([b[0] for b in batches]).contiguous(memory_format=torch.channels_last)
     y = torch.cat([b[1] for b in batches])
-    losses = []
-    for _ in range(steps):
+    losses, masters1 = [], None
+    for i in range(steps):
         loss = F.cross_entropy(m(x), y)
         opt.zero_grad()
         with amp.scale_loss(loss, opt) as s:
             s.backward()
         opt.step()
         losses.append(loss.item())
+        if i == 0:
+            masters1 = [p.detach().float().cpu() for p in amp.master_params(opt)]
     torch.cuda.synchronize()
     return {"masters": [p.detach().float().cpu() for p in amp.master_params(opt)],
-            "losses": losses, "params0": p0}
+            "masters1": masters1, "losses": losses, "params0": p0}
 
 
 # ---------------------------------------------------------------------- ZeRO Adam

@@ -167,15 +167,27 @@ def test_two_ranks_match_concatenated_batch(tmp_path, opt_level):
         assert abs(a - b) <= tol * abs(b) + atol, (ddp_loss, ref["losses"])
     if opt_level != "O0":
         return
-    worst = 0.0
-    assert len(res[0]["masters"]) == len(ref["masters"]) == len(ref["params0"])
-    for a, b, p0 in zip(res[0]["masters"], ref["masters"], ref["params0"]):
-        # compare the UPDATES (param - init): the init itself cancels out
-        da, db = a - p0, b - p0
-        scale = db.abs().max().item()
-        if scale > 0:
-            worst = max(worst, (da - db).abs().max().item() / scale)
-    assert worst < 2e-2, worst
+
+    def worst_update_diff(ma, mb):
+        worst = 0.0
+        assert len(ma) == len(mb) == len(ref["params0"])
+        for a, b, p0 in zip(ma, mb, ref["params0"]):
+            # compare the UPDATES (param - init): the init itself cancels out
+            da, db = a - p0, b - p0
+            scale = db.abs().max().item()
+            if scale > 0:
+                worst = max(worst, (da - db).abs().max().item() / scale)
+        return worst
+
+    # one step: DDP's averaged gradient IS the concatenated batch's gradient, so the
+    # first update agrees to summation-order noise in every tensor
+    w1 = worst_update_diff(res[0]["masters1"], ref["masters1"])
+    assert w1 < 1e-2, w1
+    # after 4 steps of this memorisation task the per-tensor max-relative update
+    # difference has been amplified by the dynamics (measured 0.3-9 % across boxes
+    # whose MIOpen fp32 conv algorithms differ) - a sanity bound only
+    w4 = worst_update_diff(res[0]["masters"], ref["masters"])
+    assert w4 < 0.25, w4
 
 
 def test_distributed_fused_adam_two_ranks_one_gpu(tmp_path):

@@ -127,6 +127,48 @@ def bench_bn_u(args):
         "%.0f / %.0f" % tuple(tot[v]) for v in variants) + " |")
 
 
+def bench_bn_eu(args):
+    """Elementwise BN passes (apply_k with residual + ReLU, backward_k) per shape over
+    rows-in-flight U (APEX_AMD_BN_EU) x rows per thread (elem_rpt): per-shape us, the
+    best config per shape and the ResNet-50-weighted totals of the default vs the
+    per-shape best."""
+    from apex_example_amd import _native
+
+    C_ = _native.require().bn
+    dev = "cuda"
+    default = C_.get_tuning()
+    cfgs = [(u, r) for u in (2, 4) for r in (4, 8, 16, 32)]
+    tot_def = tot_best = 0.0
+    print("| shape | count | " + " | ".join("U%d r%d" % c for c in cfgs) + " | best |")
+    print("|---|---|" + "---|" * (len(cfgs) + 1))
+    for (n, c, h, w), cnt in R50_BN.items():
+        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy, z = torch.randn_like(x), torch.randn_like(x)
+        wt, bs = torch.ones(c, device=dev), torch.zeros(c, device=dev)
+        mean, var = C_.local_stats(x)
+        invstd = (var + 1e-5).rsqrt()
+        s1, s2, _, _ = C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True)
+        row, res = [], {}
+        for (u, r) in cfgs:
+            os.environ["APEX_AMD_BN_EU"] = str(u)
+            C_.set_tuning(elem_rpt=r)
+            ta = timeit(lambda: C_.apply(x, mean, invstd, wt, bs, z, True))
+            tb = timeit(lambda: C_.backward_elemt(dy, x, mean, invstd, wt, bs, s1, s2,
+                                                  float(n * h * w), z, True, True))
+            res[(u, r)] = ta + tb
+            row.append("%.0f+%.0f" % (ta, tb))
+        best = min(res, key=res.get)
+        tot_def += cnt * res[(2, default[3])] if (2, default[3]) in res else 0.0
+        tot_best += cnt * res[best]
+        print("| %s | %d | %s | U%d r%d |" % ((n, c, h, w), cnt, " | ".join(row), *best),
+              flush=True)
+    os.environ.pop("APEX_AMD_BN_EU", None)
+    C_.set_tuning(elem_rpt=default[3])
+    print("R50-weighted apply+backward: default (U2 r%d) %.0f us, per-shape best %.0f us" % (
+        default[3], tot_def, tot_best))
+
+
 def bench_bn_tune(args):
     """Sweep the NHWC BN grid-sizing knobs; report the ResNet-50-weighted total
     (forward stats+finalize+apply, backward reduce+finalize+elementwise) per config."""
@@ -638,12 +680,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv-bm": bench_conv_bm, "optim": bench_optim,
+    {"bn": bench_bn, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv-bm": bench_conv_bm, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
