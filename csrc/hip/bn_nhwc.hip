@@ -85,9 +85,33 @@ int reduce_splits(int64_t M, const NGeom& g) {
   return (int)(want < 1 ? 1 : want);
 }
 
-int elem_blocks(int64_t M, const NGeom& g) {
+// rows per thread of the elementwise passes.  A per-shape rule from the isolated
+// sweep (tools/microbench.py bn-eu, profiles/microbench_bn_eu.txt): tensors larger
+// than the 256 MB Infinity Cache at 8 rows per thread, smaller ones at the most rows
+// per thread (up to 32) that still leaves >= 384 workgroups.  It cut apply + backward
+// 4 % R50-weighted in isolation but measured 0.25 % SLOWER in the training step
+// (same-box A/B, 9662 vs 9687 img/s: the isolated loop re-reads a cache-warm tensor),
+// so the fixed elem_rpt stays the default; APEX_AMD_BN_ELEM_AUTO=1 or
+// bn_set_tuning(elem_rpt=0) selects the rule.
+int elem_rpt_for(int64_t M, const NGeom& g, int64_t bytes) {
   const BNTuning& t = bn_tuning();
-  int64_t want = (M + (int64_t)g.rows_iter * t.elem_rpt - 1) / ((int64_t)g.rows_iter * t.elem_rpt);
+  static const bool env_auto = [] {
+    const char* e = std::getenv("APEX_AMD_BN_ELEM_AUTO");
+    return e && e[0] == '1';
+  }();
+  if (!(t.elem_auto || env_auto)) return t.elem_rpt;
+  if (bytes > (int64_t)256 << 20) return 8;
+  for (int r = 32; r > 8; r >>= 1) {
+    const int64_t blocks = (M + (int64_t)g.rows_iter * r - 1) / ((int64_t)g.rows_iter * r) * g.cblocks;
+    if (blocks >= 384) return r;
+  }
+  return 8;
+}
+
+int elem_blocks(int64_t M, const NGeom& g, int64_t bytes) {
+  const BNTuning& t = bn_tuning();
+  const int rpt = elem_rpt_for(M, g, bytes);
+  int64_t want = (M + (int64_t)g.rows_iter * rpt - 1) / ((int64_t)g.rows_iter * rpt);
   const int64_t floor_blocks = t.elem_min / g.cblocks;
   const int64_t max_by_rows = M / ((int64_t)g.rows_iter * 2);
   if (want < floor_blocks) want = floor_blocks < max_by_rows ? floor_blocks : max_by_rows;
@@ -367,7 +391,12 @@ void bn_set_tuning(int red_rpt, int red_cap, int red_min, int elem_rpt, int elem
   if (red_rpt > 0) t.red_rpt = red_rpt;
   if (red_cap > 0) t.red_cap = red_cap;
   if (red_min >= 0) t.red_min = red_min;
-  if (elem_rpt > 0) t.elem_rpt = elem_rpt;
+  if (elem_rpt > 0) {
+    t.elem_rpt = elem_rpt;
+    t.elem_auto = false;
+  } else if (elem_rpt == 0) {
+    t.elem_auto = true;  // back to the per-shape rule
+  }
   if (elem_cap > 0) t.elem_cap = elem_cap;
   if (elem_min >= 0) t.elem_min = elem_min;
 }
@@ -406,7 +435,7 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
                 int64_t C, int relu, hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({x, z, y});
   const NGeom g = ngeom(C, vec);
-  const int blocks = elem_blocks(M, g);
+  const int blocks = elem_blocks(M, g, M * C * (tx == DType::F32 ? 4 : 2));
   bn_dispatch(tx, [&](auto t0) {
     bn_dispatch(tw, [&](auto w0) {
       using T = decltype(t0);
@@ -463,7 +492,7 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
                    hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({dy, x, z, dx, dz});
   const NGeom g = ngeom(C, vec);
-  const int blocks = elem_blocks(M, g);
+  const int blocks = elem_blocks(M, g, M * C * (tx == DType::F32 ? 4 : 2));
   bn_dispatch(tx, [&](auto t0) {
     bn_dispatch(tw, [&](auto w0) {
       using T = decltype(t0);

@@ -191,6 +191,7 @@ static inline void launch_reduce_finalize(const float* slab, int splits, int64_t
 struct BNTuning {
   int red_rpt = 64, red_cap = 1024, red_min = 512;
   int elem_rpt = 16, elem_cap = 16384, elem_min = 0;
+  bool elem_auto = false;  // per-shape elem_rpt rule (bn_nhwc.hip elem_rpt_for), opt-in
 };
 BNTuning& bn_tuning();
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec);

@@ -138,9 +138,9 @@ def bench_bn_eu(args):
     dev = "cuda"
     default = C_.get_tuning()
     cfgs = [(u, r) for u in (2, 4) for r in (4, 8, 16, 32)]
-    tot_def = tot_best = 0.0
-    print("| shape | count | " + " | ".join("U%d r%d" % c for c in cfgs) + " | best |")
-    print("|---|---|" + "---|" * (len(cfgs) + 1))
+    tot_def = tot_best = tot_auto = 0.0
+    print("| shape | count | " + " | ".join("U%d r%d" % c for c in cfgs) + " | auto | best |")
+    print("|---|---|" + "---|" * (len(cfgs) + 2))
     for (n, c, h, w), cnt in R50_BN.items():
         x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
             memory_format=torch.channels_last)
@@ -158,6 +158,13 @@ def bench_bn_eu(args):
                                                   float(n * h * w), z, True, True))
             res[(u, r)] = ta + tb
             row.append("%.0f+%.0f" % (ta, tb))
+        C_.set_tuning(elem_rpt=0)  # the per-shape rule (bn_nhwc.hip elem_rpt_for)
+        os.environ["APEX_AMD_BN_EU"] = "2"
+        t_auto = (timeit(lambda: C_.apply(x, mean, invstd, wt, bs, z, True))
+                  + timeit(lambda: C_.backward_elemt(dy, x, mean, invstd, wt, bs, s1, s2,
+                                                     float(n * h * w), z, True, True)))
+        tot_auto += cnt * t_auto
+        row.append("%.0f" % t_auto)
         best = min(res, key=res.get)
         tot_def += cnt * res[(2, default[3])] if (2, default[3]) in res else 0.0
         tot_best += cnt * res[best]
@@ -165,8 +172,8 @@ def bench_bn_eu(args):
               flush=True)
     os.environ.pop("APEX_AMD_BN_EU", None)
     C_.set_tuning(elem_rpt=default[3])
-    print("R50-weighted apply+backward: default (U2 r%d) %.0f us, per-shape best %.0f us" % (
-        default[3], tot_def, tot_best))
+    print("R50-weighted apply+backward: fixed U2 r%d %.0f us, per-shape rule %.0f us, "
+          "per-shape best %.0f us" % (default[3], tot_def, tot_auto, tot_best))
 
 
 def bench_bn_tune(args):
