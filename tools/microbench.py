@@ -343,6 +343,47 @@ def bench_conv1x1_own(args):
               flush=True)
 
 
+def bench_wgrad_o1(args):
+    """amp O1 weight gradients of GPT-2-medium's dense layers (fp16 operands, T = 8192
+    tokens, fp32 weight): one GEMM writing fp32 (mm(out_dtype=fp32), what fused_dense
+    runs) vs an fp16 GEMM + cast (Apex O1's dataflow), the fp16 GEMM with PyTorch's
+    default heuristic and with TunableOp-tuned selections."""
+    dev = "cuda"
+    T = 8192
+    shapes = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096)]  # (out, in)
+    data = []
+    for (o, i) in shapes:
+        dy = torch.randn(T, o, device=dev, dtype=torch.float16)
+        x = torch.randn(T, i, device=dev, dtype=torch.float16)
+        data.append((o, i, dy, x))
+    rows = {}
+    for (o, i, dy, x) in data:
+        rows[(o, i)] = [timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)),
+                        timeit(lambda: dy.t() @ x),
+                        timeit(lambda: (dy.t() @ x).float())]
+    t = torch.cuda.tunable
+    t.enable(True)
+    t.tuning_enable(True)
+    t.set_max_tuning_duration(100)
+    t.set_max_tuning_iterations(100)
+    for (o, i, dy, x) in data:
+        for _ in range(2):  # first call tunes
+            dy.t() @ x
+            torch.mm(dy.t(), x, out_dtype=torch.float32)
+        torch.cuda.synchronize()
+        rows[(o, i)] += [timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)),
+                         timeit(lambda: dy.t() @ x), timeit(lambda: (dy.t() @ x).float())]
+    t.tuning_enable(False)
+    t.enable(False)
+    print("| dW [out, in], T=8192 | GF | fp32-out mm | fp16 mm | fp16 mm + cast | tuned: fp32-out | "
+          "fp16 | fp16 + cast |")
+    print("|---|---|---|---|---|---|---|---|")
+    for (o, i), r in rows.items():
+        gf = 2 * T * o * i / 1e9
+        print("| %d x %d | %.1f | %s |" % (o, i, gf, " | ".join(
+            "%.0f us (%.0f TF)" % (v, gf / 1e3 / (v * 1e-6)) for v in r)), flush=True)
+
+
 def bench_wgrad(args):
     """1x1-conv weight gradient dW[co,ci] = sum_m dY[m,co] X[m,ci]: MIOpen vs
     split-K hipBLASLt (bmm over S row-chunks with fp32 output, then a sum)."""
@@ -687,12 +728,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "wgrad-o1", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv-bm": bench_conv_bm, "optim": bench_optim,
+    {"bn": bench_bn, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "wgrad-o1": bench_wgrad_o1, "conv-bm": bench_conv_bm, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 

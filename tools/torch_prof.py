@@ -29,7 +29,7 @@ def main():
             w.step(w.batch)
         torch.cuda.synchronize()
     ka = prof.key_averages(group_by_input_shape=True)
-    print(ka.table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=60,
+    print(ka.table(sort_by="self_cuda_time_total", row_limit=int(os.environ.get("TORCH_PROF_ROWS", "60")), max_name_column_width=60,
                    max_shapes_column_width=90))
 
 
