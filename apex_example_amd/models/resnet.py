@@ -17,7 +17,8 @@ import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
 from ..ops.conv import Conv2d1x1, Conv2d3x3, StemConv2d
-from ..ops.pool import MaxPool2dNHWC, bn_relu_maxpool, bn_relu_maxpool_fusable
+from ..ops.pool import (GlobalAvgPool2dNHWC, MaxPool2dNHWC, bn_relu_maxpool,
+                        bn_relu_maxpool_fusable)
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1, mfma=False):
@@ -134,7 +135,7 @@ class ResNet(nn.Module):
         self.layer2 = self._make_layer(block, 128, layers[1], 2, zero_init_residual)
         self.layer3 = self._make_layer(block, 256, layers[2], 2, zero_init_residual)
         self.layer4 = self._make_layer(block, 512, layers[3], 2, zero_init_residual)
-        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.avgpool = GlobalAvgPool2dNHWC() if fused_bn else nn.AdaptiveAvgPool2d((1, 1))
         self.fc = nn.Linear(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):

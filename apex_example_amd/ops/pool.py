@@ -17,6 +17,7 @@ from .. import _native
 
 # A/B switch for the fused stem (tools, docs/PERF.md)
 _FUSE_STEM = os.environ.get("APEX_AMD_FUSE_STEM", "1") == "1"
+_GAP_KERNEL = os.environ.get("APEX_AMD_GAP_OFF", "0") != "1"
 
 
 class MaxPool2dNHWCFunction(torch.autograd.Function):
@@ -105,3 +106,36 @@ class MaxPool2dNHWC(nn.MaxPool2d):
             return MaxPool2dNHWCFunction.apply(x, k, s, p)
         return F.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.dilation,
                             self.ceil_mode, self.return_indices)
+
+
+class GlobalAvgPoolNHWCFunction(torch.autograd.Function):
+    """x.mean((2, 3), keepdim=True) whose gradient is written channels-last by one
+    vectorized kernel (csrc/hip/pool.hip gap_bwd_k).  ATen's gradient is an expanded
+    [N, C, H, W] view; the fused BN backward behind it needs a dense channels-last
+    tensor, and the resulting .contiguous() ran as strided 2-byte copies (~80 us per
+    copy for ResNet-50's [256, 2048, 7, 7] at bs 256, twice per step)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.size(2), x.size(3))
+        return x.mean((2, 3), keepdim=True)
+
+    @staticmethod
+    def backward(ctx, dy):
+        H, W = ctx.hw
+        return _native.require().pool.gap_bwd(dy, H, W)
+
+
+class GlobalAvgPool2dNHWC(nn.AdaptiveAvgPool2d):
+    """nn.AdaptiveAvgPool2d((1, 1)) with the channels-last gradient kernel on the GPU."""
+
+    def __init__(self):
+        super().__init__((1, 1))
+
+    def forward(self, x):
+        if (_GAP_KERNEL and x.is_cuda and x.dim() == 4
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+                and _native.available()):
+            return GlobalAvgPoolNHWCFunction.apply(x)
+        return super().forward(x)

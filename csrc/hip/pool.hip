@@ -151,6 +151,31 @@ __global__ void __launch_bounds__(kPoolThreads)
   }
 }
 
+// global average pool backward, NHWC: dx[n, hw, c] = dy[n, c] * inv_hw.  dy is one
+// [C] row per image (L2-resident), dx is written once with 16-byte stores in memory
+// order - the gradient of x.mean((2, 3)) materialised channels-last directly, instead
+// of an expanded view that a later .contiguous() copies with strided 2-byte stores.
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(kPoolThreads)
+    gap_bwd_k(const T* __restrict__ dy, T* __restrict__ dx, int64_t N, int64_t HW, int C,
+              float inv_hw) {
+  constexpr int V = VEC ? 8 : 1;
+  const int CV = C / V;
+  const int64_t total = N * HW * CV;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    const int64_t n = t / CV / HW;
+    float g[V];
+    if constexpr (VEC) load8(dy + n * C + cv * V, g);
+    else g[0] = to_f32(dy[n * C + cv]);
+#pragma unroll
+    for (int i = 0; i < V; ++i) g[i] *= inv_hw;
+    if constexpr (VEC) store8(dx + t * V, g);
+    else dx[t] = from_f32<T>(g[0]);
+  }
+}
+
 template <typename F>
 void pool_dispatch(DType t, F&& f) {
   switch (t) {
@@ -214,6 +239,23 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
       hipLaunchKernelGGL((maxpool_bwd_k<T, false>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
                          st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C, OH,
                          OW, k, s, p);
+  });
+}
+
+void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int C,
+                  hipStream_t st) {
+  const bool vec = C % 8 == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0;
+  const int64_t items = N * HW * (vec ? C / 8 : C);
+  if (items == 0) return;
+  const float inv_hw = 1.f / (float)HW;
+  pool_dispatch(t, [&](auto t0) {
+    using T = decltype(t0);
+    if (vec)
+      hipLaunchKernelGGL((gap_bwd_k<T, true>), dim3(pool_grid(items)), dim3(kPoolThreads), 0, st,
+                         static_cast<const T*>(dy), static_cast<T*>(dx), N, HW, C, inv_hw);
+    else
+      hipLaunchKernelGGL((gap_bwd_k<T, false>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
+                         st, static_cast<const T*>(dy), static_cast<T*>(dx), N, HW, C, inv_hw);
   });
 }
 

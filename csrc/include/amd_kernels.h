@@ -220,6 +220,9 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
                         const float* bw = nullptr, const float* bb = nullptr);
 void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
                         int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
+// global average pool backward: dx[N, HW, C] (channels-last) = dy[N, C] / HW
+void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int C,
+                  hipStream_t st);
 
 // ---- implicit-GEMM convolutions, NHWC bf16, MFMA (conv_igemm.hip) ----------
 // 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64

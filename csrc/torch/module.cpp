@@ -99,6 +99,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
   pool.def("max_bwd", &maxpool2d_nhwc_bwd_op);
+  pool.def("gap_bwd", &gap_nhwc_bwd_op, py::arg("dy"), py::arg("H"), py::arg("W"));
   pool.def("max_fwd_bn", &maxpool2d_nhwc_bn_fwd_op);
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
   conv.def("conv_fwd", &conv_nhwc_fwd_op, py::arg("x"), py::arg("w"), py::arg("stride") = 1);

@@ -58,6 +58,18 @@ at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64
   return dx;
 }
 
+at::Tensor gap_nhwc_bwd_op(at::Tensor dy, int64_t H, int64_t W) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(dy.is_cuda() && (dy.dim() == 2 || dy.dim() == 4), "gap_bwd: dy [N, C(, 1, 1)]");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(dy.numel() == N * C, "gap_bwd: dy must hold one value per (n, c)");
+  dy = dy.reshape({N, C}).contiguous();
+  at::Tensor dx =
+      at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  gap_nhwc_bwd(dy.data_ptr(), dtype_of(dy), dx.data_ptr(), N, H * W, (int)C, cur_stream());
+  return dx;
+}
+
 }  // namespace amd
 
 namespace amd {

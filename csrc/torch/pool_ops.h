@@ -15,6 +15,7 @@ std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_bn_fwd_op(
     c10::optional<at::Tensor> w, c10::optional<at::Tensor> b, int64_t k, int64_t s, int64_t p);
 at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W, int64_t k,
                                  int64_t s, int64_t p);
+at::Tensor gap_nhwc_bwd_op(at::Tensor dy, int64_t H, int64_t W);
 
 // 3x3 / 1x1 convs (stride 1 or 2), NHWC bf16, implicit GEMM on MFMA (conv_igemm.hip)
 at::Tensor conv_nhwc_fwd_op(at::Tensor x, at::Tensor w, int64_t stride);

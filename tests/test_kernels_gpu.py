@@ -601,6 +601,30 @@ def test_maxpool_nhwc(shape, k, s, p, dt):
                                atol=1e-2 if dt != torch.float32 else 1e-6)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("shape", [(3, 2048, 7, 7), (2, 12, 5, 3)])
+def test_global_avg_pool_nhwc(shape, dt):
+    """Global average pool with the channels-last gradient kernel (vector and scalar
+    paths) vs the fp32 mean: the gradient is dy / HW broadcast, written dense
+    channels-last."""
+    from apex_example_amd.ops.pool import GlobalAvgPool2dNHWC, GlobalAvgPoolNHWCFunction
+
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=DEV).to(dt).to(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    ya = GlobalAvgPool2dNHWC()(xa)
+    assert ya.grad_fn is not None and "GlobalAvgPoolNHWC" in type(ya.grad_fn).__name__
+    ref = x.float().mean((2, 3), keepdim=True)
+    tol = 1e-6 if dt == torch.float32 else 1e-2
+    torch.testing.assert_close(ya.float(), ref, rtol=tol, atol=tol)
+    dy = torch.randn_like(ya)
+    ya.backward(dy)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    want = (dy.float() / (shape[2] * shape[3])).expand(*shape)
+    torch.testing.assert_close(xa.grad.float(), want, rtol=tol, atol=tol * 1e-2)
+    assert GlobalAvgPoolNHWCFunction is not None
+
+
 @pytest.mark.parametrize("shape", [(2, 64, 64, 9, 9), (2, 128, 128, 5, 7), (3, 64, 192, 8, 8),
                                    (1, 256, 64, 14, 14), (2, 64, 128, 1, 1)])
 def test_conv3x3_mfma_igemm(shape):

@@ -384,6 +384,55 @@ def bench_wgrad_o1(args):
             "%.0f us (%.0f TF)" % (v, gf / 1e3 / (v * 1e-6)) for v in r)), flush=True)
 
 
+def bench_wgrad_dense(args):
+    """Transformer dense-layer weight gradients dW[out, in] = dY^T X over T tokens (long
+    K, small output: 16-48 output tiles of 256 x 256 cannot fill 256 CUs): one GEMM
+    (PyTorch heuristic, and the committed TunableOp table) vs split-K over S token
+    chunks (fp32 partials from one batched GEMM + the slab reduction kernel)."""
+    from apex_example_amd import _native
+    from apex_example_amd.utils.gemm_tuning import use_tuned_gemms
+
+    cv = _native.require().conv
+    dev = "cuda"
+    cases = [("bert", 16384, torch.bfloat16, torch.bfloat16),
+             ("gpt2-O1", 8192, torch.float16, torch.float32)]
+    shapes = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096)]
+    Ss = (2, 4, 8, 16)
+    print("| model | dW [out, in] | T | GF | mm | mm tuned | " +
+          " | ".join("split-K S=%d" % S for S in Ss) + " |")
+    print("|---|---|---|---|---|---|" + "---|" * len(Ss))
+    for name, T, dt, odt in cases:
+        for (o, i) in shapes:
+            dy = torch.randn(T, o, device=dev, dtype=dt)
+            x = torch.randn(T, i, device=dev, dtype=dt)
+            gf = 2 * T * o * i / 1e9
+
+            def one():
+                if odt == dt:
+                    return dy.t() @ x
+                return torch.mm(dy.t(), x, out_dtype=odt)
+
+            def splitk(S):
+                a = dy.view(S, T // S, o).transpose(1, 2)
+                b = x.view(S, T // S, i)
+                return cv.splitk_reduce(torch.bmm(a, b, out_dtype=torch.float32), odt)
+
+            t_mm = timeit(one)
+            ref = one().float()
+            torch.cuda.tunable.enable(False)
+            tuned = use_tuned_gemms("bert_large" if name == "bert" else "gpt2_medium")
+            t_tuned = timeit(one) if tuned else float("nan")
+            torch.cuda.tunable.enable(False)
+            cols = []
+            for S in Ss:
+                t = timeit(lambda S=S: splitk(S))
+                err = float((splitk(S).float() - ref).abs().max() / ref.abs().max())
+                cols.append("%.0f us (%.0f TF, err %.1e)" % (t, gf / 1e3 / (t * 1e-6), err))
+            print("| %s | %d x %d | %d | %.1f | %.0f us (%.0f TF) | %.0f us | %s |" % (
+                name, o, i, T, gf, t_mm, gf / 1e3 / (t_mm * 1e-6), t_tuned, " | ".join(cols)),
+                flush=True)
+
+
 def bench_wgrad(args):
     """1x1-conv weight gradient dW[co,ci] = sum_m dY[m,co] X[m,ci]: MIOpen vs
     split-K hipBLASLt (bmm over S row-chunks with fp32 output, then a sum)."""
@@ -728,12 +777,12 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "wgrad-o1", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "wgrad-o1": bench_wgrad_o1, "conv-bm": bench_conv_bm, "optim": bench_optim,
+    {"bn": bench_bn, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
