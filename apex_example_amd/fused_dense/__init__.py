@@ -122,9 +122,43 @@ class cast_params_once:
         return False
 
 
+# Split-K for the dense weight gradients (tools/microbench.py wgrad-dense,
+# profiles/microbench_wgrad_dense.txt): dW[out, in] = dY^T X reduces over all T tokens
+# into only 16-64 output tiles of 256 x 256, too few workgroups for 256 CUs, so one
+# GEMM runs at 300-870 TF.  Cutting T into S chunks (>= 2048 tokens each, S x tiles
+# <= 256) gives one batched GEMM with fp32 partials + the slab reduction kernel
+# writing the weight dtype: BERT-large (T = 16384) 101 -> 53 us for 1024 x 1024,
+# 163 -> 130 us for 3072 x 1024, 168 -> 150 us for 4096 x 1024; GPT-2 O1 (T = 8192,
+# fp32 dW) 57 -> 39 us / 91 -> 83 us, but slower at 64 tiles there.  APEX_AMD_DENSE_SPLITK=0
+# disables.
+_DENSE_SPLITK = os.environ.get("APEX_AMD_DENSE_SPLITK", "1") == "1"
+
+
+def _splitk_chunks(T, o, i, in_dtype, out_dtype):
+    tiles = -(-o // 256) * -(-i // 256)
+    if tiles > (64 if out_dtype == in_dtype else 48):
+        return 1
+    S = 1
+    while S < 16 and T % (2 * S) == 0 and T // (2 * S) >= 2048 and 2 * S * tiles <= 256:
+        S *= 2
+    return S
+
+
 def _wgrad(dy2, x2, dtype):
     """dW = dy2^T x2 written in the parameter's dtype by the GEMM itself (amp O1:
-    fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW)."""
+    fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW); split-K over
+    the tokens when the output has too few tiles to fill the GPU."""
+    if (_DENSE_SPLITK and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
+            and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
+            and _native.available()):
+        T, o = dy2.shape
+        i = x2.shape[1]
+        S = _splitk_chunks(T, o, i, dy2.dtype, dtype)
+        if S > 1 and (o * i) % 4 == 0 and dy2.is_contiguous() and x2.is_contiguous():
+            a = dy2.view(S, T // S, o).transpose(1, 2)
+            b = x2.view(S, T // S, i)
+            part = torch.bmm(a, b, out_dtype=torch.float32)
+            return _native.require().conv.splitk_reduce(part, dtype)
     if dtype != dy2.dtype and dy2.is_cuda and dtype == torch.float32:
         return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
     return dy2.t() @ x2

@@ -133,3 +133,20 @@ def test_skip_variants_match_plain_residual():
     (F.linear(F.gelu(F.linear(x, w, b)), w2, b2).pow(2).sum() + x.sin().sum()).backward()
     for g, t in zip(got, (x, w, b, w2, b2)):
         torch.testing.assert_close(g, t.grad)
+
+
+def test_dense_wgrad_splitk_chunking_rule():
+    """Split-K chunk counts of the dense weight gradient (measured table in
+    profiles/microbench_wgrad_dense.txt): >= 2048 tokens per chunk, S x 256-tiles <= 256,
+    no split above 64 tiles (16-bit dW) / 48 tiles (fp32 dW)."""
+    from apex_example_amd.fused_dense import _splitk_chunks
+
+    bf, h, f = torch.bfloat16, torch.float16, torch.float32
+    assert _splitk_chunks(16384, 1024, 1024, bf, bf) == 8
+    assert _splitk_chunks(16384, 3072, 1024, bf, bf) == 4
+    assert _splitk_chunks(16384, 4096, 1024, bf, bf) == 4
+    assert _splitk_chunks(8192, 1024, 1024, h, f) == 4
+    assert _splitk_chunks(8192, 3072, 1024, h, f) == 4
+    assert _splitk_chunks(8192, 4096, 1024, h, f) == 1
+    assert _splitk_chunks(2048, 1024, 1024, bf, bf) == 1
+    assert _splitk_chunks(16384, 30522, 1024, bf, bf) == 1

@@ -243,3 +243,27 @@ def test_wgrad_bgrad_epilogue(dt, wdt):
     ref_b = dy.float().sum(0)
     err_b = float((db - ref_b).abs().max()) / float(ref_b.abs().max())
     assert err_b < 1e-3, err_b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,wdt", [(torch.bfloat16, torch.bfloat16),
+                                    (torch.float16, torch.float32),
+                                    (torch.bfloat16, torch.float32)])
+@pytest.mark.parametrize("o,i", [(512, 256), (768, 1024)])
+def test_dense_wgrad_splitk(dt, wdt, o, i):
+    """fused_dense's split-K weight gradient (T token chunks, fp32 partials, slab
+    reduction into the weight dtype) vs the fp32 product, and the chunking rule."""
+    from apex_example_amd import fused_dense as fd
+
+    T = 8192
+    assert fd._splitk_chunks(T, o, i, dt, wdt) > 1
+    assert fd._splitk_chunks(16384, 1024, 1024, torch.bfloat16, torch.bfloat16) == 8
+    assert fd._splitk_chunks(8192, 4096, 1024, torch.float16, torch.float32) == 1
+    torch.manual_seed(0)
+    dy = torch.randn(T, o, device="cuda").to(dt)
+    x = torch.randn(T, i, device="cuda").to(dt)
+    dw = fd._wgrad(dy, x, wdt)
+    assert dw.dtype == wdt and dw.shape == (o, i)
+    ref = dy.double().t() @ x.double()
+    err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < (8e-3 if wdt != torch.float32 else 1e-5), err
