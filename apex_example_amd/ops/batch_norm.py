@@ -163,6 +163,17 @@ class BatchNormFunction(torch.autograd.Function):
                     dz = dz.view(ctx.orig_shape)
             return (dx, dz if ctx.has_z else None, gw if need_w else None,
                     gb if need_w else None, None, None, None, None, None, None, None, None)
+        if ctx.world == 1 and xl.is_cuda:
+            # one persistent launch (reduce + dgamma/dbeta + dx) where the activation fits
+            # the register file, else reduce + elementwise (csrc/hip/bn_persist.hip)
+            dx, dz, gw, gb = C.backward_local(dyl, xl, mean, invstd, weight, bias, zl,
+                                              ctx.fuse_relu, need_w, ctx.has_z, mask=mask)
+            if ctx.shape_channel_last:
+                dx = dx.view(ctx.orig_shape)
+                if dz is not None:
+                    dz = dz.view(ctx.orig_shape)
+            return (dx, dz if ctx.has_z else None, gw if need_w else None,
+                    gb if need_w else None, None, None, None, None, None, None, None, None)
         sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
                                                    ctx.fuse_relu, need_w, mask=mask)
         if ctx.world > 1:

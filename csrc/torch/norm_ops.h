@@ -69,4 +69,10 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
                                                         OptT z, bool relu, bool want_dz,
                                                         OptT mask);
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+    OptT z, bool relu, bool need_wgrad, bool want_dz, OptT mask);
+int bn_persist_error_op();
+void bn_persist_reset_op();
+
 }  // namespace amd

@@ -127,6 +127,53 @@ def bench_bn_u(args):
         "%.0f / %.0f" % tuple(tot[v]) for v in variants) + " |")
 
 
+def bench_bn_persist(args):
+    """A/B of the one-launch persistent BatchNorm (bn_persist.hip) against the split
+    kernels, per ResNet-50 shape: forward_local + backward_local for the BN+ReLU
+    variant (bn1/bn2) and the BN+residual+ReLU+mask variant (bn3), in us."""
+    from apex_example_amd import _native
+
+    C_ = _native.require().bn
+    dev = "cuda"
+    modes = (0, 1, 2)  # split kernels / persistent / persistent without barrier fences
+    shapes = R50_BN if not args.quick else {k: v for k, v in R50_BN.items() if k[2] <= 14}
+    print("modes per cell: split / persistent / persistent without fences (us)")
+    print("| shape | count | fwd relu | bwd relu | fwd z+mask | bwd mask |")
+    print("|---|---|---|---|---|---|")
+    tot = [0.0, 0.0]
+    for (n, c, h, w), cnt in shapes.items():
+        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        dy, z = torch.randn_like(x), torch.randn_like(x)
+        wt, bs = torch.ones(c, device=dev), torch.zeros(c, device=dev)
+        rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
+        row = []
+        for variant in ("relu", "mask"):
+            zz = z if variant == "mask" else None
+            for phase in ("fwd", "bwd"):
+                ts = []
+                for on in modes:
+                    C_.persist_enable(on)
+                    y, mean, invstd, mask = C_.forward_local(x, wt, bs, rm, rv, None, 1e-5, 0.1,
+                                                             zz, True, variant == "mask")
+                    if phase == "fwd":
+                        fn = lambda: C_.forward_local(x, wt, bs, rm, rv, None, 1e-5, 0.1, zz,
+                                                      True, variant == "mask")
+                    else:
+                        fn = lambda: C_.backward_local(dy, x, mean, invstd, wt, bs, None, True,
+                                                       True, variant == "mask", mask=mask)
+                    ts.append(timeit(fn))
+                row.append(" / ".join("%.0f" % t for t in ts))
+                w8 = cnt if variant == "relu" else 0
+                tot[0] += w8 * ts[0]
+                tot[1] += w8 * min(ts[1:])
+        C_.persist_enable(1)
+        print("| %s | %d | %s |" % ((n, c, h, w), cnt, " | ".join(row)), flush=True)
+    print("R50-weighted BN+ReLU fwd+bwd (count x relu variant): split %.0f us, best persistent %.0f us"
+          % tuple(tot))
+    print("persist barrier error word:", C_.persist_error())
+
+
 def bench_bn_eu(args):
     """Elementwise BN passes (apply_k with residual + ReLU, backward_k) per shape over
     rows-in-flight U (APEX_AMD_BN_EU) x rows per thread (elem_rpt): per-shape us, the
@@ -777,12 +824,13 @@ def bench_lamb(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
+    ap.add_argument("--quick", action="store_true", help="bn-persist: 14x14 / 7x7 shapes only")
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
+    {"bn": bench_bn, "bn-persist": bench_bn_persist, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
