@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.embedding import Embedding
 from .. import _native
 from ..normalization import FusedLayerNorm, fused_add_dropout_layer_norm
 from ..fused_dense import (fused_dense_function, fused_dense_gelu_dense_skip_function,
@@ -56,9 +57,9 @@ def _ln(cfg, n):
 class BertEmbeddings(nn.Module):
     def __init__(self, cfg):
         super().__init__()
-        self.word_embeddings = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
-        self.position_embeddings = nn.Embedding(cfg.max_position_embeddings, cfg.hidden_size)
-        self.token_type_embeddings = nn.Embedding(cfg.type_vocab_size, cfg.hidden_size)
+        self.word_embeddings = Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.position_embeddings = Embedding(cfg.max_position_embeddings, cfg.hidden_size)
+        self.token_type_embeddings = Embedding(cfg.type_vocab_size, cfg.hidden_size)
         self.LayerNorm = _ln(cfg, cfg.hidden_size)
         self.dropout = nn.Dropout(cfg.hidden_dropout_prob)
 

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.embedding import Embedding
 from .. import _native
 from ..normalization import FusedLayerNorm, fused_add_dropout_layer_norm
 from ..fused_dense import cast_params_once, fused_dense_function, fused_dense_gelu_dense_function
@@ -121,8 +122,8 @@ class GPT2LMHeadModel(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
         self.config = cfg
-        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
-        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.wte = Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wpe = Embedding(cfg.n_positions, cfg.n_embd)
         self.drop = nn.Dropout(cfg.embd_pdrop)
         self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = _ln(cfg, cfg.n_embd)

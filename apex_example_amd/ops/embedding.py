@@ -1,0 +1,59 @@
+"""Embedding lookup whose backward never synchronises the host.
+
+PyTorch's CUDA embedding backward sorts the indices and, for more than 3,072 of
+them, reads the number of unique segments back to the host (``.item()``) before it
+can size the segment reduction.  That read sits at the very end of a transformer's
+backward (the embedding is the first layer), so every step the GPU queue drains
+there and the host-side launch work of the optimizer step and the next forward
+then runs against an idle GPU: BERT-large showed 4.6 ms of idle GPU time per 51 ms
+step in its kernel trace, clustered around the optimizer (``tools/rocprof_summary.py
+--gaps``, docs/PERF.md).
+
+Here the weight gradient is one fp32 scatter-add of the output-gradient rows into a
+zeroed [vocab, hidden] buffer (``index_add_``: device atomics, no host round trip),
+cast to the weight dtype.  Forward is the regular gather.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+# APEX_AMD_SYNCFREE_EMB=0: the stock embedding backward (A/B runs)
+_ENABLED = os.environ.get("APEX_AMD_SYNCFREE_EMB", "1") == "1"
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, weight, padding_idx):
+        ctx.save_for_backward(idx)
+        ctx.shape = weight.shape
+        ctx.wdtype = weight.dtype
+        ctx.padding_idx = padding_idx
+        return F.embedding(idx, weight, padding_idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        V, H = ctx.shape
+        flat = idx.reshape(-1)
+        g = torch.zeros((V, H), dtype=torch.float32, device=dy.device)
+        g.index_add_(0, flat, dy.reshape(-1, H).float())
+        if ctx.padding_idx is not None:
+            g[ctx.padding_idx].zero_()
+        return None, g.to(ctx.wdtype), None
+
+
+class Embedding(nn.Embedding):
+    """``nn.Embedding`` with a host-sync-free backward on the GPU (dense gradients,
+    no ``max_norm`` / ``scale_grad_by_freq`` / sparse: those fall back to the stock
+    op)."""
+
+    def forward(self, idx):
+        if (_ENABLED and idx.is_cuda and not self.sparse and self.max_norm is None
+                and not self.scale_grad_by_freq and torch.is_grad_enabled()
+                and self.weight.requires_grad):
+            return _EmbeddingFn.apply(idx, self.weight, self.padding_idx)
+        return super().forward(idx)

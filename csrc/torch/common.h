@@ -53,14 +53,17 @@ inline int* opt_iptr(const c10::optional<at::Tensor>& t) {
 
 using TensorLists = std::vector<std::vector<at::Tensor>>;
 
-// Validates `lists` and returns the (cached) device launch table.
+// Validates `lists` and returns the device launch table: a cached one, or one
+// whose chunk list is cached by tensor sizes and whose tensor table is uploaded
+// for this call (mt_plan.cpp).  Hold the returned plan until the launch is issued.
 struct MTPlan {
-  at::Tensor table;  // device bytes (kept alive by the cache)
+  at::Tensor table;  // device bytes (kept alive by the cache, or by this plan)
   at::Tensor host;   // pinned source image (kept alive: graph-captured copies re-read it)
+  at::Tensor chunks; // per-call plans: the size-keyed chunk table they point into
   bool captured = false;  // built inside a graph capture: never evicted
   MTLaunch L;
 };
-const MTPlan& mt_plan(const TensorLists& lists);
+MTPlan mt_plan(const TensorLists& lists);
 
 // Shared validation: every list has the same length, matching numel per slot,
 // contiguous tensors.  Returns true if the lists live on the GPU.

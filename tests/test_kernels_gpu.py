@@ -36,9 +36,9 @@ SIZES = [1, 7, 8, 63, 64, 1000, 8191, 8192, 8193, 65536 * 2 + 5, 333333]
 
 
 def test_mt_plan_cache_eviction():
-    """More distinct tensor sets than the 512-entry launch-plan cache holds: the
-    LRU eviction path (stream-recorded table release) runs on the device and
-    every launch stays correct."""
+    """More distinct tensor sets (and sizes) than the launch-plan caches hold: the
+    per-call tables (size-keyed chunk cache overflow, pinned staging ring wrap) and
+    every launch stay correct."""
     mt = C().mt
     mt.plan_cache_clear()
     noop = torch.zeros(1, dtype=torch.int32, device=DEV)
@@ -52,6 +52,36 @@ def test_mt_plan_cache_eviction():
     torch.cuda.synchronize()
     assert torch.equal(y, x * 0.5)
     assert mt.plan_cache_size() <= 512
+    mt.plan_cache_clear()
+
+
+def test_mt_plan_changing_addresses_and_repeats():
+    """Gradient-like lists whose addresses change every call never enter the
+    address cache (no growth), a list seen twice is cached, and results stay exact
+    across hundreds of per-call tables (staging ring reuse)."""
+    mt = C().mt
+    mt.plan_cache_clear()
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    sizes = [1000, 8193, 65536 * 3 + 1, 17]
+    keep = []
+    for k in range(300):
+        xs = [torch.full((n,), float(k % 13), device=DEV) for n in sizes]
+        ys = [torch.empty_like(x) for x in xs]
+        keep.append((xs, ys))  # all alive (~500 MB): every call has new addresses
+        mt.scale(noop, [xs, ys], 2.0)
+    torch.cuda.synchronize()
+    for xs, ys in keep:
+        for x, y in zip(xs, ys):
+            assert torch.equal(y, x * 2.0)
+    assert mt.plan_cache_size() == 0
+    xs = [torch.randn(n, device=DEV) for n in sizes]
+    ys = [torch.empty_like(x) for x in xs]
+    for _ in range(3):
+        mt.scale(noop, [xs, ys], 0.25)
+    torch.cuda.synchronize()
+    assert mt.plan_cache_size() == 1
+    for x, y in zip(xs, ys):
+        assert torch.equal(y, x * 0.25)
     mt.plan_cache_clear()
 
 

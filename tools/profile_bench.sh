@@ -13,4 +13,4 @@ rm -rf "/tmp/prof_$name"
 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "/tmp/prof_$name" -o run \
   -- python3 "$repo/bench.py" --steps "$steps" "$@" > "$repo/gpurun_out/prof_$name.log" 2>&1
 python3 "$repo/tools/rocprof_summary.py" "/tmp/prof_$name" --range timed_steps --steps "$steps" \
-  --top 45 --md "$repo/gpurun_out/prof_$name.md" --names-out "$repo/gpurun_out/prof_${name}_names.tsv"
+  --top 45 --gaps 25 --md "$repo/gpurun_out/prof_$name.md" --names-out "$repo/gpurun_out/prof_${name}_names.tsv"

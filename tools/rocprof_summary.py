@@ -62,8 +62,12 @@ def main(argv=None):
     ap.add_argument("--dispatch-out", default=None)
     ap.add_argument("--names-out", default=None,
                     help="write every kernel's FULL name with calls / total us (untruncated)")
+    ap.add_argument("--gaps", type=int, default=0,
+                    help="also list the N largest idle gaps (no kernel running) with the "
+                         "kernels on both sides, and the idle total per step")
     a = ap.parse_args(argv)
     disp = []
+    spans = []
 
     files = _find(a.root, "*kernel_trace.csv")
     if not files:
@@ -90,6 +94,8 @@ def main(argv=None):
                                  (e - s) / 1e3))
                 tot[name] += (e - s) / 1e3  # us
                 cnt[name] += 1
+                if a.gaps:
+                    spans.append((s, e, name))
                 t_min = s if t_min is None else min(t_min, s)
                 t_max = e if t_max is None else max(t_max, e)
     total = sum(tot.values())
@@ -107,6 +113,21 @@ def main(argv=None):
             "(busy %.1f%%)" % (len(tot), sum(cnt.values()), total, span,
                                100.0 * total / span if span else 0.0))
     out = head + "\n\n" + "\n".join(lines) + "\n"
+    if a.gaps and spans:
+        spans.sort()
+        gaps = []
+        end, prev = spans[0][1], spans[0][2]
+        for s0, e0, n0 in spans[1:]:
+            if s0 > end:
+                gaps.append(((s0 - end) / 1e3, prev, n0))
+            if e0 > end:
+                end, prev = e0, n0
+        idle = sum(g[0] for g in gaps)
+        out += "\nidle (no kernel running): %.1f us total%s, %d gaps; largest:\n\n" % (
+            idle / div if a.steps else idle, " per step" if a.steps else "", len(gaps))
+        out += "| gap us | after | before |\n|---|---|---|\n"
+        for g, p0, n0 in sorted(gaps, key=lambda t: -t[0])[: a.gaps]:
+            out += "| %.1f | `%s` | `%s` |\n" % (g, _short(p0, 70), _short(n0, 70))
     print(out)
     if a.md:
         with open(a.md, "w") as fh:
