@@ -12,6 +12,8 @@
 // Backward is a gather, not a scatter: a thread owns 8 channels of one INPUT
 // pixel and sums dy over the <= ceil(k/s)^2 output windows that cover it and
 // picked it, so there are no atomics and every dx element is written once.
+#include <cstdlib>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -151,6 +153,164 @@ __global__ void __launch_bounds__(kPoolThreads)
   }
 }
 
+// ResNet stem specialisation (3x3, stride 2, pad 1, 8 channels per lane): every
+// window tap (forward) / covering window (backward) is loaded up front with a
+// clamped address and a validity flag, so a lane has all 9 (resp. 4 + 4) 16-byte
+// loads in flight instead of a loop of dependent, branchy single loads.  Same tap
+// order, tie / NaN rule and summation order as the generic kernels above.
+typedef unsigned p_u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ void unpack8_any(const p_u32x4& u, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const t8 a = __builtin_bit_cast(t8, u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)a[i];
+  }
+}
+
+template <typename T, bool BN>
+__global__ void __launch_bounds__(kPoolThreads)
+    maxpool3s2_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int N,
+                     int H, int W, int C, int OH, int OW, PoolBN bn) {
+  static_assert(sizeof(T) == 2, "16-bit activations");
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * CV;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    int64_t pix = t / CV;
+    const int ow = (int)(pix % OW);
+    pix /= OW;
+    const int oh = (int)(pix % OH);
+    const int n = (int)(pix / OH);
+    const int h0 = oh * 2 - 1, w0 = ow * 2 - 1;
+    p_u32x4 raw[9];
+    unsigned okm = 0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int h = h0 + kh, w = w0 + kw;
+        const bool ok = h >= 0 && h < H && w >= 0 && w < W;
+        const int hc = ok ? h : 0, wc = ok ? w : 0;
+        okm |= (ok ? 1u : 0u) << (kh * 3 + kw);
+        raw[kh * 3 + kw] = *reinterpret_cast<const p_u32x4*>(
+            x + (((int64_t)n * H + hc) * W + wc) * C + cv * 8);
+      }
+    }
+    float sc[8], sh[8];
+    if constexpr (BN) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = cv * 8 + i;
+        sc[i] = bn.invstd[c] * (bn.w ? bn.w[c] : 1.f);
+        sh[i] = (bn.b ? bn.b[c] : 0.f) - bn.mean[c] * sc[i];
+      }
+    }
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      best[i] = -INFINITY;
+      arg[i] = 0;
+    }
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (!((okm >> tap) & 1u)) continue;
+      float v[8];
+      unpack8_any<T>(raw[tap], v);
+      if constexpr (BN) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = to_f32(from_f32<T>(fmaxf(fmaf(v[i], sc[i], sh[i]), 0.f)));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (v[i] > best[i] || (v[i] != v[i] && best[i] == best[i])) {
+          best[i] = v[i];
+          arg[i] = tap;
+        }
+      }
+    }
+    const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + cv * 8;
+    store8(y + o, best);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo |= (uint32_t)(arg[i] & 0xff) << (8 * i);
+      hi |= (uint32_t)(arg[i + 4] & 0xff) << (8 * i);
+    }
+    *reinterpret_cast<uint2*>(idx + o) = make_uint2(lo, hi);
+  }
+}
+
+// input row h is covered by output rows oh = h/2 (h even: tap row 1) or
+// oh = (h-1)/2 (tap row 2) and (h+1)/2 (tap row 0) for odd h
+template <typename T>
+__global__ void __launch_bounds__(kPoolThreads)
+    maxpool3s2_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx,
+                     int N, int H, int W, int C, int OH, int OW) {
+  static_assert(sizeof(T) == 2, "16-bit activations");
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * H * W * CV;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    int64_t pix = t / CV;
+    const int w = (int)(pix % W);
+    pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    int ohs[2], khs[2], ows[2], kws[2];
+    bool oho[2], owo[2];
+    if (h & 1) {
+      ohs[0] = (h - 1) >> 1; khs[0] = 2; ohs[1] = (h + 1) >> 1; khs[1] = 0;
+    } else {
+      ohs[0] = h >> 1; khs[0] = 1; ohs[1] = 0; khs[1] = -1;
+    }
+    if (w & 1) {
+      ows[0] = (w - 1) >> 1; kws[0] = 2; ows[1] = (w + 1) >> 1; kws[1] = 0;
+    } else {
+      ows[0] = w >> 1; kws[0] = 1; ows[1] = 0; kws[1] = -1;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      oho[a] = khs[a] >= 0 && ohs[a] < OH;
+      owo[a] = kws[a] >= 0 && ows[a] < OW;
+    }
+    p_u32x4 g[4];
+    uint2 ii[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const bool ok = oho[a] && owo[b];
+        const int64_t o = (((int64_t)n * OH + (ok ? ohs[a] : 0)) * OW + (ok ? ows[b] : 0)) * C + cv * 8;
+        g[a * 2 + b] = *reinterpret_cast<const p_u32x4*>(dy + o);
+        ii[a * 2 + b] = *reinterpret_cast<const uint2*>(idx + o);
+      }
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (!(oho[a] && owo[b])) continue;
+        const int tap = khs[a] * 3 + kws[b];
+        float gv[8];
+        unpack8_any<T>(g[a * 2 + b], gv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t word = i < 4 ? ii[a * 2 + b].x : ii[a * 2 + b].y;
+          if ((int)((word >> (8 * (i & 3))) & 0xff) == tap) acc[i] += gv[i];
+        }
+      }
+    store8(dx + (((int64_t)n * H + h) * W + w) * C + cv * 8, acc);
+  }
+}
+
 // global average pool backward, NHWC: dx[n, hw, c] = dy[n, c] * inv_hw.  dy is one
 // [C] row per image (L2-resident), dx is written once with 16-byte stores in memory
 // order - the gradient of x.mean((2, 3)) materialised channels-last directly, instead
@@ -186,6 +346,16 @@ void pool_dispatch(DType t, F&& f) {
   }
 }
 
+// the specialised 3x3 / stride-2 / pad-1 kernels (output size floor((H-1)/2)+1);
+// APEX_AMD_POOL_GENERIC=1 forces the generic kernels (A/B)
+bool stem_ok(int k, int s, int p, int H, int W, int OH, int OW) {
+  static const bool generic = [] {
+    const char* e = std::getenv("APEX_AMD_POOL_GENERIC");
+    return e && e[0] == '1';
+  }();
+  return !generic && k == 3 && s == 2 && p == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1;
+}
+
 int pool_grid(int64_t items) {
   int64_t b = (items + kPoolThreads - 1) / kPoolThreads;
   if (b > 16384) b = 16384;
@@ -208,6 +378,17 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
     const dim3 g(pool_grid(items)), b(kPoolThreads);
     const T* xp = static_cast<const T*>(x);
     T* yp = static_cast<T*>(y);
+    if constexpr (sizeof(T) == 2) {
+      if (vec && stem_ok(k, s, p, H, W, OH, OW)) {
+        if (with_bn)
+          hipLaunchKernelGGL((maxpool3s2_fwd_k<T, true>), g, b, 0, st, xp, yp, idx, N, H, W, C,
+                             OH, OW, bn);
+        else
+          hipLaunchKernelGGL((maxpool3s2_fwd_k<T, false>), g, b, 0, st, xp, yp, idx, N, H, W, C,
+                             OH, OW, bn);
+        return;
+      }
+    }
     if (vec && with_bn)
       hipLaunchKernelGGL((maxpool_fwd_k<T, true, true>), g, b, 0, st, xp, yp, idx, N, H, W, C,
                          OH, OW, k, s, p, bn);
@@ -231,6 +412,14 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
   if (items == 0) return;
   pool_dispatch(t, [&](auto t0) {
     using T = decltype(t0);
+    if constexpr (sizeof(T) == 2) {
+      if (vec && stem_ok(k, s, p, H, W, OH, OW)) {
+        hipLaunchKernelGGL((maxpool3s2_bwd_k<T>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
+                           st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C, OH,
+                           OW);
+        return;
+      }
+    }
     if (vec)
       hipLaunchKernelGGL((maxpool_bwd_k<T, true>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
                          st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C, OH,

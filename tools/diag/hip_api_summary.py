@@ -33,6 +33,39 @@ def main():
                 tot[n] += d
                 cnt[n] += 1
                 mx[n] = max(mx[n], d)
+    # idle gaps on the GPU: was the next kernel's launch call issued before the gap
+    # began (device-side wait) or during it (host lag)?
+    launches = {}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                cid = row.get("Correlation_Id")
+                if cid:
+                    launches[cid] = (int(row["Start_Timestamp"]), row.get("Function", "?"))
+    kern = []
+    for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                s0 = int(row["Start_Timestamp"])
+                if ranges and not any(r0 <= s0 <= r1 for r0, r1 in ranges):
+                    continue
+                kern.append((s0, int(row["End_Timestamp"]), row.get("Kernel_Name", "?")[:60],
+                             row.get("Correlation_Id")))
+    kern.sort()
+    gaps = []
+    end = kern[0][1] if kern else 0
+    for i in range(1, len(kern)):
+        s0, e0, n0, cid = kern[i]
+        if s0 - end > 50_000:
+            call = launches.get(cid)
+            lag = (call[0] - end) / 1e3 if call else float("nan")
+            gaps.append(((s0 - end) / 1e3, lag, kern[i - 1][2], n0))
+        end = max(end, e0)
+    print("| gap us | launch call after gap start (us; >0 = host lag) | after | before |")
+    print("|---|---|---|---|")
+    for g in sorted(gaps, key=lambda t: -t[0])[:20]:
+        print("| %.1f | %.1f | `%s` | `%s` |" % g)
+    print()
     print("| HIP API | calls | total us | max us |")
     print("|---|---|---|---|")
     for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:25]:
