@@ -712,21 +712,23 @@ __global__ void __launch_bounds__(256)
   dw[((int64_t)co * taps + tap) * Cin + ci] = from_f32<TO>(sum);
 }
 
-// W'[ci][8-t][co] = W[co][t][ci]: the 180-degree-rotated, in/out-swapped 3x3
-// filter of the data gradient, as a 64x64 LDS-tiled transpose per tap
+// W'[ci][T-1-t][co] = W[co][t][ci]: the 180-degree-rotated, in/out-swapped 3x3
+// filter of the data gradient (T = 9), or the plain transpose W^T of a 1x1 filter
+// (T = 1), as a 64x64 LDS-tiled transpose per tap
 __global__ void __launch_bounds__(256)
-    rot_weight_k(const uint16_t* __restrict__ w, uint16_t* __restrict__ out, int Cout, int Cin) {
+    rot_weight_k(const uint16_t* __restrict__ w, uint16_t* __restrict__ out, int Cout, int Cin,
+                 int T) {
   __shared__ uint16_t tile[64][66];
   const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64, t = blockIdx.z;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
   for (int r = ty; r < 64; r += 4) {
     const int co = co0 + r, ci = ci0 + tx;
-    tile[r][tx] = (co < Cout && ci < Cin) ? w[((int64_t)co * 9 + t) * Cin + ci] : 0;
+    tile[r][tx] = (co < Cout && ci < Cin) ? w[((int64_t)co * T + t) * Cin + ci] : 0;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
     const int ci = ci0 + r, co = co0 + tx;
-    if (ci < Cin && co < Cout) out[((int64_t)ci * 9 + (8 - t)) * Cout + co] = tile[tx][r];
+    if (ci < Cin && co < Cout) out[((int64_t)ci * T + (T - 1 - t)) * Cout + co] = tile[tx][r];
   }
 }
 
@@ -870,7 +872,12 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
 
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st) {
   hipLaunchKernelGGL(rot_weight_k, dim3((Cout + 63) / 64, (Cin + 63) / 64, 9), dim3(256), 0, st,
-                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin);
+                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin, 9);
+}
+
+void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st) {
+  hipLaunchKernelGGL(rot_weight_k, dim3((Cout + 63) / 64, (Cin + 63) / 64, 1), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin, 1);
 }
 
 void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,

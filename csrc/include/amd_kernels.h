@@ -263,6 +263,8 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
                    bool out_fp32, hipStream_t st);
 // 16-bit W'[ci][2-r][2-s][co] = W[co][r][s][ci] (data-gradient filter)
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
+// W^T ([Cin][Cout]) of a 16-bit 1x1 filter [Cout][Cin] (LDS-tiled transpose)
+void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
 void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32, int N,
                      int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
                      hipStream_t st);

@@ -218,4 +218,15 @@ at::Tensor conv3x3_rot_weight_op(at::Tensor w) {
   return out;
 }
 
+at::Tensor conv1x1_transpose_weight_op(at::Tensor w) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 &&
+                  w.element_size() == 2, "transpose_weight: 16-bit [Cout, Cin, 1, 1] expected");
+  w = w.contiguous();
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  at::Tensor out = at::empty({Cin, Cout, 1, 1}, w.options());
+  conv1x1_transpose_weight(w.data_ptr(), out.data_ptr(), (int)Cout, (int)Cin, cur_stream());
+  return out;
+}
+
 }  // namespace amd

@@ -27,5 +27,6 @@ at::Tensor stem_pad_op(at::Tensor x);
 at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk);
 at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy);
 at::Tensor conv3x3_rot_weight_op(at::Tensor w);
+at::Tensor conv1x1_transpose_weight_op(at::Tensor w);
 
 }  // namespace amd

@@ -55,6 +55,14 @@ def test_mt_plan_cache_eviction():
     mt.plan_cache_clear()
 
 
+@pytest.mark.parametrize("co,ci", [(64, 256), (2048, 512), (72, 40), (1, 8)])
+def test_conv1x1_transpose_weight(co, ci):
+    w = torch.randn(co, ci, 1, 1, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    t = C().conv.transpose_weight(w)
+    assert t.shape == (ci, co, 1, 1) and t.is_contiguous()
+    assert torch.equal(t, w.reshape(co, ci).t().contiguous().view(ci, co, 1, 1))
+
+
 def test_mt_plan_changing_addresses_and_repeats():
     """Gradient-like lists whose addresses change every call never enter the
     address cache (no growth), a list seen twice is cached, and results stay exact
