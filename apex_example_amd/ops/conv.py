@@ -81,6 +81,9 @@ def _transpose_1x1(weight):
     weights (ATen's strided copy took ~17 us per ResNet-50 weight, 14 per step)."""
     co, ci = weight.shape[0], weight.shape[1]
     if weight.is_cuda and weight.element_size() == 2 and _native.available():
+        got = _prepared(weight)
+        if got is not None:
+            return got
         return _native.require().conv.transpose_weight(weight)
     return weight.reshape(co, ci).t().contiguous().view(ci, co, 1, 1)
 
@@ -104,6 +107,10 @@ class Conv1x1GemmFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
         ctx.save_for_backward(x, weight)
+        n, ci, h, w = x.shape
+        if ctx.needs_input_grad[0] and _own_1x1(x.dtype, weight.shape[0], ci, n * h * w) \
+                and weight.dtype == torch.bfloat16:
+            _register_prep(weight)  # its dgrad runs on the own kernel with W^T
         return _conv1x1_fwd(x, weight)
 
     @staticmethod
@@ -167,6 +174,8 @@ class Conv1x1Stride2Function(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
         ctx.save_for_backward(x, weight)
+        if ctx.needs_input_grad[0]:
+            _register_prep(weight)
         return _native.require().conv.conv_fwd(x, weight, 2)
 
     @staticmethod
@@ -230,8 +239,46 @@ def _rot_weight(weight):
     """W'[ci, co, r, s] = W[co, ci, 2-r, 2-s]: the data gradient of a 3x3 stride-1
     pad-1 conv is the same conv applied to dY with W' (one tiled-transpose kernel)."""
     if _USE_ROT_KERNEL and weight.is_cuda and weight.element_size() == 2:
+        got = _prepared(weight)
+        if got is not None:
+            return got
         return _native.require().conv.rot_weight(weight)
     return weight.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
+# Backward weight layouts (rotated 3x3 filters, transposed 1x1 filters) of every conv
+# whose data gradient runs on the own kernels, made in ONE launch per backward pass
+# (conv.prep_weights) instead of one ~10 us launch per filter (27 per ResNet-50 step).
+# Forward registers the filter; the first backward request prepares every registered
+# filter; the next forward of a filter drops its prepared copy (the optimizer may
+# have rewritten the weights in place since).  APEX_AMD_PREP_WEIGHTS=0 disables.
+_USE_PREP = os.environ.get("APEX_AMD_PREP_WEIGHTS", "1") == "1"
+_PREP_PENDING = {}   # id(weight) -> weight
+_PREP_READY = {}     # id(weight) -> (weight, prepared layout)
+
+
+def _register_prep(weight):
+    if not (_USE_PREP and weight.is_cuda and weight.element_size() == 2):
+        return
+    k = id(weight)
+    _PREP_READY.pop(k, None)
+    _PREP_PENDING[k] = weight
+
+
+def _prepared(weight):
+    k = id(weight)
+    ent = _PREP_READY.get(k)
+    if ent is not None and ent[0] is weight:
+        return ent[1]
+    if k not in _PREP_PENDING:
+        return None
+    ws = list(_PREP_PENDING.values())
+    _PREP_PENDING.clear()
+    _PREP_READY.clear()  # only the latest batch is kept (bounded memory)
+    outs = _native.require().conv.prep_weights(ws)
+    for w, o in zip(ws, outs):
+        _PREP_READY[id(w)] = (w, o)
+    return _PREP_READY[k][1]
 
 
 class Conv3x3Function(torch.autograd.Function):
@@ -245,6 +292,8 @@ class Conv3x3Function(torch.autograd.Function):
     def forward(ctx, x, weight, stride):
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
+        if ctx.needs_input_grad[0] and _USE_ROT_KERNEL:
+            _register_prep(weight)
         return _native.require().conv.conv_fwd(x, weight, stride)
 
     @staticmethod

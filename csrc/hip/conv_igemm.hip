@@ -732,6 +732,42 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Every backward-pass weight layout of a model in ONE launch: the descriptors of up to
+// kPrepMax filters travel in the kernel arguments; workgroup b finds its filter by the
+// running tile offsets and does one 64x64 tap tile of rot_weight_k's transpose.
+constexpr int kPrepMax = 48;
+struct PrepDesc {
+  const uint16_t* w;
+  uint16_t* out;
+  int Cout, Cin, T, tile0;
+};
+struct PrepArgs {
+  int n, pad;
+  PrepDesc d[kPrepMax];
+};
+
+__global__ void __launch_bounds__(256) prep_weights_k(PrepArgs a) {
+  __shared__ uint16_t tile[64][66];
+  int i = 0;
+  while (i + 1 < a.n && (int)blockIdx.x >= a.d[i + 1].tile0) ++i;
+  const PrepDesc d = a.d[i];
+  const int local = (int)blockIdx.x - d.tile0;
+  const int cot_n = (d.Cout + 63) / 64, cit_n = (d.Cin + 63) / 64;
+  const int t = local / (cot_n * cit_n), rem = local - t * cot_n * cit_n;
+  const int co0 = (rem / cit_n) * 64, ci0 = (rem % cit_n) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int co = co0 + r, ci = ci0 + tx;
+    tile[r][tx] = (co < d.Cout && ci < d.Cin) ? d.w[((int64_t)co * d.T + t) * d.Cin + ci] : 0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < d.Cin && co < d.Cout)
+      d.out[((int64_t)ci * d.T + (d.T - 1 - t)) * d.Cout + co] = tile[tx][r];
+  }
+}
+
 // per-tap kernel tiling: 128 x 128 when both channel counts allow it, else 64 x 64
 // (algo 2/3: tuning variants - deeper DMA ring with a shorter or equal K-tile)
 struct WgTapCfg {
@@ -873,6 +909,23 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st) {
   hipLaunchKernelGGL(rot_weight_k, dim3((Cout + 63) / 64, (Cin + 63) / 64, 9), dim3(256), 0, st,
                      static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin, 9);
+}
+
+void prep_weights(const void* const* w, void* const* out, const int* cout, const int* cin,
+                  const int* taps, int n, hipStream_t st) {
+  for (int b = 0; b < n; b += kPrepMax) {
+    PrepArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.n = n - b < kPrepMax ? n - b : kPrepMax;
+    int tiles = 0;
+    for (int i = 0; i < a.n; ++i) {
+      const int k = b + i;
+      a.d[i] = PrepDesc{static_cast<const uint16_t*>(w[k]), static_cast<uint16_t*>(out[k]),
+                        cout[k], cin[k], taps[k], tiles};
+      tiles += ((cout[k] + 63) / 64) * ((cin[k] + 63) / 64) * taps[k];
+    }
+    if (tiles > 0) hipLaunchKernelGGL(prep_weights_k, dim3(tiles), dim3(256), 0, st, a);
+  }
 }
 
 void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st) {

@@ -265,6 +265,10 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
 // W^T ([Cin][Cout]) of a 16-bit 1x1 filter [Cout][Cin] (LDS-tiled transpose)
 void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
+// batched backward weight layouts in one launch: filter k [cout][taps][cin] (16-bit) ->
+// out[cin][taps-1-t][cout] (taps 9: the rotated 3x3 filter; taps 1: W^T)
+void prep_weights(const void* const* w, void* const* out, const int* cout, const int* cin,
+                  const int* taps, int n, hipStream_t st);
 void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32, int N,
                      int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
                      hipStream_t st);

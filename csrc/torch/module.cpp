@@ -112,6 +112,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("stem_wgrad", &stem_wgrad_op);
   conv.def("rot_weight", &conv3x3_rot_weight_op);
   conv.def("transpose_weight", &conv1x1_transpose_weight_op);
+  conv.def("prep_weights", &conv_prep_weights_op);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);

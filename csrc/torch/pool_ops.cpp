@@ -229,4 +229,32 @@ at::Tensor conv1x1_transpose_weight_op(at::Tensor w) {
   return out;
 }
 
+std::vector<at::Tensor> conv_prep_weights_op(std::vector<at::Tensor> ws) {
+  c10::NoGradGuard no_grad_;
+  std::vector<at::Tensor> outs;
+  std::vector<const void*> in;
+  std::vector<void*> out;
+  std::vector<int> co, ci, taps;
+  std::vector<at::Tensor> keep;
+  for (auto& w : ws) {
+    TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.element_size() == 2 &&
+                    ((w.size(2) == 3 && w.size(3) == 3) || (w.size(2) == 1 && w.size(3) == 1)),
+                "prep_weights: 16-bit [Cout, Cin, 3|1, 3|1] filters expected");
+    at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+    const int64_t Cout = w.size(0), Cin = w.size(1), k = w.size(2);
+    at::Tensor o = at::empty({Cin, Cout, k, k}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+    in.push_back(wc.data_ptr());
+    out.push_back(o.data_ptr());
+    co.push_back((int)Cout);
+    ci.push_back((int)Cin);
+    taps.push_back((int)(k * k));
+    keep.push_back(wc);
+    outs.push_back(o);
+  }
+  if (!outs.empty())
+    prep_weights(in.data(), out.data(), co.data(), ci.data(), taps.data(), (int)outs.size(),
+                 cur_stream());
+  return outs;
+}
+
 }  // namespace amd

@@ -28,5 +28,6 @@ at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk);
 at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy);
 at::Tensor conv3x3_rot_weight_op(at::Tensor w);
 at::Tensor conv1x1_transpose_weight_op(at::Tensor w);
+std::vector<at::Tensor> conv_prep_weights_op(std::vector<at::Tensor> ws);
 
 }  // namespace amd

@@ -63,6 +63,38 @@ def test_conv1x1_transpose_weight(co, ci):
     assert torch.equal(t, w.reshape(co, ci).t().contiguous().view(ci, co, 1, 1))
 
 
+def test_conv_prep_weights_batched_matches_single():
+    """One-launch backward weight layouts == the per-filter rotate / transpose."""
+    cv = C().conv
+    ws = [torch.randn(co, ci, k, k, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+          for co, ci, k in [(64, 64, 3), (256, 64, 1), (128, 128, 3), (2048, 512, 1), (72, 40, 1),
+                            (512, 512, 3)] * 9]  # 54 filters: two launches of <= 48
+    outs = cv.prep_weights(ws)
+    for w, o in zip(ws, outs):
+        ref = cv.rot_weight(w) if w.size(2) == 3 else cv.transpose_weight(w)
+        assert torch.equal(o, ref)
+
+
+def test_conv_prep_weights_refreshed_after_inplace_update():
+    """A filter rewritten between steps (as the optimizer does, behind autograd's
+    back) gets a fresh prepared layout at its next forward."""
+    from apex_example_amd.ops.conv import Conv2d3x3
+
+    torch.manual_seed(0)
+    conv = Conv2d3x3(64, 64).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 64, 8, 8, device=DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    for step in range(3):
+        x.grad = None
+        y = conv(x)
+        y.float().sum().backward()
+        ref = torch.nn.functional.conv_transpose2d(
+            torch.ones_like(y, dtype=torch.float32), conv.weight.float(), padding=1)
+        assert (x.grad.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item(), step
+        with torch.no_grad():
+            conv.weight.data.copy_(torch.randn_like(conv.weight))  # like an optimizer step
+
+
 def test_mt_plan_changing_addresses_and_repeats():
     """Gradient-like lists whose addresses change every call never enter the
     address cache (no growth), a list seen twice is cached, and results stay exact
