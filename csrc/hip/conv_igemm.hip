@@ -712,6 +712,37 @@ __global__ void __launch_bounds__(256)
   dw[((int64_t)co * taps + tap) * Cin + ci] = from_f32<TO>(sum);
 }
 
+// Single-pass form for <= kRedGroup splits: sum the S slabs of 4 consecutive ci and
+// write the final dtype / KRSC layout directly (no stage slab, one launch less).
+template <typename TO>
+__global__ void __launch_bounds__(256)
+    wgrad_reduce_one_k(const float4* __restrict__ part, int S, int64_t total4, int Cout, int Cin,
+                       int taps, TO* __restrict__ dw) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total4) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  int s = 0;
+  for (; s + 1 < S; s += 2) {
+    const float4 u = part[(int64_t)s * total4 + e], v = part[(int64_t)(s + 1) * total4 + e];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  }
+  if (s < S) {
+    const float4 u = part[(int64_t)s * total4 + e];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+  }
+  const int64_t el = e * 4;  // element index in [tap][co][ci]
+  const int ci = (int)(el % Cin);
+  const int64_t r = el / Cin;
+  const int co = (int)(r % Cout);
+  const int tap = (int)(r / Cout);
+  TO* o = dw + ((int64_t)co * taps + tap) * Cin + ci;
+  o[0] = from_f32<TO>(a.x + b.x);
+  o[1] = from_f32<TO>(a.y + b.y);
+  o[2] = from_f32<TO>(a.z + b.z);
+  o[3] = from_f32<TO>(a.w + b.w);
+}
+
 // W'[ci][T-1-t][co] = W[co][t][ci]: the 180-degree-rotated, in/out-swapped 3x3
 // filter of the data gradient (T = 9), or the plain transpose W^T of a 1x1 filter
 // (T = 1), as a 64x64 LDS-tiled transpose per tap
@@ -766,6 +797,15 @@ __global__ void __launch_bounds__(256) prep_weights_k(PrepArgs a) {
     if (ci < d.Cin && co < d.Cout)
       d.out[((int64_t)ci * d.T + (d.T - 1 - t)) * d.Cout + co] = tile[tx][r];
   }
+}
+
+// APEX_AMD_REDUCE_ONE=0: always the two-stage split-K reduction (A/B)
+bool single_pass_reduce() {
+  static const bool on = [] {
+    const char* e = std::getenv("APEX_AMD_REDUCE_ONE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // per-tap kernel tiling: 128 x 128 when both channel counts allow it, else 64 x 64
@@ -870,9 +910,22 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
 #undef WGT_LAUNCH
   }
   // two-stage reduction; `part` holds S partial slabs followed by ceil(S/16)
-  // stage-1 slabs (conv_wgrad_workspace)
+  // stage-1 slabs (conv_wgrad_workspace); one pass when S <= 16 (Cin % 4 == 0)
   const int64_t nout = (int64_t)T * Cout * Cin;
   const int Gn = (S + kRedGroup - 1) / kRedGroup;
+  if (Gn == 1 && Cin % 4 == 0 && single_pass_reduce()) {
+    const int64_t n4 = nout / 4;
+    const unsigned blocks = (unsigned)((n4 + 255) / 256);
+    if (dw_fp32)
+      hipLaunchKernelGGL((wgrad_reduce_one_k<float>), dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, T,
+                         static_cast<float*>(dw));
+    else
+      hipLaunchKernelGGL((wgrad_reduce_one_k<bf16_t>), dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, T,
+                         static_cast<bf16_t*>(dw));
+    return;
+  }
   float* stage = part + (int64_t)S * nout;
   const int64_t n4 = nout / 4;
   hipLaunchKernelGGL(wgrad_reduce1_k, dim3((unsigned)((n4 + 255) / 256), Gn), dim3(256), 0, st,
@@ -894,6 +947,19 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
                    bool out_fp32, hipStream_t st) {
   const int64_t n = (int64_t)Cout * Cin;
   const int Gn = (S + kRedGroup - 1) / kRedGroup;
+  if (Gn == 1 && Cin % 4 == 0 && single_pass_reduce()) {
+    const int64_t n4 = n / 4;
+    const unsigned blocks = (unsigned)((n4 + 255) / 256);
+    if (out_fp32)
+      hipLaunchKernelGGL((wgrad_reduce_one_k<float>), dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, 1,
+                         static_cast<float*>(out));
+    else
+      hipLaunchKernelGGL((wgrad_reduce_one_k<bf16_t>), dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, 1,
+                         static_cast<bf16_t*>(out));
+    return;
+  }
   const int64_t n4 = n / 4;
   hipLaunchKernelGGL(wgrad_reduce1_k, dim3((unsigned)((n4 + 255) / 256), Gn), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(part), S, n4, reinterpret_cast<float4*>(stage));

@@ -730,11 +730,12 @@ def test_rot_weight_and_splitk_reduce():
         memory_format=torch.channels_last)
     ref = w.flip(2, 3).transpose(0, 1)
     assert torch.equal(cv.rot_weight(w), ref)
-    part = torch.randn(37, 96, 40, device=DEV)
-    torch.testing.assert_close(cv.splitk_reduce(part, torch.float32), part.sum(0), rtol=1e-5,
-                               atol=1e-5)
-    torch.testing.assert_close(cv.splitk_reduce(part, torch.bfloat16).float(), part.sum(0),
-                               rtol=1e-2, atol=5e-2)
+    for S in (37, 11, 1):  # two-stage (> 16 slabs) and single-pass reductions
+        part = torch.randn(S, 96, 40, device=DEV)
+        torch.testing.assert_close(cv.splitk_reduce(part, torch.float32), part.sum(0),
+                                   rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(cv.splitk_reduce(part, torch.bfloat16).float(), part.sum(0),
+                                   rtol=1e-2, atol=5e-2)
 
 
 # ------------------------------------------------------------------ contrib xentropy
