@@ -25,6 +25,65 @@ import torch.nn.functional as F
 
 from .. import _native
 
+# Weight gradients on a side stream (APEX_AMD_WGRAD_STREAM=0 disables): the data
+# gradient stays on the critical path of the main stream while the weight gradient
+# (MFMA-bound) runs beside it and beside the following BatchNorm backward passes
+# (HBM-bound); the main stream joins the side stream once, at the end of the
+# backward pass (an autograd final callback).  Used only where nothing reads the
+# gradient on the main stream before that join: world size 1 (no DDP bucket hooks)
+# and the weight's .grad is None (AccumulateGrad then stores the tensor without a
+# kernel); never inside a graph capture.
+_USE_WSTREAM = os.environ.get("APEX_AMD_WGRAD_STREAM", "1") == "1"
+_SIDE = {}          # device index -> side stream
+_JOIN = {}          # device index -> main stream to join at the end of backward
+
+
+def _side_ok(weight):
+    if not (_USE_WSTREAM and weight.is_cuda and weight.grad is None):
+        return False
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return False
+    return True
+
+
+def _join_side():
+    for idx, main in list(_JOIN.items()):
+        main.wait_stream(_SIDE[idx])
+    _JOIN.clear()
+
+
+class _SideWgrad:
+    """Fork point taken BEFORE the data gradient is enqueued, so the weight gradient
+    launched afterwards on the side stream can overlap it."""
+
+    def __init__(self, weight):
+        self.on = _side_ok(weight)
+        if self.on:
+            dev = weight.device
+            self.main = torch.cuda.current_stream(dev)
+            self.side = _SIDE.get(dev.index)
+            if self.side is None:
+                self.side = _SIDE[dev.index] = torch.cuda.Stream(dev)
+            self.ev = self.main.record_event()
+
+    def run(self, fn, *used):
+        if not self.on:
+            return fn()
+        self.side.wait_event(self.ev)
+        with torch.cuda.stream(self.side):
+            dw = fn()
+        for t in used:
+            t.record_stream(self.side)
+        dw.record_stream(self.main)
+        idx = self.main.device.index
+        if idx not in _JOIN:
+            _JOIN[idx] = self.main
+            torch.autograd.Variable._execution_engine.queue_callback(_join_side)
+        return dw
+
 
 def _split_k(m):
     s = 1
@@ -118,10 +177,12 @@ class Conv1x1GemmFunction(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
+        side = _SideWgrad(weight) if ctx.needs_input_grad[1] else None
         if ctx.needs_input_grad[0]:
             dx = _conv1x1_dgrad(dy, weight, x.shape)
         if ctx.needs_input_grad[1]:
-            dw = wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype).view(weight.shape)
+            dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
+                          .view(weight.shape), dy, x)
         return dx, dw
 
 
@@ -146,6 +207,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         dx = dw = None
         if dy is not None:
             dy = dy.contiguous(memory_format=torch.channels_last)
+        side = _SideWgrad(weight) if (ctx.needs_input_grad[1] and dy is not None) else None
         if ctx.needs_input_grad[0]:
             if dy is None:
                 dx = dskip
@@ -160,7 +222,8 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                     dx2 = torch.mm(_as_rows(dy), w2)
                 dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and dy is not None:
-            dw = wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype).view(weight.shape)
+            dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
+                          .view(weight.shape), dy, x)
         return dx, dw
 
 
@@ -185,10 +248,11 @@ class Conv1x1Stride2Function(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         co, ci = weight.shape[0], weight.shape[1]
         dx = dw = None
+        side = _SideWgrad(weight) if ctx.needs_input_grad[1] else None
         if ctx.needs_input_grad[0]:
             dx = cv.conv_dgrad_s2(dy, _transpose_1x1(weight), x.size(2), x.size(3))
         if ctx.needs_input_grad[1]:
-            dw = cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1)
+            dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1), dy, x)
         return dx, dw
 
 
@@ -303,17 +367,20 @@ class Conv3x3Function(torch.autograd.Function):
         cv = _native.require().conv
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
+        n_pix = x.size(0) * x.size(2) * x.size(3)
+        own_wgrad = n_pix < (1 << 22) and (
+            _WGRAD3 == "tap" or (_WGRAD3 == "nine" and stride == 1 and x.size(3) <= 56))
+        side = _SideWgrad(weight) if (ctx.needs_input_grad[1] and own_wgrad) else None
         if ctx.needs_input_grad[0]:
             if stride == 1:
                 dx = cv.conv_fwd(dy, _rot_weight(weight), 1)
             else:
                 dx = cv.conv_dgrad_s2(dy, _rot_weight(weight), x.size(2), x.size(3))
         if ctx.needs_input_grad[1]:
-            n_pix = x.size(0) * x.size(2) * x.size(3)
             if _WGRAD3 == "tap" and n_pix < (1 << 22):
-                dw = cv.conv_wgrad(dy, x, weight.dtype, 0, stride)
+                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, stride), dy, x)
             elif _WGRAD3 == "nine" and stride == 1 and x.size(3) <= 56 and n_pix < (1 << 22):
-                dw = cv.conv_wgrad(dy, x, weight.dtype, 1, 1)
+                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 1, 1), dy, x)
             else:
                 dw = torch.ops.aten.convolution_backward(
                     dy, x, weight, None, (stride, stride), (1, 1), (1, 1), False, (0, 0), 1,

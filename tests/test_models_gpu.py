@@ -267,3 +267,26 @@ def test_dense_wgrad_splitk(dt, wdt, o, i):
     ref = dy.double().t() @ x.double()
     err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
     assert err < (8e-3 if wdt != torch.float32 else 1e-5), err
+
+
+def test_resnet50_bench_step_learns_with_tuned_gemms():
+    """The headline bench step (ResNet-50 O2 bf16, bs 256, committed TunableOp GEMM
+    selections) must train: no skipped (overflowed) steps and a falling loss on the
+    repeated synthetic batch.  Guards the tuned table: one hipBLASLt selection for the
+    64->256 1x1 conv at 56x56 returned non-finite outputs, which made every step
+    overflow and skip (loss flat at ~7.1) while throughput looked normal."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "4",
+                        "--warmup", "8", "--loss-trace"], capture_output=True, text=True,
+                       timeout=110, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    trace = rec["loss_trace"]
+    assert all(v == v for v in trace), trace
+    assert trace[-1] < trace[0] - 1.0, trace
+
