@@ -59,8 +59,8 @@ class _SideWgrad:
     """Fork point taken BEFORE the data gradient is enqueued, so the weight gradient
     launched afterwards on the side stream can overlap it."""
 
-    def __init__(self, weight):
-        self.on = _side_ok(weight)
+    def __init__(self, weight, *more, enable=True):
+        self.on = enable and _side_ok(weight) and all(m is None or m.grad is None for m in more)
         if self.on:
             dev = weight.device
             self.main = torch.cuda.current_stream(dev)
@@ -77,7 +77,9 @@ class _SideWgrad:
             dw = fn()
         for t in used:
             t.record_stream(self.side)
-        dw.record_stream(self.main)
+        for t in (dw if isinstance(dw, tuple) else (dw,)):
+            if t is not None:
+                t.record_stream(self.main)
         idx = self.main.device.index
         if idx not in _JOIN:
             _JOIN[idx] = self.main
