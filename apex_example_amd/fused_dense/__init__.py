@@ -196,11 +196,24 @@ def _dense_fwd(ctx, x, weight, bias):
     return y.view(*x.shape[:-1], weight.size(0))
 
 
-def _side_dense(w_dtype):
+# APEX_AMD_DENSE_SIDE: fp32 (default: fp32-weight layers only) | all | attn | ffn | none.
+# BERT-large O2 same box: fp32 (= none there) 664.5 / 666.5, attn 664.4 / 664.1,
+# ffn 645.4 / 644.7 seq/s - its bf16 weight-gradient GEMMs only contend with the
+# data-gradient chain.
+_DENSE_SIDE = os.environ.get("APEX_AMD_DENSE_SIDE", "fp32")
+
+
+def _side_dense(w_dtype, kind="attn"):
     """Dense weight gradients on the side stream (ops/conv.py _SideWgrad) only for fp32
     weights (amp O1: the fp32 weight-gradient GEMMs overlap the fp16 data-gradient
     chain): GPT-2-medium O1 239.5 / 239.9 k -> 246.5 / 249.0 k tok/s, while BERT-large
     O2 (bf16 weights) measured 666.6 / 666.7 -> 648.7 / 648.7 seq/s (same box)."""
+    if _DENSE_SIDE in ("attn", "ffn"):
+        return kind == _DENSE_SIDE
+    if _DENSE_SIDE == "all":
+        return True
+    if _DENSE_SIDE == "none":
+        return False
     return w_dtype == torch.float32
 
 
@@ -336,7 +349,7 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
     dw2 = db2 = None
     need_b2 = ctx.b2_dtype is not None and need[4]
     w1, b1, w2, b2 = ctx.params
-    side2 = _SideWgrad(w2, b2, enable=_side_dense(ctx.w_dtypes[1])) if need[3] else None
+    side2 = _SideWgrad(w2, b2, enable=_side_dense(ctx.w_dtypes[1], "ffn")) if need[3] else None
     if need[3] and need_b2:
         dw2, db2 = side2.run(lambda: _wgrad_bgrad(dy2, h, ctx.w_dtypes[1], ctx.b2_dtype), dy2, h)
     elif need[3]:
@@ -362,7 +375,7 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
                                      p, dh.to(p.dtype))
         dpre = g.to(dh.dtype)
         db1 = _bias_grad(dpre, ctx.b1_dtype or dh.dtype)
-    side1 = _SideWgrad(w1, enable=_side_dense(ctx.w_dtypes[0])) if need[1] else None
+    side1 = _SideWgrad(w1, enable=_side_dense(ctx.w_dtypes[0], "ffn")) if need[1] else None
     dx = _dgrad(dpre, w1c, xc.shape, dskip) if need[0] else None
     x2 = xc.reshape(-1, xc.size(-1))
     dw1 = side1.run(lambda: _wgrad(dpre, x2, ctx.w_dtypes[0]), dpre, xc) if need[1] else None
