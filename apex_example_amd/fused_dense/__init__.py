@@ -171,15 +171,24 @@ def _bias_grad(g2, dtype):
     return g2.to(torch.promote_types(g2.dtype, torch.float32)).sum(0).to(dtype)
 
 
-def _dgrad(g2, w, xshape, dskip):
+def _shares_storage(a, b):
+    return a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+
+
+def _dgrad(g2, w, xshape, dskip, dy=None):
     """dX = g2 @ W, accumulated IN PLACE into the residual-branch gradient ``dskip``
     (C += A @ B, hipBLASLt beta = 1) when the input also fed a residual: the sum
     autograd would otherwise launch over the input gradient disappears.  ``dskip``
-    is the fresh gradient buffer the residual consumer's backward produced."""
+    is the fresh gradient buffer the residual consumer's backward produced - except
+    when autograd hands this layer's own output gradient to both branches (an
+    unfused ``x + dense(x)``): then ``dskip`` IS ``dy``, which the weight gradient
+    (possibly on the side stream) still reads, so the sum is formed out of place."""
     if dskip is not None:
-        if dskip.dtype == g2.dtype and dskip.is_contiguous():
+        alias = _shares_storage(dskip, g2) or (dy is not None and _shares_storage(dskip, dy))
+        if dskip.dtype == g2.dtype and dskip.is_contiguous() and not alias:
             return dskip.view(-1, w.size(1)).addmm_(g2, w).view(xshape)
-        return (dskip.float() + (g2 @ w).view(xshape).float()).to(dskip.dtype)
+        acc = torch.promote_types(dskip.dtype, torch.float32)
+        return (dskip.to(acc) + (g2 @ w).view(xshape).to(acc)).to(dskip.dtype)
     return (g2 @ w).view(xshape)
 
 
@@ -229,7 +238,7 @@ def _dense_bwd(ctx, dy, dskip=None):
     side = _SideWgrad(*ctx.params, enable=_side_dense(ctx.w_dtype)) \
         if ctx.needs_input_grad[1] else None
     if ctx.needs_input_grad[0]:
-        dx = _dgrad(dy2, wc, xc.shape, dskip)
+        dx = _dgrad(dy2, wc, xc.shape, dskip, dy)
     x2 = xc.reshape(-1, xc.size(-1))
     if ctx.needs_input_grad[1] and need_b:
         dw, db = side.run(lambda: _wgrad_bgrad(dy2, x2, ctx.w_dtype, ctx.bias_dtype), dy2, xc)
@@ -376,7 +385,7 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
         dpre = g.to(dh.dtype)
         db1 = _bias_grad(dpre, ctx.b1_dtype or dh.dtype)
     side1 = _SideWgrad(w1, enable=_side_dense(ctx.w_dtypes[0], "ffn")) if need[1] else None
-    dx = _dgrad(dpre, w1c, xc.shape, dskip) if need[0] else None
+    dx = _dgrad(dpre, w1c, xc.shape, dskip, dy) if need[0] else None
     x2 = xc.reshape(-1, xc.size(-1))
     dw1 = side1.run(lambda: _wgrad(dpre, x2, ctx.w_dtypes[0]), dpre, xc) if need[1] else None
     if ctx.b1_dtype is None or not need[2]:

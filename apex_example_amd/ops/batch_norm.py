@@ -54,7 +54,7 @@ def _to_logical(x, shape_channel_last):
 class BatchNormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
-                fuse_relu, shape_channel_last, num_batches_tracked=None):
+                fuse_relu, shape_channel_last, num_batches_tracked=None, force_collectives=False):
         C = _C()
         orig_shape = x.shape
         xl = _to_logical(x, shape_channel_last)
@@ -62,10 +62,15 @@ class BatchNormFunction(torch.autograd.Function):
         count = xl.numel() // xl.size(1)
         if process_group is False or not (dist.is_available() and dist.is_initialized()):
             world = 1  # local statistics
+            force_collectives = False
         else:
             world = dist.get_world_size(process_group)
+        # force_collectives: take the cross-rank path (packed all_gather / all_reduce)
+        # even on a 1-rank group - the test / bench hook that runs SyncBN's RCCL code
+        # on a single GPU (DistributedDataParallel has the same switch)
+        collective = world > 1 or bool(force_collectives)
         want_mask = bool(fuse_relu) and zl is not None and xl.is_cuda
-        if world == 1 and xl.is_cuda:
+        if not collective and xl.is_cuda:
             # one stats launch + one finalize (mean, invstd, running stats and
             # num_batches_tracked in the same kernel) + one apply launch
             y, mean_g, invstd, mask = C.forward_local(xl, weight, bias, running_mean,
@@ -79,7 +84,7 @@ class BatchNormFunction(torch.autograd.Function):
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
                 shape_channel_last
             return y.view(orig_shape) if shape_channel_last else y
-        if world > 1 and xl.is_cuda:
+        if collective and xl.is_cuda:
             # SyncBN: the stats kernels write [mean | var | count] into one buffer -> ONE
             # all_gather -> one combine kernel (global mean / invstd, running stats,
             # num_batches_tracked, 1/global count) -> apply.  No host sync, no cat.
@@ -99,7 +104,7 @@ class BatchNormFunction(torch.autograd.Function):
                 y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
             ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd,
                                   mask)
-            ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = pg, world, \
+            ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = pg, max(world, 2), \
                 bool(fuse_relu), inv_total, count
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
                 shape_channel_last
@@ -107,7 +112,7 @@ class BatchNormFunction(torch.autograd.Function):
         if num_batches_tracked is not None:
             num_batches_tracked.add_(1)
         mean, var = C.local_stats(xl)
-        if world > 1:
+        if collective:
             pg = process_group if process_group is not None else dist.group.WORLD
             cnt = torch.full((1,), float(count), dtype=torch.float32, device=x.device)
             packed = torch.cat([mean, var, cnt])
@@ -130,7 +135,7 @@ class BatchNormFunction(torch.autograd.Function):
             y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
         ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd, mask)
         ctx.pg = pg
-        ctx.world = world
+        ctx.world = max(world, 2) if collective else world  # > 1: collective backward
         ctx.fuse_relu = bool(fuse_relu)
         ctx.total = total
         ctx.count = count
@@ -162,7 +167,7 @@ class BatchNormFunction(torch.autograd.Function):
                 if dz is not None:
                     dz = dz.view(ctx.orig_shape)
             return (dx, dz if ctx.has_z else None, gw if need_w else None,
-                    gb if need_w else None, None, None, None, None, None, None, None, None)
+                    gb if need_w else None, None, None, None, None, None, None, None, None, None)
         if ctx.world == 1 and xl.is_cuda:
             # one persistent launch (reduce + dgamma/dbeta + dx) where the activation fits
             # the register file, else reduce + elementwise (csrc/hip/bn_persist.hip)
@@ -173,7 +178,7 @@ class BatchNormFunction(torch.autograd.Function):
                 if dz is not None:
                     dz = dz.view(ctx.orig_shape)
             return (dx, dz if ctx.has_z else None, gw if need_w else None,
-                    gb if need_w else None, None, None, None, None, None, None, None, None)
+                    gb if need_w else None, None, None, None, None, None, None, None, None, None)
         sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
                                                    ctx.fuse_relu, need_w, mask=mask)
         if ctx.world > 1:
@@ -193,18 +198,18 @@ class BatchNormFunction(torch.autograd.Function):
             if dz is not None:
                 dz = dz.view(ctx.orig_shape)
         return (dx, dz if ctx.has_z else None, gw if need_w else None, gb if need_w else None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
                    z=None, fuse_relu=False, process_group=False, shape_channel_last=False,
-                   num_batches_tracked=None):
+                   num_batches_tracked=None, force_collectives=False):
     """Functional fused BN(+z)(+ReLU).  ``process_group=False`` -> local statistics.
     ``num_batches_tracked`` (int64 tensor) is incremented on the device."""
     if training:
         return BatchNormFunction.apply(x, z, weight, bias, running_mean, running_var, eps, momentum,
                                        process_group, fuse_relu, shape_channel_last,
-                                       num_batches_tracked)
+                                       num_batches_tracked, force_collectives)
     # inference: running statistics (autograd through plain torch ops)
     if shape_channel_last:
         xs = x.movedim(-1, 1)

@@ -18,6 +18,7 @@ per chunk.
 from __future__ import annotations
 
 import os
+import threading
 
 import torch
 import torch.nn as nn
@@ -35,7 +36,8 @@ from .. import _native
 # kernel); never inside a graph capture.
 _USE_WSTREAM = os.environ.get("APEX_AMD_WGRAD_STREAM", "1") == "1"
 _SIDE = {}          # device index -> side stream
-_JOIN = {}          # device index -> main stream to join at the end of backward
+_JOIN = {}          # device index -> (main stream to join, autograd graph task id)
+_LOCK = threading.Lock()
 
 
 def _side_ok(weight):
@@ -50,9 +52,18 @@ def _side_ok(weight):
 
 
 def _join_side():
-    for idx, main in list(_JOIN.items()):
+    with _LOCK:
+        pending = list(_JOIN.items())
+        _JOIN.clear()
+    for idx, (main, _task) in pending:
         main.wait_stream(_SIDE[idx])
-    _JOIN.clear()
+
+
+def join_side_streams():
+    """Make every main stream wait for the weight-gradient side stream now (also
+    what the end-of-backward callback does).  Idempotent; for code that reads a
+    weight gradient before its backward pass finished (e.g. after an exception)."""
+    _join_side()
 
 
 class _SideWgrad:
@@ -80,9 +91,17 @@ class _SideWgrad:
         for t in (dw if isinstance(dw, tuple) else (dw,)):
             if t is not None:
                 t.record_stream(self.main)
+        # one join per backward pass (graph task): a pass that raised before its final
+        # callbacks ran leaves a stale entry behind; the next pass sees another task id
+        # and queues its own callback, which joins everything pending
         idx = self.main.device.index
-        if idx not in _JOIN:
-            _JOIN[idx] = self.main
+        task = torch._C._current_graph_task_id()
+        with _LOCK:
+            ent = _JOIN.get(idx)
+            fresh = ent is None or ent[1] != task
+            if fresh:
+                _JOIN[idx] = (self.main, task)
+        if fresh:
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
         return dw
 

@@ -6,7 +6,8 @@ import torch.distributed as dist
 
 from .distributed import DistributedDataParallel, Reducer  # noqa: F401
 from .LARC import LARC  # noqa: F401
-from .sync_batchnorm import SyncBatchNorm, SyncBatchNormPython  # noqa: F401
+from .sync_batchnorm import (SyncBatchNorm, SyncBatchNormPython,  # noqa: F401
+                             set_syncbn_force_collectives)
 
 ReduceOp = dist.ReduceOp
 

@@ -195,10 +195,20 @@ class DistributedDataParallel(Module):
             self._bucket_pgs = list(allreduce_communicators[0] if isinstance(
                 allreduce_communicators, tuple) else allreduce_communicators)
             self.num_allreduce_streams = len(self._bucket_pgs)
+        elif process_group is not None:
+            # new_group() is a collective over the WHOLE world: with a caller-given
+            # subgroup only that subgroup's ranks construct this DDP (and disjoint
+            # subgroups would pass different rank lists), so no communicator is
+            # created here.  The buckets use the caller's group (round-robin over
+            # it when num_allreduce_streams > 1); pass allreduce_communicators=
+            # [...] built on every rank for dedicated / high-priority ones.
+            if num_allreduce_streams > 1:
+                self._bucket_pgs = [process_group] * num_allreduce_streams
+            self.high_priority_streams = False
         elif num_allreduce_streams > 1:
             self._bucket_pgs = [self._new_comm_group() for _ in range(num_allreduce_streams)]
         elif self.high_priority_streams and (self.world_size > 1 or self.force_collectives):
-            # every rank constructs DDP in the same order, so this collective
+            # the whole world constructs DDP in the same order, so this collective
             # group creation lines up across ranks
             self._comm_pg = self._new_comm_group()
 
@@ -207,16 +217,19 @@ class DistributedDataParallel(Module):
             for p in self.active_params:
                 assert p.is_cuda, "NCCL backend only supports model parameters to be on GPU."
 
-        # broadcast parameters from rank 0 (apex: buffers are NOT broadcast)
+        # broadcast parameters from the group's first rank (apex: rank 0; buffers are
+        # NOT broadcast).  dist.broadcast takes a GLOBAL source rank.
         if self.world_size > 1:
-            flat_dist_call([p.data for p in self.module.parameters()], dist.broadcast, (0,),
+            src = 0 if process_group is None else dist.get_process_group_ranks(process_group)[0]
+            flat_dist_call([p.data for p in self.module.parameters()], dist.broadcast, (src,),
                            group=process_group)
         self._build_reducer()
 
     # ------------------------------------------------------------------ internals
     def _new_comm_group(self):
-        ranks = (list(range(dist.get_world_size())) if self.process_group is None
-                 else dist.get_process_group_ranks(self.process_group))
+        """A communicator over the whole world (called only when process_group is
+        None, i.e. when every rank of the world constructs this DDP)."""
+        ranks = list(range(dist.get_world_size()))
         if self.backend == "nccl" and self.high_priority_streams:
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = True

@@ -61,19 +61,24 @@ class SyncBatchNorm(_BatchNorm):
     [N, H, W, C] tensor).  A PyTorch channels_last-format [N, C, H, W] tensor
     needs no flag - its memory layout is detected and the NHWC kernels run.
     ``fuse_relu=True`` applies ReLU after the (optional) residual ``z``.
+    ``force_collectives=True`` runs the cross-rank path (packed all_gather of the
+    statistics, packed all_reduce of the gradient sums) even when the group has
+    one rank: the 1-GPU test / bench hook for SyncBN's RCCL code
+    (``set_syncbn_force_collectives``).
     """
 
     warned = False
 
     def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True,
                  track_running_stats=True, process_group=None, channel_last=False,
-                 fuse_relu=False):
+                 fuse_relu=False, force_collectives=False):
         super(SyncBatchNorm, self).__init__(num_features, eps=eps, momentum=momentum,
                                             affine=affine,
                                             track_running_stats=track_running_stats)
         self.process_group = process_group
         self.channel_last = channel_last
         self.fuse_relu = fuse_relu
+        self.force_collectives = force_collectives
 
     def _specify_process_group(self, process_group):
         self.process_group = process_group
@@ -115,15 +120,27 @@ class SyncBatchNorm(_BatchNorm):
         if not _native.available():
             return _python_sync_bn(self, input, z, exponential_average_factor, channel_last)
         pg = self.process_group
+        force = bool(getattr(self, "force_collectives", False))
         if not (dist.is_available() and dist.is_initialized()):
             pg = False
-        elif pg is None and dist.get_world_size() > 1:
+        elif pg is None and (dist.get_world_size() > 1 or force):
             pg = syncbn_comm_group()
         return BatchNormFunction.apply(input, z, self.weight, self.bias,
                                        self.running_mean if self.track_running_stats else None,
                                        self.running_var if self.track_running_stats else None,
                                        self.eps, exponential_average_factor, pg, self.fuse_relu,
-                                       channel_last, nbt)
+                                       channel_last, nbt, force)
+
+
+def set_syncbn_force_collectives(module, on=True):
+    """Turn the 1-rank collective path of every SyncBatchNorm in ``module`` on/off;
+    returns the number of layers changed."""
+    n = 0
+    for m in module.modules():
+        if isinstance(m, SyncBatchNorm):
+            m.force_collectives = bool(on)
+            n += 1
+    return n
 
 
 class _PySyncBNFunction(torch.autograd.Function):

@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--loss-trace", action="store_true",
                     help="keep every step's loss (device scalars, read after timing) in the JSON")
+    ap.add_argument("--allow-skipped-steps", action="store_true",
+                    help="do not fail when the loss scaler skipped a timed step (fp16 runs "
+                         "whose dynamic scale is still settling)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + world-size check only (launcher tests)")
     return ap.parse_args()
@@ -521,6 +524,7 @@ def main():
         torch.cuda.synchronize()
 
     sync_all()
+    skipped_before = _skipped_steps(args)
     torch.cuda.nvtx.range_push("timed_steps")
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -535,6 +539,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item())
+    # outside the timed region: how many timed steps did the loss scaler skip?
+    # (a step whose grads overflowed trains nothing; the rate would be a lie)
+    skipped_after = _skipped_steps(args)
+    skipped = (skipped_after - skipped_before) if skipped_before is not None else None
+    if world > 1 and skipped is not None:
+        t = torch.tensor([skipped], dtype=torch.int64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        skipped = int(t.item())
+    scale_now = _loss_scale(args)
 
     # optimizer step alone (secondary metric of BASELINE.json)
     torch.cuda.synchronize()
@@ -578,6 +591,8 @@ def main():
         "optimizer_step_ms": round(opt_ms, 4),
         "optimizer_step_host_ms": round(opt_host_ms, 4),
         "final_loss": round(final_loss, 4),
+        "skipped_steps": skipped,
+        "loss_scale": scale_now,
         "launcher": os.environ.get("APEX_AMD_BENCH_LAUNCHER",
                                    "torchrun" if world > 1 else "single"),
     }
@@ -594,6 +609,31 @@ def main():
     if world > 1:
         barrier()
         dist.destroy_process_group()
+    if skipped and not args.allow_skipped_steps:
+        print("bench.py: %d of the %d timed steps were skipped by the loss scaler (gradient "
+              "overflow); the throughput above does not measure training steps" % (
+                  skipped, args.steps), file=sys.stderr)
+        sys.exit(4)
+
+
+def _amp_scalers(args):
+    if args.impl != "amd":
+        return []
+    from apex_example_amd.amp._amp_state import _amp_state
+    return list(getattr(_amp_state, "loss_scalers", None) or [])
+
+
+def _skipped_steps(args):
+    """Total skipped steps of every amp loss scaler (one device read; called
+    only outside the timed region).  None for the stock comparator."""
+    if args.impl == "amd":
+        return sum(sc.skipped_steps() for sc in _amp_scalers(args))
+    return None
+
+
+def _loss_scale(args):
+    sc = _amp_scalers(args)
+    return float(sc[0].loss_scale()) if sc else None
 
 
 if __name__ == "__main__":

@@ -80,6 +80,28 @@ def ddp_grads(rank, world, message_size=10_000_000, delay=False, predivide=1.0, 
     return out
 
 
+def ddp_subgroups(rank, world, streams=1, message_size=300):
+    """Two disjoint data-parallel subgroups {0,1} and {2,3}: every rank creates both
+    groups (in the same order), then only the members of a group construct the DDP
+    over it.  Each subgroup averages over its own 2 ranks' data."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    groups = [dist.new_group(ranks=[0, 1]), dist.new_group(ranks=[2, 3])]
+    mine = groups[rank // 2]
+    model = _mlp()
+    ddp = DistributedDataParallel(model, message_size=message_size, process_group=mine,
+                                  num_allreduce_streams=streams)
+    x, y = _data(16, seed=200 + rank // 2)   # subgroup-specific batch
+    xs, ys = x.chunk(2)[rank % 2], y.chunk(2)[rank % 2]
+    out = {}
+    for it in range(2):
+        for p in model.parameters():
+            p.grad = None if it == 0 else p.grad.zero_()
+        F.cross_entropy(ddp(xs), ys).backward()
+        out["grads%d" % it] = [p.grad.detach().clone() for p in model.parameters()]
+    return out
+
+
 def ddp_bf16_precision(rank, world, fp32=None, n=4096):
     """bf16 gradient buckets averaged over ``world`` ranks; returns the reduced
     bf16 gradient and the exact fp32 average of the per-rank bf16 gradients."""

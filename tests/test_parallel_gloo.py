@@ -40,6 +40,21 @@ def test_ddp_matches_full_batch(tmp_path, kw):
         assert len(res[0]["layout"]) == 6
 
 
+@pytest.mark.parametrize("streams", [1, 2])
+def test_ddp_disjoint_subgroups(tmp_path, streams):
+    """DDP over caller-given disjoint subgroups (and >1 allreduce streams) must not
+    create world-collective communicators from inside the subgroup."""
+    res = W.run("ddp_subgroups", 4, str(tmp_path), streams=streams)
+    for sg in range(2):
+        model = W._mlp()
+        x, y = W._data(16, seed=200 + sg)
+        F.cross_entropy(model(x), y).backward()
+        for r in (2 * sg, 2 * sg + 1):
+            for it in range(2):
+                for g, p in zip(res[r]["grads%d" % it], model.parameters()):
+                    torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-6)
+
+
 def test_ddp_sum_without_average(tmp_path):
     res = W.run("ddp_grads", 2, str(tmp_path), average=False)
     ref = _single_process_grads()
