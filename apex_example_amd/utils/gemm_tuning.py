@@ -87,3 +87,58 @@ def use_tuned_gemms(name: str) -> Optional[str]:
 def tuned_entries(path: str) -> int:
     with open(path, newline="") as f:
         return sum(1 for row in csv.reader(f) if row and row[0] != "Validator")
+
+
+# ---------------------------------------------------------------- per-entry validation
+# TunableOp picks the fastest solution of each key WITHOUT a numerical check (round 2
+# shipped one selection that returned non-finite values).  The helpers below rebuild the
+# exact GEMM a table row keys on, so every committed entry can be run against an fp64
+# reference (tools/diag/tuned_gemm_validate.py, tests/test_gemm_tuning_gpu.py).
+
+_DTYPES = {"BFloat16": torch.bfloat16, "Half": torch.float16, "Float": torch.float32}
+
+
+def table_rows(path: str):
+    """[(op_signature, params_signature, solution)] of the non-validator rows."""
+    with open(path, newline="") as f:
+        return [(r[0], r[1], r[2]) for r in csv.reader(f) if len(r) >= 3 and r[0] != "Validator"]
+
+
+def parse_key(op_sig: str, params_sig: str) -> dict:
+    """'GemmTunableOp_BFloat16_TN', 'tn_M_N_K_ld_lda_ldb_ldc' -> fields (BLAS column-major
+    convention: C[m x n] = op(A) op(B), op(A) m x k)."""
+    kind, dt, _ = op_sig.split("_", 2)
+    f = params_sig.split("_")
+    if len(f) != 8 or f[4] != "ld":
+        raise ValueError("unsupported TunableOp key %r" % params_sig)
+    return {"bias": kind == "GemmAndBiasTunableOp", "dtype": _DTYPES[dt],
+            "transa": f[0][0], "transb": f[0][1], "m": int(f[1]), "n": int(f[2]),
+            "k": int(f[3]), "lda": int(f[5]), "ldb": int(f[6]), "ldc": int(f[7])}
+
+
+def key_operands(key: dict, device, seed: int = 0):
+    """Row-major operands (P [n x k], Q [k x m], bias [m] or None) whose
+    ``torch.mm(P, Q)`` / ``torch.addmm(bias, P, Q)`` (result [n x m]) is exactly the
+    key's column-major GEMM: Q plays BLAS A (transa 'n': Q has row stride lda; 't':
+    Q = W.t() with W [m x k] of row stride lda), P plays BLAS B (transb 'n': row
+    stride ldb; 't': P = V.t() with V [k x n] of row stride ldb)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    dt = key["dtype"]
+    m, n, k = key["m"], key["n"], key["k"]
+
+    def rnd(rows, cols):
+        return torch.randn(rows, cols, generator=g, device=device, dtype=torch.float32).to(dt)
+
+    Q = rnd(k, key["lda"])[:, :m] if key["transa"] == "n" else rnd(m, key["lda"])[:, :k].t()
+    P = rnd(n, key["ldb"])[:, :k] if key["transb"] == "n" else rnd(k, key["ldb"])[:, :n].t()
+    bias = rnd(1, m)[0].contiguous() if key["bias"] else None
+    return P, Q, bias
+
+
+def run_key(P, Q, bias):
+    return torch.addmm(bias, P, Q) if bias is not None else torch.mm(P, Q)
+
+
+def reference_fp64(P, Q, bias):
+    out = P.double() @ Q.double()
+    return out + bias.double() if bias is not None else out

@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=15)
     ap.add_argument("--model", default="resnet50",
-                    choices=["resnet50", "resnet18", "bert_large", "gpt2_medium"])
+                    choices=["resnet50", "resnet18", "bert_large", "gpt2_medium", "convnet"])
     ap.add_argument("--batch-size", type=int, default=None, help="per GPU")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--seq-len", type=int, default=None)
@@ -76,6 +76,11 @@ def parse():
     ap.add_argument("--no-syncbn", action="store_true",
                     help="per-GPU BatchNorm statistics at N > 1 (not the BASELINE config)")
     ap.add_argument("--message-size", type=int, default=10_000_000, help="DDP bucket elements")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="1 GPU: run the N>1 code path anyway - apex DDP (+ SyncBN for ResNet) "
+                         "with every bucket all-reduce and SyncBN all_gather / all_reduce "
+                         "issued on a 1-rank RCCL communicator (the per-GPU cost of the "
+                         "multi-GPU step, measured on one GPU)")
     ap.add_argument("--materialize-master-grads", action="store_true")
     ap.add_argument("--no-gemm-1x1", action="store_true",
                     help="keep MIOpen for the stride-1 1x1 convs (default: hipBLASLt GEMM)")
@@ -85,6 +90,9 @@ def parse():
                     help="auto: library GEMMs use the TunableOp selections in tuning/<model>.csv "
                          "(read-only, validator-checked; tools/tune_gemms.sh makes them)")
     ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--convnet-optimizer", choices=["sgd", "fused"], default="sgd",
+                    help="convnet: torch.optim.SGD as the reference program uses, or FusedSGD "
+                         "(sync-free amp)")
     ap.add_argument("--deterministic", action="store_true")
     # MIOpen immediate mode measured as fast as exhaustive find for ResNet-50 on
     # MI355X (docs/PERF.md) and avoids ~200 s of solver search on a fresh box.
@@ -184,10 +192,14 @@ def build_resnet(args, device, world):
     gemm_1x1 = args.impl == "amd" and not args.no_gemm_1x1
     model = ctor(fused_bn=fused_bn, gemm_1x1=gemm_1x1).to(device)
     # BASELINE.json's multi-GPU ResNet-50 config is DDP + SyncBN: on by default at N > 1
-    args.syncbn = world > 1 and not args.no_syncbn
+    multi = world > 1 or args.force_collectives
+    args.syncbn = multi and not args.no_syncbn
     if args.syncbn:
         if args.impl == "amd":
             model = convert_syncbn_model(model)
+            if args.force_collectives:
+                from apex_example_amd.parallel import set_syncbn_force_collectives
+                set_syncbn_force_collectives(model, True)
         else:
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
     mf = torch.channels_last if not args.no_channels_last else torch.contiguous_format
@@ -200,8 +212,9 @@ def build_resnet(args, device, world):
                        materialize_master_grads=args.materialize_master_grads)
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half,
                                     verbosity=0)
-        if world > 1:
-            model = DistributedDataParallel(model, message_size=args.message_size)
+        if multi:
+            model = DistributedDataParallel(model, message_size=args.message_size,
+                                            force_collectives=args.force_collectives)
             w.ddp = model
 
         def step(b):
@@ -243,10 +256,79 @@ def build_resnet(args, device, world):
         "optimizer": "FusedSGD(momentum=0.9, wd=5e-5)" if args.impl == "amd"
                      else "torch.optim.SGD(fused)",
         "channels_last": not args.no_channels_last, "fused_bn": fused_bn,
-        "syncbn": bool(args.syncbn and world > 1),
-        "ddp_message_size": args.message_size if world > 1 else None,
+        "syncbn": bool(args.syncbn and multi),
+        "ddp_message_size": args.message_size if multi else None,
+        "force_collectives": bool(args.force_collectives),
         "gemm_1x1": gemm_1x1, "hip_graph": bool(args.graph),
     }
+    return w
+
+
+def build_convnet(args, device, world):
+    """The reference program's own workload (test_apex_distributed_spawn.py:83-164): the
+    MNIST ConvNet, batch 100 per process, SGD lr 1e-4, amp O2 with Apex's fp16 default,
+    apex DDP; synthetic 1x28x28 batches on the device.  Besides images/s the record
+    carries the reference's own metric, the wall time of one 60,000-image epoch."""
+    from apex_example_amd import amp
+    from apex_example_amd.models import ConvNet
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    half = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    bs = args.batch_size or 100
+    lr = args.lr or 1e-4
+    opt_level = args.opt_level or "O2"
+    multi = world > 1 or args.force_collectives
+    model = ConvNet().to(device)
+    x = torch.rand(bs, 1, 28, 28, device=device)
+    y = torch.randint(0, 10, (bs,), device=device)
+    crit = torch.nn.CrossEntropyLoss().to(device)
+    w = Workload()
+    if args.impl == "amd":
+        if args.convnet_optimizer == "fused":
+            opt = FusedSGD(model.parameters(), lr=lr, materialize_master_grads=False)
+        else:
+            opt = torch.optim.SGD(model.parameters(), lr)
+        model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
+        if multi:
+            model = DistributedDataParallel(model, force_collectives=args.force_collectives)
+            w.ddp = model
+
+        def step(b):
+            loss = crit(model(b[0]).float(), b[1])
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
+            opt.step()
+            return loss
+        optname = ("FusedSGD(lr=%g)" % lr) if args.convnet_optimizer == "fused" else \
+            "torch.optim.SGD(lr=%g) (reference)" % lr
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr)
+        scaler = torch.amp.GradScaler("cuda", enabled=(half == torch.float16))
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index])
+
+        def step(b):
+            with torch.autocast("cuda", dtype=half):
+                loss = crit(model(b[0]).float(), b[1])
+            opt.zero_grad(set_to_none=True)
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+            return loss
+        optname = "torch.optim.SGD(lr=%g)" % lr
+    w.step, w.opt_only, w.batch = step, opt.step, (x, y)
+    w.units = bs
+    w.metric = "images/sec (whole node) MNIST ConvNet amp %s" % opt_level
+    w.unit = "images/s"
+    w.dtype = "bf16" if half == torch.bfloat16 else "fp16"
+    w.data = "synthetic (on-device random 1x28x28 images, random labels; random-init weights)"
+    w.steps_per_epoch = -(-60000 // (world * bs))
+    w.config = {"model": "convnet", "global_batch": bs * world, "per_gpu_batch": bs,
+                "seq_len": None, "image_size": 28, "parallelism": "dp%d" % world,
+                "impl": args.impl, "opt_level": opt_level, "optimizer": optname,
+                "force_collectives": bool(args.force_collectives)}
     return w
 
 
@@ -272,8 +354,9 @@ def build_bert(args, device, world):
         opt = FusedLAMB(model.parameters(), lr=args.lr or 6e-3, weight_decay=0.01,
                         max_grad_norm=1.0, materialize_master_grads=args.materialize_master_grads)
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
-        if world > 1:
-            model = DistributedDataParallel(model, message_size=args.message_size)
+        if world > 1 or args.force_collectives:
+            model = DistributedDataParallel(model, message_size=args.message_size,
+                                            force_collectives=args.force_collectives)
             w.ddp = model
 
         def step(b):
@@ -337,8 +420,9 @@ def build_gpt2(args, device, world):
         opt = FusedAdam(model.parameters(), lr=args.lr or 1.5e-4, weight_decay=0.01,
                         materialize_master_grads=args.materialize_master_grads)
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
-        if world > 1:
-            model = DistributedDataParallel(model, message_size=args.message_size)
+        if world > 1 or args.force_collectives:
+            model = DistributedDataParallel(model, message_size=args.message_size,
+                                            force_collectives=args.force_collectives)
             w.ddp = model
 
         def step(b):
@@ -439,6 +523,12 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     rank, world, device = init_distributed()
+    if args.force_collectives and world == 1 and args.impl == "amd":
+        # a 1-rank process group (RCCL on the GPU) for the forced collectives
+        os.environ["MASTER_PORT"] = str(_free_port())
+        kw = {"device_id": device} if device.type == "cuda" else {}
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo", rank=0,
+                                world_size=1, **kw)
     if world != args.gpus:
         print("bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s); refusing to "
               "report a number for the wrong world size" % (args.gpus, world,
@@ -466,6 +556,8 @@ def main():
 
     if args.model.startswith("resnet"):
         w = build_resnet(args, device, world)
+    elif args.model == "convnet":
+        w = build_convnet(args, device, world)
     elif args.model == "bert_large":
         w = build_bert(args, device, world)
     else:
@@ -563,7 +655,8 @@ def main():
 
     ddp_stats = None
     ddp = getattr(w, "ddp", None)
-    if world > 1 and ddp is not None and args.bucket_timing_steps > 0:
+    if ((world > 1 or args.force_collectives) and ddp is not None
+            and args.bucket_timing_steps > 0):
         ddp_stats = ddp_timing(ddp, step, batch, args.bucket_timing_steps, device)
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -598,6 +691,9 @@ def main():
     }
     if ddp_stats is not None:
         rec["ddp"] = ddp_stats
+    if getattr(w, "steps_per_epoch", None):
+        # the reference program's metric: "Training complete in" / epochs
+        rec["epoch_seconds"] = round(w.steps_per_epoch * ms_per_step / 1e3, 3)
     if trace is not None:
         rec["loss_trace"] = [round(float(v), 4) for v in trace]
     if rank == 0:
@@ -608,6 +704,7 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
     if skipped and not args.allow_skipped_steps:
         print("bench.py: %d of the %d timed steps were skipped by the loss scaler (gradient "
