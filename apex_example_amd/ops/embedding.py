@@ -9,9 +9,14 @@ then runs against an idle GPU: BERT-large showed 4.6 ms of idle GPU time per 51 
 step in its kernel trace, clustered around the optimizer (``tools/rocprof_summary.py
 --gaps``, docs/PERF.md).
 
-Here the weight gradient is one fp32 scatter-add of the output-gradient rows into a
-zeroed [vocab, hidden] buffer (``index_add_``: device atomics, no host round trip),
-cast to the weight dtype.  Forward is the regular gather.
+Here the weight gradient is deterministic AND host-sync-free
+(``csrc/hip/embedding.hip``): a stable device sort of the ids, then one launch with
+a wave per sorted position; the wave that starts a run of equal ids sums that run's
+output-gradient rows in sorted order (fp32) and writes the weight row in the weight
+dtype.  The grid is sized by the token count (known on the host), so nothing is
+read back, and the fixed summation order makes it bitwise reproducible (the float-
+atomic ``index_add_`` scatter of round 2 was not; ``APEX_AMD_EMB_BWD=atomic`` keeps
+it for A/B runs, ``=stock`` the PyTorch op).  Forward is the regular gather.
 """
 from __future__ import annotations
 
@@ -21,8 +26,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-# APEX_AMD_SYNCFREE_EMB=0: the stock embedding backward (A/B runs)
-_ENABLED = os.environ.get("APEX_AMD_SYNCFREE_EMB", "1") == "1"
+from .. import _native
+
+# APEX_AMD_EMB_BWD = det (default) | atomic | stock   (APEX_AMD_SYNCFREE_EMB=0 = stock)
+_MODE = os.environ.get("APEX_AMD_EMB_BWD", "det")
+_ENABLED = os.environ.get("APEX_AMD_SYNCFREE_EMB", "1") == "1" and _MODE != "stock"
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -38,6 +46,9 @@ class _EmbeddingFn(torch.autograd.Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         V, H = ctx.shape
+        if _MODE == "det":
+            pad = -1 if ctx.padding_idx is None else int(ctx.padding_idx) % V
+            return None, _native.require().emb.wgrad(idx, dy, V, pad, ctx.wdtype), None
         flat = idx.reshape(-1)
         g = torch.zeros((V, H), dtype=torch.float32, device=dy.device)
         g.index_add_(0, flat, dy.reshape(-1, H).float())

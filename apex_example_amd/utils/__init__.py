@@ -9,4 +9,4 @@ from .dist import (  # noqa: F401
     is_main_process,
     local_rank,
 )
-from .misc import set_cuda, set_seed  # noqa: F401
+from .misc import deterministic, set_cuda, set_deterministic, set_seed  # noqa: F401

@@ -15,6 +15,38 @@ def set_cuda(deterministic=True):
         torch.backends.cudnn.benchmark = not deterministic
 
 
+_DETERMINISTIC = False
+
+
+def set_deterministic(on=True):
+    """Framework-wide deterministic mode (the reference runs
+    with cudnn.deterministic, test_apex_distributed_spawn.py:60-67,112).
+
+    Every reduction of this framework's own kernels is already fixed-order (slab
+    partials + finalize kernels, no float atomics): optimizers / norms, LayerNorm,
+    BatchNorm, bias gradients, split-K weight-gradient reductions, attention, the
+    embedding backward (device sort + ordered run sums).  The one kernel family
+    with float atomics, the opt-in persistent BatchNorm (APEX_AMD_BN_PERSIST), is
+    switched off here, MIOpen is constrained to deterministic solvers, and PyTorch
+    ops are asked for their deterministic variants (warn-only).  Returns the mode."""
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(on)
+    if torch.cuda.is_available():
+        torch.backends.cudnn.deterministic = _DETERMINISTIC
+        torch.backends.cudnn.benchmark = False if _DETERMINISTIC else torch.backends.cudnn.benchmark
+    torch.use_deterministic_algorithms(_DETERMINISTIC, warn_only=True)
+    from .. import _native
+    if _DETERMINISTIC and _native.available():
+        _native.require().bn.persist_enable(0)
+        from ..ops import embedding
+        embedding._MODE = "det"
+    return _DETERMINISTIC
+
+
+def deterministic():
+    return _DETERMINISTIC
+
+
 def set_seed(seed):
     os.environ["PYTHONHASHSEED"] = str(seed)
     random.seed(seed)

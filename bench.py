@@ -548,6 +548,9 @@ def main():
         return
     torch.backends.cudnn.benchmark = (not args.deterministic) and args.cudnn_benchmark
     torch.backends.cudnn.deterministic = args.deterministic
+    if args.deterministic:
+        from apex_example_amd.utils import set_deterministic
+        set_deterministic(True)
     torch.manual_seed(1234 + rank)
     gemm_table = None
     if args.gemm_tuning == "auto" and not os.environ.get("PYTORCH_TUNABLEOP_ENABLED"):
@@ -665,6 +668,7 @@ def main():
     if args.model.startswith("resnet") and (w.config.get("per_gpu_batch") != 256
                                             or args.image_size != 224):
         base = None
+    w.config["deterministic"] = bool(args.deterministic)
     w.config["gemm_tuning"] = (os.path.relpath(gemm_table, ROOT) if gemm_table else
                                "env" if os.environ.get("PYTORCH_TUNABLEOP_ENABLED") else None)
     rec = {

@@ -347,4 +347,11 @@ void xentropy_bwd(const void* dloss, DType tg, const void* x, DType tx, const fl
                   const int64_t* labels, int64_t rows, int V, float smoothing,
                   int64_t padding_idx, void* dx, hipStream_t st);
 
+// ---- deterministic embedding weight gradient (embedding.hip) ------------------
+// sorted / perm: the stable sort of the T token ids and its permutation; out [V, H]
+// must be zero-filled; runs of equal ids are summed in sorted order (fp32).
+void embedding_wgrad(const int64_t* sorted, const int64_t* perm, const void* dy, DType tdy,
+                     int64_t T, int H, int64_t pad, void* out, DType tout, bool vec,
+                     hipStream_t st);
+
 }  // namespace amd

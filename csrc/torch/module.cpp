@@ -13,6 +13,7 @@
 #include "dense_ops.h"
 #include "lt_ops.h"
 #include "xent_ops.h"
+#include "emb_ops.h"
 #include "reducer.h"
 
 namespace py = pybind11;
@@ -95,6 +96,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);
+
+  auto emb = m.def_submodule("emb", "deterministic embedding weight gradient (no host sync)");
+  emb.def("wgrad", &embedding_wgrad_op, py::arg("idx"), py::arg("dy"), py::arg("V"),
+          py::arg("padding_idx"), py::arg("out_dtype"));
 
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);

@@ -38,3 +38,29 @@ def test_embedding_padding_idx_and_tied_grad():
     w = emb.weight.detach().clone().requires_grad_(True)
     F.linear(F.embedding(idx, w, padding_idx=3), w).sum().backward()
     torch.testing.assert_close(emb.weight.grad, w.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("H", [1024, 250])   # vector path / scalar path
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embedding_backward_is_deterministic(H, dtype):
+    """The default backward (csrc/hip/embedding.hip: device sort + per-run sums in
+    sorted order) is bitwise reproducible and equals the fp64 sum to one rounding."""
+    torch.manual_seed(1)
+    V = 5000
+    emb = Embedding(V, H, padding_idx=11).to(dev).to(dtype)
+    idx = torch.randint(0, V, (8, 512), device=dev)
+    idx[:, :64] = 42                      # a long run (512 repeats)
+    idx[0, :5] = 11                       # padding ids
+    dy = torch.randn(8, 512, H, device=dev).to(dtype)
+    grads = []
+    for _ in range(3):
+        emb.weight.grad = None
+        emb(idx).backward(dy)
+        grads.append(emb.weight.grad.clone())
+    assert all(torch.equal(grads[0], g) for g in grads[1:])
+    ref = torch.zeros(V, H, dtype=torch.float64, device=dev).index_add_(
+        0, idx.reshape(-1), dy.reshape(-1, H).double())
+    ref[11] = 0
+    err = (grads[0].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= (1e-6 if dtype == torch.float32 else 2 ** -8), err
+    assert grads[0].dtype == dtype and torch.count_nonzero(grads[0][11]) == 0

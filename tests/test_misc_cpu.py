@@ -133,3 +133,21 @@ def test_multiproc_launcher(tmp_path):
     bad.write_text("import sys; sys.exit(3)\n")
     assert multiproc.main(["--nproc", "2", str(bad)]) == 3
     del sys
+
+
+def test_embedding_wgrad_cpu_reference_op():
+    """The native emb.wgrad op's CPU path (token-order fp32 sums, padding row zero)."""
+    from apex_example_amd import _native
+
+    if not _native.available():
+        import pytest
+        pytest.skip("native extension not built")
+    g = torch.Generator().manual_seed(0)
+    idx = torch.randint(0, 50, (4, 30), generator=g)
+    idx[0, :3] = 7
+    dy = torch.randn(4, 30, 16, generator=g).to(torch.bfloat16)
+    out = _native.require().emb.wgrad(idx, dy, 50, 7, torch.bfloat16)
+    ref = torch.zeros(50, 16).index_add_(0, idx.reshape(-1), dy.reshape(-1, 16).float())
+    ref[7] = 0
+    assert out.dtype == torch.bfloat16 and out.shape == (50, 16)
+    torch.testing.assert_close(out.float(), ref.to(torch.bfloat16).float())
