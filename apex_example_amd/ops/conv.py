@@ -40,15 +40,42 @@ _JOIN = {}          # device index -> (main stream to join, autograd graph task 
 _LOCK = threading.Lock()
 
 
-def _side_ok(weight):
-    if not (_USE_WSTREAM and weight.is_cuda and weight.grad is None):
-        return False
+def _ddp_slot(p):
+    """(reducer, index) when ``p.grad`` is a DDP bucket view whose reducer can take a
+    side-stream gradient this iteration (parallel/distributed.py), else None."""
+    slot = getattr(p, "_amd_ddp_slot", None)
+    if slot is None:
+        return None
+    red = slot[0]()
+    if red is None or not red.async_ready_ok() or p.grad is None:
+        return None
+    return red, slot[1]
+
+
+def _side_mode(params):
+    """'free': every param's .grad is None (AccumulateGrad stores the side-stream tensor
+    without a kernel; world size 1 only: no bucket hooks read it before the join);
+    'ddp': every param's .grad is a DDP bucket view - the side stream accumulates into
+    the view itself and announces it to the reducer (csrc/torch/reducer.cpp
+    mark_ready_on_stream), which launches that bucket's all-reduce behind an event of
+    the side stream instead of the compute stream; None: no side stream."""
+    ps = [p for p in params if p is not None]
+    if not _USE_WSTREAM or not ps or not ps[0].is_cuda:
+        return None
     if torch.cuda.is_current_stream_capturing():
-        return False
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        return False
-    return True
+        return None
+    if all(p.grad is None for p in ps):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return None
+        return "free"
+    if _DDP_SIDE and all(_ddp_slot(p) is not None for p in ps):
+        return "ddp"
+    return None
+
+
+# APEX_AMD_WGRAD_STREAM_DDP=0: no side-stream weight gradients under DDP (A/B)
+_DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "1") == "1"
 
 
 def _join_side():
@@ -71,7 +98,9 @@ class _SideWgrad:
     launched afterwards on the side stream can overlap it."""
 
     def __init__(self, weight, *more, enable=True):
-        self.on = enable and _side_ok(weight) and all(m is None or m.grad is None for m in more)
+        self.params = (weight,) + more
+        self.mode = _side_mode(self.params) if enable else None
+        self.on = self.mode is not None
         if self.on:
             dev = weight.device
             self.main = torch.cuda.current_stream(dev)
@@ -86,15 +115,24 @@ class _SideWgrad:
         self.side.wait_event(self.ev)
         with torch.cuda.stream(self.side):
             dw = fn()
+            outs = dw if isinstance(dw, tuple) else (dw,)
+            if self.mode == "ddp":
+                # accumulate into the bucket views on the side stream (what
+                # AccumulateGrad would do on the compute stream), then hand autograd
+                # None so nothing reads them on the compute stream before the join
+                with torch.no_grad():
+                    for p, g in zip(self.params, outs):
+                        if g is not None:
+                            p.grad.add_(g)
         for t in used:
             t.record_stream(self.side)
-        for t in (dw if isinstance(dw, tuple) else (dw,)):
+        for t in outs:
             if t is not None:
-                t.record_stream(self.main)
+                t.record_stream(self.main if self.mode == "free" else self.side)
+        idx = self.main.device.index
         # one join per backward pass (graph task): a pass that raised before its final
         # callbacks ran leaves a stale entry behind; the next pass sees another task id
         # and queues its own callback, which joins everything pending
-        idx = self.main.device.index
         task = torch._C._current_graph_task_id()
         with _LOCK:
             ent = _JOIN.get(idx)
@@ -103,6 +141,14 @@ class _SideWgrad:
                 _JOIN[idx] = (self.main, task)
         if fresh:
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
+        if self.mode == "ddp":
+            sid = self.side.cuda_stream
+            for p, g in zip(self.params, outs):
+                if g is not None:
+                    red, i = _ddp_slot(p)
+                    red.mark_ready_on_stream(i, sid)
+            none = tuple(None for _ in outs)
+            return none if isinstance(dw, tuple) else None
         return dw
 
 

@@ -47,13 +47,31 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
     the BN reduce + elementwise kernels (ReLU condition recomputed from x)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, eps, momentum, k, s, p):
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, eps, momentum, k, s, p,
+                pg=None):
         C = _native.require()
-        mean, invstd = C.bn.train_stats(x, running_mean, running_var, nbt, float(eps),
-                                        float(momentum))
+        inv_total = None
+        if pg is None:
+            mean, invstd = C.bn.train_stats(x, running_mean, running_var, nbt, float(eps),
+                                            float(momentum))
+        else:
+            # SyncBatchNorm stem: the same packed stats exchange as ops/batch_norm.py
+            # (one all_gather of [mean | var | count]), then the fused pool pass
+            import torch.distributed as dist
+            world = dist.get_world_size(pg)
+            packed = C.bn.local_stats_packed(x)
+            gathered = torch.empty(world * packed.numel(), dtype=packed.dtype, device=x.device)
+            if dist.get_backend(pg) == "nccl":
+                dist.all_gather_into_tensor(gathered, packed, group=pg)
+            else:
+                dist.all_gather(list(gathered.chunk(world)), packed, group=pg)
+            mean, invstd, inv_total = C.bn.combine_stats_sync(
+                gathered.view(world, -1), float(eps), float(momentum), running_mean,
+                running_var, nbt)
         y, idx = C.pool.max_fwd_bn(x, mean, invstd, weight, bias, k, s, p)
         ctx.save_for_backward(x, weight, bias, mean, invstd, idx)
         ctx.geom = (x.size(2), x.size(3), k, s, p)
+        ctx.pg, ctx.inv_total = pg, inv_total
         return y
 
     @staticmethod
@@ -63,22 +81,51 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
         C = _native.require()
         dbn = C.pool.max_bwd(dy, idx, H, W, k, s, p)
         need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        sum_dy, sum_dy_xmu, gw, gb = C.bn.reduce_grad(dbn, x, mean, invstd, weight, bias, None,
-                                                      True, need_w)
-        count = x.numel() // x.size(1)
+        if ctx.pg is None:
+            sum_dy, sum_dy_xmu, gw, gb = C.bn.reduce_grad(dbn, x, mean, invstd, weight, bias,
+                                                          None, True, need_w)
+            count = float(x.numel() // x.size(1))
+        else:
+            import torch.distributed as dist
+            sum_dy, sum_dy_xmu, gw, gb = C.bn.reduce_grad(dbn, x, mean, invstd, weight, bias,
+                                                          None, True, need_w,
+                                                          sum_scale=ctx.inv_total)
+            n = sum_dy.numel()
+            dist.all_reduce(sum_dy.as_strided((2 * n,), (1,)), group=ctx.pg)
+            count = 1.0
         dx, _ = C.bn.backward_elemt(dbn, x, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
-                                    float(count), None, True, False)
+                                    count, None, True, False)
         return (dx, gw if need_w else None, gb if need_w else None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
+
+
+def _stem_pg(bn):
+    """None: local statistics (BatchNorm2dReLU); a process group: SyncBatchNorm whose
+    cross-rank statistics the fused stem exchanges itself; False: not fusable."""
+    from .batch_norm import BatchNorm2dReLU
+
+    if type(bn) is BatchNorm2dReLU:
+        return None
+    from ..parallel.sync_batchnorm import SyncBatchNorm, syncbn_comm_group
+    import torch.distributed as dist
+
+    if type(bn) is not SyncBatchNorm or bn.channel_last:
+        return False
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    if bn.process_group is not None:
+        return bn.process_group
+    if dist.get_world_size() > 1 or getattr(bn, "force_collectives", False):
+        return syncbn_comm_group()
+    return None
 
 
 def bn_relu_maxpool_fusable(x, bn, pool):
-    """True when ``pool(relu(bn(x)))`` can run as BNReLUMaxPoolFunction: a LOCAL
-    BatchNorm2dReLU only (a SyncBatchNorm needs the cross-rank statistics)."""
-    from .batch_norm import BatchNorm2dReLU
-
+    """True when ``pool(relu(bn(x)))`` can run as BNReLUMaxPoolFunction: a local
+    BatchNorm2dReLU, or a SyncBatchNorm (the statistics are exchanged first)."""
     k, s, p = pool.kernel_size, pool.stride, pool.padding
-    return (_FUSE_STEM and type(bn) is BatchNorm2dReLU and bn.fuse_relu and bn.training and bn.track_running_stats and bn.momentum is not None
+    return (_FUSE_STEM and getattr(bn, "fuse_relu", False) and _stem_pg(bn) is not False
+            and bn.training and bn.track_running_stats and bn.momentum is not None
             and x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
             and x.size(1) % 8 == 0 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and bn.weight is not None and bn.weight.dtype == torch.float32
@@ -91,7 +138,8 @@ def bn_relu_maxpool_fusable(x, bn, pool):
 def bn_relu_maxpool(x, bn, pool):
     return BNReLUMaxPoolFunction.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                        bn.num_batches_tracked, bn.eps, bn.momentum,
-                                       pool.kernel_size, pool.stride, pool.padding)
+                                       pool.kernel_size, pool.stride, pool.padding,
+                                       _stem_pg(bn))
 
 
 class MaxPool2dNHWC(nn.MaxPool2d):

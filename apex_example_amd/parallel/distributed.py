@@ -238,6 +238,10 @@ class DistributedDataParallel(Module):
 
     def _fp32_mode(self):
         if self.allreduce_always_fp32 is None:
+            import os
+            env = os.environ.get("APEX_AMD_DDP_FP32")  # A/B override of the auto rule
+            if env in ("0", "1"):
+                return int(env)
             return 2  # bf16 buckets in fp32, fp16 / fp32 native
         return 1 if self.allreduce_always_fp32 else 0
 
@@ -264,10 +268,15 @@ class DistributedDataParallel(Module):
                                          self.use_avg_op, triggers, int(self.bucket_align))
         self.reducer.set_allow_unused(self.allow_unused)
         self.reducer.set_force_collectives(self.force_collectives)
+        self.reducer.set_prof(bool(self.prof))
         if self._bucket_pgs:
             self.reducer.set_bucket_process_groups(self._bucket_pgs)
-        for p in self.active_params:
+        import weakref
+        ref = weakref.ref(self.reducer)
+        for i, p in enumerate(self.active_params):
             p._amd_grad_is_bucket_view = True
+            # side-stream weight gradients (ops/conv.py) announce themselves here
+            p._amd_ddp_slot = (ref, i)
 
     def __setstate__(self, state):
         super().__setstate__(state)

@@ -23,6 +23,14 @@
 //  * `force_collectives` issues the all-reduce even on a 1-rank communicator
 //    (legal on RCCL): the single-GPU test box then exercises launch order, the
 //    epilogue stream join and in-flight bucket consumption for real;
+//  * gradients produced on a SIDE stream (ops/conv.py weight gradients overlapping
+//    the data gradient) are accumulated into their bucket views on that stream and
+//    announced with `mark_ready_on_stream`: the reducer records an event there,
+//    and a bucket holding such gradients is launched from an internal launch stream
+//    that waits on the compute stream AND those events - the compute stream itself
+//    never waits for the side stream before the end-of-backward join;
+//  * `prof` (apex prof=True): roctx ranges around every bucket launch and the
+//    epilogue (visible in rocprofv3 --marker-trace next to the kernels);
 //  * optional per-bucket timing (HIP events on the compute stream): when each
 //    bucket was launched relative to the first gradient, when backward ended,
 //    and when each bucket's collective was joined -> the exposed
@@ -36,12 +44,18 @@
 #include <ATen/record_function.h>
 
 #include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime_api.h>
 
 #include <memory>
 #include <mutex>
+#include <string>
 
 #include "reducer.h"
+
+extern "C" int roctxRangePushA(const char* message);  // libroctx64 (what torch.cuda.nvtx uses)
+extern "C" int roctxRangePop();
 
 namespace amd {
 
@@ -57,6 +71,17 @@ struct Bucket {
   int pending = 0;
   bool launched = false;
   c10::intrusive_ptr<c10d::Work> work;
+  std::vector<hipEvent_t> waits;  // side-stream gradient events this launch must wait on
+};
+
+struct RangeGuard {  // roctx range when enabled
+  bool on;
+  RangeGuard(bool e, const std::string& name) : on(e) {
+    if (on) roctxRangePushA(name.c_str());
+  }
+  ~RangeGuard() {
+    if (on) roctxRangePop();
+  }
 };
 
 class Reducer : public std::enable_shared_from_this<Reducer> {
@@ -81,6 +106,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     for (int64_t i = (int64_t)params_.size() - 1; i >= 0; --i) order.push_back(i);
     build_layout(order);
     seen_.assign(params_.size(), 0);
+    async_marked_.assign(params_.size(), 0);
   }
 
   ~Reducer() {
@@ -91,6 +117,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     }
     for (auto e : ev_launch_) (void)hipEventDestroy(e);
     for (auto e : ev_done_) (void)hipEventDestroy(e);
+    for (auto e : ev_pool_) (void)hipEventDestroy(e);
+    for (auto& b : buckets_)
+      for (auto e : b.waits) (void)hipEventDestroy(e);
+    if (ev_main_) (void)hipEventDestroy(ev_main_);
   }
 
   void install_hooks() {
@@ -117,9 +147,35 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   }
 
   // ---- hook path (autograd engine thread) ---------------------------------
-  void mark_ready(int64_t i) {
+  void mark_ready(int64_t i) { mark_ready_impl(i, nullptr); }
+
+  // A gradient already accumulated into its bucket view by work on `stream`
+  // (side-stream weight gradients): ready once that stream reaches this point.
+  void mark_ready_on_stream(int64_t i, int64_t stream) {
+    mark_ready_impl(i, reinterpret_cast<hipStream_t>(stream));
+  }
+
+  // Side-stream gradients can be announced (iteration >= 2 of an overlapped,
+  // enabled reducer whose collectives run): the caller then writes the gradient
+  // into the bucket view itself and calls mark_ready_on_stream.
+  bool async_ready_ok() const { return enabled_ && !refresh_ && !delay_ && comm_active(); }
+
+  void mark_ready_impl(int64_t i, hipStream_t side) {
     std::lock_guard<std::mutex> g(mu_);
+    if (side) {
+      async_marked_[(size_t)i] = 1;
+    } else if (async_marked_[(size_t)i]) {
+      // the AccumulateGrad post-hook of a gradient that was announced from the side
+      // stream (the Function returned None for it; the hook still runs): consumed
+      async_marked_[(size_t)i] = 0;
+      return;
+    }
     attach_view(i);
+    if (side && enabled_ && !refresh_ && !delay_ && comm_active()) {
+      hipEvent_t e = take_event();
+      TORCH_CHECK(hipEventRecord(e, side) == hipSuccess, "hipEventRecord failed");
+      buckets_[(size_t)bucket_of_[(size_t)i]].waits.push_back(e);
+    }
     if (!enabled_) return;
     if (!callback_queued_) {
       callback_queued_ = true;
@@ -149,6 +205,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     std::lock_guard<std::mutex> g(mu_);
     callback_queued_ = false;
     if (!enabled_) return;
+    RangeGuard rg(prof_, "apex_amd::ddp_epilogue");
     const bool timed = timing_ && !refresh_ && !delay_;
     if (timed) timing_record(ev_bwd_end_);
     if (refresh_) {
@@ -198,6 +255,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   }
   bool enabled() const { return enabled_; }
   void set_force_collectives(bool f) { force_ = f; }
+  void set_prof(bool p) { prof_ = p; }
   bool force_collectives() const { return force_; }
   bool collectives_active() const { return comm_active(); }
   void set_timing(bool t) {
@@ -365,6 +423,18 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   bool comm_active() const { return world_ > 1 || force_; }
 
+  hipEvent_t take_event() {
+    if (!ev_pool_.empty()) {
+      hipEvent_t e = ev_pool_.back();
+      ev_pool_.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess,
+                "hipEventCreate failed");
+    return e;
+  }
+
   void ensure_events() {
     auto grow = [](std::vector<hipEvent_t>& v, size_t n) {
       while (v.size() < n) {
@@ -393,6 +463,33 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     B.launched = true;
     if (!comm_active()) return;
     if (timing_ && !refresh_ && !delay_) timing_record(ev_launch_[(size_t)bi]);
+    RangeGuard rg(prof_, "apex_amd::allreduce_bucket " + std::to_string(bi));
+    if (!B.waits.empty()) {
+      // launch stream = compute stream's work so far + every side-stream gradient
+      // of this bucket; the collective (and the fp32 up-cast) run behind it
+      if (!launch_stream_)
+        launch_stream_ = std::make_unique<at::hip::HIPStreamMasqueradingAsCUDA>(
+            at::hip::getStreamFromPoolMasqueradingAsCUDA(true, params_[0].device().index()));
+      hipStream_t ls = launch_stream_->stream();
+      if (!ev_main_)
+        TORCH_CHECK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming) == hipSuccess,
+                    "hipEventCreate failed");
+      TORCH_CHECK(hipEventRecord(ev_main_, c10::hip::getCurrentHIPStream().stream()) == hipSuccess,
+                  "hipEventRecord failed");
+      TORCH_CHECK(hipStreamWaitEvent(ls, ev_main_, 0) == hipSuccess, "hipStreamWaitEvent failed");
+      for (hipEvent_t e : B.waits) {
+        TORCH_CHECK(hipStreamWaitEvent(ls, e, 0) == hipSuccess, "hipStreamWaitEvent failed");
+        ev_pool_.push_back(e);  // reusable once recorded again (waits were enqueued)
+      }
+      B.waits.clear();
+      at::hip::HIPStreamGuardMasqueradingAsCUDA sg(*launch_stream_);
+      launch_body(B, bi);
+      return;
+    }
+    launch_body(B, bi);
+  }
+
+  void launch_body(Bucket& B, int64_t bi) {
     c10::NoGradGuard ng;
     if (predivide_ != 1.0) B.flat.mul_(1.0 / predivide_);
     // fp32 accumulation: 1 = every 16-bit bucket (apex allreduce_always_fp32),
@@ -412,6 +509,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   }
 
   void complete(Bucket& B) {
+    for (hipEvent_t e : B.waits) {  // announced but never launched (error paths)
+      (void)hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), e, 0);
+      ev_pool_.push_back(e);
+    }
+    B.waits.clear();
     if (!B.launched || !comm_active()) return;
     if (B.work) B.work->wait();
     c10::NoGradGuard ng;
@@ -436,6 +538,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     }
     next_ = 0;
     std::fill(seen_.begin(), seen_.end(), 0);
+    std::fill(async_marked_.begin(), async_marked_.end(), 0);
   }
 
   std::vector<at::Tensor> params_;
@@ -454,6 +557,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<at::Tensor> views_;
   std::vector<int64_t> arrival_;
   std::vector<char> seen_;
+  std::vector<char> async_marked_;
   int64_t next_ = 0;
   bool refresh_ = true;
   bool enabled_ = true;
@@ -461,6 +565,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool callback_queued_ = false;
   bool force_ = false;
   bool timing_ = false, timing_valid_ = false;
+  bool prof_ = false;
+  std::vector<hipEvent_t> ev_pool_;
+  hipEvent_t ev_main_ = nullptr;
+  std::unique_ptr<at::hip::HIPStreamMasqueradingAsCUDA> launch_stream_;
   hipEvent_t ev_start_ = nullptr, ev_bwd_end_ = nullptr;
   std::vector<hipEvent_t> ev_launch_, ev_done_;
   std::mutex mu_;
@@ -497,6 +605,10 @@ void register_reducer(pybind11::module_& m) {
       .def("enabled", &Reducer::enabled)
       .def("set_allow_unused", &Reducer::set_allow_unused)
       .def("set_force_collectives", &Reducer::set_force_collectives)
+      .def("set_prof", &Reducer::set_prof)
+      .def("mark_ready_on_stream", &Reducer::mark_ready_on_stream, py::arg("index"),
+           py::arg("stream"))
+      .def("async_ready_ok", &Reducer::async_ready_ok)
       .def("force_collectives", &Reducer::force_collectives)
       .def("collectives_active", &Reducer::collectives_active)
       .def("set_timing", &Reducer::set_timing)

@@ -310,3 +310,61 @@ def test_syncbn_forced_collectives_match_local_bn(pg, monkeypatch, residual):
         tol = dict(rtol=2 ** -7, atol=2 ** -7) if n in ("y", "dx", "dz") else \
             dict(rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(b, a, **tol, msg=n)
+
+
+def test_ddp_side_stream_weight_grads_match_main_stream(pg):
+    """under DDP the conv weight gradients run on the side stream,
+    accumulate into their bucket views there and are announced to the reducer, whose
+    bucket all-reduces (forced RCCL collectives at world 1) then wait on side-stream
+    events.  Gradients and the trained weights must be bitwise equal to the
+    main-stream path, iteration after iteration."""
+    from apex_example_amd import amp
+    from apex_example_amd.models import resnet18
+    from apex_example_amd.ops import conv as convmod
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    x = torch.randn(16, 3, 64, 64, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    results = {}
+    used = {}
+    prev = convmod._DDP_SIDE
+    try:
+        for side in (False, True):
+            convmod._DDP_SIDE = side
+            torch.manual_seed(0)
+            m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+            opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, materialize_master_grads=False)
+            m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16,
+                                    verbosity=0)
+            ddp = DistributedDataParallel(m, message_size=500_000, force_collectives=True)
+            calls = {"n": 0}
+            orig = convmod._SideWgrad.run
+
+            def counting(self, fn, *a, _orig=orig, _calls=calls):
+                if self.mode == "ddp":
+                    _calls["n"] += 1
+                return _orig(self, fn, *a)
+            convmod._SideWgrad.run = counting
+            grads = []
+            try:
+                for it in range(4):
+                    loss = torch.nn.functional.cross_entropy(ddp(x), y)
+                    opt.zero_grad()
+                    with amp.scale_loss(loss, opt) as s:
+                        s.backward()
+                    grads.append([p.grad.detach().clone() for p in m.parameters()])
+                    opt.step()
+            finally:
+                convmod._SideWgrad.run = orig
+            torch.cuda.synchronize()
+            results[side] = (grads, [p.detach().clone() for p in m.parameters()])
+            used[side] = calls["n"]
+    finally:
+        convmod._DDP_SIDE = prev
+    assert used[False] == 0 and used[True] > 0, used
+    for it, (a, b) in enumerate(zip(results[False][0], results[True][0])):
+        bad = [i for i, (u, v) in enumerate(zip(a, b)) if not torch.equal(u, v)]
+        assert not bad, (it, bad)
+    for u, v in zip(results[False][1], results[True][1]):
+        assert torch.equal(u, v)

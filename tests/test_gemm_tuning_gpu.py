@@ -4,7 +4,7 @@ check, and round 2 shipped one that returned non-finite values).
 
 The check runs tools/diag/tuned_gemm_validate.py in a child process with TunableOp's
 verbose log on, so the test also proves that each tuned run HIT its table entry
-("ResultEntry found for <op>(<params>)") instead of silently running the default."""
+("ResultEntry found for <op>,<params>") instead of silently running the default."""
 import json
 import os
 import subprocess
@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # max |C - C_ref| / max |C_ref| for fp32-accumulated GEMMs: one rounding of the output
-# (bf16 2^-9, fp16 2^-11 relative) with a 4x margin
+# (unit roundoff bf16 2^-8, fp16 2^-11) with a 2x / 4x margin.  Measured on MI355X
+# (ResNet-50 table): 1.8e-3 .. 3.5e-3 for bf16, tuned == untuned bitwise on every row.
 BOUND = {"BFloat16": 2 ** -7, "Half": 2 ** -9}
 
 
@@ -48,7 +49,7 @@ def test_every_tuned_entry_is_numerically_sound(tmp_path, name):
                 and r["untuned_finite"] and r["untuned_err"] <= bound):
             bad.append(r)
         # the tuned call looked the key up in the loaded table
-        assert "ResultEntry found for %s(%s)" % (r["op"], r["params"]) in text, (
+        assert "ResultEntry found for %s,%s" % (r["op"], r["params"]) in text, (
             r["op"], r["params"], text[-2000:])
     assert not bad, json.dumps(bad, indent=1)
     print(p.stdout)

@@ -124,7 +124,7 @@ def build(jobs: int | None = None, verbose: bool = False, clean: bool = False) -
         link = [
             os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", "--offload-arch=" + ARCH,
             *objs, "-o", out, "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
-            "-ltorch_hip", "-ltorch_python", "-lhipblaslt", "-Wl,-rpath," + tlib,
+            "-ltorch_hip", "-ltorch_python", "-lhipblaslt", "-lroctx64", "-Wl,-rpath," + tlib,
         ]
         _run(link, verbose)
         # an unresolved symbol only shows at dlopen: check the fresh .so in a child

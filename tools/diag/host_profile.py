@@ -22,15 +22,28 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     build = {"resnet50": bench.build_resnet, "bert_large": bench.build_bert,
-             "gpt2_medium": bench.build_gpt2}[args.model]
+             "gpt2_medium": bench.build_gpt2, "convnet": bench.build_convnet}[args.model]
+    opt_only = os.environ.get("HOST_PROFILE_OPT_ONLY") == "1"
     w = build(args, dev, 1)
     for _ in range(3):
         w.step(w.batch)
     torch.cuda.synchronize()
+    import time
+    fn = (lambda: w.opt_only()) if opt_only else (lambda: w.step(w.batch))
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fn()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print("host ms per call (no profiler): %.4f  (until sync %.4f)" % (
+        (t1 - t0) * 1e3 / args.steps, (time.perf_counter() - t0) * 1e3 / args.steps))
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(args.steps):
-        w.step(w.batch)
+        fn()
     torch.cuda.synchronize()
     pr.disable()
     st = pstats.Stats(pr)

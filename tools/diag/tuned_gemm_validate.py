@@ -12,7 +12,7 @@ same operands:
 Results go to a JSON list (one record per row).  Whether the tuned run really used the
 table is shown by TunableOp's own log: run with PYTORCH_TUNABLEOP_VERBOSE=3 and
 PYTORCH_TUNABLEOP_VERBOSE_FILENAME=<file>; every hit logs "ResultEntry found for
-<op>(<params>)" (tests/test_gemm_tuning_gpu.py does this and checks every key).
+<op>,<params>" (tests/test_gemm_tuning_gpu.py does this and checks every key).
 
     python tools/diag/tuned_gemm_validate.py --out gpurun_out/tuned.json resnet50 bert_large
 """
