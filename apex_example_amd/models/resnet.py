@@ -12,6 +12,8 @@ layout MIOpen's bf16 convolutions prefer on MI355X.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn as nn
 
@@ -57,6 +59,14 @@ class _BNAct(nn.Module):
         return torch.relu(y) if self.relu_after else y
 
 
+def _link_stats(conv, bnact):
+    """Let ``conv`` write the BatchNorm statistics of its output for ``bnact.bn`` in its
+    epilogue (ops/conv.py; resolved at forward time, so convert_syncbn_model's
+    replacement BN is the one that receives them)."""
+    if bnact.fused:
+        conv._amd_stats_bn = weakref.ref(bnact)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -68,6 +78,8 @@ class BasicBlock(nn.Module):
         self.conv2 = conv3x3(planes, planes, mfma=gemm_1x1)
         self.bn2 = _BNAct(planes, True, fused_bn, zero_init_residual)
         self.downsample = downsample
+        _link_stats(self.conv1, self.bn1)
+        _link_stats(self.conv2, self.bn2)
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
@@ -89,6 +101,9 @@ class Bottleneck(nn.Module):
         self.conv3 = conv1x1(width, planes * self.expansion, gemm=gemm_1x1)
         self.bn3 = _BNAct(planes * self.expansion, True, fused_bn, zero_init_residual)
         self.downsample = downsample
+        _link_stats(self.conv1, self.bn1)
+        _link_stats(self.conv2, self.bn2)
+        _link_stats(self.conv3, self.bn3)
 
     def forward(self, x):
         if isinstance(self.conv1, Conv2d1x1):
@@ -111,6 +126,7 @@ class _Downsample(nn.Module):
         super().__init__()
         self.conv = conv1x1(inplanes, outplanes, stride, gemm=gemm_1x1)
         self.bn = _BNAct(outplanes, False, fused_bn)
+        _link_stats(self.conv, self.bn)
 
     def forward(self, x):
         return self.bn(self.conv(x))

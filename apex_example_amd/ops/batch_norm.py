@@ -54,7 +54,8 @@ def _to_logical(x, shape_channel_last):
 class BatchNormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
-                fuse_relu, shape_channel_last, num_batches_tracked=None, force_collectives=False):
+                fuse_relu, shape_channel_last, num_batches_tracked=None, force_collectives=False,
+                slab=None, slab_shift=None):
         C = _C()
         orig_shape = x.shape
         xl = _to_logical(x, shape_channel_last)
@@ -71,12 +72,23 @@ class BatchNormFunction(torch.autograd.Function):
         collective = world > 1 or bool(force_collectives)
         want_mask = bool(fuse_relu) and zl is not None and xl.is_cuda
         if not collective and xl.is_cuda:
-            # one stats launch + one finalize (mean, invstd, running stats and
-            # num_batches_tracked in the same kernel) + one apply launch
-            y, mean_g, invstd, mask = C.forward_local(xl, weight, bias, running_mean,
-                                                      running_var, num_batches_tracked,
-                                                      float(eps), float(momentum), zl,
-                                                      bool(fuse_relu), want_mask)
+            if slab is not None:
+                # statistics already summed by the producing conv's epilogue
+                # (ops/conv.py): one finalize launch + the apply launch
+                mean_g, invstd = C.slab_train_stats(slab, count, slab_shift, running_mean,
+                                                    running_var, num_batches_tracked,
+                                                    float(eps), float(momentum))
+                if want_mask:
+                    y, mask = C.apply_mask(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu))
+                else:
+                    y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
+            else:
+                # one stats launch + one finalize (mean, invstd, running stats and
+                # num_batches_tracked in the same kernel) + one apply launch
+                y, mean_g, invstd, mask = C.forward_local(xl, weight, bias, running_mean,
+                                                          running_var, num_batches_tracked,
+                                                          float(eps), float(momentum), zl,
+                                                          bool(fuse_relu), want_mask)
             ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd,
                                   mask)
             ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = None, 1, bool(fuse_relu), \
@@ -89,7 +101,8 @@ class BatchNormFunction(torch.autograd.Function):
             # all_gather -> one combine kernel (global mean / invstd, running stats,
             # num_batches_tracked, 1/global count) -> apply.  No host sync, no cat.
             pg = process_group if process_group is not None else dist.group.WORLD
-            packed = C.local_stats_packed(xl)
+            packed = (C.slab_packed_stats(slab, count, slab_shift) if slab is not None
+                      else C.local_stats_packed(xl))
             gathered = torch.empty(world * packed.numel(), dtype=packed.dtype, device=x.device)
             if dist.get_backend(pg) == "nccl":
                 dist.all_gather_into_tensor(gathered, packed, group=pg)
@@ -167,7 +180,7 @@ class BatchNormFunction(torch.autograd.Function):
                 if dz is not None:
                     dz = dz.view(ctx.orig_shape)
             return (dx, dz if ctx.has_z else None, gw if need_w else None,
-                    gb if need_w else None, None, None, None, None, None, None, None, None, None)
+                    gb if need_w else None, None, None, None, None, None, None, None, None, None, None, None)
         if ctx.world == 1 and xl.is_cuda:
             # one persistent launch (reduce + dgamma/dbeta + dx) where the activation fits
             # the register file, else reduce + elementwise (csrc/hip/bn_persist.hip)
@@ -178,7 +191,7 @@ class BatchNormFunction(torch.autograd.Function):
                 if dz is not None:
                     dz = dz.view(ctx.orig_shape)
             return (dx, dz if ctx.has_z else None, gw if need_w else None,
-                    gb if need_w else None, None, None, None, None, None, None, None, None, None)
+                    gb if need_w else None, None, None, None, None, None, None, None, None, None, None, None)
         sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
                                                    ctx.fuse_relu, need_w, mask=mask)
         if ctx.world > 1:
@@ -198,18 +211,32 @@ class BatchNormFunction(torch.autograd.Function):
             if dz is not None:
                 dz = dz.view(ctx.orig_shape)
         return (dx, dz if ctx.has_z else None, gw if need_w else None, gb if need_w else None,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)
+
+
+def take_slab(x, bn):
+    """(slab, shift) when ``x`` carries the epilogue statistics a conv computed for
+    ``bn`` (ops/conv.py) - consumed once - else (None, None)."""
+    ent = getattr(x, "_amd_bn_stats", None)
+    if ent is None:
+        return None, None
+    del x._amd_bn_stats
+    slab, shift, owner = ent
+    if owner is not bn or slab.size(0) != x.size(1):
+        return None, None
+    return slab, shift
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
                    z=None, fuse_relu=False, process_group=False, shape_channel_last=False,
-                   num_batches_tracked=None, force_collectives=False):
+                   num_batches_tracked=None, force_collectives=False, slab=None, slab_shift=None):
     """Functional fused BN(+z)(+ReLU).  ``process_group=False`` -> local statistics.
-    ``num_batches_tracked`` (int64 tensor) is incremented on the device."""
+    ``num_batches_tracked`` (int64 tensor) is incremented on the device.  ``slab``:
+    per-tile statistics a producing conv already summed ([C][2][S], ops/conv.py)."""
     if training:
         return BatchNormFunction.apply(x, z, weight, bias, running_mean, running_var, eps, momentum,
                                        process_group, fuse_relu, shape_channel_last,
-                                       num_batches_tracked, force_collectives)
+                                       num_batches_tracked, force_collectives, slab, slab_shift)
     # inference: running statistics (autograd through plain torch ops)
     if shape_channel_last:
         xs = x.movedim(-1, 1)
@@ -233,7 +260,12 @@ class BatchNorm2dReLU(torch.nn.BatchNorm2d):
         super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
         self.fuse_relu = fuse_relu
 
+    def _amd_accepts_slab(self):
+        """Can take statistics from the producing conv's epilogue (ops/conv.py)."""
+        return self.training and (self.momentum is not None or not self.track_running_stats)
+
     def forward(self, x, z=None):
+        slab, shift = take_slab(x, self)
         if not x.is_cuda and not _native.available():
             y = super().forward(x)
             if z is not None:
@@ -252,4 +284,5 @@ class BatchNorm2dReLU(torch.nn.BatchNorm2d):
                               self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
                               use_batch, momentum, self.eps, z=z, fuse_relu=self.fuse_relu,
-                              process_group=False, num_batches_tracked=nbt)
+                              process_group=False, num_batches_tracked=nbt,
+                              slab=slab if use_batch else None, slab_shift=shift)

@@ -74,8 +74,11 @@ def _side_mode(params):
     return None
 
 
-# APEX_AMD_WGRAD_STREAM_DDP=0: no side-stream weight gradients under DDP (A/B)
-_DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "1") == "1"
+# APEX_AMD_WGRAD_STREAM_DDP=1: side-stream weight gradients under DDP too.  Off by
+# default: ResNet-50 with forced world-1 collectives measured 8130 img/s with it vs
+# 8949 without (same box; the side stream ends backward ~5 ms behind the compute
+# stream, and the last buckets wait for it: exposed tail 5.2 vs 0.06 ms).
+_DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "0") == "1"
 
 
 def _join_side():
@@ -192,11 +195,19 @@ def _own_1x1(x_rows_dtype, cin, cout, m):
             and x_rows_dtype == torch.bfloat16 and _native.available())
 
 
-def _conv1x1_fwd(x, weight):
-    """y = conv1x1(x) for a channels-last bf16 x: own MFMA kernel or hipBLASLt GEMM."""
+def _conv1x1_fwd(x, weight, bn=None):
+    """y = conv1x1(x) for a channels-last bf16 x: own MFMA kernel or hipBLASLt GEMM.
+    With ``bn`` (a BatchNorm consuming y) the own kernel also writes its statistics
+    wherever that beats hipBLASLt + a statistics pass (always for own-kernel shapes;
+    channel-expanding / equal shapes, where the saved pass over the 4x larger output
+    outweighs the library's edge: profiles/microbench_conv1x1_own.txt)."""
     n, ci, h, w = x.shape
     co = weight.shape[0]
-    if _own_1x1(x.dtype, ci, co, n * h * w) and weight.dtype == torch.bfloat16:
+    own = _own_1x1(x.dtype, ci, co, n * h * w)
+    if (bn is not None and weight.dtype == torch.bfloat16 and ci % 64 == 0 and co % 64 == 0
+            and (own or co >= ci) and n * h * w < (1 << 31)):
+        return _conv_fwd(x, weight, 1, bn)
+    if own and weight.dtype == torch.bfloat16:
         return _native.require().conv.conv_fwd(x, weight, 1)
     y2 = torch.mm(_as_rows(x), weight.reshape(co, ci).t())
     return y2.view(n, h, w, co).permute(0, 3, 1, 2)
@@ -229,15 +240,68 @@ def _as_rows(t):
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
+# ---------------------------------------------------------------- BN statistics in the
+# conv epilogue.  A conv whose output feeds a training-mode BatchNorm (the model links
+# them: ``conv._amd_stats_bn``) asks the own MFMA kernel to also write that BN's
+# per-M-tile shifted sums (csrc/hip/conv_igemm.hip); the BN then finalizes from that
+# slab (bn.slab_train_stats / slab_packed_stats) instead of re-reading its input with a
+# statistics pass.  The slab travels to the BN as an attribute of the conv output,
+# tagged with the BN module it was made for.  APEX_AMD_CONV_BN_STATS=0 disables.
+_CONV_BN_STATS = os.environ.get("APEX_AMD_CONV_BN_STATS", "1") == "1"
+_TLS = threading.local()
+
+
+def _stats_bn(conv, x):
+    """The BatchNorm module that will consume ``conv(x)`` if it can take epilogue
+    statistics (training mode, running-stat shift available or not), else None."""
+    if not (_CONV_BN_STATS and x.is_cuda and x.dtype == torch.bfloat16):
+        return None
+    link = getattr(conv, "_amd_stats_bn", None)
+    owner = link() if link is not None else None
+    bn = getattr(owner, "bn", None) if owner is not None else None
+    if bn is None or not bn.training or not hasattr(bn, "_amd_accepts_slab"):
+        return None
+    if not bn._amd_accepts_slab():
+        return None
+    return bn
+
+
+def _shift_of(bn):
+    rm = bn.running_mean if bn.track_running_stats else None
+    if rm is not None and rm.dtype == torch.float32 and rm.is_contiguous():
+        return rm
+    return None
+
+
+def _conv_fwd(x, weight, stride, bn):
+    """Own-kernel conv forward; with ``bn`` also the stats slab (thread-local hand-off
+    to the module, which tags the output)."""
+    cv = _native.require().conv
+    if bn is None:
+        return cv.conv_fwd(x, weight, stride)
+    shift = _shift_of(bn)
+    y, slab = cv.conv_fwd_stats(x, weight, stride, shift)
+    _TLS.slab = (slab, shift, bn)
+    return y
+
+
+def _tag_stats(y):
+    ent = getattr(_TLS, "slab", None)
+    if ent is not None:
+        _TLS.slab = None
+        y._amd_bn_stats = ent
+    return y
+
+
 class Conv1x1GemmFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, bn=None):
         ctx.save_for_backward(x, weight)
         n, ci, h, w = x.shape
         if ctx.needs_input_grad[0] and _own_1x1(x.dtype, weight.shape[0], ci, n * h * w) \
                 and weight.dtype == torch.bfloat16:
             _register_prep(weight)  # its dgrad runs on the own kernel with W^T
-        return _conv1x1_fwd(x, weight)
+        return _conv1x1_fwd(x, weight, bn)
 
     @staticmethod
     def backward(ctx, dy):
@@ -250,7 +314,7 @@ class Conv1x1GemmFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
                           .view(weight.shape), dy, x)
-        return dx, dw
+        return dx, dw, None
 
 
 class Conv1x1SkipFunction(torch.autograd.Function):
@@ -262,9 +326,9 @@ class Conv1x1SkipFunction(torch.autograd.Function):
     would otherwise launch)."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, bn=None):
         ctx.save_for_backward(x, weight)
-        return _conv1x1_fwd(x, weight), x.view_as(x)
+        return _conv1x1_fwd(x, weight, bn), x.view_as(x)
 
     @staticmethod
     def backward(ctx, dy, dskip):
@@ -291,7 +355,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1] and dy is not None:
             dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
                           .view(weight.shape), dy, x)
-        return dx, dw
+        return dx, dw, None
 
 
 class Conv1x1Stride2Function(torch.autograd.Function):
@@ -302,11 +366,11 @@ class Conv1x1Stride2Function(torch.autograd.Function):
     gradient is the per-tap split-K kernel with one tap."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, bn=None):
         ctx.save_for_backward(x, weight)
         if ctx.needs_input_grad[0]:
             _register_prep(weight)
-        return _native.require().conv.conv_fwd(x, weight, 2)
+        return _conv_fwd(x, weight, 2, bn)
 
     @staticmethod
     def backward(ctx, dy):
@@ -320,7 +384,7 @@ class Conv1x1Stride2Function(torch.autograd.Function):
             dx = cv.conv_dgrad_s2(dy, _transpose_1x1(weight), x.size(2), x.size(3))
         if ctx.needs_input_grad[1]:
             dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1), dy, x)
-        return dx, dw
+        return dx, dw, None
 
 
 class Conv2d1x1(nn.Conv2d):
@@ -332,16 +396,17 @@ class Conv2d1x1(nn.Conv2d):
 
     def forward(self, x):
         if self._gemm_ok(x):
-            return Conv1x1GemmFunction.apply(x, self.weight)
+            return _tag_stats(Conv1x1GemmFunction.apply(x, self.weight, _stats_bn(self, x)))
         if self._strided_ok(x):
-            return Conv1x1Stride2Function.apply(x, self.weight)
+            return _tag_stats(Conv1x1Stride2Function.apply(x, self.weight, _stats_bn(self, x)))
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
                         self.groups)
 
     def forward_with_skip(self, x):
         """(conv(x), x) with the residual-gradient add fused into the dgrad GEMM."""
         if self._gemm_ok(x):
-            return Conv1x1SkipFunction.apply(x, self.weight)
+            y, skip = Conv1x1SkipFunction.apply(x, self.weight, _stats_bn(self, x))
+            return _tag_stats(y), skip
         return self.forward(x), x
 
     def _strided_ok(self, x):
@@ -420,12 +485,12 @@ class Conv3x3Function(torch.autograd.Function):
     (per-tap split-K kernel)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride):
+    def forward(ctx, x, weight, stride, bn=None):
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         if ctx.needs_input_grad[0] and _USE_ROT_KERNEL:
             _register_prep(weight)
-        return _native.require().conv.conv_fwd(x, weight, stride)
+        return _conv_fwd(x, weight, stride, bn)
 
     @staticmethod
     def backward(ctx, dy):
@@ -452,7 +517,7 @@ class Conv3x3Function(torch.autograd.Function):
                 dw = torch.ops.aten.convolution_backward(
                     dy, x, weight, None, (stride, stride), (1, 1), (1, 1), False, (0, 0), 1,
                     (False, True, False))[1]
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class Conv2d3x3(nn.Conv2d):
@@ -471,7 +536,7 @@ class Conv2d3x3(nn.Conv2d):
                 and x.is_contiguous(memory_format=torch.channels_last) and self.groups == 1
                 and self.in_channels % 64 == 0 and self.out_channels % 64 == 0
                 and self.dilation == (1, 1) and self.padding == (1, 1)):
-            return Conv3x3Function.apply(x, self.weight, st)
+            return _tag_stats(Conv3x3Function.apply(x, self.weight, st, _stats_bn(self, x)))
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
                         self.groups)
 

@@ -90,8 +90,16 @@ class SyncBatchNorm(_BatchNorm):
         if input.dim() < 2:
             raise ValueError("expected at least 2D input (got {}D input)".format(input.dim()))
 
+    def _amd_accepts_slab(self):
+        """Can take statistics from the producing conv's epilogue (ops/conv.py): the
+        fused path (native kernels, NCHW-shaped input) in training mode."""
+        return (self.training and not self.channel_last and _native.available()
+                and (self.momentum is not None or not self.track_running_stats))
+
     def forward(self, input, z=None):
         self._check_input_dim(input)
+        from ..ops.batch_norm import take_slab
+        slab, shift = take_slab(input, self)
         channel_last = self.channel_last if input.dim() != 2 else False
         if (not self.training and self.track_running_stats and not channel_last
                 and not self.fuse_relu and z is None):
@@ -129,7 +137,7 @@ class SyncBatchNorm(_BatchNorm):
                                        self.running_mean if self.track_running_stats else None,
                                        self.running_var if self.track_running_stats else None,
                                        self.eps, exponential_average_factor, pg, self.fuse_relu,
-                                       channel_last, nbt, force)
+                                       channel_last, nbt, force, slab, shift)
 
 
 def set_syncbn_force_collectives(module, on=True):

@@ -377,6 +377,61 @@ __global__ void __launch_bounds__(kBNThreads)
   }
 }
 
+
+// ---------------------------------------------------------------- statistics from a
+// producer's epilogue (conv_igemm.hip conv_tap_k with a stats slab): the conv wrote,
+// per output channel, the shifted sums of its M-tiles channel-major,
+// slab[c][0|1][S]; one workgroup per channel (or a wave per channel for short slabs)
+// sums them in a fixed order (fp64 in the final combine) and produces the same
+// outputs as stats_finalize: mean (+ biased var | invstd), running-stat update,
+// num_batches_tracked += 1.
+template <int WPC>  // waves per channel
+__global__ void __launch_bounds__(kBNThreads)
+    stats_from_slab_k(const float* __restrict__ slab, int S, int C, int64_t count,
+                      const float* __restrict__ shift, BNStatsOut out) {
+  constexpr int CPB = (kBNThreads / kWave) / WPC;  // channels per workgroup
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int c = blockIdx.x * CPB + wid / WPC;
+  const int t = (wid % WPC) * kWave + lane;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    const float* p = slab + (int64_t)c * 2 * S;
+    for (int i = t; i < S; i += WPC * kWave) {
+      a += p[i];
+      b += p[S + i];
+    }
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  __shared__ float red[kBNThreads / kWave][2];
+  if (lane == 0) {
+    red[wid][0] = a;
+    red[wid][1] = b;
+  }
+  __syncthreads();
+  if (c >= C || (wid % WPC) != 0 || lane != 0) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int w = 0; w < WPC; ++w) {
+    s1 += red[wid + w][0];
+    s2 += red[wid + w][1];
+  }
+  const float sh = shift ? shift[c] : 0.f;   // read before running_mean is updated
+  const double m = s1 / (double)count;
+  double v = s2 / (double)count - m * m;
+  if (v < 0.0) v = 0.0;
+  const float mean = (float)((double)sh + m);
+  out.mean[c] = mean;
+  if (out.var) out.var[c] = (float)v;
+  if (out.invstd) out.invstd[c] = rsqrtf((float)v + out.eps);
+  if (out.running_mean) {
+    const double unb = count > 1 ? v * (double)count / (double)(count - 1) : v;
+    out.running_mean[c] = (1.f - out.momentum) * out.running_mean[c] + out.momentum * mean;
+    out.running_var[c] = (1.f - out.momentum) * out.running_var[c] + out.momentum * (float)unb;
+  }
+  if (out.nbt && c == 0) *out.nbt += 1;
+  if (out.count_out && c == 0) *out.count_out = out.count_val;
+}
+
 template <typename F>
 void vec_dispatch(bool vec, F&& f) {
   if (vec) f(std::true_type{});
@@ -408,6 +463,43 @@ void bn_get_tuning(int* o) {
 }
 
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec) { return reduce_splits(M, ngeom(C, vec)); }
+
+void bn_stats_from_slab(const float* slab, int S, int64_t C, int64_t count, const float* shift,
+                        const BNStatsOut& out, hipStream_t st) {
+  if (S >= 1024) {  // a workgroup per channel
+    hipLaunchKernelGGL((stats_from_slab_k<4>), dim3((unsigned)C), dim3(kBNThreads), 0, st, slab,
+                       S, (int)C, count, shift, out);
+  } else {          // a wave per channel
+    hipLaunchKernelGGL((stats_from_slab_k<1>), dim3((unsigned)((C + 3) / 4)), dim3(kBNThreads), 0,
+                       st, slab, S, (int)C, count, shift, out);
+  }
+}
+
+void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
+                         float* mean, float* invstd, float* running_mean, float* running_var,
+                         long long* nbt, float eps, float momentum, hipStream_t st) {
+  BNStatsOut o{};
+  o.mean = mean;
+  o.var = nullptr;
+  o.invstd = invstd;
+  o.running_mean = running_mean;
+  o.running_var = running_var;
+  o.nbt = nbt;
+  o.eps = eps;
+  o.momentum = momentum;
+  bn_stats_from_slab(slab, S, C, count, shift, o, st);
+}
+
+void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
+                          float* packed, hipStream_t st) {
+  BNStatsOut o{};
+  o.mean = packed;
+  o.var = packed + C;
+  o.invstd = nullptr;
+  o.count_out = packed + 2 * C;
+  o.count_val = (float)count;
+  bn_stats_from_slab(slab, S, C, count, shift, o, st);
+}
 
 void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
                 hipStream_t st) {

@@ -103,7 +103,8 @@ struct ConvGeom {
 template <int MODE, int BM, int BN, int WM, int WN, int NB>
 __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024) ? 1 : 2)
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
-               bf16_t* __restrict__ y, ConvGeom g) {
+               bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
+               const float* __restrict__ shift) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -242,6 +243,41 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-byte chunks per output row
   constexpr bool dense = MODE == kFwd3 || MODE == kFwd1;
+  if constexpr (dense) {
+    if (slab) {
+      // BatchNorm statistics of this output tile for the BN that consumes y (the
+      // stats pass over y disappears): per channel, the shifted sums sum(v - s) and
+      // sum((v - s)^2) over the tile's valid rows, from the bf16-ROUNDED values
+      // staged in LDS (exactly what y holds), shift s = that BN's running mean.
+      // Written channel-major, slab[c][0|1][m-tile], so the finalize kernel reads
+      // each channel's partials contiguously (deterministic fixed-order sums).
+      constexpr int RG = kCT / BN, RPG = BM / RG;
+      const int col = tid % BN, rg = tid / BN;
+      const int nv = M - m0 < BM ? M - m0 : BM;
+      const float sh = shift ? shift[n0 + col] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+      const int r0 = rg * RPG, r1 = r0 + RPG < nv ? r0 + RPG : nv;
+      for (int r = r0; r < r1; ++r) {
+        const float d = (float)T[r * BN + col] - sh;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+      }
+      float* red = reinterpret_cast<float*>(lds + BM * BN * 2);
+      red[tid] = s1;
+      red[kCT + tid] = s2;
+      __syncthreads();
+      if (rg == 0) {
+#pragma unroll
+        for (int q = 1; q < RG; ++q) {
+          s1 += red[q * BN + col];
+          s2 += red[kCT + q * BN + col];
+        }
+        const int64_t S = gridDim.x;
+        slab[((int64_t)(n0 + col) * 2) * S + mt] = s1;
+        slab[((int64_t)(n0 + col) * 2 + 1) * S + mt] = s2;
+      }
+    }
+  }
   for (int c = tid; c < BM * CPR; c += kCT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
@@ -272,25 +308,25 @@ static int conv_bm_choice() {
 
 template <int MODE>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
-                     hipStream_t st) {
+                     hipStream_t st, float* slab = nullptr, const float* shift = nullptr) {
   if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
   if (big == 3) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
   } else if (big) {
     const dim3 grid((g.M + 255) / 256, g.NC / 128, nclasses);
     if (big == 2)
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
     else
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g);
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
   } else {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3>), grid, dim3(kCT), 0, st, a, w, y, g);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
   }
 }
 
@@ -999,15 +1035,24 @@ void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipSt
                      static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin, 1);
 }
 
+int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t M = (int64_t)N * Ho * Wo;
+  const int big = Cout % 128 == 0 ? conv_bm_choice() : 0;  // launch_conv_tap's M tile
+  const int bm = big == 1 || big == 2 ? 256 : kBM;
+  return (int)((M + bm - 1) / bm);
+}
+
 void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
-                   int ksize, int stride, hipStream_t st) {
+                   int ksize, int stride, hipStream_t st, float* stats_slab,
+                   const float* stats_shift) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const ConvGeom g{Ho, Wo, H, W, stride, Ho, Wo, 1, Cin, Cout, N * Ho * Wo, ksize * ksize * Cin};
   const auto* xp = static_cast<const bf16_t*>(x);
   const auto* wp = static_cast<const bf16_t*>(w);
   auto* yp = static_cast<bf16_t*>(y);
-  if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st);
-  else launch_conv_tap<kFwd1>(xp, wp, yp, g, st);
+  if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st, stats_slab, stats_shift);
+  else launch_conv_tap<kFwd1>(xp, wp, yp, g, st, stats_slab, stats_shift);
 }
 
 // Data gradient of a stride-2 conv (3x3 pad 1 or 1x1 pad 0; H = 2*Ho, W = 2*Wo), one

@@ -108,6 +108,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pool.def("max_fwd_bn", &maxpool2d_nhwc_bn_fwd_op);
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
   conv.def("conv_fwd", &conv_nhwc_fwd_op, py::arg("x"), py::arg("w"), py::arg("stride") = 1);
+  conv.def("conv_fwd_stats", &conv_nhwc_fwd_stats_op, py::arg("x"), py::arg("w"),
+           py::arg("stride") = 1, py::arg("shift") = py::none());
   conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);
   conv.def("conv_wgrad", &conv_nhwc_wgrad_op, py::arg("dy"), py::arg("x"), py::arg("out_dtype"),
            py::arg("algo") = 0, py::arg("stride") = 1, py::arg("ksize") = 3);
@@ -129,6 +131,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("eps"), py::arg("momentum"), py::arg("z"), py::arg("relu"),
          py::arg("want_mask") = false);
   bn.def("apply_mask", &bn_apply_mask_op);
+  bn.def("slab_train_stats", &bn_slab_train_stats_op, py::arg("slab"), py::arg("count"),
+         py::arg("shift"), py::arg("running_mean"), py::arg("running_var"), py::arg("nbt"),
+         py::arg("eps"), py::arg("momentum"));
+  bn.def("slab_packed_stats", &bn_slab_packed_stats_op, py::arg("slab"), py::arg("count"),
+         py::arg("shift"));
   bn.def("set_tuning", &bn_set_tuning, py::arg("red_rpt") = -1, py::arg("red_cap") = -1,
          py::arg("red_min") = -1, py::arg("elem_rpt") = -1, py::arg("elem_cap") = -1,
          py::arg("elem_min") = -1);

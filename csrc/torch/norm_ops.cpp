@@ -639,4 +639,55 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
 int bn_persist_error_op() { return bn_persist_error(); }
 void bn_persist_reset_op() { bn_persist_reset(); }
 
+std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64_t count,
+                                                          OptT shift, OptT running_mean,
+                                                          OptT running_var, OptT nbt,
+                                                          double eps, double momentum) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
+                  slab.scalar_type() == at::kFloat && slab.is_contiguous(),
+              "bn slab stats: fp32 [C][2][S] slab expected");
+  const int64_t C = slab.size(0), S = slab.size(2);
+  auto f32 = [&](const OptT& t, const char* what) -> float* {
+    if (!has(t)) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C &&
+                    t->is_cuda(),
+                "bn slab stats: ", what, " must be a contiguous fp32 [C] GPU tensor");
+    return t->data_ptr<float>();
+  };
+  const float* sp = f32(shift, "shift");
+  float* rm = f32(running_mean, "running_mean");
+  float* rv = f32(running_var, "running_var");
+  long long* nb = nullptr;
+  if (has(nbt)) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "nbt: int64 GPU tensor");
+    nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  auto fopt = slab.options();
+  at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  bn_slab_train_stats(slab.data_ptr<float>(), (int)S, C, count, sp, mean.data_ptr<float>(),
+                      invstd.data_ptr<float>(), rm, rv, nb, (float)eps, (float)momentum,
+                      cur_stream());
+  return {mean, invstd};
+}
+
+at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
+                  slab.scalar_type() == at::kFloat && slab.is_contiguous(),
+              "bn slab stats: fp32 [C][2][S] slab expected");
+  const int64_t C = slab.size(0), S = slab.size(2);
+  const float* sp = nullptr;
+  if (has(shift)) {
+    TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
+                    shift->numel() == C,
+                "bn slab stats: shift must be contiguous fp32 [C]");
+    sp = shift->data_ptr<float>();
+  }
+  at::Tensor packed = at::empty({2 * C + 1}, slab.options());
+  bn_slab_packed_stats(slab.data_ptr<float>(), (int)S, C, count, sp, packed.data_ptr<float>(),
+                       cur_stream());
+  return packed;
+}
+
 }  // namespace amd

@@ -95,6 +95,38 @@ at::Tensor conv_nhwc_fwd_op(at::Tensor x, at::Tensor w, int64_t stride) {
   return y;
 }
 
+std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tensor w,
+                                                          int64_t stride,
+                                                          c10::optional<at::Tensor> shift) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4, "conv: 4-D GPU tensors expected");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+              "conv: bf16 only");
+  TORCH_CHECK(stride == 1 || stride == 2, "conv: stride 1 or 2");
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = w.size(0), k = w.size(2);
+  TORCH_CHECK((k == 3 || k == 1) && w.size(3) == k && w.size(1) == Cin, "conv: weight shape");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv: channels must be x64");
+  TORCH_CHECK(N * H * W < (int64_t)1 << 31, "conv: too many pixels");
+  const float* sp = nullptr;
+  if (shift.has_value() && shift->defined()) {
+    TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
+                    shift->numel() == Cout && shift->is_cuda(),
+                "conv stats: shift must be a contiguous fp32 [Cout] GPU tensor");
+    sp = shift->data_ptr<float>();
+  }
+  x = x.contiguous(at::MemoryFormat::ChannelsLast);
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  at::Tensor y = at::empty({N, Cout, Ho, Wo},
+                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int S = conv_fwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)stride);
+  at::Tensor slab = at::empty({Cout, 2, S}, x.options().dtype(at::kFloat));
+  conv_nhwc_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)Cin,
+                (int)Cout, (int)k, (int)stride, cur_stream(), slab.data_ptr<float>(), sp);
+  return {y, slab};
+}
+
 at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && wt.dim() == 4, "conv_dgrad_s2: 4-D GPU tensors");

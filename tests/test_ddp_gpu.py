@@ -341,9 +341,16 @@ def test_ddp_side_stream_weight_grads_match_main_stream(pg):
             calls = {"n": 0}
             orig = convmod._SideWgrad.run
 
-            def counting(self, fn, *a, _orig=orig, _calls=calls):
+            modes = []
+
+            def counting(self, fn, *a, _orig=orig, _calls=calls, _modes=modes):
                 if self.mode == "ddp":
                     _calls["n"] += 1
+                p = self.params[0]
+                slot = getattr(p, "_amd_ddp_slot", None)
+                red = slot[0]() if slot else None
+                _modes.append((self.mode, slot is not None, red is not None and
+                               red.async_ready_ok(), p.grad is None))
                 return _orig(self, fn, *a)
             convmod._SideWgrad.run = counting
             grads = []
@@ -359,10 +366,10 @@ def test_ddp_side_stream_weight_grads_match_main_stream(pg):
                 convmod._SideWgrad.run = orig
             torch.cuda.synchronize()
             results[side] = (grads, [p.detach().clone() for p in m.parameters()])
-            used[side] = calls["n"]
+            used[side] = (calls["n"], sorted(set(modes)))
     finally:
         convmod._DDP_SIDE = prev
-    assert used[False] == 0 and used[True] > 0, used
+    assert used[False][0] == 0 and used[True][0] > 0, used
     for it, (a, b) in enumerate(zip(results[False][0], results[True][0])):
         bad = [i for i, (u, v) in enumerate(zip(a, b)) if not torch.equal(u, v)]
         assert not bad, (it, bad)
