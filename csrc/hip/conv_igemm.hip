@@ -100,8 +100,13 @@ struct ConvGeom {
   int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
 };
 
+// NB = 1 (no DMA ring): for 1x1 convs with one or two K-tiles (K = 64 / 128: the
+// ResNet layer1-2 channel-expanding convs) - nothing to overlap inside a workgroup, so
+// the LDS goes to more resident workgroups instead (4 per CU: one's loads overlap
+// another's MFMAs and stores).
 template <int MODE, int BM, int BN, int WM, int WN, int NB>
-__global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024) ? 1 : 2)
+__global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024)
+                                           ? 1 : (NB == 1 ? 4 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
                const float* __restrict__ shift) {
@@ -113,7 +118,10 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   constexpr int AI = BM / 32;      // A wave-instructions (8 rows each) per wave per tile
   constexpr int BI = BN / 32;       // B wave-instructions per wave per tile
   constexpr int G = AI + BI;        // glds per wave per tile (vmcnt units)
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[NB * BUF];
+  // the ring, or the epilogue's bf16 tile + the statistics exchange if larger
+  constexpr int LDS_BYTES = NB * BUF > BM * BN * 2 + 2 * kCT * 4 ? NB * BUF
+                                                                  : BM * BN * 2 + 2 * kCT * 4;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -196,16 +204,23 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
     if (p < KT) CONV_ISSUE(p);
 
   for (int kt = 0; kt < KT; ++kt) {
-    // retire tile kt: leave the (NB-2) younger tiles' DMAs in flight
-    if (kt + NB - 2 < KT) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NB - 2)) : "memory");
-    } else {
+    if constexpr (NB == 1) {
+      if (kt > 0) __syncthreads();  // every wave is done reading the single buffer
+      CONV_ISSUE(kt);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      // retire tile kt: leave the (NB-2) younger tiles' DMAs in flight
+      if (kt + NB - 2 < KT) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NB > 2 ? NB - 2 : 0)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      // the buffer of tile kt+NB-1 was last read at iteration kt-1: every wave has
+      // passed this barrier, so it is free
+      if (kt + NB - 1 < KT) CONV_ISSUE(kt + NB - 1);
     }
-    __builtin_amdgcn_s_barrier();
-    // the buffer of tile kt+NB-1 was last read at iteration kt-1: every wave has
-    // passed this barrier, so it is free
-    if (kt + NB - 1 < KT) CONV_ISSUE(kt + NB - 1);
     const unsigned char* A = lds + (kt % NB) * BUF;
     const unsigned char* B = A + A_BYTES;
 #pragma unroll
@@ -306,6 +321,13 @@ static int conv_bm_choice() {
   return 0;
 }
 
+// 1x1 forward convs with at most this many 64-channel K-tiles run the NB = 1 variant
+// (APEX_AMD_CONV1X1_NB1 = 0 | 1 | 2 | ..., read per launch for A/B runs)
+static int conv1x1_nb1_max_kt() {
+  const char* e = std::getenv("APEX_AMD_CONV1X1_NB1");
+  return e ? std::atoi(e) : 1;
+}
+
 template <int MODE>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr) {
@@ -321,6 +343,9 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+  } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= conv1x1_nb1_max_kt()) {
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);

@@ -822,15 +822,64 @@ def bench_lamb(args):
             name, n, len(ps), t, bpp * n / (t * 1e-6) / 1e12, bpp))
 
 
+
+def bench_conv1x1_stats(args):
+    """Channel-expanding / reducing 1x1 conv forward feeding a BatchNorm: hipBLASLt GEMM
+    + the BN statistics pass vs the own MFMA kernel writing the statistics in its
+    epilogue (conv_fwd_stats + the slab finalize), and the own kernel alone.  Run with
+    APEX_AMD_CONV1X1_NB1=0/1/2 for the no-ring variant (read per launch)."""
+    from apex_example_amd import _native
+
+    C = _native.require()
+    dev = "cuda"
+    shapes = [(256, 64, 256, 56), (256, 256, 64, 56), (256, 128, 512, 28), (256, 512, 128, 28),
+              (256, 256, 1024, 14), (256, 1024, 256, 14), (256, 512, 2048, 7),
+              (256, 2048, 512, 7), (256, 64, 64, 56)]
+    print("| N,Cin,Cout,HW | MB | hipBLASLt | + stats pass | own | own + epilogue stats + finalize |")
+    print("|---|---|---|---|---|---|")
+    for (n, ci, co, hw) in shapes:
+        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        w = (torch.randn(co, ci, 1, 1, device=dev) * 0.05).to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        M = n * hw * hw
+        x2 = x.permute(0, 2, 3, 1).reshape(M, ci)
+        w2 = w.reshape(co, ci)
+        mb = (M * ci + M * co) * 2 / 1e6
+        rm = torch.zeros(co, device=dev)
+        rv = torch.ones(co, device=dev)
+        y_nhwc = torch.mm(x2, w2.t()).view(n, hw, hw, co).permute(0, 3, 1, 2)
+
+        def gemm_stats():
+            y = torch.mm(x2, w2.t()).view(n, hw, hw, co).permute(0, 3, 1, 2)
+            C.bn.train_stats(y, rm, rv, None, 1e-5, 0.1)
+
+        def own_stats():
+            y, slab = C.conv.conv_fwd_stats(x, w, 1, rm)
+            C.bn.slab_train_stats(slab, M, rm, rm, rv, None, 1e-5, 0.1)
+
+        t_g = timeit(lambda: torch.mm(x2, w2.t()))
+        t_gs = timeit(gemm_stats)
+        t_o = timeit(lambda: C.conv.conv_fwd(x, w, 1))
+        t_os = timeit(own_stats)
+        del y_nhwc
+
+        def bw(t):
+            return "%.0f us (%.2f TB/s)" % (t, mb / 1e6 / (t * 1e-6))
+
+        print("| %d,%d,%d,%d | %.0f | %s | %.0f us | %s | %.0f us |" % (
+            n, ci, co, hw, mb, bw(t_g), t_gs, bw(t_o), t_os), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "lamb",
                              "attn"])
     ap.add_argument("--quick", action="store_true", help="bn-persist: 14x14 / 7x7 shapes only")
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-persist": bench_bn_persist, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
+    {"bn": bench_bn, "bn-persist": bench_bn_persist, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv1x1-stats": bench_conv1x1_stats, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
      "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
