@@ -118,9 +118,9 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   constexpr int AI = BM / 32;      // A wave-instructions (8 rows each) per wave per tile
   constexpr int BI = BN / 32;       // B wave-instructions per wave per tile
   constexpr int G = AI + BI;        // glds per wave per tile (vmcnt units)
-  // the ring, or the epilogue's bf16 tile + the statistics exchange if larger
-  constexpr int LDS_BYTES = NB * BUF > BM * BN * 2 + 2 * kCT * 4 ? NB * BUF
-                                                                  : BM * BN * 2 + 2 * kCT * 4;
+  // the ring, or the epilogue's bf16 tile / statistics exchange if larger
+  constexpr int EPI_BYTES = BM * BN * 2 > 2 * kCT * 8 * 4 ? BM * BN * 2 : 2 * kCT * 8 * 4;
+  constexpr int LDS_BYTES = NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -258,40 +258,19 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-byte chunks per output row
   constexpr bool dense = MODE == kFwd3 || MODE == kFwd1;
-  if constexpr (dense) {
-    if (slab) {
-      // BatchNorm statistics of this output tile for the BN that consumes y (the
-      // stats pass over y disappears): per channel, the shifted sums sum(v - s) and
-      // sum((v - s)^2) over the tile's valid rows, from the bf16-ROUNDED values
-      // staged in LDS (exactly what y holds), shift s = that BN's running mean.
-      // Written channel-major, slab[c][0|1][m-tile], so the finalize kernel reads
-      // each channel's partials contiguously (deterministic fixed-order sums).
-      constexpr int RG = kCT / BN, RPG = BM / RG;
-      const int col = tid % BN, rg = tid / BN;
-      const int nv = M - m0 < BM ? M - m0 : BM;
-      const float sh = shift ? shift[n0 + col] : 0.f;
-      float s1 = 0.f, s2 = 0.f;
-      const int r0 = rg * RPG, r1 = r0 + RPG < nv ? r0 + RPG : nv;
-      for (int r = r0; r < r1; ++r) {
-        const float d = (float)T[r * BN + col] - sh;
-        s1 += d;
-        s2 = fmaf(d, d, s2);
-      }
-      float* red = reinterpret_cast<float*>(lds + BM * BN * 2);
-      red[tid] = s1;
-      red[kCT + tid] = s2;
-      __syncthreads();
-      if (rg == 0) {
+  // BatchNorm statistics of this output tile for the BN that consumes y (its stats
+  // pass over y disappears): a thread's 16-byte chunks all lie in ONE 8-channel
+  // column group (kCT % CPR == 0), so the bf16-ROUNDED values it stores (exactly what
+  // y holds) also feed its per-channel shifted sums sum(v - s), sum((v - s)^2) with
+  // s = that BN's running mean; the row groups are combined through LDS and written
+  // channel-major, slab[c][0|1][m-tile], for the finalize kernel (fixed order).
+  const bool want_stats = dense && slab != nullptr;
+  const int scc = tid % CPR;
+  float s1[8], s2[8], shv[8];
 #pragma unroll
-        for (int q = 1; q < RG; ++q) {
-          s1 += red[q * BN + col];
-          s2 += red[kCT + q * BN + col];
-        }
-        const int64_t S = gridDim.x;
-        slab[((int64_t)(n0 + col) * 2) * S + mt] = s1;
-        slab[((int64_t)(n0 + col) * 2 + 1) * S + mt] = s2;
-      }
-    }
+  for (int i = 0; i < 8; ++i) {
+    s1[i] = s2[i] = 0.f;
+    shv[i] = (want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
   }
   for (int c = tid; c < BM * CPR; c += kCT) {
     const int row = c / CPR, cc = c - row * CPR;
@@ -304,8 +283,43 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
       const int gh = rem / g.GW, gw = rem - gh * g.GW;
       opix = (int64_t)(n * g.YH + gh * g.ys + (z >> 1)) * g.YW + gw * g.ys + (z & 1);
     }
-    *reinterpret_cast<uint4*>(y + opix * g.NC + n0 + cc * 8) =
-        *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+    const uint4 v = *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+    *reinterpret_cast<uint4*>(y + opix * g.NC + n0 + cc * 8) = v;
+    if (want_stats) {
+      const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = __uint_as_float(wv[q] << 16) - shv[2 * q];
+        const float hi = __uint_as_float(wv[q] & 0xffff0000u) - shv[2 * q + 1];
+        s1[2 * q] += lo;
+        s2[2 * q] = fmaf(lo, lo, s2[2 * q]);
+        s1[2 * q + 1] += hi;
+        s2[2 * q + 1] = fmaf(hi, hi, s2[2 * q + 1]);
+      }
+    }
+  }
+  if (want_stats) {
+    constexpr int RGS = kCT / CPR;  // row groups (threads sharing a column group)
+    __syncthreads();                // every thread is done reading the bf16 tile
+    float* red = reinterpret_cast<float*>(lds);
+    const int rg = tid / CPR;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[rg * BN + scc * 8 + i] = s1[i];
+      red[RGS * BN + rg * BN + scc * 8 + i] = s2[i];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float a = 0.f, b = 0.f;
+#pragma unroll 4
+      for (int q = 0; q < RGS; ++q) {
+        a += red[q * BN + tid];
+        b += red[RGS * BN + q * BN + tid];
+      }
+      const int64_t S = gridDim.x;
+      slab[((int64_t)(n0 + tid) * 2) * S + mt] = a;
+      slab[((int64_t)(n0 + tid) * 2 + 1) * S + mt] = b;
+    }
   }
 }
 

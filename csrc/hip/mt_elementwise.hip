@@ -101,6 +101,24 @@ __global__ void __launch_bounds__(kMTThreads) zero_kernel(MTLaunch L) {
   }
 }
 
+// dst = src only when *flag != 0 (the overflow flag of a skipped step): restores the
+// pre-step snapshot of a guarded (non-fused) optimizer without a host round trip
+template <typename T>
+__global__ void __launch_bounds__(kMTThreads) copy_if_kernel(MTLaunch L, const int* flag) {
+  if (*flag == 0) return;
+  TileCtx c = tile_ctx(L);
+  const bool al = c.t->aligned;
+#pragma unroll
+  for (int u = 0; u < kMTUnroll; ++u) {
+    int off = lane_off(u);
+    int cnt = c.n - off;
+    if (cnt <= 0) continue;
+    float v[8];
+    ld<T>(c.t->ptr[0], c.start + off, cnt, al && cnt >= 8, v);
+    st<T>(c.t->ptr[1], c.start + off, cnt, al && cnt >= 8, v);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kMTThreads)
     norm_partials_kernel(MTLaunch L, int max_norm, float* partials, int* noop) {
@@ -201,6 +219,14 @@ void mt_fill_zero(const MTLaunch& L, DType t, hipStream_t st) {
   dispatch1(t, [&](auto tt) {
     using T = decltype(tt);
     hipLaunchKernelGGL((zero_kernel<T>), mt_grid(L), dim3(kMTThreads), 0, st, L);
+  });
+}
+
+void mt_copy_if(const MTLaunch& L, DType t, const int* flag, hipStream_t st) {
+  if (L.nchunks == 0) return;
+  dispatch1(t, [&](auto tt) {
+    using T = decltype(tt);
+    hipLaunchKernelGGL((copy_if_kernel<T>), mt_grid(L), dim3(kMTThreads), 0, st, L, flag);
   });
 }
 

@@ -27,6 +27,8 @@ void mt_check_finite(const MTLaunch& L, DType in, int* noop, hipStream_t st);
 void mt_axpby(const MTLaunch& L, DType x, DType y, DType out, ScaleArg a, ScaleArg b,
               int arg_to_check, int* noop, hipStream_t st);
 void mt_fill_zero(const MTLaunch& L, DType t, hipStream_t st);
+// [src, dst]: dst = src where *flag != 0 (guarded optimizer step restore)
+void mt_copy_if(const MTLaunch& L, DType t, const int* flag, hipStream_t st);
 
 // ----- norms (amp_C.multi_tensor_l2norm / _norm_out / max norm) ------------
 // Per-chunk partials (sum of squares, or max|x| when max_norm) -> partials[nchunks].

@@ -112,6 +112,26 @@ void mt_zero_op(const std::vector<at::Tensor>& list) {
   });
 }
 
+void mt_copy_if_op(at::Tensor flag, const TensorLists& lists) {
+  c10::NoGradGuard no_grad_;
+  if (lists.empty() || lists[0].empty()) return;
+  TORCH_CHECK(lists.size() == 2, "copy_if: [src, dst] lists expected");
+  for (size_t i = 0; i < lists[0].size(); ++i)
+    TORCH_CHECK(lists[0][i].scalar_type() == lists[1][i].scalar_type(),
+                "copy_if: src / dst dtypes must match");
+  bool gpu = mt_validate(lists, 2, 2);
+  if (!gpu) {
+    if (flag.item<int>() != 0)
+      for (size_t i = 0; i < lists[0].size(); ++i) lists[1][i].copy_(lists[0][i]);
+    return;
+  }
+  TORCH_CHECK(flag.scalar_type() == at::kInt && flag.is_cuda(), "copy_if: int32 GPU flag");
+  by_dtype_groups(lists, [&](const std::vector<int>&, const TensorLists& g) {
+    const MTPlan& P = mt_plan(g);
+    mt_copy_if(P.L, dtype_of(g[0][0]), flag.data_ptr<int>(), cur_stream());
+  });
+}
+
 std::tuple<at::Tensor, at::Tensor> mt_norm_op(at::Tensor noop, const std::vector<at::Tensor>& list,
                                               bool per_tensor, bool max_norm) {
   c10::NoGradGuard no_grad_;  // optimizer / scaler state is never differentiated

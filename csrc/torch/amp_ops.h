@@ -17,6 +17,7 @@ void mt_check_finite_op(at::Tensor noop, const std::vector<at::Tensor>& list);
 void mt_axpby_op(at::Tensor noop, const TensorLists& lists, double a, OptT a_t, bool a_inv,
                  double b, OptT b_t, bool b_inv, int64_t arg_to_check);
 void mt_zero_op(const std::vector<at::Tensor>& list);
+void mt_copy_if_op(at::Tensor flag, const TensorLists& lists);
 std::tuple<at::Tensor, at::Tensor> mt_norm_op(at::Tensor noop, const std::vector<at::Tensor>& list,
                                               bool per_tensor, bool max_norm);
 void mt_sgd_op(at::Tensor noop, const TensorLists& lists, double wd, double momentum,

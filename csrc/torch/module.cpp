@@ -52,6 +52,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mt.def("check_finite", &mt_check_finite_op);
   mt.def("axpby", &mt_axpby_op);
   mt.def("zero", &mt_zero_op);
+  mt.def("copy_if", &mt_copy_if_op);
   mt.def("norm", &mt_norm_op, py::arg("noop"), py::arg("list"), py::arg("per_tensor") = false,
          py::arg("max_norm") = false);
   mt.def("sgd", &mt_sgd_op);
