@@ -124,10 +124,14 @@ def _patch_forward(model, input_caster, output_caster):
     model._amp_old_forward = old_fwd
 
 
-def _all_fused(optimizers):
+def _FUSED():
     from ..optimizers import _FUSED_TYPES
 
-    return len(optimizers) > 0 and all(isinstance(o, _FUSED_TYPES) for o in optimizers)
+    return _FUSED_TYPES
+
+
+def _all_fused(optimizers):
+    return len(optimizers) > 0 and all(isinstance(o, _FUSED()) for o in optimizers)
 
 
 def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs=None,
@@ -198,10 +202,18 @@ def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs
     if device is None:
         device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
 
+    from . import _guard
+
+    guard = [not isinstance(o, _FUSED()) and _guard.guardable(o) for o in optimizers]
     if sync_free is None:
-        sync_free = (device.type == "cuda" and _all_fused(optimizers)
-                     and properties.loss_scale == "dynamic")
+        # fused optimizers skip an overflowed step inside their kernels; any other
+        # torch.optim optimizer gets the device-side step guard (amp/_guard.py)
+        sync_free = (device.type == "cuda" and len(optimizers) > 0
+                     and properties.loss_scale == "dynamic"
+                     and all(isinstance(o, _FUSED()) or g for o, g in zip(optimizers, guard)))
     for i, optimizer in enumerate(optimizers):
+        if sync_free and guard[i]:
+            _guard.install(optimizer)   # before amp wraps step: the guard sits innermost
         optimizers[i] = _process_optimizer(optimizer, properties)
 
     _amp_state.loss_scalers = []

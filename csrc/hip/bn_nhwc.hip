@@ -379,57 +379,58 @@ __global__ void __launch_bounds__(kBNThreads)
 
 
 // ---------------------------------------------------------------- statistics from a
-// producer's epilogue (conv_igemm.hip conv_tap_k with a stats slab): the conv wrote,
-// per output channel, the shifted sums of its M-tiles channel-major,
-// slab[c][0|1][S]; one workgroup per channel (or a wave per channel for short slabs)
-// sums them in a fixed order (fp64 in the final combine) and produces the same
-// outputs as stats_finalize: mean (+ biased var | invstd), running-stat update,
-// num_batches_tracked += 1.
-template <int WPC>  // waves per channel
+// producer's epilogue (conv_igemm.hip conv_tap_k with a stats slab): the conv wrote
+// the shifted sums of each M-tile tile-major, slab[S][0|1][C] (one coalesced row per
+// workgroup).  Long slabs are first folded 128 rows at a time (a column per thread,
+// coalesced rows); the final kernel sums the remaining rows per channel in a fixed
+// order and produces what stats_finalize does: mean (+ biased var | invstd),
+// running-stat update, num_batches_tracked += 1.
+constexpr int kFoldRows = 128;
+
 __global__ void __launch_bounds__(kBNThreads)
-    stats_from_slab_k(const float* __restrict__ slab, int S, int C, int64_t count,
+    slab_fold_k(const float* __restrict__ slab, int S, int C2, float* __restrict__ out) {
+  const int col = blockIdx.x * kBNThreads + threadIdx.x;
+  if (col >= C2) return;
+  const int r0 = blockIdx.y * kFoldRows;
+  const int r1 = r0 + kFoldRows < S ? r0 + kFoldRows : S;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    a0 += slab[(int64_t)r * C2 + col];
+    a1 += slab[(int64_t)(r + 1) * C2 + col];
+    a2 += slab[(int64_t)(r + 2) * C2 + col];
+    a3 += slab[(int64_t)(r + 3) * C2 + col];
+  }
+  for (; r < r1; ++r) a0 += slab[(int64_t)r * C2 + col];
+  out[(int64_t)blockIdx.y * C2 + col] = (a0 + a1) + (a2 + a3);
+}
+
+template <int CH>
+__global__ void __launch_bounds__(kBNThreads)
+    stats_from_rows_k(const float* __restrict__ slab, int S, int C, int64_t count,
                       const float* __restrict__ shift, BNStatsOut out) {
-  constexpr int CPB = (kBNThreads / kWave) / WPC;  // channels per workgroup
-  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int c = blockIdx.x * CPB + wid / WPC;
-  const int t = (wid % WPC) * kWave + lane;
-  float a = 0.f, b = 0.f;
-  if (c < C) {
-    const float* p = slab + (int64_t)c * 2 * S;
-    for (int i = t; i < S; i += WPC * kWave) {
-      a += p[i];
-      b += p[S + i];
+  __shared__ float sums[2 * CH];
+  const int c0 = blockIdx.x * CH;
+  slab_sum<CH>(slab, S, C, c0, sums);
+  const int k = threadIdx.x;
+  if (k < CH && c0 + k < C) {
+    const int c = c0 + k;
+    const float sh = shift ? shift[c] : 0.f;  // read before running_mean is updated
+    const double m = (double)sums[k] / (double)count;
+    double v = (double)sums[CH + k] / (double)count - m * m;
+    if (v < 0.0) v = 0.0;
+    const float mean = (float)((double)sh + m);
+    out.mean[c] = mean;
+    if (out.var) out.var[c] = (float)v;
+    if (out.invstd) out.invstd[c] = rsqrtf((float)v + out.eps);
+    if (out.running_mean) {
+      const double unb = count > 1 ? v * (double)count / (double)(count - 1) : v;
+      out.running_mean[c] = (1.f - out.momentum) * out.running_mean[c] + out.momentum * mean;
+      out.running_var[c] = (1.f - out.momentum) * out.running_var[c] + out.momentum * (float)unb;
     }
+    if (out.nbt && c == 0) *out.nbt += 1;
+    if (out.count_out && c == 0) *out.count_out = out.count_val;
   }
-  a = wave_sum(a);
-  b = wave_sum(b);
-  __shared__ float red[kBNThreads / kWave][2];
-  if (lane == 0) {
-    red[wid][0] = a;
-    red[wid][1] = b;
-  }
-  __syncthreads();
-  if (c >= C || (wid % WPC) != 0 || lane != 0) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int w = 0; w < WPC; ++w) {
-    s1 += red[wid + w][0];
-    s2 += red[wid + w][1];
-  }
-  const float sh = shift ? shift[c] : 0.f;   // read before running_mean is updated
-  const double m = s1 / (double)count;
-  double v = s2 / (double)count - m * m;
-  if (v < 0.0) v = 0.0;
-  const float mean = (float)((double)sh + m);
-  out.mean[c] = mean;
-  if (out.var) out.var[c] = (float)v;
-  if (out.invstd) out.invstd[c] = rsqrtf((float)v + out.eps);
-  if (out.running_mean) {
-    const double unb = count > 1 ? v * (double)count / (double)(count - 1) : v;
-    out.running_mean[c] = (1.f - out.momentum) * out.running_mean[c] + out.momentum * mean;
-    out.running_var[c] = (1.f - out.momentum) * out.running_var[c] + out.momentum * (float)unb;
-  }
-  if (out.nbt && c == 0) *out.nbt += 1;
-  if (out.count_out && c == 0) *out.count_out = out.count_val;
 }
 
 template <typename F>
@@ -464,20 +465,32 @@ void bn_get_tuning(int* o) {
 
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec) { return reduce_splits(M, ngeom(C, vec)); }
 
+int64_t bn_slab_workspace(int S, int64_t C) {
+  return S > 2 * kFoldRows ? (int64_t)((S + kFoldRows - 1) / kFoldRows) * 2 * C : 0;
+}
+
 void bn_stats_from_slab(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                        const BNStatsOut& out, hipStream_t st) {
-  if (S >= 1024) {  // a workgroup per channel
-    hipLaunchKernelGGL((stats_from_slab_k<4>), dim3((unsigned)C), dim3(kBNThreads), 0, st, slab,
-                       S, (int)C, count, shift, out);
-  } else {          // a wave per channel
-    hipLaunchKernelGGL((stats_from_slab_k<1>), dim3((unsigned)((C + 3) / 4)), dim3(kBNThreads), 0,
-                       st, slab, S, (int)C, count, shift, out);
+                        const BNStatsOut& out, float* ws, hipStream_t st) {
+  const float* rows = slab;
+  int R = S;
+  if (S > 2 * kFoldRows) {  // fold 128 rows at a time first
+    R = (S + kFoldRows - 1) / kFoldRows;
+    const int C2 = (int)(2 * C);
+    hipLaunchKernelGGL(slab_fold_k, dim3((unsigned)((C2 + kBNThreads - 1) / kBNThreads),
+                                         (unsigned)R),
+                       dim3(kBNThreads), 0, st, slab, S, C2, ws);
+    rows = ws;
   }
+  fin_dispatch(C, [&](auto ch) {
+    constexpr int CH = decltype(ch)::value;
+    hipLaunchKernelGGL((stats_from_rows_k<CH>), dim3((unsigned)((C + CH - 1) / CH)),
+                       dim3(kBNThreads), 0, st, rows, R, (int)C, count, shift, out);
+  });
 }
 
 void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
                          float* mean, float* invstd, float* running_mean, float* running_var,
-                         long long* nbt, float eps, float momentum, hipStream_t st) {
+                         long long* nbt, float eps, float momentum, float* ws, hipStream_t st) {
   BNStatsOut o{};
   o.mean = mean;
   o.var = nullptr;
@@ -487,18 +500,18 @@ void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, con
   o.nbt = nbt;
   o.eps = eps;
   o.momentum = momentum;
-  bn_stats_from_slab(slab, S, C, count, shift, o, st);
+  bn_stats_from_slab(slab, S, C, count, shift, o, ws, st);
 }
 
 void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                          float* packed, hipStream_t st) {
+                          float* packed, float* ws, hipStream_t st) {
   BNStatsOut o{};
   o.mean = packed;
   o.var = packed + C;
   o.invstd = nullptr;
   o.count_out = packed + 2 * C;
   o.count_val = (float)count;
-  bn_stats_from_slab(slab, S, C, count, shift, o, st);
+  bn_stats_from_slab(slab, S, C, count, shift, o, ws, st);
 }
 
 void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,

@@ -197,6 +197,14 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
+  // epilogue BN statistics (see the store loop): this thread's 8 channels' shift,
+  // loaded now so the latency hides under the K loop
+  constexpr int CPR = BN / 8;  // 16-byte chunks per output row
+  const bool want_stats = (MODE == kFwd3 || MODE == kFwd1) && slab != nullptr;
+  const int scc = tid % CPR;
+  float shv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) shv[i] = (want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
 
   // prologue: NB-1 tiles in flight
 #pragma unroll
@@ -256,22 +264,16 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
         T[row * BN + col] = (bf16_t)acc[i][j][e];
       }
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 16-byte chunks per output row
   constexpr bool dense = MODE == kFwd3 || MODE == kFwd1;
   // BatchNorm statistics of this output tile for the BN that consumes y (its stats
   // pass over y disappears): a thread's 16-byte chunks all lie in ONE 8-channel
   // column group (kCT % CPR == 0), so the bf16-ROUNDED values it stores (exactly what
   // y holds) also feed its per-channel shifted sums sum(v - s), sum((v - s)^2) with
   // s = that BN's running mean; the row groups are combined through LDS and written
-  // channel-major, slab[c][0|1][m-tile], for the finalize kernel (fixed order).
-  const bool want_stats = dense && slab != nullptr;
-  const int scc = tid % CPR;
-  float s1[8], s2[8], shv[8];
+  // tile-major, slab[m-tile][0|1][c], for the finalize kernels (fixed order).
+  float s1[8], s2[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    s1[i] = s2[i] = 0.f;
-    shv[i] = (want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
-  }
+  for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
   for (int c = tid; c < BM * CPR; c += kCT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
@@ -316,9 +318,10 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
         a += red[q * BN + tid];
         b += red[RGS * BN + q * BN + tid];
       }
-      const int64_t S = gridDim.x;
-      slab[((int64_t)(n0 + tid) * 2) * S + mt] = a;
-      slab[((int64_t)(n0 + tid) * 2 + 1) * S + mt] = b;
+      // tile-major [S][2][C]: one coalesced row segment per workgroup
+      float* row = slab + (int64_t)mt * 2 * g.NC;
+      row[n0 + tid] = a;
+      row[g.NC + n0 + tid] = b;
     }
   }
 }

@@ -248,7 +248,7 @@ void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int 
 // 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64
 bool conv3x3_nhwc_supported(int Cin, int Cout);
 // y is N x Ho x Wo x Cout, Ho = (H-1)/stride + 1; w is [Cout][k*k][Cin]
-// stats_slab (optional, fp32 [Cout][2][conv_fwd_mtiles(...)]): per M-tile shifted sums
+// stats_slab (optional, fp32 [conv_fwd_mtiles(...)][2][Cout]): per M-tile shifted sums
 // sum(y - shift[c]), sum((y - shift[c])^2) of the bf16 output for the consuming BN
 void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
                    int ksize, int stride, hipStream_t st, float* stats_slab = nullptr,
@@ -256,11 +256,13 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride);
 // BatchNorm statistics from such a slab: local training mode (mean, invstd, running
 // stats, num_batches_tracked) or SyncBN's packed [mean | biased var | count]
+// (slab is tile-major [S][2][C]; ws: bn_slab_workspace(S, C) floats, may be 0)
+int64_t bn_slab_workspace(int S, int64_t C);
 void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
                          float* mean, float* invstd, float* running_mean, float* running_var,
-                         long long* nbt, float eps, float momentum, hipStream_t st);
+                         long long* nbt, float eps, float momentum, float* ws, hipStream_t st);
 void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                          float* packed, hipStream_t st);
+                          float* packed, float* ws, hipStream_t st);
 // data gradient of a stride-2 conv (H, W even); wt = rotated 3x3 filter / W^T for 1x1
 void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, int W, int Cin,
                         int Cout, int ksize, hipStream_t st);

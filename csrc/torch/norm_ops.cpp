@@ -646,8 +646,8 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
-              "bn slab stats: fp32 [C][2][S] slab expected");
-  const int64_t C = slab.size(0), S = slab.size(2);
+              "bn slab stats: fp32 [S][2][C] slab expected");
+  const int64_t S = slab.size(0), C = slab.size(2);
   auto f32 = [&](const OptT& t, const char* what) -> float* {
     if (!has(t)) return nullptr;
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C &&
@@ -665,9 +665,10 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
   }
   auto fopt = slab.options();
   at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, fopt);
   bn_slab_train_stats(slab.data_ptr<float>(), (int)S, C, count, sp, mean.data_ptr<float>(),
                       invstd.data_ptr<float>(), rm, rv, nb, (float)eps, (float)momentum,
-                      cur_stream());
+                      ws.data_ptr<float>(), cur_stream());
   return {mean, invstd};
 }
 
@@ -675,8 +676,8 @@ at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
-              "bn slab stats: fp32 [C][2][S] slab expected");
-  const int64_t C = slab.size(0), S = slab.size(2);
+              "bn slab stats: fp32 [S][2][C] slab expected");
+  const int64_t S = slab.size(0), C = slab.size(2);
   const float* sp = nullptr;
   if (has(shift)) {
     TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
@@ -685,8 +686,9 @@ at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift) {
     sp = shift->data_ptr<float>();
   }
   at::Tensor packed = at::empty({2 * C + 1}, slab.options());
+  at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, slab.options());
   bn_slab_packed_stats(slab.data_ptr<float>(), (int)S, C, count, sp, packed.data_ptr<float>(),
-                       cur_stream());
+                       ws.data_ptr<float>(), cur_stream());
   return packed;
 }
 

@@ -75,7 +75,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
 int bn_persist_error_op();
 void bn_persist_reset_op();
 
-// BatchNorm statistics from a producer's channel-major stats slab [C][2][S]
+// BatchNorm statistics from a producer's tile-major stats slab [S][2][C]
 // (conv.conv_fwd_stats): local training mode -> (mean, invstd) with the running-stat
 // and num_batches_tracked updates; packed mode -> [mean | biased var | count] (SyncBN)
 std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64_t count,

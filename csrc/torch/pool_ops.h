@@ -20,7 +20,7 @@ at::Tensor gap_nhwc_bwd_op(at::Tensor dy, int64_t H, int64_t W);
 // 3x3 / 1x1 convs (stride 1 or 2), NHWC bf16, implicit GEMM on MFMA (conv_igemm.hip)
 at::Tensor conv_nhwc_fwd_op(at::Tensor x, at::Tensor w, int64_t stride);
 // forward conv that also writes the consuming BatchNorm's per-tile statistics:
-// returns (y, slab [Cout][2][S] fp32); shift: that BN's running mean (or None)
+// returns (y, slab [S][2][Cout] fp32); shift: that BN's running mean (or None)
 std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tensor w,
                                                           int64_t stride,
                                                           c10::optional<at::Tensor> shift);
