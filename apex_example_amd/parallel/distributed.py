@@ -13,11 +13,16 @@ is the C++ ``_C.reducer.Reducer``:
 * the end-of-backward epilogue makes the compute stream wait on every bucket
   and raises if a bucket was never reduced.
 
-Bucket size (``message_size``, elements): Apex's default 1e7 elements.  On an
-8x MI355X node every GPU talks to the 7 others over point-to-point xGMI links
-(~153 GB/s each); RCCL's ring/tree channels spread one collective over those
-links, so a bucket only needs to be large enough to amortise RCCL's per-call
-latency (tens of us) - see docs/DDP_TUNING.md and tools/allreduce_sweep.py.
+Bucket size (``message_size``, elements): Apex's default 1e7, or ``"auto"``: a
+bucket of XGMI_BUCKET_BYTES (32 MiB) ON THE WIRE - elements = 32 MiB / the size
+of the dtype the collective actually moves (fp32 for bf16 buckets under the fp32
+accumulation default).  The sizing model (docs/DDP_TUNING.md): an 8-rank RCCL
+all-reduce over the fully connected xGMI mesh (7 links x ~153 GB/s per GPU)
+costs t(S) = a + 2(n-1)/n * S / B with a ~ 30 us per call and B ~ 300 GB/s
+of bus bandwidth for multi-channel rings; a bucket must be >= ~16 MB to keep a
+under 20 % of t (link-rate), and the LAST bucket's t is exposed after backward,
+so buckets much above ~64 MB lengthen the tail.  32 MiB sits in that window for
+1..8 ranks; see tools/allreduce_sweep.py to refit a and B on a node.
 
 Communicators (RCCL): the buckets go to a DEDICATED process group whose HIP
 streams are created high-priority (``ProcessGroupNCCL.Options
@@ -42,6 +47,9 @@ import torch.distributed as dist
 from torch.nn.modules import Module
 
 from .. import _native
+
+
+XGMI_BUCKET_BYTES = 32 << 20
 
 
 def _group_world(pg):
@@ -171,7 +179,7 @@ class DistributedDataParallel(Module):
         self.process_group = process_group
         self.backend = dist.get_backend(process_group)
         self.world_size = _group_world(process_group)
-        self.message_size = int(message_size)
+        self._message_size_arg = message_size
         self.delay_allreduce = delay_allreduce
         self.retain_allreduce_buffers = retain_allreduce_buffers
         self.allreduce_always_fp32 = allreduce_always_fp32
@@ -213,6 +221,7 @@ class DistributedDataParallel(Module):
             self._comm_pg = self._new_comm_group()
 
         self.active_params = self._collect_params()
+        self.message_size = self._resolve_message_size(message_size)
         if self.backend == "nccl":
             for p in self.active_params:
                 assert p.is_cuda, "NCCL backend only supports model parameters to be on GPU."
@@ -235,6 +244,18 @@ class DistributedDataParallel(Module):
             opts.is_high_priority_stream = True
             return dist.new_group(ranks=ranks, pg_options=opts)
         return dist.new_group(ranks=ranks)
+
+    def _resolve_message_size(self, message_size):
+        """Elements per bucket: an int as given (Apex semantics) or "auto" - 32 MiB of
+        wire bytes for the dtype the bucket collective moves (module docstring)."""
+        if message_size != "auto":
+            return int(message_size)
+        dtypes = [p.dtype for p in self.active_params] or [torch.float32]
+        dom = max(set(dtypes), key=dtypes.count)
+        mode = self._fp32_mode()
+        wire = 4 if (dom == torch.float32 or mode == 1
+                     or (mode == 2 and dom == torch.bfloat16)) else torch.finfo(dom).bits // 8
+        return max(1, XGMI_BUCKET_BYTES // wire)
 
     def _fp32_mode(self):
         if self.allreduce_always_fp32 is None:

@@ -75,7 +75,9 @@ def parse():
                     help="SyncBatchNorm across ranks (the default for ResNet at N > 1)")
     ap.add_argument("--no-syncbn", action="store_true",
                     help="per-GPU BatchNorm statistics at N > 1 (not the BASELINE config)")
-    ap.add_argument("--message-size", type=int, default=10_000_000, help="DDP bucket elements")
+    ap.add_argument("--message-size", default="auto",
+                    help="DDP bucket elements, or 'auto' = 32 MiB on the wire (the xGMI sizing "
+                         "model of parallel/distributed.py, docs/DDP_TUNING.md)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="1 GPU: run the N>1 code path anyway - apex DDP (+ SyncBN for ResNet) "
                          "with every bucket all-reduce and SyncBN all_gather / all_reduce "
@@ -518,6 +520,8 @@ def ddp_timing(ddp, step, batch, steps, device):
 
 def main():
     args = parse()
+    if args.message_size != "auto":
+        args.message_size = int(args.message_size)
     from apex_example_amd.utils.dist import barrier, init_distributed
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:

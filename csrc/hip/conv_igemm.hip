@@ -102,11 +102,12 @@ struct ConvGeom {
 
 // NB = 1 (no DMA ring): for 1x1 convs with one or two K-tiles (K = 64 / 128: the
 // ResNet layer1-2 channel-expanding convs) - nothing to overlap inside a workgroup, so
-// the LDS goes to more resident workgroups instead (4 per CU: one's loads overlap
-// another's MFMAs and stores).
+// the LDS goes to more resident workgroups instead (3 per CU: one's loads overlap
+// another's MFMAs and stores; 4 would cap the registers at 128 and spill the epilogue
+// statistics).
 template <int MODE, int BM, int BN, int WM, int WN, int NB>
 __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024)
-                                           ? 1 : (NB == 1 ? 4 : 2))
+                                           ? 1 : (NB == 1 ? 3 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
                const float* __restrict__ shift) {

@@ -102,6 +102,19 @@ def ddp_subgroups(rank, world, streams=1, message_size=300):
     return out
 
 
+def ddp_auto_size(rank, world):
+    """message_size='auto': 32 MiB on the wire for the dtype the collective moves."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    out = {}
+    for name, dt, fp32 in (("bf16", torch.bfloat16, None), ("bf16_native", torch.bfloat16, False),
+                           ("fp16", torch.float16, None), ("fp32", torch.float32, None)):
+        m = nn.Linear(64, 64).to(dt)
+        ddp = DistributedDataParallel(m, message_size="auto", allreduce_always_fp32=fp32)
+        out[name] = ddp.message_size
+    return out
+
+
 def ddp_bf16_precision(rank, world, fp32=None, n=4096):
     """bf16 gradient buckets averaged over ``world`` ranks; returns the reduced
     bf16 gradient and the exact fp32 average of the per-rank bf16 gradients."""

@@ -55,6 +55,13 @@ def test_ddp_disjoint_subgroups(tmp_path, streams):
                     torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-6)
 
 
+def test_ddp_auto_message_size(tmp_path):
+    res = W.run("ddp_auto_size", 2, str(tmp_path))[0]
+    mib32 = 32 << 20
+    assert res == {"bf16": mib32 // 4, "bf16_native": mib32 // 2, "fp16": mib32 // 2,
+                   "fp32": mib32 // 4}
+
+
 def test_ddp_sum_without_average(tmp_path):
     res = W.run("ddp_grads", 2, str(tmp_path), average=False)
     ref = _single_process_grads()
