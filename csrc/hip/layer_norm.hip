@@ -16,6 +16,8 @@
 //  * a generic block-per-row path covers odd widths / unaligned rows.
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -287,21 +289,46 @@ __global__ void __launch_bounds__(kLNThreads)
     if (gamma && col < n2) load8(gamma + col, g[k]);
   }
 
-  for (int64_t row = row0; row < n1; row += wstride) {
-    const float mu = rms ? 0.f : mean[row];
-    const float iv = invvar[row];
-    float xv[VPT][8], dv[VPT][8];
-    float s1 = 0.f, s2 = 0.f;  // sum(dy*g), sum(dy*g*xhat)
+  // One row of lookahead: the next row's x / dy (/ residual gradient) loads are issued
+  // before the current row's reductions and stores, so a wave always has a row of
+  // loads in flight (the grid is capped at 1024 waves, each walking several rows:
+  // without the lookahead every row paid the full load latency - 1.7 TB/s measured
+  // for GPT-2-medium's fp32 joins, 16 B/element).
+  float xn[VPT][8], dn[VPT][8], en[VPT][8];
+  auto load_row = [&](int64_t r, float (&xa)[VPT][8], float (&da)[VPT][8],
+                      float (&ea)[VPT][8]) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       int col = (k * kWave + lane) * 8;
       if (col < n2) {
-        load8(x + row * n2 + col, xv[k]);
-        load8(reinterpret_cast<const TY*>(dy) + row * n2 + col, dv[k]);
+        load8(x + r * n2 + col, xa[k]);
+        load8(reinterpret_cast<const TY*>(dy) + r * n2 + col, da[k]);
+        if constexpr (FUSE) {
+          if (fu.dres) load8(static_cast<const T*>(fu.dres) + r * n2 + col, ea[k]);
+        }
       } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xv[k][i] = dv[k][i] = 0.f;
+        for (int i = 0; i < 8; ++i) xa[k][i] = da[k][i] = 0.f;
       }
+    }
+  };
+  if (row0 < n1) load_row(row0, xn, dn, en);
+  for (int64_t row = row0; row < n1; row += wstride) {
+    float xv[VPT][8], dv[VPT][8], ev[VPT][8];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xv[k][i] = xn[k][i];
+        dv[k][i] = dn[k][i];
+        ev[k][i] = en[k][i];
+      }
+    const float mu = rms ? 0.f : mean[row];
+    const float iv = invvar[row];
+    if (row + wstride < n1) load_row(row + wstride, xn, dn, en);
+    float s1 = 0.f, s2 = 0.f;  // sum(dy*g), sum(dy*g*xhat)
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float xh = (xv[k][i] - mu) * iv;
@@ -331,10 +358,8 @@ __global__ void __launch_bounds__(kLNThreads)
       }
       if constexpr (FUSE) {
         if (fu.dres) {
-          float e[8];
-          load8(static_cast<const T*>(fu.dres) + row * n2 + col, e);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += e[i];
+          for (int i = 0; i < 8; ++i) o[i] += ev[k][i];
         }
         const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
         float hd[8];
@@ -488,9 +513,20 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// fast backward grid: at most kLNBwdBlocks x 4 waves, each walking rows with a row of
+// lookahead (APEX_AMD_LN_BWD_BLOCKS overrides, for A/B sweeps); fewer blocks also
+// shrink the dgamma/dbeta partial buffer the column-sum kernel reads
+static inline int ln_bwd_block_cap() {
+  static const int cap = [] {
+    const char* e = std::getenv("APEX_AMD_LN_BWD_BLOCKS");
+    return e ? std::atoi(e) : 256;
+  }();
+  return cap > 0 ? cap : 256;
+}
+
 static inline int ln_bwd_blocks(int64_t n1) {
   int64_t b = (n1 + kLNWaves - 1) / kLNWaves;
-  if (b > 1024) b = 1024;  // bounds the partial buffer (nblocks x 2 x n2 floats)
+  if (b > ln_bwd_block_cap()) b = ln_bwd_block_cap();
   return (int)(b > 0 ? b : 1);
 }
 static inline int ln_generic_parts(int64_t n1) {
