@@ -95,7 +95,12 @@ class FusedSGD(FusedOptimizerBase):
                 scale, inv = self._scale_args(s["scaled"])
                 noop = self._noop(dev)
                 flag = None
-                if self._sync_free() and dev.type == "cuda" and momentum != 0:
+                if dampening == 0:
+                    # the momentum buffers start at zero, so mom*0 + (1-0)*g == g bitwise:
+                    # Apex's first-run initialisation needs no flag (and no per-step
+                    # mark_step_done launch) when there is no dampening
+                    first_run = False
+                elif self._sync_free() and dev.type == "cuda" and momentum != 0:
                     flag = self._dev_flag((gid, key), dev, first_run)
                 amp_C.multi_tensor_sgd(65536, noop, lists, weight_decay, momentum, dampening,
                                        lr, nesterov, first_run, self.wd_after_momentum, scale,

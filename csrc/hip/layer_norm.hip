@@ -275,71 +275,51 @@ __global__ void __launch_bounds__(kLNThreads)
   const float inv_n = 1.f / (float)n2;
   const bool want_part = part != nullptr;
 
-  float g[VPT][8];
+  // Register budget (occupancy is what hides the load latency here: every wave walks
+  // only a few rows): gamma is NOT kept across rows - it is loaded 8 columns at a
+  // time where dg = dy*gamma is formed and dg overwrites dy; xhat overwrites x.
+  // 142 -> ~100 VGPRs for the fp32 GPT-2 joins (3 -> 5 waves per SIMD).
   float adg[VPT][8], adb[VPT][8];
 #pragma unroll
-  for (int k = 0; k < VPT; ++k) {
-    int col = (k * kWave + lane) * 8;
+  for (int k = 0; k < VPT; ++k)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      adg[k][i] = 0.f;
-      adb[k][i] = 0.f;
-      g[k][i] = 1.f;
-    }
-    if (gamma && col < n2) load8(gamma + col, g[k]);
-  }
+    for (int i = 0; i < 8; ++i) adg[k][i] = adb[k][i] = 0.f;
 
-  // One row of lookahead: the next row's x / dy (/ residual gradient) loads are issued
-  // before the current row's reductions and stores, so a wave always has a row of
-  // loads in flight (the grid is capped at 1024 waves, each walking several rows:
-  // without the lookahead every row paid the full load latency - 1.7 TB/s measured
-  // for GPT-2-medium's fp32 joins, 16 B/element).
-  float xn[VPT][8], dn[VPT][8], en[VPT][8];
-  auto load_row = [&](int64_t r, float (&xa)[VPT][8], float (&da)[VPT][8],
-                      float (&ea)[VPT][8]) {
+  for (int64_t row = row0; row < n1; row += wstride) {
+    const float mu = rms ? 0.f : mean[row];
+    const float iv = invvar[row];
+    float xv[VPT][8], dv[VPT][8];
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       int col = (k * kWave + lane) * 8;
       if (col < n2) {
-        load8(x + r * n2 + col, xa[k]);
-        load8(reinterpret_cast<const TY*>(dy) + r * n2 + col, da[k]);
-        if constexpr (FUSE) {
-          if (fu.dres) load8(static_cast<const T*>(fu.dres) + r * n2 + col, ea[k]);
-        }
+        load8(x + row * n2 + col, xv[k]);
+        load8(reinterpret_cast<const TY*>(dy) + row * n2 + col, dv[k]);
       } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xa[k][i] = da[k][i] = 0.f;
+        for (int i = 0; i < 8; ++i) xv[k][i] = dv[k][i] = 0.f;
       }
     }
-  };
-  if (row0 < n1) load_row(row0, xn, dn, en);
-  for (int64_t row = row0; row < n1; row += wstride) {
-    float xv[VPT][8], dv[VPT][8], ev[VPT][8];
-#pragma unroll
-    for (int k = 0; k < VPT; ++k)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        xv[k][i] = xn[k][i];
-        dv[k][i] = dn[k][i];
-        ev[k][i] = en[k][i];
-      }
-    const float mu = rms ? 0.f : mean[row];
-    const float iv = invvar[row];
-    if (row + wstride < n1) load_row(row + wstride, xn, dn, en);
     float s1 = 0.f, s2 = 0.f;  // sum(dy*g), sum(dy*g*xhat)
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
+      int col = (k * kWave + lane) * 8;
+      float g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = 1.f;
+      if (gamma && col < n2) load8(gamma + col, g);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float xh = (xv[k][i] - mu) * iv;
+        const float xh = (xv[k][i] - mu) * iv;
         xv[k][i] = xh;  // keep xhat
-        float dg = dv[k][i] * g[k][i];
-        s1 += dg;
-        s2 = fmaf(dg, xh, s2);
         if (want_part) {
           adg[k][i] = fmaf(dv[k][i], xh, adg[k][i]);
           adb[k][i] += dv[k][i];
         }
+        const float dg = dv[k][i] * g[i];
+        dv[k][i] = dg;  // keep dy*gamma
+        s1 += dg;
+        s2 = fmaf(dg, xh, s2);
       }
     }
     s1 = wave_sum(s1) * inv_n;
@@ -352,14 +332,15 @@ __global__ void __launch_bounds__(kLNThreads)
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float dg = dv[k][i] * g[k][i];
-        float t = rms ? (dg - xv[k][i] * s2) : (dg - s1 - xv[k][i] * s2);
+        const float t = rms ? (dv[k][i] - xv[k][i] * s2) : (dv[k][i] - s1 - xv[k][i] * s2);
         o[i] = t * iv;
       }
       if constexpr (FUSE) {
         if (fu.dres) {
+          float e[8];
+          load8(static_cast<const T*>(fu.dres) + row * n2 + col, e);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += ev[k][i];
+          for (int i = 0; i < 8; ++i) o[i] += e[i];
         }
         const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
         float hd[8];
@@ -513,15 +494,15 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// fast backward grid: at most kLNBwdBlocks x 4 waves, each walking rows with a row of
-// lookahead (APEX_AMD_LN_BWD_BLOCKS overrides, for A/B sweeps); fewer blocks also
-// shrink the dgamma/dbeta partial buffer the column-sum kernel reads
+// fast backward grid: at most 1024 blocks x 4 waves walking rows (APEX_AMD_LN_BWD_BLOCKS
+// overrides, for A/B sweeps; 256 with a row of load lookahead measured 126 vs 77 us per
+// GPT-2 join - occupancy, not lookahead, hides the latency)
 static inline int ln_bwd_block_cap() {
   static const int cap = [] {
     const char* e = std::getenv("APEX_AMD_LN_BWD_BLOCKS");
-    return e ? std::atoi(e) : 256;
+    return e ? std::atoi(e) : 1024;
   }();
-  return cap > 0 ? cap : 256;
+  return cap > 0 ? cap : 1024;
 }
 
 static inline int ln_bwd_blocks(int64_t n1) {
