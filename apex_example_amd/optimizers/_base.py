@@ -103,15 +103,8 @@ class FusedOptimizerBase(torch.optim.Optimizer):
             return s, True
         return 1.0 / s, False
 
-    def _launch_sets(self, gid, group):
-        """OrderedDict key -> dict(grads, params, copies, scaled).
-
-        Cached per group: a steady-state step sees the very same grad tensors
-        (DDP bucket views, amp's persistent grads), so after one C-speed identity
-        check of the current grads against the cached ones the whole set - and
-        the state lists hung on it by ``_state_lists`` - is reused.  Rebuilding
-        costs ~1 us per tensor of Python, which for ResNet-50's 161 tensors was
-        more host time than the 0.1 ms the kernel runs."""
+    def _amp_key(self, gid):
+        """(key, grad sources) of group gid: which tensors own the grads the kernels read."""
         stash = self._amp()
         amp_path = bool(stash is not None and getattr(stash, "master_weights", False)
                         and stash.lazy_init_called)
@@ -120,19 +113,56 @@ class FusedOptimizerBase(torch.optim.Optimizer):
             srcs = (stash.fp16_groups[gid] if fold else stash.fp32_from_fp16_groups[gid],
                     stash.fp32_from_fp32_groups[gid])
         else:
-            srcs = (group["params"],)
-        grads = list(itertools.chain.from_iterable(map(_GRAD, s) for s in srcs))
+            srcs = (self.param_groups[gid]["params"],)
         # amp O1 folded unscale: the (fp32) grads still carry the loss scale
         o1_scaled = bool(not amp_path and stash is not None
                          and getattr(stash, "grads_scaled", False))
-        key = (amp_path, fold, o1_scaled)
+        return (amp_path, fold, o1_scaled), srcs
+
+    def _launch_sets(self, gid, group):
+        """OrderedDict key -> dict(grads, params, copies, scaled, owners).
+
+        Cached per group.  Steady state: every set carries a native ``StepPlan``
+        (``_set_plans``) that reads the grads from their owners in C++, so the step
+        never walks the parameters in Python - ``refresh()`` (one call per set) checks
+        that every owner still has a grad of the planned dtype / size and that no
+        other parameter gained one.  Without plans (CPU-less native build, first step)
+        a C-speed identity check of the current grads against the cached ones decides;
+        rebuilding costs ~1 us per tensor of Python, which for ResNet-50's 161 tensors
+        was more host time than the 0.1 ms the kernel runs."""
+        key, srcs = self._amp_key(gid)
         c = self._set_cache.get(gid)
-        if (c is not None and c[0] == key and len(c[1]) == len(grads)
-                and all(map(operator.is_, c[1], grads))):
-            return c[2]
-        sets = self._build_launch_sets(gid, group, stash, amp_path, fold, o1_scaled)
-        self._set_cache[gid] = (key, grads, sets)
+        grads = None
+        if c is not None and c[0] == key:
+            if c[3]:
+                if all(s["_plan"].refresh() for s in c[2].values()):
+                    return c[2]
+            else:
+                grads = list(itertools.chain.from_iterable(map(_GRAD, s) for s in srcs))
+                if len(c[1]) == len(grads) and all(map(operator.is_, c[1], grads)):
+                    return c[2]
+        if grads is None:
+            grads = list(itertools.chain.from_iterable(map(_GRAD, s) for s in srcs))
+        stash = self._amp()
+        sets = self._build_launch_sets(gid, group, stash, key[0], key[1], key[2])
+        absent = [t for src in srcs for t in src if t.grad is None]
+        self._set_cache[gid] = [key, grads, sets, False, absent]
         return sets
+
+    def _set_plans(self, gid, sets, fixed):
+        """Attach a native StepPlan to every set of group gid (``fixed(s)`` -> the
+        non-grad lists of the set's launch); from the next step on the group takes
+        the plan path (CPU tensors too: the plan calls the CPU kernels).  No-op
+        without the extension."""
+        c = self._set_cache.get(gid)
+        if c is None or c[2] is not sets or c[3] or not _native.available():
+            return
+        plans = [_native.require().mt.StepPlan(s["owners"], fixed(s)) for s in sets.values()]
+        for s, pl in zip(sets.values(), plans):
+            s["_plan"] = pl
+        if plans:
+            plans[0].set_absent(c[4])
+            c[3] = True
 
     def _state_lists(self, s, names, init=torch.zeros_like):
         """Per-set lists of optimizer state tensors (``self.state[p][name]``),
@@ -154,11 +184,12 @@ class FusedOptimizerBase(torch.optim.Optimizer):
     def _build_launch_sets(self, gid, group, stash, amp_path, fold, o1_scaled=False):
         sets = OrderedDict()
 
-        def add(key, g, p, c, scaled):
+        def add(key, g, p, c, scaled, owner):
             s = sets.get(key)
             if s is None:
                 s = sets[key] = {"grads": [], "params": [], "copies": [] if c is not None else None,
-                                 "scaled": scaled}
+                                 "scaled": scaled, "owners": []}
+            s["owners"].append(owner)
             s["grads"].append(g)
             s["params"].append(p)
             if c is not None:
@@ -171,24 +202,32 @@ class FusedOptimizerBase(torch.optim.Optimizer):
                     continue
                 if g.is_sparse:
                     raise RuntimeError("fused optimizers do not support sparse gradients")
-                add((g.dtype, master.dtype, model_p.dtype, fold), g, master, model_p, fold)
+                add((g.dtype, master.dtype, model_p.dtype, fold), g, master, model_p, fold,
+                    model_p if fold else master)
             for p in stash.fp32_from_fp32_groups[gid]:
                 if p.grad is None:
                     continue
-                add((p.grad.dtype, p.dtype, None, False), p.grad, p, None, False)
+                add((p.grad.dtype, p.dtype, None, False), p.grad, p, None, False, p)
         else:
             for p in group["params"]:
                 if p.grad is None:
                     continue
                 if p.grad.is_sparse:
                     raise RuntimeError("fused optimizers do not support sparse gradients")
-                add((p.grad.dtype, p.dtype, None, o1_scaled), p.grad, p, None, o1_scaled)
+                add((p.grad.dtype, p.dtype, None, o1_scaled), p.grad, p, None, o1_scaled, p)
         return sets
 
     def _scale_args(self, scaled):
         if not scaled:
             return 1.0, False
         return self._fold_scale()
+
+    def _plan_scale(self, scaled):
+        """(value, tensor or None, invert) of the scale argument, for StepPlan calls."""
+        v, inv = self._scale_args(scaled)
+        if isinstance(v, torch.Tensor):
+            return 1.0, v, inv
+        return float(v), None, inv
 
     def _dev_step(self, gid, device):
         """int32 device counter of completed steps for group gid (sync-free mode)."""

@@ -46,9 +46,23 @@ class FusedAdam(FusedOptimizerBase):
             dev = next(iter(sets.values()))["params"][0].device
             step, step_t = self._step_value(gid, group, dev)
             noop = self._noop(dev)
-            for key, s in sets.items():
+            planned, last = True, len(sets) - 1
+            for i, (key, s) in enumerate(sets.items()):
                 # exponential moving averages of the gradient and its square
                 m, v = self._state_lists(s, ("exp_avg", "exp_avg_sq"))
+                plan = s.get("_plan")
+                if plan is not None:
+                    sv, st, inv = self._plan_scale(s["scaled"])
+                    lr = group["lr"]
+                    lv, lt = (1.0, lr) if isinstance(lr, torch.Tensor) else (float(lr), None)
+                    # the last set also advances the device step counter (same launch order
+                    # as _after_step)
+                    if not plan.adam(noop, lv, lt, beta1, beta2, group["eps"], step, step_t,
+                                     self.adam_w_mode, bool(bias_correction),
+                                     group["weight_decay"], sv, st, inv, i == last):
+                        raise RuntimeError("FusedAdam: launch set changed inside step()")
+                    continue
+                planned = False
                 lists = [s["grads"], s["params"], m, v]
                 if s["copies"] is not None:
                     lists.append(s["copies"])
@@ -57,5 +71,8 @@ class FusedAdam(FusedOptimizerBase):
                                         group["eps"], step_t if step_t is not None else step,
                                         self.adam_w_mode, bias_correction,
                                         group["weight_decay"], scale=scale_v, scale_inv=inv)
-            self._after_step(gid, dev, step_t, noop)
+            if not planned:
+                self._after_step(gid, dev, step_t, noop)
+                self._set_plans(gid, sets, lambda s: [s["params"]] + list(s["_state"][1]) + (
+                    [s["copies"]] if s["copies"] is not None else []))
         return loss

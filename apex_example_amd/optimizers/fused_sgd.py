@@ -80,7 +80,9 @@ class FusedSGD(FusedOptimizerBase):
             dampening = group["dampening"]
             nesterov = group["nesterov"]
             lr = group["lr"]
-            for key, s in self._launch_sets(gid, group).items():
+            sets = self._launch_sets(gid, group)
+            planned = True
+            for key, s in sets.items():
                 params = s["params"]
                 dev = params[0].device
                 cached = s.get("_moms")
@@ -89,10 +91,6 @@ class FusedSGD(FusedOptimizerBase):
                     s["_moms"] = moms
                 else:
                     moms, first_run = cached, False
-                lists = [s["grads"], params, moms]
-                if s["copies"] is not None:
-                    lists.append(s["copies"])
-                scale, inv = self._scale_args(s["scaled"])
                 noop = self._noop(dev)
                 flag = None
                 if dampening == 0:
@@ -102,13 +100,28 @@ class FusedSGD(FusedOptimizerBase):
                     first_run = False
                 elif self._sync_free() and dev.type == "cuda" and momentum != 0:
                     flag = self._dev_flag((gid, key), dev, first_run)
-                amp_C.multi_tensor_sgd(65536, noop, lists, weight_decay, momentum, dampening,
-                                       lr, nesterov, first_run, self.wd_after_momentum, scale,
-                                       scale_inv=inv, first_run_flag=flag)
+                plan = s.get("_plan")
+                if plan is not None:
+                    sv, st, inv = self._plan_scale(s["scaled"])
+                    if not plan.sgd(noop, weight_decay, momentum, dampening, lr, nesterov,
+                                    first_run, flag, self.wd_after_momentum, sv, st, inv):
+                        raise RuntimeError("FusedSGD: launch set changed inside step()")
+                else:
+                    planned = False
+                    lists = [s["grads"], params, moms]
+                    if s["copies"] is not None:
+                        lists.append(s["copies"])
+                    scale, inv = self._scale_args(s["scaled"])
+                    amp_C.multi_tensor_sgd(65536, noop, lists, weight_decay, momentum, dampening,
+                                           lr, nesterov, first_run, self.wd_after_momentum, scale,
+                                           scale_inv=inv, first_run_flag=flag)
                 if flag is not None:
                     from .. import _native
 
                     _native.require().mt.mark_step_done(flag, noop)
+            if not planned:
+                self._set_plans(gid, sets, lambda s: [s["params"], s["_moms"]] + (
+                    [s["copies"]] if s["copies"] is not None else []))
 
         self.most_recent_scale = 1.0
         self.scale_set_by_backward = False

@@ -589,10 +589,6 @@ def main():
     if args.graph:
         if world > 1:
             raise SystemExit("--graph is single-GPU only in this version")
-        if not args.model.startswith("resnet"):
-            # BERT-large's captured step hung on its first replay (MI355X, round 2,
-            # docs/PERF.md); capture is validated for the ResNet models only
-            raise SystemExit("--graph is validated for the ResNet models only")
         # drop every reference to an eager autograd graph (its AccumulateGrad
         # nodes would pin the default stream), then warm the capture path on a
         # side stream (allocator pools, multi-tensor plan caches)

@@ -6,6 +6,8 @@
 // tensor so the optimizer step needs no host synchronisation.
 #include "amp_ops.h"
 
+#include <c10/hip/HIPGraphsC10Utils.h>
+
 #include "../cpu/cpu_ops.h"
 #include "common.h"
 
@@ -378,6 +380,118 @@ void update_loss_scale_op(at::Tensor scale, at::Tensor unskipped, c10::optional<
   update_loss_scale(scale.data_ptr<float>(), unskipped.data_ptr<int>(), opt_iptr(skipped),
                     overflow.data_ptr<int>(), (float)factor, (int)window, (float)min_scale,
                     (float)max_scale, dynamic ? 1 : 0, cur_stream(), opt_fptr(applied));
+}
+
+// ------------------------------------------------------------------ StepPlan
+StepPlan::StepPlan(std::vector<at::Tensor> owners, TensorLists fixed) : owners_(std::move(owners)) {
+  TORCH_CHECK(!owners_.empty() && !fixed.empty(), "StepPlan: empty launch set");
+  lists_.reserve(fixed.size() + 1);
+  lists_.emplace_back(owners_.size());
+  for (auto& l : fixed) {
+    TORCH_CHECK(l.size() == owners_.size(), "StepPlan: list sizes differ");
+    lists_.push_back(std::move(l));
+  }
+  gptr_.assign(owners_.size(), nullptr);
+  gtype_ = at::ScalarType::Undefined;
+  gpu_ = lists_[1][0].is_cuda();
+}
+
+bool StepPlan::refresh() {
+  for (const auto& t : absent_)
+    if (t.grad().defined()) return false;
+  bool moved = false;
+  for (size_t i = 0; i < owners_.size(); ++i) {
+    const at::Tensor& g = owners_[i].grad();
+    if (!g.defined()) return false;
+    void* p = g.data_ptr();
+    if (p == gptr_[i] && g.unsafeGetTensorImpl() == lists_[0][i].unsafeGetTensorImpl()) continue;
+    if (gtype_ == at::ScalarType::Undefined) gtype_ = g.scalar_type();
+    if (g.scalar_type() != gtype_ || g.numel() != lists_[1][i].numel() || g.is_sparse() ||
+        !g.is_non_overlapping_and_dense())
+      return false;
+    lists_[0][i] = g;
+    gptr_[i] = p;
+    moved = true;
+  }
+  if (moved) {
+    mt_validate(lists_, 2, kMaxDepth);  // strides of a new grad vs. its param
+    fresh_ = false;
+  }
+  return true;
+}
+
+// the launch table: built (or fetched from the address cache) once per grad layout
+bool StepPlan::gpu_launch_ready() {
+  if (!gpu_) return false;
+  if (!fresh_) {
+    plan_ = mt_plan(lists_);
+    fresh_ = true;
+    ++rebuilds_;
+  } else if (c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None) {
+    plan_.captured = true;  // (the plan owns its table: it outlives the graph)
+  }
+  return true;
+}
+
+bool StepPlan::sgd(at::Tensor noop, double wd, double momentum, double dampening, double lr,
+                   bool nesterov, bool first_run, OptT first_run_flag, bool wd_after_momentum,
+                   double scale, OptT scale_t, bool scale_inv) {
+  c10::NoGradGuard no_grad_;
+  if (!refresh()) return false;
+  const int depth = (int)lists_.size();
+  TORCH_CHECK(depth == 3 || depth == 4, "sgd plan: [grads, params, moms(, copies)]");
+  if (!gpu_launch_ready()) {
+    mt_sgd_op(noop, lists_, wd, momentum, dampening, lr, c10::nullopt, nesterov, first_run,
+              first_run_flag, wd_after_momentum, scale, scale_t, scale_inv);
+    return true;
+  }
+  SgdArgs a;
+  a.wd = (float)wd;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.lr = (float)lr;
+  a.nesterov = nesterov;
+  a.first_run = first_run;
+  a.wd_after_momentum = wd_after_momentum;
+  a.scale = make_scale(scale, scale_t, scale_inv);
+  a.lr_ptr = nullptr;
+  a.first_run_flag = opt_iptr(first_run_flag);
+  DType copy = depth == 4 ? dtype_of(lists_[3][0]) : dtype_of(lists_[1][0]);
+  mt_sgd(plan_.L, depth, dtype_of(lists_[0][0]), dtype_of(lists_[1][0]), dtype_of(lists_[2][0]),
+         copy, a, noop_ptr(noop), cur_stream());
+  return true;
+}
+
+bool StepPlan::adam(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
+                    int64_t step, OptT step_t, int64_t mode, bool bias_correction, double wd,
+                    double scale, OptT scale_t, bool scale_inv, bool advance) {
+  c10::NoGradGuard no_grad_;
+  if (!refresh()) return false;
+  const int depth = (int)lists_.size();
+  TORCH_CHECK(depth == 4 || depth == 5, "adam plan: [grads, params, m, v(, copies)]");
+  if (!gpu_launch_ready()) {
+    mt_adam_op(noop, lists_, lr, lr_t, beta1, beta2, eps, step, step_t, mode, bias_correction, wd,
+               scale, scale_t, scale_inv);
+  } else {
+    AdamArgs a;
+    a.lr = (float)lr;
+    a.beta1 = (float)beta1;
+    a.beta2 = (float)beta2;
+    a.eps = (float)eps;
+    a.wd = (float)wd;
+    a.step = (int)step;
+    a.step_ptr = opt_iptr(step_t);
+    a.mode = (int)mode;
+    a.bias_correction = bias_correction ? 1 : 0;
+    a.scale = make_scale(scale, scale_t, scale_inv);
+    a.lr_ptr = opt_fptr(lr_t);
+    DType copy = depth == 5 ? dtype_of(lists_[4][0]) : dtype_of(lists_[1][0]);
+    mt_adam(plan_.L, depth, dtype_of(lists_[0][0]), dtype_of(lists_[1][0]), copy, a,
+            noop_ptr(noop), cur_stream());
+  }
+  if (advance && step_t.has_value() && step_t->defined())
+    advance_step_op(*step_t, noop.defined() ? OptT(noop) : OptT());
+  return true;
 }
 
 void advance_step_op(at::Tensor step, c10::optional<at::Tensor> noop) {

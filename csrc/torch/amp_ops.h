@@ -5,6 +5,8 @@
 #include <tuple>
 #include <vector>
 
+#include "common.h"
+
 namespace amd {
 
 using TensorLists = std::vector<std::vector<at::Tensor>>;
@@ -45,6 +47,39 @@ void advance_step_op(at::Tensor step, OptT noop);
 void mark_step_done_op(at::Tensor flag, OptT noop);
 void flat_scale_op(at::Tensor in, at::Tensor out, double scale, OptT scale_t, bool invert,
                    OptT noop);
+
+// A prepared optimizer launch set (the optimizer-step fast path): the fixed lists
+// (params, optimizer state, 16-bit model copies) are converted from Python once;
+// the gradient list is read from the owners' .grad each step in C++, and the
+// device launch table is re-built only when a gradient moved.  A step is then
+// one Python->C++ call per launch set with scalar arguments only.
+class StepPlan {
+ public:
+  StepPlan(std::vector<at::Tensor> owners, TensorLists fixed);
+  // false: some owner has no grad / a grad of another dtype, size or layout (the
+  // caller re-plans); nothing was launched
+  bool refresh();
+  bool sgd(at::Tensor noop, double wd, double momentum, double dampening, double lr,
+           bool nesterov, bool first_run, OptT first_run_flag, bool wd_after_momentum,
+           double scale, OptT scale_t, bool scale_inv);
+  bool adam(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
+            int64_t step, OptT step_t, int64_t mode, bool bias_correction, double wd,
+            double scale, OptT scale_t, bool scale_inv, bool advance_step);
+  // tensors that must stay without a grad (a param gaining one changes the sets)
+  void set_absent(std::vector<at::Tensor> absent) { absent_ = std::move(absent); }
+  int64_t size() const { return (int64_t)owners_.size(); }
+  int64_t rebuilds() const { return rebuilds_; }
+
+ private:
+  bool gpu_launch_ready();
+  std::vector<at::Tensor> owners_, absent_;
+  TensorLists lists_;  // [grads, fixed...]
+  std::vector<void*> gptr_;
+  at::ScalarType gtype_;
+  MTPlan plan_;
+  bool gpu_ = false, fresh_ = false;
+  int64_t rebuilds_ = 0;
+};
 
 void mt_plan_cache_clear();
 int64_t mt_plan_cache_size();

@@ -67,6 +67,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mt.def("advance_step", &advance_step_op);
   mt.def("mark_step_done", &mark_step_done_op);
   mt.def("flat_scale", &flat_scale_op);
+  py::class_<StepPlan, std::shared_ptr<StepPlan>>(mt, "StepPlan")
+      .def(py::init<std::vector<at::Tensor>, TensorLists>(), py::arg("owners"), py::arg("fixed"))
+      .def("refresh", &StepPlan::refresh)
+      .def("set_absent", &StepPlan::set_absent)
+      .def("sgd", &StepPlan::sgd)
+      .def("adam", &StepPlan::adam)
+      .def("size", &StepPlan::size)
+      .def("rebuilds", &StepPlan::rebuilds);
   mt.def("plan_cache_clear", &mt_plan_cache_clear);
   mt.def("plan_cache_size", &mt_plan_cache_size);
 

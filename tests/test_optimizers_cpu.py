@@ -176,3 +176,44 @@ def test_larc(clip):
             alr = min(alr / 0.1, 1.0)
         exp = r - 0.1 * (g + 1e-3 * r) * alr
         torch.testing.assert_close(p.detach(), exp, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_step_plan_path_tracks_grads(kind, monkeypatch):
+    """The native StepPlan fast path (optimizers/_base.py): grads re-allocated every
+    step (moved), persistent grads updated in place, a parameter that gains a grad
+    mid-run and one that loses it - all must match the per-step Python launch path
+    (plans disabled) bitwise, step for step (and torch.optim.SGD for sgd)."""
+    ps, ref = _pair((10, 300, 7, 33))
+    slow = [r.detach().clone().requires_grad_(True) for r in ref]
+    if kind == "sgd":
+        mk = lambda ts: FusedSGD(ts, lr=0.1, momentum=0.9, weight_decay=1e-3)  # noqa: E731
+        o2 = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=1e-3)
+    else:
+        mk = lambda ts: FusedAdam(ts, lr=1e-2, weight_decay=1e-2)  # noqa: E731
+        o2 = None
+    o1, o3 = mk(ps), mk(slow)
+    monkeypatch.setattr(o3, "_set_plans", lambda *a: None)
+    g = torch.Generator().manual_seed(7)
+    for i in range(8):
+        for j, (p, r, q) in enumerate(zip(ps, ref, slow)):
+            # param 3 has no grad before step 4; param 1 loses its grad at step 6
+            if (j == 3 and i < 4) or (j == 1 and i == 6):
+                p.grad = r.grad = q.grad = None
+                continue
+            gr = torch.randn(p.shape, generator=g)
+            if i % 2 and p.grad is not None:
+                p.grad.copy_(gr)              # same tensor, new values
+            else:
+                p.grad = gr.clone()           # a new tensor (moved grad)
+            r.grad, q.grad = gr.clone(), gr.clone()
+        o1.step()
+        o3.step()
+        if o2 is not None:
+            o2.step()
+        for p, r, q in zip(ps, ref, slow):
+            assert torch.equal(p, q)
+            if o2 is not None:
+                torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
+    sets = o1._set_cache[0][2]
+    assert all("_plan" in s for s in sets.values())  # the plan path ran

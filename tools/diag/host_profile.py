@@ -30,6 +30,15 @@ def main():
     torch.cuda.synchronize()
     import time
     fn = (lambda: w.opt_only()) if opt_only else (lambda: w.step(w.batch))
+    # per-call host time of the first calls after a training step (bench.py's
+    # optimizer-step metric is taken right after its timed loop)
+    per = []
+    for _ in range(6):
+        h0 = time.perf_counter()
+        fn()
+        per.append((time.perf_counter() - h0) * 1e6)
+    torch.cuda.synchronize()
+    print("first calls after a train step, host us: " + " ".join("%.0f" % t for t in per))
     for _ in range(5):
         fn()
     torch.cuda.synchronize()

@@ -803,6 +803,33 @@ def bench_ln(args):
             tbs(2 * nb, res[1][0]), tbs(3 * nb, res[0][1]), tbs(3 * nb, res[1][1])))
 
 
+def bench_ln_join(args):
+    """GPT-2-medium O1 sublayer join in isolation: s = x + dropout(h), y = LN(s) with an
+    fp32 residual x and fp16 h / y (bs 8 x seq 1024 rows).  Bytes: fwd reads x, h and
+    writes s, y; bwd reads s, dy, ds_ext and writes ds, dh."""
+    from apex_example_amd.normalization import FusedLayerNorm, fused_add_dropout_layer_norm
+
+    dev = "cuda"
+    print("| rows x n2 | p | fwd | bwd (ds, dh, dg, db) | blocks env |")
+    print("|---|---|---|---|---|")
+    for rows, n2, p in [(8192, 1024, 0.1), (8192, 1024, 0.0), (16384, 1024, 0.1)]:
+        x = torch.randn(rows, n2, device=dev, requires_grad=True)
+        h = torch.randn(rows, n2, device=dev, dtype=torch.float16, requires_grad=True)
+        ln = FusedLayerNorm(n2).to(dev)
+        dy = torch.randn(rows, n2, device=dev, dtype=torch.float16)
+        ds = torch.randn(rows, n2, device=dev)
+        tf = timeit(lambda: fused_add_dropout_layer_norm(x, h, ln, p, True, True))
+        y, s = fused_add_dropout_layer_norm(x, h, ln, p, True, True)
+        assert y.dtype == torch.float16 and s.dtype == torch.float32
+        tb = timeit(lambda: torch.autograd.grad((y, s), [x, h, ln.weight, ln.bias], (dy, ds),
+                                                retain_graph=True))
+        fb = rows * n2 * (4 + 2 + 4 + 2)
+        bb = rows * n2 * (4 + 2 + 4 + 4 + 2)
+        print("| %dx%d | %.1f | %.1f us (%.2f TB/s) | %.1f us (%.2f TB/s) | %s |" % (
+            rows, n2, p, tf, fb / tf / 1e6, tb, bb / tb / 1e6,
+            os.environ.get("APEX_AMD_LN_BWD_BLOCKS", "default")), flush=True)
+
+
 def bench_lamb(args):
     from apex_example_amd.optimizers import FusedAdam, FusedLAMB
     from apex_example_amd.models.bert import bert_large
@@ -873,14 +900,14 @@ def bench_conv1x1_stats(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "ln-join", "lamb",
                              "attn"])
     ap.add_argument("--quick", action="store_true", help="bn-persist: 14x14 / 7x7 shapes only")
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
     {"bn": bench_bn, "bn-persist": bench_bn_persist, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv1x1-stats": bench_conv1x1_stats, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
-     "ln": bench_ln, "lamb": bench_lamb, "wgrad": bench_wgrad,
+     "ln": bench_ln, "ln-join": bench_ln_join, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
 
