@@ -19,10 +19,59 @@ shape).
 """
 from __future__ import annotations
 
+import os
+import threading
+
 import torch
 import torch.distributed as dist
 
 from .. import _native
+
+# BN backward folded into the consuming conv's data-gradient epilogue (BnBwdSrc below);
+# APEX_AMD_CONV_BN_BWD=0 keeps the separate reduction pass
+_BWD_EPI = os.environ.get("APEX_AMD_CONV_BN_BWD", "1") == "1"
+_TLS = threading.local()
+FUSED_BWD_CALLS = [0]  # BN backwards that took the epilogue sums (diagnostics / tests)
+
+
+class BnBwdSrc:
+    """What a stride-1 data-gradient conv that consumes this BN's output needs to do the
+    BN's backward reduction in its epilogue (ops/conv.py, csrc/hip/conv_igemm.hip
+    ConvBnEpi): the BN input x, the batch mean / invstd, the affine parameters and how
+    to rebuild the ReLU mask (0 none, 1 the forward's bitmask, 2 recompute from x).
+    The conv stores g = mask * dL/dy instead of dL/dy and leaves (g's address, the
+    per-tile sums slab) in ``result``; this BN's backward then skips its reduction
+    pass - and, with a residual, its dz store (dz is g).  The output tensor carries
+    the record as ``_amd_bn_src``."""
+    __slots__ = ("x", "mean", "invstd", "weight", "bias", "mask", "relu_mode", "result")
+
+    def __init__(self, x, mean, invstd, weight, bias, mask, relu_mode):
+        self.x, self.mean, self.invstd = x, mean, invstd
+        self.weight, self.bias, self.mask, self.relu_mode = weight, bias, mask, relu_mode
+        self.result = None
+
+
+def _bwd_src(x, xl, mean, invstd, weight, bias, mask, fuse_relu, has_z):
+    if not (_BWD_EPI and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x is xl and x.size(1) % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return None
+    if fuse_relu and has_z:
+        if mask is None:
+            return None
+        mode = 1
+    elif fuse_relu:
+        if any(t is not None and t.dtype != torch.float32 for t in (weight, bias)):
+            return None
+        mode = 2
+    else:
+        mode = 0
+    return BnBwdSrc(x, mean, invstd, weight, bias, mask, mode)
+
+
+def bn_src_of(x):
+    """The BnBwdSrc of ``x`` when x is a fused BN's output (else None)."""
+    return getattr(x, "_amd_bn_src", None)
 
 
 _TUNED = False
@@ -91,6 +140,8 @@ class BatchNormFunction(torch.autograd.Function):
                                                           bool(fuse_relu), want_mask)
             ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd,
                                   mask)
+            ctx.src = _TLS.src = _bwd_src(x, xl, mean_g, invstd, weight, bias, mask,
+                                          bool(fuse_relu), zl is not None)
             ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = None, 1, bool(fuse_relu), \
                 None, count
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
@@ -117,6 +168,8 @@ class BatchNormFunction(torch.autograd.Function):
                 y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
             ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd,
                                   mask)
+            ctx.src = _TLS.src = _bwd_src(x, xl, mean_g, invstd, weight, bias, mask,
+                                          bool(fuse_relu), zl is not None)
             ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = pg, max(world, 2), \
                 bool(fuse_relu), inv_total, count
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
@@ -147,6 +200,7 @@ class BatchNormFunction(torch.autograd.Function):
         else:
             y, mask = C.apply(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu)), None
         ctx.save_for_backward(xl, zl if mask is None else None, weight, bias, mean_g, invstd, mask)
+        ctx.src = None
         ctx.pg = pg
         ctx.world = max(world, 2) if collective else world  # > 1: collective backward
         ctx.fuse_relu = bool(fuse_relu)
@@ -163,6 +217,29 @@ class BatchNormFunction(torch.autograd.Function):
         xl, zl, weight, bias, mean, invstd, mask = ctx.saved_tensors
         dyl = _to_logical(dy, ctx.shape_channel_last)
         need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        src = ctx.src
+        res = src.result if src is not None else None
+        if res is not None:
+            src.result = None
+        if res is not None and res[0] == dyl.data_ptr() and dyl.is_contiguous(
+                memory_format=torch.channels_last):
+            # the consuming conv's dgrad epilogue already applied the ReLU mask (dy is
+            # g) and summed (g, g*(x-mean)) per tile: no reduction pass, no dz store
+            FUSED_BWD_CALLS[0] += 1
+            if ctx.world > 1:
+                sum_dy, sum_dy_xmu, gw, gb = C.slab_reduce_grad(res[1], invstd, weight, need_w,
+                                                               sum_scale=ctx.total)
+                n = sum_dy.numel()
+                dist.all_reduce(sum_dy.as_strided((2 * n,), (1,)), group=ctx.pg)
+                total = 1.0
+            else:
+                sum_dy, sum_dy_xmu, gw, gb = C.slab_reduce_grad(res[1], invstd, weight, need_w)
+                total = float(ctx.count)
+            dx, _ = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
+                                     total, None, False, False)
+            return (dx, dyl if ctx.has_z else None, gw if need_w else None,
+                    gb if need_w else None, None, None, None, None, None, None, None, None, None,
+                    None, None)
         if ctx.world > 1 and xl.is_cuda:
             # SyncBN: the reduce writes (sum_dy | sum_dy_xmu) / global_count into one [2C]
             # buffer (the scale is a device scalar from the forward's combine) -> ONE
@@ -234,9 +311,15 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentu
     ``num_batches_tracked`` (int64 tensor) is incremented on the device.  ``slab``:
     per-tile statistics a producing conv already summed ([C][2][S], ops/conv.py)."""
     if training:
-        return BatchNormFunction.apply(x, z, weight, bias, running_mean, running_var, eps, momentum,
-                                       process_group, fuse_relu, shape_channel_last,
-                                       num_batches_tracked, force_collectives, slab, slab_shift)
+        _TLS.src = None
+        y = BatchNormFunction.apply(x, z, weight, bias, running_mean, running_var, eps, momentum,
+                                    process_group, fuse_relu, shape_channel_last,
+                                    num_batches_tracked, force_collectives, slab, slab_shift)
+        src = _TLS.src
+        if src is not None:
+            _TLS.src = None
+            y._amd_bn_src = src
+        return y
     # inference: running statistics (autograd through plain torch ops)
     if shape_channel_last:
         xs = x.movedim(-1, 1)

@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from .batch_norm import bn_src_of
 
 # Weight gradients on a side stream (APEX_AMD_WGRAD_STREAM=0 disables): the data
 # gradient stays on the critical path of the main stream while the weight gradient
@@ -293,13 +294,39 @@ def _tag_stats(y):
     return y
 
 
+# ---------------------------------------------------------------- BN backward in the
+# data-gradient epilogue.  A conv whose input is a fused BN's output (the BN tagged it
+# with a BnBwdSrc, ops/batch_norm.py) computes its stride-1 data gradient on the own
+# MFMA kernel with the ConvBnEpi epilogue (csrc/hip/conv_igemm.hip): it stores
+# g = relu_mask * (dY W^T [+ the residual gradient]) and that BN's per-tile sums, and the
+# BN's backward then runs only its elementwise pass.  APEX_AMD_CONV_BN_BWD=0 disables
+# (ops/batch_norm.py).
+
+
+def _bnbwd_ok(dy, weight, src, xshape):
+    return (src is not None and dy.is_cuda and dy.dtype == torch.bfloat16
+            and weight.dtype == torch.bfloat16 and tuple(src.x.shape) == tuple(xshape)
+            and dy.size(1) % 64 == 0 and xshape[1] % 64 == 0
+            and xshape[0] * xshape[2] * xshape[3] < (1 << 31) and _native.available())
+
+
+def _dgrad_bn(dy, wprep, add, src):
+    """g = mask * (conv(dy, wprep) + add) with the BN sums; hands them to the BN."""
+    g, slab = _native.require().conv.conv_fwd_bnbwd(
+        dy, wprep, add, src.x, src.mask, src.mean, src.invstd, src.weight, src.bias,
+        src.relu_mode)
+    src.result = (g.data_ptr(), slab)
+    return g
+
+
 class Conv1x1GemmFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bn=None):
+    def forward(ctx, x, weight, bn=None, src=None):
         ctx.save_for_backward(x, weight)
+        ctx.src = src
         n, ci, h, w = x.shape
-        if ctx.needs_input_grad[0] and _own_1x1(x.dtype, weight.shape[0], ci, n * h * w) \
-                and weight.dtype == torch.bfloat16:
+        if ctx.needs_input_grad[0] and weight.dtype == torch.bfloat16 and (
+                src is not None or _own_1x1(x.dtype, weight.shape[0], ci, n * h * w)):
             _register_prep(weight)  # its dgrad runs on the own kernel with W^T
         return _conv1x1_fwd(x, weight, bn)
 
@@ -310,11 +337,15 @@ class Conv1x1GemmFunction(torch.autograd.Function):
         dx = dw = None
         side = _SideWgrad(weight) if ctx.needs_input_grad[1] else None
         if ctx.needs_input_grad[0]:
-            dx = _conv1x1_dgrad(dy, weight, x.shape)
+            if _bnbwd_ok(dy, weight, ctx.src, x.shape):
+                dx = _dgrad_bn(dy, _transpose_1x1(weight), None, ctx.src)
+            else:
+                dx = _conv1x1_dgrad(dy, weight, x.shape)
+        ctx.src = None
         if ctx.needs_input_grad[1]:
             dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
                           .view(weight.shape), dy, x)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class Conv1x1SkipFunction(torch.autograd.Function):
@@ -326,8 +357,11 @@ class Conv1x1SkipFunction(torch.autograd.Function):
     would otherwise launch)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bn=None):
+    def forward(ctx, x, weight, bn=None, src=None):
         ctx.save_for_backward(x, weight)
+        ctx.src = src
+        if src is not None and ctx.needs_input_grad[0] and weight.dtype == torch.bfloat16:
+            _register_prep(weight)
         return _conv1x1_fwd(x, weight, bn), x.view_as(x)
 
     @staticmethod
@@ -339,9 +373,17 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         if dy is not None:
             dy = dy.contiguous(memory_format=torch.channels_last)
         side = _SideWgrad(weight) if (ctx.needs_input_grad[1] and dy is not None) else None
+        src, ctx.src = ctx.src, None
         if ctx.needs_input_grad[0]:
             if dy is None:
                 dx = dskip
+            elif _bnbwd_ok(dy, weight, src, x.shape) and (
+                    dskip is None or (dskip.dtype == torch.bfloat16 and dskip.shape == x.shape)):
+                # dx = mask * (dskip + dy W^T) with the producing BN's sums (its residual
+                # gradient dz is this same tensor)
+                add = (dskip.contiguous(memory_format=torch.channels_last)
+                       if dskip is not None else None)
+                dx = _dgrad_bn(dy, _transpose_1x1(weight), add, src)
             else:
                 w2 = weight.reshape(co, ci)
                 if dskip is not None:
@@ -355,7 +397,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1] and dy is not None:
             dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
                           .view(weight.shape), dy, x)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class Conv1x1Stride2Function(torch.autograd.Function):
@@ -396,7 +438,8 @@ class Conv2d1x1(nn.Conv2d):
 
     def forward(self, x):
         if self._gemm_ok(x):
-            return _tag_stats(Conv1x1GemmFunction.apply(x, self.weight, _stats_bn(self, x)))
+            return _tag_stats(Conv1x1GemmFunction.apply(x, self.weight, _stats_bn(self, x),
+                                                        bn_src_of(x)))
         if self._strided_ok(x):
             return _tag_stats(Conv1x1Stride2Function.apply(x, self.weight, _stats_bn(self, x)))
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
@@ -405,7 +448,8 @@ class Conv2d1x1(nn.Conv2d):
     def forward_with_skip(self, x):
         """(conv(x), x) with the residual-gradient add fused into the dgrad GEMM."""
         if self._gemm_ok(x):
-            y, skip = Conv1x1SkipFunction.apply(x, self.weight, _stats_bn(self, x))
+            y, skip = Conv1x1SkipFunction.apply(x, self.weight, _stats_bn(self, x),
+                                                bn_src_of(x))
             return _tag_stats(y), skip
         return self.forward(x), x
 
@@ -485,9 +529,10 @@ class Conv3x3Function(torch.autograd.Function):
     (per-tap split-K kernel)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, bn=None):
+    def forward(ctx, x, weight, stride, bn=None, src=None):
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
+        ctx.src = src if stride == 1 else None
         if ctx.needs_input_grad[0] and _USE_ROT_KERNEL:
             _register_prep(weight)
         return _conv_fwd(x, weight, stride, bn)
@@ -503,8 +548,11 @@ class Conv3x3Function(torch.autograd.Function):
         own_wgrad = n_pix < (1 << 22) and (
             _WGRAD3 == "tap" or (_WGRAD3 == "nine" and stride == 1 and x.size(3) <= 56))
         side = _SideWgrad(weight) if (ctx.needs_input_grad[1] and own_wgrad) else None
+        src, ctx.src = ctx.src, None
         if ctx.needs_input_grad[0]:
-            if stride == 1:
+            if stride == 1 and _bnbwd_ok(dy, weight, src, x.shape):
+                dx = _dgrad_bn(dy, _rot_weight(weight), None, src)
+            elif stride == 1:
                 dx = cv.conv_fwd(dy, _rot_weight(weight), 1)
             else:
                 dx = cv.conv_dgrad_s2(dy, _rot_weight(weight), x.size(2), x.size(3))
@@ -517,7 +565,7 @@ class Conv3x3Function(torch.autograd.Function):
                 dw = torch.ops.aten.convolution_backward(
                     dy, x, weight, None, (stride, stride), (1, 1), (1, 1), False, (0, 0), 1,
                     (False, True, False))[1]
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class Conv2d3x3(nn.Conv2d):
@@ -536,7 +584,8 @@ class Conv2d3x3(nn.Conv2d):
                 and x.is_contiguous(memory_format=torch.channels_last) and self.groups == 1
                 and self.in_channels % 64 == 0 and self.out_channels % 64 == 0
                 and self.dilation == (1, 1) and self.padding == (1, 1)):
-            return _tag_stats(Conv3x3Function.apply(x, self.weight, st, _stats_bn(self, x)))
+            return _tag_stats(Conv3x3Function.apply(x, self.weight, st, _stats_bn(self, x),
+                                                    bn_src_of(x)))
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
                         self.groups)
 

@@ -19,6 +19,7 @@ from __future__ import annotations
 import functools
 import itertools
 import operator
+import os
 from collections import OrderedDict
 
 import torch
@@ -27,6 +28,9 @@ from .. import _native
 
 
 _GRAD = operator.attrgetter("grad")
+# native StepPlan launches from the second step on (APEX_AMD_STEP_PLAN=0: the per-step
+# Python launch path, for A/B runs)
+_STEP_PLAN = os.environ.get("APEX_AMD_STEP_PLAN", "1") == "1"
 
 
 class FusedOptimizerBase(torch.optim.Optimizer):
@@ -155,7 +159,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         the plan path (CPU tensors too: the plan calls the CPU kernels).  No-op
         without the extension."""
         c = self._set_cache.get(gid)
-        if c is None or c[2] is not sets or c[3] or not _native.available():
+        if c is None or c[2] is not sets or c[3] or not _STEP_PLAN or not _native.available():
             return
         plans = [_native.require().mt.StepPlan(s["owners"], fixed(s)) for s in sets.values()]
         for s, pl in zip(sets.values(), plans):

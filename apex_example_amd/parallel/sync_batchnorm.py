@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from torch.nn.modules.batchnorm import _BatchNorm
 
 from .. import _native
-from ..ops.batch_norm import BatchNormFunction
+from ..ops.batch_norm import BatchNormFunction  # noqa: F401  (re-exported)
 
 
 _COMM_GROUPS = {}
@@ -133,11 +133,16 @@ class SyncBatchNorm(_BatchNorm):
             pg = False
         elif pg is None and (dist.get_world_size() > 1 or force):
             pg = syncbn_comm_group()
-        return BatchNormFunction.apply(input, z, self.weight, self.bias,
-                                       self.running_mean if self.track_running_stats else None,
-                                       self.running_var if self.track_running_stats else None,
-                                       self.eps, exponential_average_factor, pg, self.fuse_relu,
-                                       channel_last, nbt, force, slab, shift)
+        from ..ops.batch_norm import batch_norm_act
+
+        # (batch_norm_act tags the output for the consuming conv's BN-backward epilogue)
+        return batch_norm_act(input, self.weight, self.bias,
+                              self.running_mean if self.track_running_stats else None,
+                              self.running_var if self.track_running_stats else None,
+                              True, exponential_average_factor, self.eps, z=z,
+                              fuse_relu=self.fuse_relu, process_group=pg,
+                              shape_channel_last=channel_last, num_batches_tracked=nbt,
+                              force_collectives=force, slab=slab, slab_shift=shift)
 
 
 def set_syncbn_force_collectives(module, on=True):

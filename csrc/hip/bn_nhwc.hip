@@ -514,6 +514,29 @@ void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, co
   bn_stats_from_slab(slab, S, C, count, shift, o, ws, st);
 }
 
+// BN backward sums from a data-gradient conv's epilogue (conv_nhwc_fwd_bnbwd): the slab
+// [S][2][C] holds per-M-tile (sum g, sum g*(x-mean)) - the layout reduce_k's partials
+// have - so after the 128-row fold of long slabs the usual reduce finalize applies.
+void bn_slab_reduce_grad(const float* slab, int S, int64_t C, const float* invstd,
+                         float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, DType tw,
+                         float* ws, hipStream_t st, const float* sum_scale) {
+  const float* rows = slab;
+  int R = S;
+  if (S > 2 * kFoldRows) {
+    R = (S + kFoldRows - 1) / kFoldRows;
+    const int C2 = (int)(2 * C);
+    hipLaunchKernelGGL(slab_fold_k, dim3((unsigned)((C2 + kBNThreads - 1) / kBNThreads),
+                                         (unsigned)R),
+                       dim3(kBNThreads), 0, st, slab, S, C2, ws);
+    rows = ws;
+  }
+  bn_dispatch(tw, [&](auto w0) {
+    using TW = decltype(w0);
+    launch_reduce_finalize<TW>(rows, R, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
+                               static_cast<TW*>(gb), st, sum_scale);
+  });
+}
+
 void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
                 hipStream_t st) {
   const bool vec = (C % 8 == 0) && all_aligned({x});

@@ -100,17 +100,130 @@ struct ConvGeom {
   int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
 };
 
+// BN-backward epilogue (conv_tap_k EPI == 1, ConvBnEpi).  Each thread owns one 8-channel
+// column group of the BM x BN output tile and visits ROWS of its rows.  bnbwd_prefetch
+// issues every global load the epilogue needs (residual gradient, BN input x, ReLU
+// bitmask byte, the channel constants) BEFORE the accumulators go to LDS, so their
+// latency hides under the tile write and barrier - the pass is otherwise a chain of
+// dependent loads with few waves per CU.  bnbwd_store then forms, per row chunk,
+// o = T (+ add), g = relu_mask ? o : 0 rounded to bf16, stores g in place of o and
+// accumulates the BN's backward sums of exactly those values: sum(g), sum(g*(x-mean)).
+template <int BM, int BN>
+struct BnPre {
+  static constexpr int CPR = BN / 8;
+  static constexpr int RGS = kCT / CPR;  // row groups; a thread visits rows rg, rg + RGS, ...
+  static constexpr int ROWS = BM / RGS;
+  uint4 av[ROWS], xv[ROWS];
+  unsigned mk[ROWS];
+  float mu[8], sc[8], sh[8];
+};
+
+template <int MODE>
+__device__ __forceinline__ int64_t out_pix(const ConvGeom& g, int m, int z) {
+  if constexpr (MODE == kFwd3 || MODE == kFwd1) {
+    return m;
+  } else {
+    const int GHW = g.GH * g.GW;
+    const int n = m / GHW;
+    const int rem = m - n * GHW;
+    const int gh = rem / g.GW, gw = rem - gh * g.GW;
+    return (int64_t)(n * g.YH + gh * g.ys + (z >> 1)) * g.YW + gw * g.ys + (z & 1);
+  }
+}
+
+template <int MODE, int BM, int BN>
+__device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEpi& ep, int m0,
+                                               int n0, int z, BnPre<BM, BN>& P) {
+  using PT = BnPre<BM, BN>;
+  const int tid = threadIdx.x;
+  const int cc = tid % PT::CPR, rg = tid / PT::CPR;
+  const int c0 = n0 + cc * 8;
+  const int NC = g.NC;
+  const bf16_t* addp = static_cast<const bf16_t*>(ep.add);
+  const bf16_t* xp = static_cast<const bf16_t*>(ep.xbn);
+#pragma unroll
+  for (int q = 0; q < PT::ROWS; ++q) {
+    const int m = m0 + q * PT::RGS + rg;
+    const int64_t opix = out_pix<MODE>(g, m < g.M ? m : 0, z);
+    const int64_t off = opix * NC + c0;
+    P.av[q] = addp ? *reinterpret_cast<const uint4*>(addp + off) : make_uint4(0, 0, 0, 0);
+    P.xv[q] = *reinterpret_cast<const uint4*>(xp + off);
+    P.mk[q] = ep.relu_mode == 1 ? ep.rmask[opix * (NC >> 3) + (c0 >> 3)] : 0xffu;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    P.mu[i] = ep.mean[c0 + i];
+    P.sc[i] = P.sh[i] = 0.f;
+    if (ep.relu_mode == 2) {
+      const float wv = ep.w ? ep.w[c0 + i] : 1.f, bv = ep.b ? ep.b[c0 + i] : 0.f;
+      P.sc[i] = ep.invstd[c0 + i] * wv;
+      P.sh[i] = bv - P.mu[i] * P.sc[i];
+    }
+  }
+}
+
+template <int MODE, int BM, int BN>
+__device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict__ y,
+                                            const ConvGeom& g, const ConvBnEpi& ep, int m0,
+                                            int n0, int z, const BnPre<BM, BN>& P,
+                                            float (&s1)[8], float (&s2)[8]) {
+  using PT = BnPre<BM, BN>;
+  const int tid = threadIdx.x;
+  const int cc = tid % PT::CPR, rg = tid / PT::CPR;
+  const int c0 = n0 + cc * 8;
+  const bool add = ep.add != nullptr;
+#pragma unroll
+  for (int q = 0; q < PT::ROWS; ++q) {
+    const int row = q * PT::RGS + rg;
+    const int m = m0 + row;
+    if (m >= g.M) continue;
+    const uint4 tv = *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+    const unsigned tw[4] = {tv.x, tv.y, tv.z, tv.w};
+    const unsigned aw[4] = {P.av[q].x, P.av[q].y, P.av[q].z, P.av[q].w};
+    const unsigned xw[4] = {P.xv[q].x, P.xv[q].y, P.xv[q].z, P.xv[q].w};
+    unsigned ow[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float o[2], xx[2];
+      o[0] = __uint_as_float(tw[k] << 16);
+      o[1] = __uint_as_float(tw[k] & 0xffff0000u);
+      if (add) {  // the residual gradient (rounded once more, as a separate add would)
+        o[0] += __uint_as_float(aw[k] << 16);
+        o[1] += __uint_as_float(aw[k] & 0xffff0000u);
+      }
+      xx[0] = __uint_as_float(xw[k] << 16);
+      xx[1] = __uint_as_float(xw[k] & 0xffff0000u);
+      unsigned short hb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = 2 * k + h;
+        bool keep = true;
+        if (ep.relu_mode == 1) keep = (P.mk[q] >> i) & 1u;
+        else if (ep.relu_mode == 2) keep = fmaf(xx[h], P.sc[i], P.sh[i]) > 0.f;
+        const bf16_t gb = (bf16_t)(keep ? o[h] : 0.f);
+        const float gv = (float)gb;
+        s1[i] += gv;
+        s2[i] = fmaf(gv, xx[h] - P.mu[i], s2[i]);
+        hb[h] = __builtin_bit_cast(unsigned short, gb);
+      }
+      ow[k] = (unsigned)hb[0] | ((unsigned)hb[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(y + out_pix<MODE>(g, m, z) * g.NC + c0) =
+        make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+}
+
 // NB = 1 (no DMA ring): for 1x1 convs with one or two K-tiles (K = 64 / 128: the
 // ResNet layer1-2 channel-expanding convs) - nothing to overlap inside a workgroup, so
 // the LDS goes to more resident workgroups instead (3 per CU: one's loads overlap
 // another's MFMAs and stores; 4 would cap the registers at 128 and spill the epilogue
 // statistics).
-template <int MODE, int BM, int BN, int WM, int WN, int NB>
+template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0>
 __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024)
-                                           ? 1 : (NB == 1 ? 3 : 2))
+                                           ? 1 : (NB == 1 && EPI == 0 ? 3 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
-               const float* __restrict__ shift) {
+               const float* __restrict__ shift, ConvBnEpi ep) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -201,11 +314,14 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   // epilogue BN statistics (see the store loop): this thread's 8 channels' shift,
   // loaded now so the latency hides under the K loop
   constexpr int CPR = BN / 8;  // 16-byte chunks per output row
-  const bool want_stats = (MODE == kFwd3 || MODE == kFwd1) && slab != nullptr;
+  // EPI == 1 (BN-backward epilogue, ConvBnEpi): slab gets sum(g), sum(g * (x - mean))
+  const bool want_stats = EPI == 1 ? slab != nullptr
+                                   : (MODE == kFwd3 || MODE == kFwd1) && slab != nullptr;
   const int scc = tid % CPR;
   float shv[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) shv[i] = (want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
+  for (int i = 0; i < 8; ++i)
+    shv[i] = (EPI == 0 && want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
 
   // prologue: NB-1 tiles in flight
 #pragma unroll
@@ -253,6 +369,8 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   __syncthreads();
 
   // epilogue: accumulators -> bf16 tile in LDS -> coalesced 16-byte row stores
+  BnPre<BM, BN> pre;
+  if constexpr (EPI == 1) bnbwd_prefetch<MODE, BM, BN>(g, ep, m0, n0, z, pre);
   bf16_t* T = reinterpret_cast<bf16_t*>(lds);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -275,6 +393,9 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   float s1[8], s2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+  if constexpr (EPI == 1) {
+    bnbwd_store<MODE, BM, BN>(T, y, g, ep, m0, n0, z, pre, s1, s2);
+  } else
   for (int c = tid; c < BM * CPR; c += kCT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
@@ -319,8 +440,9 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
         a += red[q * BN + tid];
         b += red[RGS * BN + q * BN + tid];
       }
-      // tile-major [S][2][C]: one coalesced row segment per workgroup
-      float* row = slab + (int64_t)mt * 2 * g.NC;
+      // tile-major [S][2][C]: one coalesced row segment per workgroup (the parity
+      // classes of a stride-2 dgrad, blockIdx.z, own rows after the M tiles)
+      float* row = slab + ((int64_t)z * gridDim.x + mt) * 2 * g.NC;
       row[n0 + tid] = a;
       row[g.NC + n0 + tid] = b;
     }
@@ -346,30 +468,31 @@ static int conv1x1_nb1_max_kt() {
   return e ? std::atoi(e) : 1;
 }
 
-template <int MODE>
+template <int MODE, int EPI = 0>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
-                     hipStream_t st, float* slab = nullptr, const float* shift = nullptr) {
+                     hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
+                     const ConvBnEpi& ep = ConvBnEpi{}) {
   if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
   if (big == 3) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (big) {
     const dim3 grid((g.M + 255) / 256, g.NC / 128, nclasses);
     if (big == 2)
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
     else
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= conv1x1_nb1_max_kt()) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   }
 }
 
@@ -1096,6 +1219,18 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
   auto* yp = static_cast<bf16_t*>(y);
   if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st, stats_slab, stats_shift);
   else launch_conv_tap<kFwd1>(xp, wp, yp, g, st, stats_slab, stats_shift);
+}
+
+void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H, int W, int Cin,
+                         int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,
+                         hipStream_t st) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const ConvGeom g{Ho, Wo, H, W, stride, Ho, Wo, 1, Cin, Cout, N * Ho * Wo, ksize * ksize * Cin};
+  const auto* xp = static_cast<const bf16_t*>(dy);
+  const auto* wp = static_cast<const bf16_t*>(w);
+  auto* yp = static_cast<bf16_t*>(gout);
+  if (ksize == 3) launch_conv_tap<kFwd3, 1>(xp, wp, yp, g, st, slab, nullptr, ep);
+  else launch_conv_tap<kFwd1, 1>(xp, wp, yp, g, st, slab, nullptr, ep);
 }
 
 // Data gradient of a stride-2 conv (3x3 pad 1 or 1x1 pad 0; H = 2*Ho, W = 2*Wo), one

@@ -254,6 +254,25 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
                    int ksize, int stride, hipStream_t st, float* stats_slab = nullptr,
                    const float* stats_shift = nullptr);
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride);
+// BatchNorm-backward epilogue of a data-gradient conv (conv_nhwc_fwd on dY with the
+// rotated / transposed filter): the conv output o (+ add, the residual gradient) is
+// the gradient of a BN(+ReLU) output; the kernel stores g = relu_mask(x) * o instead
+// and writes that BN's per-M-tile sums [S][2][C]: sum(g), sum(g * (x - mean)).
+// relu_mode 0: no ReLU; 1: bitmask rmask [M][C/8] from the forward; 2: recompute
+// x * invstd * w + (b - mean * invstd * w) > 0 (w, b fp32 or null = 1 / 0).
+struct ConvBnEpi {
+  const void* add;       // bf16 [M][C] or null
+  const void* xbn;       // bf16 [M][C]: the BN input
+  const uint8_t* rmask;  // relu_mode 1
+  const float* mean;     // [C]
+  const float* invstd;   // [C] (relu_mode 2)
+  const float* w;        // [C] or null (relu_mode 2)
+  const float* b;        // [C] or null (relu_mode 2)
+  int relu_mode;
+};
+void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* g, int N, int H, int W, int Cin,
+                         int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,
+                         hipStream_t st);
 // BatchNorm statistics from such a slab: local training mode (mean, invstd, running
 // stats, num_batches_tracked) or SyncBN's packed [mean | biased var | count]
 // (slab is tile-major [S][2][C]; ws: bn_slab_workspace(S, C) floats, may be 0)
@@ -263,6 +282,11 @@ void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, con
                          long long* nbt, float eps, float momentum, float* ws, hipStream_t st);
 void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
                           float* packed, float* ws, hipStream_t st);
+// BN backward sums (sum_dy, sum_dy_xmu [* sum_scale], dgamma, dbeta) from a
+// conv_nhwc_fwd_bnbwd slab; ws: bn_slab_workspace(S, C) floats
+void bn_slab_reduce_grad(const float* slab, int S, int64_t C, const float* invstd,
+                         float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, DType tw,
+                         float* ws, hipStream_t st, const float* sum_scale = nullptr);
 // data gradient of a stride-2 conv (H, W even); wt = rotated 3x3 filter / W^T for 1x1
 void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, int W, int Cin,
                         int Cout, int ksize, hipStream_t st);

@@ -117,6 +117,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pool.def("max_fwd_bn", &maxpool2d_nhwc_bn_fwd_op);
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
   conv.def("conv_fwd", &conv_nhwc_fwd_op, py::arg("x"), py::arg("w"), py::arg("stride") = 1);
+  conv.def("conv_fwd_bnbwd", &conv_nhwc_fwd_bnbwd_op, py::arg("dy"), py::arg("w"),
+           py::arg("add"), py::arg("x"), py::arg("rmask"), py::arg("mean"), py::arg("invstd"),
+           py::arg("bn_weight"), py::arg("bn_bias"), py::arg("relu_mode"));
   conv.def("conv_fwd_stats", &conv_nhwc_fwd_stats_op, py::arg("x"), py::arg("w"),
            py::arg("stride") = 1, py::arg("shift") = py::none());
   conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);
@@ -143,6 +146,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bn.def("slab_train_stats", &bn_slab_train_stats_op, py::arg("slab"), py::arg("count"),
          py::arg("shift"), py::arg("running_mean"), py::arg("running_var"), py::arg("nbt"),
          py::arg("eps"), py::arg("momentum"));
+  bn.def("slab_reduce_grad", &bn_slab_reduce_grad_op, py::arg("slab"), py::arg("invstd"),
+         py::arg("weight"), py::arg("need_wgrad"), py::arg("sum_scale") = py::none());
   bn.def("slab_packed_stats", &bn_slab_packed_stats_op, py::arg("slab"), py::arg("count"),
          py::arg("shift"));
   bn.def("set_tuning", &bn_set_tuning, py::arg("red_rpt") = -1, py::arg("red_cap") = -1,

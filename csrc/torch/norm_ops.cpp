@@ -672,6 +672,40 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
   return {mean, invstd};
 }
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_op(
+    at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
+                  slab.scalar_type() == at::kFloat && slab.is_contiguous(),
+              "bn slab reduce: fp32 [S][2][C] slab expected");
+  const int64_t S = slab.size(0), C = slab.size(2);
+  TORCH_CHECK(invstd.is_cuda() && invstd.scalar_type() == at::kFloat && invstd.numel() == C,
+              "bn slab reduce: invstd must be fp32 [C]");
+  auto fopt = slab.options();
+  // one [2C] buffer (sum_dy | sum_dy_xmu): SyncBN all-reduces it in place
+  at::Tensor packed = at::empty({2 * C}, fopt);
+  at::Tensor sum_dy = packed.narrow(0, 0, C), sum_dy_xmu = packed.narrow(0, C, C);
+  at::Tensor gw, gb;
+  DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
+  if (need_wgrad && has(weight)) {
+    gw = at::empty_like(*weight);
+    gb = at::empty_like(*weight);
+  }
+  const float* scale = nullptr;
+  if (has(sum_scale)) {
+    TORCH_CHECK(sum_scale->is_cuda() && sum_scale->scalar_type() == at::kFloat &&
+                    sum_scale->numel() == 1,
+                "bn slab reduce: sum_scale must be a 1-element fp32 GPU tensor");
+    scale = sum_scale->data_ptr<float>();
+  }
+  at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, fopt);
+  bn_slab_reduce_grad(slab.data_ptr<float>(), (int)S, C, invstd.contiguous().data_ptr<float>(),
+                      sum_dy.data_ptr<float>(), sum_dy_xmu.data_ptr<float>(),
+                      gw.defined() ? gw.data_ptr() : nullptr, gb.defined() ? gb.data_ptr() : nullptr,
+                      tw, ws.data_ptr<float>(), cur_stream(), scale);
+  return {sum_dy, sum_dy_xmu, gw, gb};
+}
+
 at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&

@@ -82,6 +82,8 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
                                                           OptT shift, OptT running_mean,
                                                           OptT running_var, OptT nbt,
                                                           double eps, double momentum);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_op(
+    at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale);
 at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift);
 
 }  // namespace amd

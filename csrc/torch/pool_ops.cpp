@@ -127,6 +127,68 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tens
   return {y, slab};
 }
 
+// Stride-1 data-gradient conv (dy with the rotated 3x3 / transposed 1x1 filter) whose
+// output is the gradient of a BN(+ReLU) output: stores g = relu_mask * (conv + add) and
+// returns it with that BN's per-M-tile backward sums [S][2][C] (ConvBnEpi).
+std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
+    at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> add, at::Tensor xbn,
+    c10::optional<at::Tensor> rmask, at::Tensor mean, at::Tensor invstd,
+    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && w.dim() == 4, "conv_bnbwd: 4-D GPU tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  xbn.scalar_type() == at::kBFloat16,
+              "conv_bnbwd: bf16 only");
+  const int64_t N = dy.size(0), Cin = dy.size(1), H = dy.size(2), W = dy.size(3);
+  const int64_t Cout = w.size(0), k = w.size(2);
+  TORCH_CHECK((k == 3 || k == 1) && w.size(3) == k && w.size(1) == Cin, "conv_bnbwd: weight");
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cin, (int)Cout), "conv_bnbwd: channels must be x64");
+  TORCH_CHECK(N * H * W < (int64_t)1 << 31, "conv_bnbwd: too many pixels");
+  TORCH_CHECK(relu_mode >= 0 && relu_mode <= 2, "conv_bnbwd: relu_mode 0 | 1 | 2");
+  const auto cl = at::MemoryFormat::ChannelsLast;
+  auto same_out = [&](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.size(0) == N && t.size(1) == Cout &&
+                    t.size(2) == H && t.size(3) == W && t.scalar_type() == at::kBFloat16 &&
+                    t.is_contiguous(cl),
+                "conv_bnbwd: ", what, " must be a channels-last bf16 tensor shaped like the output");
+  };
+  same_out(xbn, "x");
+  ConvBnEpi ep{};
+  if (add.has_value() && add->defined()) {
+    same_out(*add, "add");
+    ep.add = add->data_ptr();
+  }
+  ep.xbn = xbn.data_ptr();
+  auto vecf = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() == Cout,
+                "conv_bnbwd: ", what, " must be a contiguous fp32 [C] GPU tensor");
+    return t->data_ptr<float>();
+  };
+  ep.mean = vecf(mean, "mean");
+  ep.invstd = vecf(invstd, "invstd");
+  ep.w = vecf(bn_w, "weight");
+  ep.b = vecf(bn_b, "bias");
+  TORCH_CHECK(ep.mean && ep.invstd, "conv_bnbwd: mean / invstd required");
+  ep.relu_mode = (int)relu_mode;
+  if (relu_mode == 1) {
+    TORCH_CHECK(rmask.has_value() && rmask->defined() && rmask->is_cuda() &&
+                    rmask->scalar_type() == at::kByte && rmask->is_contiguous() &&
+                    rmask->numel() == N * H * W * (Cout / 8),
+                "conv_bnbwd: relu_mode 1 needs the forward's [M][C/8] uint8 bitmask");
+    ep.rmask = rmask->data_ptr<uint8_t>();
+  }
+  dy = dy.contiguous(cl);
+  w = w.contiguous(cl);
+  at::Tensor g = at::empty({N, Cout, H, W}, dy.options().memory_format(cl));
+  const int S = conv_fwd_mtiles((int)N, (int)H, (int)W, (int)Cout, 1);
+  at::Tensor slab = at::empty({S, 2, Cout}, dy.options().dtype(at::kFloat));
+  conv_nhwc_fwd_bnbwd(dy.data_ptr(), w.data_ptr(), g.data_ptr(), (int)N, (int)H, (int)W,
+                      (int)Cin, (int)Cout, (int)k, 1, ep, slab.data_ptr<float>(), cur_stream());
+  return {g, slab};
+}
+
 at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && wt.dim() == 4, "conv_dgrad_s2: 4-D GPU tensors");

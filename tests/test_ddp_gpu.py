@@ -333,7 +333,8 @@ def test_ddp_side_stream_weight_grads_match_main_stream(pg):
         for side in (False, True):
             convmod._DDP_SIDE = side
             torch.manual_seed(0)
-            m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+            m = resnet18(num_classes=10, fused_bn=True, gemm_1x1=True).cuda().to(
+                memory_format=torch.channels_last)
             opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, materialize_master_grads=False)
             m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16,
                                     verbosity=0)
@@ -366,7 +367,7 @@ def test_ddp_side_stream_weight_grads_match_main_stream(pg):
                 convmod._SideWgrad.run = orig
             torch.cuda.synchronize()
             results[side] = (grads, [p.detach().clone() for p in m.parameters()])
-            used[side] = (calls["n"], sorted(set(modes)))
+            used[side] = (calls["n"], sorted(set(modes), key=str))
     finally:
         convmod._DDP_SIDE = prev
     assert used[False][0] == 0 and used[True][0] > 0, used

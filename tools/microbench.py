@@ -830,6 +830,77 @@ def bench_ln_join(args):
             os.environ.get("APEX_AMD_LN_BWD_BLOCKS", "default")), flush=True)
 
 
+def bench_conv_bnbwd(args):
+    """BN backward folded into the dgrad conv epilogue vs the unfused chain, per ResNet-50
+    shape (bs 256): unfused = dgrad (own kernel, or the hipBLASLt addmm with the residual
+    gradient) + BN reduce + BN elementwise backward (+ dz); fused = conv_fwd_bnbwd +
+    slab_reduce_grad + elementwise backward (no dz)."""
+    from apex_example_amd import _native
+
+    C = _native.require()
+    dev = "cuda"
+    cl = torch.channels_last
+    print("| case | dy -> BN ch @ HW | unfused us (dgrad / reduce / elem) | fused us (conv / fin+elem) | saved |")
+    print("|---|---|---|---|---|")
+    cases = []
+    for hw, p in ((56, 64), (28, 128), (14, 256), (7, 512)):
+        cases.append(("3x3 -> bn1", p, p, hw, 3, 2, False))
+        cases.append(("1x1 4p->p -> bn2", 4 * p, p, hw, 1, 2, False))
+        cases.append(("1x1 p->4p +skip -> bn3", p, 4 * p, hw, 1, 1, True))
+    tot = [0.0, 0.0]
+    for name, cd, co, hw, k, mode, skip in cases:
+        n = 256
+        dy = torch.randn(n, cd, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+        wt = (torch.randn(co, cd, k, k, device=dev) / (cd * k * k) ** 0.5).to(
+            torch.bfloat16).contiguous(memory_format=cl)
+        x = torch.randn(n, co, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+        add = torch.randn_like(x) if skip else None
+        mean = torch.zeros(co, device=dev)
+        invstd = torch.ones(co, device=dev)
+        bw, bb = torch.ones(co, device=dev), torch.zeros(co, device=dev)
+        z = torch.randn_like(x) if skip else None
+        _, mask = C.bn.apply_mask(x, mean, invstd, bw, bb, z, True) if skip else (None, None)
+        M = n * hw * hw
+        w2 = wt.reshape(co, cd).t().contiguous() if k == 1 else None
+
+        def dgrad():
+            if skip:
+                return torch.addmm(add.permute(0, 2, 3, 1).reshape(M, co),
+                                   dy.permute(0, 2, 3, 1).reshape(M, cd), w2)
+            return C.conv.conv_fwd(dy, wt, 1)
+        o = dgrad()
+        o4 = o if not skip else o.view(n, hw, hw, co).permute(0, 3, 1, 2)
+        zz = None if skip else None
+
+        def red():
+            return C.bn.reduce_grad(o4, x, mean, invstd, bw, bb, zz, True, True, mask=mask)
+        sdy, sdx, _, _ = red()
+
+        def elem():
+            return C.bn.backward_elemt(o4, x, mean, invstd, bw, bb, sdy, sdx, float(M), zz, True,
+                                       skip, mask=mask)
+        t_d, t_r, t_e = timeit(dgrad), timeit(red), timeit(elem)
+        g, slab = C.conv.conv_fwd_bnbwd(dy, wt, add, x, mask, mean, invstd, bw, bb,
+                                        1 if skip else mode)
+
+        def fused_conv():
+            return C.conv.conv_fwd_bnbwd(dy, wt, add, x, mask, mean, invstd, bw, bb,
+                                         1 if skip else mode)
+
+        def fin_elem():
+            a, b_, _, _ = C.bn.slab_reduce_grad(slab, invstd, bw, True)
+            return C.bn.backward_elemt(g, x, mean, invstd, bw, bb, a, b_, float(M), None, False,
+                                       False)
+        t_f, t_fe = timeit(fused_conv), timeit(fin_elem)
+        un, fu = t_d + t_r + t_e, t_f + t_fe
+        tot[0] += un
+        tot[1] += fu
+        print("| %s | %d -> %d @ %d | %.0f (%.0f / %.0f / %.0f) | %.0f (%.0f / %.0f) | %+.0f |" % (
+            name, cd, co, hw, un, t_d, t_r, t_e, fu, t_f, t_fe, un - fu), flush=True)
+    print("| total (one layer per case) | | %.0f | %.0f | %+.0f |" % (tot[0], tot[1],
+                                                                    tot[0] - tot[1]))
+
+
 def bench_lamb(args):
     from apex_example_amd.optimizers import FusedAdam, FusedLAMB
     from apex_example_amd.models.bert import bert_large
@@ -900,14 +971,14 @@ def bench_conv1x1_stats(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "ln-join", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "ln-join", "conv-bnbwd", "lamb",
                              "attn"])
     ap.add_argument("--quick", action="store_true", help="bn-persist: 14x14 / 7x7 shapes only")
     ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
                     help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
     {"bn": bench_bn, "bn-persist": bench_bn_persist, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv1x1-stats": bench_conv1x1_stats, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
-     "ln": bench_ln, "ln-join": bench_ln_join, "lamb": bench_lamb, "wgrad": bench_wgrad,
+     "ln": bench_ln, "ln-join": bench_ln_join, "conv-bnbwd": bench_conv_bnbwd, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 
 
