@@ -127,17 +127,39 @@ def _dev_scalar(v, device):
     return torch.tensor(float(v), dtype=torch.float32, device=device)
 
 
+def _per_tensor(vals, n, dev):
+    """Per-tensor scalars (a tensor or a list of numbers / 1-element tensors) as a
+    contiguous fp32 device array [n] (no host sync for device inputs)."""
+    if isinstance(vals, torch.Tensor):
+        t = vals.reshape(-1)
+    elif all(isinstance(v, torch.Tensor) for v in vals):
+        t = torch.stack([v.reshape(()) for v in vals])
+    else:
+        t = torch.tensor([float(v) for v in vals], dtype=torch.float32)
+    t = t.to(device=dev, dtype=torch.float32).contiguous()
+    assert t.numel() == n, "one value per tensor expected"
+    return t
+
+
 def multi_tensor_lamb_stage1_cuda(chunk_size, noop_flag, tensor_lists, per_tensor_decay, step,
                                   beta1, beta2, epsilon, global_grad_norm, max_global_grad_norm):
     """Legacy two-stage LAMB, stage 1 (apex csrc/multi_tensor_lamb_stage_1.cu): Adam
     moments of the clipped grad and the update u = m^/(sqrt(v^)+eps) + decay_i * p
     written into tensor_lists[4].  API parity for callers of the old interface (the
-    fused path is multi_tensor_lamb): composed from device tensor ops with the
-    overflow flag and the global norm kept on the device - no host sync."""
+    fused path is multi_tensor_lamb).  GPU: one multi-tensor launch
+    (csrc/hip/mt_optim.hip lamb_legacy1_kernel) reading the overflow flag and the global
+    norm on the device; CPU: the same math from tensor ops."""
     g, p, m, v, u = tensor_lists
     if not g:
         return
     dev = p[0].device
+    if dev.type == "cuda" and _native.available():
+        _C().lamb_legacy_stage1(noop_flag, [list(g), list(p), list(m), list(v), list(u)],
+                                _per_tensor(per_tensor_decay, len(g), dev), int(step),
+                                float(beta1), float(beta2), float(epsilon),
+                                _dev_scalar(global_grad_norm, dev).reshape(1),
+                                float(max_global_grad_norm))
+        return
     keep = noop_flag.reshape(()).to(dev).eq(0)
     gn = _dev_scalar(global_grad_norm, dev)
     mx = float(max_global_grad_norm)
@@ -161,11 +183,17 @@ def multi_tensor_lamb_stage2_cuda(chunk_size, noop_flag, tensor_lists, per_tenso
                                   per_tensor_update_norm, lr, weight_decay=0.0, use_nvlamb=False):
     """Legacy LAMB stage 2: p -= lr * (||p|| / ||u||) * u per tensor (trust ratio 1
     when a norm is zero, plain lr when neither weight decay nor nvlamb applies).
-    Device-side like stage 1: no host sync."""
+    GPU: one launch (lamb_legacy2_kernel); CPU: tensor ops.  No host sync either way."""
     p, u = tensor_lists[:2]
     if not p:
         return
     dev = p[0].device
+    if dev.type == "cuda" and _native.available():
+        _C().lamb_legacy_stage2(noop_flag, [list(p), list(u)],
+                                _per_tensor(per_tensor_param_norm, len(p), dev),
+                                _per_tensor(per_tensor_update_norm, len(p), dev), float(lr),
+                                float(weight_decay), bool(use_nvlamb))
+        return
     keep = noop_flag.reshape(()).to(dev).eq(0)
     with torch.no_grad():
         for i in range(len(p)):

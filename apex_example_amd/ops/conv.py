@@ -303,11 +303,21 @@ def _tag_stats(y):
 # (ops/batch_norm.py).
 
 
-def _bnbwd_ok(dy, weight, src, xshape):
+# Where the epilogue pays (tools/microbench.py conv-bnbwd, profiles/microbench_conv_bnbwd.txt,
+# one MI355X): with a residual gradient to add (the bottleneck's conv1 dgrad feeding the
+# previous block's bn3) it replaces the hipBLASLt addmm + reduce pass + dz store and wins
+# 10-260 us per layer; without one (bn1 / bn2) the extra read of the BN input in the
+# epilogue costs more than the reduce pass it saves except on small layers (7x7: M =
+# 12544), so those fuse only below APEX_AMD_CONV_BN_BWD_MAXM output pixels.
+_BNBWD_MAX_M = int(os.environ.get("APEX_AMD_CONV_BN_BWD_MAXM", "16384"))
+
+
+def _bnbwd_ok(dy, weight, src, xshape, has_add=False):
+    m = xshape[0] * xshape[2] * xshape[3]
     return (src is not None and dy.is_cuda and dy.dtype == torch.bfloat16
             and weight.dtype == torch.bfloat16 and tuple(src.x.shape) == tuple(xshape)
-            and dy.size(1) % 64 == 0 and xshape[1] % 64 == 0
-            and xshape[0] * xshape[2] * xshape[3] < (1 << 31) and _native.available())
+            and dy.size(1) % 64 == 0 and xshape[1] % 64 == 0 and m < (1 << 31)
+            and (has_add or m <= _BNBWD_MAX_M) and _native.available())
 
 
 def _dgrad_bn(dy, wprep, add, src):
@@ -377,7 +387,7 @@ class Conv1x1SkipFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if dy is None:
                 dx = dskip
-            elif _bnbwd_ok(dy, weight, src, x.shape) and (
+            elif _bnbwd_ok(dy, weight, src, x.shape, has_add=dskip is not None) and (
                     dskip is None or (dskip.dtype == torch.bfloat16 and dskip.shape == x.shape)):
                 # dx = mask * (dskip + dy W^T) with the producing BN's sums (its residual
                 # gradient dz is this same tensor)

@@ -323,6 +323,12 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   for (int i = 0; i < 8; ++i)
     shv[i] = (EPI == 0 && want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
 
+  // BN-backward epilogue operands: issued before the first tile so they arrive during
+  // the K loop (oldest in the vmcnt queue, so the counted waits below only ever wait
+  // for them early, never skip them); a __syncthreads() fences them anyway
+  BnPre<BM, BN> pre;
+  if constexpr (EPI == 1) bnbwd_prefetch<MODE, BM, BN>(g, ep, m0, n0, z, pre);
+
   // prologue: NB-1 tiles in flight
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
@@ -369,8 +375,6 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   __syncthreads();
 
   // epilogue: accumulators -> bf16 tile in LDS -> coalesced 16-byte row stores
-  BnPre<BM, BN> pre;
-  if constexpr (EPI == 1) bnbwd_prefetch<MODE, BM, BN>(g, ep, m0, n0, z, pre);
   bf16_t* T = reinterpret_cast<bf16_t*>(lds);
 #pragma unroll
   for (int i = 0; i < FM; ++i)

@@ -325,6 +325,121 @@ __global__ void __launch_bounds__(kMTThreads)
   }
 }
 
+// ---------------------------------------------------------------- legacy two-stage LAMB
+// (apex csrc/multi_tensor_lamb_stage_1.cu / _2.cu semantics; lists [g, p, m, v, u] and
+// [p, u], m / v / u stored in the parameter type)
+template <typename TG, typename TP>
+__global__ void __launch_bounds__(kMTThreads)
+    lamb_legacy1_kernel(MTLaunch L, LambLegacyArgs a, const int* noop) {
+  if (skip_step(noop)) return;
+  const float gn = *a.global_grad_norm;
+  const float inv_clip = gn > a.max_grad_norm ? a.max_grad_norm / gn : 1.f;
+  const float ib1 = 1.f / a.bc1, ib2 = 1.f / a.bc2;
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const TileCtx c = tile_ctx(L, ch);
+    const float decay = a.decay[L.chunks[ch].tensor];
+    const bool al = c.t->aligned;
+#pragma unroll 1
+    for (int h = 0; h < kMTUnroll / UA; ++h) {
+      float g[UA][8], p[UA][8], m[UA][8], v[UA][8];
+#pragma unroll
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+        ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+        ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+        ld<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+        ld<TP>(c.t->ptr[3], idx, cnt, vec, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float gi = g[u][i] * inv_clip;
+          m[u][i] = fmaf(a.beta1, m[u][i], (1.f - a.beta1) * gi);
+          v[u][i] = fmaf(a.beta2, v[u][i], (1.f - a.beta2) * gi * gi);
+          const float den = sqrtf(v[u][i] * ib2) + a.eps;
+          g[u][i] = fmaf(decay, p[u][i], (m[u][i] * ib1) / den);  // u (in g's registers)
+        }
+        st<TP>(c.t->ptr[2], idx, cnt, vec, m[u]);
+        st<TP>(c.t->ptr[3], idx, cnt, vec, v[u]);
+        st<TP>(c.t->ptr[4], idx, cnt, vec, g[u]);
+      }
+    }
+  }
+}
+
+template <typename TP, typename TU>
+__global__ void __launch_bounds__(kMTThreads)
+    lamb_legacy2_kernel(MTLaunch L, LambLegacyArgs a, const int* noop) {
+  if (skip_step(noop)) return;
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
+    const int tensor = L.chunks[ch].tensor;
+    const TileCtx c = tile_ctx(L, ch);
+    const bool al = c.t->aligned;
+    float ratio = a.lr;
+    if (a.use_nvlamb || a.wd != 0.f) {
+      const float pn = a.param_norms[tensor], un = a.update_norms[tensor];
+      ratio = (pn != 0.f && un != 0.f) ? a.lr * (pn / un) : a.lr;
+    }
+#pragma unroll 1
+    for (int h = 0; h < kMTUnroll / UA; ++h) {
+      float p[UA][8], uu[UA][8];
+#pragma unroll
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+        ld<TP>(c.t->ptr[0], idx, cnt, vec, p[u]);
+        ld<TU>(c.t->ptr[1], idx, cnt, vec, uu[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UA; ++u) {
+        const int off = lane_off(h * UA + u), cnt = c.n - off;
+        if (cnt <= 0) continue;
+        const bool vec = al && cnt >= 8;
+        const int64_t idx = c.start + off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[u][i] = fmaf(-ratio, uu[u][i], p[u][i]);
+        st<TP>(c.t->ptr[0], idx, cnt, vec, p[u]);
+      }
+    }
+  }
+}
+
+void mt_lamb_legacy_stage1(const MTLaunch& L, DType g, DType p, const LambLegacyArgs& a,
+                           const int* noop, hipStream_t st) {
+  if (L.nchunks == 0) return;
+  dispatch1(g, [&](auto tg) {
+    dispatch1(p, [&](auto tp) {
+      using TG = decltype(tg);
+      using TP = decltype(tp);
+      hipLaunchKernelGGL((lamb_legacy1_kernel<TG, TP>), mt_pgrid(L), dim3(kMTThreads), 0, st, L,
+                         a, noop);
+    });
+  });
+}
+
+void mt_lamb_legacy_stage2(const MTLaunch& L, DType p, DType u, const LambLegacyArgs& a,
+                           const int* noop, hipStream_t st) {
+  if (L.nchunks == 0) return;
+  dispatch1(p, [&](auto tp) {
+    dispatch1(u, [&](auto tu) {
+      using TP = decltype(tp);
+      using TU = decltype(tu);
+      hipLaunchKernelGGL((lamb_legacy2_kernel<TP, TU>), mt_pgrid(L), dim3(kMTThreads), 0, st, L,
+                         a, noop);
+    });
+  });
+}
+
 void mt_lamb_stage1(const MTLaunch& L, DType g, DType p, const LambArgs& a, float* partials,
                     const int* noop, hipStream_t st) {
   if (L.nchunks == 0) return;

@@ -90,6 +90,25 @@ void mt_lamb_stage1(const MTLaunch& L, DType g, DType p, const LambArgs& a, floa
 void mt_lamb_stage2(const MTLaunch& L, int depth, DType p, DType copy, const LambArgs& a,
                     const float* param_norms, const float* update_norms, const int* noop,
                     hipStream_t st);
+// Legacy two-stage LAMB interface (apex multi_tensor_lamb_stage1_cuda / stage2_cuda):
+// stage 1 lists [g, p, m, v, u]: Adam moments of g / clip (clip = max(1, ||g|| / max_norm),
+// ||g|| a device scalar), u = m^ / (sqrt(v^) + eps) + decay[t] * p;  stage 2 lists [p, u]:
+// p -= ratio_t * u with ratio_t = lr * ||p_t|| / ||u_t|| (nvlamb or wd != 0; lr when a norm
+// is 0) - per-tensor decay / norms are device arrays [ntensors]
+struct LambLegacyArgs {
+  float beta1, beta2, eps, bc1, bc2;  // bias corrections 1 - beta^step
+  const float* global_grad_norm;
+  float max_grad_norm;
+  const float* decay;
+  float lr, wd;
+  int use_nvlamb;
+  const float* param_norms;
+  const float* update_norms;
+};
+void mt_lamb_legacy_stage1(const MTLaunch& L, DType g, DType p, const LambLegacyArgs& a,
+                           const int* noop, hipStream_t st);
+void mt_lamb_legacy_stage2(const MTLaunch& L, DType p, DType u, const LambLegacyArgs& a,
+                           const int* noop, hipStream_t st);
 
 struct NovoArgs {
   float lr, beta1, beta2, eps, wd;

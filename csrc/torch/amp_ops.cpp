@@ -6,6 +6,8 @@
 // tensor so the optimizer step needs no host synchronisation.
 #include "amp_ops.h"
 
+#include <cmath>
+
 #include <c10/hip/HIPGraphsC10Utils.h>
 
 #include "../cpu/cpu_ops.h"
@@ -294,6 +296,63 @@ void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, c10::optio
     mt_lamb_stage2(P2.L, (int)s2.size(), dtype_of(g[1][0]), copy, a, norms.data_ptr<float>(),
                    norms.data_ptr<float>() + P1.L.ntensors, noop_ptr(noop), cur_stream());
   });
+}
+
+// Legacy two-stage LAMB (apex amp_C.multi_tensor_lamb_stage1_cuda / stage2_cuda): GPU only,
+// the CPU facade composes the same math from tensor ops (amp_C.py)
+void mt_lamb_legacy_stage1_op(at::Tensor noop, const TensorLists& lists, at::Tensor decay,
+                              int64_t step, double beta1, double beta2, double eps,
+                              at::Tensor global_grad_norm, double max_grad_norm) {
+  c10::NoGradGuard no_grad_;
+  if (lists.empty() || lists[0].empty()) return;
+  TORCH_CHECK(lists.size() == 5, "lamb stage 1: lists [g, p, m, v, u]");
+  TORCH_CHECK(mt_validate(lists, 5, 5), "lamb stage 1: GPU tensors only");
+  const int64_t n = (int64_t)lists[0].size();
+  TORCH_CHECK(decay.is_cuda() && decay.scalar_type() == at::kFloat && decay.numel() == n &&
+                  decay.is_contiguous(),
+              "lamb stage 1: per_tensor_decay must be a contiguous fp32 GPU tensor [ntensors]");
+  TORCH_CHECK(global_grad_norm.is_cuda() && global_grad_norm.scalar_type() == at::kFloat &&
+                  global_grad_norm.numel() >= 1,
+              "lamb stage 1: global_grad_norm must be an fp32 GPU scalar");
+  TORCH_CHECK(step >= 1, "lamb stage 1: step >= 1");
+  LambLegacyArgs a{};
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.bc1 = (float)(1.0 - std::pow(beta1, (double)step));
+  a.bc2 = (float)(1.0 - std::pow(beta2, (double)step));
+  a.global_grad_norm = global_grad_norm.data_ptr<float>();
+  a.max_grad_norm = (float)max_grad_norm;
+  a.decay = decay.data_ptr<float>();
+  for (int d = 2; d < 5; ++d)
+    TORCH_CHECK(lists[d][0].scalar_type() == lists[1][0].scalar_type(),
+                "lamb stage 1: m / v / u must match the parameter dtype");
+  const MTPlan P = mt_plan(lists);
+  mt_lamb_legacy_stage1(P.L, dtype_of(lists[0][0]), dtype_of(lists[1][0]), a, noop_ptr(noop),
+                        cur_stream());
+}
+
+void mt_lamb_legacy_stage2_op(at::Tensor noop, const TensorLists& lists, at::Tensor param_norms,
+                              at::Tensor update_norms, double lr, double weight_decay,
+                              bool use_nvlamb) {
+  c10::NoGradGuard no_grad_;
+  if (lists.empty() || lists[0].empty()) return;
+  TORCH_CHECK(lists.size() == 2, "lamb stage 2: lists [p, u]");
+  TORCH_CHECK(mt_validate(lists, 2, 2), "lamb stage 2: GPU tensors only");
+  const int64_t n = (int64_t)lists[0].size();
+  for (const at::Tensor* t : {&param_norms, &update_norms})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == n &&
+                    t->is_contiguous(),
+                "lamb stage 2: per-tensor norms must be contiguous fp32 GPU tensors [ntensors]");
+  LambLegacyArgs a{};
+  a.lr = (float)lr;
+  a.wd = (float)weight_decay;
+  a.use_nvlamb = use_nvlamb ? 1 : 0;
+  a.param_norms = param_norms.data_ptr<float>();
+  a.update_norms = update_norms.data_ptr<float>();
+  const MTPlan P = mt_plan(lists);
+  mt_lamb_legacy_stage2(P.L, dtype_of(lists[0][0]), dtype_of(lists[1][0]), a, noop_ptr(noop),
+                        cur_stream());
 }
 
 void mt_novograd_op(at::Tensor noop, const TensorLists& lists, at::Tensor v, at::Tensor grad_norms,

@@ -33,6 +33,12 @@ void mt_lamb_op(at::Tensor noop, const TensorLists& lists, double lr, OptT lr_t,
                 double beta2, double eps, int64_t step, OptT step_t, bool bias_correction,
                 double wd, bool grad_averaging, int64_t mode, OptT global_grad_norm,
                 double max_grad_norm, bool use_nvlamb, double scale, OptT scale_t, bool scale_inv);
+void mt_lamb_legacy_stage1_op(at::Tensor noop, const TensorLists& lists, at::Tensor decay,
+                              int64_t step, double beta1, double beta2, double eps,
+                              at::Tensor global_grad_norm, double max_grad_norm);
+void mt_lamb_legacy_stage2_op(at::Tensor noop, const TensorLists& lists, at::Tensor param_norms,
+                              at::Tensor update_norms, double lr, double weight_decay,
+                              bool use_nvlamb);
 void mt_novograd_op(at::Tensor noop, const TensorLists& lists, at::Tensor v, at::Tensor grad_norms,
                     bool first_step, double lr, OptT lr_t, double beta1, double beta2, double eps,
                     int64_t step, OptT step_t, bool bias_correction, double wd,

@@ -58,6 +58,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mt.def("sgd", &mt_sgd_op);
   mt.def("adam", &mt_adam_op);
   mt.def("lamb", &mt_lamb_op);
+  mt.def("lamb_legacy_stage1", &mt_lamb_legacy_stage1_op);
+  mt.def("lamb_legacy_stage2", &mt_lamb_legacy_stage2_op);
   mt.def("novograd", &mt_novograd_op);
   mt.def("adagrad", &mt_adagrad_op);
   mt.def("update_loss_scale", &update_loss_scale_op, py::arg("scale"), py::arg("unskipped"),

@@ -293,7 +293,7 @@ def ddp_amp_vs_local(rank, world, opt_level="O2", fused=False, iters=3):
     return {"diffs": diffs}
 
 
-def gpu_ddp_resnet(rank, world, steps=4, syncbn=False, lr=0.05, opt_level="O2"):
+def gpu_ddp_resnet(rank, world, steps=4, syncbn=False, lr=0.05, opt_level="O2", hw=32):
     """Two ranks sharing cuda:0 over gloo (RCCL refuses two ranks on one GPU): the
     GPU-side DDP path of bench.py - amp O2 bf16, fused BN, GEMM convs, FusedSGD,
     bucket views - must keep replicas identical and match a one-process run on
@@ -312,7 +312,7 @@ def gpu_ddp_resnet(rank, world, steps=4, syncbn=False, lr=0.05, opt_level="O2"):
     opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, materialize_master_grads=False)
     m, opt = amp.initialize(m, opt, opt_level=opt_level, half_dtype=torch.bfloat16, verbosity=0)
     ddp = DistributedDataParallel(m, message_size=200_000)
-    x, y = _resnet_batch(rank)
+    x, y = _resnet_batch(rank, hw=hw)
     losses, masters1 = [], None
     for i in range(steps):
         loss = F.cross_entropy(ddp(x), y)
@@ -330,14 +330,14 @@ def gpu_ddp_resnet(rank, world, steps=4, syncbn=False, lr=0.05, opt_level="O2"):
             "views": all(getattr(p, "_amd_grad_is_bucket_view", False) for p in m.parameters())}
 
 
-def _resnet_batch(rank, bs=8):
+def _resnet_batch(rank, bs=8, hw=32):
     g = torch.Generator().manual_seed(5 + rank)
-    x = torch.randn(bs, 3, 32, 32, generator=g).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(bs, 3, hw, hw, generator=g).cuda().to(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (bs,), generator=g).cuda()
     return x, y
 
 
-def gpu_resnet_reference(world=2, steps=4, lr=0.05, opt_level="O2"):
+def gpu_resnet_reference(world=2, steps=4, lr=0.05, opt_level="O2", hw=32):
     """One process, the concatenated per-rank batches of ``gpu_ddp_resnet``,
     local BN (= SyncBN statistics over the global batch), no DDP."""
     from apex_example_amd import amp
@@ -351,7 +351,7 @@ def gpu_resnet_reference(world=2, steps=4, lr=0.05, opt_level="O2"):
     p0 = [p.detach().float().cpu().clone() for p in m.parameters()]
     opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, materialize_master_grads=False)
     m, opt = amp.initialize(m, opt, opt_level=opt_level, half_dtype=torch.bfloat16, verbosity=0)
-    batches = [_resnet_batch(r) for r in range(world)]
+    batches = [_resnet_batch(r, hw=hw) for r in range(world)]
     x = torch.cat([b[0] for b in batches]).contiguous(memory_format=torch.channels_last)
     y = torch.cat([b[1] for b in batches])
     losses, masters1 = [], None

@@ -100,7 +100,10 @@ def _count_epilogue(monkeypatch):
 def test_bn_relu_conv_chain_matches_fp32(k, monkeypatch):
     """x -> BN -> ReLU -> conv (own kernels, bf16) vs fp32 nn.BatchNorm2d + ReLU + conv."""
     from apex_example_amd.ops import BatchNorm2dReLU
+    from apex_example_amd.ops import conv as convmod
     from apex_example_amd.ops.conv import Conv2d1x1, Conv2d3x3
+
+    monkeypatch.setattr(convmod, "_BNBWD_MAX_M", 1 << 30)   # fuse at every size here
 
     calls = _count_epilogue(monkeypatch)
     torch.manual_seed(0)
@@ -162,6 +165,9 @@ def test_bottleneck_layer_grads_match_unfused(monkeypatch):
     x0 = _bf(torch.randn(4, 128, 28, 28, device=dev))
     r = torch.randn(4, 256, 28, 28, device=dev)
     grads = {}
+    from apex_example_amd.ops import conv as convmod
+
+    monkeypatch.setattr(convmod, "_BNBWD_MAX_M", 1 << 30)   # fuse at every size here
     for fused in (False, True):
         monkeypatch.setattr(bnmod, "_BWD_EPI", fused)
         calls = _count_epilogue(monkeypatch)

@@ -153,16 +153,25 @@ def test_two_ranks_match_concatenated_batch(tmp_path, opt_level):
     on another the 4th loss, 0.099, differed by 9e-4 - the fp32 convolutions are
     MIOpen's, whose algorithm choice varies by box - hence 2e-3 relative + 1e-3
     absolute).
-    In bf16 (O2) the two runs round differently and this tiny memorisation task
-    amplifies that (measured 0.2 % at step 1, 2.6 % at step 2, tens of % by step
-    4), so only the first two losses are pinned."""
+    In bf16 (O2) the two runs round differently, and at 32x32 images the deepest BNs
+    normalise over 8-16 values per channel: their gradients are so ill-conditioned that
+    two single-process runs differing only in BN-statistics summation order already
+    disagree by ~20 % (relative L2) in the first update and by up to 8 % in the step-2
+    loss (tools/diag/ddp_stats_diff.py).  O2 therefore runs on 64x64 images (4x the BN
+    population per channel), where the step-2 losses of DDP + SyncBN and of the
+    concatenated-batch reference agree to 0.4-0.8 % (same tool, DDP_DIFF_HW=64): pinned
+    at 0.5 % (step 1) and 2 % (step 2)."""
     steps = 4 if opt_level == "O0" else 2
+    hw = 32 if opt_level == "O0" else 64
     res = W.run("gpu_ddp_resnet", 2, str(tmp_path), syncbn=True, lr=0.01,
-                opt_level=opt_level, steps=steps)
-    ref = W.gpu_resnet_reference(world=2, lr=0.01, opt_level=opt_level, steps=steps)
+                opt_level=opt_level, steps=steps, hw=hw)
+    ref = W.gpu_resnet_reference(world=2, lr=0.01, opt_level=opt_level, steps=steps, hw=hw)
     # the rank losses are per-half means; the global loss is their average
     ddp_loss = [(a + b) / 2 for a, b in zip(res[0]["losses"], res[1]["losses"])]
-    tol, atol = (2e-3, 1e-3) if opt_level == "O0" else (5e-2, 0.0)
+    if opt_level != "O0":
+        assert abs(ddp_loss[0] - ref["losses"][0]) <= 5e-3 * abs(ref["losses"][0]), (
+            ddp_loss, ref["losses"])
+    tol, atol = (2e-3, 1e-3) if opt_level == "O0" else (2e-2, 0.0)
     for a, b in zip(ddp_loss, ref["losses"]):
         assert abs(a - b) <= tol * abs(b) + atol, (ddp_loss, ref["losses"])
     if opt_level != "O0":

@@ -1034,3 +1034,47 @@ def test_conv1x1_own_kernel_matches_gemm(shape, monkeypatch):
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(outs[0][2], outs[1][2], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("pdt", [torch.float32, torch.bfloat16])
+def test_legacy_lamb_stages_native_match_cpu(pdt):
+    """amp_C.multi_tensor_lamb_stage{1,2}_cuda on the GPU run the native kernels
+    (mt_optim.hip lamb_legacy1/2_kernel); they must match the CPU composition of the
+    Apex formulas, honour the noop flag and leave no host sync (device norms)."""
+    from apex_example_amd import amp_C
+
+    torch.manual_seed(0)
+    shapes = [(7,), (3, 5), (1000, 33)]
+    mk = lambda f: [f(s) for s in shapes]  # noqa: E731
+    g = mk(lambda s: torch.randn(s))
+    p = mk(lambda s: torch.randn(s).to(pdt).float())
+    m = mk(lambda s: (torch.randn(s) * 0.1).to(pdt).float())
+    v = mk(lambda s: (torch.rand(s) * 0.1).to(pdt).float())
+    decay = [0.01, 0.0, 0.02]
+    b1, b2, eps, step, gn, mx, lr = 0.9, 0.999, 1e-6, 3, 4.0, 1.0, 0.1
+    cpu = [[t.clone() for t in lst] for lst in (g, p, m, v)] + [[torch.zeros(s) for s in shapes]]
+    gpu = [[t.to(dev) for t in g]] + [[t.to(dev, pdt) for t in lst] for lst in (p, m, v)] + \
+        [[torch.zeros(s, device=dev, dtype=pdt) for s in shapes]]
+    noop_c = torch.zeros(1, dtype=torch.int32)
+    noop_g = torch.zeros(1, dtype=torch.int32, device=dev)
+    before = [t.clone() for lst in gpu for t in lst]
+    amp_C.multi_tensor_lamb_stage1_cuda(0, noop_g + 1, gpu, decay, step, b1, b2, eps,
+                                        torch.tensor([gn], device=dev), mx)
+    for a, b in zip(before, [t for lst in gpu for t in lst]):
+        assert torch.equal(a, b)
+    amp_C.multi_tensor_lamb_stage1_cuda(0, noop_c, cpu, decay, step, b1, b2, eps,
+                                        torch.tensor([gn]), mx)
+    amp_C.multi_tensor_lamb_stage1_cuda(0, noop_g, gpu, decay, step, b1, b2, eps,
+                                        torch.tensor([gn], device=dev), mx)
+    tol = dict(rtol=1e-5, atol=1e-6) if pdt == torch.float32 else dict(rtol=1e-2, atol=1e-3)
+    for lc, lg in zip(cpu[2:], gpu[2:]):
+        for a, b in zip(lc, lg):
+            torch.testing.assert_close(b.float().cpu(), a.to(pdt).float(), **tol)
+    pn_c = [t.norm() for t in cpu[1]]
+    un_c = [t.norm() for t in cpu[4]]
+    pn_g = torch.stack([t.float().norm() for t in gpu[1]])
+    un_g = torch.stack([t.float().norm() for t in gpu[4]])
+    amp_C.multi_tensor_lamb_stage2_cuda(0, noop_c, [cpu[1], cpu[4]], pn_c, un_c, lr, 0.01)
+    amp_C.multi_tensor_lamb_stage2_cuda(0, noop_g, [gpu[1], gpu[4]], pn_g, un_g, lr, 0.01)
+    for a, b in zip(cpu[1], gpu[1]):
+        torch.testing.assert_close(b.float().cpu(), a.to(pdt).float(), **tol)

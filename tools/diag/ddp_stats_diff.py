@@ -5,7 +5,7 @@ batch (gpu_resnet_reference)?  Runs each with APEX_AMD_CONV_BN_STATS=1 / 0 in ch
 processes and prints the worst per-parameter update difference after step 1 between
 every pair (tests/test_ddp_gpu.py::test_two_ranks_match_concatenated_batch[O2]).
 
-    python tools/diag/ddp_stats_diff.py
+    python tools/diag/ddp_stats_diff.py          # DDP_DIFF_HW=64: 64x64 images
 """
 import os
 import subprocess
@@ -17,6 +17,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
+HW = int(os.environ.get("DDP_DIFF_HW", "32"))
+
+
 def child(kind, out):
     import torch
 
@@ -24,11 +27,11 @@ def child(kind, out):
 
     if kind == "ddp":
         res = W.run("gpu_ddp_resnet", 2, tempfile.mkdtemp(), syncbn=True, lr=0.01,
-                    opt_level="O2", steps=2)
+                    opt_level="O2", steps=2, hw=HW)
         r = {"masters1": res[0]["masters1"], "losses": [(a + b) / 2 for a, b in
                                                        zip(res[0]["losses"], res[1]["losses"])]}
     else:
-        ref = W.gpu_resnet_reference(world=2, lr=0.01, opt_level="O2", steps=2)
+        ref = W.gpu_resnet_reference(world=2, lr=0.01, opt_level="O2", steps=2, hw=HW)
         r = {"masters1": ref["masters1"], "losses": ref["losses"], "p0": ref["params0"]}
     torch.save(r, out)
 
