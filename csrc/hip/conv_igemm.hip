@@ -49,6 +49,16 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not wait for
+// outstanding global loads / stores (vmcnt), so prefetches and output stores stay in
+// flight; the empty asm statements keep the compiler from moving memory operations
+// across it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // bijective blockIdx -> tile remap keeping consecutive tiles on one XCD
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
@@ -147,7 +157,7 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
     const int64_t opix = out_pix<MODE>(g, m < g.M ? m : 0, z);
     const int64_t off = opix * NC + c0;
     P.av[q] = addp ? *reinterpret_cast<const uint4*>(addp + off) : make_uint4(0, 0, 0, 0);
-    P.xv[q] = *reinterpret_cast<const uint4*>(xp + off);
+    P.xv[q] = (ep.diag & 1) ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(xp + off);
     P.mk[q] = ep.relu_mode == 1 ? ep.rmask[opix * (NC >> 3) + (c0 >> 3)] : 0xffu;
   }
 #pragma unroll
@@ -162,16 +172,18 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
   }
 }
 
-template <int MODE, int BM, int BN>
-__device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict__ y,
-                                            const ConvGeom& g, const ConvBnEpi& ep, int m0,
-                                            int n0, int z, const BnPre<BM, BN>& P,
-                                            float (&s1)[8], float (&s2)[8]) {
+// one specialisation per (ReLU-mask mode, residual add): the per-element mode tests are
+// compile-time, so the unrolled store loop is straight-line code (runtime tests there
+// made the compiler branch around every element: +30-60 us per ResNet-50 layer)
+template <int MODE, int BM, int BN, int RM, bool ADD>
+__device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restrict__ y,
+                                              const ConvGeom& g, int m0, int n0, int z,
+                                              const BnPre<BM, BN>& P, float (&s1)[8],
+                                              float (&s2)[8]) {
   using PT = BnPre<BM, BN>;
   const int tid = threadIdx.x;
   const int cc = tid % PT::CPR, rg = tid / PT::CPR;
   const int c0 = n0 + cc * 8;
-  const bool add = ep.add != nullptr;
 #pragma unroll
   for (int q = 0; q < PT::ROWS; ++q) {
     const int row = q * PT::RGS + rg;
@@ -187,7 +199,7 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
       float o[2], xx[2];
       o[0] = __uint_as_float(tw[k] << 16);
       o[1] = __uint_as_float(tw[k] & 0xffff0000u);
-      if (add) {  // the residual gradient (rounded once more, as a separate add would)
+      if constexpr (ADD) {  // the residual gradient (rounded once more, as a separate add would)
         o[0] += __uint_as_float(aw[k] << 16);
         o[1] += __uint_as_float(aw[k] & 0xffff0000u);
       }
@@ -198,8 +210,8 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
       for (int h = 0; h < 2; ++h) {
         const int i = 2 * k + h;
         bool keep = true;
-        if (ep.relu_mode == 1) keep = (P.mk[q] >> i) & 1u;
-        else if (ep.relu_mode == 2) keep = fmaf(xx[h], P.sc[i], P.sh[i]) > 0.f;
+        if constexpr (RM == 1) keep = (P.mk[q] >> i) & 1u;
+        else if constexpr (RM == 2) keep = fmaf(xx[h], P.sc[i], P.sh[i]) > 0.f;
         const bf16_t gb = (bf16_t)(keep ? o[h] : 0.f);
         const float gv = (float)gb;
         s1[i] += gv;
@@ -210,6 +222,22 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
     }
     *reinterpret_cast<uint4*>(y + out_pix<MODE>(g, m, z) * g.NC + c0) =
         make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+}
+
+template <int MODE, int BM, int BN>
+__device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict__ y,
+                                            const ConvGeom& g, const ConvBnEpi& ep, int m0,
+                                            int n0, int z, const BnPre<BM, BN>& P,
+                                            float (&s1)[8], float (&s2)[8]) {
+  const bool add = ep.add != nullptr;
+  switch (ep.relu_mode * 2 + (add ? 1 : 0)) {
+    case 0: bnbwd_store_t<MODE, BM, BN, 0, false>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 1: bnbwd_store_t<MODE, BM, BN, 0, true>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 2: bnbwd_store_t<MODE, BM, BN, 1, false>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 3: bnbwd_store_t<MODE, BM, BN, 1, true>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 4: bnbwd_store_t<MODE, BM, BN, 2, false>(T, y, g, m0, n0, z, P, s1, s2); break;
+    default: bnbwd_store_t<MODE, BM, BN, 2, true>(T, y, g, m0, n0, z, P, s1, s2); break;
   }
 }
 
@@ -323,11 +351,12 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   for (int i = 0; i < 8; ++i)
     shv[i] = (EPI == 0 && want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
 
-  // BN-backward epilogue operands: issued before the first tile so they arrive during
-  // the K loop (oldest in the vmcnt queue, so the counted waits below only ever wait
-  // for them early, never skip them); a __syncthreads() fences them anyway
+  // BN-backward epilogue operands (EPI == 1): issued after the K loop - issued earlier
+  // they would sit at the head of the in-order vmcnt queue and every counted wait of the
+  // loop would stall on them (measured: no gain from a prefetch at kernel start) - and
+  // consumed after barriers that wait for LDS only, so they fly under the accumulator ->
+  // LDS tile write instead of being waited for at a __syncthreads()
   BnPre<BM, BN> pre;
-  if constexpr (EPI == 1) bnbwd_prefetch<MODE, BM, BN>(g, ep, m0, n0, z, pre);
 
   // prologue: NB-1 tiles in flight
 #pragma unroll
@@ -372,7 +401,14 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
     }
   }
 #undef CONV_ISSUE
-  __syncthreads();
+  // (the K loop ended on a vmcnt(0) wait: no tile DMA is in flight; an LDS-only barrier
+  // leaves the epilogue prefetch of EPI == 1 outstanding)
+  if constexpr (EPI == 1) {
+    bnbwd_prefetch<MODE, BM, BN>(g, ep, m0, n0, z, pre);
+    lds_barrier();
+  } else {
+    __syncthreads();
+  }
 
   // epilogue: accumulators -> bf16 tile in LDS -> coalesced 16-byte row stores
   bf16_t* T = reinterpret_cast<bf16_t*>(lds);
@@ -386,7 +422,11 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
         const int col = wn * TN + j * 16 + fr;
         T[row * BN + col] = (bf16_t)acc[i][j][e];
       }
-  __syncthreads();
+  if constexpr (EPI == 1) {
+    lds_barrier();
+  } else {
+    __syncthreads();
+  }
   constexpr bool dense = MODE == kFwd3 || MODE == kFwd1;
   // BatchNorm statistics of this output tile for the BN that consumes y (its stats
   // pass over y disappears): a thread's 16-byte chunks all lie in ONE 8-channel
@@ -428,7 +468,9 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   }
   if (want_stats) {
     constexpr int RGS = kCT / CPR;  // row groups (threads sharing a column group)
-    __syncthreads();                // every thread is done reading the bf16 tile
+    // every thread is done reading the bf16 tile (an LDS-only barrier: the output
+    // stores just issued need not complete before the statistics exchange)
+    lds_barrier();
     float* red = reinterpret_cast<float*>(lds);
     const int rg = tid / CPR;
 #pragma unroll
@@ -436,7 +478,7 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
       red[rg * BN + scc * 8 + i] = s1[i];
       red[RGS * BN + rg * BN + scc * 8 + i] = s2[i];
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < BN) {
       float a = 0.f, b = 0.f;
 #pragma unroll 4
@@ -472,6 +514,13 @@ static int conv1x1_nb1_max_kt() {
   return e ? std::atoi(e) : 1;
 }
 
+// APEX_AMD_BNBWD_NB2 = 0 | 1 (read per launch, A/B runs): 64-wide BN-backward epilogue
+// tiles on the 2-deep ring
+static bool bnbwd_nb2() {
+  const char* e = std::getenv("APEX_AMD_BNBWD_NB2");
+  return e ? e[0] == '1' : true;
+}
+
 template <int MODE, int EPI = 0>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
@@ -494,6 +543,11 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  } else if (EPI == 1 && bnbwd_nb2()) {
+    // BN-backward epilogue on 64-wide tiles: a 2-deep ring (48 KB of LDS -> 3 workgroups
+    // per CU instead of 2), so more K loops run under each workgroup's epilogue reads
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);

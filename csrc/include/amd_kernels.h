@@ -288,6 +288,7 @@ struct ConvBnEpi {
   const float* w;        // [C] or null (relu_mode 2)
   const float* b;        // [C] or null (relu_mode 2)
   int relu_mode;
+  int diag;              // timing experiments only: bit 0 = do not read x (sums are wrong)
 };
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* g, int N, int H, int W, int Cin,
                          int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,
