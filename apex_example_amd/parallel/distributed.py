@@ -150,6 +150,16 @@ class DistributedDataParallel(Module):
     high-priority streams; default on), ``force_collectives`` (issue the bucket
     all-reduces even at world size 1 - test hook for 1-GPU boxes),
     ``allreduce_always_fp32=None`` (auto: fp32 accumulation for bf16 buckets).
+
+    ``retain_allreduce_buffers``: in Apex it keeps the flat all-reduced buffers alive
+    after the backward (they are otherwise freed once unflattened into ``.grad``) and
+    exposes them as ``allreduce_buffers``.  Here every parameter's ``.grad`` is a view
+    into its persistent flat bucket, so the buffers are always retained and
+    ``allreduce_buffers`` always returns them; the flag is accepted for API parity and
+    changes nothing (``tests/test_parallel_gloo.py`` checks the buffers alias the grads).
+    ``prof=True``: roctx ranges around the forward and, in the C++ reducer, around each
+    bucket's launch and the post-backward finalize (Apex ranges its hook and
+    ``comm_ready_buckets``).
     """
 
     def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,

@@ -115,6 +115,27 @@ def ddp_auto_size(rank, world):
     return out
 
 
+def ddp_retain_buffers(rank, world):
+    """retain_allreduce_buffers=True (Apex): the all-reduced flat buffers stay
+    accessible as ``allreduce_buffers`` after backward - here every .grad is a view
+    into them."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    model = _mlp()
+    ddp = DistributedDataParallel(model, message_size=700, retain_allreduce_buffers=True)
+    x, y = _data(8 * world)
+    xs, ys = x.chunk(world)[rank], y.chunk(world)[rank]
+    F.cross_entropy(ddp(xs), ys).backward()
+    bufs = ddp.allreduce_buffers
+    spans = [(b.data_ptr(), b.data_ptr() + b.numel() * b.element_size()) for b in bufs]
+    inside = [any(lo <= p.grad.data_ptr() < hi for lo, hi in spans) for p in model.parameters()]
+    total = sum(b.numel() for b in bufs)
+    return {"n_bufs": len(bufs), "inside": inside, "total": total,
+            "n_params": sum(p.numel() for p in model.parameters()),
+            "buf_sum": float(sum(b.double().sum() for b in bufs)),
+            "grad_sum": float(sum(p.grad.double().sum() for p in model.parameters()))}
+
+
 def ddp_bf16_precision(rank, world, fp32=None, n=4096):
     """bf16 gradient buckets averaged over ``world`` ranks; returns the reduced
     bf16 gradient and the exact fp32 average of the per-rank bf16 gradients."""

@@ -228,15 +228,23 @@ def test_syncbn_gpu_two_ranks_matches_global_batch(tmp_path):
     dy = torch.randn(sum(sizes), C, 6, 6, generator=g)
     (y * dy).sum().backward()
     ys = torch.cat([r["y"] for r in res])
-    torch.testing.assert_close(ys, y.detach(), rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(torch.cat([r["dx"] for r in res]), x.grad, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(torch.cat([r["dz"] for r in res]), z.grad, rtol=3e-2, atol=3e-2)
-    # dgamma / dbeta are per-rank partial sums (DDP all-reduces them as gradients)
-    torch.testing.assert_close(res[0]["dw"] + res[1]["dw"], bn.weight.grad, rtol=3e-2, atol=5e-2)
-    torch.testing.assert_close(res[0]["db"] + res[1]["db"], bn.bias.grad, rtol=3e-2, atol=5e-2)
+
+    def rel(a, b):  # max error relative to the tensor's scale
+        return float((a - b).abs().max() / b.abs().max())
+    # bf16 outputs (y, dx, dz; 2^-8 relative rounding): two ulps at the tensor's scale.
+    # The inputs of the fp32 reference are the same bf16-rounded values, so only the
+    # output rounding and the summation order differ.
+    assert rel(ys, y.detach()) < 8e-3
+    # (dx also carries dy's rounding to bf16 - the gradient of a bf16 output - through k1)
+    assert rel(torch.cat([r["dx"] for r in res]), x.grad) < 1.2e-2
+    assert rel(torch.cat([r["dz"] for r in res]), z.grad) < 8e-3
+    # dgamma / dbeta are per-rank partial sums (DDP all-reduces them as gradients); fp32
+    # sums of bf16-rounded dy
+    assert rel(res[0]["dw"] + res[1]["dw"], bn.weight.grad) < 4e-3
+    assert rel(res[0]["db"] + res[1]["db"], bn.bias.grad) < 4e-3
     for r in res:
-        torch.testing.assert_close(r["rm"], bn.running_mean, rtol=1e-2, atol=1e-2)
-        torch.testing.assert_close(r["rv"], bn.running_var, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(r["rm"], bn.running_mean, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(r["rv"], bn.running_var, rtol=1e-4, atol=1e-5)
         assert r["nbt"] == 1
 
 

@@ -62,6 +62,14 @@ def test_ddp_auto_message_size(tmp_path):
                    "fp32": mib32 // 4}
 
 
+def test_ddp_retain_allreduce_buffers(tmp_path):
+    """The all-reduced buffers are retained and the grads are views into them."""
+    for r in W.run("ddp_retain_buffers", 2, str(tmp_path)):
+        assert r["n_bufs"] > 1 and all(r["inside"])
+        assert r["total"] >= r["n_params"]
+        assert abs(r["buf_sum"] - r["grad_sum"]) <= 1e-6 * max(1.0, abs(r["grad_sum"]))
+
+
 def test_ddp_sum_without_average(tmp_path):
     res = W.run("ddp_grads", 2, str(tmp_path), average=False)
     ref = _single_process_grads()
