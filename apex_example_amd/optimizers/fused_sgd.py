@@ -67,6 +67,25 @@ class FusedSGD(FusedOptimizerBase):
                 momentums.append(param_state["momentum_buffer"])
         return momentums, first_run
 
+    def _step_pair(self, sets, wd, momentum, lr, nesterov):
+        """amp O2's two launch sets of a group (16-bit-copy set + fp32 set) in ONE
+        native launch (StepPlan.sgd_pair), once both carry plans and their momentum
+        buffers exist.  False: launch them one by one."""
+        if len(sets) != 2:
+            return False
+        a, b = sets.values()
+        if a["copies"] is None:
+            a, b = b, a
+        pa, pb = a.get("_plan"), b.get("_plan")
+        if (pa is None or pb is None or a["copies"] is None or b["copies"] is not None
+                or "_moms" not in a or "_moms" not in b):
+            return False
+        dev = a["params"][0].device
+        sa, ta, ia = self._plan_scale(a["scaled"])
+        sb, tb, ib = self._plan_scale(b["scaled"])
+        return pa.sgd_pair(pb, self._noop(dev), wd, momentum, 0.0, lr, nesterov,
+                           self.wd_after_momentum, sa, ta, ia, sb, tb, ib)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -81,6 +100,8 @@ class FusedSGD(FusedOptimizerBase):
             nesterov = group["nesterov"]
             lr = group["lr"]
             sets = self._launch_sets(gid, group)
+            if dampening == 0 and self._step_pair(sets, weight_decay, momentum, lr, nesterov):
+                continue
             planned = True
             for key, s in sets.items():
                 params = s["params"]

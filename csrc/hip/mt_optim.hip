@@ -34,50 +34,102 @@ __device__ __forceinline__ float lr_of(const float* p, float v) { return p ? *p 
 
 // --------------------------------------------------------------------------
 // SGD
+struct SgdConsts {
+  float sc, lr;
+  bool first, has_mom, load_m;
+};
+__device__ __forceinline__ SgdConsts sgd_consts(const SgdArgs& a) {
+  SgdConsts k;
+  k.sc = get_scale(a.scale);
+  k.lr = lr_of(a.lr_ptr, a.lr);
+  k.first = a.first_run_flag ? (*a.first_run_flag == 0) : (a.first_run != 0);
+  k.has_mom = a.momentum != 0.f;
+  k.load_m = k.has_mom && !k.first;
+  return k;
+}
+
+template <typename TG, typename TP, typename TM, typename TC, int DEPTH>
+__device__ __forceinline__ void sgd_chunk(const MTLaunch& L, int ch, const SgdArgs& a,
+                                          const SgdConsts& k) {
+  const TileCtx c = tile_ctx(L, ch);
+  const bool al = c.t->aligned;
+  float g[kMTUnroll][8], p[kMTUnroll][8], m[kMTUnroll][8];
+#pragma unroll
+  for (int u = 0; u < kMTUnroll; ++u) {
+    const int off = lane_off(u), cnt = c.n - off;
+    if (cnt <= 0) continue;
+    const bool vec = al && cnt >= 8;
+    const int64_t idx = c.start + off;
+    ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
+    ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+    if (k.load_m) ld<TM>(c.t->ptr[2], idx, cnt, vec, m[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < kMTUnroll; ++u) {
+    const int off = lane_off(u), cnt = c.n - off;
+    if (cnt <= 0) continue;
+    const bool vec = al && cnt >= 8;
+    const int64_t idx = c.start + off;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float gi = g[u][i] * k.sc;
+      if (a.wd != 0.f && !a.wd_after_momentum) gi = fmaf(a.wd, p[u][i], gi);
+      if (k.has_mom) {
+        m[u][i] = k.first ? gi : fmaf(m[u][i], a.momentum, (1.f - a.dampening) * gi);
+        gi = a.nesterov ? fmaf(a.momentum, m[u][i], gi) : m[u][i];
+      }
+      if (a.wd != 0.f && a.wd_after_momentum) gi = fmaf(a.wd, p[u][i], gi);
+      p[u][i] = fmaf(-k.lr, gi, p[u][i]);
+    }
+    st<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
+    if (k.has_mom) st<TM>(c.t->ptr[2], idx, cnt, vec, m[u]);
+    if (DEPTH == 4) st<TC>(c.t->ptr[3], idx, cnt, vec, p[u]);
+  }
+}
+
 template <typename TG, typename TP, typename TM, typename TC, int DEPTH>
 __global__ void __launch_bounds__(kMTThreads) sgd_kernel(MTLaunch L, SgdArgs a, const int* noop) {
   if (skip_step(noop)) return;
-  const float sc = get_scale(a.scale);
-  const float lr = lr_of(a.lr_ptr, a.lr);
-  const bool first = a.first_run_flag ? (*a.first_run_flag == 0) : (a.first_run != 0);
-  const bool has_mom = a.momentum != 0.f;
-  const bool load_m = has_mom && !first;
-  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x) {
-    const TileCtx c = tile_ctx(L, ch);
-    const bool al = c.t->aligned;
-    float g[kMTUnroll][8], p[kMTUnroll][8], m[kMTUnroll][8];
-#pragma unroll
-    for (int u = 0; u < kMTUnroll; ++u) {
-      const int off = lane_off(u), cnt = c.n - off;
-      if (cnt <= 0) continue;
-      const bool vec = al && cnt >= 8;
-      const int64_t idx = c.start + off;
-      ld<TG>(c.t->ptr[0], idx, cnt, vec, g[u]);
-      ld<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
-      if (load_m) ld<TM>(c.t->ptr[2], idx, cnt, vec, m[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < kMTUnroll; ++u) {
-      const int off = lane_off(u), cnt = c.n - off;
-      if (cnt <= 0) continue;
-      const bool vec = al && cnt >= 8;
-      const int64_t idx = c.start + off;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float gi = g[u][i] * sc;
-        if (a.wd != 0.f && !a.wd_after_momentum) gi = fmaf(a.wd, p[u][i], gi);
-        if (has_mom) {
-          m[u][i] = first ? gi : fmaf(m[u][i], a.momentum, (1.f - a.dampening) * gi);
-          gi = a.nesterov ? fmaf(a.momentum, m[u][i], gi) : m[u][i];
-        }
-        if (a.wd != 0.f && a.wd_after_momentum) gi = fmaf(a.wd, p[u][i], gi);
-        p[u][i] = fmaf(-lr, gi, p[u][i]);
-      }
-      st<TP>(c.t->ptr[1], idx, cnt, vec, p[u]);
-      if (has_mom) st<TM>(c.t->ptr[2], idx, cnt, vec, m[u]);
-      if (DEPTH == 4) st<TC>(c.t->ptr[3], idx, cnt, vec, p[u]);
-    }
+  const SgdConsts k = sgd_consts(a);
+  for (int ch = blockIdx.x; ch < L.nchunks; ch += gridDim.x)
+    sgd_chunk<TG, TP, TM, TC, DEPTH>(L, ch, a, k);
+}
+
+// Two launch sets of one param group in ONE launch (FusedSGD's amp O2 step: the
+// 16-bit-copy set [g16, p32, m32, c16] and the fp32 BatchNorm set [g32, p32, m32]):
+// chunk ids below A.nchunks belong to set A - a block-uniform branch - so the small
+// second set costs no launch of its own.
+template <typename TGA, typename TCA>
+__global__ void __launch_bounds__(kMTThreads)
+    sgd_pair_kernel(MTLaunch A, SgdArgs aa, MTLaunch B, SgdArgs ab, const int* noop) {
+  if (skip_step(noop)) return;
+  const SgdConsts ka = sgd_consts(aa), kb = sgd_consts(ab);
+  const int n = A.nchunks + B.nchunks;
+  for (int ch = blockIdx.x; ch < n; ch += gridDim.x) {
+    if (ch < A.nchunks) sgd_chunk<TGA, float, float, TCA, 4>(A, ch, aa, ka);
+    else sgd_chunk<float, float, float, float, 3>(B, ch - A.nchunks, ab, kb);
   }
+}
+
+bool mt_sgd_pair(const MTLaunch& A, DType ga, DType pa, DType ca, const SgdArgs& aa,
+                 const MTLaunch& B, DType gb, DType pb, const SgdArgs& ab, const int* noop,
+                 hipStream_t st) {
+  if (pa != DType::F32 || pb != DType::F32 || gb != DType::F32 || ca == DType::F32 ||
+      ga == DType::F64 || ca == DType::F64)
+    return false;
+  MTLaunch both = A;
+  both.nchunks = A.nchunks + B.nchunks;
+  const dim3 grid = mt_pgrid(both);
+  dispatch1(ga, [&](auto tg) {
+    dispatch1(ca, [&](auto tc) {
+      using TG = decltype(tg);
+      using TC = decltype(tc);
+      if constexpr (!std::is_same<TC, float>::value)
+        hipLaunchKernelGGL((sgd_pair_kernel<TG, TC>), grid, dim3(kMTThreads), 0, st, A, aa, B, ab,
+                           noop);
+    });
+  });
+  return true;
 }
 
 void mt_sgd(const MTLaunch& L, int depth, DType g, DType p, DType m, DType copy, const SgdArgs& a,

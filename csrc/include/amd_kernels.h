@@ -51,6 +51,11 @@ struct SgdArgs {
 // depth 3: [g, p, m]; depth 4: [g, p, m, p_copy]
 void mt_sgd(const MTLaunch& L, int depth, DType g, DType p, DType m, DType copy,
             const SgdArgs& a, const int* noop, hipStream_t st);
+// two SGD launch sets in one launch: A = [g, p32, m32, copy16] (depth 4), B = [g32, p32, m32]
+// (depth 3); false (nothing launched) for other dtype combinations
+bool mt_sgd_pair(const MTLaunch& A, DType ga, DType pa, DType ca, const SgdArgs& aa,
+                 const MTLaunch& B, DType gb, DType pb, const SgdArgs& ab, const int* noop,
+                 hipStream_t st);
 // after an SGD step: first_run_flag = 1 unless the step was skipped (noop set)
 void mark_step_done(int* flag, const int* noop, hipStream_t st);
 

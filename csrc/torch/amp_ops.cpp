@@ -521,6 +521,35 @@ bool StepPlan::sgd(at::Tensor noop, double wd, double momentum, double dampening
   return true;
 }
 
+bool StepPlan::sgd_pair(StepPlan& o, at::Tensor noop, double wd, double momentum,
+                        double dampening, double lr, bool nesterov, bool wd_after_momentum,
+                        double scale, OptT scale_t, bool scale_inv, double other_scale,
+                        OptT other_scale_t, bool other_scale_inv) {
+  c10::NoGradGuard no_grad_;
+  if (lists_.size() != 4 || o.lists_.size() != 3) return false;
+  if (!refresh() || !o.refresh()) return false;
+  if (!gpu_launch_ready() || !o.gpu_launch_ready()) return false;
+  auto args = [&](double sv, const OptT& st, bool inv) {
+    SgdArgs a;
+    a.wd = (float)wd;
+    a.momentum = (float)momentum;
+    a.dampening = (float)dampening;
+    a.lr = (float)lr;
+    a.nesterov = nesterov;
+    a.first_run = false;
+    a.wd_after_momentum = wd_after_momentum;
+    a.scale = make_scale(sv, st, inv);
+    a.lr_ptr = nullptr;
+    a.first_run_flag = nullptr;
+    return a;
+  };
+  return mt_sgd_pair(plan_.L, dtype_of(lists_[0][0]), dtype_of(lists_[1][0]),
+                     dtype_of(lists_[3][0]), args(scale, scale_t, scale_inv), o.plan_.L,
+                     dtype_of(o.lists_[0][0]), dtype_of(o.lists_[1][0]),
+                     args(other_scale, other_scale_t, other_scale_inv), noop_ptr(noop),
+                     cur_stream());
+}
+
 bool StepPlan::adam(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
                     int64_t step, OptT step_t, int64_t mode, bool bias_correction, double wd,
                     double scale, OptT scale_t, bool scale_inv, bool advance) {

@@ -68,6 +68,12 @@ class StepPlan {
   bool sgd(at::Tensor noop, double wd, double momentum, double dampening, double lr,
            bool nesterov, bool first_run, OptT first_run_flag, bool wd_after_momentum,
            double scale, OptT scale_t, bool scale_inv);
+  // this set and `other` (an fp32 set, e.g. the BatchNorm parameters) in ONE launch
+  // (mt_sgd_pair); false when either set cannot (dtypes, CPU, a moved-away grad) - the
+  // caller then launches the sets one by one
+  bool sgd_pair(StepPlan& other, at::Tensor noop, double wd, double momentum, double dampening,
+                double lr, bool nesterov, bool wd_after_momentum, double scale, OptT scale_t,
+                bool scale_inv, double other_scale, OptT other_scale_t, bool other_scale_inv);
   bool adam(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
             int64_t step, OptT step_t, int64_t mode, bool bias_correction, double wd,
             double scale, OptT scale_t, bool scale_inv, bool advance_step);

@@ -74,6 +74,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("refresh", &StepPlan::refresh)
       .def("set_absent", &StepPlan::set_absent)
       .def("sgd", &StepPlan::sgd)
+      .def("sgd_pair", &StepPlan::sgd_pair)
       .def("adam", &StepPlan::adam)
       .def("size", &StepPlan::size)
       .def("rebuilds", &StepPlan::rebuilds);

@@ -258,3 +258,49 @@ def test_folded_unscale_matches_materialized_across_growth(opt_level, sync_free)
     assert sa == sb and sa[-1] > sa[0], (sa, sb)
     for x, y in zip(a, b):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_sgd_native_plan_and_pair_launch_match_python_path(monkeypatch):
+    """FusedSGD's steady-state native path (StepPlan per launch set, and the amp O2
+    16-bit-copy + fp32 BatchNorm sets in ONE launch, mt_sgd_pair) is bitwise the
+    per-step Python launch path."""
+    from apex_example_amd import amp
+    from apex_example_amd.models import resnet18
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.optimizers import _base
+    from apex_example_amd.optimizers import fused_sgd as fs
+
+    x = torch.randn(8, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    out, pairs = {}, {"n": 0}
+    orig_pair = fs.FusedSGD._step_pair
+
+    def counting(self, *a):
+        r = orig_pair(self, *a)
+        pairs["n"] += int(bool(r))
+        return r
+    monkeypatch.setattr(fs.FusedSGD, "_step_pair", counting)
+    for plan in (False, True):
+        monkeypatch.setattr(_base, "_STEP_PLAN", plan)
+        torch.manual_seed(0)
+        m = resnet18(num_classes=10, fused_bn=True, gemm_1x1=True).cuda().to(
+            memory_format=torch.channels_last)
+        opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4,
+                       materialize_master_grads=False)
+        m, opt = amp.initialize(m, opt, opt_level="O2", half_dtype=torch.bfloat16, verbosity=0)
+        n0 = pairs["n"]
+        for _ in range(4):
+            loss = torch.nn.functional.cross_entropy(m(x).float(), y)
+            opt.zero_grad()
+            with amp.scale_loss(loss, opt) as s:
+                s.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        out[plan] = [p.detach().clone() for p in amp.master_params(opt)] + \
+            [p.detach().clone() for p in m.parameters()]
+        if plan:
+            assert pairs["n"] - n0 >= 2   # steps 3 and 4 (plans exist from step 2's end)
+        else:
+            assert pairs["n"] == n0
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)
