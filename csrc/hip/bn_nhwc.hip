@@ -381,11 +381,14 @@ __global__ void __launch_bounds__(kBNThreads)
 // ---------------------------------------------------------------- statistics from a
 // producer's epilogue (conv_igemm.hip conv_tap_k with a stats slab): the conv wrote
 // the shifted sums of each M-tile tile-major, slab[S][0|1][C] (one coalesced row per
-// workgroup).  Long slabs are first folded 128 rows at a time (a column per thread,
+// workgroup).  Long slabs are first folded kFoldRows rows at a time (a column per thread,
 // coalesced rows); the final kernel sums the remaining rows per channel in a fixed
 // order and produces what stats_finalize does: mean (+ biased var | invstd),
 // running-stat update, num_batches_tracked += 1.
-constexpr int kFoldRows = 128;
+// 32 rows per fold workgroup: a 6,272-tile slab (56x56 layers at bs 256) folds in ~200
+// workgroups of 8 four-load chains instead of 49 of 32 chains (~15 -> ~5 us per fold,
+// `profiles/resnet50_o2_serial_r3.md`; the finalize then sums <= 200 rows per channel)
+constexpr int kFoldRows = 32;
 
 __global__ void __launch_bounds__(kBNThreads)
     slab_fold_k(const float* __restrict__ slab, int S, int C2, float* __restrict__ out) {
@@ -473,7 +476,7 @@ void bn_stats_from_slab(const float* slab, int S, int64_t C, int64_t count, cons
                         const BNStatsOut& out, float* ws, hipStream_t st) {
   const float* rows = slab;
   int R = S;
-  if (S > 2 * kFoldRows) {  // fold 128 rows at a time first
+  if (S > 2 * kFoldRows) {  // fold kFoldRows rows at a time first
     R = (S + kFoldRows - 1) / kFoldRows;
     const int C2 = (int)(2 * C);
     hipLaunchKernelGGL(slab_fold_k, dim3((unsigned)((C2 + kBNThreads - 1) / kBNThreads),

@@ -1043,6 +1043,7 @@ def test_legacy_lamb_stages_native_match_cpu(pdt):
     Apex formulas, honour the noop flag and leave no host sync (device norms)."""
     from apex_example_amd import amp_C
 
+    dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     shapes = [(7,), (3, 5), (1000, 33)]
     mk = lambda f: [f(s) for s in shapes]  # noqa: E731
