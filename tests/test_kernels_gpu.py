@@ -1077,5 +1077,9 @@ def test_legacy_lamb_stages_native_match_cpu(pdt):
     un_g = torch.stack([t.float().norm() for t in gpu[4]])
     amp_C.multi_tensor_lamb_stage2_cuda(0, noop_c, [cpu[1], cpu[4]], pn_c, un_c, lr, 0.01)
     amp_C.multi_tensor_lamb_stage2_cuda(0, noop_g, [gpu[1], gpu[4]], pn_g, un_g, lr, 0.01)
+    # p - ratio * u with ratio from norms reduced in a different order (CPU vs device):
+    # a few ulps of the update (fp32), or one bf16 ulp at |p| ~ 1 where the rounded
+    # result sits on a rounding boundary (measured: 3 of 33,000 elements)
+    tol2 = dict(rtol=1e-4, atol=2e-5) if pdt == torch.float32 else dict(rtol=1e-2, atol=8e-3)
     for a, b in zip(cpu[1], gpu[1]):
-        torch.testing.assert_close(b.float().cpu(), a.to(pdt).float(), **tol)
+        torch.testing.assert_close(b.float().cpu(), a.to(pdt).float(), **tol2)
