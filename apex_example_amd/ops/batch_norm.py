@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from . import _ddp_direct
 
 # BN backward folded into the consuming conv's data-gradient epilogue (BnBwdSrc below);
 # APEX_AMD_CONV_BN_BWD=0 keeps the separate reduction pass
@@ -106,6 +107,7 @@ class BatchNormFunction(torch.autograd.Function):
                 fuse_relu, shape_channel_last, num_batches_tracked=None, force_collectives=False,
                 slab=None, slab_shift=None):
         C = _C()
+        ctx.params = (weight, bias)   # the Parameter objects (DDP bucket slots live on them)
         orig_shape = x.shape
         xl = _to_logical(x, shape_channel_last)
         zl = _to_logical(z, shape_channel_last) if z is not None else None
@@ -227,8 +229,15 @@ class BatchNormFunction(torch.autograd.Function):
             # g) and summed (g, g*(x-mean)) per tile: no reduction pass, no dz store
             FUSED_BWD_CALLS[0] += 1
             if ctx.world > 1:
+                direct = _ddp_direct.slots(*ctx.params) if need_w else None
+                tw, tb = (ctx.params[0].grad, ctx.params[1].grad) if direct else (None, None)
                 sum_dy, sum_dy_xmu, gw, gb = C.slab_reduce_grad(res[1], invstd, weight, need_w,
-                                                               sum_scale=ctx.total)
+                                                               sum_scale=ctx.total,
+                                                               grad_weight=tw, grad_bias=tb)
+                if direct:
+                    # dgamma / dbeta accumulated into the DDP bucket views by the finalize
+                    _ddp_direct.mark_ready(direct)
+                    need_w = False
                 n = sum_dy.numel()
                 dist.all_reduce(sum_dy.as_strided((2 * n,), (1,)), group=ctx.pg)
                 total = 1.0
@@ -244,9 +253,15 @@ class BatchNormFunction(torch.autograd.Function):
             # SyncBN: the reduce writes (sum_dy | sum_dy_xmu) / global_count into one [2C]
             # buffer (the scale is a device scalar from the forward's combine) -> ONE
             # in-place all_reduce yields the global means -> elementwise pass
+            direct = _ddp_direct.slots(*ctx.params) if need_w else None
+            tw, tb = (ctx.params[0].grad, ctx.params[1].grad) if direct else (None, None)
             sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
                                                        ctx.fuse_relu, need_w, mask=mask,
-                                                       sum_scale=ctx.total)
+                                                       sum_scale=ctx.total, grad_weight=tw,
+                                                       grad_bias=tb)
+            if direct:
+                _ddp_direct.mark_ready(direct)
+                need_w = False
             n = sum_dy.numel()
             packed = sum_dy.as_strided((2 * n,), (1,))  # sum_dy_xmu follows sum_dy in memory
             dist.all_reduce(packed, group=ctx.pg)

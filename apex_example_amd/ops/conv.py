@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from . import _ddp_direct
 from .batch_norm import bn_src_of
 
 # Weight gradients on a side stream (APEX_AMD_WGRAD_STREAM=0 disables): the data
@@ -126,7 +127,7 @@ class _SideWgrad:
                 # None so nothing reads them on the compute stream before the join
                 with torch.no_grad():
                     for p, g in zip(self.params, outs):
-                        if g is not None:
+                        if g is not None and g is not p.grad:  # (not already accumulated)
                             p.grad.add_(g)
         for t in used:
             t.record_stream(self.side)
@@ -156,6 +157,23 @@ class _SideWgrad:
         return dw
 
 
+def _side_out(side, weight, cl=False):
+    """The bucket view a DDP-mode side-stream weight gradient accumulates into directly
+    (same kernels and rounding as the main-stream direct path), else None."""
+    if side is None or not side.on or side.mode != "ddp" or weight.grad is None:
+        return None
+    g = weight.grad
+    ok = g.is_contiguous(memory_format=torch.channels_last) if cl else g.is_contiguous()
+    return g if ok else None
+
+
+def _wgrad_1x1_w(dy, x, weight, out=None):
+    """1x1 weight gradient shaped like the weight, or accumulated into ``out`` (returned
+    as the very same tensor, so a DDP-mode side stream knows not to add it again)."""
+    r = wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=out)
+    return r if out is not None else r.view(weight.shape)
+
+
 def _split_k(m):
     s = 1
     while s < 128 and m % (2 * s) == 0 and m // (2 * s) >= 2048:
@@ -163,20 +181,29 @@ def _split_k(m):
     return s
 
 
-def wgrad_1x1(dy_rows, x_rows, out_dtype):
-    """dW[co, ci] = dy_rows^T @ x_rows, split-K over the rows (fp32 partials)."""
+def wgrad_1x1(dy_rows, x_rows, out_dtype, out=None):
+    """dW[co, ci] = dy_rows^T @ x_rows, split-K over the rows (fp32 partials).  ``out``:
+    accumulate into that [co, ci]-contiguous gradient (a DDP bucket view) instead."""
     m, co = dy_rows.shape
     ci = x_rows.shape[1]
     S = _split_k(m)
     if S == 1:
-        return torch.mm(dy_rows.t(), x_rows, out_dtype=torch.float32).to(out_dtype)
-    a = dy_rows.view(S, m // S, co).transpose(1, 2)
-    b = x_rows.view(S, m // S, ci)
-    part = torch.bmm(a, b, out_dtype=torch.float32)
-    if _USE_SPLITK_REDUCE and out_dtype in (torch.bfloat16, torch.float32) and (co * ci) % 4 == 0:
-        # one two-stage slab reduction writing the weight dtype directly
-        return _native.require().conv.splitk_reduce(part, out_dtype)
-    return part.sum(0).to(out_dtype)
+        r = torch.mm(dy_rows.t(), x_rows, out_dtype=torch.float32).to(out_dtype)
+    else:
+        a = dy_rows.view(S, m // S, co).transpose(1, 2)
+        b = x_rows.view(S, m // S, ci)
+        part = torch.bmm(a, b, out_dtype=torch.float32)
+        if (_USE_SPLITK_REDUCE and out_dtype in (torch.bfloat16, torch.float32)
+                and (co * ci) % 4 == 0):
+            # one two-stage slab reduction writing the weight dtype directly
+            r = _native.require().conv.splitk_reduce(
+                part, out_dtype, out.view(co, ci) if out is not None else None)
+            return out if out is not None else r
+        r = part.sum(0).to(out_dtype)
+    if out is not None:
+        out.view(co, ci).add_(r)
+        return out
+    return r
 
 
 # Stride-1 1x1 convs on the own MFMA implicit-GEMM kernel (conv_tap_k, kFwd1) where
@@ -353,8 +380,14 @@ class Conv1x1GemmFunction(torch.autograd.Function):
                 dx = _conv1x1_dgrad(dy, weight, x.shape)
         ctx.src = None
         if ctx.needs_input_grad[1]:
-            dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
-                          .view(weight.shape), dy, x)
+            direct = None if side.on else _ddp_direct.slots(weight)
+            if direct is not None and weight.grad.is_contiguous():
+                # accumulate straight into the DDP bucket view, no autograd add kernel
+                wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=weight.grad)
+                _ddp_direct.mark_ready(direct)
+            else:
+                so = _side_out(side, weight)
+                dw = side.run(lambda: _wgrad_1x1_w(dy, x, weight, so), dy, x)
         return dx, dw, None, None
 
 
@@ -405,8 +438,13 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                     dx2 = torch.mm(_as_rows(dy), w2)
                 dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and dy is not None:
-            dw = side.run(lambda: wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype)
-                          .view(weight.shape), dy, x)
+            direct = None if side.on else _ddp_direct.slots(weight)
+            if direct is not None and weight.grad.is_contiguous():
+                wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=weight.grad)
+                _ddp_direct.mark_ready(direct)
+            else:
+                so = _side_out(side, weight)
+                dw = side.run(lambda: _wgrad_1x1_w(dy, x, weight, so), dy, x)
         return dx, dw, None, None
 
 
@@ -435,7 +473,14 @@ class Conv1x1Stride2Function(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = cv.conv_dgrad_s2(dy, _transpose_1x1(weight), x.size(2), x.size(3))
         if ctx.needs_input_grad[1]:
-            dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1), dy, x)
+            direct = None if side.on else _ddp_direct.slots(weight)
+            if direct is not None and weight.grad.is_contiguous(
+                    memory_format=torch.channels_last):
+                cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1, out=weight.grad)
+                _ddp_direct.mark_ready(direct)
+            else:
+                so = _side_out(side, weight, cl=True)
+                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1, out=so), dy, x)
         return dx, dw, None
 
 
@@ -566,11 +611,24 @@ class Conv3x3Function(torch.autograd.Function):
                 dx = cv.conv_fwd(dy, _rot_weight(weight), 1)
             else:
                 dx = cv.conv_dgrad_s2(dy, _rot_weight(weight), x.size(2), x.size(3))
-        if ctx.needs_input_grad[1]:
+        direct = None
+        if ctx.needs_input_grad[1] and own_wgrad and not side.on:
+            direct = _ddp_direct.slots(weight)
+            if direct is not None and not weight.grad.is_contiguous(
+                    memory_format=torch.channels_last):
+                direct = None
+        if direct is not None:
+            # accumulate straight into the DDP bucket view, no autograd add kernel
+            cv.conv_wgrad(dy, x, weight.dtype, 0 if _WGRAD3 == "tap" else 1,
+                          stride if _WGRAD3 == "tap" else 1, out=weight.grad)
+            _ddp_direct.mark_ready(direct)
+        elif ctx.needs_input_grad[1]:
+            so = _side_out(side, weight, cl=True)
             if _WGRAD3 == "tap" and n_pix < (1 << 22):
-                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, stride), dy, x)
+                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, stride, out=so),
+                              dy, x)
             elif _WGRAD3 == "nine" and stride == 1 and x.size(3) <= 56 and n_pix < (1 << 22):
-                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 1, 1), dy, x)
+                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 1, 1, out=so), dy, x)
             else:
                 dw = torch.ops.aten.convolution_backward(
                     dy, x, weight, None, (stride, stride), (1, 1), (1, 1), False, (0, 0), 1,

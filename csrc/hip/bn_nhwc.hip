@@ -41,6 +41,12 @@ NGeom ngeom(int64_t C, bool vec) {
 
 }  // namespace
 
+namespace {
+thread_local bool g_bn_grad_accumulate = false;
+}
+bool bn_grad_accumulate() { return g_bn_grad_accumulate; }
+void bn_set_grad_accumulate(bool on) { g_bn_grad_accumulate = on; }
+
 BNTuning& bn_tuning() {
   static BNTuning t;
   return t;

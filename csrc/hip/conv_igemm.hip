@@ -959,7 +959,7 @@ __global__ void __launch_bounds__(256)
 template <typename TO>
 __global__ void __launch_bounds__(256)
     wgrad_reduce2_k(const float* __restrict__ stage, int Gn, int Cout, int Cin, TO* __restrict__ dw,
-                    int taps) {
+                    int taps, int accum) {
   const int64_t total = (int64_t)taps * Cout * Cin;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
@@ -969,7 +969,8 @@ __global__ void __launch_bounds__(256)
   const int tap = (int)(r / Cout);
   float sum = 0.f;
   for (int g = 0; g < Gn; ++g) sum += stage[(int64_t)g * total + e];
-  dw[((int64_t)co * taps + tap) * Cin + ci] = from_f32<TO>(sum);
+  TO* o = dw + ((int64_t)co * taps + tap) * Cin + ci;
+  *o = from_f32<TO>(accum ? to_f32(*o) + sum : sum);
 }
 
 // Single-pass form for <= kRedGroup splits: sum the S slabs of 4 consecutive ci and
@@ -977,7 +978,7 @@ __global__ void __launch_bounds__(256)
 template <typename TO>
 __global__ void __launch_bounds__(256)
     wgrad_reduce_one_k(const float4* __restrict__ part, int S, int64_t total4, int Cout, int Cin,
-                       int taps, TO* __restrict__ dw) {
+                       int taps, TO* __restrict__ dw, int accum) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total4) return;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
@@ -997,10 +998,13 @@ __global__ void __launch_bounds__(256)
   const int co = (int)(r % Cout);
   const int tap = (int)(r / Cout);
   TO* o = dw + ((int64_t)co * taps + tap) * Cin + ci;
-  o[0] = from_f32<TO>(a.x + b.x);
-  o[1] = from_f32<TO>(a.y + b.y);
-  o[2] = from_f32<TO>(a.z + b.z);
-  o[3] = from_f32<TO>(a.w + b.w);
+  float v[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+  if (accum) {  // accumulate into an existing gradient (a DDP bucket view): one rounding
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += to_f32(o[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = from_f32<TO>(v[i]);
 }
 
 // W'[ci][T-1-t][co] = W[co][t][ci]: the 180-degree-rotated, in/out-swapped 3x3
@@ -1133,7 +1137,7 @@ int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize) {
 
 void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32, int N,
                      int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
-                     hipStream_t st) {
+                     hipStream_t st, bool accum) {
   const auto* dyp = static_cast<const bf16_t*>(dy);
   const auto* xp = static_cast<const bf16_t*>(x);
   const int T = ksize * ksize;
@@ -1179,11 +1183,11 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
     if (dw_fp32)
       hipLaunchKernelGGL((wgrad_reduce_one_k<float>), dim3(blocks), dim3(256), 0, st,
                          reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, T,
-                         static_cast<float*>(dw));
+                         static_cast<float*>(dw), accum ? 1 : 0);
     else
       hipLaunchKernelGGL((wgrad_reduce_one_k<bf16_t>), dim3(blocks), dim3(256), 0, st,
                          reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, T,
-                         static_cast<bf16_t*>(dw));
+                         static_cast<bf16_t*>(dw), accum ? 1 : 0);
     return;
   }
   float* stage = part + (int64_t)S * nout;
@@ -1193,10 +1197,10 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
   const unsigned blocks = (unsigned)((nout + 255) / 256);
   if (dw_fp32)
     hipLaunchKernelGGL((wgrad_reduce2_k<float>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<float*>(dw), T);
+                       Cin, static_cast<float*>(dw), T, accum ? 1 : 0);
   else
     hipLaunchKernelGGL((wgrad_reduce2_k<bf16_t>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<bf16_t*>(dw), T);
+                       Cin, static_cast<bf16_t*>(dw), T, accum ? 1 : 0);
 }
 
 int64_t splitk_reduce_workspace(int S, int64_t n) {
@@ -1204,7 +1208,7 @@ int64_t splitk_reduce_workspace(int S, int64_t n) {
 }
 
 void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, void* out,
-                   bool out_fp32, hipStream_t st) {
+                   bool out_fp32, hipStream_t st, bool accum) {
   const int64_t n = (int64_t)Cout * Cin;
   const int Gn = (S + kRedGroup - 1) / kRedGroup;
   if (Gn == 1 && Cin % 4 == 0 && single_pass_reduce()) {
@@ -1213,11 +1217,11 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
     if (out_fp32)
       hipLaunchKernelGGL((wgrad_reduce_one_k<float>), dim3(blocks), dim3(256), 0, st,
                          reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, 1,
-                         static_cast<float*>(out));
+                         static_cast<float*>(out), accum ? 1 : 0);
     else
       hipLaunchKernelGGL((wgrad_reduce_one_k<bf16_t>), dim3(blocks), dim3(256), 0, st,
                          reinterpret_cast<const float4*>(part), S, n4, Cout, Cin, 1,
-                         static_cast<bf16_t*>(out));
+                         static_cast<bf16_t*>(out), accum ? 1 : 0);
     return;
   }
   const int64_t n4 = n / 4;
@@ -1226,10 +1230,10 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
   const unsigned blocks = (unsigned)((n + 255) / 256);
   if (out_fp32)
     hipLaunchKernelGGL((wgrad_reduce2_k<float>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<float*>(out), 1);
+                       Cin, static_cast<float*>(out), 1, accum ? 1 : 0);
   else
     hipLaunchKernelGGL((wgrad_reduce2_k<bf16_t>), dim3(blocks), dim3(256), 0, st, stage, Gn, Cout,
-                       Cin, static_cast<bf16_t*>(out), 1);
+                       Cin, static_cast<bf16_t*>(out), 1, accum ? 1 : 0);
 }
 
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st) {

@@ -309,6 +309,16 @@ void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, co
                           float* packed, float* ws, hipStream_t st);
 // BN backward sums (sum_dy, sum_dy_xmu [* sum_scale], dgamma, dbeta) from a
 // conv_nhwc_fwd_bnbwd slab; ws: bn_slab_workspace(S, C) floats
+// Host-side switch read when the BN backward finalize is launched (this thread): dgamma /
+// dbeta ACCUMULATE into the caller's gradient buffers - DDP bucket views - instead of
+// being written fresh, saving autograd's two add kernels per BatchNorm (BNAccumScope)
+bool bn_grad_accumulate();
+void bn_set_grad_accumulate(bool on);
+struct BNAccumScope {
+  bool prev;
+  explicit BNAccumScope(bool on) : prev(bn_grad_accumulate()) { bn_set_grad_accumulate(on); }
+  ~BNAccumScope() { bn_set_grad_accumulate(prev); }
+};
 void bn_slab_reduce_grad(const float* slab, int S, int64_t C, const float* invstd,
                          float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, DType tw,
                          float* ws, hipStream_t st, const float* sum_scale = nullptr);
@@ -324,7 +334,7 @@ int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize);  // floats
 // generic split-K slab reduction: out[co][ci] = sum_s part[s][co][ci] (n % 4 == 0)
 int64_t splitk_reduce_workspace(int S, int64_t n);
 void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, void* out,
-                   bool out_fp32, hipStream_t st);
+                   bool out_fp32, hipStream_t st, bool accum = false);
 // 16-bit W'[ci][2-r][2-s][co] = W[co][r][s][ci] (data-gradient filter)
 void conv3x3_rot_weight(const void* w, void* out, int Cout, int Cin, hipStream_t st);
 // W^T ([Cin][Cout]) of a 16-bit 1x1 filter [Cout][Cin] (LDS-tiled transpose)
@@ -335,7 +345,7 @@ void prep_weights(const void* const* w, void* const* out, const int* cout, const
                   const int* taps, int n, hipStream_t st);
 void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool dw_fp32, int N,
                      int H, int W, int Cin, int Cout, int ksize, int stride, int S, int algo,
-                     hipStream_t st);
+                     hipStream_t st, bool accum = false);
 
 // ---- ResNet stem: 7x7 / stride 2 / pad 3, 3 -> 64 channels, NHWC bf16 (stem_conv.hip) ----
 bool stem_conv_supported(int N, int H, int W);

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(kBNThreads)
     reduce_finalize(const float* __restrict__ slab, int splits, int C,
                     const float* __restrict__ invstd, float* __restrict__ sum_dy,
                     float* __restrict__ sum_dy_xmu, TW* __restrict__ gw, TW* __restrict__ gb,
-                    const float* __restrict__ sum_scale) {
+                    const float* __restrict__ sum_scale, int accum) {
   __shared__ float sums[2 * CH];
   const int c0 = blockIdx.x * CH;
   slab_sum<CH>(slab, splits, C, c0, sums);
@@ -140,8 +140,9 @@ __global__ void __launch_bounds__(kBNThreads)
     const float sc = sum_scale ? *sum_scale : 1.f;
     sum_dy[c] = s1 * sc;
     sum_dy_xmu[c] = s2 * sc;
-    if (gw) gw[c] = from_f32<TW>(s2 * invstd[c]);
-    if (gb) gb[c] = from_f32<TW>(s1);
+    // accum: add into existing gradients (DDP bucket views) instead of overwriting
+    if (gw) gw[c] = from_f32<TW>(s2 * invstd[c] + (accum ? to_f32(gw[c]) : 0.f));
+    if (gb) gb[c] = from_f32<TW>(s1 + (accum ? to_f32(gb[c]) : 0.f));
   }
 }
 
@@ -179,7 +180,7 @@ static inline void launch_reduce_finalize(const float* slab, int splits, int64_t
     constexpr int CH = decltype(ch)::value;
     hipLaunchKernelGGL((reduce_finalize<TW, CH>), dim3((unsigned)((C + CH - 1) / CH)),
                        dim3(kBNThreads), 0, st, slab, splits, (int)C, invstd, sum_dy, sum_dy_xmu,
-                       gw, gb, sum_scale);
+                       gw, gb, sum_scale, bn_grad_accumulate() ? 1 : 0);
   });
 }
 

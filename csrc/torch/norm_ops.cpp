@@ -495,9 +495,32 @@ std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mea
   return bn_apply_impl(x, mean, invstd, weight, bias, z, relu, true);
 }
 
+namespace {
+// dgamma / dbeta destinations: fresh tensors, or caller-given gradients to ACCUMULATE into
+// (DDP bucket views; the finalize adds instead of writing - BNAccumScope)
+bool grad_targets(const OptT& weight, bool need, const OptT& gw_in, const OptT& gb_in,
+                  at::Tensor& gw, at::Tensor& gb) {
+  if (!need || !has(weight)) return false;
+  if (has(gw_in) && has(gb_in)) {
+    TORCH_CHECK(gw_in->is_cuda() && gb_in->is_cuda() && gw_in->is_contiguous() &&
+                    gb_in->is_contiguous() && gw_in->numel() == weight->numel() &&
+                    gb_in->numel() == weight->numel() &&
+                    gw_in->scalar_type() == weight->scalar_type() &&
+                    gb_in->scalar_type() == weight->scalar_type(),
+                "batch norm: grad_weight / grad_bias targets must match the weight");
+    gw = *gw_in;
+    gb = *gb_in;
+    return true;
+  }
+  gw = at::empty_like(*weight);
+  gb = at::empty_like(*weight);
+  return false;
+}
+}  // namespace
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-    OptT z, bool relu, bool need_wgrad, OptT mask, OptT sum_scale) {
+    OptT z, bool relu, bool need_wgrad, OptT mask, OptT sum_scale, OptT gw_in, OptT gb_in) {
   BNView v = bn_view(x);
   TORCH_CHECK(!has(mask) || x.is_cuda(), "batch norm: ReLU mask is a GPU-path feature");
   if (!x.is_cuda()) {
@@ -514,6 +537,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     if (need_wgrad && has(weight)) {
       gw = (sum_dy_xmu * invstd).to(weight->scalar_type());
       gb = sum_dy.to(weight->scalar_type());
+      if (has(gw_in) && has(gb_in)) {
+        gw_in->add_(gw);
+        gb_in->add_(gb);
+        gw = *gw_in;
+        gb = *gb_in;
+      }
     }
     if (has(sum_scale)) {
       sum_dy = sum_dy * *sum_scale;
@@ -529,10 +558,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
   at::Tensor sum_dy = at::empty({v.C}, fopt), sum_dy_xmu = at::empty({v.C}, fopt);
   at::Tensor gw, gb;
   DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
-  if (need_wgrad && has(weight)) {
-    gw = at::empty_like(*weight);
-    gb = at::empty_like(*weight);
-  }
+  const bool accum = grad_targets(weight, need_wgrad, gw_in, gb_in, gw, gb);
+  BNAccumScope accum_scope(accum);
   at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
   at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
   at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
@@ -673,7 +700,8 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_op(
-    at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale) {
+    at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale,
+    OptT gw_in, OptT gb_in) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
@@ -687,10 +715,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_o
   at::Tensor sum_dy = packed.narrow(0, 0, C), sum_dy_xmu = packed.narrow(0, C, C);
   at::Tensor gw, gb;
   DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
-  if (need_wgrad && has(weight)) {
-    gw = at::empty_like(*weight);
-    gb = at::empty_like(*weight);
-  }
+  const bool accum = grad_targets(weight, need_wgrad, gw_in, gb_in, gw, gb);
+  BNAccumScope accum_scope(accum);
   const float* scale = nullptr;
   if (has(sum_scale)) {
     TORCH_CHECK(sum_scale->is_cuda() && sum_scale->scalar_type() == at::kFloat &&

@@ -216,7 +216,7 @@ at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_
 }
 
 at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
-                              int64_t stride, int64_t ksize) {
+                              int64_t stride, int64_t ksize, c10::optional<at::Tensor> out) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16,
@@ -238,11 +238,22 @@ at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dt
                                   (int)stride, (int)algo);
   at::Tensor part = at::empty({conv_wgrad_workspace(S, (int)Cin, (int)Cout, (int)ksize)},
                               x.options().dtype(at::kFloat));
-  at::Tensor dw = at::empty({Cout, Cin, ksize, ksize},
-                            x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  // out: accumulate into an existing gradient (a DDP bucket view) instead of a new tensor
+  const bool accum = out.has_value() && out->defined();
+  at::Tensor dw;
+  if (accum) {
+    dw = *out;
+    TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == out_dtype && dw.dim() == 4 &&
+                    dw.size(0) == Cout && dw.size(1) == Cin && dw.size(2) == ksize &&
+                    dw.size(3) == ksize && dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_wgrad: out must be a channels-last [Cout, Cin, k, k] tensor of out_dtype");
+  } else {
+    dw = at::empty({Cout, Cin, ksize, ksize},
+                   x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  }
   conv_nhwc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(),
                   out_dtype == at::kFloat, (int)N, (int)H, (int)W, (int)Cin, (int)Cout, (int)ksize,
-                  (int)stride, S, (int)algo, cur_stream());
+                  (int)stride, S, (int)algo, cur_stream(), accum);
   return dw;
 }
 
@@ -293,17 +304,28 @@ at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy) {
   return out;
 }
 
-at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype) {
+at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype,
+                            c10::optional<at::Tensor> out_acc) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&
                   part.is_contiguous(), "splitk_reduce: contiguous fp32 [S, M, N] expected");
   const int64_t S = part.size(0), M = part.size(1), N = part.size(2);
   TORCH_CHECK((M * N) % 4 == 0, "splitk_reduce: M*N must be a multiple of 4");
   at::Tensor stage = at::empty({splitk_reduce_workspace((int)S, M * N)}, part.options());
-  at::Tensor out = at::empty({M, N}, part.options().dtype(out_dtype));
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "splitk_reduce: out dtype");
+  // out_acc: accumulate into an existing [M, N]-contiguous tensor (a DDP bucket view)
+  const bool accum = out_acc.has_value() && out_acc->defined();
+  at::Tensor out;
+  if (accum) {
+    out = *out_acc;
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == out_dtype && out.numel() == M * N &&
+                    out.is_contiguous(),
+                "splitk_reduce: accumulation target must be a contiguous tensor of M*N elements");
+  } else {
+    out = at::empty({M, N}, part.options().dtype(out_dtype));
+  }
   splitk_reduce(part.data_ptr<float>(), (int)S, (int)M, (int)N, stage.data_ptr<float>(),
-                out.data_ptr(), out_dtype == at::kFloat, cur_stream());
+                out.data_ptr(), out_dtype == at::kFloat, cur_stream(), accum);
   return out;
 }
 

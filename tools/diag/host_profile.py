@@ -21,6 +21,11 @@ def main():
     args = bench.parse()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if args.force_collectives:  # a 1-rank RCCL group, as bench.py makes for this mode
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     build = {"resnet50": bench.build_resnet, "bert_large": bench.build_bert,
              "gpt2_medium": bench.build_gpt2, "convnet": bench.build_convnet}[args.model]
     opt_only = os.environ.get("HOST_PROFILE_OPT_ONLY") == "1"
