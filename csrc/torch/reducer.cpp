@@ -151,8 +151,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   // A gradient already accumulated into its bucket view by work on `stream`
   // (side-stream weight gradients): ready once that stream reaches this point.
+  // announced by the caller (a side stream, or a kernel that accumulated straight into
+  // the bucket view on the compute stream - which may be the null stream, handle 0)
   void mark_ready_on_stream(int64_t i, int64_t stream) {
-    mark_ready_impl(i, reinterpret_cast<hipStream_t>(stream));
+    mark_ready_impl(i, reinterpret_cast<hipStream_t>(stream), true);
   }
 
   // Side-stream gradients can be announced (iteration >= 2 of an overlapped,
@@ -160,9 +162,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   // into the bucket view itself and calls mark_ready_on_stream.
   bool async_ready_ok() const { return enabled_ && !refresh_ && !delay_ && comm_active(); }
 
-  void mark_ready_impl(int64_t i, hipStream_t side) {
+  void mark_ready_impl(int64_t i, hipStream_t side, bool announced = false) {
     std::lock_guard<std::mutex> g(mu_);
-    if (side) {
+    if (announced) {
       async_marked_[(size_t)i] = 1;
     } else if (async_marked_[(size_t)i]) {
       // the AccumulateGrad post-hook of a gradient that was announced from the side
@@ -171,7 +173,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       return;
     }
     attach_view(i);
-    if (side && enabled_ && !refresh_ && !delay_ && comm_active()) {
+    if (announced && enabled_ && !refresh_ && !delay_ && comm_active()) {
       hipEvent_t e = take_event();
       TORCH_CHECK(hipEventRecord(e, side) == hipSuccess, "hipEventRecord failed");
       buckets_[(size_t)bucket_of_[(size_t)i]].waits.push_back(e);
