@@ -41,7 +41,7 @@ def slots(*params):
 
 
 def mark_ready(sl):
-    """Announce the parameters of ``slots()`` as ready on the current stream."""
-    sid = torch.cuda.current_stream().cuda_stream
+    """Announce the parameters of ``slots()`` as ready (accumulated on the compute
+    stream, which every bucket launch waits for anyway: no per-parameter event)."""
     for red, i in sl:
-        red.mark_ready_on_stream(i, sid)
+        red.mark_ready_direct(i)

@@ -70,6 +70,14 @@ def _bwd_src(x, xl, mean, invstd, weight, bias, mask, fuse_relu, has_z):
     return BnBwdSrc(x, mean, invstd, weight, bias, mask, mode)
 
 
+def _allreduce(t, pg):
+    """In-place SUM all-reduce: one C++ c10d call for RCCL (no Python wrapper cost)."""
+    if dist.get_backend(pg) == "nccl":
+        _native.require().reducer.syncbn_allreduce(t, pg)
+    else:
+        dist.all_reduce(t, group=pg)
+
+
 def bn_src_of(x):
     """The BnBwdSrc of ``x`` when x is a fused BN's output (else None)."""
     return getattr(x, "_amd_bn_src", None)
@@ -156,14 +164,19 @@ class BatchNormFunction(torch.autograd.Function):
             pg = process_group if process_group is not None else dist.group.WORLD
             packed = (C.slab_packed_stats(slab, count, slab_shift) if slab is not None
                       else C.local_stats_packed(xl))
-            gathered = torch.empty(world * packed.numel(), dtype=packed.dtype, device=x.device)
             if dist.get_backend(pg) == "nccl":
-                dist.all_gather_into_tensor(gathered, packed, group=pg)
+                # all_gather + combine in one C++ call (csrc/torch/reducer.cpp): the Python
+                # c10d wrapper cost ~20 us of host time per layer
+                mean_g, invstd, inv_total = _native.require().reducer.syncbn_allgather_combine(
+                    packed, pg, float(eps), float(momentum), running_mean, running_var,
+                    num_batches_tracked)
             else:  # gloo with GPU tensors (tests): list form into views of `gathered`
+                gathered = torch.empty(world * packed.numel(), dtype=packed.dtype,
+                                       device=x.device)
                 dist.all_gather(list(gathered.chunk(world)), packed, group=pg)
-            mean_g, invstd, inv_total = C.combine_stats_sync(
-                gathered.view(world, -1), float(eps), float(momentum), running_mean, running_var,
-                num_batches_tracked)
+                mean_g, invstd, inv_total = C.combine_stats_sync(
+                    gathered.view(world, -1), float(eps), float(momentum), running_mean,
+                    running_var, num_batches_tracked)
             if want_mask:
                 y, mask = C.apply_mask(xl, mean_g, invstd, weight, bias, zl, bool(fuse_relu))
             else:
@@ -239,7 +252,7 @@ class BatchNormFunction(torch.autograd.Function):
                     _ddp_direct.mark_ready(direct)
                     need_w = False
                 n = sum_dy.numel()
-                dist.all_reduce(sum_dy.as_strided((2 * n,), (1,)), group=ctx.pg)
+                _allreduce(sum_dy.as_strided((2 * n,), (1,)), ctx.pg)
                 total = 1.0
             else:
                 sum_dy, sum_dy_xmu, gw, gb = C.slab_reduce_grad(res[1], invstd, weight, need_w)
@@ -264,7 +277,7 @@ class BatchNormFunction(torch.autograd.Function):
                 need_w = False
             n = sum_dy.numel()
             packed = sum_dy.as_strided((2 * n,), (1,))  # sum_dy_xmu follows sum_dy in memory
-            dist.all_reduce(packed, group=ctx.pg)
+            _allreduce(packed, ctx.pg)
             dx, dz = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
                                       1.0, zl, ctx.fuse_relu, ctx.has_z, mask=mask)
             if ctx.shape_channel_last:

@@ -53,6 +53,7 @@
 #include <string>
 
 #include "reducer.h"
+#include "norm_ops.h"
 
 extern "C" int roctxRangePushA(const char* message);  // libroctx64 (what torch.cuda.nvtx uses)
 extern "C" int roctxRangePop();
@@ -156,13 +157,18 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void mark_ready_on_stream(int64_t i, int64_t stream) {
     mark_ready_impl(i, reinterpret_cast<hipStream_t>(stream), true);
   }
+  // announced from the compute stream itself (the gradient was accumulated into the
+  // bucket view by a kernel on it): no event - the bucket launch already waits for the
+  // compute stream
+  void mark_ready_direct(int64_t i) { mark_ready_impl(i, nullptr, true, false); }
 
   // Side-stream gradients can be announced (iteration >= 2 of an overlapped,
   // enabled reducer whose collectives run): the caller then writes the gradient
   // into the bucket view itself and calls mark_ready_on_stream.
   bool async_ready_ok() const { return enabled_ && !refresh_ && !delay_ && comm_active(); }
 
-  void mark_ready_impl(int64_t i, hipStream_t side, bool announced = false) {
+  void mark_ready_impl(int64_t i, hipStream_t side, bool announced = false,
+                       bool with_event = true) {
     std::lock_guard<std::mutex> g(mu_);
     if (announced) {
       async_marked_[(size_t)i] = 1;
@@ -173,7 +179,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       return;
     }
     attach_view(i);
-    if (announced && enabled_ && !refresh_ && !delay_ && comm_active()) {
+    if (announced && with_event && enabled_ && !refresh_ && !delay_ && comm_active()) {
       hipEvent_t e = take_event();
       TORCH_CHECK(hipEventRecord(e, side) == hipSuccess, "hipEventRecord failed");
       buckets_[(size_t)bucket_of_[(size_t)i]].waits.push_back(e);
@@ -594,8 +600,34 @@ std::shared_ptr<Reducer> make_reducer(std::vector<at::Tensor> params,
 
 }  // namespace
 
+// ---- SyncBatchNorm collectives from C++ (ops/batch_norm.py's RCCL path): one call per
+// BN layer instead of the Python c10d wrappers (~20 us of host time each, 2 per layer
+// per step: ResNet-50 went host-bound at world 1 with forced collectives).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> syncbn_allgather_combine(
+    at::Tensor packed, c10::intrusive_ptr<c10d::ProcessGroup> pg, double eps, double momentum,
+    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+    c10::optional<at::Tensor> nbt) {
+  c10::NoGradGuard ng;
+  TORCH_CHECK(packed.is_cuda() && packed.is_contiguous(), "syncbn: packed stats on the GPU");
+  const int world = pg->getSize();
+  at::Tensor gathered = at::empty({world * packed.numel()}, packed.options());
+  pg->_allgather_base(gathered, packed)->wait();  // stream-ordered for RCCL (no host block)
+  return bn_combine_stats_sync_op(gathered.view({world, -1}), eps, momentum, running_mean,
+                                  running_var, nbt);
+}
+
+void syncbn_allreduce(at::Tensor t, c10::intrusive_ptr<c10d::ProcessGroup> pg) {
+  c10::NoGradGuard ng;
+  std::vector<at::Tensor> ts{t};
+  pg->allreduce(ts)->wait();
+}
+
 void register_reducer(pybind11::module_& m) {
   namespace py = pybind11;
+  m.def("syncbn_allgather_combine", &syncbn_allgather_combine, py::arg("packed"), py::arg("pg"),
+        py::arg("eps"), py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"),
+        py::arg("nbt") = py::none());
+  m.def("syncbn_allreduce", &syncbn_allreduce, py::arg("t"), py::arg("pg"));
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init(&make_reducer), py::arg("params"), py::arg("process_group"),
            py::arg("message_size") = 10000000, py::arg("allreduce_fp32_mode") = 0,
@@ -611,6 +643,7 @@ void register_reducer(pybind11::module_& m) {
       .def("mark_ready_on_stream", &Reducer::mark_ready_on_stream, py::arg("index"),
            py::arg("stream"))
       .def("async_ready_ok", &Reducer::async_ready_ok)
+      .def("mark_ready_direct", &Reducer::mark_ready_direct)
       .def("force_collectives", &Reducer::force_collectives)
       .def("collectives_active", &Reducer::collectives_active)
       .def("set_timing", &Reducer::set_timing)
