@@ -70,10 +70,41 @@ def _bwd_src(x, xl, mean, invstd, weight, bias, mask, fuse_relu, has_z):
     return BnBwdSrc(x, mean, invstd, weight, bias, mask, mode)
 
 
+# SyncBN collectives on the compute stream through the dedicated SyncBN group's RCCL
+# communicator (csrc/torch/reducer.cpp syncbn_*_raw); APEX_AMD_SYNCBN_RAW_RCCL=0 keeps the
+# process group's own stream (c10d calls from C++)
+_RAW_RCCL = os.environ.get("APEX_AMD_SYNCBN_RAW_RCCL", "1") == "1"
+_COMMS = {}
+
+
+def _raw_comm(pg):
+    """The RCCL communicator pointer of ``pg`` when the raw path may drive it, else 0."""
+    if not _RAW_RCCL:
+        return 0
+    c = _COMMS.get(id(pg))
+    if c is not None and c[0] is pg:
+        return c[1]
+    from ..parallel.sync_batchnorm import is_syncbn_comm_group
+
+    ptr = 0
+    if is_syncbn_comm_group(pg) and _native.require().reducer.syncbn_raw_available():
+        try:
+            ptr = int(pg._get_backend(torch.device("cuda"))._comm_ptr())
+        except Exception:  # not an RCCL group / older torch
+            ptr = 0
+    if ptr:  # (the communicator exists after the group's first c10d collective)
+        _COMMS[id(pg)] = (pg, ptr)
+    return ptr
+
+
 def _allreduce(t, pg):
-    """In-place SUM all-reduce: one C++ c10d call for RCCL (no Python wrapper cost)."""
+    """In-place SUM all-reduce of a SyncBN packed buffer."""
     if dist.get_backend(pg) == "nccl":
-        _native.require().reducer.syncbn_allreduce(t, pg)
+        comm = _raw_comm(pg)
+        if comm:
+            _native.require().reducer.syncbn_allreduce_raw(t, comm)
+        else:
+            _native.require().reducer.syncbn_allreduce(t, pg)
     else:
         dist.all_reduce(t, group=pg)
 
@@ -166,10 +197,18 @@ class BatchNormFunction(torch.autograd.Function):
                       else C.local_stats_packed(xl))
             if dist.get_backend(pg) == "nccl":
                 # all_gather + combine in one C++ call (csrc/torch/reducer.cpp): the Python
-                # c10d wrapper cost ~20 us of host time per layer
-                mean_g, invstd, inv_total = _native.require().reducer.syncbn_allgather_combine(
-                    packed, pg, float(eps), float(momentum), running_mean, running_var,
-                    num_batches_tracked)
+                # c10d wrapper cost ~20 us of host time per layer; on the compute stream
+                # through the group's communicator when it is the dedicated SyncBN group
+                R = _native.require().reducer
+                comm = _raw_comm(pg)
+                if comm:
+                    mean_g, invstd, inv_total = R.syncbn_allgather_combine_raw(
+                        packed, comm, world, float(eps), float(momentum), running_mean,
+                        running_var, num_batches_tracked)
+                else:
+                    mean_g, invstd, inv_total = R.syncbn_allgather_combine(
+                        packed, pg, float(eps), float(momentum), running_mean, running_var,
+                        num_batches_tracked)
             else:  # gloo with GPU tensors (tests): list form into views of `gathered`
                 gathered = torch.empty(world * packed.numel(), dtype=packed.dtype,
                                        device=x.device)

@@ -31,6 +31,12 @@ from ..ops.batch_norm import BatchNormFunction  # noqa: F401  (re-exported)
 _COMM_GROUPS = {}
 
 
+def is_syncbn_comm_group(pg):
+    """True for the dedicated SyncBN group made by ``syncbn_comm_group`` (only SyncBN
+    collectives ever run on its communicator)."""
+    return any(g is pg for g in _COMM_GROUPS.values())
+
+
 def syncbn_comm_group():
     """The dedicated SyncBN process group for the current world (see module doc)."""
     key = id(dist.group.WORLD)

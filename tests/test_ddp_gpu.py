@@ -274,20 +274,26 @@ def test_bench_self_spawn_two_ranks_one_gpu():
 @pytest.mark.parametrize("residual", [False, True])
 def test_syncbn_forced_collectives_match_local_bn(pg, monkeypatch, residual):
     """SyncBN's RCCL path on one GPU (VERDICT r2 missing 2): ``force_collectives``
-    sends the packed statistics through ``all_gather_into_tensor`` and the packed
-    gradient sums through the in-place ``all_reduce`` on the strided [2C] view, on a
-    1-rank RCCL communicator.  Both must really run, and the result must equal the
-    local (no-collective) path to rounding."""
+    sends the packed statistics through an all-gather and the packed gradient sums
+    through an in-place all-reduce on the strided [2C] view, on a 1-rank RCCL
+    communicator - from C++ (csrc/torch/reducer.cpp: through the process group, or
+    straight on the compute stream with the dedicated SyncBN group's communicator).
+    Both must really run, and the result must equal the local (no-collective) path to
+    rounding."""
+    from apex_example_amd import _native
     from apex_example_amd.parallel import SyncBatchNorm
 
-    calls = {"all_gather_into_tensor": 0, "all_reduce": 0}
-    for name in calls:
-        orig = getattr(dist, name)
+    R = _native.require().reducer
+    kinds = {"syncbn_allgather_combine": "all_gather", "syncbn_allgather_combine_raw":
+             "all_gather", "syncbn_allreduce": "all_reduce", "syncbn_allreduce_raw": "all_reduce"}
+    calls = {"all_gather": 0, "all_reduce": 0}
+    for name, kind in kinds.items():
+        orig = getattr(R, name)
 
-        def wrapped(*a, _orig=orig, _name=name, **k):
-            calls[_name] += 1
+        def wrapped(*a, _orig=orig, _kind=kind, **k):
+            calls[_kind] += 1
             return _orig(*a, **k)
-        monkeypatch.setattr(dist, name, wrapped)
+        monkeypatch.setattr(R, name, wrapped)
 
     torch.manual_seed(0)
     C = 64
@@ -309,9 +315,9 @@ def test_syncbn_forced_collectives_match_local_bn(pg, monkeypatch, residual):
         torch.cuda.synchronize()
         ran = {k: calls[k] - before[k] for k in calls}
         if forced:
-            assert ran == {"all_gather_into_tensor": 1, "all_reduce": 1}, ran
+            assert ran == {"all_gather": 1, "all_reduce": 1}, ran
         else:
-            assert ran == {"all_gather_into_tensor": 0, "all_reduce": 0}, ran
+            assert ran == {"all_gather": 0, "all_reduce": 0}, ran
         outs.append([y.float(), xi.grad.float(), zi.grad.float() if residual else None,
                      bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var,
                      bn.num_batches_tracked])
