@@ -79,11 +79,16 @@ _COMMS = {}
 
 def _raw_comm(pg):
     """The RCCL communicator pointer of ``pg`` when the raw path may drive it, else 0."""
+    return _raw_comm_rank(pg)[0]
+
+
+def _raw_comm_rank(pg):
+    """(communicator pointer or 0, this process's rank in ``pg``)."""
     if not _RAW_RCCL:
-        return 0
+        return 0, -1
     c = _COMMS.get(id(pg))
     if c is not None and c[0] is pg:
-        return c[1]
+        return c[1], c[2]
     from ..parallel.sync_batchnorm import is_syncbn_comm_group
 
     ptr = 0
@@ -92,9 +97,10 @@ def _raw_comm(pg):
             ptr = int(pg._get_backend(torch.device("cuda"))._comm_ptr())
         except Exception:  # not an RCCL group / older torch
             ptr = 0
+    rank = dist.get_rank(pg)
     if ptr:  # (the communicator exists after the group's first c10d collective)
-        _COMMS[id(pg)] = (pg, ptr)
-    return ptr
+        _COMMS[id(pg)] = (pg, ptr, rank)
+    return ptr, rank
 
 
 def _allreduce(t, pg):
@@ -193,18 +199,26 @@ class BatchNormFunction(torch.autograd.Function):
             # all_gather -> one combine kernel (global mean / invstd, running stats,
             # num_batches_tracked, 1/global count) -> apply.  No host sync, no cat.
             pg = process_group if process_group is not None else dist.group.WORLD
-            packed = (C.slab_packed_stats(slab, count, slab_shift) if slab is not None
-                      else C.local_stats_packed(xl))
-            if dist.get_backend(pg) == "nccl":
+            nccl = dist.get_backend(pg) == "nccl"
+            comm, rank = _raw_comm_rank(pg) if nccl else (0, -1)
+            gathered = slot = None
+            if comm:
+                # the stats kernels write straight into this rank's slot of the gather
+                # destination: the all_gather runs in place (no send-buffer copy)
+                n = 2 * xl.size(1) + 1
+                gathered = torch.empty(world * n, dtype=torch.float32, device=x.device)
+                slot = gathered[rank * n:(rank + 1) * n]
+            packed = (C.slab_packed_stats(slab, count, slab_shift, out=slot) if slab is not None
+                      else C.local_stats_packed(xl, out=slot))
+            if nccl:
                 # all_gather + combine in one C++ call (csrc/torch/reducer.cpp): the Python
                 # c10d wrapper cost ~20 us of host time per layer; on the compute stream
                 # through the group's communicator when it is the dedicated SyncBN group
                 R = _native.require().reducer
-                comm = _raw_comm(pg)
                 if comm:
                     mean_g, invstd, inv_total = R.syncbn_allgather_combine_raw(
                         packed, comm, world, float(eps), float(momentum), running_mean,
-                        running_var, num_batches_tracked)
+                        running_var, num_batches_tracked, gathered=gathered, rank=rank)
                 else:
                     mean_g, invstd, inv_total = R.syncbn_allgather_combine(
                         packed, pg, float(eps), float(momentum), running_mean, running_var,

@@ -163,6 +163,12 @@ int attn_base_flag() {
   return (e && e[0] == '1') ? 1 : 0;
 }
 
+// APEX_AMD_ATTN_FWD=1|2: forward kernel variant (read per launch, for A/B runs)
+int attn_fwd_variant() {
+  const char* e = std::getenv("APEX_AMD_ATTN_FWD");
+  return (e && e[0] == '2') ? 2 : 1;
+}
+
 // ---------------------------------------------------------------------------- forward
 // Block -> (tile, b*H+h).  Dispatch order is the flattened block id (x fastest) and
 // consecutive ids go to consecutive XCDs, so: (1) the tiles of one head are gridDim.y
@@ -337,6 +343,219 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
         for (int dt = 0; dt < 2; ++dt)
           o[dt] = mfma32<T>(lds_tr8<T>(Vl, vlo[dt][t][s], vhi[dt][t][s]), pf, o[dt]);
       }
+  }
+
+  const float lt = l + __shfl_xor(l, 32);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (q < a.S) {
+    store_dT<T>(static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD, o, hl, inv);
+    if (hl == 0) a.lse[(int64_t)bh * a.lse_stride + q] = m + log2f(lt);
+  }
+}
+
+// the other 32-lane half's value of x (lane ^ 32) on the VALU (v_permlane32_swap)
+// instead of an LDS round trip (ds_bpermute)
+__device__ __forceinline__ float max_halves(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
+// Forward, software-pipelined (APEX_AMD_ATTN_FWD=2 selects it; A/B against attn_fwd_k):
+// the QK^T MFMAs of tile kt+1 are issued in the same basic block as the softmax of
+// tile kt, so the matrix pipe and the VALU work on independent streams of one wave;
+// K/V pass through a 3-deep LDS ring (tile kt's V, tile kt+1's K, tile kt+2 in
+// flight).  Tiles that need no mask for any query of the workgroup run this body;
+// boundary / diagonal tiles take the masked, unpipelined body afterwards.
+template <typename T, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
+  typedef typename Frag<T>::v8 v8;
+  constexpr int TB = 2 * kAKT * kARow;  // one (K, V) tile: 16 KiB
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * TB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hl = lane >> 5, c32 = lane & 31;
+  int tile, bh;
+  tile_of_block(CAUSAL, true, 0, tile, bh);
+  const int b = bh / a.H, hh = bh - b * a.H;
+  const int qb0 = tile * 128;
+  const int q = qb0 + wid * 32 + c32;
+  const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
+  const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
+  const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
+
+  v8 qf[4];
+  {
+    const int qq = q < a.S ? q : a.S - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[s] = *reinterpret_cast<const v8*>(Q + (int64_t)qq * a.qss + 16 * s + 8 * hl);
+  }
+  int nkt = (a.S + kAKT - 1) / kAKT;
+  if (CAUSAL) {
+    const int last = (qb0 + 127 < a.S ? qb0 + 127 : a.S - 1) / kAKT + 1;
+    nkt = last < nkt ? last : nkt;
+  }
+  // tiles [0, nfull): every key < S and (causal) below every query of the workgroup
+  int nfull = a.S / kAKT;
+  if (CAUSAL) nfull = nfull < qb0 / kAKT ? nfull : qb0 / kAKT;
+  nfull = nfull < nkt ? nfull : nkt;
+
+  const int lrow = lane >> 3, pch = lane & 7;
+  auto issue = [&](int kt) {  // 4 LDS-DMA instructions per lane
+    unsigned char* Kl = lds + (kt % 3) * TB;
+    unsigned char* Vl = Kl + kAKT * kARow;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wid * 2 + i) * 8 + lrow;
+      const int key = kt * kAKT + row;
+      const int kk = key < a.S ? key : a.S - 1;
+      const int chk = (swz_rows(row, pch) - row * kARow) >> 4;
+      const int chv = (swz_tr(row, pch) - row * kARow) >> 4;
+      glds16(K + (int64_t)kk * a.kss + chk * 8, Kl + (wid * 2 + i) * 1024);
+      glds16(V + (int64_t)kk * a.vss + chv * 8, Vl + (wid * 2 + i) * 1024);
+    }
+  };
+  int koff[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) koff[t][s] = swz_rows(32 * t + c32, 2 * s + hl);
+  int vlo[2][2][2], vhi[2][2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = 32 * t + 16 * s + 4 * hl;
+        const int c0 = 32 * dt + ((lane >> 4) & 1) * 16;
+        vlo[dt][t][s] = tr_addr(r0, c0, lane);
+        vhi[dt][t][s] = tr_addr(r0 + 8, c0, lane);
+      }
+  auto qk = [&](f32x16_t (&x)[2], int kt) {
+    const unsigned char* Kl = lds + (kt % 3) * TB;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[t][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) x[t] = mfma32<T>(lds_row8<T>(Kl, koff[t][s]), qf[s], x[t]);
+    }
+  };
+  // wait until tile kt+1 has landed (the only DMA in flight), then refill the slot
+  // tile kt-1 used (every wave is past its P.V after the barrier)
+  auto top = [&](int kt) {
+    if (kt + 1 < nkt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 2 < nkt) issue(kt + 2);
+    }
+  };
+
+  f32x16_t o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[0][i] = o[1][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  // softmax of x (tile at k0; masked or not) folded into (m, l, o), then O += P.V
+  auto finish = [&](f32x16_t (&x)[2], int kt, bool need_mask) {
+    const unsigned char* Vl = lds + (kt % 3) * TB + kAKT * kARow;
+    const int k0 = kt * kAKT;
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= a.S || (CAUSAL && key > q)) x[t][r] = -INFINITY;
+        }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, x[t][r]);
+    tmax = max_halves(tmax);
+    const float mnew = fmaxf(m, tmax * a.scale_log2);
+    float psum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(fmaf(x[t][r], a.scale_log2, -mnew));
+        psum += p;
+        x[t][r] = p;
+      }
+    const bool grow = __any(mnew != m);
+    const float alpha = grow ? exp2f(m - mnew) : 1.f;
+    m = mnew;
+    l = l * alpha + psum;
+    if (grow) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+      }
+    }
+    if (DROP) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
+          x[t][r] = drop_keep(hsh, key, a.thr16) ? x[t][r] * a.inv_keep : 0.f;
+          x[t][r + 1] = drop_keep(hsh, key + 1, a.thr16) ? x[t][r + 1] * a.inv_keep : 0.f;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const v8 pf = acc_frag<T>(x[t], s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = mfma32<T>(lds_tr8<T>(Vl, vlo[dt][t][s], vhi[dt][t][s]), pf, o[dt]);
+      }
+  };
+
+  issue(0);
+  if (1 < nkt) issue(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (2 < nkt) issue(2);
+  f32x16_t sc[2];
+  qk(sc, 0);
+  // invariant at the top of iteration kt: tiles <= kt+1 issued, sc = S of tile kt
+  int kt = 0;
+  for (; kt + 1 < nfull; ++kt) {  // pipelined: S(kt+1) beside softmax(kt)
+    if (kt > 0) top(kt);
+    f32x16_t sn[2];
+    qk(sn, kt + 1);
+    finish(sc, kt, false);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) sc[t] = sn[t];
+  }
+  if (kt < nfull) {  // last full tile: next tile's S only if one follows
+    if (kt > 0) top(kt);
+    if (kt + 1 < nkt) {
+      f32x16_t sn[2];
+      qk(sn, kt + 1);
+      finish(sc, kt, false);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) sc[t] = sn[t];
+    } else {
+      finish(sc, kt, false);
+    }
+    ++kt;
+  }
+  for (; kt < nkt; ++kt) {  // masked tail (boundary / causal diagonal)
+    if (kt > 0) top(kt);
+    const int k0 = kt * kAKT;
+    if (CAUSAL && k0 > qb0 + wid * 32 + 31) continue;  // whole tile masked for this wave
+    if (kt > nfull) qk(sc, kt);
+    const bool need_mask = (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
+    finish(sc, kt, need_mask);
   }
 
   const float lt = l + __shfl_xor(l, 32);
@@ -728,8 +947,17 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   a.base = attn_base_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr16 != 0;
+  const bool v2 = !a.base && attn_fwd_variant() == 2;
 #define ATTN_FWD_LAUNCH(T)                                                                     \
-  if (L.causal) {                                                                              \
+  if (v2) {                                                                                    \
+    if (L.causal) {                                                                            \
+      if (drop) hipLaunchKernelGGL((attn_fwd2_k<T, true, true>), grid, block, 0, st, a);       \
+      else hipLaunchKernelGGL((attn_fwd2_k<T, true, false>), grid, block, 0, st, a);           \
+    } else {                                                                                   \
+      if (drop) hipLaunchKernelGGL((attn_fwd2_k<T, false, true>), grid, block, 0, st, a);      \
+      else hipLaunchKernelGGL((attn_fwd2_k<T, false, false>), grid, block, 0, st, a);          \
+    }                                                                                          \
+  } else if (L.causal) {                                                                       \
     if (drop) hipLaunchKernelGGL((attn_fwd_k<T, true, true>), grid, block, 0, st, a);          \
     else hipLaunchKernelGGL((attn_fwd_k<T, true, false>), grid, block, 0, st, a);              \
   } else {                                                                                     \

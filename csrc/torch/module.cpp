@@ -155,7 +155,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("weight"), py::arg("need_wgrad"), py::arg("sum_scale") = py::none(),
          py::arg("grad_weight") = py::none(), py::arg("grad_bias") = py::none());
   bn.def("slab_packed_stats", &bn_slab_packed_stats_op, py::arg("slab"), py::arg("count"),
-         py::arg("shift"));
+         py::arg("shift"), py::arg("out") = py::none());
   bn.def("set_tuning", &bn_set_tuning, py::arg("red_rpt") = -1, py::arg("red_cap") = -1,
          py::arg("red_min") = -1, py::arg("elem_rpt") = -1, py::arg("elem_cap") = -1,
          py::arg("elem_min") = -1);
@@ -169,7 +169,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("need_wgrad"), py::arg("mask") = py::none(),
          py::arg("sum_scale") = py::none(), py::arg("grad_weight") = py::none(),
          py::arg("grad_bias") = py::none());
-  bn.def("local_stats_packed", &bn_local_stats_packed_op);
+  bn.def("local_stats_packed", &bn_local_stats_packed_op, py::arg("x"),
+         py::arg("out") = py::none());
   bn.def("combine_stats_sync", &bn_combine_stats_sync_op, py::arg("gathered"), py::arg("eps"),
          py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"),
          py::arg("nbt") = py::none());

@@ -299,7 +299,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
 
 // SyncBN forward, local part: [mean(C) | var(C) | count] in ONE buffer written by the
 // stats kernels (the count by the finalize kernel), ready for the all_gather
-at::Tensor bn_local_stats_packed_op(at::Tensor x) {
+// `out`: write into that contiguous fp32 [2C+1] buffer instead (the caller's slot of the
+// all_gather destination: the gather then runs in place, no send-buffer copy)
+static at::Tensor packed_out(OptT out, int64_t C, const at::TensorOptions& fopt) {
+  if (!has(out)) return at::empty({2 * C + 1}, fopt);
+  TORCH_CHECK(out->is_cuda() && out->scalar_type() == at::kFloat && out->is_contiguous() &&
+                  out->numel() == 2 * C + 1,
+              "bn packed stats: out must be a contiguous fp32 [2C+1] GPU tensor");
+  return *out;
+}
+
+at::Tensor bn_local_stats_packed_op(at::Tensor x, OptT out) {
   c10::NoGradGuard no_grad_;
   BNView v = bn_view(x);
   if (!x.is_cuda()) {
@@ -309,7 +319,7 @@ at::Tensor bn_local_stats_packed_op(at::Tensor x) {
   }
   x = conform(x, v);
   auto fopt = x.options().dtype(at::kFloat);
-  at::Tensor packed = at::empty({2 * v.C + 1}, fopt);
+  at::Tensor packed = packed_out(out, v.C, fopt);
   at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
   float* p = packed.data_ptr<float>();
   bn_local_stats(x.data_ptr(), dtype_of(x), v.outer, v.C, v.inner, v.cl, p, p + v.C,
@@ -732,7 +742,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_o
   return {sum_dy, sum_dy_xmu, gw, gb};
 }
 
-at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift) {
+at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift, OptT out) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
@@ -745,7 +755,7 @@ at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift) {
                 "bn slab stats: shift must be contiguous fp32 [C]");
     sp = shift->data_ptr<float>();
   }
-  at::Tensor packed = at::empty({2 * C + 1}, slab.options());
+  at::Tensor packed = packed_out(out, C, slab.options());
   at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, slab.options());
   bn_slab_packed_stats(slab.data_ptr<float>(), (int)S, C, count, sp, packed.data_ptr<float>(),
                        ws.data_ptr<float>(), cur_stream());

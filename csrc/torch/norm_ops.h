@@ -41,7 +41,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_op(at::Tensor me
 // with C % 8 == 0 and relu; otherwise the 4th result is undefined / None).
 // SyncBN: packed local stats [mean | var | count] and the combine of the gathered
 // [world, 2C+1] stats -> (mean, invstd, 1/global count)
-at::Tensor bn_local_stats_packed_op(at::Tensor x);
+at::Tensor bn_local_stats_packed_op(at::Tensor x, OptT out = c10::nullopt);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_combine_stats_sync_op(
     at::Tensor gathered, double eps, double momentum, OptT running_mean, OptT running_var,
     OptT nbt);
@@ -85,6 +85,7 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_op(
     at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale,
     OptT grad_weight = c10::nullopt, OptT grad_bias = c10::nullopt);
-at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift);
+at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift,
+                                   OptT out = c10::nullopt);
 
 }  // namespace amd

@@ -651,13 +651,24 @@ bool syncbn_raw_available() { return rccl_allgather() && rccl_allreduce(); }
 std::tuple<at::Tensor, at::Tensor, at::Tensor> syncbn_allgather_combine_raw(
     at::Tensor packed, int64_t comm, int64_t world, double eps, double momentum,
     c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
-    c10::optional<at::Tensor> nbt) {
+    c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> gathered_in, int64_t rank) {
   c10::NoGradGuard ng;
   TORCH_CHECK(syncbn_raw_available(), "syncbn: RCCL entry points not found");
   TORCH_CHECK(comm != 0 && world >= 1, "syncbn: no communicator");
   TORCH_CHECK(packed.is_cuda() && packed.is_contiguous() && packed.scalar_type() == at::kFloat,
               "syncbn: packed fp32 stats on the GPU");
-  at::Tensor gathered = at::empty({world * packed.numel()}, packed.options());
+  at::Tensor gathered;
+  if (gathered_in.has_value() && gathered_in->defined()) {
+    // in-place gather: the stats kernels wrote this rank's slot of the destination
+    // (RCCL skips the send-buffer copy; at world 1 the collective is a no-op)
+    gathered = *gathered_in;
+    TORCH_CHECK(gathered.is_contiguous() && gathered.scalar_type() == at::kFloat &&
+                    gathered.numel() == world * packed.numel() && rank >= 0 && rank < world &&
+                    packed.data_ptr<float>() == gathered.data_ptr<float>() + rank * packed.numel(),
+                "syncbn: packed must be rank's slot of gathered");
+  } else {
+    gathered = at::empty({world * packed.numel()}, packed.options());
+  }
   const ncclResult_t r = rccl_allgather()(packed.data_ptr(), gathered.data_ptr(),
                                           (size_t)packed.numel(), ncclFloat32,
                                           reinterpret_cast<ncclComm_t>(comm),
@@ -683,7 +694,8 @@ void register_reducer(pybind11::module_& m) {
   m.def("syncbn_raw_available", &syncbn_raw_available);
   m.def("syncbn_allgather_combine_raw", &syncbn_allgather_combine_raw, py::arg("packed"),
         py::arg("comm"), py::arg("world"), py::arg("eps"), py::arg("momentum"),
-        py::arg("running_mean"), py::arg("running_var"), py::arg("nbt") = py::none());
+        py::arg("running_mean"), py::arg("running_var"), py::arg("nbt") = py::none(),
+        py::arg("gathered") = py::none(), py::arg("rank") = -1);
   m.def("syncbn_allreduce_raw", &syncbn_allreduce_raw, py::arg("t"), py::arg("comm"));
   m.def("syncbn_allgather_combine", &syncbn_allgather_combine, py::arg("packed"), py::arg("pg"),
         py::arg("eps"), py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"),
