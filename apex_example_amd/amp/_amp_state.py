@@ -46,7 +46,21 @@ def maybe_print(msg, rank0=False):
 
 def master_params(optimizer):
     """Generator over the parameters the optimizer updates (fp32 masters under
-    O2), as ``apex.amp.master_params``."""
+    O2), as ``apex.amp.master_params``.
+
+    Folded-unscale mode (amp O1 + a fused optimizer built with
+    ``materialize_master_grads=False``) leaves the grads loss-scaled after
+    ``scale_loss`` exits - the optimizer kernel divides by the scale itself.  Asking
+    for the master params is what Apex code does before touching grads
+    (``clip_grad_norm_(amp.master_params(opt), max_norm)``), so a pending scale is
+    removed here, in place and once, and the step then runs on unscaled grads.
+    (Under O2 that mode keeps no fp32 master grads at all; clip with the default
+    ``materialize_master_grads=True``.)"""
+    stash = getattr(optimizer, "_amp_stash", None)
+    if stash is not None and getattr(stash, "grads_scaled", False):
+        from ._process_optimizer import _unscale_pending
+
+        _unscale_pending(optimizer)
     for group in optimizer.param_groups:
         for p in group["params"]:
             yield p

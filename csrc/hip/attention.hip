@@ -21,11 +21,12 @@
 //     ((row>>1)&1)<<2 swizzle (transposed reads) - both conflict-free;
 //   * dropout keeps are a counter-based hash of (seed, b*H+h, query, key) so the
 //     backward regenerates them bit-exactly.
-// Backward = preprocess (D = rowsum(dO*O)), a dK/dV kernel (workgroup owns 128
-// keys, loops over queries, "unswapped" S = Q.K^T so dV = P^T.dO and
-// dK = dS^T.Q sum over the register rows) and a dQ kernel (workgroup owns 128
-// queries, swapped orientation so dQ = dS.K sums over register rows) - no
-// atomics (bitwise reproducible), no LDS transposes of score tiles.
+// Backward = a dQ kernel (workgroup owns 128 queries, swapped orientation so
+// dQ = dS.K sums over register rows; it also forms D = rowsum(dO*O) from the dO
+// fragments it holds anyway) followed by a dK/dV kernel (workgroup owns 128 keys,
+// loops over queries, "unswapped" S = Q.K^T so dV = P^T.dO and dK = dS^T.Q sum
+// over the register rows) - no atomics (bitwise reproducible), no LDS transposes
+// of score tiles, no preprocess launch.
 #include <cstdlib>
 
 #include "amd_dev.h"
@@ -96,10 +97,19 @@ __device__ __forceinline__ int tr_addr(int r0, int c0, int lane) {
   return swz_tr(r0 + q, col >> 3) + ((col >> 2) & 1) * 8;
 }
 
-// counter-based dropout bits: one 32-bit hash per (query, key pair), 16 bits per key
-__device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q,
-                                              uint32_t kp) {
-  uint32_t x = seed ^ (bh * 0x9E3779B1u) ^ (q * 0x85EBCA77u) ^ (kp * 0xC2B2AE3Du);
+// Counter-based dropout bits: one 32-bit hash per (query, key pair), 16 bits per key.
+// The hash input is a point of a Weyl lattice, base(seed, b*H+h) + q*kDropQ +
+// (key>>1)*kDropK (mod 2^32), so a kernel steps from one (query, key pair) to the next
+// with ONE add whose lattice offset is a compile-time literal; the mixer uses the
+// full-rate 24-bit multiply (v_mul_u32_u24) where the classic 32-bit finalizers need
+// the quarter-rate v_mul_lo_u32 (measured: 2-3 v_mul_lo_u32 per hash were ~60 % of the
+// dropout VALU time).  Statistics checked against the 32-bit finalizer on 2M-score
+// grids (keep rate, neighbour correlations along q / k / diagonal, 2-D spectrum,
+// 16-bit uniformity); tests/test_attention_gpu.py mirrors it bit for bit.
+constexpr uint32_t kDropQ = 0x85EBCA77u, kDropK = 0xC2B2AE3Du;
+
+__device__ __forceinline__ uint32_t drop_base(uint32_t seed, uint32_t bh) {
+  uint32_t x = seed ^ (bh * 0x9E3779B1u);
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
@@ -107,15 +117,38 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32
   x ^= x >> 16;
   return x;
 }
+
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16;
+  x = __umul24(x, 0xE9846Bu) ^ (x >> 24);
+  x ^= x >> 13;
+  x = __umul24(x, 0x8B3C2Du) ^ (x >> 24);
+  x ^= x >> 16;
+  return x;
+}
+
+// the closed form; the kernels' incremental lattice steps compute exactly this
+[[maybe_unused]] __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q,
+                                              uint32_t kp) {
+  return drop_mix(drop_base(seed, bh) + q * kDropQ + kp * kDropK);
+}
+
+// raw v_exp_f32: exp2f() expands to a denormal-safe sequence (compare, select, ldexp:
+// 5-6 VALU per score); softmax arguments are <= 0 and a result below 2^-126 may flush
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ bool drop_keep(uint32_t h, int key, uint32_t thr16) {
   const uint32_t v = (key & 1) ? (h >> 16) : (h & 0xffffu);
   return v >= thr16;
 }
 
+// one v_cvt_pk_{bf16,f16}_f32 per pair (converting the two floats separately and
+// merging the halves cost 4 VALU per pair: ~50 of the forward's ~215 VALU per tile)
 template <typename T>
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  T x = (T)a, y = (T)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, t2));
 }
 
 // registers 8s..8s+7 of a 32x32 accumulator as a 16-bit MFMA fragment
@@ -155,7 +188,7 @@ struct AttnArgs {
   uint32_t thr16;    // dropout threshold (p * 65536), 0 = no dropout
   float inv_keep;    // 1 / (1 - p)
   uint32_t seed;
-  int base;  // APEX_AMD_ATTN_BASE=1: round-1 behaviour (eager rescale / per-lane hashes), A/B only
+  int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
 };
 
 int attn_base_flag() {
@@ -167,6 +200,13 @@ int attn_base_flag() {
 int attn_fwd_variant() {
   const char* e = std::getenv("APEX_AMD_ATTN_FWD");
   return (e && e[0] == '2') ? 2 : 1;
+}
+
+// APEX_AMD_ATTN_DQ_IL=0: dQ kernel without the interleaved clean-tile body (A/B;
+// measured 3-4 % slower)
+int attn_dq_interleave() {
+  const char* e = std::getenv("APEX_AMD_ATTN_DQ_IL");
+  return (e && e[0] == '0') ? 0 : 1;
 }
 
 // ---------------------------------------------------------------------------- forward
@@ -195,13 +235,18 @@ template <typename T, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   typedef typename Frag<T>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * kAKT * kARow];  // 2 x (K, V)
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
   tile_of_block(CAUSAL, true, a.base, tile, bh);
   const int b = bh / a.H, hh = bh - b * a.H;
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;  // this lane's query
+  // dropout lattice point of (q, key pair 2hl) at key tile 0
+  const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
+                                    (uint32_t)(2 * hl) * kDropK
+                              : 0u;
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
   const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
@@ -303,14 +348,14 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
     // raised its running max (alpha == 1 exactly: same math, 32 fewer multiplies
     // per tile - the common case once the first tiles have set the max)
     const bool grow = a.base || __any(mnew != m);
-    const float alpha = grow ? exp2f(m - mnew) : 1.f;
+    const float alpha = grow ? fexp2(m - mnew) : 1.f;
     m = mnew;
     float psum = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(fmaf(x[t][r], a.scale_log2, -mnew));
+        const float p = fexp2(fmaf(x[t][r], a.scale_log2, -mnew));
         psum += p;
         x[t][r] = p;
       }
@@ -322,15 +367,16 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
         o[1][i] *= alpha;
       }
     }
-    if (DROP) {
+    if (DROP) {  // dropped P (the 1/(1-p) factor is applied to O once, at the store)
+      const uint32_t tb = dbase + (uint32_t)(k0 >> 1) * kDropK;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;  // even
-          const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
-          x[t][r] = drop_keep(hsh, key, a.thr16) ? x[t][r] * a.inv_keep : 0.f;
-          x[t][r + 1] = drop_keep(hsh, key + 1, a.thr16) ? x[t][r + 1] * a.inv_keep : 0.f;
+          // key pair (k0 + 32t + (r&3) + 8(r>>2) + 4hl) >> 1: a literal lattice step
+          const uint32_t hsh = drop_mix(tb + (uint32_t)(16 * t + ((r >> 1) & 1) + 4 * (r >> 2)) * kDropK);
+          x[t][r] = (hsh & 0xffffu) >= a.thr16 ? x[t][r] : 0.f;
+          x[t][r + 1] = (hsh >> 16) >= a.thr16 ? x[t][r + 1] : 0.f;
         }
     }
     // O^T[d][q] += V^T[d][key] . P^T[key][q]
@@ -346,7 +392,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   }
 
   const float lt = l + __shfl_xor(l, 32);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const float inv = lt > 0.f ? (DROP ? a.inv_keep : 1.f) / lt : 0.f;
   if (q < a.S) {
     store_dT<T>(static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD, o, hl, inv);
     if (hl == 0) a.lse[(int64_t)bh * a.lse_stride + q] = m + log2f(lt);
@@ -372,13 +418,17 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
   typedef typename Frag<T>::v8 v8;
   constexpr int TB = 2 * kAKT * kARow;  // one (K, V) tile: 16 KiB
   __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * TB];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
   tile_of_block(CAUSAL, true, 0, tile, bh);
   const int b = bh / a.H, hh = bh - b * a.H;
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;
+  const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
+                                    (uint32_t)(2 * hl) * kDropK
+                              : 0u;
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
   const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
@@ -482,12 +532,12 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(fmaf(x[t][r], a.scale_log2, -mnew));
+        const float p = fexp2(fmaf(x[t][r], a.scale_log2, -mnew));
         psum += p;
         x[t][r] = p;
       }
     const bool grow = __any(mnew != m);
-    const float alpha = grow ? exp2f(m - mnew) : 1.f;
+    const float alpha = grow ? fexp2(m - mnew) : 1.f;
     m = mnew;
     l = l * alpha + psum;
     if (grow) {
@@ -497,15 +547,16 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
         o[1][i] *= alpha;
       }
     }
-    if (DROP) {
+    if (DROP) {  // dropped P (the 1/(1-p) factor is applied to O once, at the store)
+      const uint32_t tb = dbase + (uint32_t)(k0 >> 1) * kDropK;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
-          x[t][r] = drop_keep(hsh, key, a.thr16) ? x[t][r] * a.inv_keep : 0.f;
-          x[t][r + 1] = drop_keep(hsh, key + 1, a.thr16) ? x[t][r + 1] * a.inv_keep : 0.f;
+          // key pair (k0 + 32t + (r&3) + 8(r>>2) + 4hl) >> 1: a literal lattice step
+          const uint32_t hsh = drop_mix(tb + (uint32_t)(16 * t + ((r >> 1) & 1) + 4 * (r >> 2)) * kDropK);
+          x[t][r] = (hsh & 0xffffu) >= a.thr16 ? x[t][r] : 0.f;
+          x[t][r + 1] = (hsh >> 16) >= a.thr16 ? x[t][r + 1] : 0.f;
         }
     }
 #pragma unroll
@@ -559,7 +610,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
   }
 
   const float lt = l + __shfl_xor(l, 32);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const float inv = lt > 0.f ? (DROP ? a.inv_keep : 1.f) / lt : 0.f;
   if (q < a.S) {
     store_dT<T>(static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD, o, hl, inv);
     if (hl == 0) a.lse[(int64_t)bh * a.lse_stride + q] = m + log2f(lt);
@@ -585,34 +636,8 @@ struct AttnBwdArgs {
   uint32_t thr16;
   float inv_keep;
   uint32_t seed;
-  int base;  // APEX_AMD_ATTN_BASE=1: round-1 behaviour (eager rescale / per-lane hashes), A/B only
+  int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
 };
-
-// D[b,h,q] = sum_d dO * O: 8 lanes per (b, q, h) row, one 16-byte load each
-template <typename T>
-__global__ void __launch_bounds__(256) attn_bwd_pre_k(AttnBwdArgs a) {
-  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
-  const int part = threadIdx.x & 7;
-  const int64_t rows = (int64_t)a.B * a.S * a.H;
-  float acc = 0.f;
-  int b = 0, q = 0, hh = 0;
-  if (row < rows) {
-    hh = (int)(row % a.H);
-    const int64_t bq = row / a.H;
-    q = (int)(bq % a.S);
-    b = (int)(bq / a.S);
-    float ov[8], dv[8];
-    load8(static_cast<const T*>(a.o) + b * a.osb + (int64_t)q * a.oss + hh * a.osh + part * 8, ov);
-    load8(static_cast<const T*>(a.dout) + b * a.dsb + (int64_t)q * a.dss + hh * a.dsh + part * 8,
-          dv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc += ov[i] * dv[i];
-  }
-  acc += __shfl_xor(acc, 1);
-  acc += __shfl_xor(acc, 2);
-  acc += __shfl_xor(acc, 4);
-  if (row < rows && part == 0) a.D[((int64_t)b * a.H + hh) * a.lse_stride + q] = acc;
-}
 
 // dK / dV: a workgroup owns 128 keys (32 per wave, one per lane column), loops
 // over 64-query tiles.  Scores are computed unswapped, S[q][key] = Q . K^T with
@@ -629,7 +654,8 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
   constexpr int IMG = kAKT * kARow;     // 8 KiB
   constexpr int BUF = 4 * IMG + 1024;   // Q rows, Q tr, dO rows, dO tr, {lse, D}
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
   tile_of_block(CAUSAL, false, a.base, tile, bh);
@@ -638,6 +664,10 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
   const int kw0 = kb0 + wid * 32;
   const int key = kw0 + c32;
   const int kk = key < a.S ? key : a.S - 1;
+  // dropout lattice point of (query key & 1, this lane's key pair)
+  const uint32_t kdrop = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)(key >> 1) * kDropK +
+                                    (uint32_t)(key & 1) * kDropQ
+                              : 0u;
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* dO = static_cast<const T*>(a.dout) + b * a.dsb + hh * a.dsh;
   const float* lse = a.lse + (int64_t)bh * a.lse_stride;
@@ -717,11 +747,9 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
     const float* st_lse = reinterpret_cast<const float*>(base + 4 * IMG);
     const float* st_D = st_lse + 64;
     const int q0 = qt * kAKT;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int qh0 = q0 + 32 * h;
-      if (CAUSAL && qh0 + 31 < kw0) continue;  // every query of this half precedes every key
-      f32x16_t sc, dp;
+    // the four stages of one 32-query half h (S / dP products, softmax backward,
+    // mask, dV / dK products)
+    auto sdp = [&](int h, f32x16_t& sc, f32x16_t& dp) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) sc[i] = dp[i] = 0.f;
 #pragma unroll
@@ -729,8 +757,8 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
         sc = mfma32<T>(lds_row8<T>(Qr, roff[h][s]), kf[s], sc);
         dp = mfma32<T>(lds_row8<T>(Or, roff[h][s]), vf[s], dp);
       }
-      // wave-uniform: does any (query, key) of this 32 x 32 block need a mask?
-      const bool need_mask = (qh0 + 31 >= a.S) || (CAUSAL && kw0 + 31 > qh0);
+    };
+    auto softmax_bwd = [&](int h, f32x16_t& sc, f32x16_t& dp) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int li = 32 * h + 8 * g + 4 * hl;  // local query of register 4g
@@ -742,16 +770,12 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
         // (lane ^ 1) each hash every other query and swap the results over DPP
         // (quad_perm [1,0,3,2]), so a lane computes 2 hashes per 4 queries, not 4
         uint32_t hq[4];
-        if (DROP && a.base) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            hq[e] = drop_hash(a.seed, (uint32_t)bh, (uint32_t)(q0 + li + e), (uint32_t)(key >> 1));
-        } else if (DROP) {
+        if (DROP) {
+          const uint32_t qhb = kdrop + (uint32_t)(q0 + 32 * h + 4 * hl) * kDropQ;
 #pragma unroll
           for (int pr = 0; pr < 2; ++pr) {
-            const uint32_t v = drop_hash(a.seed, (uint32_t)bh,
-                                         (uint32_t)(q0 + li + 2 * pr + (key & 1)),
-                                         (uint32_t)(key >> 1));
+            // query q0 + li + 2pr + (key & 1): a literal lattice step from qhb
+            const uint32_t v = drop_mix(qhb + (uint32_t)(8 * g + 2 * pr) * kDropQ);
             const uint32_t w = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
             hq[2 * pr] = (key & 1) ? w : v;
             hq[2 * pr + 1] = (key & 1) ? v : w;
@@ -760,16 +784,25 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
-          const int q = q0 + li + e;
-          float z = 1.f;
-          if (DROP) z = drop_keep(hq[e], key, a.thr16) ? a.inv_keep : 0.f;
-          float p = exp2f(fmaf(sc[r], a.scale_log2, -lsev[e]));
-          float ds = p * fmaf(dp[r], z, -Dv[e]);
-          if (need_mask && !(q < a.S && !(CAUSAL && key > q))) p = ds = 0.f;
-          sc[r] = DROP ? p * z : p;
-          dp[r] = ds;
+          bool keep = true;
+          if (DROP) keep = drop_keep(hq[e], key, a.thr16);
+          float p = fexp2(fmaf(sc[r], a.scale_log2, -lsev[e]));
+          // dropped dP scaled by 1/(1-p); the dropped P feeding dV^T is left unscaled
+          // (the factor is applied to dV once, at the store)
+          const float dpz = DROP ? (keep ? dp[r] * a.inv_keep : 0.f) : dp[r];
+          sc[r] = (DROP && !keep) ? 0.f : p;
+          dp[r] = p * (dpz - Dv[e]);
         }
       }
+    };
+    auto mask = [&](int h, f32x16_t& sc, f32x16_t& dp) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = q0 + 32 * h + 8 * (r >> 2) + 4 * hl + (r & 3);
+        if (!(q < a.S && !(CAUSAL && key > q))) sc[r] = dp[r] = 0.f;
+      }
+    };
+    auto accum = [&](int h, const f32x16_t& sc, const f32x16_t& dp) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const v8 pf = acc_frag<T>(sc, s);
@@ -780,12 +813,38 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
           dk[dt] = mfma32<T>(lds_tr8<T>(Qt, tlo[dt][h][s], thi[dt][h][s]), sf, dk[dt]);
         }
       }
+    };
+    // wave-uniform: no (query, key) of the whole 64 x 32 tile needs a mask - the
+    // common case runs both halves as ONE straight-line block, so the compiler can
+    // put half 1's S / dP MFMAs beside half 0's softmax VALU and half 0's dV / dK
+    // MFMAs beside half 1's (a block split by a mask branch serialises them)
+    const bool clean = (q0 + kAKT <= a.S) && (!CAUSAL || kw0 + 31 <= q0);
+    if (clean) {
+      f32x16_t sc0, dp0, sc1, dp1;
+      sdp(0, sc0, dp0);
+      sdp(1, sc1, dp1);
+      softmax_bwd(0, sc0, dp0);
+      accum(0, sc0, dp0);
+      softmax_bwd(1, sc1, dp1);
+      accum(1, sc1, dp1);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int qh0 = q0 + 32 * h;
+        if (CAUSAL && qh0 + 31 < kw0) continue;  // every query of this half precedes every key
+        f32x16_t sc, dp;
+        sdp(h, sc, dp);
+        softmax_bwd(h, sc, dp);
+        // wave-uniform: does any (query, key) of this 32 x 32 block need a mask?
+        if ((qh0 + 31 >= a.S) || (CAUSAL && kw0 + 31 > qh0)) mask(h, sc, dp);
+        accum(h, sc, dp);
+      }
     }
   }
 
   if (key < a.S) {
     store_dT<T>(static_cast<T*>(a.dv) + b * a.dvsb + (int64_t)key * a.dvss + hh * a.dvsh, dv, hl,
-                1.f);
+                DROP ? a.inv_keep : 1.f);
     store_dT<T>(static_cast<T*>(a.dk) + b * a.dksb + (int64_t)key * a.dkss + hh * a.dksh, dk, hl,
                 a.scale);
   }
@@ -796,12 +855,13 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
 // lse / D are scalars and dQ^T = K^T . dS^T consumes dS^T from the accumulator.
 // K sits in LDS as a row image (A of S^T) and a transposed image (A of dQ^T);
 // V as a row image (A of dP^T = V . dO^T).
-template <typename T, bool CAUSAL, bool DROP>
+template <typename T, bool CAUSAL, bool DROP, bool IL = true>
 __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   typedef typename Frag<T>::v8 v8;
   constexpr int IMG = kAKT * kARow;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 3 * IMG];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
   tile_of_block(CAUSAL, true, a.base, tile, bh);
@@ -809,6 +869,9 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;
   const int qq = q < a.S ? q : a.S - 1;
+  const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
+                                    (uint32_t)(2 * hl) * kDropK
+                              : 0u;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
   const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
 
@@ -823,7 +886,22 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
     }
   }
   const float lse_q = a.lse[(int64_t)bh * a.lse_stride + qq];
-  const float D_q = a.D[(int64_t)bh * a.lse_stride + qq];
+  // D = rowsum(dO * O) of this lane's query, from the dO fragments already in
+  // registers (the two 32-lane halves hold complementary d ranges); written for the
+  // dK / dV kernel, which runs after this one (no separate preprocess launch)
+  float D_q;
+  {
+    const T* Opr = static_cast<const T*>(a.o) + b * a.osb + hh * a.osh + (int64_t)qq * a.oss;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const v8 ov = *reinterpret_cast<const v8*>(Opr + 16 * s + 8 * hl);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part = fmaf((float)of[s][j], (float)ov[j], part);
+    }
+    D_q = part + __shfl_xor(part, 32);
+    if (hl == 0 && q < a.S) a.D[(int64_t)bh * a.lse_stride + q] = D_q;
+  }
 
   int nkt = (a.S + kAKT - 1) / kAKT;
   if (CAUSAL) {
@@ -881,47 +959,65 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
     const unsigned char* Vr = base + 2 * IMG;
     const int k0 = kt * kAKT;
     if (CAUSAL && k0 > qb0 + wid * 32 + 31) continue;
-    f32x16_t sc[2], dp[2];
+    const uint32_t tb = dbase + (uint32_t)(k0 >> 1) * kDropK;
+    // stages of one 32-key half t: S^T / dP^T products, dS^T, mask, dQ^T product
+    auto sdp = [&](int t, f32x16_t& sc, f32x16_t& dp) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sc[t][i] = dp[t][i] = 0.f;
+      for (int i = 0; i < 16; ++i) sc[i] = dp[i] = 0.f;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        sc[t] = mfma32<T>(lds_row8<T>(Kr, koff[t][s]), qf[s], sc[t]);
-        dp[t] = mfma32<T>(lds_row8<T>(Vr, koff[t][s]), of[s], dp[t]);
+        sc = mfma32<T>(lds_row8<T>(Kr, koff[t][s]), qf[s], sc);
+        dp = mfma32<T>(lds_row8<T>(Vr, koff[t][s]), of[s], dp);
       }
-    }
-    const bool need_mask = (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
+    };
+    auto dsoft = [&](int t, f32x16_t& sc, const f32x16_t& dp) {
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;  // even
-        float z0 = 1.f, z1 = 1.f;
+        float dp0 = dp[r], dp1 = dp[r + 1];
         if (DROP) {
-          const uint32_t hsh = drop_hash(a.seed, (uint32_t)bh, (uint32_t)q, (uint32_t)(key >> 1));
-          z0 = drop_keep(hsh, key, a.thr16) ? a.inv_keep : 0.f;
-          z1 = drop_keep(hsh, key + 1, a.thr16) ? a.inv_keep : 0.f;
+          const uint32_t hsh = drop_mix(tb + (uint32_t)(16 * t + ((r >> 1) & 1) + 4 * (r >> 2)) * kDropK);
+          dp0 = (hsh & 0xffffu) >= a.thr16 ? dp0 * a.inv_keep : 0.f;
+          dp1 = (hsh >> 16) >= a.thr16 ? dp1 * a.inv_keep : 0.f;
         }
-        float d0 = exp2f(fmaf(sc[t][r], a.scale_log2, -lse_q)) * fmaf(dp[t][r], z0, -D_q);
-        float d1 = exp2f(fmaf(sc[t][r + 1], a.scale_log2, -lse_q)) * fmaf(dp[t][r + 1], z1, -D_q);
-        if (need_mask) {
-          if (!(key < a.S && !(CAUSAL && key > q))) d0 = 0.f;
-          if (!(key + 1 < a.S && !(CAUSAL && key + 1 > q))) d1 = 0.f;
-        }
-        sc[t][r] = d0;
-        sc[t][r + 1] = d1;
+        sc[r] = fexp2(fmaf(sc[r], a.scale_log2, -lse_q)) * (dp0 - D_q);
+        sc[r + 1] = fexp2(fmaf(sc[r + 1], a.scale_log2, -lse_q)) * (dp1 - D_q);
       }
+    };
+    auto mask = [&](int t, f32x16_t& sc) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (!(key < a.S && !(CAUSAL && key > q))) sc[r] = 0.f;
+      }
+    };
+    auto accum = [&](int t, const f32x16_t& sc) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const v8 sf = acc_frag<T>(sc[t], s);
+        const v8 sf = acc_frag<T>(sc, s);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
           dq[dt] = mfma32<T>(lds_tr8<T>(Kt, tlo[dt][t][s], thi[dt][t][s]), sf, dq[dt]);
       }
+    };
+    f32x16_t sc0, dp0, sc1, dp1;
+    sdp(0, sc0, dp0);
+    sdp(1, sc1, dp1);
+    // wave-uniform; unmasked tiles run as one straight-line block (half 0's dQ MFMAs
+    // beside half 1's softmax VALU)
+    const bool need_mask = (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
+    if (IL && !need_mask) {
+      dsoft(0, sc0, dp0);
+      accum(0, sc0);
+      dsoft(1, sc1, dp1);
+      accum(1, sc1);
+    } else {
+      dsoft(0, sc0, dp0);
+      dsoft(1, sc1, dp1);
+      mask(0, sc0);
+      mask(1, sc1);
+      accum(0, sc0);
+      accum(1, sc1);
+    }
   }
   if (q < a.S)
     store_dT<T>(static_cast<T*>(a.dq) + b * a.dqsb + (int64_t)q * a.dqss + hh * a.dqsh, dq, hl,
@@ -992,27 +1088,28 @@ void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
   a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
   a.seed = L.seed;
   a.base = attn_base_flag();
-  const int64_t rows = (int64_t)L.B * L.S * L.H;
-  const unsigned pre_blocks = (unsigned)((rows * 8 + 255) / 256);
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr16 != 0;
+  const bool dq_il = attn_dq_interleave();
+#define DQ_LAUNCH(T, C, D)                                                                     \
+  if (dq_il) hipLaunchKernelGGL((attn_bwd_dq_k<T, C, D, true>), grid, block, 0, st, a);          \
+  else hipLaunchKernelGGL((attn_bwd_dq_k<T, C, D, false>), grid, block, 0, st, a)
 #define ATTN_BWD_LAUNCH(T)                                                                     \
-  hipLaunchKernelGGL((attn_bwd_pre_k<T>), dim3(pre_blocks), dim3(256), 0, st, a);               \
   if (L.causal) {                                                                              \
     if (drop) {                                                                                \
+      DQ_LAUNCH(T, true, true);                                                                \
       hipLaunchKernelGGL((attn_bwd_dkdv_k<T, true, true>), grid, block, 0, st, a);             \
-      hipLaunchKernelGGL((attn_bwd_dq_k<T, true, true>), grid, block, 0, st, a);               \
     } else {                                                                                   \
+      DQ_LAUNCH(T, true, false);                                                               \
       hipLaunchKernelGGL((attn_bwd_dkdv_k<T, true, false>), grid, block, 0, st, a);            \
-      hipLaunchKernelGGL((attn_bwd_dq_k<T, true, false>), grid, block, 0, st, a);              \
     }                                                                                          \
   } else {                                                                                     \
     if (drop) {                                                                                \
+      DQ_LAUNCH(T, false, true);                                                               \
       hipLaunchKernelGGL((attn_bwd_dkdv_k<T, false, true>), grid, block, 0, st, a);            \
-      hipLaunchKernelGGL((attn_bwd_dq_k<T, false, true>), grid, block, 0, st, a);              \
     } else {                                                                                   \
+      DQ_LAUNCH(T, false, false);                                                              \
       hipLaunchKernelGGL((attn_bwd_dkdv_k<T, false, false>), grid, block, 0, st, a);           \
-      hipLaunchKernelGGL((attn_bwd_dq_k<T, false, false>), grid, block, 0, st, a);             \
     }                                                                                          \
   }
   if (L.dtype == DType::BF16) {
@@ -1021,6 +1118,7 @@ void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
     ATTN_BWD_LAUNCH(half_t)
   }
 #undef ATTN_BWD_LAUNCH
+#undef DQ_LAUNCH
 }
 
 }  // namespace amd

@@ -1,5 +1,6 @@
 """amp on the GPU: sync-free dynamic loss scaling, overflow skip, O1/O2/O3 end to end."""
 import copy
+import math
 
 import pytest
 import torch
@@ -304,3 +305,47 @@ def test_fused_sgd_native_plan_and_pair_launch_match_python_path(monkeypatch):
             assert pairs["n"] == n0
     for a, b in zip(out[False], out[True]):
         assert torch.equal(a, b)
+
+
+def test_folded_unscale_clip_through_master_params():
+    """amp O1 + FusedAdam(materialize_master_grads=False) keeps the grads loss-scaled
+    after scale_loss; Apex's documented clip between backward and step,
+    clip_grad_norm_(amp.master_params(opt), max_norm), must still see unscaled grads
+    (master_params removes the pending scale once, in place) and match the
+    materialized path step for step."""
+    from apex_example_amd import amp
+    from apex_example_amd.amp import amp as amp_mod
+    from apex_example_amd.optimizers import FusedAdam
+
+    def run(materialize):
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(),
+                                    torch.nn.Linear(64, 4)).to(DEV)
+        opt = FusedAdam(model.parameters(), lr=1e-2, materialize_master_grads=materialize)
+        model, opt = amp.initialize(model, opt, opt_level="O1", verbosity=0,
+                                    loss_scale="dynamic")
+        torch.manual_seed(1)
+        norms = []
+        for _ in range(6):
+            x = torch.randn(16, 32, device=DEV) * 10
+            y = torch.randint(0, 4, (16,), device=DEV)
+            opt.zero_grad()
+            loss = F.cross_entropy(model(x), y)
+            with amp.scale_loss(loss, opt) as s:
+                s.backward()
+            norms.append(float(torch.nn.utils.clip_grad_norm_(amp.master_params(opt), 0.05)))
+            opt.step()
+        out = [p.detach().float().clone() for p in amp.master_params(opt)]
+        amp_mod.deinit()
+        amp._amp_state.handle = None
+        return out, norms
+
+    a, na = run(True)
+    b, nb = run(False)
+    # overflowed steps (inf norm: skipped by both paths) aside, the clip is active
+    fin = [i for i, n in enumerate(na) if math.isfinite(n)]
+    assert len(fin) >= 2 and all(na[i] > 0.05 for i in fin), na
+    for x, y in zip(na, nb):
+        assert (x == y) if not math.isfinite(x) else abs(x - y) <= 1e-4 * abs(x), (na, nb)
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)

@@ -22,18 +22,32 @@ def _mul32(a, c):
     return (a * c) & M32
 
 
-def drop_keep_mask(B, H, S, seed, p):
-    """[B, H, S(q), S(k)] keep mask of the kernels' hash (int64 torch arithmetic)."""
-    thr = int(p * 65536 + 0.5)
-    bh = torch.arange(B * H, dtype=torch.int64).view(B, H, 1, 1)
-    q = torch.arange(S, dtype=torch.int64).view(1, 1, S, 1)
-    key = torch.arange(S, dtype=torch.int64).view(1, 1, 1, S)
-    kp = key >> 1
-    x = (seed ^ _mul32(bh, 0x9E3779B1) ^ _mul32(q, 0x85EBCA77) ^ _mul32(kp, 0xC2B2AE3D)) & M32
+def _murmur32(x):
     x = x ^ (x >> 16)
     x = _mul32(x, 0x7FEB352D)
     x = x ^ (x >> 15)
     x = _mul32(x, 0x846CA68B)
+    return x ^ (x >> 16)
+
+
+def _umul24(x, c):
+    return ((x & 0xFFFFFF) * (c & 0xFFFFFF)) & M32
+
+
+def drop_keep_mask(B, H, S, seed, p):
+    """[B, H, S(q), S(k)] keep mask of the kernels' hash (int64 torch arithmetic):
+    drop_mix(drop_base(seed, bh) + q * kDropQ + (key >> 1) * kDropK), low 16 bits for
+    even keys, high 16 for odd ones (csrc/hip/attention.hip)."""
+    thr = int(p * 65536 + 0.5)
+    bh = torch.arange(B * H, dtype=torch.int64).view(B, H, 1, 1)
+    q = torch.arange(S, dtype=torch.int64).view(1, 1, S, 1)
+    key = torch.arange(S, dtype=torch.int64).view(1, 1, 1, S)
+    base = _murmur32((seed ^ _mul32(bh, 0x9E3779B1)) & M32)
+    x = (base + _mul32(q, 0x85EBCA77) + _mul32(key >> 1, 0xC2B2AE3D)) & M32
+    x = x ^ (x >> 16)
+    x = _umul24(x, 0xE9846B) ^ (x >> 24)
+    x = x ^ (x >> 13)
+    x = _umul24(x, 0x8B3C2D) ^ (x >> 24)
     x = x ^ (x >> 16)
     v = torch.where((key & 1) == 1, x >> 16, x & 0xFFFF)
     return (v >= thr), 65536.0 / (65536 - thr)

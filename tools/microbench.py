@@ -681,26 +681,29 @@ def bench_attn(args):
         # dropout hashes); APEX_AMD_ATTN_FWD=2: the software-pipelined forward - both
         # read per launch, so every variant runs in this process
         variants = [("gfx950/base", {"APEX_AMD_ATTN_BASE": "1"}), ("gfx950", {}),
-                    ("gfx950/fwd2", {"APEX_AMD_ATTN_FWD": "2"})]
+                    ("gfx950/fwd2", {"APEX_AMD_ATTN_FWD": "2"}),
+                    ("gfx950/dq-il0", {"APEX_AMD_ATTN_DQ_IL": "0"})]
         if args.quick:
             variants = variants[1:]
+        keys = ("APEX_AMD_ATTN_BASE", "APEX_AMD_ATTN_FWD", "APEX_AMD_ATTN_DQ_IL")
         for vname, env in variants:
-            for key in ("APEX_AMD_ATTN_BASE", "APEX_AMD_ATTN_FWD"):
+            for key in keys:
                 os.environ.pop(key, None)
             os.environ.update(env)
             for p in (0.0, 0.1):  # training runs use attention dropout 0.1
                 f = lambda p=p: fused_attention(q, k, v, causal=causal, dropout_p=p)  # noqa: E731
-                tf_ = timeit(f)
+                tf_ = timeit(f, iters=50, warmup=10)
                 o = f()
-                tb = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True))
+                tb = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True),
+                            iters=50, warmup=10)
                 fl = 4 * b * h * s_ * s_ * d * (0.5 if causal else 1.0)
                 print("%-12s %-12s p=%.1f fwd %.0f us (%.0f TF)  bwd %.0f us (%.0f TF)" % (
                     vname, name, p, tf_,
                     fl / (tf_ * 1e-6) / 1e12, tb, 2.5 * fl / (tb * 1e-6) / 1e12), flush=True)
-        for key in ("APEX_AMD_ATTN_BASE", "APEX_AMD_ATTN_FWD"):
+        for key in keys:
             os.environ.pop(key, None)
-        if args.quick:
-            return
+    if args.quick:
+        return
     for lib in ("default", "ck"):
         try:
             torch.backends.cuda.preferred_rocm_fa_library(lib)
