@@ -423,9 +423,12 @@ void xentropy_bwd(const void* dloss, DType tg, const void* x, DType tx, const fl
 
 // ---- deterministic embedding weight gradient (embedding.hip) ------------------
 // sorted / perm: the stable sort of the T token ids and its permutation; out [V, H]
-// must be zero-filled; runs of equal ids are summed in sorted order (fp32).
+// must be zero-filled; runs of equal ids are summed in sorted order (fp32), runs
+// longer than 256 positions in chunk partials (slots: embedding_wgrad_slots(T, H)
+// floats of workspace) joined in chunk order.
+int64_t embedding_wgrad_slots(int64_t T, int H);
 void embedding_wgrad(const int64_t* sorted, const int64_t* perm, const void* dy, DType tdy,
                      int64_t T, int H, int64_t pad, void* out, DType tout, bool vec,
-                     hipStream_t st);
+                     float* slots, hipStream_t st);
 
 }  // namespace amd

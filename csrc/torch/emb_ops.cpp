@@ -1,4 +1,4 @@
-// Deterministic embedding weight gradient: device sort + one run-sum launch (GPU), or a
+// Deterministic embedding weight gradient: device sort + run-sum launches (GPU), or a
 // sequential scatter in token order (CPU reference path).
 #include "emb_ops.h"
 
@@ -32,9 +32,10 @@ at::Tensor embedding_wgrad_op(at::Tensor idx, at::Tensor dy, int64_t V, int64_t 
   // 8-column vectors: every row start is then 16-byte aligned for 16-bit and fp32 data
   const bool vec = H % 8 == 0 && reinterpret_cast<uintptr_t>(dy2.data_ptr()) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0;
+  at::Tensor slots = at::empty({embedding_wgrad_slots(T, (int)H)}, dy.options().dtype(at::kFloat));
   embedding_wgrad(sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dy2.data_ptr(),
                   dtype_of(dy2), T, (int)H, padding_idx, out.data_ptr(), dtype_of(out),
-                  vec, cur_stream());
+                  vec, slots.data_ptr<float>(), cur_stream());
   return out;
 }
 

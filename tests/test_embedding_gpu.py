@@ -64,3 +64,40 @@ def test_embedding_backward_is_deterministic(H, dtype):
     err = (grads[0].double() - ref).abs().max().item() / ref.abs().max().item()
     assert err <= (1e-6 if dtype == torch.float32 else 2 ** -8), err
     assert grads[0].dtype == dtype and torch.count_nonzero(grads[0][11]) == 0
+
+
+@pytest.mark.parametrize("case", ["token_type", "boundaries", "long_pad"])
+def test_embedding_backward_long_runs_chunked(case):
+    """Runs longer than one 256-position chunk are summed as chunk partials joined in
+    order (BERT's 2-row token-type table: two runs of ~8k tokens): exact vs fp64 to one
+    rounding, bitwise reproducible, including runs that start / end on chunk boundaries
+    and a long padding run."""
+    torch.manual_seed(2)
+    H = 1024
+    if case == "token_type":
+        V, pad = 2, None
+        idx = torch.randint(0, 2, (32, 512), device=dev)
+    elif case == "boundaries":
+        V, pad = 16, None
+        lens = [256, 256, 257, 255, 1, 512, 768, 3, 300, 1]
+        idx = torch.cat([torch.full((n,), i, dtype=torch.long) for i, n in enumerate(lens)])
+        idx = idx[torch.randperm(idx.numel())].to(dev)
+    else:
+        V, pad = 8, 5
+        idx = torch.randint(0, V, (4096,), device=dev)
+        idx[:3000] = 5
+    emb = Embedding(V, H, padding_idx=pad).to(dev).to(torch.bfloat16)
+    dy = torch.randn(*idx.shape, H, device=dev).to(torch.bfloat16)
+    grads = []
+    for _ in range(2):
+        emb.weight.grad = None
+        emb(idx).backward(dy)
+        grads.append(emb.weight.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    ref = torch.zeros(V, H, dtype=torch.float64, device=dev).index_add_(
+        0, idx.reshape(-1), dy.reshape(-1, H).double())
+    if pad is not None:
+        ref[pad] = 0
+        assert torch.count_nonzero(grads[0][pad]) == 0
+    err = (grads[0].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 2 ** -8, err
