@@ -521,6 +521,16 @@ static bool bnbwd_nb2() {
   return e ? e[0] == '1' : true;
 }
 
+// APEX_AMD_CONV64_NB2 = 0 | 1 (read per launch, A/B runs): 64-wide output tiles without
+// the BN-backward epilogue on the 2-deep ring too (48 KB of LDS: 3 workgroups per CU
+// instead of 2, so more workgroups' DMA prologues and epilogues overlap others' K loops
+// on the short-K layer-1 shapes).  ResNet-50 same-box A/B: 10,465 / 10,455 -> 10,540 /
+// 10,530 img/s.
+static bool conv64_nb2() {
+  const char* e = std::getenv("APEX_AMD_CONV64_NB2");
+  return e ? e[0] == '1' : true;
+}
+
 template <int MODE, int EPI = 0>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
@@ -543,7 +553,7 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (EPI == 1 && bnbwd_nb2()) {
+  } else if ((EPI == 1 && bnbwd_nb2()) || (EPI == 0 && conv64_nb2())) {
     // BN-backward epilogue on 64-wide tiles: a 2-deep ring (48 KB of LDS -> 3 workgroups
     // per CU instead of 2), so more K loops run under each workgroup's epilogue reads
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
