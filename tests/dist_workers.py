@@ -21,11 +21,11 @@ def free_port():
     return p
 
 
-def _entry(rank, world, port, fn_name, out, kw):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _entry(rank, world, rdzv, fn_name, out, kw):
+    # file rendezvous: a port picked by free_port() can be taken by another process on a
+    # shared box between the pick and the child's bind (EADDRINUSE seen on a GPU box)
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + rdzv, rank=rank, world_size=world)
     try:
         res = globals()[fn_name](rank, world, **kw)
         torch.save(res, os.path.join(out, "rank%d.pt" % rank))
@@ -35,7 +35,10 @@ def _entry(rank, world, port, fn_name, out, kw):
 
 
 def run(fn_name, world, out, **kw):
-    mp.spawn(_entry, args=(world, free_port(), fn_name, out, kw), nprocs=world, join=True)
+    rdzv = os.path.join(out, "rdzv_%s_%d" % (fn_name, os.getpid()))
+    if os.path.exists(rdzv):
+        os.remove(rdzv)
+    mp.spawn(_entry, args=(world, rdzv, fn_name, out, kw), nprocs=world, join=True)
     return [torch.load(os.path.join(out, "rank%d.pt" % r), weights_only=False)
             for r in range(world)]
 

@@ -20,11 +20,12 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def pg():
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(W.free_port())
+def pg(tmp_path_factory):
+    # file rendezvous (no port to race for on a shared box)
+    rdzv = str(tmp_path_factory.mktemp("pg") / "rdzv")
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    dist.init_process_group("nccl", init_method="file://" + rdzv, rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
     yield
     dist.destroy_process_group()
 
