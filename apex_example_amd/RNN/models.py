@@ -1,3 +1,9 @@
+"""``apex.RNN`` model factories: LSTM / GRU / ReLU / Tanh over the
+MIOpen-backed ``nn`` RNNs, plus the multiplicative LSTM, whose recurrence MIOpen does
+not provide.  The mLSTM computes the input-side projections of every timestep as one
+GEMM per layer ([T*B, in] x [in, 5H]) before the time loop, leaving two small GEMMs
+and the gate pointwise work per step.
+"""
 from __future__ import annotations
 
 import torch
@@ -60,9 +66,23 @@ class mLSTMCell(nn.Module):  # noqa: N801
         self.w_mhh = nn.Linear(hidden_size, hidden_size, bias=False)
 
     def forward(self, x, state):
+        return self.recur(self.w_ih(x), self.w_mih(x), state)
+
+    def input_proj(self, x):
+        """(W_x x + b, W_mx x) for a whole sequence [T, B, in] in one GEMM."""
+        H = self.hidden_size
+        w = torch.cat([self.w_ih.weight, self.w_mih.weight])
+        b = None
+        if self.w_ih.bias is not None:
+            b = torch.cat([self.w_ih.bias, self.w_ih.bias.new_zeros(H)])
+        xa = F.linear(x, w, b)
+        return xa[..., :4 * H], xa[..., 4 * H:]
+
+    def recur(self, xg, xm, state):
+        """One step from the precomputed input projections xg = W_x x + b, xm = W_mx x."""
         h, c = state
-        m = self.w_mih(x) * self.w_mhh(h)
-        i, f, g, o = (self.w_ih(x) + self.w_hh(m)).chunk(4, -1)
+        m = xm * self.w_mhh(h)
+        i, f, g, o = (xg + self.w_hh(m)).chunk(4, -1)
         c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
         h = torch.sigmoid(o) * torch.tanh(c)
         return h, c
@@ -92,9 +112,10 @@ class _MLSTM(nn.Module):
         new_states = []
         for li, cell in enumerate(self.cells):
             h, c = states[li]
+            xg, xm = cell.input_proj(out)
             ys = []
             for t in range(T):
-                h, c = cell(out[t], (h, c))
+                h, c = cell.recur(xg[t], xm[t], (h, c))
                 ys.append(h)
             out = torch.stack(ys)
             if self.dropout and li + 1 < len(self.cells):
