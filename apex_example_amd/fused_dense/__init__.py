@@ -31,6 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from ..ops import _ddp_direct
 from ..ops.conv import _SideWgrad
 
 __all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function", "cast_params_once",
@@ -145,10 +146,15 @@ def _splitk_chunks(T, o, i, in_dtype, out_dtype):
     return S
 
 
-def _wgrad(dy2, x2, dtype):
+_ADDMM_F32 = False  # torch.addmm(out_dtype=fp32, out=) usable (cleared on first failure)
+
+
+def _wgrad(dy2, x2, dtype, out=None):
     """dW = dy2^T x2 written in the parameter's dtype by the GEMM itself (amp O1:
     fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW); split-K over
-    the tokens when the output has too few tiles to fill the GPU."""
+    the tokens when the output has too few tiles to fill the GPU.  ``out``: accumulate
+    into that [o, i]-contiguous tensor (a DDP bucket view, see _direct_slots) and
+    return it - the slab reduction or the GEMM's beta = 1 does the add."""
     if (_DENSE_SPLITK and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
             and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
             and _native.available()):
@@ -159,10 +165,48 @@ def _wgrad(dy2, x2, dtype):
             a = dy2.view(S, T // S, o).transpose(1, 2)
             b = x2.view(S, T // S, i)
             part = torch.bmm(a, b, out_dtype=torch.float32)
-            return _native.require().conv.splitk_reduce(part, dtype)
+            return _native.require().conv.splitk_reduce(part, dtype, out=out)
     if dtype != dy2.dtype and dy2.is_cuda and dtype == torch.float32:
-        return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+        global _ADDMM_F32
+        if out is not None and _ADDMM_F32:
+            # fp32 C += fp16 A @ B in the GEMM (beta = 1), no separate add pass
+            o2 = out.view(dy2.size(1), x2.size(1))
+            try:
+                torch.addmm(o2, dy2.t(), x2, out_dtype=torch.float32, out=o2)
+                return out
+            except (RuntimeError, TypeError):
+                _ADDMM_F32 = False
+        r = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+        return r if out is None else out.add_(r.view_as(out))
+    if out is not None:
+        if out.dtype == dy2.dtype:
+            return out.view(dy2.size(1), x2.size(1)).addmm_(dy2.t(), x2).view_as(out)
+        return out.add_((dy2.t() @ x2).view_as(out))
     return dy2.t() @ x2
+
+
+def _direct_slots(side, weight, w_dtype):
+    """DDP reducer slots when the weight gradient can accumulate straight into the
+    weight's bucket view on the compute stream (ops/_ddp_direct.py: no AccumulateGrad
+    add kernel per weight - GPT-2-medium O1 under DDP ran 96 of them, ~1.4 ms per step,
+    `profiles/gpt2_medium_forced_collectives_r3.md`), else None."""
+    if side is None or side.on or weight is None:
+        return None
+    g = weight.grad
+    if g is None or not g.is_cuda or g.dtype != w_dtype or not g.is_contiguous():
+        return None
+    return _ddp_direct.slots(weight)
+
+
+def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):
+    """The weight gradient for autograd, or None after accumulating it into the DDP
+    bucket view and announcing the parameter to the reducer."""
+    direct = _direct_slots(side, weight, w_dtype)
+    if direct is None:
+        return side.run(lambda: _wgrad(dy2, x2, w_dtype), dy2, *used)
+    _wgrad(dy2, x2, w_dtype, out=weight.grad)
+    _ddp_direct.mark_ready(direct)
+    return None
 
 
 def _bias_grad(g2, dtype):
@@ -240,7 +284,12 @@ def _dense_bwd(ctx, dy, dskip=None):
     if ctx.needs_input_grad[0]:
         dx = _dgrad(dy2, wc, xc.shape, dskip, dy)
     x2 = xc.reshape(-1, xc.size(-1))
-    if ctx.needs_input_grad[1] and need_b:
+    direct = _direct_slots(side, ctx.params[0], ctx.w_dtype) if ctx.needs_input_grad[1] else None
+    if direct is not None:
+        dw = _wgrad_maybe_direct(side, ctx.params[0], ctx.w_dtype, dy2, x2, xc)
+        if need_b:
+            db = _bias_grad(dy2, ctx.bias_dtype)
+    elif ctx.needs_input_grad[1] and need_b:
         dw, db = side.run(lambda: _wgrad_bgrad(dy2, x2, ctx.w_dtype, ctx.bias_dtype), dy2, xc)
     elif ctx.needs_input_grad[1]:
         dw = side.run(lambda: _wgrad(dy2, x2, ctx.w_dtype), dy2, xc)
@@ -359,7 +408,11 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
     need_b2 = ctx.b2_dtype is not None and need[4]
     w1, b1, w2, b2 = ctx.params
     side2 = _SideWgrad(w2, b2, enable=_side_dense(ctx.w_dtypes[1], "ffn")) if need[3] else None
-    if need[3] and need_b2:
+    if need[3] and _direct_slots(side2, w2, ctx.w_dtypes[1]) is not None:
+        dw2 = _wgrad_maybe_direct(side2, w2, ctx.w_dtypes[1], dy2, h)
+        if need_b2:
+            db2 = _bias_grad(dy2, ctx.b2_dtype)
+    elif need[3] and need_b2:
         dw2, db2 = side2.run(lambda: _wgrad_bgrad(dy2, h, ctx.w_dtypes[1], ctx.b2_dtype), dy2, h)
     elif need[3]:
         dw2 = side2.run(lambda: _wgrad(dy2, h, ctx.w_dtypes[1]), dy2, h)
@@ -387,7 +440,7 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
     side1 = _SideWgrad(w1, enable=_side_dense(ctx.w_dtypes[0], "ffn")) if need[1] else None
     dx = _dgrad(dpre, w1c, xc.shape, dskip, dy) if need[0] else None
     x2 = xc.reshape(-1, xc.size(-1))
-    dw1 = side1.run(lambda: _wgrad(dpre, x2, ctx.w_dtypes[0]), dpre, xc) if need[1] else None
+    dw1 = _wgrad_maybe_direct(side1, w1, ctx.w_dtypes[0], dpre, x2, xc) if need[1] else None
     if ctx.b1_dtype is None or not need[2]:
         db1 = None
     return dx, dw1, db1, dw2, db2, None
