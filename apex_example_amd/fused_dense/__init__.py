@@ -250,6 +250,8 @@ def _dense_fwd(ctx, x, weight, bias):
     ctx.bias_dtype = bias.dtype if bias is not None else None
     ctx.w_dtype = weight.dtype
     ctx.params = (weight, bias)  # leaves: side-stream weight gradients check .grad
+    if ctx.needs_input_grad[1]:
+        _ddp_direct.note_use(weight)
     return y.view(*x.shape[:-1], weight.size(0))
 
 
@@ -397,6 +399,7 @@ def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
     ctx.tanh = approximate == "tanh"
     ctx.w_dtypes = (w1.dtype, w2.dtype)
     ctx.params = (w1, b1, w2, b2)
+    _ddp_direct.note_use(*(w for w, k in ((w1, 1), (w2, 3)) if ctx.needs_input_grad[k]))
     return y.view(*x.shape[:-1], w2.size(0))
 
 

@@ -9,6 +9,15 @@ accumulate their final reduction into the view (one rounding) and announce the
 parameter to the reducer on the current stream; autograd gets None for it (the
 reducer's AccumulateGrad hook still fires and consumes the announcement).
 ``APEX_AMD_DDP_DIRECT_GRAD=0`` keeps the autograd path.
+
+An announcement is only sound when that ONE use of the parameter produces its whole
+gradient for the iteration.  So (a) the DDP wrapper excludes parameters listed more than
+once in the module tree (tied weights, ``Reducer.set_no_direct``); (b) the own ops count
+their forward uses of each parameter (``note_use``) and go direct only for a parameter
+used exactly once this iteration (a module called twice takes the autograd path, which
+sums both uses before one AccumulateGrad); (c) the reducer refuses a second announcement
+and, if an autograd gradient of some other use lands on top of an announced one, it
+excludes the parameter from then on and raises if the bucket was already launched.
 """
 from __future__ import annotations
 
@@ -19,23 +28,50 @@ import torch
 _ON = os.environ.get("APEX_AMD_DDP_DIRECT_GRAD", "1") == "1"
 
 
+def note_use(*params):
+    """Count one forward use of each DDP-registered parameter in this iteration (called
+    by the own ops' forwards for the parameters they may later announce)."""
+    if not _ON:
+        return
+    for p in params:
+        slot = getattr(p, "_amd_ddp_slot", None) if p is not None else None
+        if slot is None:
+            continue
+        red = slot[0]()
+        if red is None:
+            continue
+        it = red.iteration()
+        u = getattr(p, "_amd_ddp_uses", None)
+        p._amd_ddp_uses = (it, u[1] + 1) if (u is not None and u[0] == it) else (it, 1)
+
+
+def slot(p):
+    """(reducer, index) when ``p.grad`` is a bucket view its reducer will take an early
+    ready mark for this iteration and ``p`` had exactly one counted forward use, else None."""
+    s = getattr(p, "_amd_ddp_slot", None) if p is not None else None
+    if s is None or p.grad is None:
+        return None
+    red = s[0]()
+    if red is None or not red.async_ready_ok() or not red.direct_ok(s[1]):
+        return None
+    u = getattr(p, "_amd_ddp_uses", None)
+    if u is None or u[1] != 1 or u[0] != red.iteration():
+        return None
+    return red, s[1]
+
+
 def slots(*params):
     """[(reducer, index)] when every param's .grad is a bucket view its reducer will take
-    an early ready mark for this iteration, else None."""
+    an early ready mark for this iteration (``slot``), else None."""
     if not _ON:
         return None
     out = []
     for p in params:
-        if p is None:
+        sl = slot(p)
+        if sl is None:
             return None
-        slot = getattr(p, "_amd_ddp_slot", None)
-        if slot is None or p.grad is None:
-            return None
-        red = slot[0]()
-        if red is None or not red.async_ready_ok():
-            return None
-        out.append((red, slot[1]))
-    if torch.cuda.is_current_stream_capturing():
+        out.append(sl)
+    if params[0].is_cuda and torch.cuda.is_current_stream_capturing():
         return None
     return out
 

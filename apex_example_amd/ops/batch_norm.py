@@ -72,7 +72,24 @@ def _bwd_src(x, xl, mean, invstd, weight, bias, mask, fuse_relu, has_z):
 
 # SyncBN collectives on the compute stream through the dedicated SyncBN group's RCCL
 # communicator (csrc/torch/reducer.cpp syncbn_*_raw); APEX_AMD_SYNCBN_RAW_RCCL=0 keeps the
-# process group's own stream (c10d calls from C++)
+# process group's own stream (c10d calls from C++).
+#
+# Failure detection: the raw calls are invisible to ProcessGroupNCCL's work tracking, so
+# its watchdog never times out a SyncBN collective itself.  A dead or diverged peer is
+# still caught: the raw collective stalls the COMPUTE stream (the host does not block on
+# it), the host goes on to enqueue the step's DDP bucket collectives - c10d works on the
+# DDP communicator, stream-ordered behind the stalled compute stream - and those time out
+# after the process group's timeout (bench.py --pg-timeout, 300 s) and the watchdog aborts
+# the process (TORCH_NCCL_ASYNC_ERROR_HANDLING).  Without DDP in the step (SyncBN alone),
+# set APEX_AMD_SYNCBN_RAW_RCCL=0 to keep every collective under the watchdog.
+#
+# Two communicators in flight (SyncBN on the compute stream, DDP buckets on their own
+# high-priority stream) cannot deadlock each other: each communicator's collectives are
+# issued in the same order on every rank (SyncBN: layer order of one program; DDP: the
+# rank-0-synchronised bucket order), the two never wait on each other's kernels, and an
+# RCCL collective occupies one workgroup per channel (<= RCCL's channel count, see
+# bench.py --rccl-channels), so both kernels fit on the 256 CUs at once whatever their
+# relative order on a rank; the compute kernels around them are finite, never spinning.
 _RAW_RCCL = os.environ.get("APEX_AMD_SYNCBN_RAW_RCCL", "1") == "1"
 _COMMS = {}
 
@@ -103,8 +120,61 @@ def _raw_comm_rank(pg):
     return ptr, rank
 
 
+# SyncBN collective timing (bench.py's timing steps at N > 1 / --force-collectives): HIP
+# events on the compute stream around every SyncBN collective, so the record shows what
+# the 2 latency-bound collectives per BN layer cost the step (including waiting for the
+# slowest peer).  None = off; else a list of (kind, start event, end event).
+_SBN_EVENTS = None
+
+
+def syncbn_timing(on=True):
+    """Start (clear) or stop recording SyncBN collective timing events."""
+    global _SBN_EVENTS
+    _SBN_EVENTS = [] if on else None
+
+
+def syncbn_timing_result():
+    """{"calls", "ms", "allgather_ms", "allreduce_ms"} summed over the recorded
+    collectives (synchronizes on the last event); None if nothing was recorded."""
+    ev = _SBN_EVENTS
+    if not ev:
+        return None
+    ev[-1][2].synchronize()
+    out = {"calls": len(ev), "ms": 0.0, "allgather_ms": 0.0, "allreduce_ms": 0.0}
+    for kind, a, b in ev:
+        ms = a.elapsed_time(b)
+        out["ms"] += ms
+        out[kind + "_ms"] += ms
+    return out
+
+
+class _SbnTimer:
+    def __init__(self, kind):
+        self.kind = kind
+
+    def __enter__(self):
+        if _SBN_EVENTS is not None:
+            self.a = torch.cuda.Event(enable_timing=True)
+            self.a.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _SBN_EVENTS is not None and hasattr(self, "a"):
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            _SBN_EVENTS.append((self.kind, self.a, b))
+        return False
+
+
 def _allreduce(t, pg):
     """In-place SUM all-reduce of a SyncBN packed buffer."""
+    if t.is_cuda and _SBN_EVENTS is not None:
+        with _SbnTimer("allreduce"):
+            return _allreduce_body(t, pg)
+    return _allreduce_body(t, pg)
+
+
+def _allreduce_body(t, pg):
     if dist.get_backend(pg) == "nccl":
         comm = _raw_comm(pg)
         if comm:
@@ -113,6 +183,21 @@ def _allreduce(t, pg):
             _native.require().reducer.syncbn_allreduce(t, pg)
     else:
         dist.all_reduce(t, group=pg)
+
+
+# calls that gathered SyncBN statistics through a rank slot of the gather buffer
+# (tests/test_ddp_gpu.py checks the rank > 0 slot arithmetic ran)
+SLOT_GATHER_CALLS = [0]
+
+
+def _gather_slot(C, world, rank, device):
+    """The [world * (2C + 1)] gather destination and this rank's [2C + 1] slot of it
+    (mean | var | count, the layout of local_stats_packed / slab_packed_stats)."""
+    n = 2 * C + 1
+    assert 0 <= rank < world, (rank, world)
+    gathered = torch.empty(world * n, dtype=torch.float32, device=device)
+    SLOT_GATHER_CALLS[0] += 1
+    return gathered, gathered[rank * n:(rank + 1) * n]
 
 
 def bn_src_of(x):
@@ -153,6 +238,8 @@ class BatchNormFunction(torch.autograd.Function):
                 slab=None, slab_shift=None):
         C = _C()
         ctx.params = (weight, bias)   # the Parameter objects (DDP bucket slots live on them)
+        if ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            _ddp_direct.note_use(weight, bias)
         orig_shape = x.shape
         xl = _to_logical(x, shape_channel_last)
         zl = _to_logical(z, shape_channel_last) if z is not None else None
@@ -200,14 +287,13 @@ class BatchNormFunction(torch.autograd.Function):
             # num_batches_tracked, 1/global count) -> apply.  No host sync, no cat.
             pg = process_group if process_group is not None else dist.group.WORLD
             nccl = dist.get_backend(pg) == "nccl"
-            comm, rank = _raw_comm_rank(pg) if nccl else (0, -1)
+            comm, rank = _raw_comm_rank(pg) if nccl else (0, dist.get_rank(pg))
             gathered = slot = None
-            if comm:
+            if comm or not nccl:
                 # the stats kernels write straight into this rank's slot of the gather
-                # destination: the all_gather runs in place (no send-buffer copy)
-                n = 2 * xl.size(1) + 1
-                gathered = torch.empty(world * n, dtype=torch.float32, device=x.device)
-                slot = gathered[rank * n:(rank + 1) * n]
+                # destination: the RCCL all_gather runs in place (no send-buffer copy).
+                # gloo (the multi-process GPU tests) takes the same slot arithmetic.
+                gathered, slot = _gather_slot(xl.size(1), world, rank, x.device)
             packed = (C.slab_packed_stats(slab, count, slab_shift, out=slot) if slab is not None
                       else C.local_stats_packed(xl, out=slot))
             if nccl:
@@ -215,18 +301,19 @@ class BatchNormFunction(torch.autograd.Function):
                 # c10d wrapper cost ~20 us of host time per layer; on the compute stream
                 # through the group's communicator when it is the dedicated SyncBN group
                 R = _native.require().reducer
-                if comm:
-                    mean_g, invstd, inv_total = R.syncbn_allgather_combine_raw(
-                        packed, comm, world, float(eps), float(momentum), running_mean,
-                        running_var, num_batches_tracked, gathered=gathered, rank=rank)
-                else:
-                    mean_g, invstd, inv_total = R.syncbn_allgather_combine(
-                        packed, pg, float(eps), float(momentum), running_mean, running_var,
-                        num_batches_tracked)
+                with _SbnTimer("allgather"):
+                    if comm:
+                        mean_g, invstd, inv_total = R.syncbn_allgather_combine_raw(
+                            packed, comm, world, float(eps), float(momentum), running_mean,
+                            running_var, num_batches_tracked, gathered=gathered, rank=rank)
+                    else:
+                        mean_g, invstd, inv_total = R.syncbn_allgather_combine(
+                            packed, pg, float(eps), float(momentum), running_mean,
+                            running_var, num_batches_tracked)
             else:  # gloo with GPU tensors (tests): list form into views of `gathered`
-                gathered = torch.empty(world * packed.numel(), dtype=packed.dtype,
-                                       device=x.device)
-                dist.all_gather(list(gathered.chunk(world)), packed, group=pg)
+                # (send a copy: gloo does not take a send buffer inside the output)
+                with _SbnTimer("allgather"):
+                    dist.all_gather(list(gathered.chunk(world)), packed.clone(), group=pg)
                 mean_g, invstd, inv_total = C.combine_stats_sync(
                     gathered.view(world, -1), float(eps), float(momentum), running_mean,
                     running_var, num_batches_tracked)
@@ -289,8 +376,11 @@ class BatchNormFunction(torch.autograd.Function):
         res = src.result if src is not None else None
         if res is not None:
             src.result = None
-        if res is not None and res[0] == dyl.data_ptr() and dyl.is_contiguous(
-                memory_format=torch.channels_last):
+        # the epilogue's g, untouched since: an in-place accumulation by another consumer
+        # of this BN's output (autograd's InputBuffer adds into g) bumps its version, and
+        # the slab sums would then miss that contribution -> the reduce pass below
+        if res is not None and res[0] == dyl.data_ptr() and res[2] == dyl._version and (
+                dyl.is_contiguous(memory_format=torch.channels_last)):
             # the consuming conv's dgrad epilogue already applied the ReLU mask (dy is
             # g) and summed (g, g*(x-mean)) per tile: no reduction pass, no dz store
             FUSED_BWD_CALLS[0] += 1

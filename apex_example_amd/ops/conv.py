@@ -45,13 +45,7 @@ _LOCK = threading.Lock()
 def _ddp_slot(p):
     """(reducer, index) when ``p.grad`` is a DDP bucket view whose reducer can take a
     side-stream gradient this iteration (parallel/distributed.py), else None."""
-    slot = getattr(p, "_amd_ddp_slot", None)
-    if slot is None:
-        return None
-    red = slot[0]()
-    if red is None or not red.async_ready_ok() or p.grad is None:
-        return None
-    return red, slot[1]
+    return _ddp_direct.slot(p)
 
 
 def _side_mode(params):
@@ -352,7 +346,7 @@ def _dgrad_bn(dy, wprep, add, src):
     g, slab = _native.require().conv.conv_fwd_bnbwd(
         dy, wprep, add, src.x, src.mask, src.mean, src.invstd, src.weight, src.bias,
         src.relu_mode)
-    src.result = (g.data_ptr(), slab)
+    src.result = (g.data_ptr(), slab, g._version)
     return g
 
 
@@ -361,6 +355,8 @@ class Conv1x1GemmFunction(torch.autograd.Function):
     def forward(ctx, x, weight, bn=None, src=None):
         ctx.save_for_backward(x, weight)
         ctx.src = src
+        if ctx.needs_input_grad[1]:
+            _ddp_direct.note_use(weight)
         n, ci, h, w = x.shape
         if ctx.needs_input_grad[0] and weight.dtype == torch.bfloat16 and (
                 src is not None or _own_1x1(x.dtype, weight.shape[0], ci, n * h * w)):
@@ -403,6 +399,8 @@ class Conv1x1SkipFunction(torch.autograd.Function):
     def forward(ctx, x, weight, bn=None, src=None):
         ctx.save_for_backward(x, weight)
         ctx.src = src
+        if ctx.needs_input_grad[1]:
+            _ddp_direct.note_use(weight)
         if src is not None and ctx.needs_input_grad[0] and weight.dtype == torch.bfloat16:
             _register_prep(weight)
         return _conv1x1_fwd(x, weight, bn), x.view_as(x)
@@ -458,6 +456,8 @@ class Conv1x1Stride2Function(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bn=None):
         ctx.save_for_backward(x, weight)
+        if ctx.needs_input_grad[1]:
+            _ddp_direct.note_use(weight)
         if ctx.needs_input_grad[0]:
             _register_prep(weight)
         return _conv_fwd(x, weight, 2, bn)
@@ -588,6 +588,8 @@ class Conv3x3Function(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         ctx.src = src if stride == 1 else None
+        if ctx.needs_input_grad[1]:
+            _ddp_direct.note_use(weight)
         if ctx.needs_input_grad[0] and _USE_ROT_KERNEL:
             _register_prep(weight)
         return _conv_fwd(x, weight, stride, bn)

@@ -33,6 +33,10 @@ _MODE = os.environ.get("APEX_AMD_EMB_BWD", "det")
 _ENABLED = os.environ.get("APEX_AMD_SYNCFREE_EMB", "1") == "1" and _MODE != "stock"
 
 
+# dtypes the deterministic kernel reads / writes (anything else: the scatter below)
+_DET_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
+
+
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, weight, padding_idx):
@@ -46,12 +50,13 @@ class _EmbeddingFn(torch.autograd.Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         V, H = ctx.shape
-        if _MODE == "det":
+        if _MODE == "det" and dy.dtype in _DET_DTYPES and ctx.wdtype in _DET_DTYPES:
             pad = -1 if ctx.padding_idx is None else int(ctx.padding_idx) % V
             return None, _native.require().emb.wgrad(idx, dy, V, pad, ctx.wdtype), None
         flat = idx.reshape(-1)
-        g = torch.zeros((V, H), dtype=torch.float32, device=dy.device)
-        g.index_add_(0, flat, dy.reshape(-1, H).float())
+        acc = torch.promote_types(dy.dtype, torch.float32)  # fp64 stays fp64
+        g = torch.zeros((V, H), dtype=acc, device=dy.device)
+        g.index_add_(0, flat, dy.reshape(-1, H).to(acc))
         if ctx.padding_idx is not None:
             g[ctx.padding_idx].zero_()
         return None, g.to(ctx.wdtype), None

@@ -32,10 +32,20 @@ they never queue behind (or interleave with) collectives other code issues on
 the default group - SyncBatchNorm uses its own communicator as well
 (``parallel.sync_batchnorm``).
 
-Precision: bf16 buckets are all-reduced in fp32 by default (RCCL rounds the
-running sum to the wire dtype at every ring hop; with an 8-bit mantissa that
-costs ~3 bits over 8 ranks) - ``allreduce_always_fp32=None`` means "fp32 for
-bf16 buckets, native for fp16" (Apex's fp16 behaviour); True / False force it.
+Precision: bf16 buckets are reduced in fp32 by default (RCCL rounds the running
+sum to the wire dtype at every ring hop; with an 8-bit mantissa that costs ~3 bits
+over 8 ranks) - ``allreduce_always_fp32=None`` means "fp32 sums for bf16 buckets,
+native for fp16" (Apex's fp16 behaviour); True / False force an fp32 / native
+all-reduce for every 16-bit bucket.  How the fp32 sum of a bf16 bucket travels
+(``bf16_wire``, env ``APEX_AMD_DDP_BF16_WIRE``):
+
+* ``"rsag"`` (default): fp32 reduce-scatter + in-place bf16 all-gather - each rank's
+  shard is summed in fp32 and rounded to bf16 once, exactly the fp32 all-reduce's
+  values, at (n-1)/n x 6 bytes per element on the wire instead of 2 (n-1)/n x 4;
+* ``"fp32"``: one fp32 all-reduce of an up-cast copy (8 bytes per element);
+* ``"native"``: bf16 all-reduce (4 bytes per element, rounded at every hop).
+
+docs/DDP_TUNING.md records the measurements behind the default.
 """
 from __future__ import annotations
 
@@ -168,7 +178,7 @@ class DistributedDataParallel(Module):
                  allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
                  process_group=None, allow_unused=False, bucket_align=64, use_avg_op=None,
-                 high_priority_streams=True, force_collectives=False):
+                 high_priority_streams=True, force_collectives=False, bf16_wire=None):
         super().__init__()
         if not dist.is_initialized():
             raise RuntimeError("DistributedDataParallel requires torch.distributed to be "
@@ -203,6 +213,10 @@ class DistributedDataParallel(Module):
             use_avg_op = self.backend == "nccl"
         self.use_avg_op = bool(use_avg_op)
         self.force_collectives = bool(force_collectives)
+        import os
+        self.bf16_wire = bf16_wire or os.environ.get("APEX_AMD_DDP_BF16_WIRE", "rsag")
+        if self.bf16_wire not in ("rsag", "fp32", "native"):
+            raise ValueError("bf16_wire must be 'rsag', 'fp32' or 'native'")
         self._trigger_params = allreduce_trigger_params
         self.custom_allreduce_triggers = allreduce_trigger_params is not None
 
@@ -264,17 +278,35 @@ class DistributedDataParallel(Module):
         dom = max(set(dtypes), key=dtypes.count)
         mode = self._fp32_mode()
         wire = 4 if (dom == torch.float32 or mode == 1
-                     or (mode == 2 and dom == torch.bfloat16)) else torch.finfo(dom).bits // 8
+                     or (mode in (2, 3) and dom == torch.bfloat16)) else torch.finfo(dom).bits // 8
         return max(1, XGMI_BUCKET_BYTES // wire)
 
     def _fp32_mode(self):
+        """Reducer fp32 mode: 0 native, 1 every 16-bit bucket as an fp32 all-reduce,
+        2 bf16 buckets as an fp32 all-reduce, 3 bf16 buckets as an fp32 reduce-scatter
+        + bf16 all-gather (fp16 / fp32 buckets native in 2 and 3)."""
         if self.allreduce_always_fp32 is None:
             import os
             env = os.environ.get("APEX_AMD_DDP_FP32")  # A/B override of the auto rule
-            if env in ("0", "1"):
+            if env in ("0", "1", "2", "3"):
                 return int(env)
-            return 2  # bf16 buckets in fp32, fp16 / fp32 native
+            return {"rsag": 3, "fp32": 2, "native": 0}[self.bf16_wire]
         return 1 if self.allreduce_always_fp32 else 0
+
+    def wire_format(self):
+        """How each bucket dtype travels: {dtype name: 'fp32 all-reduce' | ...}."""
+        mode = self._fp32_mode()
+        out = {}
+        for p in self.active_params:
+            d = p.dtype
+            if d in (torch.bfloat16, torch.float16) and (
+                    mode == 1 or (mode == 2 and d == torch.bfloat16)):
+                out[str(d)] = "fp32 all-reduce"
+            elif d == torch.bfloat16 and mode == 3:
+                out[str(d)] = "fp32 reduce-scatter + bf16 all-gather"
+            else:
+                out[str(d)] = "%s all-reduce" % str(d).replace("torch.", "")
+        return out
 
     def _collect_params(self):
         seen = set()
@@ -302,6 +334,14 @@ class DistributedDataParallel(Module):
         self.reducer.set_prof(bool(self.prof))
         if self._bucket_pgs:
             self.reducer.set_bucket_process_groups(self._bucket_pgs)
+        # parameters listed more than once in the module tree (tied weights) get their
+        # gradient from several uses: never announced early (ops/_ddp_direct.py)
+        uses = {}
+        for _, p in self.module.named_parameters(remove_duplicate=False):
+            uses[id(p)] = uses.get(id(p), 0) + 1
+        shared = [i for i, p in enumerate(self.active_params) if uses.get(id(p), 0) > 1]
+        if shared:
+            self.reducer.set_no_direct(shared)
         import weakref
         ref = weakref.ref(self.reducer)
         for i, p in enumerate(self.active_params):

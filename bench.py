@@ -101,6 +101,16 @@ def parse():
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="MIOpen find (solver search) instead of immediate mode")
     ap.add_argument("--opt-step-iters", type=int, default=20)
+    ap.add_argument("--pg-timeout", type=int, default=300,
+                    help="process-group timeout, seconds: a collective hang at N ranks fails "
+                         "within this instead of the 30-minute default")
+    ap.add_argument("--rccl-channels", type=int, default=0,
+                    help="cap RCCL at this many channels (NCCL_MIN/MAX_NCHANNELS; one workgroup "
+                         "per channel) so bucket all-reduces leave the backward kernels their CUs; "
+                         "0 = RCCL's own choice")
+    ap.add_argument("--ddp-bf16-wire", choices=["rsag", "fp32", "native"], default=None,
+                    help="how a bf16 DDP bucket travels: fp32 reduce-scatter + bf16 all-gather "
+                         "(default), fp32 all-reduce, or native bf16 all-reduce")
     ap.add_argument("--bucket-timing-steps", type=int, default=5,
                     help="N > 1: extra untimed steps with per-bucket DDP timing (0 = off)")
     ap.add_argument("--json-out", default=None)
@@ -216,7 +226,8 @@ def build_resnet(args, device, world):
                                     verbosity=0)
         if multi:
             model = DistributedDataParallel(model, message_size=args.message_size,
-                                            force_collectives=args.force_collectives)
+                                            force_collectives=args.force_collectives,
+                                            bf16_wire=args.ddp_bf16_wire)
             w.ddp = model
 
         def step(b):
@@ -358,7 +369,8 @@ def build_bert(args, device, world):
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
         if world > 1 or args.force_collectives:
             model = DistributedDataParallel(model, message_size=args.message_size,
-                                            force_collectives=args.force_collectives)
+                                            force_collectives=args.force_collectives,
+                                            bf16_wire=args.ddp_bf16_wire)
             w.ddp = model
 
         def step(b):
@@ -424,7 +436,8 @@ def build_gpt2(args, device, world):
         model, opt = amp.initialize(model, opt, opt_level=opt_level, half_dtype=half, verbosity=0)
         if world > 1 or args.force_collectives:
             model = DistributedDataParallel(model, message_size=args.message_size,
-                                            force_collectives=args.force_collectives)
+                                            force_collectives=args.force_collectives,
+                                            bf16_wire=args.ddp_bf16_wire)
             w.ddp = model
 
         def step(b):
@@ -465,16 +478,41 @@ def build_gpt2(args, device, world):
     return w
 
 
+def _bucket_comm(ddp, b, pg):
+    """One bucket's collective(s) in the DDP's wire format (comm-only timing)."""
+    mode = ddp._fp32_mode()
+    if b.dtype == torch.bfloat16 and mode == 3:
+        cb = b.float()
+        n = dist.get_world_size(pg)
+        shard = torch.empty(cb.numel() // n, dtype=torch.float32, device=cb.device)
+        dist.reduce_scatter_tensor(shard, cb, group=pg)
+        mine = b.view(n, -1)[dist.get_rank(pg)]
+        mine.copy_(shard)
+        dist.all_gather_into_tensor(b, mine, group=pg)
+        return
+    up = b.dtype != torch.float32 and (mode == 1 or (mode == 2 and b.dtype == torch.bfloat16))
+    dist.all_reduce(b.float() if up else b, group=pg)
+
+
 def ddp_timing(ddp, step, batch, steps, device):
     """Per-bucket DDP timing over a few extra (untimed) steps: when each bucket's
-    all-reduce was launched during backward, the exposed post-backward tail
-    (end of backward -> every collective joined), and the same buckets
-    all-reduced back to back with nothing else running (the comm-only cost the
-    overlap has to hide).  Max over ranks."""
+    collective was launched during backward, the exposed post-backward tail
+    (end of backward -> every collective joined), the same buckets reduced back to
+    back with nothing else running (the comm-only cost the overlap has to hide), and
+    what the SyncBN collectives cost the compute stream.  Max over ranks."""
+    from apex_example_amd.ops import batch_norm as bnmod
+
     ddp.enable_bucket_timing(True)
     tails, bwd, launches = [], [], None
+    sbn_ms, sbn_calls = [], []
     for _ in range(steps):
+        bnmod.syncbn_timing(True)
         step(batch)
+        sb = bnmod.syncbn_timing_result()
+        bnmod.syncbn_timing(False)
+        if sb is not None:
+            sbn_ms.append(sb["ms"])
+            sbn_calls.append(sb["calls"])
         t = ddp.bucket_timing()
         if t is None:
             continue
@@ -494,28 +532,36 @@ def ddp_timing(ddp, step, batch, steps, device):
         if i == 1:
             e0.record()
         for b in bufs:
-            cb = b.float() if (b.dtype == torch.bfloat16 and ddp._fp32_mode() == 2) else b
-            dist.all_reduce(cb, group=pg)
+            _bucket_comm(ddp, b, pg)
     e1.record()
     torch.cuda.synchronize()
     comm_ms = e0.elapsed_time(e1) / reps
     ddp.zero_grad_buckets()  # the buckets above were summed, not averaged
-    v = torch.tensor([sum(tails) / len(tails), sum(bwd) / len(bwd), comm_ms],
+    sbn = sum(sbn_ms) / len(sbn_ms) if sbn_ms else 0.0
+    v = torch.tensor([sum(tails) / len(tails), sum(bwd) / len(bwd), comm_ms, sbn],
                      dtype=torch.float64, device=device)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
-    tail, bw, comm = [float(x) for x in v.tolist()]
-    return {
+    tail, bw, comm, sbn = [float(x) for x in v.tolist()]
+    rec = {
         "buckets": len(numels),
         "bucket_mb": [round(n * bufs[i].element_size() / 2**20, 2) for i, n in enumerate(numels)],
         "message_size": ddp.message_size,
-        "allreduce_fp32_accumulate_bf16": ddp._fp32_mode() == 2,
+        "wire": ddp.wire_format(),
+        "allreduce_fp32_accumulate_bf16": ddp._fp32_mode() in (2, 3),
         "high_priority_streams": ddp.high_priority_streams,
+        "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS", "rccl default"),
         "backward_ms": round(bw, 3),
         "exposed_tail_ms": round(tail, 3),
         "comm_only_ms": round(comm, 3),
         "launch_ms": [round(x, 3) for x in launches],
         "timing_steps": len(tails),
     }
+    if sbn_ms:
+        # HIP-event time of the SyncBN all_gather (+ combine) / all_reduce calls on the
+        # compute stream per step, including waiting for the slowest peer
+        rec["syncbn_ms_per_step"] = round(sbn, 3)
+        rec["syncbn_calls"] = int(max(sbn_calls))
+    return rec
 
 
 def main():
@@ -526,13 +572,19 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
-    rank, world, device = init_distributed()
+    if args.rccl_channels > 0:
+        # read by RCCL when a communicator is created (before any process group exists)
+        os.environ["NCCL_MIN_NCHANNELS"] = str(args.rccl_channels)
+        os.environ["NCCL_MAX_NCHANNELS"] = str(args.rccl_channels)
+    rank, world, device = init_distributed(timeout_s=args.pg_timeout)
     if args.force_collectives and world == 1 and args.impl == "amd":
         # a 1-rank process group (RCCL on the GPU) for the forced collectives
+        import datetime
         os.environ["MASTER_PORT"] = str(_free_port())
         kw = {"device_id": device} if device.type == "cuda" else {}
         dist.init_process_group("nccl" if device.type == "cuda" else "gloo", rank=0,
-                                world_size=1, **kw)
+                                world_size=1, timeout=datetime.timedelta(seconds=args.pg_timeout),
+                                **kw)
     if world != args.gpus:
         print("bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s); refusing to "
               "report a number for the wrong world size" % (args.gpus, world,
@@ -669,6 +721,10 @@ def main():
                                             or args.image_size != 224):
         base = None
     w.config["deterministic"] = bool(args.deterministic)
+    if ddp is not None:
+        w.config["ddp_wire"] = ddp.wire_format()
+        w.config["rccl_channels"] = args.rccl_channels or "rccl default"
+        w.config["pg_timeout_s"] = args.pg_timeout
     w.config["gemm_tuning"] = (os.path.relpath(gemm_table, ROOT) if gemm_table else
                                "env" if os.environ.get("PYTORCH_TUNABLEOP_ENABLED") else None)
     rec = {

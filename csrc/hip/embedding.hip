@@ -15,6 +15,8 @@
 //
 // Lanes own 8 consecutive columns (one 16-byte load of a 16-bit dY row chunk); a
 // run's rows are read 4 at a time so several loads are in flight per lane.
+#include <cstdlib>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -170,7 +172,8 @@ void dispatch_t(DType t, F&& f) {
   switch (t) {
     case DType::F32: f(float{}); break;
     case DType::F16: f(half_t{}); break;
-    default: f(bf16_t{}); break;
+    case DType::BF16: f(bf16_t{}); break;
+    default: abort();  // callers (csrc/torch/emb_ops.cpp) admit fp32 / fp16 / bf16 only
   }
 }
 

@@ -23,6 +23,12 @@ at::Tensor embedding_wgrad_op(at::Tensor idx, at::Tensor dy, int64_t V, int64_t 
     return out.copy_(acc);
   }
   TORCH_CHECK(flat.is_cuda(), "embedding_wgrad: ids must be on the gradient's device");
+  auto kdt = [](c10::ScalarType t) {
+    return t == at::kFloat || t == at::kHalf || t == at::kBFloat16;
+  };
+  TORCH_CHECK(kdt(dy.scalar_type()) && kdt(out_dtype),
+              "embedding_wgrad: fp32 / fp16 / bf16 gradients only (got ", dy.scalar_type(),
+              " -> ", out_dtype, ")");
   TORCH_CHECK(H < ((int64_t)1 << 31), "embedding_wgrad: hidden size too large");
   if (T == 0) return out;
   at::Tensor sorted, perm;

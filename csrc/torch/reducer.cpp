@@ -75,6 +75,8 @@ struct Bucket {
   bool launched = false;
   c10::intrusive_ptr<c10d::Work> work;
   std::vector<hipEvent_t> waits;  // side-stream gradient events this launch must wait on
+  bool split = false;  // reduced as fp32 reduce-scatter + 16-bit all-gather (fp32 mode 3)
+  at::Tensor shard;    // that reduce-scatter's fp32 output (kept until the join)
 };
 
 struct RangeGuard {  // roctx range when enabled
@@ -110,6 +112,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     build_layout(order);
     seen_.assign(params_.size(), 0);
     async_marked_.assign(params_.size(), 0);
+    no_direct_.assign(params_.size(), 0);
   }
 
   ~Reducer() {
@@ -134,8 +137,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       const int64_t idx = (int64_t)i;
       auto key = acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
           [weak, idx](const torch::autograd::variable_list& outputs,
-                      const torch::autograd::variable_list&) {
-            if (auto self = weak.lock()) self->mark_ready(idx);
+                      const torch::autograd::variable_list& inputs) {
+            if (auto self = weak.lock())
+              self->mark_ready_hook(idx, !inputs.empty() && inputs[0].defined());
             return outputs;
           }));
       accs_.push_back(acc);
@@ -151,6 +155,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   // ---- hook path (autograd engine thread) ---------------------------------
   void mark_ready(int64_t i) { mark_ready_impl(i, nullptr); }
+  // the AccumulateGrad post-hook; `had_grad`: autograd accumulated a gradient into the
+  // parameter's .grad (bucket view) in this call
+  void mark_ready_hook(int64_t i, bool had_grad) {
+    mark_ready_impl(i, nullptr, false, true, had_grad);
+  }
 
   // A gradient already accumulated into its bucket view by work on `stream`
   // (side-stream weight gradients): ready once that stream reaches this point.
@@ -169,15 +178,50 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   // into the bucket view itself and calls mark_ready_on_stream.
   bool async_ready_ok() const { return enabled_ && !refresh_ && !delay_ && comm_active(); }
 
+  // Direct / side-stream announcements are only sound for a parameter whose ONE use per
+  // iteration produces its whole gradient.  Parameters the Python wrapper found shared
+  // (tied weights: listed more than once in the module tree) are excluded from the
+  // start; a parameter that turns out to receive an autograd gradient on top of an
+  // announced one (a functional use outside the module tree) is excluded from then on.
+  void set_no_direct(const std::vector<int64_t>& idx) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int64_t i : idx) {
+      TORCH_CHECK(i >= 0 && i < (int64_t)params_.size(), "set_no_direct: bad index");
+      no_direct_[(size_t)i] = 1;
+    }
+  }
+  bool direct_ok(int64_t i) const {
+    return i >= 0 && i < (int64_t)no_direct_.size() && !no_direct_[(size_t)i];
+  }
+  // iterations completed (forward-use counting in ops/_ddp_direct.py keys on it)
+  int64_t iteration() const { return iteration_; }
+
   void mark_ready_impl(int64_t i, hipStream_t side, bool announced = false,
-                       bool with_event = true) {
+                       bool with_event = true, bool had_grad = false) {
     std::lock_guard<std::mutex> g(mu_);
     if (announced) {
+      TORCH_CHECK(!async_marked_[(size_t)i] && !seen_[(size_t)i],
+                  "DistributedDataParallel: parameter ", i,
+                  " was announced twice in one backward pass (a module used more than once "
+                  "per iteration on the direct-gradient path)");
       async_marked_[(size_t)i] = 1;
     } else if (async_marked_[(size_t)i]) {
       // the AccumulateGrad post-hook of a gradient that was announced from the side
       // stream (the Function returned None for it; the hook still runs): consumed
       async_marked_[(size_t)i] = 0;
+      if (had_grad) {
+        // another use of the parameter accumulated an autograd gradient into the same
+        // bucket view: correct only while its bucket has not been handed to the
+        // collective yet.  Never announce this parameter again.
+        no_direct_[(size_t)i] = 1;
+        const Bucket& b = buckets_[(size_t)bucket_of_[(size_t)i]];
+        TORCH_CHECK(!enabled_ || refresh_ || delay_ || !b.launched,
+                    "DistributedDataParallel: parameter ", i,
+                    " received an autograd gradient after its directly accumulated one was "
+                    "already being all-reduced (a parameter shared between an own-kernel op "
+                    "and another op); it uses the autograd path from the next iteration on, "
+                    "or set APEX_AMD_DDP_DIRECT_GRAD=0");
+      }
       return;
     }
     attach_view(i);
@@ -380,7 +424,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     for (size_t b = 0; b < nb.size(); ++b) {
       Bucket& B = nb[b];
       const at::Tensor& p0 = params_[(size_t)B.params[0]];
-      int64_t padded = (B.numel + align_ - 1) / align_ * align_;
+      // padded to align_ * world: the reduce-scatter / all-gather form of fp32 mode 3
+      // cuts the flat buffer into world equal shards
+      const int64_t unit = align_ * (int64_t)world_;
+      int64_t padded = (B.numel + unit - 1) / unit * unit;
       B.flat = at::zeros({padded}, p0.options().dtype(B.dtype));
       for (size_t k = 0; k < B.params.size(); ++k) {
         int64_t i = B.params[k];
@@ -474,7 +521,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     if (!comm_active()) return;
     if (timing_ && !refresh_ && !delay_) timing_record(ev_launch_[(size_t)bi]);
     RangeGuard rg(prof_, "apex_amd::allreduce_bucket " + std::to_string(bi));
-    if (!B.waits.empty()) {
+    if (!B.waits.empty() || (split_mode(B) && params_[0].is_cuda())) {
       // launch stream = compute stream's work so far + every side-stream gradient
       // of this bucket; the collective (and the fp32 up-cast) run behind it
       if (!launch_stream_)
@@ -499,9 +546,45 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     launch_body(B, bi);
   }
 
+  // fp32 mode 3: a bf16 bucket is reduced as an fp32 reduce-scatter (each rank's shard
+  // summed in fp32 over the ring, rounded to bf16 ONCE) followed by an in-place bf16
+  // all-gather: the same values as the fp32 all-reduce of mode 2 at 6 instead of 8 wire
+  // bytes per element ((n-1)/n x (4 + 2) vs 2 (n-1)/n x 4).
+  bool split_mode(const Bucket& B) const { return fp32_mode_ == 3 && B.dtype == at::kBFloat16; }
+
+  void launch_split(Bucket& B, int64_t bi) {
+    // runs on the launch stream (launch()): the compute stream never waits for the
+    // reduce-scatter; the fp32 -> bf16 shard conversion sits between the collectives
+    auto& pg = (bucket_pgs_.empty()) ? pg_ : bucket_pgs_[(size_t)bi % bucket_pgs_.size()];
+    const int64_t P = B.flat.numel();
+    TORCH_CHECK(P % world_ == 0, "reducer: bucket not padded to the world size");
+    const int64_t sh = P / world_;
+    const bool avg = use_avg_ && average_ && predivide_ == 1.0;
+    B.comm = B.flat.to(at::kFloat);
+    B.shard = at::empty({sh}, B.comm.options());
+    c10d::ReduceScatterOptions ro;
+    ro.reduceOp = avg ? c10d::ReduceOp(c10d::ReduceOp::AVG) : c10d::ReduceOp(c10d::ReduceOp::SUM);
+    {
+      RECORD_FUNCTION("apex_amd::ddp_reduce_scatter_bucket", std::vector<c10::IValue>({B.comm}));
+      pg->_reduce_scatter_base(B.shard, B.comm, ro)->wait();  // this stream waits, not the host
+    }
+    double factor = 1.0;
+    if (!avg && average_) factor = predivide_ / (double)world_;
+    if (factor != 1.0) B.shard.mul_(factor);
+    at::Tensor mine = B.flat.narrow(0, (int64_t)rank_ * sh, sh);
+    mine.copy_(B.shard);  // the single rounding to bf16
+    RECORD_FUNCTION("apex_amd::ddp_all_gather_bucket", std::vector<c10::IValue>({B.flat}));
+    B.work = pg->_allgather_base(B.flat, mine);  // in place: rank r's shard is its slot
+    B.split = true;
+  }
+
   void launch_body(Bucket& B, int64_t bi) {
     c10::NoGradGuard ng;
     if (predivide_ != 1.0) B.flat.mul_(1.0 / predivide_);
+    if (split_mode(B)) {
+      launch_split(B, bi);
+      return;
+    }
     // fp32 accumulation: 1 = every 16-bit bucket (apex allreduce_always_fp32),
     // 2 = bf16 buckets only (8-bit mantissa: summing 8 ranks in bf16 rounds at
     // every ring hop).  The fp32 copy is a transient caching-allocator block
@@ -527,6 +610,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     if (!B.launched || !comm_active()) return;
     if (B.work) B.work->wait();
     c10::NoGradGuard ng;
+    if (B.split) {  // averaged and rounded before the all-gather
+      B.split = false;
+      B.work.reset();
+      B.comm = at::Tensor();
+      B.shard = at::Tensor();
+      return;
+    }
     const bool avg = use_avg_ && average_ && predivide_ == 1.0;
     double factor = 1.0;
     if (!avg && average_) factor = predivide_ / (double)world_;
@@ -549,6 +639,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     next_ = 0;
     std::fill(seen_.begin(), seen_.end(), 0);
     std::fill(async_marked_.begin(), async_marked_.end(), 0);
+    ++iteration_;
   }
 
   std::vector<at::Tensor> params_;
@@ -568,6 +659,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<int64_t> arrival_;
   std::vector<char> seen_;
   std::vector<char> async_marked_;
+  std::vector<char> no_direct_;
+  int64_t iteration_ = 0;
   int64_t next_ = 0;
   bool refresh_ = true;
   bool enabled_ = true;
@@ -717,6 +810,9 @@ void register_reducer(pybind11::module_& m) {
            py::arg("stream"))
       .def("async_ready_ok", &Reducer::async_ready_ok)
       .def("mark_ready_direct", &Reducer::mark_ready_direct)
+      .def("set_no_direct", &Reducer::set_no_direct)
+      .def("direct_ok", &Reducer::direct_ok)
+      .def("iteration", &Reducer::iteration)
       .def("force_collectives", &Reducer::force_collectives)
       .def("collectives_active", &Reducer::collectives_active)
       .def("set_timing", &Reducer::set_timing)

@@ -157,6 +157,120 @@ def ddp_bf16_precision(rank, world, fp32=None, n=4096):
     return {"grad": p.grad.float().clone(), "exact": exact}
 
 
+def ddp_bf16_wire(rank, world, wire="rsag", n=4099, message_size=1000, iters=2):
+    """bf16 buckets (sizes not multiples of world x alignment) reduced through the given
+    wire format; returns every iteration's reduced gradients and the exact fp64 average
+    of the per-rank bf16 gradients."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    sizes = [n, n + 13, 2 * n + 7]
+    mod = nn.Module()
+    mod.ps = nn.ParameterList([nn.Parameter(torch.ones(k, dtype=torch.bfloat16)) for k in sizes])
+    mod.forward = lambda cs: sum((p.float() * c).sum() for p, c in zip(mod.ps, cs))
+    ddp = DistributedDataParallel(mod, bf16_wire=wire, message_size=message_size)
+    out, exact = [], []
+    for it in range(iters):
+        cs = [[torch.randn(k, generator=torch.Generator().manual_seed(1000 * it + 10 * r + j))
+               * (1.0 + 0.37 * r) for j, k in enumerate(sizes)] for r in range(world)]
+        for p in mod.ps:
+            if p.grad is not None:
+                p.grad.zero_()
+        ddp(cs[rank]).backward()
+        out.append([p.grad.float().clone() for p in mod.ps])
+        exact.append([sum(cs[r][j].to(torch.bfloat16).double() for r in range(world)) / world
+                      for j in range(len(sizes))])
+    return {"grads": out, "exact": exact, "wire": ddp.wire_format(),
+            "mode": ddp._fp32_mode()}
+
+
+class _DirectMul(torch.autograd.Function):
+    """y = x * w whose weight gradient goes the own ops' direct way when DDP allows it
+    (accumulated into the bucket view + announced; autograd gets None)."""
+    DIRECT = [0]
+
+    @staticmethod
+    def forward(ctx, x, w):
+        from apex_example_amd.ops import _ddp_direct
+
+        ctx.save_for_backward(x, w)
+        ctx.w = w
+        if ctx.needs_input_grad[1]:
+            _ddp_direct.note_use(w)
+        return x * w
+
+    @staticmethod
+    def backward(ctx, g):
+        from apex_example_amd.ops import _ddp_direct
+
+        x, w = ctx.saved_tensors
+        gw = (g * x).sum(0)
+        sl = _ddp_direct.slots(ctx.w)
+        if sl is not None:
+            with torch.no_grad():
+                ctx.w.grad.add_(gw)
+            _ddp_direct.mark_ready(sl)
+            _DirectMul.DIRECT[0] += 1
+            gw = None
+        return g * w, gw
+
+
+class _DirectNet(nn.Module):
+    def __init__(self, case):
+        super().__init__()
+        self.case = case
+        self.a = nn.Parameter(torch.linspace(0.5, 1.5, 8))
+        self.b = nn.Parameter(torch.linspace(-1.0, 1.0, 8))
+        self.c = nn.Parameter(torch.linspace(2.0, 3.0, 8))   # always used once
+        if case == "tied":
+            self.sub = nn.Module()
+            self.sub.w = self.a                                  # a listed twice
+
+    def forward(self, x):
+        h = _DirectMul.apply(x, self.c)
+        if self.case == "twice":       # one module's weight used twice in a forward
+            h = _DirectMul.apply(_DirectMul.apply(h, self.a), self.a)
+        elif self.case == "tied":      # tied weight: used through both names
+            h = _DirectMul.apply(_DirectMul.apply(h, self.a), self.sub.w)
+        else:                          # "functional": a direct use + a plain autograd use
+            h = _DirectMul.apply(h, self.a) + h * self.a
+        return (_DirectMul.apply(h, self.b) ** 2).sum()
+
+
+def ddp_direct_shared(rank, world, case="twice", iters=3):
+    """Shared / multiply-used parameters on the direct-gradient path: grads
+    must equal the full-batch autograd reference, or (functional use after a launched
+    bucket) the reducer raises its explicit error; the parameter is then excluded."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    net = _DirectNet(case)
+    ref = _DirectNet(case)
+    ref.load_state_dict(net.state_dict())
+    ddp = DistributedDataParallel(net, message_size=1)  # one bucket per parameter
+    _DirectMul.DIRECT[0] = 0
+    out, refs, err = [], [], None
+    for it in range(iters):
+        xs = [torch.randn(4, 8, generator=torch.Generator().manual_seed(50 * it + r))
+              for r in range(world)]
+        for p in net.parameters():  # (bucket views: zeroed in place)
+            if p.grad is not None:
+                p.grad.zero_()
+        try:
+            ddp(xs[rank]).backward()
+        except RuntimeError as e:
+            err = str(e)
+            break
+        out.append({k: v.grad.clone() for k, v in net.named_parameters()})
+        loss = sum(ref(x) for x in xs) / world
+        ref.zero_grad()
+        loss.backward()
+        refs.append({k: v.grad.clone() for k, v in ref.named_parameters()})
+    red = ddp.reducer
+    idx = {id(p): i for i, p in enumerate(ddp.active_params)}
+    return {"grads": out, "refs": refs, "err": err, "direct": _DirectMul.DIRECT[0],
+            "direct_ok": {k: bool(red.direct_ok(idx[id(p)])) for k, p in net.named_parameters()}}
+
+
 def ddp_train_amp(rank, world, inject_rank=-1):
     """amp O2 (bf16, CPU) + DDP + FusedSGD: training + overflow consensus."""
     from apex_example_amd import amp
@@ -244,10 +358,12 @@ def gpu_syncbn_step(rank, world, sizes=(4, 6), fuse_relu=True):
     """The GPU SyncBN path (packed stats, one all_gather, device-scaled backward
     sums, one all_reduce) with two ranks sharing cuda:0 over gloo, channels-last
     bf16 with residual + ReLU, vs. BN over the concatenated batch in fp32."""
+    from apex_example_amd.ops import batch_norm as bnmod
     from apex_example_amd.parallel import SyncBatchNorm
 
     torch.cuda.set_device(0)
     torch.manual_seed(0)
+    slots0 = bnmod.SLOT_GATHER_CALLS[0]
     C = 16
     full = torch.randn(sum(sizes), C, 6, 6) * 2 + 1
     zfull = torch.randn(sum(sizes), C, 6, 6)
@@ -269,7 +385,8 @@ def gpu_syncbn_step(rank, world, sizes=(4, 6), fuse_relu=True):
     return {"y": y.detach().float().cpu(), "dx": x.grad.detach().float().cpu(),
             "dz": z.grad.detach().float().cpu(), "dw": bn.weight.grad.cpu(),
             "db": bn.bias.grad.cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
-            "nbt": int(bn.num_batches_tracked)}
+            "nbt": int(bn.num_batches_tracked),
+            "slot_calls": bnmod.SLOT_GATHER_CALLS[0] - slots0}
 
 
 def syncbn_groups(rank, world):

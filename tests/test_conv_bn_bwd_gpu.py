@@ -185,3 +185,47 @@ def test_bottleneck_layer_grads_match_unfused(monkeypatch):
         err = float((a - b).abs().max() / (b.abs().max() + 1e-12))
         # the residual gradient is rounded to bf16 once more on the fused path
         assert err < 2e-2, (i, err)
+
+
+def test_bn_output_fanout_falls_back_to_reduce(monkeypatch):
+    """a fused BN's output feeding the epilogue conv AND another consumer created
+    EARLIER in forward - autograd adds that consumer's gradient in place into the conv's g
+    (InputBuffer), so the slab sums would miss it.  The BN backward must notice (version
+    counter) and take the reduce pass; gradients match the fp32 reference."""
+    from apex_example_amd.ops import BatchNorm2dReLU
+    from apex_example_amd.ops import batch_norm as bnmod
+    from apex_example_amd.ops import conv as convmod
+    from apex_example_amd.ops.conv import Conv2d1x1
+
+    monkeypatch.setattr(convmod, "_BNBWD_MAX_M", 1 << 30)
+    calls = _count_epilogue(monkeypatch)
+    torch.manual_seed(0)
+    N, C, H, W, Co = 8, 64, 14, 14, 128
+    x0 = torch.randn(N, C, H, W, device=dev) * 2 + 0.5
+    bn = BatchNorm2dReLU(C, fuse_relu=True).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    conv = Conv2d1x1(C, Co).to(dev).to(torch.bfloat16).to(memory_format=CL)
+    ref_bn = torch.nn.BatchNorm2d(C).to(dev)
+    ref_bn.load_state_dict(bn.state_dict())
+    w32 = conv.weight.detach().float().clone().requires_grad_(True)
+
+    x = _bf(x0).requires_grad_(True)
+    h = bn(x)
+    side = (h.float() * 0.5).sum((2, 3))          # second consumer, created first
+    y = conv(h)
+    r = torch.randn_like(y.float())
+    fused0 = bnmod.FUSED_BWD_CALLS[0]
+    ((y.float() * r).sum() + (side ** 2).sum()).backward()
+    assert calls["n"] == 1                          # the epilogue conv ran ...
+    assert bnmod.FUSED_BWD_CALLS[0] == fused0       # ... but the BN did not trust its sums
+
+    xr = x.detach().float().requires_grad_(True)
+    hr = torch.relu(ref_bn(xr))
+    yr = F.conv2d(hr, w32)
+    ((yr * r).sum() + ((hr * 0.5).sum((2, 3)) ** 2).sum()).backward()
+    for got, want in ((x.grad.float(), xr.grad), (bn.weight.grad, ref_bn.weight.grad),
+                      (bn.bias.grad, ref_bn.bias.grad)):
+        err = float((got - want).abs().max() / want.abs().max())
+        assert err < 3e-2, err

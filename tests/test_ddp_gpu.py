@@ -247,6 +247,9 @@ def test_syncbn_gpu_two_ranks_matches_global_batch(tmp_path):
         torch.testing.assert_close(r["rm"], bn.running_mean, rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(r["rv"], bn.running_var, rtol=1e-4, atol=1e-5)
         assert r["nbt"] == 1
+        # both ranks gathered through their slot of the shared destination (the raw
+        # RCCL path's in-place layout; rank 1 writes at offset 2C + 1)
+        assert r["slot_calls"] == 1
 
 
 def test_bench_self_spawn_two_ranks_one_gpu():
@@ -506,3 +509,69 @@ def test_ddp_direct_dense_weight_gradients_match_autograd_path(pg, monkeypatch, 
                 continue
             scale = float(a.abs().max()) + 1e-30
             assert float((a - b).abs().max()) / scale < tol, it
+
+
+class _SharedNet(torch.nn.Module):
+    """A 3x3 conv called twice per forward and a FusedDense head tied to an Embedding
+    (parameters with more than one use per iteration)."""
+
+    def __init__(self):
+        super().__init__()
+        from apex_example_amd.fused_dense import FusedDense
+        from apex_example_amd.ops.conv import Conv2d3x3
+        from apex_example_amd.ops.embedding import Embedding
+
+        self.conv = Conv2d3x3(64, 64)
+        self.other = Conv2d3x3(64, 64)          # used once: goes direct
+        self.emb = Embedding(96, 64)
+        self.head = FusedDense(64, 96, bias=False)
+        self.head.weight = self.emb.weight      # tied
+
+    def forward(self, x, ids):
+        h = self.conv(torch.relu(self.conv(x)))  # same weight, two uses
+        h = self.other(h)
+        v = h.mean((2, 3)) + self.emb(ids)       # [B, 64]
+        return self.head(v).float()
+
+
+def test_ddp_direct_path_shared_parameters_gpu(pg, monkeypatch):
+    """Own-kernel ops whose parameter is used twice (same conv module called twice) or
+    tied (FusedDense head = Embedding table) under DDP with forced RCCL collectives: no
+    'received a gradient twice' error, gradients equal to the autograd path (direct off),
+    the tied weight excluded from the direct path and the once-used conv still direct."""
+    from apex_example_amd.ops import _ddp_direct
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    x = torch.randn(8, 64, 16, 16, device="cuda").to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    ids = torch.randint(0, 96, (8,), device="cuda")
+    grads, marks = {}, {}
+    orig = _ddp_direct.mark_ready
+    for on in (False, True):
+        monkeypatch.setattr(_ddp_direct, "_ON", on)
+        count = {"n": 0}
+
+        def counting(sl, _c=count):
+            _c["n"] += len(sl)
+            return orig(sl)
+        monkeypatch.setattr(_ddp_direct, "mark_ready", counting)
+        torch.manual_seed(0)
+        m = _SharedNet().cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+        ddp = DistributedDataParallel(m, message_size=20_000, force_collectives=True)
+        gs = []
+        for it in range(3):
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.grad.zero_()
+            (ddp(x, ids) ** 2).mean().backward()
+            gs.append([p.grad.detach().float().clone() for p in m.parameters()])
+        torch.cuda.synchronize()
+        grads[on], marks[on] = gs, count["n"]
+        if on:
+            idx = {id(p): i for i, p in enumerate(ddp.active_params)}
+            assert not ddp.reducer.direct_ok(idx[id(m.emb.weight)])
+    assert marks[False] == 0 and marks[True] >= 2, marks  # `other` went direct (its. 2, 3)
+    for it in range(3):
+        for a, b in zip(grads[False][it], grads[True][it]):
+            scale = float(a.abs().max()) + 1e-30
+            assert float((a - b).abs().max()) / scale < 2e-2, it

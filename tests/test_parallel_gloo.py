@@ -200,3 +200,69 @@ def test_ddp_bf16_buckets_reduce_in_fp32(tmp_path):
     # relative error bound of ONE bf16 rounding (2^-9) for the fp32 path
     rel = ((auto[0]["grad"] - exact).abs() / exact.abs().clamp_min(1e-3)).max().item()
     assert rel <= 2 ** -8
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_bf16_wire_formats_match_fp64_average(tmp_path, world):
+    """bf16 buckets: the fp32 reduce-scatter + bf16 all-gather wire (default) and the fp32
+    all-reduce both give the fp64 average rounded ONCE to bf16 (bucket sizes that are not
+    multiples of world x alignment: padded shards); native bf16 is never better."""
+    res = {}
+    for wire in ("rsag", "fp32", "native"):
+        d = tmp_path / wire
+        d.mkdir()
+        res[wire] = W.run("ddp_bf16_wire", world, str(d), wire=wire)
+    assert res["rsag"][0]["mode"] == 3 and res["fp32"][0]["mode"] == 2
+    assert "reduce-scatter" in res["rsag"][0]["wire"]["torch.bfloat16"]
+    for r in res["rsag"] + res["fp32"]:
+        for got, ex in zip(r["grads"], r["exact"]):
+            for g, e in zip(got, ex):
+                # within half an ulp of bf16 (+ the fp32 sum's own rounding) of the exact
+                # average: one rounding
+                ulp = torch.finfo(torch.bfloat16).eps * e.abs().clamp_min(1e-30)
+                assert bool(((g.double() - e).abs() <= 0.5 * ulp + 1e-6 * e.abs()).all())
+    for a, b in zip(res["rsag"], res["fp32"]):  # same values, fewer wire bytes
+        for ga, gb in zip(a["grads"], b["grads"]):
+            for x, y in zip(ga, gb):
+                assert torch.equal(x, y)
+    for r in res["rsag"][1:]:  # identical on every rank
+        for ga, gb in zip(r["grads"], res["rsag"][0]["grads"]):
+            for x, y in zip(ga, gb):
+                assert torch.equal(x, y)
+    err = {w: max(float((g.double() - e).abs().max()) for got, ex in
+                  zip(res[w][0]["grads"], res[w][0]["exact"]) for g, e in zip(got, ex))
+           for w in res}
+    assert err["native"] >= err["rsag"]
+
+
+@pytest.mark.parametrize("case", ["twice", "tied"])
+def test_ddp_direct_path_shared_parameters(tmp_path, case):
+    """A module called twice / a tied weight never takes the direct-gradient path (one
+    announcement would carry only part of the gradient): gradients equal the full-batch
+    reference; the once-used parameter still goes direct."""
+    res = W.run("ddp_direct_shared", 2, str(tmp_path), case=case)
+    for r in res:
+        assert r["err"] is None, r["err"]
+        assert r["direct"] > 0  # `c` (and `b`) went direct from iteration 2 on
+        for got, ref in zip(r["grads"], r["refs"]):
+            for k in ref:
+                torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6)
+        if case == "tied":
+            assert r["direct_ok"]["a"] is False
+        assert r["direct_ok"]["c"] is True
+
+
+def test_ddp_direct_path_functional_second_use(tmp_path):
+    """A parameter announced by a direct op AND used by a plain autograd op: the reducer
+    either still had the bucket open (the late autograd gradient lands in the view before
+    the launch: correct) or raises its explicit error; the parameter is excluded from the
+    direct path afterwards."""
+    res = W.run("ddp_direct_shared", 2, str(tmp_path), case="functional")
+    for r in res:
+        if r["err"] is not None:
+            assert "received an autograd gradient" in r["err"], r["err"]
+        else:
+            for got, ref in zip(r["grads"], r["refs"]):
+                for k in ref:
+                    torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6)
+        assert r["direct_ok"]["a"] is False
