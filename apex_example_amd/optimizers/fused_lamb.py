@@ -46,6 +46,10 @@ class FusedLAMB(FusedOptimizerBase):
                 loss = closure()
 
         all_sets = [self._launch_sets(gid, group) for gid, group in enumerate(self.param_groups)]
+        if all(s.get("_plan") is not None for sets in all_sets for s in sets.values()) and any(
+                all_sets):
+            self._planned_step(all_sets)
+            return loss
         # global grad norm over every group (Apex: blend of the fp32 and fp16 norms)
         scaled, unscaled = [], []
         for sets in all_sets:
@@ -91,4 +95,49 @@ class FusedLAMB(FusedOptimizerBase):
                                         self.use_nvlamb, model_copies=s["copies"], scale=scale_v,
                                         scale_inv=inv)
             self._after_step(gid, dev, step_t, noop)
+            self._set_plans(gid, sets, lambda s: [s["params"]] + list(s["_state"][1]) + (
+                [s["copies"]] if s["copies"] is not None else []))
         return loss
+
+    def _planned_step(self, all_sets):
+        """Steady state: every launch set on its native StepPlan (csrc/torch/amp_ops.cpp) -
+        the global grad norm is one norm per set written into one device vector (unscaled
+        in the same call) and one norm of that vector; each set's two LAMB stages are one
+        C++ call with scalar arguments (no tensor lists cross from Python)."""
+        flat = [s for sets in all_sets for s in sets.values()]
+        dev = flat[0]["params"][0].device
+        noop = self._noop(dev)
+        dummy = self._dummy(str(dev) + ":scratch")
+        bufs = self.__dict__.setdefault("_norm_bufs", {})
+        buf = bufs.get((str(dev), len(flat)))
+        if buf is None:
+            buf = bufs[(str(dev), len(flat))] = torch.empty(len(flat), dtype=torch.float32,
+                                                            device=dev)
+        for i, s in enumerate(flat):
+            if s["scaled"]:
+                sv, _inv = self._fold_scale()
+                ok = s["_plan"].grad_norm_into(buf, i, dummy, 1.0 if isinstance(
+                    sv, torch.Tensor) else float(sv), sv if isinstance(sv, torch.Tensor) else None)
+            else:
+                ok = s["_plan"].grad_norm_into(buf, i, dummy, 1.0, None)
+            if not ok:
+                raise RuntimeError("FusedLAMB: launch set changed inside step()")
+        global_grad_norm = buf if len(flat) == 1 else buf.norm().reshape(1)
+        for gid, group in enumerate(self.param_groups):
+            sets = all_sets[gid]
+            if not sets:
+                continue
+            beta1, beta2 = group["betas"]
+            step, step_t = self._step_value(gid, group, dev)
+            last = len(sets) - 1
+            for i, s in enumerate(sets.values()):
+                sv, st, inv = self._plan_scale(s["scaled"])
+                lr = group["lr"]
+                lv, lt = (1.0, lr) if isinstance(lr, torch.Tensor) else (float(lr), None)
+                if not s["_plan"].lamb(noop, lv, lt, beta1, beta2, group["eps"], step, step_t,
+                                       bool(group["bias_correction"]), group["weight_decay"],
+                                       bool(group["grad_averaging"]), self.adam_w_mode,
+                                       global_grad_norm,
+                                       group.get("max_grad_norm", self.defaults["max_grad_norm"]),
+                                       self.use_nvlamb, sv, st, inv, i == last):
+                    raise RuntimeError("FusedLAMB: launch set changed inside step()")

@@ -475,7 +475,103 @@ bool StepPlan::refresh() {
   if (moved) {
     mt_validate(lists_, 2, kMaxDepth);  // strides of a new grad vs. its param
     fresh_ = false;
+    ++gen_;
   }
+  return true;
+}
+
+namespace {
+// a sub-table built inside a graph capture must never be evicted / rebuilt under it
+void mark_if_capturing(MTPlan& p) {
+  if (c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None)
+    p.captured = true;
+}
+}  // namespace
+
+bool StepPlan::grad_norm_into(at::Tensor out, int64_t slot, at::Tensor flag, double scale,
+                              OptT scale_t) {
+  c10::NoGradGuard no_grad_;
+  if (!refresh()) return false;
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && slot >= 0 &&
+                  slot < out.numel(), "grad_norm_into: fp32 output slot");
+  at::Tensor dst = out.narrow(0, slot, 1);
+  if (!gpu_) {
+    dst.copy_(std::get<0>(mt_norm_op(flag, lists_[0], false, false)));
+  } else {
+    auto fopt = at::TensorOptions().dtype(at::kFloat).device(out.device());
+    if (ngen_ != gen_) {
+      nplan_ = mt_plan(TensorLists{lists_[0]});
+      npart_ = at::empty({(int64_t)nplan_.L.nchunks}, fopt);
+      ngen_ = gen_;
+    }
+    mark_if_capturing(nplan_);
+    mt_norm_partials(nplan_.L, dtype_of(lists_[0][0]), 0, npart_.data_ptr<float>(),
+                     noop_ptr(flag), cur_stream());
+    mt_norm_finalize(nplan_.L, npart_.data_ptr<float>(), 1, 0, dst.data_ptr<float>(), nullptr,
+                     cur_stream());
+  }
+  if (scale_t.has_value() && scale_t->defined()) dst.div_(*scale_t);
+  else if (scale != 1.0) dst.mul_(scale);
+  return true;
+}
+
+bool StepPlan::lamb(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
+                    int64_t step, OptT step_t, bool bias_correction, double wd,
+                    bool grad_averaging, int64_t mode, at::Tensor global_grad_norm,
+                    double max_grad_norm, bool use_nvlamb, double scale, OptT scale_t,
+                    bool scale_inv, bool advance) {
+  c10::NoGradGuard no_grad_;
+  if (!refresh()) return false;
+  const int depth = (int)lists_.size();
+  TORCH_CHECK(depth == 4 || depth == 5, "lamb plan: [grads, params, m, v(, copies)]");
+  if (!gpu_) {
+    mt_lamb_op(noop, lists_, lr, lr_t, beta1, beta2, eps, step, step_t, bias_correction, wd,
+               grad_averaging, mode, OptT(global_grad_norm), max_grad_norm, use_nvlamb, scale,
+               scale_t, scale_inv);
+  } else {
+    TORCH_CHECK(lists_[2][0].scalar_type() == lists_[1][0].scalar_type() &&
+                    lists_[3][0].scalar_type() == lists_[1][0].scalar_type(),
+                "lamb: exp_avg / exp_avg_sq must match the parameter dtype");
+    LambArgs a;
+    a.lr = (float)lr;
+    a.beta1 = (float)beta1;
+    a.beta2 = (float)beta2;
+    a.eps = (float)eps;
+    a.wd = (float)wd;
+    a.step = (int)step;
+    a.step_ptr = opt_iptr(step_t);
+    a.mode = (int)mode;
+    a.bias_correction = bias_correction ? 1 : 0;
+    a.grad_averaging = grad_averaging ? 1 : 0;
+    a.global_grad_norm = global_grad_norm.data_ptr<float>();
+    a.max_grad_norm = (float)max_grad_norm;
+    a.use_nvlamb = use_nvlamb ? 1 : 0;
+    a.scale = make_scale(scale, scale_t, scale_inv);
+    a.lr_ptr = opt_fptr(lr_t);
+    auto fopt = at::TensorOptions().dtype(at::kFloat).device(lists_[1][0].device());
+    if (l1gen_ != gen_) {
+      l1plan_ = mt_plan(sub(lists_, {0, 1, 2, 3}));
+      l1part_ = at::empty({2 * (int64_t)l1plan_.L.nchunks}, fopt);
+      l1norm_ = at::empty({2 * (int64_t)l1plan_.L.ntensors}, fopt);
+      l1gen_ = gen_;
+    }
+    if (!l2ok_) {  // params / state / copies never move: built once
+      l2plan_ = mt_plan(depth == 5 ? sub(lists_, {1, 2, 3, 4}) : sub(lists_, {1, 2, 3}));
+      l2ok_ = true;
+    }
+    mark_if_capturing(l1plan_);
+    mark_if_capturing(l2plan_);
+    mt_lamb_stage1(l1plan_.L, dtype_of(lists_[0][0]), dtype_of(lists_[1][0]), a,
+                   l1part_.data_ptr<float>(), noop_ptr(noop), cur_stream());
+    mt_norm_finalize(l1plan_.L, l1part_.data_ptr<float>(), 2, 0, nullptr,
+                     l1norm_.data_ptr<float>(), cur_stream());
+    DType copy = depth == 5 ? dtype_of(lists_[4][0]) : dtype_of(lists_[1][0]);
+    mt_lamb_stage2(l2plan_.L, depth - 1, dtype_of(lists_[1][0]), copy, a,
+                   l1norm_.data_ptr<float>(), l1norm_.data_ptr<float>() + l1plan_.L.ntensors,
+                   noop_ptr(noop), cur_stream());
+  }
+  if (advance && step_t.has_value() && step_t->defined())
+    advance_step_op(*step_t, noop.defined() ? OptT(noop) : OptT());
   return true;
 }
 

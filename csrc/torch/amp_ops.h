@@ -77,6 +77,16 @@ class StepPlan {
   bool adam(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
             int64_t step, OptT step_t, int64_t mode, bool bias_correction, double wd,
             double scale, OptT scale_t, bool scale_inv, bool advance_step);
+  // ||grads||_2 of this set into out[slot] (fp32 device vector), unscaled: divided by
+  // scale_t when given, else multiplied by scale; `flag` is a scratch overflow flag the
+  // norm kernels may write (never the step's noop flag)
+  bool grad_norm_into(at::Tensor out, int64_t slot, at::Tensor flag, double scale, OptT scale_t);
+  // FusedLAMB's two stages (mt_lamb_op) on cached launch tables: stage 1 + per-tensor
+  // norm finalize on [grads, params, m, v], stage 2 on [params, m, v(, copies)]
+  bool lamb(at::Tensor noop, double lr, OptT lr_t, double beta1, double beta2, double eps,
+            int64_t step, OptT step_t, bool bias_correction, double wd, bool grad_averaging,
+            int64_t mode, at::Tensor global_grad_norm, double max_grad_norm, bool use_nvlamb,
+            double scale, OptT scale_t, bool scale_inv, bool advance_step);
   // tensors that must stay without a grad (a param gaining one changes the sets)
   void set_absent(std::vector<at::Tensor> absent) { absent_ = std::move(absent); }
   int64_t size() const { return (int64_t)owners_.size(); }
@@ -91,6 +101,11 @@ class StepPlan {
   MTPlan plan_;
   bool gpu_ = false, fresh_ = false;
   int64_t rebuilds_ = 0;
+  // sub-launch tables (grad norm, LAMB stage 1 / 2), rebuilt when the grads moved (gen_)
+  int64_t gen_ = 0, ngen_ = -1, l1gen_ = -1;
+  bool l2ok_ = false;
+  MTPlan nplan_, l1plan_, l2plan_;
+  at::Tensor npart_, l1part_, l1norm_;
 };
 
 void mt_plan_cache_clear();

@@ -76,6 +76,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("sgd", &StepPlan::sgd)
       .def("sgd_pair", &StepPlan::sgd_pair)
       .def("adam", &StepPlan::adam)
+      .def("grad_norm_into", &StepPlan::grad_norm_into)
+      .def("lamb", &StepPlan::lamb)
       .def("size", &StepPlan::size)
       .def("rebuilds", &StepPlan::rebuilds);
   mt.def("plan_cache_clear", &mt_plan_cache_clear);

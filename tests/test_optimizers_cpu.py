@@ -178,7 +178,7 @@ def test_larc(clip):
         torch.testing.assert_close(p.detach(), exp, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("kind", ["sgd", "adam", "lamb"])
 def test_step_plan_path_tracks_grads(kind, monkeypatch):
     """The native StepPlan fast path (optimizers/_base.py): grads re-allocated every
     step (moved), persistent grads updated in place, a parameter that gains a grad
@@ -189,8 +189,11 @@ def test_step_plan_path_tracks_grads(kind, monkeypatch):
     if kind == "sgd":
         mk = lambda ts: FusedSGD(ts, lr=0.1, momentum=0.9, weight_decay=1e-3)  # noqa: E731
         o2 = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=1e-3)
-    else:
+    elif kind == "adam":
         mk = lambda ts: FusedAdam(ts, lr=1e-2, weight_decay=1e-2)  # noqa: E731
+        o2 = None
+    else:
+        mk = lambda ts: FusedLAMB(ts, lr=1e-2, weight_decay=1e-2)  # noqa: E731
         o2 = None
     o1, o3 = mk(ps), mk(slow)
     monkeypatch.setattr(o3, "_set_plans", lambda *a: None)
