@@ -525,6 +525,18 @@ class Conv2d1x1(nn.Conv2d):
 # 3x3 weight gradient: "tap" = per-tap MFMA kernel (default), "nine" = the all-taps
 # strip kernel (W <= 56), "miopen" = MIOpen's convolution_backward
 _WGRAD3 = os.environ.get("APEX_AMD_WGRAD3", "tap")
+# 64 -> 64 channel 3x3 stride-1 weight gradients (ResNet layer 1) on the strip-ring kernel
+# (csrc/hip/conv_igemm.hip conv3x3_wgrad_c64_k, algo 4); APEX_AMD_WGRAD64=0 keeps the
+# per-tap kernel
+_WGRAD64 = os.environ.get("APEX_AMD_WGRAD64", "1") == "1"
+
+
+def _wgrad3_algo(x, weight, stride):
+    """conv_wgrad algo for a 3x3 weight gradient under _WGRAD3 == "tap"."""
+    if (_WGRAD64 and stride == 1 and x.size(1) == 64 and weight.size(0) == 64
+            and x.size(3) <= 56):
+        return 4
+    return 0
 # A/B switches for the reduction / rotation kernels (tools, docs/PERF.md)
 _USE_SPLITK_REDUCE = os.environ.get("APEX_AMD_SPLITK_REDUCE", "1") == "1"
 _USE_ROT_KERNEL = os.environ.get("APEX_AMD_ROT_KERNEL", "1") == "1"
@@ -621,13 +633,15 @@ class Conv3x3Function(torch.autograd.Function):
                 direct = None
         if direct is not None:
             # accumulate straight into the DDP bucket view, no autograd add kernel
-            cv.conv_wgrad(dy, x, weight.dtype, 0 if _WGRAD3 == "tap" else 1,
+            cv.conv_wgrad(dy, x, weight.dtype,
+                          _wgrad3_algo(x, weight, stride) if _WGRAD3 == "tap" else 1,
                           stride if _WGRAD3 == "tap" else 1, out=weight.grad)
             _ddp_direct.mark_ready(direct)
         elif ctx.needs_input_grad[1]:
             so = _side_out(side, weight, cl=True)
             if _WGRAD3 == "tap" and n_pix < (1 << 22):
-                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, stride, out=so),
+                algo = _wgrad3_algo(x, weight, stride)
+                dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, algo, stride, out=so),
                               dy, x)
             elif _WGRAD3 == "nine" and stride == 1 and x.size(3) <= 56 and n_pix < (1 << 22):
                 dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 1, 1, out=so), dy, x)

@@ -118,10 +118,10 @@ struct ConvGeom {
 // dependent loads with few waves per CU.  bnbwd_store then forms, per row chunk,
 // o = T (+ add), g = relu_mask ? o : 0 rounded to bf16, stores g in place of o and
 // accumulates the BN's backward sums of exactly those values: sum(g), sum(g*(x-mean)).
-template <int BM, int BN>
+template <int BM, int BN, int CT = kCT>
 struct BnPre {
   static constexpr int CPR = BN / 8;
-  static constexpr int RGS = kCT / CPR;  // row groups; a thread visits rows rg, rg + RGS, ...
+  static constexpr int RGS = CT / CPR;  // row groups; a thread visits rows rg, rg + RGS, ...
   static constexpr int ROWS = BM / RGS;
   uint4 av[ROWS], xv[ROWS];
   unsigned mk[ROWS];
@@ -141,10 +141,10 @@ __device__ __forceinline__ int64_t out_pix(const ConvGeom& g, int m, int z) {
   }
 }
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int CT>
 __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEpi& ep, int m0,
-                                               int n0, int z, BnPre<BM, BN>& P) {
-  using PT = BnPre<BM, BN>;
+                                               int n0, int z, BnPre<BM, BN, CT>& P) {
+  using PT = BnPre<BM, BN, CT>;
   const int tid = threadIdx.x;
   const int cc = tid % PT::CPR, rg = tid / PT::CPR;
   const int c0 = n0 + cc * 8;
@@ -175,12 +175,12 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
 // one specialisation per (ReLU-mask mode, residual add): the per-element mode tests are
 // compile-time, so the unrolled store loop is straight-line code (runtime tests there
 // made the compiler branch around every element: +30-60 us per ResNet-50 layer)
-template <int MODE, int BM, int BN, int RM, bool ADD>
+template <int MODE, int BM, int BN, int CT, int RM, bool ADD>
 __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restrict__ y,
                                               const ConvGeom& g, int m0, int n0, int z,
-                                              const BnPre<BM, BN>& P, float (&s1)[8],
+                                              const BnPre<BM, BN, CT>& P, float (&s1)[8],
                                               float (&s2)[8]) {
-  using PT = BnPre<BM, BN>;
+  using PT = BnPre<BM, BN, CT>;
   const int tid = threadIdx.x;
   const int cc = tid % PT::CPR, rg = tid / PT::CPR;
   const int c0 = n0 + cc * 8;
@@ -225,19 +225,19 @@ __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restric
   }
 }
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int CT>
 __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict__ y,
                                             const ConvGeom& g, const ConvBnEpi& ep, int m0,
-                                            int n0, int z, const BnPre<BM, BN>& P,
+                                            int n0, int z, const BnPre<BM, BN, CT>& P,
                                             float (&s1)[8], float (&s2)[8]) {
   const bool add = ep.add != nullptr;
   switch (ep.relu_mode * 2 + (add ? 1 : 0)) {
-    case 0: bnbwd_store_t<MODE, BM, BN, 0, false>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 1: bnbwd_store_t<MODE, BM, BN, 0, true>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 2: bnbwd_store_t<MODE, BM, BN, 1, false>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 3: bnbwd_store_t<MODE, BM, BN, 1, true>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 4: bnbwd_store_t<MODE, BM, BN, 2, false>(T, y, g, m0, n0, z, P, s1, s2); break;
-    default: bnbwd_store_t<MODE, BM, BN, 2, true>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 0: bnbwd_store_t<MODE, BM, BN, CT, 0, false>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 1: bnbwd_store_t<MODE, BM, BN, CT, 0, true>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 2: bnbwd_store_t<MODE, BM, BN, CT, 1, false>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 3: bnbwd_store_t<MODE, BM, BN, CT, 1, true>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 4: bnbwd_store_t<MODE, BM, BN, CT, 2, false>(T, y, g, m0, n0, z, P, s1, s2); break;
+    default: bnbwd_store_t<MODE, BM, BN, CT, 2, true>(T, y, g, m0, n0, z, P, s1, s2); break;
   }
 }
 
@@ -246,22 +246,28 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
 // the LDS goes to more resident workgroups instead (3 per CU: one's loads overlap
 // another's MFMAs and stores; 4 would cap the registers at 128 and spill the epilogue
 // statistics).
-template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0>
-__global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes > 80 * 1024)
-                                           ? 1 : (NB == 1 && EPI == 0 ? 3 : 2))
+// CT = 512 (8 waves, one workgroup per CU): the 256 x 128 tile on a 3-deep ring (144 KB of
+// LDS), 64 x 64 per wave - two waves per SIMD like the 2-workgroup 128 x 128 form, but two
+// tiles' DMAs stay in flight across every barrier instead of one.
+template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0, int CT = kCT>
+__global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
+                                       NB * (BM + BN) * kRowBytes > 80 * 1024)
+                                          ? 1 : (NB == 1 && EPI == 0 ? 3 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
                const float* __restrict__ shift, ConvBnEpi ep) {
-  static_assert(WM * WN == 4, "4 waves");
+  constexpr int NW = CT / 64;
+  static_assert(WM * WN == NW, "one wave per output sub-tile");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
   constexpr int BUF = A_BYTES + B_BYTES;
-  constexpr int AI = BM / 32;      // A wave-instructions (8 rows each) per wave per tile
-  constexpr int BI = BN / 32;       // B wave-instructions per wave per tile
+  constexpr int AI = BM / (8 * NW);  // A wave-instructions (8 rows each) per wave per tile
+  constexpr int BI = BN / (8 * NW);  // B wave-instructions per wave per tile
+  static_assert(AI >= 1 && BI >= 1, "tile rows per wave");
   constexpr int G = AI + BI;        // glds per wave per tile (vmcnt units)
   // the ring, or the epilogue's bf16 tile / statistics exchange if larger
-  constexpr int EPI_BYTES = BM * BN * 2 > 2 * kCT * 8 * 4 ? BM * BN * 2 : 2 * kCT * 8 * 4;
+  constexpr int EPI_BYTES = BM * BN * 2 > 2 * CT * 8 * 4 ? BM * BN * 2 : 2 * CT * 8 * 4;
   constexpr int LDS_BYTES = NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
@@ -284,7 +290,7 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   unsigned amask[AI];
 #pragma unroll
   for (int q = 0; q < AI; ++q) {
-    const int row = wid * (BM / 4) + q * 8 + lrow;
+    const int row = wid * (BM / NW) + q * 8 + lrow;
     const int ch = pchunk ^ ((row >> 1) & 7);
     const int m = m0 + row;
     const int mm = m < M ? m : 0;
@@ -307,7 +313,7 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   const bf16_t* bbase[BI];
 #pragma unroll
   for (int q = 0; q < BI; ++q) {
-    const int row = wid * (BN / 4) + q * 8 + lrow;
+    const int row = wid * (BN / NW) + q * 8 + lrow;
     bbase[q] = wt + (int64_t)(n0 + row) * g.kb_stride + (pchunk ^ ((row >> 1) & 7)) * 8;
   }
   const int kc_per_tap = KC / kBK;
@@ -326,10 +332,10 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
     _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                        \
       const bool ok = (amask[q] >> tap_) & 1u;                                              \
       glds16(ok ? (const void*)(abase[q] + aoff_) : (const void*)g_zero16,                  \
-             A_ + (wid * (BM / 4) + q * 8) * kRowBytes);                                   \
+             A_ + (wid * (BM / NW) + q * 8) * kRowBytes);                                  \
     }                                                                                       \
     _Pragma("unroll") for (int q = 0; q < BI; ++q)                                          \
-      glds16(bbase[q] + boff_, B_ + (wid * (BN / 4) + q * 8) * kRowBytes);                  \
+      glds16(bbase[q] + boff_, B_ + (wid * (BN / NW) + q * 8) * kRowBytes);                 \
   }
 
   f32x4_t acc[FM][FN];
@@ -356,7 +362,7 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   // loop would stall on them (measured: no gain from a prefetch at kernel start) - and
   // consumed after barriers that wait for LDS only, so they fly under the accumulator ->
   // LDS tile write instead of being waited for at a __syncthreads()
-  BnPre<BM, BN> pre;
+  BnPre<BM, BN, CT> pre;
 
   // prologue: NB-1 tiles in flight
 #pragma unroll
@@ -404,7 +410,7 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
   // (the K loop ended on a vmcnt(0) wait: no tile DMA is in flight; an LDS-only barrier
   // leaves the epilogue prefetch of EPI == 1 outstanding)
   if constexpr (EPI == 1) {
-    bnbwd_prefetch<MODE, BM, BN>(g, ep, m0, n0, z, pre);
+    bnbwd_prefetch<MODE, BM, BN, CT>(g, ep, m0, n0, z, pre);
     lds_barrier();
   } else {
     __syncthreads();
@@ -438,9 +444,9 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
   if constexpr (EPI == 1) {
-    bnbwd_store<MODE, BM, BN>(T, y, g, ep, m0, n0, z, pre, s1, s2);
+    bnbwd_store<MODE, BM, BN, CT>(T, y, g, ep, m0, n0, z, pre, s1, s2);
   } else
-  for (int c = tid; c < BM * CPR; c += kCT) {
+  for (int c = tid; c < BM * CPR; c += CT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
     if (m >= M) continue;
@@ -467,7 +473,7 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
     }
   }
   if (want_stats) {
-    constexpr int RGS = kCT / CPR;  // row groups (threads sharing a column group)
+    constexpr int RGS = CT / CPR;  // row groups (threads sharing a column group)
     // every thread is done reading the bf16 tile (an LDS-only barrier: the output
     // stores just issued need not complete before the statistics exchange)
     lds_barrier();
@@ -498,14 +504,21 @@ __global__ void __launch_bounds__(kCT, (BM == 256 || NB * (BM + BN) * kRowBytes 
 // M-tile choice: 128 (2 workgroups / CU, 64x64 per wave) or 256 (1 workgroup / CU,
 // 128x64 per wave: 1/3 less LDS read traffic per MFMA; 2- or 3-deep DMA ring).
 // APEX_AMD_CONV_BM = 128 | 256 | 256x3 for A/B runs (tools/microbench.py conv3x3).
+// 256w8 = 256 x 128 tiles, 8 waves (64 x 64 each), 3-deep ring, one workgroup per CU;
+// 256w8n2 the same on a 2-deep ring; 128w8 = 128 x 128, 8 waves (32 x 64), 3-deep.
 static int conv_bm_choice() {
   const char* e = std::getenv("APEX_AMD_CONV_BM");
   if (!e) return 0;
   if (std::strcmp(e, "256") == 0) return 1;
   if (std::strcmp(e, "256x3") == 0) return 2;
   if (std::strcmp(e, "128x3") == 0) return 3;
+  if (std::strcmp(e, "256w8") == 0) return 4;
+  if (std::strcmp(e, "256w8n2") == 0) return 5;
+  if (std::strcmp(e, "128w8") == 0) return 6;
   return 0;
 }
+
+static int conv_bm_of(int big) { return big == 1 || big == 2 || big == 4 || big == 5 ? 256 : 128; }
 
 // 1x1 forward convs with at most this many 64-channel K-tiles run the NB = 1 variant
 // (APEX_AMD_CONV1X1_NB1 = 0 | 1 | 2 | ..., read per launch for A/B runs)
@@ -538,7 +551,16 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
-  if (big == 3) {
+  if (big >= 4) {
+    const int bm = conv_bm_of(big);
+    const dim3 grid((g.M + bm - 1) / bm, g.NC / 128, nclasses);
+    if (big == 4)
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 4, 2, 3, EPI, 512>), grid, dim3(512), 0, st, a, w, y, g, slab, shift, ep);
+    else if (big == 5)
+      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 4, 2, 2, EPI, 512>), grid, dim3(512), 0, st, a, w, y, g, slab, shift, ep);
+    else
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 4, 2, 3, EPI, 512>), grid, dim3(512), 0, st, a, w, y, g, slab, shift, ep);
+  } else if (big == 3) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (big) {
@@ -765,6 +787,160 @@ __global__ void __launch_bounds__(kCT, 1)
           const int ci = ci0 + wn * 32 + j * 16 + fr;
           out[(int64_t)co * Cin + ci] = acc[t][i][j][e];
         }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// 3x3 stride-1 weight gradient for 64 -> 64 channels (ResNet layer 1), all 9 taps per
+// workgroup on a strip RING.  The per-tap kernel below reads each dY / X pixel row once
+// per tap for a 64 x 64 output tile - for 64 channels that is 9x the operand traffic per
+// MFMA and the kernel ends up L2 / LDS bound (357 TF standalone, 128 TF beside the
+// side-stream work).  Here one workgroup owns the whole [64 co] x [9 taps x 64 ci] output
+// and a contiguous range of K-tiles (64 padded-row pixels, q = h*(W+2) + w: the two pad
+// columns are dummy K rows whose dY is zero, so tap (r, s) of pixel q reads the padded
+// input at q + r*(W+2) + s - one contiguous strip of 64 + 2*(W+2) + 2 rows serves all 9
+// taps).  Consecutive K-tiles' strips overlap by all but 64 rows, so the strip lives in
+// a 256-row LDS ring: each K-tile DMAs only its 64 dY rows and the 64 strip rows past the
+// current frontier (16 KB instead of 31), the first K-tile of an image the whole strip.
+// The ring's 16-byte chunks carry tr_swz<128>'s row swizzle, which depends on row bits 1
+// and 3 only, so a read offset moves with the ring base by a plain add + wrap mask.
+// 8 waves: (k half of the K-tile) x (a quarter of the 576 output columns, 9 MFMA column
+// blocks = 64 x 144 per wave); the two k halves are summed through LDS at the end and
+// the workgroup writes one fp32 partial [tap][co][ci] slab for wgrad_reduce*_k.
+constexpr int kW64Ring = 256;                     // strip ring rows (x 128 B = 32 KB)
+constexpr int kW64BK = 64;                        // pixels per K-tile
+
+__global__ void __launch_bounds__(512, 1)
+    conv3x3_wgrad_c64_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                        float* __restrict__ part, int H, int W, int kpi, int kps, int total_kt) {
+  constexpr int RB = 128;                                   // 64 channels x bf16
+  constexpr int A_BYTES = kW64BK * RB;                      // 8 KB per dY K-tile
+  constexpr int RING_BYTES = kW64Ring * RB;                 // 32 KB
+  constexpr int NFB = 9;                                    // column blocks per wave
+  constexpr int EX_BYTES = 4 * 64 * NFB * 16 * 4;           // k-half exchange, 147,456 B
+  constexpr int LOOP_BYTES = RING_BYTES + 2 * A_BYTES;
+  constexpr int LDSB = EX_BYTES > LOOP_BYTES ? EX_BYTES : LOOP_BYTES;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDSB];
+  unsigned char* ring = lds;
+  unsigned char* abuf = lds + RING_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid >> 2, wn = wid & 3;
+  const int Wp = W + 2, HWp = H * Wp;
+  const int SR = (kW64BK + 2 * Wp + 2 + 7) & ~7;            // strip rows (8-row aligned)
+  const float invWp = 1.f / (float)Wp;
+  const int kt_begin = blockIdx.x * kps;
+  const int kt_end = kt_begin + kps < total_kt ? kt_begin + kps : total_kt;
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  // one 8-row DMA group of strip rows [P, P + 8) of image n into the ring (P % 8 == 0)
+  auto strip_group = [&](int n, int P) {
+    const int row = P + lrow;
+    const int pos = row & (kW64Ring - 1);
+    const int chunk = (tr_swz<RB>(pos, pch) - pos * RB) >> 4;
+    const int hp = fdiv(row, Wp, invWp), wp = row - hp * Wp;
+    const bool ok = hp >= 1 && hp <= H && wp >= 1 && wp <= W;
+    const void* src = ok ? (const void*)(x + (((int64_t)n * H + hp - 1) * W + wp - 1) * 64 + chunk * 8)
+                         : (const void*)g_zero16;
+    glds16(src, ring + (P & (kW64Ring - 1)) * RB);
+  };
+  // the 8 dY row groups of K-tile (n, q0)
+  auto a_tile = [&](int n, int q0, int buf) {  // 8 row groups: one per wave
+    const int row = wid * 8 + lrow;
+    const int chunk = (tr_swz<RB>(row, pch) - row * RB) >> 4;
+    const int qq = q0 + row;
+    const int h_ = fdiv(qq, Wp, invWp), w_ = qq - h_ * Wp;
+    const bool ok = qq < HWp && w_ < W;
+    const void* src = ok ? (const void*)(dy + (((int64_t)n * H + h_) * W + w_) * 64 + chunk * 8)
+                         : (const void*)g_zero16;
+    glds16(src, abuf + buf * A_BYTES + wid * 1024);
+  };
+
+  // loop-invariant transposed-read offsets.  A (dY image, 64 co): k rows wk*32 + ...
+  unsigned alo[2], ahi[2];
+  {
+    const int kb = wk * 32 + (lane >> 4) * 8;
+    tr_offsets<RB>(kb, 0, lane, alo[0], ahi[0]);
+    tr_offsets<RB>(kb, 32, lane, alo[1], ahi[1]);
+  }
+  // B (strip ring): column block cb = wn * 9 + j -> tap = cb / 4, ci block cb % 4; the
+  // offsets at ring base 0 - a K-tile adds base * 128 and wraps at 32 KB
+  unsigned blo[NFB], bhi[NFB];
+#pragma unroll
+  for (int j = 0; j < NFB; ++j) {
+    const int cb = wn * NFB + j, tap = cb >> 2, cib = cb & 3;
+    const int kb = wk * 32 + (lane >> 4) * 8 + (tap / 3) * Wp + (tap % 3);
+    tr_offsets<RB>(kb, cib * 16, lane, blo[j], bhi[j]);
+  }
+
+  f32x4_t acc[4][NFB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NFB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  int t = kt_begin;
+  while (t < kt_end) {
+    const int n = t / kpi;
+    const int seg_end = (n + 1) * kpi < kt_end ? (n + 1) * kpi : kt_end;
+    int q0 = (t - n * kpi) * kW64BK;
+    // segment prologue: the whole strip [q0, q0 + SR) and the first dY tile
+    for (int grp = wid; grp * 8 < SR; grp += 8) strip_group(n, q0 + grp * 8);
+    a_tile(n, q0, t & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (; t < seg_end; ++t, q0 += kW64BK) {
+      if (t + 1 < seg_end) {
+        // next K-tile: its dY rows + the 64 strip rows past the frontier q0 + SR
+        a_tile(n, q0 + kW64BK, (t + 1) & 1);
+        strip_group(n, q0 + SR + wid * 8);
+      }
+      const unsigned char* A = abuf + (t & 1) * A_BYTES;
+      const unsigned base = (unsigned)(q0 & (kW64Ring - 1)) * RB;
+      bf16x8 af[4];
+      af[0] = tr_pair(A, alo[0], ahi[0]);
+      af[1] = tr_pair(A, alo[0] ^ 32u, ahi[0] ^ 32u);
+      af[2] = tr_pair(A, alo[1], ahi[1]);
+      af[3] = tr_pair(A, alo[1] ^ 32u, ahi[1] ^ 32u);
+#pragma unroll
+      for (int j = 0; j < NFB; ++j) {
+        const bf16x8 bf = tr_pair(ring, (blo[j] + base) & (RING_BYTES - 1),
+                                  (bhi[j] + base) & (RING_BYTES - 1));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  // k halves: waves wk = 1 hand their accumulators to wk = 0 through LDS
+  float* E = reinterpret_cast<float*>(lds);
+  const int fr = lane & 15, fg = lane >> 4;
+  __syncthreads();
+  if (wk == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NFB; ++j)
+        *reinterpret_cast<f32x4_t*>(E + (((wn * 4 + i) * NFB + j) * 64 + lane) * 4) = acc[i][j];
+  }
+  __syncthreads();
+  if (wk == 0) {
+    float* out = part + (int64_t)blockIdx.x * 9 * 64 * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NFB; ++j) {
+        const f32x4_t o = *reinterpret_cast<const f32x4_t*>(E + (((wn * 4 + i) * NFB + j) * 64 + lane) * 4);
+        const int cb = wn * NFB + j, tap = cb >> 2, ci = (cb & 3) * 16 + fr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = i * 16 + fg * 4 + e;
+          out[((int64_t)tap * 64 + co) * 64 + ci] = acc[i][j][e] + o[e];
+        }
+      }
   }
 }
 
@@ -1103,6 +1279,15 @@ WgTapCfg wg_tap_cfg(int Cin, int Cout, int algo) {
 bool conv3x3_nhwc_supported(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
 
 int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int stride, int algo) {
+  if (algo == 4) {
+    // one 8-wave workgroup per CU; K-tile ranges of whole images where possible (each
+    // image boundary costs a full strip load)
+    const int kpi = (H * (W + 2) + kW64BK - 1) / kW64BK;
+    const int total = N * kpi;
+    int S = N <= 256 ? N : 256;
+    if (S < 1) S = 1;
+    return S > total ? total : S;
+  }
   if (algo == 1) {
     const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;  // K-tiles per image
     const int total = N * kpi;
@@ -1139,7 +1324,12 @@ int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int str
   return best;
 }
 
-bool conv3x3_wgrad_supported(int W, int algo) { return algo != 1 || W <= kWgMaxW; }
+bool conv3x3_wgrad_supported(int W, int algo) { return (algo != 1 && algo != 4) || W <= kWgMaxW; }
+
+// the strip-ring kernel's shapes: 3x3 stride 1, 64 -> 64 channels, W <= 56
+bool conv3x3_wgrad_c64_ok(int W, int Cin, int Cout, int ksize, int stride) {
+  return ksize == 3 && stride == 1 && Cin == 64 && Cout == 64 && W <= kWgMaxW;
+}
 
 int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize) {
   return (int64_t)(S + (S + kRedGroup - 1) / kRedGroup) * ksize * ksize * Cout * Cin;
@@ -1151,7 +1341,13 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
   const auto* dyp = static_cast<const bf16_t*>(dy);
   const auto* xp = static_cast<const bf16_t*>(x);
   const int T = ksize * ksize;
-  if (algo == 1) {
+  if (algo == 4) {
+    const int kpi = (H * (W + 2) + kW64BK - 1) / kW64BK;
+    const int total = N * kpi;
+    const int kps = (total + S - 1) / S;
+    hipLaunchKernelGGL(conv3x3_wgrad_c64_k, dim3((unsigned)S), dim3(512), 0, st, dyp, xp, part,
+                       H, W, kpi, kps, total);
+  } else if (algo == 1) {
     const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;
     const int total = N * kpi;
     const int kps = (total + S - 1) / S;
@@ -1277,7 +1473,7 @@ int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t M = (int64_t)N * Ho * Wo;
   const int big = Cout % 128 == 0 ? conv_bm_choice() : 0;  // launch_conv_tap's M tile
-  const int bm = big == 1 || big == 2 ? 256 : kBM;
+  const int bm = conv_bm_of(big);
   return (int)((M + bm - 1) / bm);
 }
 

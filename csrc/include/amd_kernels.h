@@ -327,9 +327,11 @@ void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, 
                         int Cout, int ksize, hipStream_t st);
 // weight gradient: split-K over output pixels into fp32 partials [S][k*k][Cout][Cin],
 // then a reduce into dW (KRSC, bf16 or fp32).  algo 0 = per-tap MFMA kernel,
-// 1 = all-9-taps strip kernel (3x3 stride 1, W <= 56)
+// 1 = all-9-taps strip kernel (3x3 stride 1, W <= 56), 4 = 64-channel strip-ring kernel
+// (3x3 stride 1, Cin = Cout = 64, W <= 56: conv3x3_wgrad_c64_ok)
 int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int stride, int algo);
 bool conv3x3_wgrad_supported(int W, int algo);
+bool conv3x3_wgrad_c64_ok(int W, int Cin, int Cout, int ksize, int stride);
 int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize);  // floats
 // generic split-K slab reduction: out[co][ci] = sum_s part[s][co][ci] (n % 4 == 0)
 int64_t splitk_reduce_workspace(int S, int64_t n);

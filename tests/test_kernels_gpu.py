@@ -1083,3 +1083,35 @@ def test_legacy_lamb_stages_native_match_cpu(pdt):
     tol2 = dict(rtol=1e-4, atol=2e-5) if pdt == torch.float32 else dict(rtol=1e-2, atol=8e-3)
     for a, b in zip(cpu[1], gpu[1]):
         torch.testing.assert_close(b.float().cpu(), a.to(pdt).float(), **tol2)
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 9), (3, 56, 56), (5, 28, 31), (1, 1, 1), (7, 4, 56),
+                                   (300, 8, 8)])
+def test_conv3x3_wgrad_c64_strip_ring(shape):
+    """64 -> 64 channel 3x3 weight gradient on the strip-ring kernel (algo 4): K-tile
+    ranges crossing image boundaries (segment prologues), the ring wrapping, widths up to
+    56, more images than workgroups; fp32 and bf16 outputs and accumulation into an
+    existing gradient vs the fp32 reference."""
+    from apex_example_amd import _native
+
+    n, h, w = shape
+    torch.manual_seed(11)
+    x = torch.randn(n, 64, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    dy = torch.randn(n, 64, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    wref = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), torch.zeros(64, 64, 3, 3, device=DEV), None, (1, 1), (1, 1),
+        (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    cv = _native.require().conv
+    tol = 1e-3 * wref.abs().max().item()
+    got = cv.conv_wgrad(dy, x, torch.float32, 4)
+    torch.testing.assert_close(got, wref, rtol=1e-4, atol=tol)
+    base = torch.randn_like(wref).contiguous(memory_format=torch.channels_last)
+    acc = base.clone()
+    cv.conv_wgrad(dy, x, torch.float32, 4, out=acc)
+    torch.testing.assert_close(acc, base + wref, rtol=1e-4, atol=tol)
+    got16 = cv.conv_wgrad(dy, x, torch.bfloat16, 4)
+    torch.testing.assert_close(got16.float(), wref, rtol=1e-2, atol=1e-2 * wref.abs().max().item())
+    # the per-tap kernel agrees too (what the model ran before)
+    torch.testing.assert_close(got, cv.conv_wgrad(dy, x, torch.float32, 0), rtol=1e-4, atol=tol)

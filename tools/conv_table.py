@@ -101,9 +101,12 @@ def rows_for(kind, ci, co, H, stride, iters, check):
         ours = {"fwd": lambda: cv.conv_fwd(x, w, stride),
                 "dgrad": (lambda: cv.conv_fwd(dy, wr, 1)) if stride == 1 else
                          (lambda: cv.conv_dgrad_s2(dy, wr, H, H)),
-                "wgrad": lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0, stride)}
+                "wgrad": lambda: cv.conv_wgrad(dy, x, torch.bfloat16,
+                                               C._wgrad3_algo(x, w, stride), stride)}
         libs = {"fwd": {"miopen": lib_conv}, "dgrad": {"miopen": lib_dgrad},
                 "wgrad": {"miopen": lib_wgrad}}
+        if C._wgrad3_algo(x, w, stride) != 0:  # the per-tap kernel it replaced
+            libs["wgrad"]["per-tap"] = lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0, stride)
         refs = {"fwd": lambda: F.conv2d(x.float(), w.float(), stride=stride, padding=1),
                 "dgrad": None, "wgrad": None}
         outs = {"fwd": lambda: ours["fwd"]()}
@@ -157,8 +160,8 @@ def main():
     torch.backends.cudnn.benchmark = False
     rows = []
     print("| layer | calls/step | dir | GFLOP | ours us | TF/s | % peak | MIOpen us | "
-          "hipBLASLt us | winner | rel err |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|")
+          "hipBLASLt us | other | winner | rel err |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     tot = {"ours": 0.0, "best": 0.0}
     for (kind, ci, co, H, s, calls) in LAYERS:
         if a.only and kind != a.only:
@@ -169,9 +172,11 @@ def main():
             lib = r["lib_us"]
             tot["ours"] += calls * r["us"]
             tot["best"] += calls * min([r["us"]] + list(lib.values()))
-            print("| %s | %d | %s | %.1f | %.1f | %.0f | %.1f | %s | %s | %s | %s |" % (
+            other = ", ".join("%s %s" % (k2, v) for k2, v in lib.items()
+                              if k2 not in ("miopen", "hipblaslt")) or "-"
+            print("| %s | %d | %s | %.1f | %.1f | %.0f | %.1f | %s | %s | %s | %s | %s |" % (
                 r["layer"], calls, r["dir"], r["gflop"], r["us"], r["tflops"], r["pct_peak"],
-                lib.get("miopen", "-"), lib.get("hipblaslt", "-"), r["winner"],
+                lib.get("miopen", "-"), lib.get("hipblaslt", "-"), other, r["winner"],
                 "%.1e" % r["rel_err"] if r["rel_err"] is not None else "-"), flush=True)
     print("\nweighted per step (calls x us): ours %.0f us, best-of(ours, libraries) %.0f us" % (
         tot["ours"], tot["best"]))

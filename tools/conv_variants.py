@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""A/B of the implicit-GEMM conv tilings (csrc/hip/conv_igemm.hip launch_conv_tap,
+APEX_AMD_CONV_BM) on every ResNet-50 shape that runs on the 128-multiple path: 3x3
+forward (with the BN-statistics epilogue the model uses) and stride-1 data gradient,
+stride-2 3x3 forward, own-kernel 1x1 forwards.  Interleaved rounds in one process,
+random data; every variant's output must equal the default tiling's bitwise (same
+per-element accumulation order).
+
+    python tools/conv_variants.py [--variants default 256w8 ...] [--rounds 3]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PEAK_TF = 2500.0
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def cl(t):
+    return t.to(memory_format=torch.channels_last)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", nargs="+", default=["default", "256w8", "256w8n2", "128w8"])
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from apex_example_amd import _native
+    from apex_example_amd.ops.conv import _rot_weight
+
+    cv = _native.require().conv
+    dev = "cuda"
+    N = 256
+    cases = []
+    for (c, hw, s) in [(128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2), (256, 28, 2),
+                       (512, 14, 2)]:
+        g = torch.Generator(device=dev).manual_seed(c + hw)
+        x = cl(torch.randn(N, c, hw, hw, device=dev, generator=g).to(torch.bfloat16))
+        w = cl((torch.randn(c, c, 3, 3, device=dev, generator=g) * 0.03).to(torch.bfloat16))
+        ho = hw // s
+        gf = 2.0 * N * ho * ho * c * c * 9 / 1e9
+        shift = torch.zeros(c, device=dev)
+        cases.append(("3x3 fwd+stats %d@%d s%d" % (c, hw, s), gf,
+                      lambda x=x, w=w, s=s, sh=shift: cv.conv_fwd_stats(x, w, s, sh)[0]))
+        if s == 1:
+            dy = cl(torch.randn(N, c, hw, hw, device=dev, generator=g).to(torch.bfloat16))
+            wr = _rot_weight(w)
+            cases.append(("3x3 dgrad %d@%d" % (c, hw), gf,
+                          lambda dy=dy, wr=wr: cv.conv_fwd(dy, wr, 1)))
+    for (ci, co, hw) in [(256, 128, 56), (512, 128, 28), (512, 256, 28), (1024, 256, 14),
+                         (1024, 512, 14), (512, 2048, 7), (2048, 512, 7), (128, 512, 28),
+                         (256, 1024, 14)]:
+        g = torch.Generator(device=dev).manual_seed(ci + co + hw)
+        x = cl(torch.randn(N, ci, hw, hw, device=dev, generator=g).to(torch.bfloat16))
+        w = cl((torch.randn(co, ci, 1, 1, device=dev, generator=g) * 0.03).to(torch.bfloat16))
+        gf = 2.0 * N * hw * hw * ci * co / 1e9
+        cases.append(("1x1 fwd %d->%d@%d" % (ci, co, hw), gf,
+                      lambda x=x, w=w: cv.conv_fwd(x, w, 1)))
+    res = {(n, v): [] for n, _, _ in cases for v in a.variants}
+    bad = []
+    for name, gf, fn in cases:
+        os.environ.pop("APEX_AMD_CONV_BM", None)
+        ref = fn().clone()
+        for v in a.variants:
+            if v != "default":
+                os.environ["APEX_AMD_CONV_BM"] = v
+            else:
+                os.environ.pop("APEX_AMD_CONV_BM", None)
+            if not torch.equal(fn(), ref):
+                bad.append((name, v))
+    for _ in range(a.rounds):
+        for name, gf, fn in cases:
+            for v in a.variants:
+                if v != "default":
+                    os.environ["APEX_AMD_CONV_BM"] = v
+                else:
+                    os.environ.pop("APEX_AMD_CONV_BM", None)
+                res[(name, v)].append(timeit(fn, a.iters))
+    os.environ.pop("APEX_AMD_CONV_BM", None)
+    print("| conv | GFLOP | " + " | ".join(a.variants) + " |")
+    print("|---|---|" + "---|" * len(a.variants))
+    for name, gf, _ in cases:
+        cells = []
+        for v in a.variants:
+            t = min(res[(name, v)])
+            cells.append("%.1f us (%.0f TF, %.0f%%)" % (t, gf / t * 1e3, gf / t * 1e3 / PEAK_TF * 100))
+        print("| %s | %.1f | %s |" % (name, gf, " | ".join(cells)), flush=True)
+    print("\nmismatches vs default:", bad if bad else "none")
+
+
+if __name__ == "__main__":
+    main()
