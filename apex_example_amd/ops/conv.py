@@ -17,6 +17,7 @@ per chunk.
 """
 from __future__ import annotations
 
+import collections
 import os
 import threading
 
@@ -75,14 +76,30 @@ def _side_mode(params):
 # 8949 without (same box; the side stream ends backward ~5 ms behind the compute
 # stream, and the last buckets wait for it: exposed tail 5.2 vs 0.06 ms).
 _DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "0") == "1"
+# Bounded side-stream lag: the main stream waits for the weight gradient enqueued
+# APEX_AMD_WGRAD_LAG launches earlier (0 = unbounded; default 4 under DDP, where the last
+# buckets cannot launch before the side stream reaches their gradients), and
+# APEX_AMD_WGRAD_STREAM_PRIO=high creates the side stream with high priority (its weight
+# gradients then run ahead of the data-gradient chain instead of trailing it).
+_LAG = int(os.environ.get("APEX_AMD_WGRAD_LAG", "-1"))
+_SIDE_PRIO = os.environ.get("APEX_AMD_WGRAD_STREAM_PRIO", "normal")
+_SIDE_EVENTS = {}   # device index -> deque of side-stream events, oldest first
 
 
 def _join_side():
     with _LOCK:
         pending = list(_JOIN.items())
         _JOIN.clear()
+        for idx, _ in pending:
+            _SIDE_EVENTS.pop(idx, None)
     for idx, (main, _task) in pending:
         main.wait_stream(_SIDE[idx])
+
+
+def _lag_for(mode):
+    if _LAG >= 0:
+        return _LAG
+    return 4 if mode == "ddp" else 0
 
 
 def join_side_streams():
@@ -105,7 +122,8 @@ class _SideWgrad:
             self.main = torch.cuda.current_stream(dev)
             self.side = _SIDE.get(dev.index)
             if self.side is None:
-                self.side = _SIDE[dev.index] = torch.cuda.Stream(dev)
+                prio = torch.cuda.Stream.priority_range()[1] if _SIDE_PRIO == "high" else 0
+                self.side = _SIDE[dev.index] = torch.cuda.Stream(dev, priority=prio)
             self.ev = self.main.record_event()
 
     def run(self, fn, *used):
@@ -133,11 +151,22 @@ class _SideWgrad:
         # callbacks ran leaves a stale entry behind; the next pass sees another task id
         # and queues its own callback, which joins everything pending
         task = torch._C._current_graph_task_id()
+        lag = _lag_for(self.mode)
+        wait_ev = None
         with _LOCK:
             ent = _JOIN.get(idx)
             fresh = ent is None or ent[1] != task
             if fresh:
                 _JOIN[idx] = (self.main, task)
+                _SIDE_EVENTS.pop(idx, None)
+            if lag > 0:
+                q = _SIDE_EVENTS.setdefault(idx, collections.deque())
+                q.append(self.side.record_event())
+                if len(q) > lag:
+                    wait_ev = q.popleft()
+        if wait_ev is not None:
+            # the main stream may run at most `lag` weight gradients ahead of the side stream
+            self.main.wait_event(wait_ev)
         if fresh:
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
         if self.mode == "ddp":

@@ -24,6 +24,12 @@ under 20 % of t (link-rate), and the LAST bucket's t is exposed after backward,
 so buckets much above ~64 MB lengthen the tail.  32 MiB sits in that window for
 1..8 ranks; see tools/allreduce_sweep.py to refit a and B on a node.
 
+Tapered tail (``tapered_buckets``, default on; env ``APEX_AMD_DDP_TAPER=0`` for Apex's
+plain size cut): buckets are cut from the END of the gradient-arrival order with limits
+message_size/16, /8, /4, /2, then message_size - the buckets that can only launch when
+backward ends (the first layers' gradients arrive last) are small, so the exposed
+all-reduce tail is short, and the early gradients still travel in full buckets.
+
 Communicators (RCCL): the buckets go to a DEDICATED process group whose HIP
 streams are created high-priority (``ProcessGroupNCCL.Options
 (is_high_priority_stream=True)``), not to the default group: bucket
@@ -50,6 +56,7 @@ docs/DDP_TUNING.md records the measurements behind the default.
 from __future__ import annotations
 
 import contextlib
+import os
 import warnings
 
 import torch
@@ -178,7 +185,8 @@ class DistributedDataParallel(Module):
                  allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
                  process_group=None, allow_unused=False, bucket_align=64, use_avg_op=None,
-                 high_priority_streams=True, force_collectives=False, bf16_wire=None):
+                 high_priority_streams=True, force_collectives=False, bf16_wire=None,
+                 tapered_buckets=None):
         super().__init__()
         if not dist.is_initialized():
             raise RuntimeError("DistributedDataParallel requires torch.distributed to be "
@@ -213,10 +221,12 @@ class DistributedDataParallel(Module):
             use_avg_op = self.backend == "nccl"
         self.use_avg_op = bool(use_avg_op)
         self.force_collectives = bool(force_collectives)
-        import os
         self.bf16_wire = bf16_wire or os.environ.get("APEX_AMD_DDP_BF16_WIRE", "rsag")
         if self.bf16_wire not in ("rsag", "fp32", "native"):
             raise ValueError("bf16_wire must be 'rsag', 'fp32' or 'native'")
+        if tapered_buckets is None:
+            tapered_buckets = os.environ.get("APEX_AMD_DDP_TAPER", "1") == "1"
+        self.tapered_buckets = bool(tapered_buckets)
         self._trigger_params = allreduce_trigger_params
         self.custom_allreduce_triggers = allreduce_trigger_params is not None
 
@@ -286,7 +296,6 @@ class DistributedDataParallel(Module):
         2 bf16 buckets as an fp32 all-reduce, 3 bf16 buckets as an fp32 reduce-scatter
         + bf16 all-gather (fp16 / fp32 buckets native in 2 and 3)."""
         if self.allreduce_always_fp32 is None:
-            import os
             env = os.environ.get("APEX_AMD_DDP_FP32")  # A/B override of the auto rule
             if env in ("0", "1", "2", "3"):
                 return int(env)
@@ -330,6 +339,8 @@ class DistributedDataParallel(Module):
                                          self.gradient_average, self.delay_allreduce,
                                          self.use_avg_op, triggers, int(self.bucket_align))
         self.reducer.set_allow_unused(self.allow_unused)
+        if not self.tapered_buckets:
+            self.reducer.set_tapered(False)
         self.reducer.set_force_collectives(self.force_collectives)
         self.reducer.set_prof(bool(self.prof))
         if self._bucket_pgs:

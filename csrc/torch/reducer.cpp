@@ -301,6 +301,15 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   // ---- python-facing helpers ---------------------------------------------
   void set_enabled(bool e) { enabled_ = e; }
+  // tapered tail buckets on / off (rebuilds the layout in the current order)
+  void set_tapered(bool t) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (t == tapered_) return;
+    tapered_ = t;
+    std::vector<int64_t> order = current_order();
+    build_layout(order);
+    if (timing_) ensure_events();
+  }
   // apex num_allreduce_streams / allreduce_communicators: bucket b goes to
   // bucket_pgs[b % n] (separate RCCL communicators -> separate streams).
   void set_bucket_process_groups(std::vector<c10::intrusive_ptr<c10d::ProcessGroup>> pgs) {
@@ -390,9 +399,55 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     grad = v;
   }
 
-  void build_layout(const std::vector<int64_t>& order) {
-    std::vector<Bucket> nb;
-    std::vector<int64_t> bucket_of(params_.size(), -1), offset_of(params_.size(), 0);
+  // Tapered tail (default; no custom triggers): per dtype the buckets are cut from the
+  // END of the arrival order with limits message_size/16, /8, /4, /2, then message_size,
+  // so the buckets that can only launch as backward ends (the first layers' gradients
+  // arrive last) are small and their all-reduce - the exposed tail - is short, while the
+  // early gradients still travel in full-size buckets.  Buckets launch in the order their
+  // LAST gradient arrives.
+  void build_tapered(const std::vector<int64_t>& order, std::vector<Bucket>& nb) {
+    std::map<at::ScalarType, std::vector<int64_t>> by_type;
+    std::vector<int64_t> pos(params_.size(), 0);
+    for (size_t k = 0; k < order.size(); ++k) {
+      pos[(size_t)order[k]] = (int64_t)k;
+      by_type[params_[(size_t)order[k]].scalar_type()].push_back(order[k]);
+    }
+    for (auto& kv : by_type) {
+      const std::vector<int64_t>& ps = kv.second;
+      std::vector<std::vector<int64_t>> groups;  // from the end of the order
+      int64_t limit = std::max<int64_t>(1, message_size_ / 16), acc = 0;
+      std::vector<int64_t> cur;
+      for (auto it = ps.rbegin(); it != ps.rend(); ++it) {
+        cur.push_back(*it);
+        acc += params_[(size_t)*it].numel();
+        if (acc >= limit) {
+          groups.push_back(cur);
+          cur.clear();
+          acc = 0;
+          limit = std::min<int64_t>(message_size_, limit * 2);
+        }
+      }
+      if (!cur.empty()) groups.push_back(cur);
+      for (auto g = groups.rbegin(); g != groups.rend(); ++g) {
+        Bucket b;
+        b.dtype = kv.first;
+        for (auto it = g->rbegin(); it != g->rend(); ++it) {  // arrival order inside
+          int64_t off = (b.numel + align_ - 1) / align_ * align_;
+          b.params.push_back(*it);
+          b.offsets.push_back(off);
+          b.numel = off + params_[(size_t)*it].numel();
+        }
+        nb.push_back(std::move(b));
+      }
+    }
+    std::stable_sort(nb.begin(), nb.end(), [&](const Bucket& a, const Bucket& b) {
+      return pos[(size_t)a.params.back()] < pos[(size_t)b.params.back()];
+    });
+  }
+
+  // Apex's rule: per dtype, close a bucket once it holds message_size elements or at an
+  // allreduce trigger parameter
+  void build_sized(const std::vector<int64_t>& order, std::vector<Bucket>& nb) {
     std::map<at::ScalarType, Bucket> open;
     auto close = [&](at::ScalarType t) {
       auto it = open.find(t);
@@ -419,7 +474,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     }
     std::sort(rest.begin(), rest.end());
     for (auto& r : rest) close(r.second);
+  }
 
+  void build_layout(const std::vector<int64_t>& order) {
+    std::vector<Bucket> nb;
+    std::vector<int64_t> bucket_of(params_.size(), -1), offset_of(params_.size(), 0);
+    if (tapered_ && triggers_.empty()) build_tapered(order, nb);
+    else build_sized(order, nb);
     std::vector<at::Tensor> new_views(params_.size());
     for (size_t b = 0; b < nb.size(); ++b) {
       Bucket& B = nb[b];
@@ -453,6 +514,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     buckets_ = std::move(nb);
     bucket_of_ = std::move(bucket_of);
     views_ = std::move(new_views);
+  }
+
+  std::vector<int64_t> current_order() const {
+    std::vector<int64_t> order;
+    for (const auto& b : buckets_)
+      for (int64_t i : b.params) order.push_back(i);
+    return order;
   }
 
   void rebuild_from_arrival() {
@@ -661,6 +729,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<char> async_marked_;
   std::vector<char> no_direct_;
   int64_t iteration_ = 0;
+  bool tapered_ = true;
   int64_t next_ = 0;
   bool refresh_ = true;
   bool enabled_ = true;
@@ -811,6 +880,7 @@ void register_reducer(pybind11::module_& m) {
       .def("async_ready_ok", &Reducer::async_ready_ok)
       .def("mark_ready_direct", &Reducer::mark_ready_direct)
       .def("set_no_direct", &Reducer::set_no_direct)
+      .def("set_tapered", &Reducer::set_tapered)
       .def("direct_ok", &Reducer::direct_ok)
       .def("iteration", &Reducer::iteration)
       .def("force_collectives", &Reducer::force_collectives)

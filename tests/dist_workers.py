@@ -271,6 +271,25 @@ def ddp_direct_shared(rank, world, case="twice", iters=3):
             "direct_ok": {k: bool(red.direct_ok(idx[id(p)])) for k, p in net.named_parameters()}}
 
 
+def ddp_layout(rank, world, tapered=True, message_size=4000):
+    """Bucket layout (in launch order) and numels of a chain of linear layers whose
+    gradients arrive last-layer first, plus the gradients of one backward."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    layers = [nn.Linear(32, 32) for _ in range(12)]
+    net = nn.Sequential(*layers)
+    ddp = DistributedDataParallel(net, message_size=message_size, tapered_buckets=tapered)
+    x = torch.randn(4, 32, generator=torch.Generator().manual_seed(rank))
+    for _ in range(2):  # iteration 1 records the arrival order, 2 runs the new layout
+        for p in net.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        ddp(x).square().sum().backward()
+    return {"numels": [int(n) for n in ddp.reducer.bucket_numels()],
+            "grads": [p.grad.clone() for p in net.parameters()]}
+
+
 def ddp_train_amp(rank, world, inject_rank=-1):
     """amp O2 (bf16, CPU) + DDP + FusedSGD: training + overflow consensus."""
     from apex_example_amd import amp

@@ -266,3 +266,22 @@ def test_ddp_direct_path_functional_second_use(tmp_path):
                 for k in ref:
                     torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6)
         assert r["direct_ok"]["a"] is False
+
+
+def test_ddp_tapered_tail_buckets(tmp_path):
+    """Tapered layout: the buckets cut from the end of the arrival order grow from
+    message_size/16 to message_size, so the last-launched bucket (the first layers'
+    gradients, which arrive last) is small; gradients are identical to Apex's plain
+    size cut."""
+    (tmp_path / "t").mkdir()
+    (tmp_path / "p").mkdir()
+    tap = W.run("ddp_layout", 2, str(tmp_path / "t"), tapered=True)
+    plain = W.run("ddp_layout", 2, str(tmp_path / "p"), tapered=False)
+    nt, npl = tap[0]["numels"], plain[0]["numels"]
+    assert nt[-1] <= 4000 // 16 + 1056 + 64   # one layer past the /16 limit, aligned
+    assert nt[-1] < npl[-1] or len(npl) == 1
+    assert len(nt) > len(npl)
+    assert sum(nt) >= 12 * 1056
+    for a, b in zip(tap, plain):
+        for x, y in zip(a["grads"], b["grads"]):
+            torch.testing.assert_close(x, y)
