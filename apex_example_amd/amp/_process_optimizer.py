@@ -48,18 +48,29 @@ def _zero_or_none(params):
 
     Apex sets them to None (grad copy elision).  Grads that are DDP bucket views
     are zeroed in place instead so they stay views (one launch for all)."""
-    views = []
+    vparams = []
     for p in params:
         if p.grad is None:
             continue
         if getattr(p, "_amd_grad_is_bucket_view", False):
-            views.append(p.grad)
+            vparams.append(p)
         else:
             p.grad = None
+    views = _lazy_zero(vparams)
     if views:
         from .. import amp_C
 
         amp_C.multi_tensor_zero(65536, None, [views])
+
+
+def _lazy_zero(params):
+    """Bucket-view grads zeroed lazily by their DDP reducer where it allows (the grads are
+    detached and the next backward overwrites the views, ops/_ddp_direct.py); returns
+    the grads that still need a zero kernel."""
+    if not params:
+        return []
+    from ..ops import _ddp_direct
+    return _ddp_direct.lazy_zero(params)
 
 
 def _stash_grad(stash, param):
@@ -377,12 +388,16 @@ def _process_optimizer(optimizer, properties):
             stash = self._amp_stash
             self._amp_lazy_init()
             # Zero the model grads.
-            views = []
+            views, vparams = [], []
             for param in stash.all_fp16_params + stash.all_fp32_from_fp32_params:
                 if param.grad is not None:
                     if param.grad.requires_grad:  # (bucket views never require grad)
                         param.grad = param.grad.detach()
-                    views.append(param.grad)
+                    if getattr(param, "_amd_grad_is_bucket_view", False):
+                        vparams.append(param)
+                    else:
+                        views.append(param.grad)
+            views.extend(_lazy_zero(vparams))
             if views:
                 from .. import amp_C
 

@@ -153,12 +153,13 @@ def _splitk_chunks(T, o, i, in_dtype, out_dtype):
 _ADDMM_F32 = os.environ.get("APEX_AMD_ADDMM_F32", "1") == "1"
 
 
-def _wgrad(dy2, x2, dtype, out=None):
+def _wgrad(dy2, x2, dtype, out=None, accumulate=True):
     """dW = dy2^T x2 written in the parameter's dtype by the GEMM itself (amp O1:
     fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW); split-K over
     the tokens when the output has too few tiles to fill the GPU.  ``out``: accumulate
     into that [o, i]-contiguous tensor (a DDP bucket view, see _direct_slots) and
-    return it - the slab reduction or the GEMM's beta = 1 does the add."""
+    return it - the slab reduction or the GEMM's beta = 1 does the add; with
+    ``accumulate=False`` (a lazily zeroed bucket view) overwrite it (beta = 0)."""
     if (_DENSE_SPLITK and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
             and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
             and _native.available()):
@@ -169,23 +170,29 @@ def _wgrad(dy2, x2, dtype, out=None):
             a = dy2.view(S, T // S, o).transpose(1, 2)
             b = x2.view(S, T // S, i)
             part = torch.bmm(a, b, out_dtype=torch.float32)
-            return _native.require().conv.splitk_reduce(part, dtype, out=out)
+            return _native.require().conv.splitk_reduce(part, dtype, out=out,
+                                                        accumulate=accumulate)
     if dtype != dy2.dtype and dy2.is_cuda and dtype == torch.float32:
         global _ADDMM_F32
         if out is not None and _ADDMM_F32:
-            # fp32 C += fp16 A @ B in the GEMM (beta = 1), no separate add pass
+            # fp32 C (+)= fp16 A @ B in the GEMM (beta = 1 / 0), no separate add pass
             o2 = out.view(dy2.size(1), x2.size(1))
             try:
-                torch.addmm(o2, dy2.t(), x2, out_dtype=torch.float32, out=o2)
+                torch.addmm(o2, dy2.t(), x2, beta=1 if accumulate else 0,
+                            out_dtype=torch.float32, out=o2)
                 return out
             except (RuntimeError, TypeError):
                 _ADDMM_F32 = False
         r = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
-        return r if out is None else out.add_(r.view_as(out))
+        if out is None:
+            return r
+        return out.add_(r.view_as(out)) if accumulate else out.copy_(r.view_as(out))
     if out is not None:
         if out.dtype == dy2.dtype:
-            return out.view(dy2.size(1), x2.size(1)).addmm_(dy2.t(), x2).view_as(out)
-        return out.add_((dy2.t() @ x2).view_as(out))
+            return out.view(dy2.size(1), x2.size(1)).addmm_(
+                dy2.t(), x2, beta=1 if accumulate else 0).view_as(out)
+        r = (dy2.t() @ x2).view_as(out)
+        return out.add_(r) if accumulate else out.copy_(r)
     return dy2.t() @ x2
 
 
@@ -196,10 +203,13 @@ def _direct_slots(side, weight, w_dtype):
     `profiles/gpt2_medium_forced_collectives_r3.md`), else None."""
     if side is None or side.on or weight is None:
         return None
-    g = weight.grad
+    sl = _ddp_direct.slots(weight)
+    if sl is None:
+        return None
+    g, _acc = _ddp_direct.grad_target(weight)
     if g is None or not g.is_cuda or g.dtype != w_dtype or not g.is_contiguous():
         return None
-    return _ddp_direct.slots(weight)
+    return sl
 
 
 def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):
@@ -208,7 +218,8 @@ def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):
     direct = _direct_slots(side, weight, w_dtype)
     if direct is None:
         return side.run(lambda: _wgrad(dy2, x2, w_dtype), dy2, *used)
-    _wgrad(dy2, x2, w_dtype, out=weight.grad)
+    tgt, acc = _ddp_direct.grad_target(weight)
+    _wgrad(dy2, x2, w_dtype, out=tgt, accumulate=acc)
     _ddp_direct.mark_ready(direct)
     return None
 

@@ -26,6 +26,8 @@ import os
 import torch
 
 _ON = os.environ.get("APEX_AMD_DDP_DIRECT_GRAD", "1") == "1"
+# lazy zeroing of bucket-view gradients (APEX_AMD_DDP_LAZY_ZERO=0: a zero kernel per step)
+_LAZY = os.environ.get("APEX_AMD_DDP_LAZY_ZERO", "1") == "1"
 
 
 def note_use(*params):
@@ -46,13 +48,16 @@ def note_use(*params):
 
 
 def slot(p):
-    """(reducer, index) when ``p.grad`` is a bucket view its reducer will take an early
-    ready mark for this iteration and ``p`` had exactly one counted forward use, else None."""
+    """(reducer, index) when ``p.grad`` is a bucket view (or the bucket view was lazily
+    zeroed, ``grad_target``) its reducer will take an early ready mark for this iteration
+    and ``p`` had exactly one counted forward use, else None."""
     s = getattr(p, "_amd_ddp_slot", None) if p is not None else None
-    if s is None or p.grad is None:
+    if s is None:
         return None
     red = s[0]()
     if red is None or not red.async_ready_ok() or not red.direct_ok(s[1]):
+        return None
+    if p.grad is None and red.lazy_view(s[1]) is None:
         return None
     u = getattr(p, "_amd_ddp_uses", None)
     if u is None or u[1] != 1 or u[0] != red.iteration():
@@ -74,6 +79,38 @@ def slots(*params):
     if params[0].is_cuda and torch.cuda.is_current_stream_capturing():
         return None
     return out
+
+
+def grad_target(p):
+    """(tensor, accumulate) where a direct-path kernel puts ``p``'s gradient (after
+    ``slot(p)`` succeeded): ``p.grad`` to accumulate into, or - the bucket was lazily
+    zeroed by the optimizer's zero_grad (csrc/torch/reducer.cpp lazy_zero) - the stale
+    bucket view to OVERWRITE (beta = 0; no memset of the buckets per step)."""
+    g = p.grad
+    if g is not None:
+        return g, True
+    s = p._amd_ddp_slot
+    return s[0]().lazy_view(s[1]), False
+
+
+def lazy_zero(params):
+    """zero_grad for bucket-view gradients: detach them from their views and mark the
+    views stale (the reducer's lazy_zero) where the reducer sees the next backward
+    through; returns the gradients that still need a zeroing kernel."""
+    rest = []
+    by_red = {}
+    for p in params:
+        s = getattr(p, "_amd_ddp_slot", None) if _LAZY else None
+        red = s[0]() if s is not None else None
+        if red is None or p.grad is None or not red.lazy_zero_ok():
+            if p.grad is not None:
+                rest.append(p.grad)
+            continue
+        ent = by_red.setdefault(id(red), (red, []))
+        ent[1].append(s[1])
+    for red, idx in by_red.values():
+        red.lazy_zero(idx)
+    return rest
 
 
 def mark_ready(sl):

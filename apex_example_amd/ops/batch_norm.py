@@ -200,6 +200,20 @@ def _gather_slot(C, world, rank, device):
     return gathered, gathered[rank * n:(rank + 1) * n]
 
 
+def _direct_targets(params, need_w):
+    """(slots, dgamma target, dbeta target, accumulate) of the DDP direct path for a BN's
+    affine pair, or (None, None, None, True): both targets must be bucket views in the
+    same state (accumulated or lazily zeroed)."""
+    direct = _ddp_direct.slots(*params) if need_w else None
+    if direct is None:
+        return None, None, None, True
+    tw, aw = _ddp_direct.grad_target(params[0])
+    tb, ab = _ddp_direct.grad_target(params[1])
+    if aw != ab:
+        return None, None, None, True
+    return direct, tw, tb, aw
+
+
 def bn_src_of(x):
     """The BnBwdSrc of ``x`` when x is a fused BN's output (else None)."""
     return getattr(x, "_amd_bn_src", None)
@@ -385,11 +399,11 @@ class BatchNormFunction(torch.autograd.Function):
             # g) and summed (g, g*(x-mean)) per tile: no reduction pass, no dz store
             FUSED_BWD_CALLS[0] += 1
             if ctx.world > 1:
-                direct = _ddp_direct.slots(*ctx.params) if need_w else None
-                tw, tb = (ctx.params[0].grad, ctx.params[1].grad) if direct else (None, None)
+                direct, tw, tb, acc = _direct_targets(ctx.params, need_w)
                 sum_dy, sum_dy_xmu, gw, gb = C.slab_reduce_grad(res[1], invstd, weight, need_w,
                                                                sum_scale=ctx.total,
-                                                               grad_weight=tw, grad_bias=tb)
+                                                               grad_weight=tw, grad_bias=tb,
+                                                               accumulate=acc)
                 if direct:
                     # dgamma / dbeta accumulated into the DDP bucket views by the finalize
                     _ddp_direct.mark_ready(direct)
@@ -409,12 +423,11 @@ class BatchNormFunction(torch.autograd.Function):
             # SyncBN: the reduce writes (sum_dy | sum_dy_xmu) / global_count into one [2C]
             # buffer (the scale is a device scalar from the forward's combine) -> ONE
             # in-place all_reduce yields the global means -> elementwise pass
-            direct = _ddp_direct.slots(*ctx.params) if need_w else None
-            tw, tb = (ctx.params[0].grad, ctx.params[1].grad) if direct else (None, None)
+            direct, tw, tb, acc = _direct_targets(ctx.params, need_w)
             sum_dy, sum_dy_xmu, gw, gb = C.reduce_grad(dyl, xl, mean, invstd, weight, bias, zl,
                                                        ctx.fuse_relu, need_w, mask=mask,
                                                        sum_scale=ctx.total, grad_weight=tw,
-                                                       grad_bias=tb)
+                                                       grad_bias=tb, accumulate=acc)
             if direct:
                 _ddp_direct.mark_ready(direct)
                 need_w = False

@@ -140,7 +140,11 @@ class _SideWgrad:
                 with torch.no_grad():
                     for p, g in zip(self.params, outs):
                         if g is not None and g is not p.grad:  # (not already accumulated)
-                            p.grad.add_(g)
+                            tgt, acc = _ddp_direct.grad_target(p)
+                            if acc:
+                                tgt.add_(g)
+                            else:  # a lazily zeroed bucket view: overwrite
+                                tgt.copy_(g)
         for t in used:
             t.record_stream(self.side)
         for t in outs:
@@ -204,9 +208,10 @@ def _split_k(m):
     return s
 
 
-def wgrad_1x1(dy_rows, x_rows, out_dtype, out=None):
+def wgrad_1x1(dy_rows, x_rows, out_dtype, out=None, accumulate=True):
     """dW[co, ci] = dy_rows^T @ x_rows, split-K over the rows (fp32 partials).  ``out``:
-    accumulate into that [co, ci]-contiguous gradient (a DDP bucket view) instead."""
+    accumulate into that [co, ci]-contiguous gradient (a DDP bucket view) instead, or
+    overwrite it (``accumulate=False``: a lazily zeroed bucket view)."""
     m, co = dy_rows.shape
     ci = x_rows.shape[1]
     S = _split_k(m)
@@ -220,11 +225,14 @@ def wgrad_1x1(dy_rows, x_rows, out_dtype, out=None):
                 and (co * ci) % 4 == 0):
             # one two-stage slab reduction writing the weight dtype directly
             r = _native.require().conv.splitk_reduce(
-                part, out_dtype, out.view(co, ci) if out is not None else None)
+                part, out_dtype, out.view(co, ci) if out is not None else None, accumulate)
             return out if out is not None else r
         r = part.sum(0).to(out_dtype)
     if out is not None:
-        out.view(co, ci).add_(r)
+        if accumulate:
+            out.view(co, ci).add_(r)
+        else:
+            out.view(co, ci).copy_(r)
         return out
     return r
 
@@ -406,9 +414,10 @@ class Conv1x1GemmFunction(torch.autograd.Function):
         ctx.src = None
         if ctx.needs_input_grad[1]:
             direct = None if side.on else _ddp_direct.slots(weight)
-            if direct is not None and weight.grad.is_contiguous():
+            tgt, acc = _ddp_direct.grad_target(weight) if direct is not None else (None, True)
+            if direct is not None and tgt.is_contiguous():
                 # accumulate straight into the DDP bucket view, no autograd add kernel
-                wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=weight.grad)
+                wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=tgt, accumulate=acc)
                 _ddp_direct.mark_ready(direct)
             else:
                 so = _side_out(side, weight)
@@ -466,8 +475,9 @@ class Conv1x1SkipFunction(torch.autograd.Function):
                 dx = dx2.view(n, h, w, ci).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and dy is not None:
             direct = None if side.on else _ddp_direct.slots(weight)
-            if direct is not None and weight.grad.is_contiguous():
-                wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=weight.grad)
+            tgt, acc = _ddp_direct.grad_target(weight) if direct is not None else (None, True)
+            if direct is not None and tgt.is_contiguous():
+                wgrad_1x1(_as_rows(dy), _as_rows(x), weight.dtype, out=tgt, accumulate=acc)
                 _ddp_direct.mark_ready(direct)
             else:
                 so = _side_out(side, weight)
@@ -503,9 +513,9 @@ class Conv1x1Stride2Function(torch.autograd.Function):
             dx = cv.conv_dgrad_s2(dy, _transpose_1x1(weight), x.size(2), x.size(3))
         if ctx.needs_input_grad[1]:
             direct = None if side.on else _ddp_direct.slots(weight)
-            if direct is not None and weight.grad.is_contiguous(
-                    memory_format=torch.channels_last):
-                cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1, out=weight.grad)
+            tgt, acc = _ddp_direct.grad_target(weight) if direct is not None else (None, True)
+            if direct is not None and tgt.is_contiguous(memory_format=torch.channels_last):
+                cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1, out=tgt, accumulate=acc)
                 _ddp_direct.mark_ready(direct)
             else:
                 so = _side_out(side, weight, cl=True)
@@ -657,14 +667,15 @@ class Conv3x3Function(torch.autograd.Function):
         direct = None
         if ctx.needs_input_grad[1] and own_wgrad and not side.on:
             direct = _ddp_direct.slots(weight)
-            if direct is not None and not weight.grad.is_contiguous(
-                    memory_format=torch.channels_last):
-                direct = None
+            if direct is not None:
+                tgt, acc = _ddp_direct.grad_target(weight)
+                if not tgt.is_contiguous(memory_format=torch.channels_last):
+                    direct = None
         if direct is not None:
             # accumulate straight into the DDP bucket view, no autograd add kernel
             cv.conv_wgrad(dy, x, weight.dtype,
                           _wgrad3_algo(x, weight, stride) if _WGRAD3 == "tap" else 1,
-                          stride if _WGRAD3 == "tap" else 1, out=weight.grad)
+                          stride if _WGRAD3 == "tap" else 1, out=tgt, accumulate=acc)
             _ddp_direct.mark_ready(direct)
         elif ctx.needs_input_grad[1]:
             so = _side_out(side, weight, cl=True)

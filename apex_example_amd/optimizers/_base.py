@@ -268,17 +268,23 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         (one multi-tensor launch); the amp stash learns that they are zero."""
         if set_to_none is None:
             set_to_none = self.set_grad_none
-        grads = []
+        grads, views = [], []
         for group in self.param_groups:
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if set_to_none and not getattr(p, "_amd_grad_is_bucket_view", False):
+                if getattr(p, "_amd_grad_is_bucket_view", False):
+                    views.append(p)  # zeroed lazily where the DDP reducer allows it
+                    continue
+                if set_to_none:
                     p.grad = None
                     continue
                 if p.grad.requires_grad:
                     p.grad = p.grad.detach()
                 grads.append(p.grad)
+        if views:
+            from ..ops import _ddp_direct
+            grads.extend(_ddp_direct.lazy_zero(views))
         if grads:
             _native.require().mt.zero(grads)
         stash = self._amp()

@@ -130,9 +130,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);
   conv.def("conv_wgrad", &conv_nhwc_wgrad_op, py::arg("dy"), py::arg("x"), py::arg("out_dtype"),
            py::arg("algo") = 0, py::arg("stride") = 1, py::arg("ksize") = 3,
-           py::arg("out") = py::none());
+           py::arg("out") = py::none(), py::arg("accumulate") = true);
   conv.def("splitk_reduce", &splitk_reduce_op, py::arg("part"), py::arg("out_dtype"),
-           py::arg("out") = py::none());
+           py::arg("out") = py::none(), py::arg("accumulate") = true);
   conv.def("stem_pad", &stem_pad_op);
   conv.def("stem_fwd", &stem_fwd_op);
   conv.def("stem_wgrad", &stem_wgrad_op);
@@ -155,7 +155,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("eps"), py::arg("momentum"));
   bn.def("slab_reduce_grad", &bn_slab_reduce_grad_op, py::arg("slab"), py::arg("invstd"),
          py::arg("weight"), py::arg("need_wgrad"), py::arg("sum_scale") = py::none(),
-         py::arg("grad_weight") = py::none(), py::arg("grad_bias") = py::none());
+         py::arg("grad_weight") = py::none(), py::arg("grad_bias") = py::none(),
+         py::arg("accumulate") = true);
   bn.def("slab_packed_stats", &bn_slab_packed_stats_op, py::arg("slab"), py::arg("count"),
          py::arg("shift"), py::arg("out") = py::none());
   bn.def("set_tuning", &bn_set_tuning, py::arg("red_rpt") = -1, py::arg("red_cap") = -1,
@@ -170,7 +171,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("z"), py::arg("relu"),
          py::arg("need_wgrad"), py::arg("mask") = py::none(),
          py::arg("sum_scale") = py::none(), py::arg("grad_weight") = py::none(),
-         py::arg("grad_bias") = py::none());
+         py::arg("grad_bias") = py::none(), py::arg("accumulate") = true);
   bn.def("local_stats_packed", &bn_local_stats_packed_op, py::arg("x"),
          py::arg("out") = py::none());
   bn.def("combine_stats_sync", &bn_combine_stats_sync_op, py::arg("gathered"), py::arg("eps"),

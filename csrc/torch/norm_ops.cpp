@@ -508,8 +508,9 @@ std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mea
 namespace {
 // dgamma / dbeta destinations: fresh tensors, or caller-given gradients to ACCUMULATE into
 // (DDP bucket views; the finalize adds instead of writing - BNAccumScope)
+// (accumulate = false: the given targets are lazily zeroed DDP bucket views, overwritten)
 bool grad_targets(const OptT& weight, bool need, const OptT& gw_in, const OptT& gb_in,
-                  at::Tensor& gw, at::Tensor& gb) {
+                  at::Tensor& gw, at::Tensor& gb, bool accumulate = true) {
   if (!need || !has(weight)) return false;
   if (has(gw_in) && has(gb_in)) {
     TORCH_CHECK(gw_in->is_cuda() && gb_in->is_cuda() && gw_in->is_contiguous() &&
@@ -520,7 +521,7 @@ bool grad_targets(const OptT& weight, bool need, const OptT& gw_in, const OptT& 
                 "batch norm: grad_weight / grad_bias targets must match the weight");
     gw = *gw_in;
     gb = *gb_in;
-    return true;
+    return accumulate;
   }
   gw = at::empty_like(*weight);
   gb = at::empty_like(*weight);
@@ -530,7 +531,8 @@ bool grad_targets(const OptT& weight, bool need, const OptT& gw_in, const OptT& 
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
-    OptT z, bool relu, bool need_wgrad, OptT mask, OptT sum_scale, OptT gw_in, OptT gb_in) {
+    OptT z, bool relu, bool need_wgrad, OptT mask, OptT sum_scale, OptT gw_in, OptT gb_in,
+    bool accumulate) {
   BNView v = bn_view(x);
   TORCH_CHECK(!has(mask) || x.is_cuda(), "batch norm: ReLU mask is a GPU-path feature");
   if (!x.is_cuda()) {
@@ -568,7 +570,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
   at::Tensor sum_dy = at::empty({v.C}, fopt), sum_dy_xmu = at::empty({v.C}, fopt);
   at::Tensor gw, gb;
   DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
-  const bool accum = grad_targets(weight, need_wgrad, gw_in, gb_in, gw, gb);
+  const bool accum = grad_targets(weight, need_wgrad, gw_in, gb_in, gw, gb, accumulate);
   BNAccumScope accum_scope(accum);
   at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
   at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
@@ -711,7 +713,7 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_op(
     at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale,
-    OptT gw_in, OptT gb_in) {
+    OptT gw_in, OptT gb_in, bool accumulate) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
@@ -725,7 +727,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_o
   at::Tensor sum_dy = packed.narrow(0, 0, C), sum_dy_xmu = packed.narrow(0, C, C);
   at::Tensor gw, gb;
   DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
-  const bool accum = grad_targets(weight, need_wgrad, gw_in, gb_in, gw, gb);
+  const bool accum = grad_targets(weight, need_wgrad, gw_in, gb_in, gw, gb, accumulate);
   BNAccumScope accum_scope(accum);
   const float* scale = nullptr;
   if (has(sum_scale)) {

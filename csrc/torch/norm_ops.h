@@ -61,7 +61,8 @@ std::tuple<at::Tensor, at::Tensor> bn_apply_mask_op(at::Tensor x, at::Tensor mea
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_reduce_grad_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
     OptT z, bool relu, bool need_wgrad, OptT mask,
-    OptT sum_scale, OptT grad_weight = c10::nullopt, OptT grad_bias = c10::nullopt);
+    OptT sum_scale, OptT grad_weight = c10::nullopt, OptT grad_bias = c10::nullopt,
+    bool accumulate = true);
 std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tensor x,
                                                         at::Tensor mean, at::Tensor invstd,
                                                         OptT weight, OptT bias, at::Tensor sum_dy,
@@ -84,7 +85,7 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
                                                           double eps, double momentum);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_op(
     at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale,
-    OptT grad_weight = c10::nullopt, OptT grad_bias = c10::nullopt);
+    OptT grad_weight = c10::nullopt, OptT grad_bias = c10::nullopt, bool accumulate = true);
 at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift,
                                    OptT out = c10::nullopt);
 

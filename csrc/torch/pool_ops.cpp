@@ -216,7 +216,8 @@ at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_
 }
 
 at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
-                              int64_t stride, int64_t ksize, c10::optional<at::Tensor> out) {
+                              int64_t stride, int64_t ksize, c10::optional<at::Tensor> out,
+                              bool accumulate) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16,
@@ -241,10 +242,12 @@ at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dt
                                   (int)stride, (int)algo);
   at::Tensor part = at::empty({conv_wgrad_workspace(S, (int)Cin, (int)Cout, (int)ksize)},
                               x.options().dtype(at::kFloat));
-  // out: accumulate into an existing gradient (a DDP bucket view) instead of a new tensor
-  const bool accum = out.has_value() && out->defined();
+  // out: accumulate into an existing gradient (a DDP bucket view) instead of a new tensor,
+  // or (accumulate = false: a lazily zeroed bucket view) overwrite it
+  const bool given = out.has_value() && out->defined();
+  const bool accum = given && accumulate;
   at::Tensor dw;
-  if (accum) {
+  if (given) {
     dw = *out;
     TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == out_dtype && dw.dim() == 4 &&
                     dw.size(0) == Cout && dw.size(1) == Cin && dw.size(2) == ksize &&
@@ -308,7 +311,7 @@ at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy) {
 }
 
 at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype,
-                            c10::optional<at::Tensor> out_acc) {
+                            c10::optional<at::Tensor> out_acc, bool accumulate) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&
                   part.is_contiguous(), "splitk_reduce: contiguous fp32 [S, M, N] expected");
@@ -317,9 +320,10 @@ at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype,
   at::Tensor stage = at::empty({splitk_reduce_workspace((int)S, M * N)}, part.options());
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "splitk_reduce: out dtype");
   // out_acc: accumulate into an existing [M, N]-contiguous tensor (a DDP bucket view)
-  const bool accum = out_acc.has_value() && out_acc->defined();
+  const bool given = out_acc.has_value() && out_acc->defined();
+  const bool accum = given && accumulate;  // false: overwrite the given tensor
   at::Tensor out;
-  if (accum) {
+  if (given) {
     out = *out_acc;
     TORCH_CHECK(out.is_cuda() && out.scalar_type() == out_dtype && out.numel() == M * N &&
                     out.is_contiguous(),

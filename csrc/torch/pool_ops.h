@@ -30,9 +30,9 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
     c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode);
 at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W);
 at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
-                              int64_t stride, int64_t ksize, c10::optional<at::Tensor> out);
+                              int64_t stride, int64_t ksize, c10::optional<at::Tensor> out, bool accumulate = true);
 at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype,
-                            c10::optional<at::Tensor> out_acc);
+                            c10::optional<at::Tensor> out_acc, bool accumulate = true);
 at::Tensor stem_pad_op(at::Tensor x);
 at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk);
 at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy);

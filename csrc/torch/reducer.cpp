@@ -113,6 +113,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     seen_.assign(params_.size(), 0);
     async_marked_.assign(params_.size(), 0);
     no_direct_.assign(params_.size(), 0);
+    lazy_.assign(params_.size(), 0);
   }
 
   ~Reducer() {
@@ -196,9 +197,50 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   // iterations completed (forward-use counting in ops/_ddp_direct.py keys on it)
   int64_t iteration() const { return iteration_; }
 
+  // Lazy zeroing (the optimizers' zero_grad on bucket-view gradients): instead of a
+  // memset of the buckets, the parameters' .grad are detached from their views and the
+  // views marked stale.  The next backward's first contribution then WRITES the view:
+  // AccumulateGrad stores its tensor as .grad and the ready hook copies it into the view
+  // (the copy replaces the add it would have run), a direct-path kernel writes the view
+  // with beta = 0 (lazy_view()); a parameter without a gradient gets a zeroed view at
+  // the end of backward (allow_unused) as before.  Only while the reducer will see this
+  // backward through (enabled, not delay_allreduce).
+  bool lazy_zero_ok() const { return enabled_ && !delay_; }
+  void lazy_zero(const std::vector<int64_t>& idx) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(lazy_zero_ok(), "lazy_zero: reducer disabled or delaying");
+    for (int64_t i : idx) {
+      TORCH_CHECK(i >= 0 && i < (int64_t)params_.size(), "lazy_zero: bad index");
+      at::Tensor& grad = params_[(size_t)i].mutable_grad();
+      if (grad.defined() && !grad.is_same(views_[(size_t)i])) {
+        // a gradient that is not the view (never attached): zero it the old way
+        c10::NoGradGuard ng;
+        grad.zero_();
+        continue;
+      }
+      grad = at::Tensor();
+      lazy_[(size_t)i] = 1;
+    }
+  }
+  // the stale view of a lazily zeroed parameter, for a direct-path kernel to WRITE
+  // (undefined when the parameter is not lazy: accumulate into .grad instead)
+  at::Tensor lazy_view(int64_t i) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (i < 0 || i >= (int64_t)params_.size() || !lazy_[(size_t)i] ||
+        params_[(size_t)i].grad().defined())
+      return at::Tensor();
+    return views_[(size_t)i];
+  }
+
   void mark_ready_impl(int64_t i, hipStream_t side, bool announced = false,
                        bool with_event = true, bool had_grad = false) {
     std::lock_guard<std::mutex> g(mu_);
+    if (announced && lazy_[(size_t)i] && !params_[(size_t)i].grad().defined()) {
+      // a lazily zeroed parameter announced by a direct-path / side-stream kernel: that
+      // kernel WROTE its view (lazy_view()), so the view becomes the gradient as it is
+      params_[(size_t)i].mutable_grad() = views_[(size_t)i];
+      lazy_[(size_t)i] = 0;
+    }
     if (announced) {
       TORCH_CHECK(!async_marked_[(size_t)i] && !seen_[(size_t)i],
                   "DistributedDataParallel: parameter ", i,
@@ -392,6 +434,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     at::Tensor& p = params_[(size_t)i];
     at::Tensor& grad = p.mutable_grad();
     const at::Tensor& v = views_[(size_t)i];
+    lazy_[(size_t)i] = 0;
     if (grad.defined() && grad.is_same(v)) return;
     c10::NoGradGuard ng;
     if (grad.defined()) v.copy_(grad);
@@ -728,6 +771,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<char> seen_;
   std::vector<char> async_marked_;
   std::vector<char> no_direct_;
+  std::vector<char> lazy_;
   int64_t iteration_ = 0;
   bool tapered_ = true;
   int64_t next_ = 0;
@@ -881,6 +925,9 @@ void register_reducer(pybind11::module_& m) {
       .def("mark_ready_direct", &Reducer::mark_ready_direct)
       .def("set_no_direct", &Reducer::set_no_direct)
       .def("set_tapered", &Reducer::set_tapered)
+      .def("lazy_zero_ok", &Reducer::lazy_zero_ok)
+      .def("lazy_zero", &Reducer::lazy_zero)
+      .def("lazy_view", &Reducer::lazy_view)
       .def("direct_ok", &Reducer::direct_ok)
       .def("iteration", &Reducer::iteration)
       .def("force_collectives", &Reducer::force_collectives)
