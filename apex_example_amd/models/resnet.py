@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
-from ..ops.conv import Conv2d1x1, Conv2d3x3, StemConv2d
+from ..ops.conv import Conv2d1x1, Conv2d3x3, StemConv2d, conv1x1_pair_s2
 from ..ops.pool import (GlobalAvgPool2dNHWC, MaxPool2dNHWC, bn_relu_maxpool,
                         bn_relu_maxpool_fusable)
 
@@ -106,7 +106,14 @@ class Bottleneck(nn.Module):
         _link_stats(self.conv3, self.bn3)
 
     def forward(self, x):
-        if isinstance(self.conv1, Conv2d1x1):
+        if (isinstance(self.conv1, Conv2d1x1) and self.downsample is not None
+                and self.downsample.conv.stride == (2, 2)):
+            # conv1 and the stride-2 downsample projection read the same input: one
+            # Function keeps the projection's input gradient compact (strided pixels
+            # only) and conv1's dgrad adds it on the even pixels (ops/conv.py)
+            out, proj = conv1x1_pair_s2(self.conv1, self.downsample.conv, x)
+            identity = self.downsample.bn(proj)
+        elif isinstance(self.conv1, Conv2d1x1):
             # the block input feeds conv1 and the residual branch (identity or the
             # downsample conv): the two input gradients are summed inside conv1's
             # dgrad GEMM (C += dY @ W into the branch's gradient), not by a separate

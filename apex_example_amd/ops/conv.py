@@ -61,7 +61,10 @@ def _side_mode(params):
         return None
     if torch.cuda.is_current_stream_capturing():
         return None
-    if all(p.grad is None for p in ps):
+    if all(p.grad is None for p in ps) and not any(
+            getattr(p, "_amd_grad_is_bucket_view", False) for p in ps):
+        # (a DDP parameter whose bucket view was lazily zeroed also has no .grad, but its
+        # ready hook copies the gradient on the compute stream: never 'free')
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             return None
@@ -378,11 +381,13 @@ def _bnbwd_ok(dy, weight, src, xshape, has_add=False):
             and (has_add or m <= _BNBWD_MAX_M) and _native.available())
 
 
-def _dgrad_bn(dy, wprep, add, src):
-    """g = mask * (conv(dy, wprep) + add) with the BN sums; hands them to the BN."""
+def _dgrad_bn(dy, wprep, add, src, add_stride2=False):
+    """g = mask * (conv(dy, wprep) + add) with the BN sums; hands them to the BN.
+    ``add_stride2``: ``add`` is the COMPACT [N, C, H/2, W/2] gradient of a stride-2 1x1
+    conv over the same input, landing on the even pixels only."""
     g, slab = _native.require().conv.conv_fwd_bnbwd(
         dy, wprep, add, src.x, src.mask, src.mean, src.invstd, src.weight, src.bias,
-        src.relu_mode)
+        src.relu_mode, add_stride2)
     src.result = (g.data_ptr(), slab, g._version)
     return g
 
@@ -521,6 +526,109 @@ class Conv1x1Stride2Function(torch.autograd.Function):
                 so = _side_out(side, weight, cl=True)
                 dw = side.run(lambda: cv.conv_wgrad(dy, x, weight.dtype, 0, 2, 1, out=so), dy, x)
         return dx, dw, None
+
+
+# A bottleneck's first block in layers 2-4: the block input feeds conv1 (1x1, stride 1)
+# and the stride-2 1x1 downsample projection.  As two Functions, the downsample's input
+# gradient is a full-size tensor that is zero on 3 of 4 pixels (its data-gradient kernel
+# writes all of them) and conv1's data gradient reads it back as the residual term.  One
+# Function for both convs keeps that gradient COMPACT - the plain 1x1 GEMM dY_d W_d on the
+# strided pixels - and conv1's dgrad epilogue adds it onto the even pixels only
+# (ConvBnEpi.add_s2).  APEX_AMD_CONV_PAIR_S2=0 keeps the two Functions.
+_PAIR_S2 = os.environ.get("APEX_AMD_CONV_PAIR_S2", "1") == "1"
+PAIR_S2_CALLS = [0]  # backward passes that took the compact path (tests)
+
+
+class Conv1x1PairS2Function(torch.autograd.Function):
+    """(conv1x1(x, w1), conv1x1_stride2(x, wd)) over one input."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd, bn1=None, bnd=None, src=None):
+        ctx.save_for_backward(x, w1, wd)
+        ctx.src = src
+        for w, k in ((w1, 1), (wd, 2)):
+            if ctx.needs_input_grad[k]:
+                _ddp_direct.note_use(w)
+        if ctx.needs_input_grad[0]:
+            _register_prep(w1)
+            _register_prep(wd)
+        y1 = _conv1x1_fwd(x, w1, bn1)
+        ent1 = getattr(_TLS, "slab", None)
+        _TLS.slab = None
+        yd = _conv_fwd(x, wd, 2, bnd)
+        ent2 = getattr(_TLS, "slab", None)
+        _TLS.slab = None
+        _TLS.pair = (ent1, ent2)
+        return y1, yd
+
+    @staticmethod
+    def backward(ctx, dy1, dyd):
+        x, w1, wd = ctx.saved_tensors
+        n, ci, h, w = x.shape
+        cv = _native.require().conv
+        src, ctx.src = ctx.src, None
+        dx = dw1 = dwd = None
+        if dy1 is not None:
+            dy1 = dy1.contiguous(memory_format=torch.channels_last)
+        if dyd is not None:
+            dyd = dyd.contiguous(memory_format=torch.channels_last)
+        side1 = _SideWgrad(w1) if (ctx.needs_input_grad[1] and dy1 is not None) else None
+        sided = _SideWgrad(wd) if (ctx.needs_input_grad[2] and dyd is not None) else None
+        if ctx.needs_input_grad[0]:
+            # the downsample's input gradient on the strided pixels only: dY_d W_d
+            cd = (_conv1x1_dgrad(dyd, wd, (n, ci, h // 2, w // 2)).contiguous(
+                memory_format=torch.channels_last) if dyd is not None else None)
+            if dy1 is None:
+                dx = torch.zeros_like(x)
+                if cd is not None:
+                    dx[:, :, ::2, ::2] = cd
+            elif cd is not None and _bnbwd_ok(dy1, w1, src, x.shape, has_add=True):
+                PAIR_S2_CALLS[0] += 1
+                dx = _dgrad_bn(dy1, _transpose_1x1(w1), cd, src, add_stride2=True)
+            else:
+                dx = _conv1x1_dgrad(dy1, w1, x.shape).contiguous(
+                    memory_format=torch.channels_last)
+                if cd is not None:
+                    dx[:, :, ::2, ::2] += cd
+        if side1 is not None:
+            direct = None if side1.on else _ddp_direct.slots(w1)
+            tgt, acc = _ddp_direct.grad_target(w1) if direct is not None else (None, True)
+            if direct is not None and tgt.is_contiguous():
+                wgrad_1x1(_as_rows(dy1), _as_rows(x), w1.dtype, out=tgt, accumulate=acc)
+                _ddp_direct.mark_ready(direct)
+            else:
+                so = _side_out(side1, w1)
+                dw1 = side1.run(lambda: _wgrad_1x1_w(dy1, x, w1, so), dy1, x)
+        if sided is not None:
+            direct = None if sided.on else _ddp_direct.slots(wd)
+            tgt, acc = _ddp_direct.grad_target(wd) if direct is not None else (None, True)
+            if direct is not None and tgt.is_contiguous(memory_format=torch.channels_last):
+                cv.conv_wgrad(dyd, x, wd.dtype, 0, 2, 1, out=tgt, accumulate=acc)
+                _ddp_direct.mark_ready(direct)
+            else:
+                so = _side_out(sided, wd, cl=True)
+                dwd = sided.run(lambda: cv.conv_wgrad(dyd, x, wd.dtype, 0, 2, 1, out=so), dyd, x)
+        return dx, dw1, dwd, None, None, None
+
+
+def conv1x1_pair_s2(conv1, convd, x):
+    """(conv1(x), convd(x)) for a stride-1 ``Conv2d1x1`` and a stride-2 ``Conv2d1x1`` over
+    the same input - one Function with a compact downsample gradient where the own
+    kernels apply, else the two convs as usual."""
+    if (_PAIR_S2 and isinstance(conv1, Conv2d1x1) and isinstance(convd, Conv2d1x1)
+            and conv1._gemm_ok(x) and convd._strided_ok(x) and x.dtype == torch.bfloat16
+            and conv1.weight.dtype == torch.bfloat16 and _native.available()):
+        y1, yd = Conv1x1PairS2Function.apply(x, conv1.weight, convd.weight,
+                                             _stats_bn(conv1, x), _stats_bn(convd, x),
+                                             bn_src_of(x))
+        ent1, ent2 = getattr(_TLS, "pair", (None, None))
+        _TLS.pair = (None, None)
+        if ent1 is not None:
+            y1._amd_bn_stats = ent1
+        if ent2 is not None:
+            yd._amd_bn_stats = ent2
+        return y1, yd
+    return conv1(x), convd(x)
 
 
 class Conv2d1x1(nn.Conv2d):

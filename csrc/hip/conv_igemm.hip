@@ -156,7 +156,19 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
     const int m = m0 + q * PT::RGS + rg;
     const int64_t opix = out_pix<MODE>(g, m < g.M ? m : 0, z);
     const int64_t off = opix * NC + c0;
-    P.av[q] = addp ? *reinterpret_cast<const uint4*>(addp + off) : make_uint4(0, 0, 0, 0);
+    if (ep.add_s2 && addp) {
+      // compact stride-2 residual gradient: pixel (n, h, w) receives add[n][h/2][w/2] when
+      // h and w are even (dense output pixels: opix = m on a GH x GW grid)
+      const int GHW = g.GH * g.GW;
+      const int mm = m < g.M ? m : 0;
+      const int n = mm / GHW, rem = mm - n * GHW;
+      const int h = rem / g.GW, w = rem - h * g.GW;
+      const int64_t coff = ((int64_t)(n * (g.GH >> 1) + (h >> 1)) * (g.GW >> 1) + (w >> 1)) * NC + c0;
+      P.av[q] = ((h | w) & 1) ? make_uint4(0, 0, 0, 0)
+                              : *reinterpret_cast<const uint4*>(addp + coff);
+    } else {
+      P.av[q] = addp ? *reinterpret_cast<const uint4*>(addp + off) : make_uint4(0, 0, 0, 0);
+    }
     P.xv[q] = (ep.diag & 1) ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(xp + off);
     P.mk[q] = ep.relu_mode == 1 ? ep.rmask[opix * (NC >> 3) + (c0 >> 3)] : 0xffu;
   }

@@ -294,6 +294,8 @@ struct ConvBnEpi {
   const float* b;        // [C] or null (relu_mode 2)
   int relu_mode;
   int diag;              // timing experiments only: bit 0 = do not read x (sums are wrong)
+  int add_s2;            // 1: `add` is COMPACT [N][H/2][W/2][C] and lands on the even
+                         // (h, w) pixels only (a stride-2 1x1 downsample's input gradient)
 };
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* g, int N, int H, int W, int Cin,
                          int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,

@@ -124,7 +124,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("conv_fwd", &conv_nhwc_fwd_op, py::arg("x"), py::arg("w"), py::arg("stride") = 1);
   conv.def("conv_fwd_bnbwd", &conv_nhwc_fwd_bnbwd_op, py::arg("dy"), py::arg("w"),
            py::arg("add"), py::arg("x"), py::arg("rmask"), py::arg("mean"), py::arg("invstd"),
-           py::arg("bn_weight"), py::arg("bn_bias"), py::arg("relu_mode"));
+           py::arg("bn_weight"), py::arg("bn_bias"), py::arg("relu_mode"),
+           py::arg("add_stride2") = false);
   conv.def("conv_fwd_stats", &conv_nhwc_fwd_stats_op, py::arg("x"), py::arg("w"),
            py::arg("stride") = 1, py::arg("shift") = py::none());
   conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);

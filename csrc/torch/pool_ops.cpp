@@ -134,7 +134,8 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tens
 std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
     at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> add, at::Tensor xbn,
     c10::optional<at::Tensor> rmask, at::Tensor mean, at::Tensor invstd,
-    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode) {
+    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode,
+    bool add_stride2) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && w.dim() == 4, "conv_bnbwd: 4-D GPU tensors");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
@@ -156,7 +157,18 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
   same_out(xbn, "x");
   ConvBnEpi ep{};
   if (add.has_value() && add->defined()) {
-    same_out(*add, "add");
+    if (add_stride2) {
+      // the compact gradient of a stride-2 1x1 conv over this output (even pixels only)
+      TORCH_CHECK(k == 1 && H % 2 == 0 && W % 2 == 0 && add->is_cuda() && add->dim() == 4 &&
+                      add->size(0) == N && add->size(1) == Cout && add->size(2) == H / 2 &&
+                      add->size(3) == W / 2 && add->scalar_type() == at::kBFloat16 &&
+                      add->is_contiguous(cl),
+                  "conv_bnbwd: a stride-2 add must be channels-last bf16 [N, C, H/2, W/2] "
+                  "(1x1 conv, even H and W)");
+      ep.add_s2 = 1;
+    } else {
+      same_out(*add, "add");
+    }
     ep.add = add->data_ptr();
   }
   ep.xbn = xbn.data_ptr();

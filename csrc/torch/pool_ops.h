@@ -27,7 +27,8 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tens
 std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
     at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> add, at::Tensor xbn,
     c10::optional<at::Tensor> rmask, at::Tensor mean, at::Tensor invstd,
-    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode);
+    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode,
+    bool add_stride2 = false);
 at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W);
 at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
                               int64_t stride, int64_t ksize, c10::optional<at::Tensor> out, bool accumulate = true);

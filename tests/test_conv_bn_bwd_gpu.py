@@ -229,3 +229,43 @@ def test_bn_output_fanout_falls_back_to_reduce(monkeypatch):
                       (bn.bias.grad, ref_bn.bias.grad)):
         err = float((got - want).abs().max() / want.abs().max())
         assert err < 3e-2, err
+
+
+def test_stride2_block_compact_downsample_gradient(monkeypatch):
+    """A layer-2-style first block (stride-2 3x3 + stride-2 1x1 downsample) behind a fused
+    BN: conv1 and the downsample run as ONE Function whose downsample input gradient stays
+    compact and is added on the even pixels in conv1's dgrad epilogue (ConvBnEpi.add_s2).
+    Input, BN and weight gradients match the two-Function path; the compact path ran."""
+    from apex_example_amd.models.resnet import Bottleneck, _Downsample
+    from apex_example_amd.ops import BatchNorm2dReLU
+    from apex_example_amd.ops import conv as convmod
+
+    torch.manual_seed(3)
+    x0 = _bf(torch.randn(4, 256, 28, 28, device=dev) * 1.5)
+    r = torch.randn(4, 512, 14, 14, device=dev)
+    grads = {}
+    for pair in (False, True):
+        monkeypatch.setattr(convmod, "_PAIR_S2", pair)
+        torch.manual_seed(0)
+        pre = BatchNorm2dReLU(256, fuse_relu=True)          # tags its output (BnBwdSrc)
+        ds = _Downsample(256, 512, 2, True, gemm_1x1=True)
+        blk = Bottleneck(256, 128, 2, ds, fused_bn=True, gemm_1x1=True)
+        m = torch.nn.Sequential(pre, blk)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                with torch.no_grad():
+                    mod.weight.uniform_(0.5, 1.5)
+                    mod.bias.uniform_(-0.2, 0.2)
+        m = m.to(dev).to(memory_format=CL)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Conv2d):
+                mod.to(torch.bfloat16)
+        x = x0.clone().requires_grad_(True)
+        n0 = convmod.PAIR_S2_CALLS[0]
+        (m(x).float() * r).sum().backward()
+        torch.cuda.synchronize()
+        assert convmod.PAIR_S2_CALLS[0] - n0 == (1 if pair else 0)
+        grads[pair] = [x.grad.float()] + [p.grad.float() for p in m.parameters()]
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        err = float((a - b).abs().max() / (b.abs().max() + 1e-12))
+        assert err < 2e-2, (i, err)

@@ -1,20 +1,45 @@
-"""Run the MFMA conv kernels on two ResNet-50 shapes (for rocprofv3 --pmc)."""
+#!/usr/bin/env python3
+"""Run ONE implicit-GEMM conv shape many times (for rocprofv3 --pmc passes): 3x3 forward
+of `--c` channels at `--hw`, tiling `--variant` (APEX_AMD_CONV_BM), or the 64-channel
+weight gradient (`--wgrad algo`)."""
+import argparse
 import os
 import sys
 
+import torch
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-import torch  # noqa: E402
 
-from apex_example_amd import _native  # noqa: E402
 
-cv = _native.require().conv
-for (n, c, hw) in [(256, 64, 56), (256, 256, 14)]:
-    x = torch.randn(n, c, hw, hw, device="cuda", dtype=torch.bfloat16).to(
-        memory_format=torch.channels_last)
-    w = (torch.randn(c, c, 3, 3, device="cuda", dtype=torch.bfloat16) * 0.05).to(
-        memory_format=torch.channels_last)
-    for _ in range(3):
-        cv.conv_fwd(x, w)
-        cv.conv_wgrad(x, x, torch.bfloat16)
-torch.cuda.synchronize()
-print("done")
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c", type=int, default=128)
+    ap.add_argument("--hw", type=int, default=28)
+    ap.add_argument("--variant", default="default")
+    ap.add_argument("--wgrad", type=int, default=-1)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    if a.variant != "default":
+        os.environ["APEX_AMD_CONV_BM"] = a.variant
+    from apex_example_amd import _native
+
+    cv = _native.require().conv
+    g = torch.Generator(device="cuda").manual_seed(0)
+    cl = torch.channels_last
+    x = torch.randn(256, a.c, a.hw, a.hw, device="cuda", generator=g).to(torch.bfloat16).to(
+        memory_format=cl)
+    w = (torch.randn(a.c, a.c, 3, 3, device="cuda", generator=g) * 0.03).to(torch.bfloat16).to(
+        memory_format=cl)
+    dy = torch.randn(256, a.c, a.hw, a.hw, device="cuda", generator=g).to(torch.bfloat16).to(
+        memory_format=cl)
+    for _ in range(a.iters):
+        if a.wgrad >= 0:
+            cv.conv_wgrad(dy, x, torch.bfloat16, a.wgrad, 1)
+        else:
+            cv.conv_fwd(x, w, 1)
+    torch.cuda.synchronize()
+    print("done")
+
+
+if __name__ == "__main__":
+    main()
