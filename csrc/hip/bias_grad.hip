@@ -182,6 +182,19 @@ void gelu_fwd(const void* x, void* y, DType t, int64_t n, bool tanh_approx, hipS
   else go(float{});
 }
 
+void colsum_finalize(const float* part, int S, int N, void* out, DType tb, hipStream_t st) {
+  const dim3 g2((unsigned)((N + 63) / 64));
+  if (tb == DType::F32)
+    hipLaunchKernelGGL(colsum_final_k<float>, g2, dim3(256), 0, st, part, S, N,
+                       static_cast<float*>(out));
+  else if (tb == DType::BF16)
+    hipLaunchKernelGGL(colsum_final_k<bf16_t>, g2, dim3(256), 0, st, part, S, N,
+                       static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(colsum_final_k<half_t>, g2, dim3(256), 0, st, part, S, N,
+                       static_cast<half_t*>(out));
+}
+
 int colsum_splits(int64_t M, int N) {
   const int cb = (N + kCsCols - 1) / kCsCols;
   int64_t S = (1024 + cb - 1) / cb;        // ~4 blocks per CU (2 per CU measured slower)

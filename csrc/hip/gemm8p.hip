@@ -1,0 +1,342 @@
+// C[M, N] = A[M, K] . B[N, K]^T on the gfx950 matrix cores: a 256 x 256 workgroup tile,
+// 8 wave64s (2 x 4, 128 x 64 accumulators each = 128 VGPRs), bf16 in / fp32 accumulate,
+// with the K loop as 8 PHASES per two 64-deep K-tiles:
+//
+//   phase = { ds_read the fragments this phase needs | DMA one half-tile (2 glds per wave) |
+//             [counted vmcnt] | s_barrier | 16 MFMAs (one 64 x 32 quadrant of the wave's
+//             tile, K = 64) at raised priority | s_barrier }
+//
+// A tile's A and B operands live in LDS as four 16 KB half-tile regions - A_q0 / A_q1 (the
+// wave rows of quadrant row 0 / 1) and B_n0 / B_n1 (quadrant column 0 / 1) - in two
+// buffers (even / odd K-tiles): 128 KB.  Each region is read in exactly one phase of its
+// tile (A_q0 and B_n0 in phase 1, B_n1 in 2, A_q1 in 3; phase 4 reuses registers), so it
+// can be refilled two phases later: the DMA of every region is issued the second phase
+// after its last read, one region per phase, and only phases 4 and 8 wait - vmcnt(4), the
+// two youngest regions (the next tile's) stay in flight across the barrier.  Every region
+// thus has ~4-6 phases (~1000+ cycles of MFMA work) to arrive, and no wave ever waits for
+// vmcnt(0) inside the loop (the 2-barrier 128 x 128 conv kernel's ceiling).
+//
+// LDS rows are 64 bf16 (128 B) with the 16-byte chunks XOR-swizzled by (row >> 1) & 7 on
+// the DMA's SOURCE side (the DMA writes lane-linearly), so the 16 rows a ds_read_b128 lane
+// group touches hit distinct bank slots.  Workgroups are remapped so the tiles of one
+// A row panel run on one XCD (its 4 MB L2 then serves the panel to all of them).
+//
+// Epilogues (G8Epi): plain bf16 store; bias + GELU with the pre-activation kept (the FFN
+// input projection); dGELU from the saved pre-activation + the bias gradient's per-tile
+// column sums (the FFN data gradient).  M may be ragged (zero-page rows); N % 256 == 0,
+// K % 128 == 0.
+#include <cstdlib>
+
+#include "amd_dev.h"
+#include "amd_kernels.h"
+
+namespace amd {
+
+namespace {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kG8T = 512;       // threads
+constexpr int kG8Half = 16384;  // one half-tile region: 128 rows x 128 B
+
+__device__ uint4 g8_zero16[4];  // zero source for rows past M
+
+__device__ __forceinline__ int g8_swz(int row, int chunk) {
+  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+__device__ __forceinline__ void g8_glds(const void* g, unsigned char* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// s_barrier that the compiler may not move memory operations across (the raw builtin is
+// not a memory barrier to it) and that waits for nothing: DMAs stay in flight
+__device__ __forceinline__ void g8_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int g8_xcd_remap(int bid, int nwg) {
+  const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / 8;
+}
+
+__device__ __forceinline__ float g8_gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float g8_gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+__device__ __forceinline__ float g8_dgelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+__device__ __forceinline__ float g8_dgelu_erf(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[8 * kG8Half];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int ntn = p.N >> 8;
+  const int bid = g8_xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int KT = p.K >> 6;
+
+  // DMA geometry: half-tile wave-instruction j = wid * 2 + i fills region rows j*8 .. j*8+7,
+  // lane -> (row j*8 + lane/8, physical chunk lane%8) fetching the logical chunk that the
+  // swizzle stores there
+  const int lrow = lane >> 3, pch = lane & 7;
+  const bf16_t* srcA[2][2];
+  bool okA[2][2];
+  const bf16_t* srcB[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = (wid * 2 + i) * 8 + lrow;
+      const int ch = pch ^ ((rr >> 1) & 7);
+      const int arow = m0 + (rr >> 6) * 128 + q * 64 + (rr & 63);
+      okA[q][i] = arow < p.M;
+      srcA[q][i] = static_cast<const bf16_t*>(p.A) + (int64_t)(okA[q][i] ? arow : 0) * p.lda + ch * 8;
+      const int brow = n0 + (rr >> 5) * 64 + q * 32 + (rr & 31);
+      srcB[q][i] = static_cast<const bf16_t*>(p.B) + (int64_t)brow * p.ldb + ch * 8;
+    }
+
+  // region r of buffer (T & 1): 0 = A_q0, 1 = A_q1, 2 = B_n0, 3 = B_n1.  Tiles past the end
+  // re-fetch the last tile (into regions no longer read) so every phase issues the same
+  // number of DMAs and the counted waits stay exact.
+  auto stage = [&](int r, int T) {
+    unsigned char* dst = lds + ((T & 1) * 4 + r) * kG8Half + wid * 2048;
+    const int64_t koff = (int64_t)(T < KT ? T : KT - 1) * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const void* src;
+      if (r < 2) src = okA[r][i] ? (const void*)(srcA[r][i] + koff) : (const void*)g8_zero16;
+      else src = (const void*)(srcB[r - 2][i] + koff);
+      g8_glds(src, dst + i * 1024);
+    }
+  };
+
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+  auto readA = [&](int buf, int q, bf16x8 (&a)[4][2]) {
+    const unsigned char* R = lds + (buf * 4 + q) * kG8Half;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        a[i][ks] = *reinterpret_cast<const bf16x8*>(R + g8_swz(wm * 64 + i * 16 + fr, ks * 4 + fg));
+  };
+  auto readB = [&](int buf, int q, bf16x8 (&b)[2][2]) {
+    const unsigned char* R = lds + (buf * 4 + 2 + q) * kG8Half;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        b[j][ks] = *reinterpret_cast<const bf16x8*>(R + g8_swz(wn * 32 + j * 16 + fr, ks * 4 + fg));
+  };
+
+  f32x4_t acc[2][2][4][2];
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+#define G8_MMA(QM, QN, AR, BR)                                                          \
+  {                                                                                     \
+    __builtin_amdgcn_s_setprio(1);                                                      \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                       \
+      acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AR[i][ks], BR[j][ks],  \
+                                                                  acc[QM][QN][i][j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                      \
+  }
+
+  // prologue: tile 0 complete, tile 1's A_q0 / B_n0 in flight
+  stage(0, 0);
+  stage(2, 0);
+  stage(3, 0);
+  stage(1, 0);
+  stage(0, 1);
+  stage(2, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  g8_barrier();
+
+  for (int t = 0; t < KT; t += 2) {
+    // ---------------- tile t (buffer 0)
+    readA(0, 0, a0);  // phase 1
+    readB(0, 0, b0);
+    stage(3, t + 1);
+    g8_barrier();
+    G8_MMA(0, 0, a0, b0);
+    g8_barrier();
+    readB(0, 1, b1);  // phase 2
+    stage(1, t + 1);
+    g8_barrier();
+    G8_MMA(0, 1, a0, b1);
+    g8_barrier();
+    readA(0, 1, a1);  // phase 3
+    stage(0, t + 2);
+    g8_barrier();
+    G8_MMA(1, 1, a1, b1);
+    g8_barrier();
+    stage(2, t + 2);  // phase 4: retire tile t+1 (its DMAs are older than the last two)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    g8_barrier();
+    G8_MMA(1, 0, a1, b0);
+    g8_barrier();
+    // ---------------- tile t+1 (buffer 1)
+    readA(1, 0, a0);  // phase 5
+    readB(1, 0, b0);
+    stage(3, t + 2);
+    g8_barrier();
+    G8_MMA(0, 0, a0, b0);
+    g8_barrier();
+    readB(1, 1, b1);  // phase 6
+    stage(1, t + 2);
+    g8_barrier();
+    G8_MMA(0, 1, a0, b1);
+    g8_barrier();
+    readA(1, 1, a1);  // phase 7
+    stage(0, t + 3);
+    g8_barrier();
+    G8_MMA(1, 1, a1, b1);
+    g8_barrier();
+    stage(2, t + 3);  // phase 8: retire tile t+2
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    g8_barrier();
+    G8_MMA(1, 0, a1, b0);
+    g8_barrier();
+  }
+#undef G8_MMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: accumulators -> bf16 tile in LDS (the whole 128 KB) -> 16-byte row stores
+  bf16_t* T = reinterpret_cast<bf16_t*>(lds);
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = wm * 128 + qm * 64 + i * 16 + fg * 4 + e;
+            const int col = wn * 64 + qn * 32 + j * 16 + fr;
+            float v = acc[qm][qn][i][j][e];
+            if constexpr (EPI == 1) {  // bias before the one rounding, as addmm does
+              if (p.bias)
+                v += p.bias_f32 ? static_cast<const float*>(p.bias)[n0 + col]
+                                : (float)static_cast<const bf16_t*>(p.bias)[n0 + col];
+            }
+            T[row * 256 + col] = (bf16_t)v;
+          }
+  __syncthreads();
+  // each thread: one 8-column chunk (fixed for all its rows: 512 % 32 == 0) of 16 rows
+  const int cc = tid & 31, rg = tid >> 5;
+  bf16_t* Cp = static_cast<bf16_t*>(p.C);
+  bf16_t* auxp = static_cast<bf16_t*>(p.aux);
+  const int col0 = n0 + cc * 8;
+  float colsum[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) colsum[k] = 0.f;
+  for (int row = rg; row < 256; row += kG8T / 32) {
+    const int gm = m0 + row;
+    if (gm >= p.M) break;
+    const uint4 v = *reinterpret_cast<const uint4*>(T + row * 256 + cc * 8);
+    if constexpr (EPI == 0) {
+      *reinterpret_cast<uint4*>(Cp + (int64_t)gm * p.ldc + col0) = v;
+    } else {
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+      float x[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x[2 * k] = __uint_as_float(w[k] << 16);
+        x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      }
+      if constexpr (EPI == 1) {
+        // pre = acc + bias (one bf16 rounding, as the unfused addmm), h = gelu(pre)
+        bf16x8 pre, h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          pre[k] = (bf16_t)x[k];
+          h[k] = (bf16_t)(p.tanh ? g8_gelu_tanh(x[k]) : g8_gelu_erf(x[k]));
+        }
+        if (auxp) *reinterpret_cast<bf16x8*>(auxp + (int64_t)gm * p.ldc + col0) = pre;
+        *reinterpret_cast<bf16x8*>(Cp + (int64_t)gm * p.ldc + col0) = h;
+      } else {
+        // dpre = dh * gelu'(pre), dh = this GEMM's output rounded to bf16; bias gradient
+        // partial sums of the bf16-rounded dpre
+        const bf16x8 pre = *reinterpret_cast<const bf16x8*>(auxp + (int64_t)gm * p.ldc + col0);
+        bf16x8 d;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float pf = (float)pre[k];
+          const bf16_t db = (bf16_t)(x[k] * (p.tanh ? g8_dgelu_tanh(pf) : g8_dgelu_erf(pf)));
+          d[k] = db;
+          colsum[k] += (float)db;
+        }
+        *reinterpret_cast<bf16x8*>(Cp + (int64_t)gm * p.ldc + col0) = d;
+      }
+    }
+  }
+  if constexpr (EPI == 2) {
+    if (p.colsum) {
+      // the 16 row groups of each column chunk through LDS, one row of the [Mtiles][N]
+      // partial-sum slab per workgroup (fixed order: deterministic)
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[rg * 256 + cc * 8 + k] = colsum[k];
+      __syncthreads();
+      if (tid < 256) {
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < kG8T / 32; ++g) s += red[g * 256 + tid];
+        p.colsum[(int64_t)tm * p.N + n0 + tid] = s;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool gemm8p_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && N % 256 == 0 && K >= 128 && K % 128 == 0;
+}
+
+int gemm8p_mtiles(int M) { return (M + 255) / 256; }
+
+void gemm8p(const G8Args& a, int epi, hipStream_t st) {
+  const int grid = gemm8p_mtiles(a.M) * (a.N / 256);
+  if (epi == 1)
+    hipLaunchKernelGGL(gemm8p_k<1>, dim3(grid), dim3(kG8T), 0, st, a);
+  else if (epi == 2)
+    hipLaunchKernelGGL(gemm8p_k<2>, dim3(grid), dim3(kG8T), 0, st, a);
+  else
+    hipLaunchKernelGGL(gemm8p_k<0>, dim3(grid), dim3(kG8T), 0, st, a);
+}
+
+}  // namespace amd

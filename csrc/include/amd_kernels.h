@@ -268,6 +268,26 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
 void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int C,
                   hipStream_t st);
 
+// ---- 256 x 256 8-phase MFMA GEMM (gemm8p.hip) ---------------------------------
+// C[M, N] = A[M, K] . B[N, K]^T, bf16 row-major (K contiguous), fp32 accumulation.
+// epi 0: C = bf16(acc); 1: pre = bf16(acc + bias) -> aux (if non-null), C = gelu(pre);
+// 2: C = bf16(bf16(acc) * gelu'(aux)) and colsum[M-tile][N] = per-tile column sums of C.
+// Requires N % 256 == 0, K % 128 == 0 (gemm8p_supported); M ragged.
+struct G8Args {
+  const void* A;               // bf16
+  const void* B;               // bf16
+  void* C;                     // bf16
+  int M, N, K, lda, ldb, ldc;  // ldc also strides aux
+  const void* bias;            // [N] bf16 (or fp32 when bias_f32), epi 1
+  int bias_f32;
+  void* aux;                   // bf16 [M][ldc] pre-activation: written (epi 1) / read (epi 2)
+  float* colsum;               // [ceil(M / 256)][N] (epi 2), may be null
+  int tanh;                    // GELU flavour: 1 tanh approximation, 0 erf
+};
+bool gemm8p_supported(int M, int N, int K);
+int gemm8p_mtiles(int M);
+void gemm8p(const G8Args& a, int epi, hipStream_t st);
+
 // ---- implicit-GEMM convolutions, NHWC bf16, MFMA (conv_igemm.hip) ----------
 // 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64
 bool conv3x3_nhwc_supported(int Cin, int Cout);
@@ -369,6 +389,8 @@ void stem_wgrad(const void* xp, const void* dy, float* part, int S, int N, int H
 // g = dh * relu'(y) / dh * sigmoid'(y) from the saved output y (passed as `pre`) is
 // computed in the same pass and written to out_dpre.  part: S * N floats.
 int colsum_splits(int64_t M, int N);
+// out[n] = sum_s part[s][n] (fp32 partial slab [S][N]) in dtype tb
+void colsum_finalize(const float* part, int S, int N, void* out, DType tb, hipStream_t st);
 // y = gelu(x) (erf or tanh), n % 8 == 0, 16-byte aligned
 void gelu_fwd(const void* x, void* y, DType t, int64_t n, bool tanh_approx, hipStream_t st);
 void colsum(const void* x, const void* pre, void* out_dpre, DType t, int64_t M, int N,

@@ -100,4 +100,71 @@ std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tenso
   return {dpre, out};
 }
 
+bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
+  return a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 &&
+         a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+         a.stride(1) == 1 && b.stride(1) == 1 && a.size(1) == b.size(1) &&
+         a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+         reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+         reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 && a.size(0) < (1 << 30) &&
+         gemm8p_supported((int)a.size(0), (int)b.size(0), (int)a.size(1));
+}
+
+std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
+                                  c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
+                                  bool want_pre, bool tanh_approx,
+                                  c10::optional<at::ScalarType> bias_grad_dtype) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(gemm8p_ok(a, b), "gemm8p: bf16 [M, K] x [N, K] with N % 256 == 0, K % 128 == 0, "
+              "unit column stride, 16-byte aligned rows");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8p: epi 0 | 1 | 2");
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
+  at::Tensor c = at::empty({M, N}, a.options());
+  G8Args g{};
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.C = c.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = (int)a.stride(0);
+  g.ldb = (int)b.stride(0);
+  g.ldc = (int)N;
+  g.tanh = tanh_approx ? 1 : 0;
+  std::vector<at::Tensor> out{c};
+  if (epi == 1) {
+    if (bias.has_value() && bias->defined()) {
+      TORCH_CHECK(bias->is_cuda() && bias->is_contiguous() && bias->numel() == N &&
+                      (bias->scalar_type() == at::kBFloat16 || bias->scalar_type() == at::kFloat),
+                  "gemm8p: bias must be a contiguous bf16 / fp32 [N] GPU tensor");
+      g.bias = bias->data_ptr();
+      g.bias_f32 = bias->scalar_type() == at::kFloat ? 1 : 0;
+    }
+    if (want_pre) {
+      at::Tensor pre = at::empty({M, N}, a.options());
+      g.aux = pre.data_ptr();
+      out.push_back(pre);
+    }
+  } else if (epi == 2) {
+    TORCH_CHECK(aux.has_value() && aux->defined() && aux->is_cuda() &&
+                    aux->scalar_type() == at::kBFloat16 && aux->is_contiguous() &&
+                    aux->numel() == M * N,
+                "gemm8p: epi 2 needs the contiguous bf16 [M, N] pre-activation");
+    g.aux = aux->data_ptr();
+  }
+  at::Tensor part;
+  if (epi == 2 && bias_grad_dtype.has_value()) {
+    part = at::empty({(int64_t)gemm8p_mtiles((int)M), N}, a.options().dtype(at::kFloat));
+    g.colsum = part.data_ptr<float>();
+  }
+  gemm8p(g, (int)epi, cur_stream());
+  if (part.defined()) {
+    at::Tensor db = at::empty({N}, a.options().dtype(*bias_grad_dtype));
+    colsum_finalize(part.data_ptr<float>(), (int)part.size(0), (int)N, db.data_ptr(),
+                    dtype_of(db), cur_stream());
+    out.push_back(db);
+  }
+  return out;
+}
+
 }  // namespace amd

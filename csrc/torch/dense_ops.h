@@ -19,4 +19,14 @@ at::Tensor gelu_fwd_op(at::Tensor x, bool tanh_approx);
 std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tensor y, int64_t act,
                                                         at::ScalarType out_dtype);
 
+// The own 256 x 256 8-phase MFMA GEMM (csrc/hip/gemm8p.hip): C = A . B^T for bf16 A [M, K]
+// and B [N, K] (row-major), with the FFN epilogues.  epi 0: [C]; epi 1: bias + GELU ->
+// [h, pre (when want_pre)]; epi 2: dGELU from aux = pre -> [dpre, bias grad (when
+// bias_grad_dtype is given)].  gemm8p_ok: the shape / dtype / layout qualifies.
+bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b);
+std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
+                                  c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
+                                  bool want_pre, bool tanh_approx,
+                                  c10::optional<at::ScalarType> bias_grad_dtype);
+
 }  // namespace amd

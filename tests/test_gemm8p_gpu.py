@@ -1,0 +1,69 @@
+"""The own 256 x 256 8-phase MFMA GEMM (csrc/hip/gemm8p.hip) against fp32 references:
+plain C = A B^T at ragged M / several N, K; the FFN forward epilogue (bias + GELU, the
+pre-activation kept) and the FFN backward epilogue (dGELU from the pre-activation + bias
+gradient column sums), both GELU flavours."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _dn():
+    from apex_example_amd import _native
+    return _native.require().dense
+
+
+@pytest.mark.parametrize("mnk", [(256, 256, 128), (1000, 512, 256), (4096, 1024, 1024),
+                                 (333, 4096, 384), (16384, 256, 1024)])
+def test_gemm8p_plain(mnk):
+    m, n, k = mnk
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    a = torch.randn(m, k, device=DEV, generator=g).to(torch.bfloat16)
+    b = torch.randn(n, k, device=DEV, generator=g).to(torch.bfloat16)
+    assert _dn().gemm8p_ok(a, b)
+    c, = _dn().gemm8p(a, b)
+    ref = a.float() @ b.float().t()
+    err = float((c.float() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2, err
+    # bitwise-stable across calls (no atomics, fixed order)
+    assert torch.equal(c, _dn().gemm8p(a, b)[0])
+
+
+def test_gemm8p_strided_rows():
+    """Row strides larger than K (views of a wider matrix)."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    big = torch.randn(512, 640, device=DEV, generator=g).to(torch.bfloat16)
+    a = big[:, :512]
+    b = torch.randn(768, 640, device=DEV, generator=g).to(torch.bfloat16)[:, 128:]
+    c, = _dn().gemm8p(a, b)
+    ref = a.float() @ b.float().t()
+    assert float((c.float() - ref).abs().max() / ref.abs().max()) < 1e-2
+
+
+@pytest.mark.parametrize("tanh", [False, True])
+@pytest.mark.parametrize("bias_dtype", [torch.bfloat16, torch.float32])
+def test_gemm8p_gelu_epilogues(tanh, bias_dtype):
+    m, n, k = 1536, 1024, 512
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(m, k, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV, generator=g) / k ** 0.5).to(torch.bfloat16)
+    bias = (torch.randn(n, device=DEV, generator=g) * 0.1).to(bias_dtype)
+    approx = "tanh" if tanh else "none"
+    h, pre = _dn().gemm8p(x, w, 1, bias=bias, want_pre=True, tanh=tanh)
+    pre_ref = (x.float() @ w.float().t() + bias.float())
+    assert float((pre.float() - pre_ref).abs().max()) < 3e-2
+    h_ref = F.gelu(pre.float(), approximate=approx)   # gelu of the rounded pre-activation
+    assert float((h.float() - h_ref).abs().max()) < 2e-2
+    # backward: dpre = dh * gelu'(pre), dh = dy @ W2^T computed by the GEMM
+    dy = torch.randn(m, 768, device=DEV, generator=g).to(torch.bfloat16)
+    w2t = (torch.randn(n, 768, device=DEV, generator=g) / 768 ** 0.5).to(torch.bfloat16)
+    dpre, db = _dn().gemm8p(dy, w2t, 2, aux=pre, tanh=tanh, bias_grad_dtype=torch.float32)
+    dh = (dy.float() @ w2t.float().t()).to(torch.bfloat16).float()
+    p = pre.float().requires_grad_(True)
+    gref, = torch.autograd.grad(F.gelu(p, approximate=approx), p, dh)
+    scale = float(gref.abs().max())
+    assert float((dpre.float() - gref).abs().max()) / scale < 2e-2
+    db_ref = dpre.float().sum(0)
+    torch.testing.assert_close(db, db_ref, rtol=1e-3, atol=1e-2)
