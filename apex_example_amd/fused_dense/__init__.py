@@ -385,6 +385,33 @@ def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype):
     return _wgrad(dy2, x2, w_dtype), _bias_grad(dy2, b_dtype)
 
 
+# The FFN on the own 8-phase MFMA GEMM (csrc/hip/gemm8p.hip) with its epilogues: forward
+# h = gelu(x W1^T + b1) keeping the pre-activation (no separate GELU pass), backward
+# dpre = (dy W2) * gelu'(pre) with the b1 gradient's column sums (no dh round trip, no
+# column-sum kernels).  bf16 / fp16 operands, N % 256 == 0, K % 128 == 0.  APEX_AMD_GEMM8P=0
+# keeps the library GEMM + streaming kernels.
+_G8 = os.environ.get("APEX_AMD_GEMM8P", "1") == "1"
+_T_CACHE = {}  # id(weight) -> (weight, version, data_ptr, transposed copy)
+
+
+def _g8_ok(a, b, *more):
+    return (_G8 and a.is_cuda and a.dtype in (torch.bfloat16, torch.float16)
+            and b.dtype == a.dtype
+            and all(t is None or t.dtype in (a.dtype, torch.float32) for t in more)
+            and _native.available() and _native.require().dense.gemm8p_ok(a, b))
+
+
+def _transposed(w):
+    """w^T contiguous, cached while the weight is unchanged (in-place optimizer updates
+    bump its version)."""
+    ent = _T_CACHE.get(id(w))
+    if ent is not None and ent[0] is w and ent[1] == w._version and ent[2] == w.data_ptr():
+        return ent[3]
+    t = w.t().contiguous()
+    _T_CACHE[id(w)] = (w, w._version, w.data_ptr(), t)
+    return t
+
+
 def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
     dt = _compute_dtype(x)
     with torch.autocast("cuda", enabled=False):
@@ -392,7 +419,11 @@ def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
         w1c, b1c, w2c, b2c = _cast(w1, dt), _cast(b1, dt), _cast(w2, dt), _cast(b2, dt)
         x2 = xc.reshape(-1, xc.size(-1))
         res = None
-        if approximate == "tanh" and _lt_ok(x2, w1c, b1c):
+        if approximate in ("tanh", "none") and _g8_ok(x2, w1c, b1c):
+            h, pre = _native.require().dense.gemm8p(x2, w1c, 1, bias=b1c, want_pre=True,
+                                                    tanh=approximate == "tanh")
+            res = (h, pre)
+        elif approximate == "tanh" and _lt_ok(x2, w1c, b1c):
             # one GEMM: h = gelu(x W1^T + b1) with pre as the epilogue's aux output
             res = _lt_call("gelu_fwd_lt", x2, w1c, b1c)
         if res is not None:
@@ -437,7 +468,14 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
     elif need_b2:
         db2 = _bias_grad(dy2, ctx.b2_dtype)
     res = None
-    if ctx.tanh and _lt_ok(dy2, w2c, pre):
+    if (_G8 and dy2.dtype in (torch.bfloat16, torch.float16) and pre.dtype == dy2.dtype
+            and w2c.dtype == dy2.dtype and pre.is_contiguous() and dy2.is_cuda
+            and _g8_ok(dy2, _transposed(w2c))):
+        # one GEMM on the own kernel: dpre = (dy W2) * gelu'(pre) + the b1 column sums
+        res = tuple(_native.require().dense.gemm8p(
+            dy2, _transposed(w2c), 2, aux=pre, tanh=ctx.tanh,
+            bias_grad_dtype=ctx.b1_dtype or dy2.dtype))
+    elif ctx.tanh and _lt_ok(dy2, w2c, pre):
         # one GEMM: dpre = (dy W2) * gelu'(pre) and its column sums, dh never stored
         res = _lt_call("dgelu_bgrad_lt", dy2, w2c, pre, ctx.b1_dtype or dy2.dtype)
     if res is not None:

@@ -21,7 +21,7 @@
 // group touches hit distinct bank slots.  Workgroups are remapped so the tiles of one
 // A row panel run on one XCD (its 4 MB L2 then serves the panel to all of them).
 //
-// Epilogues (G8Epi): plain bf16 store; bias + GELU with the pre-activation kept (the FFN
+// bf16 or fp16 operands (v_mfma_f32_16x16x32_bf16 / _f16).  Epilogues: plain store; bias + GELU with the pre-activation kept (the FFN
 // input projection); dGELU from the saved pre-activation + the bias gradient's per-tile
 // column sums (the FFN data gradient).  M may be ragged (zero-page rows); N % 256 == 0,
 // K % 128 == 0.
@@ -84,8 +84,23 @@ __device__ __forceinline__ float g8_dgelu_erf(float x) {
   return cdf + x * pdf;
 }
 
-template <int EPI>
+template <typename T> struct G8T;
+template <> struct G8T<bf16_t> {
+  typedef bf16x8 v8;
+  static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct G8T<half_t> {
+  typedef f16x8 v8;
+  static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <typename TT, int EPI>
 __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
+  typedef typename G8T<TT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[8 * kG8Half];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -100,9 +115,9 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
   // lane -> (row j*8 + lane/8, physical chunk lane%8) fetching the logical chunk that the
   // swizzle stores there
   const int lrow = lane >> 3, pch = lane & 7;
-  const bf16_t* srcA[2][2];
+  const TT* srcA[2][2];
   bool okA[2][2];
-  const bf16_t* srcB[2][2];
+  const TT* srcB[2][2];
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -111,9 +126,9 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
       const int ch = pch ^ ((rr >> 1) & 7);
       const int arow = m0 + (rr >> 6) * 128 + q * 64 + (rr & 63);
       okA[q][i] = arow < p.M;
-      srcA[q][i] = static_cast<const bf16_t*>(p.A) + (int64_t)(okA[q][i] ? arow : 0) * p.lda + ch * 8;
+      srcA[q][i] = static_cast<const TT*>(p.A) + (int64_t)(okA[q][i] ? arow : 0) * p.lda + ch * 8;
       const int brow = n0 + (rr >> 5) * 64 + q * 32 + (rr & 31);
-      srcB[q][i] = static_cast<const bf16_t*>(p.B) + (int64_t)brow * p.ldb + ch * 8;
+      srcB[q][i] = static_cast<const TT*>(p.B) + (int64_t)brow * p.ldb + ch * 8;
     }
 
   // region r of buffer (T & 1): 0 = A_q0, 1 = A_q1, 2 = B_n0, 3 = B_n1.  Tiles past the end
@@ -132,22 +147,22 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
   };
 
   const int fr = lane & 15, fg = lane >> 4;
-  bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
-  auto readA = [&](int buf, int q, bf16x8 (&a)[4][2]) {
+  v8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+  auto readA = [&](int buf, int q, v8 (&a)[4][2]) {
     const unsigned char* R = lds + (buf * 4 + q) * kG8Half;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        a[i][ks] = *reinterpret_cast<const bf16x8*>(R + g8_swz(wm * 64 + i * 16 + fr, ks * 4 + fg));
+        a[i][ks] = *reinterpret_cast<const v8*>(R + g8_swz(wm * 64 + i * 16 + fr, ks * 4 + fg));
   };
-  auto readB = [&](int buf, int q, bf16x8 (&b)[2][2]) {
+  auto readB = [&](int buf, int q, v8 (&b)[2][2]) {
     const unsigned char* R = lds + (buf * 4 + 2 + q) * kG8Half;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        b[j][ks] = *reinterpret_cast<const bf16x8*>(R + g8_swz(wn * 32 + j * 16 + fr, ks * 4 + fg));
+        b[j][ks] = *reinterpret_cast<const v8*>(R + g8_swz(wn * 32 + j * 16 + fr, ks * 4 + fg));
   };
 
   f32x4_t acc[2][2][4][2];
@@ -166,8 +181,7 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                    \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                       \
-      acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AR[i][ks], BR[j][ks],  \
-                                                                  acc[QM][QN][i][j], 0, 0, 0); \
+      acc[QM][QN][i][j] = G8T<TT>::mma(AR[i][ks], BR[j][ks], acc[QM][QN][i][j]);         \
     __builtin_amdgcn_s_setprio(0);                                                      \
   }
 
@@ -232,7 +246,7 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
   __syncthreads();
 
   // epilogue: accumulators -> bf16 tile in LDS (the whole 128 KB) -> 16-byte row stores
-  bf16_t* T = reinterpret_cast<bf16_t*>(lds);
+  TT* T = reinterpret_cast<TT*>(lds);
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -249,15 +263,15 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
             if constexpr (EPI == 1) {  // bias before the one rounding, as addmm does
               if (p.bias)
                 v += p.bias_f32 ? static_cast<const float*>(p.bias)[n0 + col]
-                                : (float)static_cast<const bf16_t*>(p.bias)[n0 + col];
+                                : (float)static_cast<const TT*>(p.bias)[n0 + col];
             }
-            T[row * 256 + col] = (bf16_t)v;
+            T[row * 256 + col] = (TT)v;
           }
   __syncthreads();
   // each thread: one 8-column chunk (fixed for all its rows: 512 % 32 == 0) of 16 rows
   const int cc = tid & 31, rg = tid >> 5;
-  bf16_t* Cp = static_cast<bf16_t*>(p.C);
-  bf16_t* auxp = static_cast<bf16_t*>(p.aux);
+  TT* Cp = static_cast<TT*>(p.C);
+  TT* auxp = static_cast<TT*>(p.aux);
   const int col0 = n0 + cc * 8;
   float colsum[8];
 #pragma unroll
@@ -265,40 +279,33 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
   for (int row = rg; row < 256; row += kG8T / 32) {
     const int gm = m0 + row;
     if (gm >= p.M) break;
-    const uint4 v = *reinterpret_cast<const uint4*>(T + row * 256 + cc * 8);
+    const v8 v = *reinterpret_cast<const v8*>(T + row * 256 + cc * 8);
     if constexpr (EPI == 0) {
-      *reinterpret_cast<uint4*>(Cp + (int64_t)gm * p.ldc + col0) = v;
+      *reinterpret_cast<v8*>(Cp + (int64_t)gm * p.ldc + col0) = v;
     } else {
-      const unsigned w[4] = {v.x, v.y, v.z, v.w};
       float x[8];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        x[2 * k] = __uint_as_float(w[k] << 16);
-        x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-      }
+      for (int k = 0; k < 8; ++k) x[k] = (float)v[k];
       if constexpr (EPI == 1) {
-        // pre = acc + bias (one bf16 rounding, as the unfused addmm), h = gelu(pre)
-        bf16x8 pre, h;
+        // pre = acc + bias (one rounding, as the unfused addmm), h = gelu(pre)
+        v8 h;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          pre[k] = (bf16_t)x[k];
-          h[k] = (bf16_t)(p.tanh ? g8_gelu_tanh(x[k]) : g8_gelu_erf(x[k]));
-        }
-        if (auxp) *reinterpret_cast<bf16x8*>(auxp + (int64_t)gm * p.ldc + col0) = pre;
-        *reinterpret_cast<bf16x8*>(Cp + (int64_t)gm * p.ldc + col0) = h;
+        for (int k = 0; k < 8; ++k) h[k] = (TT)(p.tanh ? g8_gelu_tanh(x[k]) : g8_gelu_erf(x[k]));
+        if (auxp) *reinterpret_cast<v8*>(auxp + (int64_t)gm * p.ldc + col0) = v;
+        *reinterpret_cast<v8*>(Cp + (int64_t)gm * p.ldc + col0) = h;
       } else {
         // dpre = dh * gelu'(pre), dh = this GEMM's output rounded to bf16; bias gradient
         // partial sums of the bf16-rounded dpre
-        const bf16x8 pre = *reinterpret_cast<const bf16x8*>(auxp + (int64_t)gm * p.ldc + col0);
-        bf16x8 d;
+        const v8 pre = *reinterpret_cast<const v8*>(auxp + (int64_t)gm * p.ldc + col0);
+        v8 d;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float pf = (float)pre[k];
-          const bf16_t db = (bf16_t)(x[k] * (p.tanh ? g8_dgelu_tanh(pf) : g8_dgelu_erf(pf)));
+          const TT db = (TT)(x[k] * (p.tanh ? g8_dgelu_tanh(pf) : g8_dgelu_erf(pf)));
           d[k] = db;
           colsum[k] += (float)db;
         }
-        *reinterpret_cast<bf16x8*>(Cp + (int64_t)gm * p.ldc + col0) = d;
+        *reinterpret_cast<v8*>(Cp + (int64_t)gm * p.ldc + col0) = d;
       }
     }
   }
@@ -331,12 +338,17 @@ int gemm8p_mtiles(int M) { return (M + 255) / 256; }
 
 void gemm8p(const G8Args& a, int epi, hipStream_t st) {
   const int grid = gemm8p_mtiles(a.M) * (a.N / 256);
-  if (epi == 1)
-    hipLaunchKernelGGL(gemm8p_k<1>, dim3(grid), dim3(kG8T), 0, st, a);
-  else if (epi == 2)
-    hipLaunchKernelGGL(gemm8p_k<2>, dim3(grid), dim3(kG8T), 0, st, a);
-  else
-    hipLaunchKernelGGL(gemm8p_k<0>, dim3(grid), dim3(kG8T), 0, st, a);
+  auto go = [&](auto t0) {
+    using TT = decltype(t0);
+    if (epi == 1)
+      hipLaunchKernelGGL((gemm8p_k<TT, 1>), dim3(grid), dim3(kG8T), 0, st, a);
+    else if (epi == 2)
+      hipLaunchKernelGGL((gemm8p_k<TT, 2>), dim3(grid), dim3(kG8T), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm8p_k<TT, 0>), dim3(grid), dim3(kG8T), 0, st, a);
+  };
+  if (a.fp16) go(half_t{});
+  else go(bf16_t{});
 }
 
 }  // namespace amd

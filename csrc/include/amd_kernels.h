@@ -269,7 +269,7 @@ void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int 
                   hipStream_t st);
 
 // ---- 256 x 256 8-phase MFMA GEMM (gemm8p.hip) ---------------------------------
-// C[M, N] = A[M, K] . B[N, K]^T, bf16 row-major (K contiguous), fp32 accumulation.
+// C[M, N] = A[M, K] . B[N, K]^T, bf16 / fp16 row-major (K contiguous), fp32 accumulation.
 // epi 0: C = bf16(acc); 1: pre = bf16(acc + bias) -> aux (if non-null), C = gelu(pre);
 // 2: C = bf16(bf16(acc) * gelu'(aux)) and colsum[M-tile][N] = per-tile column sums of C.
 // Requires N % 256 == 0, K % 128 == 0 (gemm8p_supported); M ragged.
@@ -283,6 +283,7 @@ struct G8Args {
   void* aux;                   // bf16 [M][ldc] pre-activation: written (epi 1) / read (epi 2)
   float* colsum;               // [ceil(M / 256)][N] (epi 2), may be null
   int tanh;                    // GELU flavour: 1 tanh approximation, 0 erf
+  int fp16;                    // operands / outputs fp16 instead of bf16
 };
 bool gemm8p_supported(int M, int N, int K);
 int gemm8p_mtiles(int M);

@@ -102,7 +102,8 @@ std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tenso
 
 bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
   return a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 &&
-         a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+         (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf) &&
+         b.scalar_type() == a.scalar_type() &&
          a.stride(1) == 1 && b.stride(1) == 1 && a.size(1) == b.size(1) &&
          a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
          reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
@@ -115,7 +116,7 @@ std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
                                   bool want_pre, bool tanh_approx,
                                   c10::optional<at::ScalarType> bias_grad_dtype) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(gemm8p_ok(a, b), "gemm8p: bf16 [M, K] x [N, K] with N % 256 == 0, K % 128 == 0, "
+  TORCH_CHECK(gemm8p_ok(a, b), "gemm8p: bf16 / fp16 [M, K] x [N, K] with N % 256 == 0, K % 128 == 0, "
               "unit column stride, 16-byte aligned rows");
   TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8p: epi 0 | 1 | 2");
   const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
@@ -131,12 +132,13 @@ std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
   g.ldb = (int)b.stride(0);
   g.ldc = (int)N;
   g.tanh = tanh_approx ? 1 : 0;
+  g.fp16 = a.scalar_type() == at::kHalf ? 1 : 0;
   std::vector<at::Tensor> out{c};
   if (epi == 1) {
     if (bias.has_value() && bias->defined()) {
       TORCH_CHECK(bias->is_cuda() && bias->is_contiguous() && bias->numel() == N &&
-                      (bias->scalar_type() == at::kBFloat16 || bias->scalar_type() == at::kFloat),
-                  "gemm8p: bias must be a contiguous bf16 / fp32 [N] GPU tensor");
+                      (bias->scalar_type() == a.scalar_type() || bias->scalar_type() == at::kFloat),
+                  "gemm8p: bias must be a contiguous [N] GPU tensor of the operand dtype or fp32");
       g.bias = bias->data_ptr();
       g.bias_f32 = bias->scalar_type() == at::kFloat ? 1 : 0;
     }
@@ -147,7 +149,7 @@ std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
     }
   } else if (epi == 2) {
     TORCH_CHECK(aux.has_value() && aux->defined() && aux->is_cuda() &&
-                    aux->scalar_type() == at::kBFloat16 && aux->is_contiguous() &&
+                    aux->scalar_type() == a.scalar_type() && aux->is_contiguous() &&
                     aux->numel() == M * N,
                 "gemm8p: epi 2 needs the contiguous bf16 [M, N] pre-activation");
     g.aux = aux->data_ptr();

@@ -15,13 +15,14 @@ def _dn():
     return _native.require().dense
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("mnk", [(256, 256, 128), (1000, 512, 256), (4096, 1024, 1024),
                                  (333, 4096, 384), (16384, 256, 1024)])
-def test_gemm8p_plain(mnk):
+def test_gemm8p_plain(mnk, dtype):
     m, n, k = mnk
     g = torch.Generator(device=DEV).manual_seed(m + n + k)
-    a = torch.randn(m, k, device=DEV, generator=g).to(torch.bfloat16)
-    b = torch.randn(n, k, device=DEV, generator=g).to(torch.bfloat16)
+    a = torch.randn(m, k, device=DEV, generator=g).to(dtype)
+    b = torch.randn(n, k, device=DEV, generator=g).to(dtype)
     assert _dn().gemm8p_ok(a, b)
     c, = _dn().gemm8p(a, b)
     ref = a.float() @ b.float().t()
@@ -43,12 +44,14 @@ def test_gemm8p_strided_rows():
 
 
 @pytest.mark.parametrize("tanh", [False, True])
-@pytest.mark.parametrize("bias_dtype", [torch.bfloat16, torch.float32])
-def test_gemm8p_gelu_epilogues(tanh, bias_dtype):
+@pytest.mark.parametrize("dtype,bias_dtype", [(torch.bfloat16, torch.bfloat16),
+                                              (torch.bfloat16, torch.float32),
+                                              (torch.float16, torch.float16)])
+def test_gemm8p_gelu_epilogues(tanh, dtype, bias_dtype):
     m, n, k = 1536, 1024, 512
     g = torch.Generator(device=DEV).manual_seed(7)
-    x = torch.randn(m, k, device=DEV, generator=g).to(torch.bfloat16)
-    w = (torch.randn(n, k, device=DEV, generator=g) / k ** 0.5).to(torch.bfloat16)
+    x = torch.randn(m, k, device=DEV, generator=g).to(dtype)
+    w = (torch.randn(n, k, device=DEV, generator=g) / k ** 0.5).to(dtype)
     bias = (torch.randn(n, device=DEV, generator=g) * 0.1).to(bias_dtype)
     approx = "tanh" if tanh else "none"
     h, pre = _dn().gemm8p(x, w, 1, bias=bias, want_pre=True, tanh=tanh)
@@ -57,10 +60,10 @@ def test_gemm8p_gelu_epilogues(tanh, bias_dtype):
     h_ref = F.gelu(pre.float(), approximate=approx)   # gelu of the rounded pre-activation
     assert float((h.float() - h_ref).abs().max()) < 2e-2
     # backward: dpre = dh * gelu'(pre), dh = dy @ W2^T computed by the GEMM
-    dy = torch.randn(m, 768, device=DEV, generator=g).to(torch.bfloat16)
-    w2t = (torch.randn(n, 768, device=DEV, generator=g) / 768 ** 0.5).to(torch.bfloat16)
+    dy = torch.randn(m, 768, device=DEV, generator=g).to(dtype)
+    w2t = (torch.randn(n, 768, device=DEV, generator=g) / 768 ** 0.5).to(dtype)
     dpre, db = _dn().gemm8p(dy, w2t, 2, aux=pre, tanh=tanh, bias_grad_dtype=torch.float32)
-    dh = (dy.float() @ w2t.float().t()).to(torch.bfloat16).float()
+    dh = (dy.float() @ w2t.float().t()).to(dtype).float()
     p = pre.float().requires_grad_(True)
     gref, = torch.autograd.grad(F.gelu(p, approximate=approx), p, dh)
     scale = float(gref.abs().max())

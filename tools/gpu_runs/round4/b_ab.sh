@@ -5,6 +5,9 @@ cd /root/repo
 export TMPDIR=/tmp
 O=gpurun_out/r4b
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gemm8p_gpu.py > $O/gemm8p_tests.log 2>&1
+timeout -k 10 300 python -u tools/gemm8p_bench.py > $O/gemm8p_bench.md 2>&1
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
   tests/test_ddp_gpu.py tests/test_amp_gpu.py tests/test_graph_gpu.py tests/test_conv_bn_bwd_gpu.py \
   tests/test_models_gpu.py > $O/tests.log 2>&1
