@@ -111,6 +111,11 @@ def parse():
     ap.add_argument("--ddp-bf16-wire", choices=["rsag", "fp32", "native"], default=None,
                     help="how a bf16 DDP bucket travels: fp32 reduce-scatter + bf16 all-gather "
                          "(default), fp32 all-reduce, or native bf16 all-reduce")
+    ap.add_argument("--main-stream-priority", choices=["default", "high"],
+                    default=os.environ.get("APEX_AMD_MAIN_STREAM_PRIO", "default"),
+                    help="high: run the training step on a high-priority HIP stream, so its "
+                         "critical-path kernels win the CUs over the side-stream weight "
+                         "gradients")
     ap.add_argument("--bucket-timing-steps", type=int, default=5,
                     help="N > 1: extra untimed steps with per-bucket DDP timing (0 = off)")
     ap.add_argument("--json-out", default=None)
@@ -622,6 +627,11 @@ def main():
     else:
         w = build_gpt2(args, device, world)
     step, batch = w.step, w.batch
+    if args.main_stream_priority == "high" and device.type == "cuda":
+        hp = torch.cuda.Stream(device, priority=torch.cuda.Stream.priority_range()[1])
+        hp.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(hp)  # every later launch of this thread goes to it
+    w.config["main_stream_priority"] = args.main_stream_priority
 
     log(rank, "[bench] impl=%s model=%s units/gpu/step=%d world=%d warmup=%d steps=%d" % (
         args.impl, args.model, w.units, world, args.warmup, args.steps))
