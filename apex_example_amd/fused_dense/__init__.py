@@ -388,9 +388,10 @@ def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype):
 # The FFN on the own 8-phase MFMA GEMM (csrc/hip/gemm8p.hip) with its epilogues: forward
 # h = gelu(x W1^T + b1) keeping the pre-activation (no separate GELU pass), backward
 # dpre = (dy W2) * gelu'(pre) with the b1 gradient's column sums (no dh round trip, no
-# column-sum kernels).  bf16 / fp16 operands, N % 256 == 0, K % 128 == 0.  APEX_AMD_GEMM8P=0
-# keeps the library GEMM + streaming kernels.
-_G8 = os.environ.get("APEX_AMD_GEMM8P", "1") == "1"
+# column-sum kernels).  bf16 / fp16 operands, N % 256 == 0, K % 128 == 0.  Opt-in
+# (APEX_AMD_GEMM8P=1) while the kernel trails hipBLASLt on these shapes
+# (profiles/r4/gemm8p_bench.md).
+_G8 = os.environ.get("APEX_AMD_GEMM8P", "0") == "1"
 _T_CACHE = {}  # id(weight) -> (weight, version, data_ptr, transposed copy)
 
 

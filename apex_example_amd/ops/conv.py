@@ -74,18 +74,23 @@ def _side_mode(params):
     return None
 
 
-# APEX_AMD_WGRAD_STREAM_DDP=1: side-stream weight gradients under DDP too.  Off by
-# default: ResNet-50 with forced world-1 collectives measured 8130 img/s with it vs
-# 8949 without (same box; the side stream ends backward ~5 ms behind the compute
-# stream, and the last buckets wait for it: exposed tail 5.2 vs 0.06 ms).
-_DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "0") == "1"
+# Side-stream weight gradients under DDP (APEX_AMD_WGRAD_STREAM_DDP=0 disables): on a
+# HIGH-priority side stream of their own (its wgrads then keep pace with the data
+# gradients instead of trailing them; the last buckets wait for the side stream) with a
+# bounded lag.  ResNet-50 with forced world-1 collectives, same box: 9,865 / 9,871 img/s
+# without, 8,083 / 8,079 with a normal-priority side stream (exposed tail 0.9 ms),
+# 10,418 / 10,417 with the high-priority one (tail 0.14 ms) - 98.6 % of the plain step
+# (profiles/r4/).
+_DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "1") == "1"
 # Bounded side-stream lag: the main stream waits for the weight gradient enqueued
 # APEX_AMD_WGRAD_LAG launches earlier (0 = unbounded; default 4 under DDP, where the last
 # buckets cannot launch before the side stream reaches their gradients), and
 # APEX_AMD_WGRAD_STREAM_PRIO=high creates the side stream with high priority (its weight
 # gradients then run ahead of the data-gradient chain instead of trailing it).
 _LAG = int(os.environ.get("APEX_AMD_WGRAD_LAG", "-1"))
-_SIDE_PRIO = os.environ.get("APEX_AMD_WGRAD_STREAM_PRIO", "normal")
+# priority of the side stream: "auto" = high under DDP, normal for the single-GPU 'free'
+# mode (same box: 10,565 / 10,534 img/s normal vs 10,531 / 10,500 high there)
+_SIDE_PRIO = os.environ.get("APEX_AMD_WGRAD_STREAM_PRIO", "auto")
 _SIDE_EVENTS = {}   # device index -> deque of side-stream events, oldest first
 
 
@@ -96,7 +101,9 @@ def _join_side():
         for idx, _ in pending:
             _SIDE_EVENTS.pop(idx, None)
     for idx, (main, _task) in pending:
-        main.wait_stream(_SIDE[idx])
+        for key, side in list(_SIDE.items()):
+            if key[0] == idx:
+                main.wait_stream(side)
 
 
 def _lag_for(mode):
@@ -123,10 +130,12 @@ class _SideWgrad:
         if self.on:
             dev = weight.device
             self.main = torch.cuda.current_stream(dev)
-            self.side = _SIDE.get(dev.index)
+            high = _SIDE_PRIO == "high" or (_SIDE_PRIO == "auto" and self.mode == "ddp")
+            key = (dev.index, high)
+            self.side = _SIDE.get(key)
             if self.side is None:
-                prio = torch.cuda.Stream.priority_range()[1] if _SIDE_PRIO == "high" else 0
-                self.side = _SIDE[dev.index] = torch.cuda.Stream(dev, priority=prio)
+                prio = torch.cuda.Stream.priority_range()[1] if high else 0
+                self.side = _SIDE[key] = torch.cuda.Stream(dev, priority=prio)
             self.ev = self.main.record_event()
 
     def run(self, fn, *used):

@@ -276,10 +276,17 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
   float colsum[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) colsum[k] = 0.f;
-  for (int row = rg; row < 256; row += kG8T / 32) {
+  // all 16 LDS rows first (one lgkmcnt wait), then the stores / epilogue math
+  v8 rv[256 / (kG8T / 32)];
+#pragma unroll
+  for (int q = 0; q < 256 / (kG8T / 32); ++q)
+    rv[q] = *reinterpret_cast<const v8*>(T + (rg + q * (kG8T / 32)) * 256 + cc * 8);
+#pragma unroll
+  for (int q = 0; q < 256 / (kG8T / 32); ++q) {
+    const int row = rg + q * (kG8T / 32);
     const int gm = m0 + row;
-    if (gm >= p.M) break;
-    const v8 v = *reinterpret_cast<const v8*>(T + row * 256 + cc * 8);
+    if (gm >= p.M) continue;
+    const v8 v = rv[q];
     if constexpr (EPI == 0) {
       *reinterpret_cast<v8*>(Cp + (int64_t)gm * p.ldc + col0) = v;
     } else {
