@@ -25,6 +25,7 @@
 // input projection); dGELU from the saved pre-activation + the bias gradient's per-tile
 // column sums (the FFN data gradient).  M may be ragged (zero-page rows); N % 256 == 0,
 // K % 128 == 0.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -103,8 +104,20 @@ __global__ void __launch_bounds__(kG8T, 1) gemm8p_k(G8Args p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR math
   const int wm = wid >> 2, wn = wid & 3;
   const int ntn = p.N >> 8;
+  // XCD x runs a contiguous range of tile ids; within it the ids go down groups of
+  // group_m m-tiles first, so the ~32 tiles an XCD runs at once form a group_m x 8 block
+  // (group_m A panels + 8 B panels through its L2 per K-step instead of 1 + 32)
   const int bid = g8_xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = bid / ntn, tn = bid - tm * ntn;
+  int tm, tn;
+  if (p.group_m > 1) {
+    const int mt = gridDim.x / ntn, gsz = p.group_m * ntn, g = bid / gsz;
+    const int first = g * p.group_m, rows = min(p.group_m, mt - first), r = bid - g * gsz;
+    tm = first + r % rows;
+    tn = r / rows;
+  } else {
+    tm = bid / ntn;
+    tn = bid - tm * ntn;
+  }
   const int m0 = tm * 256, n0 = tn * 256;
   const int KT = p.K >> 6;
 
@@ -461,7 +474,18 @@ static int g8_sched() {
   return v;
 }
 
-void gemm8p(const G8Args& a, int epi, hipStream_t st) {
+// APEX_AMD_G8_GROUPM: m-tiles per tile-order group (default 4; 1 = row-major tile order)
+static int g8_group_m() {
+  static const int v = [] {
+    const char* e = std::getenv("APEX_AMD_G8_GROUPM");
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  return v;
+}
+
+void gemm8p(const G8Args& a0, int epi, hipStream_t st) {
+  G8Args a = a0;
+  a.group_m = g8_group_m();
   const int grid = gemm8p_mtiles(a.M) * (a.N / 256);
   auto launch = [&](auto t0, auto s0) {
     using TT = decltype(t0);

@@ -284,6 +284,7 @@ struct G8Args {
   float* colsum;               // [ceil(M / 256)][N] (epi 2), may be null
   int tanh;                    // GELU flavour: 1 tanh approximation, 0 erf
   int fp16;                    // operands / outputs fp16 instead of bf16
+  int group_m;                 // tile order: groups of group_m m-tiles (set by gemm8p())
 };
 bool gemm8p_supported(int M, int N, int K);
 int gemm8p_mtiles(int M);
