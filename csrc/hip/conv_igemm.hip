@@ -34,6 +34,9 @@ namespace {
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kCT = 256;  // threads
+#ifndef CONV_INTERLEAVE
+#define CONV_INTERLEAVE 1
+#endif
 constexpr int kBM = 128;
 constexpr int kBK = 64;
 constexpr int kRowBytes = kBK * 2;  // 128
@@ -108,6 +111,7 @@ __device__ __forceinline__ void conv_tap(int z, int t, int& dh, int& dw, int& wt
 // B rows ([NC][taps][KC]) are kb_stride elements long
 struct ConvGeom {
   int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
+  int burst;  // 1: the 4-wave ring issues each tile's DMA as one burst (A/B reference)
 };
 
 // BN-backward epilogue (conv_tap_k EPI == 1, ConvBnEpi).  Each thread owns one 8-channel
@@ -376,46 +380,207 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   // LDS tile write instead of being waited for at a __syncthreads()
   BnPre<BM, BN, CT> pre;
 
-  // prologue: NB-1 tiles in flight
-#pragma unroll
-  for (int p = 0; p < NB - 1; ++p)
-    if (p < KT) CONV_ISSUE(p);
-
-  for (int kt = 0; kt < KT; ++kt) {
-    if constexpr (NB == 1) {
-      if (kt > 0) __syncthreads();  // every wave is done reading the single buffer
-      CONV_ISSUE(kt);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+  // the halo's zero source, pinned in VGPRs: re-materialised inside the loop it is a
+  // GOT load (SMEM), whose lgkmcnt(0) wait would also wait for the fragment reads
+  const void* zsrc = (const void*)g_zero16;
+  asm volatile("" : "+v"(zsrc));
+  // a tile's DMA geometry, computed once per tile (scalar): buffer, A offset, tap, B offset
+  struct TileSrc {
+    unsigned char* A;
+    int64_t aoff;
+    int tap, boff;
+  };
+  auto tile_src = [&](int kt_) {
+    TileSrc t;
+    t.tap = kt_ / kc_per_tap;
+    const int c0_ = (kt_ - t.tap * kc_per_tap) * kBK;
+    int dh_, dw_, wt_;
+    conv_tap<MODE>(z, t.tap, dh_, dw_, wt_);
+    t.A = lds + (kt_ % NB) * BUF;
+    t.aoff = (int64_t)(dh_ * g.AW + dw_) * KC + c0_;
+    t.boff = wt_ * KC + c0_;
+    return t;
+  };
+  auto piece = [&](const TileSrc& t, int q) {
+    if (q < AI) {
+      const bool ok = (amask[q] >> t.tap) & 1u;
+      const void* src = (const void*)(abase[q] + t.aoff);
+      glds16(ok ? src : zsrc, t.A + (wid * (BM / NW) + q * 8) * kRowBytes);
     } else {
-      // retire tile kt: leave the (NB-2) younger tiles' DMAs in flight
-      if (kt + NB - 2 < KT) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NB > 2 ? NB - 2 : 0)) : "memory");
+      const int qb = q - AI;
+      glds16(bbase[qb] + t.boff, t.A + A_BYTES + (wid * (BN / NW) + qb * 8) * kRowBytes);
+    }
+  };
+  bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+  auto rd_a = [&](int kt_, int ks, bf16x8 (&af)[FM]) {
+    const unsigned char* A = lds + (kt_ % NB) * BUF;
+    const int ch = ks * 4 + fg;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
+  };
+  auto rd_b = [&](int kt_, int ks, bf16x8 (&bfr)[FN]) {
+    const unsigned char* B = lds + (kt_ % NB) * BUF + A_BYTES;
+    const int ch = ks * 4 + fg;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
+  };
+  auto rd = [&](int kt_, int ks, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
+    const unsigned char* A = lds + (kt_ % NB) * BUF;
+    const unsigned char* B = A + A_BYTES;
+    const int ch = ks * 4 + fg;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
+  };
+
+  // 4-wave forms on a 2- or 3-deep ring: both k-steps' fragments read ahead, DMA pieces
+  // between the MFMA rows (CONV_INTERLEAVE=0 at build time: the burst form, for A/B)
+  constexpr bool interleave = CONV_INTERLEAVE != 0;
+  if constexpr (CT == 512 && NB == 3) {
+    // 8-wave form: ONE barrier per K-tile.  Phase A multiplies k-step 0 of tile kt from
+    // registers while it reads k-step 1's fragments and issues the last PA DMA pieces of
+    // tile kt+2 between the MFMA rows; phase B waits for tile kt+1 (vmcnt(G) leaves all
+    // of tile kt+2 in flight), passes the barrier, and multiplies k-step 1 while it reads
+    // tile kt+1's k-step-0 fragments and issues the first PB pieces of tile kt+3.  Tile
+    // T's buffer (T % 3) was last read in phase A(T-3), retired (lgkmcnt(0)) before
+    // barrier B(T-3), after which its first pieces go out; a DMA piece costs ~60 issue
+    // cycles, which the partner wave's MFMAs hide when it sits between MFMA rows instead
+    // of in a burst after a barrier, and a whole tile (48 KB at 256 x 128) stays in
+    // flight across every barrier.
+    constexpr int PA = (G + 1) / 2, PB = G - PA;
+    static_assert(PA <= FM && PB <= FM, "DMA pieces per MFMA row");
+    if (KT > 0) {
+      const TileSrc t0 = tile_src(0);
+#pragma unroll
+      for (int q = 0; q < G; ++q) piece(t0, q);
+    }
+    if (KT > 1) {
+      const TileSrc t1 = tile_src(1);
+#pragma unroll
+      for (int q = 0; q < G; ++q) piece(t1, q);
+    }
+    if (KT > 2) {
+      const TileSrc t2 = tile_src(2);
+#pragma unroll
+      for (int q = 0; q < PB; ++q) piece(t2, q);
+    }
+    if (KT > 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + PB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    rd(0, 0, fa0, fb0);
+    for (int kt = 0; kt < KT; ++kt) {
+      const bool more = kt + 2 < KT, more3 = kt + 3 < KT;
+      const TileSrc tA = tile_src(more ? kt + 2 : kt);
+      const TileSrc tB = tile_src(more3 ? kt + 3 : kt);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i < PA && more) piece(tA, PB + i);
+        if (i == 0) rd(kt, 1, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (more) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // the buffer of tile kt+NB-1 was last read at iteration kt-1: every wave has
-      // passed this barrier, so it is free
-      if (kt + NB - 1 < KT) CONV_ISSUE(kt + NB - 1);
-    }
-    const unsigned char* A = lds + (kt % NB) * BUF;
-    const unsigned char* B = A + A_BYTES;
+      asm volatile("" ::: "memory");
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 4 + fg;
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i < PB && more3) piece(tB, i);
+        if (i == 0 && kt + 1 < KT) rd(kt + 1, 0, fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
+    // prologue: NB-1 tiles in flight
+  #pragma unroll
+    for (int p = 0; p < NB - 1; ++p)
+      if (p < KT) CONV_ISSUE(p);
+
+    for (int kt = 0; kt < KT; ++kt) {
+      if constexpr (NB == 1) {
+        if (kt > 0) __syncthreads();  // every wave is done reading the single buffer
+        CONV_ISSUE(kt);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      } else {
+        // retire tile kt: leave the (NB-2) younger tiles' DMAs in flight
+        if (kt + NB - 2 < KT) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (NB > 2 ? NB - 2 : 0)) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (interleave && !g.burst) {
+          // both k-steps' fragments first, then the MFMA rows with tile kt+NB-1's DMA
+          // pieces between them (the buffer of tile kt+NB-1 was last read at iteration
+          // kt-1: every wave has passed this barrier, so it is free)
+          const bool issue = kt + NB - 1 < KT;
+          const TileSrc tn = tile_src(issue ? kt + NB - 1 : kt);
+          bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+          // (at most 15 LDS reads may be outstanding for a counted lgkmcnt: k-step 1's B
+          // fragments go out after the first MFMA row)
+          rd(kt, 0, fa0, fb0);
+          __builtin_amdgcn_sched_barrier(0);
+          rd_a(kt, 1, fa1);
+          __builtin_amdgcn_sched_barrier(0);
+          constexpr int PER = (G + 2 * FM - 1) / (2 * FM);
+#pragma unroll
+          for (int r = 0; r < 2 * FM; ++r) {
+            const int i = r % FM;
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  r < FM ? fa0[i] : fa1[i], r < FM ? fb0[j] : fb1[j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (r == 0) rd_b(kt, 1, fb1);
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+              if (issue && r * PER + u < G) piece(tn, r * PER + u);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          continue;
+        }
+        if (kt + NB - 1 < KT) CONV_ISSUE(kt + NB - 1);
+      }
+      const unsigned char* A = lds + (kt % NB) * BUF;
+      const unsigned char* B = A + A_BYTES;
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = ks * 4 + fg;
+        bf16x8 af[FM], bfr[FN];
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
+  #pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+  #pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
   }
 #undef CONV_ISSUE
@@ -556,11 +721,20 @@ static bool conv64_nb2() {
   return e ? e[0] == '1' : true;
 }
 
+// APEX_AMD_CONV_BURST=1 (read per launch, A/B runs): the 4-wave kernels' pre-round-4 K
+// loop - each tile's DMA pieces as one burst after the barrier, fragments read per k-step
+static int conv_burst() {
+  const char* e = std::getenv("APEX_AMD_CONV_BURST");
+  return e ? (e[0] == '1' ? 1 : 0) : 1;
+}
+
 template <int MODE, int EPI = 0>
-void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
+void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g0,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
                      const ConvBnEpi& ep = ConvBnEpi{}) {
-  if (g.M == 0) return;
+  if (g0.M == 0) return;
+  ConvGeom g = g0;
+  g.burst = conv_burst();
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
   if (big >= 4) {

@@ -38,6 +38,18 @@ def cl(t):
     return t.to(memory_format=torch.channels_last)
 
 
+def _select(v):
+    """variant name -> env: 'default', an APEX_AMD_CONV_BM value, 'burst' / 'ileave' (the
+    4-wave K loop with each tile's DMA as one burst / with read-ahead and DMA pieces
+    between the MFMA rows, APEX_AMD_CONV_BURST=1 / 0)"""
+    os.environ.pop("APEX_AMD_CONV_BM", None)
+    os.environ.pop("APEX_AMD_CONV_BURST", None)
+    if v in ("burst", "ileave"):
+        os.environ["APEX_AMD_CONV_BURST"] = "1" if v == "burst" else "0"
+    elif v != "default":
+        os.environ["APEX_AMD_CONV_BM"] = v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", nargs="+", default=["default", "256w8", "256w8n2", "128w8"])
@@ -78,24 +90,18 @@ def main():
     res = {(n, v): [] for n, _, _ in cases for v in a.variants}
     bad = []
     for name, gf, fn in cases:
-        os.environ.pop("APEX_AMD_CONV_BM", None)
+        _select("default")
         ref = fn().clone()
         for v in a.variants:
-            if v != "default":
-                os.environ["APEX_AMD_CONV_BM"] = v
-            else:
-                os.environ.pop("APEX_AMD_CONV_BM", None)
+            _select(v)
             if not torch.equal(fn(), ref):
                 bad.append((name, v))
     for _ in range(a.rounds):
         for name, gf, fn in cases:
             for v in a.variants:
-                if v != "default":
-                    os.environ["APEX_AMD_CONV_BM"] = v
-                else:
-                    os.environ.pop("APEX_AMD_CONV_BM", None)
+                _select(v)
                 res[(name, v)].append(timeit(fn, a.iters))
-    os.environ.pop("APEX_AMD_CONV_BM", None)
+    _select("default")
     print("| conv | GFLOP | " + " | ".join(a.variants) + " |")
     print("|---|---|" + "---|" * len(a.variants))
     for name, gf, _ in cases:
