@@ -47,6 +47,22 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
+// LDS image of a K-tile of RB-byte rows (RB = 2 * BK): 16-byte chunks XOR-swizzled so the
+// 16 rows a ds_read_b128 lane group reads (rows fr = lane & 15, chunk lane >> 4 (+4 k))
+// hit distinct bank slots.  128-byte rows: key (row >> 1) & 7.  64-byte rows (four rows per
+// 256-byte bank line, so bank slot = 4 (row & 3) + chunk): key ((row >> 2) & 1) << 1 -
+// each group's rows {0-3, 12-15} x chunk c and {4-11} x chunk c ^ 1 land on 16 distinct
+// slots.
+template <int RB>
+__device__ __forceinline__ int swz_key(int row) {
+  if constexpr (RB == 128) return (row >> 1) & 7;
+  else return ((row >> 2) & 1) << 1;
+}
+template <int RB>
+__device__ __forceinline__ int swzr(int row, int chunk) {
+  return row * RB + ((chunk ^ swz_key<RB>(row)) << 4);
+}
+
 __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
@@ -265,9 +281,12 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
 // CT = 512 (8 waves, one workgroup per CU): the 256 x 128 tile on a 3-deep ring (144 KB of
 // LDS), 64 x 64 per wave - two waves per SIMD like the 2-workgroup 128 x 128 form, but two
 // tiles' DMAs stay in flight across every barrier instead of one.
-template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0, int CT = kCT>
+// BK = 32: 64-byte K-tile rows - half the LDS per ring stage, so a 4-deep ring fits two
+// workgroups per CU with three stages (48 KB) in flight instead of one 32 KB tile.
+template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0, int CT = kCT,
+          int BK = kBK>
 __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
-                                       NB * (BM + BN) * kRowBytes > 80 * 1024)
+                                       NB * (BM + BN) * BK * 2 > 80 * 1024)
                                           ? 1 : (NB == 1 && EPI == 0 ? 3 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
@@ -276,10 +295,14 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   static_assert(WM * WN == NW, "one wave per output sub-tile");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
+  constexpr int RB = BK * 2;        // bytes per K-tile row
+  constexpr int LPR = RB / 16;      // DMA lanes per row
+  constexpr int RPI = 64 / LPR;     // rows per DMA wave-instruction
+  constexpr int KS = BK / 32;       // MFMA k-steps per K-tile
+  constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB;
   constexpr int BUF = A_BYTES + B_BYTES;
-  constexpr int AI = BM / (8 * NW);  // A wave-instructions (8 rows each) per wave per tile
-  constexpr int BI = BN / (8 * NW);  // B wave-instructions per wave per tile
+  constexpr int AI = BM / (RPI * NW);  // A wave-instructions (RPI rows each) per wave per tile
+  constexpr int BI = BN / (RPI * NW);  // B wave-instructions per wave per tile
   static_assert(AI >= 1 && BI >= 1, "tile rows per wave");
   constexpr int G = AI + BI;        // glds per wave per tile (vmcnt units)
   // the ring, or the epilogue's bf16 tile / statistics exchange if larger
@@ -298,7 +321,7 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   // DMA lane geometry: wave `wid` fills A rows [wid*32, wid*32+32) as AI
   // instructions of 8 rows; lane -> (row = base + lane/8, physical chunk lane%8)
   // fetching the logical chunk that the swizzle stores at that position.
-  const int lrow = lane >> 3, pchunk = lane & 7;
+  const int lrow = lane / LPR, pchunk = lane % LPR;
   // per DMA row: source pointer at the centre pixel / channel chunk, and a bit
   // mask of the taps whose pixel is inside the A image (so the K loop only adds a
   // wave-uniform offset and tests one bit per row)
@@ -306,8 +329,8 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   unsigned amask[AI];
 #pragma unroll
   for (int q = 0; q < AI; ++q) {
-    const int row = wid * (BM / NW) + q * 8 + lrow;
-    const int ch = pchunk ^ ((row >> 1) & 7);
+    const int row = wid * (BM / NW) + q * RPI + lrow;
+    const int ch = pchunk ^ swz_key<RB>(row);
     const int m = m0 + row;
     const int mm = m < M ? m : 0;
     const int n = mm / GHW;
@@ -329,16 +352,16 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   const bf16_t* bbase[BI];
 #pragma unroll
   for (int q = 0; q < BI; ++q) {
-    const int row = wid * (BN / NW) + q * 8 + lrow;
-    bbase[q] = wt + (int64_t)(n0 + row) * g.kb_stride + (pchunk ^ ((row >> 1) & 7)) * 8;
+    const int row = wid * (BN / NW) + q * RPI + lrow;
+    bbase[q] = wt + (int64_t)(n0 + row) * g.kb_stride + (pchunk ^ swz_key<RB>(row)) * 8;
   }
-  const int kc_per_tap = KC / kBK;
+  const int kc_per_tap = KC / BK;
   const int KT = ntaps * kc_per_tap;
 
 #define CONV_ISSUE(kt_)                                                                     \
   {                                                                                         \
     const int tap_ = (kt_) / kc_per_tap;                                                    \
-    const int c0_ = ((kt_) - tap_ * kc_per_tap) * kBK;                                      \
+    const int c0_ = ((kt_) - tap_ * kc_per_tap) * BK;                                       \
     int dh_, dw_, wt_;                                                                      \
     conv_tap<MODE>(z, tap_, dh_, dw_, wt_);                                                 \
     const int64_t aoff_ = (int64_t)(dh_ * g.AW + dw_) * KC + c0_;                           \
@@ -348,10 +371,10 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
     _Pragma("unroll") for (int q = 0; q < AI; ++q) {                                        \
       const bool ok = (amask[q] >> tap_) & 1u;                                              \
       glds16(ok ? (const void*)(abase[q] + aoff_) : (const void*)g_zero16,                  \
-             A_ + (wid * (BM / NW) + q * 8) * kRowBytes);                                  \
+             A_ + (wid * (BM / NW) + q * RPI) * RB);                                       \
     }                                                                                       \
     _Pragma("unroll") for (int q = 0; q < BI; ++q)                                          \
-      glds16(bbase[q] + boff_, B_ + (wid * (BN / NW) + q * 8) * kRowBytes);                 \
+      glds16(bbase[q] + boff_, B_ + (wid * (BN / NW) + q * RPI) * RB);                      \
   }
 
   f32x4_t acc[FM][FN];
@@ -393,7 +416,7 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   auto tile_src = [&](int kt_) {
     TileSrc t;
     t.tap = kt_ / kc_per_tap;
-    const int c0_ = (kt_ - t.tap * kc_per_tap) * kBK;
+    const int c0_ = (kt_ - t.tap * kc_per_tap) * BK;
     int dh_, dw_, wt_;
     conv_tap<MODE>(z, t.tap, dh_, dw_, wt_);
     t.A = lds + (kt_ % NB) * BUF;
@@ -405,10 +428,10 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
     if (q < AI) {
       const bool ok = (amask[q] >> t.tap) & 1u;
       const void* src = (const void*)(abase[q] + t.aoff);
-      glds16(ok ? src : zsrc, t.A + (wid * (BM / NW) + q * 8) * kRowBytes);
+      glds16(ok ? src : zsrc, t.A + (wid * (BM / NW) + q * RPI) * RB);
     } else {
       const int qb = q - AI;
-      glds16(bbase[qb] + t.boff, t.A + A_BYTES + (wid * (BN / NW) + qb * 8) * kRowBytes);
+      glds16(bbase[qb] + t.boff, t.A + A_BYTES + (wid * (BN / NW) + qb * RPI) * RB);
     }
   };
   bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
@@ -417,14 +440,14 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
     const int ch = ks * 4 + fg;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
+      af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, ch));
   };
   auto rd_b = [&](int kt_, int ks, bf16x8 (&bfr)[FN]) {
     const unsigned char* B = lds + (kt_ % NB) * BUF + A_BYTES;
     const int ch = ks * 4 + fg;
 #pragma unroll
     for (int j = 0; j < FN; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
+      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swzr<RB>(wn * TN + j * 16 + fr, ch));
   };
   auto rd = [&](int kt_, int ks, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
     const unsigned char* A = lds + (kt_ % NB) * BUF;
@@ -432,16 +455,16 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
     const int ch = ks * 4 + fg;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
+      af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, ch));
 #pragma unroll
     for (int j = 0; j < FN; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
+      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swzr<RB>(wn * TN + j * 16 + fr, ch));
   };
 
   // 4-wave forms on a 2- or 3-deep ring: both k-steps' fragments read ahead, DMA pieces
   // between the MFMA rows (CONV_INTERLEAVE=0 at build time: the burst form, for A/B)
   constexpr bool interleave = CONV_INTERLEAVE != 0;
-  if constexpr (CT == 512 && NB == 3) {
+  if constexpr (CT == 512 && NB == 3 && BK == 64) {
     // 8-wave form: ONE barrier per K-tile.  Phase A multiplies k-step 0 of tile kt from
     // registers while it reads k-step 1's fragments and issues the last PA DMA pieces of
     // tile kt+2 between the MFMA rows; phase B waits for tile kt+1 (vmcnt(G) leaves all
@@ -531,7 +554,7 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (interleave && !g.burst) {
+        if (interleave && BK == 64 && !g.burst) {
           // both k-steps' fragments first, then the MFMA rows with tile kt+NB-1's DMA
           // pieces between them (the buffer of tile kt+NB-1 was last read at iteration
           // kt-1: every wave has passed this barrier, so it is free)
@@ -566,15 +589,15 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
       const unsigned char* A = lds + (kt % NB) * BUF;
       const unsigned char* B = A + A_BYTES;
   #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         const int ch = ks * 4 + fg;
         bf16x8 af[FM], bfr[FN];
   #pragma unroll
         for (int i = 0; i < FM; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * TM + i * 16 + fr, ch));
+          af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, ch));
   #pragma unroll
         for (int j = 0; j < FN; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * TN + j * 16 + fr, ch));
+          bfr[j] = *reinterpret_cast<const bf16x8*>(B + swzr<RB>(wn * TN + j * 16 + fr, ch));
   #pragma unroll
         for (int i = 0; i < FM; ++i)
   #pragma unroll
@@ -692,6 +715,8 @@ static int conv_bm_choice() {
   if (std::strcmp(e, "256w8") == 0) return 4;
   if (std::strcmp(e, "256w8n2") == 0) return 5;
   if (std::strcmp(e, "128w8") == 0) return 6;
+  if (std::strcmp(e, "bk32") == 0) return 7;
+  if (std::strcmp(e, "bk32n3") == 0) return 8;
   return 0;
 }
 
@@ -721,6 +746,28 @@ static bool conv64_nb2() {
   return e ? e[0] == '1' : true;
 }
 
+// 32-deep K-tiles on a 3-deep ring of 16 KB stages (APEX_AMD_CONV_BK32 = auto | 0 | 1, read
+// per launch): 48 KB in flight per workgroup instead of one 32 KB tile and up to 3
+// workgroups per CU - the 128 x 128 convs are latency-bound on their 2-deep ring.  Same-box
+// microbench (tools/conv_variants.py, profiles/r4/f/variants*.md): it wins where the
+// grid is large (128@28 3x3 94.8 -> 86.3 us, 1x1 256->1024@14 58.9 -> 44.2 us) and loses
+// where a grid of <= 784 workgroups leaves each CU one or two long K loops (3x3 256@14
+// 82 -> 96 us: twice the barriers per K), so "auto" takes it from 1024 workgroups up.
+static bool conv_bk32(unsigned wgs) {
+  const char* e = std::getenv("APEX_AMD_CONV_BK32");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return wgs >= 1024;
+}
+// the 64-wide-tile form (APEX_AMD_CONV_BK32_64 = 0 | 1, default on): layer-1 3x3 64@56
+// 111.1 -> 105.6 us fwd, 102.7 -> 99.4 us dgrad; ResNet-50 same box, two runs each:
+// 10,357 / 10,359 img/s (no BK = 32), 10,490 / 10,563 (128-wide tiles only), 10,564 /
+// 10,596 (both; profiles/r4/f/)
+static bool conv_bk32_64() {
+  const char* e = std::getenv("APEX_AMD_CONV_BK32_64");
+  return e ? e[0] == '1' : true;
+}
+
 // APEX_AMD_CONV_BURST=1 (read per launch, A/B runs): the 4-wave kernels' pre-round-4 K
 // loop - each tile's DMA pieces as one burst after the barrier, fragments read per k-step
 static int conv_burst() {
@@ -737,7 +784,14 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   g.burst = conv_burst();
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
-  if (big >= 4) {
+  if (big == 7 || big == 8) {
+    // 32-deep K-tiles: a 4- (or 3-) deep ring of 16 KB stages, two workgroups per CU
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
+    if (big == 7)
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 4, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    else
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  } else if (big >= 4) {
     const int bm = conv_bm_of(big);
     const dim3 grid((g.M + bm - 1) / bm, g.NC / 128, nclasses);
     if (big == 4)
@@ -760,7 +814,14 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    if (conv_bk32(grid.x * grid.y * grid.z))
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    else
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  } else if (conv_bk32_64() && !(EPI == 1 && !bnbwd_nb2())) {
+    // 64-wide tiles with 32-deep K-tiles on a 3-deep ring (36 KB of LDS)
+    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if ((EPI == 1 && bnbwd_nb2()) || (EPI == 0 && conv64_nb2())) {
     // BN-backward epilogue on 64-wide tiles: a 2-deep ring (48 KB of LDS -> 3 workgroups
     // per CU instead of 2), so more K loops run under each workgroup's epilogue reads

@@ -42,9 +42,14 @@ def _select(v):
     """variant name -> env: 'default', an APEX_AMD_CONV_BM value, 'burst' / 'ileave' (the
     4-wave K loop with each tile's DMA as one burst / with read-ahead and DMA pieces
     between the MFMA rows, APEX_AMD_CONV_BURST=1 / 0)"""
-    os.environ.pop("APEX_AMD_CONV_BM", None)
-    os.environ.pop("APEX_AMD_CONV_BURST", None)
-    if v in ("burst", "ileave"):
+    for k in ("APEX_AMD_CONV_BM", "APEX_AMD_CONV_BURST", "APEX_AMD_CONV_BK32",
+              "APEX_AMD_CONV_BK32_64"):
+        os.environ.pop(k, None)
+    if v in ("bk32on", "bk32off"):  # the auto BK = 32 choice forced on / off
+        os.environ["APEX_AMD_CONV_BK32"] = "1" if v == "bk32on" else "0"
+    elif v == "bk32w64":  # the 64-wide-tile BK = 32 form
+        os.environ["APEX_AMD_CONV_BK32_64"] = "1"
+    elif v in ("burst", "ileave"):
         os.environ["APEX_AMD_CONV_BURST"] = "1" if v == "burst" else "0"
     elif v != "default":
         os.environ["APEX_AMD_CONV_BM"] = v
@@ -63,8 +68,8 @@ def main():
     dev = "cuda"
     N = 256
     cases = []
-    for (c, hw, s) in [(128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2), (256, 28, 2),
-                       (512, 14, 2)]:
+    for (c, hw, s) in [(64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2),
+                       (256, 28, 2), (512, 14, 2)]:
         g = torch.Generator(device=dev).manual_seed(c + hw)
         x = cl(torch.randn(N, c, hw, hw, device=dev, generator=g).to(torch.bfloat16))
         w = cl((torch.randn(c, c, 3, 3, device=dev, generator=g) * 0.03).to(torch.bfloat16))
@@ -78,7 +83,7 @@ def main():
             wr = _rot_weight(w)
             cases.append(("3x3 dgrad %d@%d" % (c, hw), gf,
                           lambda dy=dy, wr=wr: cv.conv_fwd(dy, wr, 1)))
-    for (ci, co, hw) in [(256, 128, 56), (512, 128, 28), (512, 256, 28), (1024, 256, 14),
+    for (ci, co, hw) in [(256, 64, 56), (64, 256, 56), (256, 128, 56), (512, 128, 28), (512, 256, 28), (1024, 256, 14),
                          (1024, 512, 14), (512, 2048, 7), (2048, 512, 7), (128, 512, 28),
                          (256, 1024, 14)]:
         g = torch.Generator(device=dev).manual_seed(ci + co + hw)
