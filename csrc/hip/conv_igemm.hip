@@ -1513,6 +1513,7 @@ struct WgTapCfg {
 WgTapCfg wg_tap_cfg(int Cin, int Cout, int algo) {
   if (Cin % 128 == 0 && Cout % 128 == 0) {
     if (algo == 2) return {128, 128, 32, 4};
+    if (algo == 5) return {128, 128, 32, 3};
     if (algo == 3) return {128, 128, 64, 3};
     return {128, 128, 64, 2};
   }
@@ -1614,7 +1615,9 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
                      H, W, Ho, Wo, stride, T, Cin, Cout, M, kps, total_kt, gx)
     const bool s1 = stride == 1;
     if (c.BM == 128) {
-      if (c.BK == 32) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 4, false);
+      if (c.BK == 32 && c.NB == 3 && s1) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 3, true);
+      else if (c.BK == 32 && c.NB == 3) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 3, false);
+      else if (c.BK == 32) WGT_LAUNCH(128, 128, 2, 2, 1, 32, 4, false);
       else if (c.NB == 3) WGT_LAUNCH(128, 128, 2, 2, 1, 64, 3, false);
       else if (s1) WGT_LAUNCH(128, 128, 2, 2, 1, 64, 2, true);
       else WGT_LAUNCH(128, 128, 2, 2, 1, 64, 2, false);
