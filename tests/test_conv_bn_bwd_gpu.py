@@ -269,3 +269,52 @@ def test_stride2_block_compact_downsample_gradient(monkeypatch):
     for i, (a, b) in enumerate(zip(grads[False], grads[True])):
         err = float((a - b).abs().max() / (b.abs().max() + 1e-12))
         assert err < 2e-2, (i, err)
+
+
+# K-loop / tiling variants of conv_tap_k selected per launch by environment (A/B switches
+# and the auto choice): all accumulate the same products in the same k order, so every
+# variant must be bitwise equal to the default - plain forward, forward with the BN
+# statistics epilogue, and the BN-backward epilogue (with and without a residual add)
+_VARIANTS = [
+    {"APEX_AMD_CONV_BK32": "1"},                    # 32-deep ring on every 128-wide grid
+    {"APEX_AMD_CONV_BK32": "0", "APEX_AMD_CONV_BK32_64": "0"},  # the 64-deep rings only
+    {"APEX_AMD_CONV_BURST": "0"},                   # read-ahead + interleaved DMA pieces
+    {"APEX_AMD_CONV_BM": "256w8"},                  # 8-wave one-barrier pipeline
+    {"APEX_AMD_CONV_BM": "bk32"},                   # 32-deep, 4-deep ring
+]
+
+
+@pytest.mark.parametrize("variant", range(len(_VARIANTS)))
+@pytest.mark.parametrize("shape", [
+    # (N, C_in, H, W, C_out, k)
+    (2, 128, 14, 14, 128, 3),
+    (3, 64, 28, 28, 64, 3),
+    (2, 256, 7, 7, 512, 1),
+    (3, 128, 9, 11, 256, 3),    # M = 297: partial last tile
+])
+def test_conv_variants_bitwise_equal(shape, variant, monkeypatch):
+    N, Ci, H, W, Co, k = shape
+    C = _C()
+    torch.manual_seed(1)
+    x = _bf(torch.randn(N, Ci, H, W, device=dev))
+    wt = _bf(torch.randn(Co, Ci, k, k, device=dev) / (Ci * k * k) ** 0.5)
+    xb = _bf(torch.randn(N, Co, H, W, device=dev) * 1.3 + 0.2)
+    add = _bf(torch.randn(N, Co, H, W, device=dev))
+    mean = torch.randn(Co, device=dev) * 0.1
+    invstd = torch.rand(Co, device=dev) + 0.5
+    bw, bb = torch.randn(Co, device=dev), torch.randn(Co, device=dev) * 0.2
+    shift = torch.randn(Co, device=dev) * 0.1
+
+    def run():
+        y = C.conv.conv_fwd(x, wt, 1)
+        ys, slab = C.conv.conv_fwd_stats(x, wt, 1, shift)
+        g0, s0 = C.conv.conv_fwd_bnbwd(x, wt, None, xb, None, mean, invstd, bw, bb, 2)
+        g1, s1 = C.conv.conv_fwd_bnbwd(x, wt, add, xb, None, mean, invstd, bw, bb, 2)
+        return [y, ys, slab, g0, s0, g1, s1]
+
+    ref = [t.clone() for t in run()]
+    for kk, v in _VARIANTS[variant].items():
+        monkeypatch.setenv(kk, v)
+    got = run()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)

@@ -780,7 +780,7 @@ def test_xentropy_misaligned_rows_and_half_loss():
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-4)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3, 5])
 @pytest.mark.parametrize("shape", [(2, 64, 64, 9, 9), (3, 128, 128, 5, 7), (2, 64, 192, 8, 8),
                                    (1, 256, 128, 14, 14), (4, 128, 256, 7, 7),
                                    (2, 64, 64, 1, 1), (8, 64, 64, 30, 30)])
