@@ -316,5 +316,13 @@ def test_conv_variants_bitwise_equal(shape, variant, monkeypatch):
     for kk, v in _VARIANTS[variant].items():
         monkeypatch.setenv(kk, v)
     got = run()
-    for a, b in zip(ref, got):
-        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(ref, got)):
+        if i in (2, 4, 6) and (a.shape != b.shape or
+                               _VARIANTS[variant].get("APEX_AMD_CONV_BM") == "256w8"):
+            # statistics slabs hold one row pair per M tile, summed over the tile's row
+            # groups: the 8-wave 256-row tiling has half the rows and twice the row
+            # groups, so only the per-channel totals compare (fp32 summation order)
+            torch.testing.assert_close(a.double().sum(0), b.double().sum(0), rtol=1e-5,
+                                       atol=1e-3)
+            continue
+        assert torch.equal(a, b), i
