@@ -378,8 +378,11 @@ def _tag_stats(y):
 # previous block's bn3) it replaces the hipBLASLt addmm + reduce pass + dz store and wins
 # 10-260 us per layer; without one (bn1 / bn2) the extra read of the BN input in the
 # epilogue costs more than the reduce pass it saves except on small layers (7x7: M =
-# 12544), so those fuse only below APEX_AMD_CONV_BN_BWD_MAXM output pixels.
-_BNBWD_MAX_M = int(os.environ.get("APEX_AMD_CONV_BN_BWD_MAXM", "16384"))
+# 12544), so those fuse only below APEX_AMD_CONV_BN_BWD_MAXM output pixels.  Round 4
+# (32-deep K ring): 65536 takes the 14x14 layers (M = 50176) in too - ResNet-50 same box,
+# two runs each: 10,582 / 10,576 img/s at 16384, 10,595 / 10,633 with the 14x14 layers,
+# 10,613 / 10,549 with every layer (profiles/r4/i/).
+_BNBWD_MAX_M = int(os.environ.get("APEX_AMD_CONV_BN_BWD_MAXM", "65536"))
 
 
 def _bnbwd_ok(dy, weight, src, xshape, has_add=False):
