@@ -32,7 +32,7 @@ import torch.nn.functional as F
 
 from .. import _native
 from ..ops import _ddp_direct
-from ..ops.conv import _SideWgrad
+from ..ops.conv import _SideWgrad, _side_out
 
 __all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function", "cast_params_once",
            "fused_dense_gelu_dense_function", "dense_no_bias_function", "fused_dense_skip_function",
@@ -212,12 +212,30 @@ def _direct_slots(side, weight, w_dtype):
     return sl
 
 
+def _side_wgrad(side, weight, w_dtype, dy2, x2):
+    """The weight-gradient closure for ``side.run``: under a DDP-mode side stream it
+    writes the (possibly lazily zeroed) bucket view itself (ops/conv.py _side_out) - no
+    fresh gradient + copy per weight (96 copies / 1.3 ms per GPT-2 step before)."""
+    so, sa = _side_out(side, weight)
+    if so is not None and so.dtype != w_dtype:
+        so, sa = None, True
+    return lambda: _wgrad(dy2, x2, w_dtype, out=so, accumulate=sa)
+
+
+def _side_wgrad_bgrad(side, weight, w_dtype, b_dtype, dy2, x2):
+    """As _side_wgrad for a (weight, bias) pair: dW into the bucket view, db fresh."""
+    so, sa = _side_out(side, weight)
+    if so is None or so.dtype != w_dtype:
+        return lambda: _wgrad_bgrad(dy2, x2, w_dtype, b_dtype)
+    return lambda: (_wgrad(dy2, x2, w_dtype, out=so, accumulate=sa), _bias_grad(dy2, b_dtype))
+
+
 def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):
     """The weight gradient for autograd, or None after accumulating it into the DDP
     bucket view and announcing the parameter to the reducer."""
     direct = _direct_slots(side, weight, w_dtype)
     if direct is None:
-        return side.run(lambda: _wgrad(dy2, x2, w_dtype), dy2, *used)
+        return side.run(_side_wgrad(side, weight, w_dtype, dy2, x2), dy2, *used)
     tgt, acc = _ddp_direct.grad_target(weight)
     _wgrad(dy2, x2, w_dtype, out=tgt, accumulate=acc)
     _ddp_direct.mark_ready(direct)
@@ -307,9 +325,10 @@ def _dense_bwd(ctx, dy, dskip=None):
         if need_b:
             db = _bias_grad(dy2, ctx.bias_dtype)
     elif ctx.needs_input_grad[1] and need_b:
-        dw, db = side.run(lambda: _wgrad_bgrad(dy2, x2, ctx.w_dtype, ctx.bias_dtype), dy2, xc)
+        dw, db = side.run(_side_wgrad_bgrad(side, ctx.params[0], ctx.w_dtype, ctx.bias_dtype,
+                                            dy2, x2), dy2, xc)
     elif ctx.needs_input_grad[1]:
-        dw = side.run(lambda: _wgrad(dy2, x2, ctx.w_dtype), dy2, xc)
+        dw = side.run(_side_wgrad(side, ctx.params[0], ctx.w_dtype, dy2, x2), dy2, xc)
     elif need_b:
         db = _bias_grad(dy2, ctx.bias_dtype)
     return dx, dw, db
@@ -463,9 +482,10 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
         if need_b2:
             db2 = _bias_grad(dy2, ctx.b2_dtype)
     elif need[3] and need_b2:
-        dw2, db2 = side2.run(lambda: _wgrad_bgrad(dy2, h, ctx.w_dtypes[1], ctx.b2_dtype), dy2, h)
+        dw2, db2 = side2.run(_side_wgrad_bgrad(side2, w2, ctx.w_dtypes[1], ctx.b2_dtype, dy2, h),
+                             dy2, h)
     elif need[3]:
-        dw2 = side2.run(lambda: _wgrad(dy2, h, ctx.w_dtypes[1]), dy2, h)
+        dw2 = side2.run(_side_wgrad(side2, w2, ctx.w_dtypes[1], dy2, h), dy2, h)
     elif need_b2:
         db2 = _bias_grad(dy2, ctx.b2_dtype)
     res = None
