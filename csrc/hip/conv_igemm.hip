@@ -128,6 +128,7 @@ __device__ __forceinline__ void conv_tap(int z, int t, int& dh, int& dw, int& wt
 struct ConvGeom {
   int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
   int burst;  // 1: the 4-wave ring issues each tile's DMA as one burst (A/B reference)
+  int lpt;    // stride-2 dgrad parity classes heaviest first (APEX_AMD_DGRAD_LPT, default 1)
 };
 
 // BN-backward epilogue (conv_tap_k EPI == 1, ConvBnEpi).  Each thread owns one 8-channel
@@ -314,7 +315,12 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   const int wm = wid / WN, wn = wid % WN;
   const int mt = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = mt * BM, n0 = blockIdx.y * BN;
-  const int z = blockIdx.z;
+  // parity classes of a stride-2 3x3 dgrad in longest-first order: blockIdx.z is
+  // dispatched slowest, so the 4-tap class (z = 3) goes out first and the 1-tap class
+  // fills the tail (ResNet-50 shapes 118 -> 107, 103 -> 90, 93 -> 82 us,
+  // tools/dgrad_s2_bench.py; the 1x1 form's only real class, z = 0, is already first)
+  const int z = MODE == kDgrad3 && g.lpt ? (int)gridDim.z - 1 - (int)blockIdx.z
+                                         : (int)blockIdx.z;
   const int ntaps = conv_ntaps<MODE>(z);
   const int KC = g.KC, M = g.M, GHW = g.GH * g.GW;
 
@@ -782,6 +788,10 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   if (g0.M == 0) return;
   ConvGeom g = g0;
   g.burst = conv_burst();
+  {
+    const char* e = std::getenv("APEX_AMD_DGRAD_LPT");
+    g.lpt = e ? (e[0] == '1') : 1;
+  }
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
   if (big == 7 || big == 8) {
