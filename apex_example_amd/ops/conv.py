@@ -91,6 +91,15 @@ _LAG = int(os.environ.get("APEX_AMD_WGRAD_LAG", "-1"))
 # priority of the side stream: "auto" = high under DDP, normal for the single-GPU 'free'
 # mode (same box: 10,565 / 10,534 img/s normal vs 10,531 / 10,500 high there)
 _SIDE_PRIO = os.environ.get("APEX_AMD_WGRAD_STREAM_PRIO", "auto")
+# CU partitioning for the side stream (APEX_AMD_WGRAD_STREAM_CUS = 1 | 2 | 3 quarters of the
+# CUs, 0 = all): the weight-gradient GEMMs then run on that share of every XCD instead of
+# competing with the data-gradient chain for every CU (csrc/torch/module.cpp
+# cu_masked_stream; a CU-masked stream has the default priority).  Measured far slower, so
+# off: same box, two runs each, GPT-2-medium 247.3 / 247.8 k tok/s with the plain side
+# stream vs 129 k (1/4 of the CUs), 154 k (1/2), 154 k (3/4); ResNet-50 10,566 / 10,511
+# vs 7,181 / 7,165 img/s (1/2 and 3/4) - the masked queue costs far more than the CU
+# contention it removes (profiles/r4/m/).
+_SIDE_CUS = int(os.environ.get("APEX_AMD_WGRAD_STREAM_CUS", "0"))
 _SIDE_EVENTS = {}   # device index -> deque of side-stream events, oldest first
 
 
@@ -134,8 +143,13 @@ class _SideWgrad:
             key = (dev.index, high)
             self.side = _SIDE.get(key)
             if self.side is None:
-                prio = torch.cuda.Stream.priority_range()[1] if high else 0
-                self.side = _SIDE[key] = torch.cuda.Stream(dev, priority=prio)
+                if 0 < _SIDE_CUS < 4:
+                    h = _native.require().cu_masked_stream(dev.index, _SIDE_CUS)
+                    self.side = torch.cuda.ExternalStream(h, device=dev)
+                else:
+                    prio = torch.cuda.Stream.priority_range()[1] if high else 0
+                    self.side = torch.cuda.Stream(dev, priority=prio)
+                _SIDE[key] = self.side
             self.ev = self.main.record_event()
 
     def run(self, fn, *used):
