@@ -62,6 +62,27 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// Tile DMA addressing: a wave-uniform tile base (SGPRs, one scalar multiply-add per
+// tile) plus a loop-invariant per-lane 32-bit byte offset (row * row stride + swizzled
+// chunk), which selects the saddr form of global_load_lds.  Computing the 64-bit
+// address per tile and lane instead (clamped row * stride) cost 8 v_mul_lo_u32 + 4
+// v_mad_u64_u32 per forward tile - quarter-rate VALU, ~1/5 of the no-dropout forward's
+// VALU cycles.  Only a tile that reaches past S takes the clamped per-lane path.  The
+// binding keeps row strides below 2^24 elements so the offsets fit 32 bits.
+__device__ __forceinline__ void glds16o(const void* tile_base, uint32_t off, unsigned char* l) {
+  glds16(static_cast<const char*>(tile_base) + off, l);
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t row_off(int row, int64_t stride, int chunk) {
+  return (uint32_t)row * (uint32_t)stride * (uint32_t)sizeof(T) + (uint32_t)chunk * 16u;
+}
+
+template <typename T>
+__device__ __forceinline__ const T* tile_base(const T* p, int row0, int64_t stride) {
+  return p + (int64_t)row0 * stride;
+}
+
 // LDS images of a [64 rows][64 d] 16-bit tile (128-B rows)
 __device__ __forceinline__ int swz_rows(int row, int chunk) {   // for ds_read_b128 row reads
   return row * kARow + ((chunk ^ ((row >> 1) & 7)) << 4);
@@ -189,7 +210,13 @@ struct AttnArgs {
   float inv_keep;    // 1 / (1 - p)
   uint32_t seed;
   int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
+  int addr64;  // APEX_AMD_ATTN_ADDR64=1: per-lane 64-bit tile DMA addresses (A/B only)
 };
+
+int attn_addr64_flag() {
+  const char* e = std::getenv("APEX_AMD_ATTN_ADDR64");
+  return (e && e[0] == '1') ? 1 : 0;
+}
 
 int attn_base_flag() {
   const char* e = std::getenv("APEX_AMD_ATTN_BASE");
@@ -231,6 +258,14 @@ __device__ __forceinline__ void tile_of_block(bool causal, bool heavy_high, int 
   tile = (causal && heavy_high) ? nt - 1 - t : t;
 }
 
+// the other 32-lane half's value of x (lane ^ 32) on the VALU (v_permlane32_swap)
+// instead of an LDS round trip (ds_bpermute)
+__device__ __forceinline__ float max_halves(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
 template <typename T, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   typedef typename Frag<T>::v8 v8;
@@ -267,9 +302,26 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   }
   // DMA: each wave fills 16 rows of K and of V per tile (2 x 1 KiB instructions each)
   const int lrow = lane >> 3, pch = lane & 7;
+  uint32_t kof[2], vof[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wid * 2 + i) * 8 + lrow;
+    kof[i] = row_off<T>(row, a.kss, (swz_rows(row, pch) - row * kARow) >> 4);  // logical chunk at pch
+    vof[i] = row_off<T>(row, a.vss, (swz_tr(row, pch) - row * kARow) >> 4);
+  }
   auto issue = [&](int kt, int buf) {
     unsigned char* Kl = lds + buf * 2 * kAKT * kARow;
     unsigned char* Vl = Kl + kAKT * kARow;
+    if ((kt + 1) * kAKT <= a.S && !a.addr64) {
+      const T* kb = tile_base(K, kt * kAKT, a.kss);
+      const T* vb = tile_base(V, kt * kAKT, a.vss);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        glds16o(kb, kof[i], Kl + (wid * 2 + i) * 1024);
+        glds16o(vb, vof[i], Vl + (wid * 2 + i) * 1024);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = (wid * 2 + i) * 8 + lrow;
@@ -306,15 +358,14 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
         vhi[dt][t][s] = tr_addr(r0 + 8, c0, lane);
       }
 
-  issue(0, 0);
-  for (int kt = 0; kt < nkt; ++kt) {
+  auto step = [&](int kt, int buf) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 1 < nkt) issue(kt + 1, (kt + 1) & 1);
-    const unsigned char* Kl = lds + (kt & 1) * 2 * kAKT * kARow;
+    if (kt + 1 < nkt) issue(kt + 1, buf ^ 1);
+    const unsigned char* Kl = lds + buf * 2 * kAKT * kARow;
     const unsigned char* Vl = Kl + kAKT * kARow;
     const int k0 = kt * kAKT;
-    if (CAUSAL && k0 > qb0 + wid * 32 + 31) continue;  // whole tile masked for this wave
+    if (CAUSAL && k0 > qb0 + wid * 32 + 31) return;  // whole tile masked for this wave
 
     f32x16_t x[2];
 #pragma unroll
@@ -342,7 +393,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, x[t][r]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    tmax = max_halves(tmax);
     const float mnew = fmaxf(m, tmax * a.scale_log2);
     // the O / l rescale by exp2(m - mnew) is skipped while no query of the wave
     // raised its running max (alpha == 1 exactly: same math, 32 fewer multiplies
@@ -389,7 +440,9 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
         for (int dt = 0; dt < 2; ++dt)
           o[dt] = mfma32<T>(lds_tr8<T>(Vl, vlo[dt][t][s], vhi[dt][t][s]), pf, o[dt]);
       }
-  }
+  };
+  issue(0, 0);
+  for (int kt = 0; kt < nkt; ++kt) step(kt, kt & 1);
 
   const float lt = l + __shfl_xor(l, 32);
   const float inv = lt > 0.f ? (DROP ? a.inv_keep : 1.f) / lt : 0.f;
@@ -397,14 +450,6 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
     store_dT<T>(static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD, o, hl, inv);
     if (hl == 0) a.lse[(int64_t)bh * a.lse_stride + q] = m + log2f(lt);
   }
-}
-
-// the other 32-lane half's value of x (lane ^ 32) on the VALU (v_permlane32_swap)
-// instead of an LDS round trip (ds_bpermute)
-__device__ __forceinline__ float max_halves(float x) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
 }
 
 // Forward, software-pipelined (APEX_AMD_ATTN_FWD=2 selects it; A/B against attn_fwd_k):
@@ -451,9 +496,26 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
   nfull = nfull < nkt ? nfull : nkt;
 
   const int lrow = lane >> 3, pch = lane & 7;
+  uint32_t kof[2], vof[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wid * 2 + i) * 8 + lrow;
+    kof[i] = row_off<T>(row, a.kss, (swz_rows(row, pch) - row * kARow) >> 4);
+    vof[i] = row_off<T>(row, a.vss, (swz_tr(row, pch) - row * kARow) >> 4);
+  }
   auto issue = [&](int kt) {  // 4 LDS-DMA instructions per lane
     unsigned char* Kl = lds + (kt % 3) * TB;
     unsigned char* Vl = Kl + kAKT * kARow;
+    if ((kt + 1) * kAKT <= a.S && !a.addr64) {
+      const T* kb = tile_base(K, kt * kAKT, a.kss);
+      const T* vb = tile_base(V, kt * kAKT, a.vss);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        glds16o(kb, kof[i], Kl + (wid * 2 + i) * 1024);
+        glds16o(vb, vof[i], Vl + (wid * 2 + i) * 1024);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = (wid * 2 + i) * 8 + lrow;
@@ -637,6 +699,7 @@ struct AttnBwdArgs {
   float inv_keep;
   uint32_t seed;
   int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
+  int addr64;  // APEX_AMD_ATTN_ADDR64=1: per-lane 64-bit tile DMA addresses (A/B only)
 };
 
 // dK / dV: a workgroup owns 128 keys (32 per wave, one per lane column), loops
@@ -690,6 +753,13 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
   const int lrow = lane >> 3, pch = lane & 7;
   auto issue = [&](int qt, int buf) {
     unsigned char* base = lds + buf * BUF;
+    if (wid == 0) {  // lanes 0-15: lse[q0 .. q0+63], 16-31: D[...], 32-63: pad (lse again)
+      const int seg = (lane >> 4) & 1, part = lane & 15;
+      const float* src = (seg ? Dr : lse) + qt * kAKT + part * 4;
+      glds16(src, base + 4 * IMG);
+    }
+    // (per-lane 64-bit addresses: the 32-bit offset form needs 8 more VGPRs here and
+    // spilled at this kernel's ~250)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = (wid * 2 + i) * 8 + lrow;
@@ -704,11 +774,6 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
       glds16(qrow + cht * 8, dst + IMG);
       glds16(drow + chr * 8, dst + 2 * IMG);
       glds16(drow + cht * 8, dst + 3 * IMG);
-    }
-    if (wid == 0) {  // lanes 0-15: lse[q0 .. q0+63], 16-31: D[...], 32-63: pad (lse again)
-      const int seg = (lane >> 4) & 1, part = lane & 15;
-      const float* src = (seg ? Dr : lse) + qt * kAKT + part * 4;
-      glds16(src, base + 4 * IMG);
     }
   };
 
@@ -909,9 +974,30 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
     nkt = last < nkt ? last : nkt;
   }
   const int lrow = lane >> 3, pch = lane & 7;
+  uint32_t kro[2], kto[2], vro[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wid * 2 + i) * 8 + lrow;
+    const int chr = (swz_rows(row, pch) - row * kARow) >> 4;
+    kro[i] = row_off<T>(row, a.kss, chr);
+    kto[i] = row_off<T>(row, a.kss, (swz_tr(row, pch) - row * kARow) >> 4);
+    vro[i] = row_off<T>(row, a.vss, chr);
+  }
   // images per buffer: 0 = K rows, 1 = K transposed, 2 = V rows
   auto issue = [&](int kt, int buf) {
     unsigned char* base = lds + buf * 3 * IMG;
+    if ((kt + 1) * kAKT <= a.S && !a.addr64) {
+      const T* kb = tile_base(K, kt * kAKT, a.kss);
+      const T* vb = tile_base(V, kt * kAKT, a.vss);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        unsigned char* dst = base + (wid * 2 + i) * 1024;
+        glds16o(kb, kro[i], dst);
+        glds16o(kb, kto[i], dst + IMG);
+        glds16o(vb, vro[i], dst + 2 * IMG);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = (wid * 2 + i) * 8 + lrow;
@@ -1041,9 +1127,18 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
   a.seed = L.seed;
   a.base = attn_base_flag();
+  a.addr64 = attn_addr64_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr16 != 0;
   const bool v2 = !a.base && attn_fwd_variant() == 2;
+#define FWD1(T)                                                                                \
+  if (L.causal) {                                                                              \
+    if (drop) hipLaunchKernelGGL((attn_fwd_k<T, true, true>), grid, block, 0, st, a);          \
+    else hipLaunchKernelGGL((attn_fwd_k<T, true, false>), grid, block, 0, st, a);              \
+  } else {                                                                                     \
+    if (drop) hipLaunchKernelGGL((attn_fwd_k<T, false, true>), grid, block, 0, st, a);         \
+    else hipLaunchKernelGGL((attn_fwd_k<T, false, false>), grid, block, 0, st, a);             \
+  }
 #define ATTN_FWD_LAUNCH(T)                                                                     \
   if (v2) {                                                                                    \
     if (L.causal) {                                                                            \
@@ -1053,12 +1148,8 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
       if (drop) hipLaunchKernelGGL((attn_fwd2_k<T, false, true>), grid, block, 0, st, a);      \
       else hipLaunchKernelGGL((attn_fwd2_k<T, false, false>), grid, block, 0, st, a);          \
     }                                                                                          \
-  } else if (L.causal) {                                                                       \
-    if (drop) hipLaunchKernelGGL((attn_fwd_k<T, true, true>), grid, block, 0, st, a);          \
-    else hipLaunchKernelGGL((attn_fwd_k<T, true, false>), grid, block, 0, st, a);              \
   } else {                                                                                     \
-    if (drop) hipLaunchKernelGGL((attn_fwd_k<T, false, true>), grid, block, 0, st, a);         \
-    else hipLaunchKernelGGL((attn_fwd_k<T, false, false>), grid, block, 0, st, a);             \
+    FWD1(T)                                                                                    \
   }
   if (L.dtype == DType::BF16) {
     ATTN_FWD_LAUNCH(bf16_t)
@@ -1066,6 +1157,7 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
     ATTN_FWD_LAUNCH(half_t)
   }
 #undef ATTN_FWD_LAUNCH
+#undef FWD1
 }
 
 void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
@@ -1088,6 +1180,7 @@ void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
   a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
   a.seed = L.seed;
   a.base = attn_base_flag();
+  a.addr64 = attn_addr64_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr16 != 0;
   const bool dq_il = attn_dq_interleave();

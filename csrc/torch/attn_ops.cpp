@@ -13,6 +13,9 @@ void check_view(const at::Tensor& t, const char* what) {
   TORCH_CHECK(((uintptr_t)t.data_ptr() % 16) == 0 && t.stride(0) % 8 == 0 &&
                   t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
               "attn: ", what, ": 16-byte aligned rows required");
+  // the kernels' tile DMA uses 32-bit per-lane row offsets (csrc/hip/attention.hip)
+  TORCH_CHECK(t.stride(1) >= 0 && t.stride(1) < (int64_t{1} << 24), "attn: ", what,
+              ": sequence stride must be below 2^24 elements");
 }
 
 bool view_ok(const at::Tensor& t) {

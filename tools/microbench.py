@@ -12,6 +12,7 @@ from __future__ import annotations
 import argparse
 import os
 import sys
+import time
 
 import torch
 import torch.nn.functional as F
@@ -682,10 +683,23 @@ def bench_attn(args):
         # read per launch, so every variant runs in this process
         variants = [("gfx950/base", {"APEX_AMD_ATTN_BASE": "1"}), ("gfx950", {}),
                     ("gfx950/fwd2", {"APEX_AMD_ATTN_FWD": "2"}),
-                    ("gfx950/dq-il0", {"APEX_AMD_ATTN_DQ_IL": "0"})]
+                    ("gfx950/dq-il0", {"APEX_AMD_ATTN_DQ_IL": "0"}),
+                    ("gfx950/addr64", {"APEX_AMD_ATTN_ADDR64": "1"})]
         if args.quick:
             variants = variants[1:]
-        keys = ("APEX_AMD_ATTN_BASE", "APEX_AMD_ATTN_FWD", "APEX_AMD_ATTN_DQ_IL")
+        keys = ("APEX_AMD_ATTN_BASE", "APEX_AMD_ATTN_FWD", "APEX_AMD_ATTN_DQ_IL",
+                "APEX_AMD_ATTN_ADDR64")
+        # ~2 s of untimed calls first: without it the first variant timed read 10 %
+        # slower than the same kernels later in the process (clock / first-use ramp)
+        A = _native.require().attn
+        o, lse = A.fwd(q, k, v, causal, 0.1, 1234, 1.0 / d ** 0.5)
+        dq, dk, dv = (torch.empty_like(t) for t in (q, k, v))
+        t_end = time.time() + 2.0
+        while time.time() < t_end:
+            for _ in range(10):
+                A.fwd(q, k, v, causal, 0.1, 1234, 1.0 / d ** 0.5)
+                A.bwd(do, q, k, v, o, lse, causal, 0.1, 1234, 1.0 / d ** 0.5, dq, dk, dv)
+            torch.cuda.synchronize()
         for vname, env in variants:
             for key in keys:
                 os.environ.pop(key, None)
