@@ -24,6 +24,16 @@ under 20 % of t (link-rate), and the LAST bucket's t is exposed after backward,
 so buckets much above ~64 MB lengthen the tail.  32 MiB sits in that window for
 1..8 ranks; see tools/allreduce_sweep.py to refit a and B on a node.
 
+Calibration (``"auto"`` at world size > 1, env ``APEX_AMD_DDP_CALIBRATE=0`` to skip):
+at construction DDP times fp32 all-reduces of 1, 8 and 32 MiB on its own bucket
+communicator, takes the slowest rank's median per size (one MAX all-reduce, so every
+rank derives the same number), fits ``a`` and ``B`` by least squares and sizes the
+bucket from the link-rate rule - the smallest power-of-two MiB with a <= 20 % of t(S),
+clamped to [8, 64] MiB - instead of the model's assumed constants.  The fit and the
+choice are kept in ``ddp.calibration`` (bench.py writes them to its JSON), so the
+driver's multi-GPU runs record the node's own a and B.  A fit that is not physical
+(a <= 0 or B <= 0: noise) keeps the 32 MiB default.
+
 Tapered tail (``tapered_buckets``, default on; env ``APEX_AMD_DDP_TAPER=0`` for Apex's
 plain size cut): buckets are cut from the END of the gradient-arrival order with limits
 message_size/16, /8, /4, /2, then message_size - the buckets that can only launch when
@@ -67,6 +77,8 @@ from .. import _native
 
 
 XGMI_BUCKET_BYTES = 32 << 20
+_CAL_SIZES_MIB = (1, 8, 32)
+_CAL_MIN_MIB, _CAL_MAX_MIB = 8, 64
 
 
 def _group_world(pg):
@@ -255,6 +267,7 @@ class DistributedDataParallel(Module):
             self._comm_pg = self._new_comm_group()
 
         self.active_params = self._collect_params()
+        self.calibration = None
         self.message_size = self._resolve_message_size(message_size)
         if self.backend == "nccl":
             for p in self.active_params:
@@ -289,7 +302,69 @@ class DistributedDataParallel(Module):
         mode = self._fp32_mode()
         wire = 4 if (dom == torch.float32 or mode == 1
                      or (mode in (2, 3) and dom == torch.bfloat16)) else torch.finfo(dom).bits // 8
-        return max(1, XGMI_BUCKET_BYTES // wire)
+        nbytes = XGMI_BUCKET_BYTES
+        if self.world_size > 1 and os.environ.get("APEX_AMD_DDP_CALIBRATE", "1") != "0":
+            self.calibration = self._calibrate()
+            nbytes = self.calibration["bucket_mib"] << 20
+        return max(1, nbytes // wire)
+
+    def _calibrate(self, sizes_mib=_CAL_SIZES_MIB, warmup=3, reps=7):
+        """Measure t(S) of an fp32 all-reduce on the bucket communicator and size the
+        bucket from the fit (module docstring).  Collective: every rank of the group
+        runs the same calls in the same order."""
+        import time
+
+        pg = self._comm_pg if self._comm_pg is not None else dist.group.WORLD
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" \
+            else torch.device("cpu")
+        n = self.world_size
+        med = []
+        for mib in sizes_mib:
+            buf = torch.zeros((mib << 20) // 4, dtype=torch.float32, device=dev)
+            ts = []
+            for i in range(warmup + reps):
+                if dev.type == "cuda":
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
+                        enable_timing=True)
+                    e0.record()
+                    dist.all_reduce(buf, group=pg)
+                    e1.record()
+                    e1.synchronize()
+                    dt = e0.elapsed_time(e1) * 1e-3
+                else:
+                    t0 = time.perf_counter()
+                    dist.all_reduce(buf, group=pg)
+                    dt = time.perf_counter() - t0
+                if i >= warmup:
+                    ts.append(dt)
+            med.append(sorted(ts)[len(ts) // 2])
+            del buf
+        # the slowest rank's times: identical inputs to the fit on every rank
+        v = torch.tensor(med, dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=pg)
+        t = [float(x) for x in v.tolist()]
+        S = [float(m << 20) for m in sizes_mib]
+        k = len(S)
+        sm, tm = sum(S) / k, sum(t) / k
+        var = sum((x - sm) ** 2 for x in S)
+        slope = sum((x - sm) * (y - tm) for x, y in zip(S, t)) / var if var > 0 else 0.0
+        a = tm - slope * sm
+        ring = 2.0 * (n - 1) / n
+        rec = {"sizes_mib": list(sizes_mib), "t_us": [round(x * 1e6, 1) for x in t],
+               "collective": "fp32 all_reduce", "ranks": n}
+        if a <= 0 or slope <= 0:
+            rec.update({"a_us": round(a * 1e6, 2), "busbw_gbps": None,
+                        "bucket_mib": XGMI_BUCKET_BYTES >> 20, "fit": "unphysical: default kept"})
+            return rec
+        busbw = ring / slope
+        need = 4.0 * a * busbw / ring  # a <= 20 % of t(S)
+        mib = _CAL_MIN_MIB
+        while mib < _CAL_MAX_MIB and (mib << 20) < need:
+            mib *= 2
+        rec.update({"a_us": round(a * 1e6, 2), "busbw_gbps": round(busbw / 1e9, 1),
+                    "link_rate_min_mib": round(need / 2**20, 2), "bucket_mib": mib,
+                    "fit": "least squares"})
+        return rec
 
     def _fp32_mode(self):
         """Reducer fp32 mode: 0 native, 1 every 16-bit bucket as an fp32 all-reduce,

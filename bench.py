@@ -551,6 +551,7 @@ def ddp_timing(ddp, step, batch, steps, device):
         "buckets": len(numels),
         "bucket_mb": [round(n * bufs[i].element_size() / 2**20, 2) for i, n in enumerate(numels)],
         "message_size": ddp.message_size,
+        "calibration": ddp.calibration,
         "wire": ddp.wire_format(),
         "allreduce_fp32_accumulate_bf16": ddp._fp32_mode() in (2, 3),
         "high_priority_streams": ddp.high_priority_streams,

@@ -106,9 +106,11 @@ def ddp_subgroups(rank, world, streams=1, message_size=300):
 
 
 def ddp_auto_size(rank, world):
-    """message_size='auto': 32 MiB on the wire for the dtype the collective moves."""
+    """message_size='auto': 32 MiB on the wire for the dtype the collective moves
+    (the sizing rule alone: calibration off)."""
     from apex_example_amd.parallel import DistributedDataParallel
 
+    os.environ["APEX_AMD_DDP_CALIBRATE"] = "0"
     out = {}
     for name, dt, fp32 in (("bf16", torch.bfloat16, None), ("bf16_native", torch.bfloat16, False),
                            ("fp16", torch.float16, None), ("fp32", torch.float32, None)):
@@ -116,6 +118,20 @@ def ddp_auto_size(rank, world):
         ddp = DistributedDataParallel(m, message_size="auto", allreduce_always_fp32=fp32)
         out[name] = ddp.message_size
     return out
+
+
+def ddp_calibrate(rank, world):
+    """message_size='auto' at world > 1: the bucket size comes from a measured
+    all-reduce fit, identical on every rank."""
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    os.environ.pop("APEX_AMD_DDP_CALIBRATE", None)
+    m = nn.Linear(64, 64)
+    ddp = DistributedDataParallel(m, message_size="auto")
+    x = torch.randn(4, 64)
+    ddp(x).sum().backward()  # the reducer still works after the calibration collectives
+    return {"cal": ddp.calibration, "message_size": ddp.message_size,
+            "grad": m.weight.grad.clone()}
 
 
 def ddp_retain_buffers(rank, world):

@@ -62,6 +62,19 @@ def test_ddp_auto_message_size(tmp_path):
                    "fp32": mib32 // 4}
 
 
+def test_ddp_auto_message_size_calibrated(tmp_path):
+    """world 2: 'auto' fits a + 2(n-1)/n S / B to timed all-reduces and every rank
+    picks the same power-of-two bucket in [8, 64] MiB."""
+    res = W.run("ddp_calibrate", 2, str(tmp_path))
+    c0, c1 = res[0]["cal"], res[1]["cal"]
+    assert c0 == c1
+    assert c0["sizes_mib"] == [1, 8, 32] and len(c0["t_us"]) == 3 and c0["ranks"] == 2
+    mib = c0["bucket_mib"]
+    assert mib in (8, 16, 32, 64)
+    assert res[0]["message_size"] == res[1]["message_size"] == (mib << 20) // 4
+    torch.testing.assert_close(res[0]["grad"], res[1]["grad"])
+
+
 def test_ddp_retain_allreduce_buffers(tmp_path):
     """The all-reduced buffers are retained and the grads are views into them."""
     for r in W.run("ddp_retain_buffers", 2, str(tmp_path)):
