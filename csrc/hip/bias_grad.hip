@@ -14,6 +14,8 @@
 // or dpre = dh * act'(y) from the layer's saved OUTPUT y (ReLU: y > 0; sigmoid:
 // y (1 - y); apex.mlp) - write it and its column partials, so the bias gradient
 // costs no extra read of dpre.
+#include <cstdlib>
+
 #include "amd_dev.h"
 #include "amd_kernels.h"
 
@@ -135,6 +137,55 @@ __global__ void __launch_bounds__(256)
   if (sl == 0 && c < N) out[c] = from_f32<TO>((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]));
 }
 
+// stage 2, narrow: 16 columns x 16 split lanes per block, each lane summing S/16
+// partials with 4 loads in flight - 4x the blocks of colsum_final_k and a quarter of
+// its dependent load rounds (the wide form ran 6-11 us per call in the BERT / GPT-2
+// steps for ~0.5 MB of partials: 16 blocks of latency chains).  Same summation
+// order across the partials of one split lane, so deterministic
+template <typename TO>
+__global__ void __launch_bounds__(256)
+    colsum_final16_k(const float* __restrict__ part, int S, int N, TO* __restrict__ out) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    int s = sl;
+    for (; s + 48 < S; s += 64) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t[i] += part[(int64_t)(s + 16 * i) * N + c];
+    }
+    for (; s < S; s += 16) t[0] += part[(int64_t)s * N + c];
+  }
+  red[sl][cl] = (t[0] + t[1]) + (t[2] + t[3]);
+  __syncthreads();
+  if (sl == 0 && c < N) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a += red[q][cl];
+    out[c] = from_f32<TO>(a);
+  }
+}
+
+// APEX_AMD_COLSUM_FINAL=64: the wide stage 2 (A/B)
+bool colsum_final_wide() {
+  static const bool wide = [] {
+    const char* e = std::getenv("APEX_AMD_COLSUM_FINAL");
+    return e && e[0] == '6';
+  }();
+  return wide;
+}
+
+template <typename TO>
+void launch_final(const float* part, int S, int N, TO* out, hipStream_t st) {
+  if (colsum_final_wide())
+    hipLaunchKernelGGL(colsum_final_k<TO>, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, part,
+                       S, N, out);
+  else
+    hipLaunchKernelGGL(colsum_final16_k<TO>, dim3((unsigned)((N + 15) / 16)), dim3(256), 0, st,
+                       part, S, N, out);
+}
+
 __device__ __forceinline__ float gelu_f(float x, bool tanh_approx) {
   if (tanh_approx) {
     const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -183,16 +234,9 @@ void gelu_fwd(const void* x, void* y, DType t, int64_t n, bool tanh_approx, hipS
 }
 
 void colsum_finalize(const float* part, int S, int N, void* out, DType tb, hipStream_t st) {
-  const dim3 g2((unsigned)((N + 63) / 64));
-  if (tb == DType::F32)
-    hipLaunchKernelGGL(colsum_final_k<float>, g2, dim3(256), 0, st, part, S, N,
-                       static_cast<float*>(out));
-  else if (tb == DType::BF16)
-    hipLaunchKernelGGL(colsum_final_k<bf16_t>, g2, dim3(256), 0, st, part, S, N,
-                       static_cast<bf16_t*>(out));
-  else
-    hipLaunchKernelGGL(colsum_final_k<half_t>, g2, dim3(256), 0, st, part, S, N,
-                       static_cast<half_t*>(out));
+  if (tb == DType::F32) launch_final(part, S, N, static_cast<float*>(out), st);
+  else if (tb == DType::BF16) launch_final(part, S, N, static_cast<bf16_t*>(out), st);
+  else launch_final(part, S, N, static_cast<half_t*>(out), st);
 }
 
 int colsum_splits(int64_t M, int N) {
@@ -235,16 +279,7 @@ void colsum(const void* x, const void* pre, void* out_dpre, DType t, int64_t M, 
   if (t == DType::BF16) launch1(bf16_t{});
   else if (t == DType::F16) launch1(half_t{});
   else launch1(float{});
-  const dim3 g2((unsigned)((N + 63) / 64));
-  if (tb == DType::F32)
-    hipLaunchKernelGGL(colsum_final_k<float>, g2, dim3(256), 0, st, part, S, N,
-                       static_cast<float*>(bias_grad));
-  else if (tb == DType::BF16)
-    hipLaunchKernelGGL(colsum_final_k<bf16_t>, g2, dim3(256), 0, st, part, S, N,
-                       static_cast<bf16_t*>(bias_grad));
-  else
-    hipLaunchKernelGGL(colsum_final_k<half_t>, g2, dim3(256), 0, st, part, S, N,
-                       static_cast<half_t*>(bias_grad));
+  colsum_finalize(part, S, N, bias_grad, tb, st);
 }
 
 }  // namespace amd
