@@ -245,6 +245,78 @@ __global__ void __launch_bounds__(kPoolThreads)
   }
 }
 
+// Backward, one thread per 2x2 input block (rows 2i, 2i+1 x cols 2j, 2j+1) x 8
+// channels: the block is covered by outputs (i..i+1) x (j..j+1), so the 4 dy / 4 index
+// loads of a thread serve 4 input pixels instead of 1 (the per-input form below issues
+// 4x the loads for the same bytes).  Per input the contributions are summed in the
+// per-input kernel's order ((oh, ow) row-major), so the two are bitwise equal.
+template <typename T>
+__global__ void __launch_bounds__(kPoolThreads)
+    maxpool3s2_bwd2_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                      T* __restrict__ dx, int N, int H, int W, int C, int OH, int OW) {
+  static_assert(sizeof(T) == 2, "16-bit activations");
+  const int CV = C / 8, BH = (H + 1) / 2, BW = (W + 1) / 2;
+  const int64_t total = (int64_t)N * BH * BW * CV;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    int64_t pix = t / CV;
+    const int j = (int)(pix % BW);
+    pix /= BW;
+    const int i = (int)(pix % BH);
+    const int n = (int)(pix / BH);
+    // outputs (i + a, j + b), a, b in {0, 1}
+    float g[4][8];
+    uint32_t wd[4][2];
+    bool ok[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int q = a * 2 + b;
+        ok[q] = i + a < OH && j + b < OW;
+        const int64_t o = (((int64_t)n * OH + (ok[q] ? i + a : i)) * OW + (ok[q] ? j + b : j)) * C +
+                          cv * 8;
+        unpack8_any<T>(*reinterpret_cast<const p_u32x4*>(dy + o), g[q]);
+        const uint2 w2 = *reinterpret_cast<const uint2*>(idx + o);
+        wd[q][0] = w2.x;
+        wd[q][1] = w2.y;
+      }
+    auto tap_of = [&](int q, int c) { return (int)((wd[q][c >> 2] >> (8 * (c & 3))) & 0xff); };
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const int h = 2 * i + dh;
+      if (h >= H) continue;
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int w = 2 * j + dw;
+        if (w >= W) continue;
+        float acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+        // contributing outputs in (oh, ow) row-major order: even offset -> only a/b = 0
+        // (tap 1); odd -> a/b = 0 (tap 2) then 1 (tap 0)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if (a == 1 && dh == 0) continue;
+          const int kh = dh == 0 ? 1 : (a == 0 ? 2 : 0);
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b == 1 && dw == 0) continue;
+            const int kw = dw == 0 ? 1 : (b == 0 ? 2 : 0);
+            const int q = a * 2 + b;
+            if (!ok[q]) continue;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+              if (tap_of(q, c) == kh * 3 + kw) acc[c] += g[q][c];
+          }
+        }
+        store8(dx + (((int64_t)n * H + h) * W + w) * C + cv * 8, acc);
+      }
+    }
+  }
+}
+
 // input row h is covered by output rows oh = h/2 (h even: tap row 1) or
 // oh = (h-1)/2 (tap row 2) and (h+1)/2 (tap row 0) for odd h
 template <typename T>
@@ -414,9 +486,17 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
     using T = decltype(t0);
     if constexpr (sizeof(T) == 2) {
       if (vec && stem_ok(k, s, p, H, W, OH, OW)) {
-        hipLaunchKernelGGL((maxpool3s2_bwd_k<T>), dim3(pool_grid(items)), dim3(kPoolThreads), 0,
-                           st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C, OH,
-                           OW);
+        const char* e = std::getenv("APEX_AMD_POOL_BWD1");  // per launch: A/B tests
+        if (e && e[0] == '1') {
+          hipLaunchKernelGGL((maxpool3s2_bwd_k<T>), dim3(pool_grid(items)), dim3(kPoolThreads),
+                             0, st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W,
+                             C, OH, OW);
+        } else {
+          const int64_t blk = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+          hipLaunchKernelGGL((maxpool3s2_bwd2_k<T>), dim3(pool_grid(blk)), dim3(kPoolThreads),
+                             0, st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W,
+                             C, OH, OW);
+        }
         return;
       }
     }

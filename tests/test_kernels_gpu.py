@@ -671,6 +671,28 @@ def test_maxpool_nhwc(shape, k, s, p, dt):
                                atol=1e-2 if dt != torch.float32 else 1e-6)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 24, 9, 11), (1, 8, 10, 7)])
+def test_maxpool3s2_backward_variants_bitwise(shape, monkeypatch):
+    """The 2x2-block stem max-pool backward (default) vs the per-input kernel
+    (APEX_AMD_POOL_BWD1=1, read per launch): same contributions in the same order."""
+    from apex_example_amd.ops.pool import MaxPool2dNHWC
+
+    torch.manual_seed(1)
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x[:, :, ::3, ::2] = 0.5  # ties across overlapping windows
+    dy = None
+    grads = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("APEX_AMD_POOL_BWD1", flag)
+        xa = x.clone().requires_grad_(True)
+        y = MaxPool2dNHWC(3, 2, 1)(xa)
+        if dy is None:
+            dy = torch.randn_like(y)
+        y.backward(dy)
+        grads.append(xa.grad)
+    assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("shape", [(3, 2048, 7, 7), (2, 12, 5, 3)])
 def test_global_avg_pool_nhwc(shape, dt):
