@@ -22,6 +22,7 @@ namespace amd {
 namespace {
 
 constexpr int kPoolThreads = 256;
+constexpr int kPoolBNMaxC = 512;  // BN-fused stem max-pool: channels held in LDS
 
 struct PoolBN {
   const float *mean, *invstd, *w, *b;  // fp32 [C]; w / b optional
@@ -176,6 +177,19 @@ __global__ void __launch_bounds__(kPoolThreads)
                      int H, int W, int C, int OH, int OW, PoolBN bn) {
   static_assert(sizeof(T) == 2, "16-bit activations");
   const int CV = C / 8;
+  // BN scale / shift of every channel, once per workgroup into LDS (C <= kPoolBNMaxC,
+  // checked on the host): per thread they were 32+ scalar global loads next to the 9
+  // 16-byte data loads
+  __shared__ __attribute__((aligned(16))) float s_sc[BN ? kPoolBNMaxC : 1];
+  __shared__ __attribute__((aligned(16))) float s_sh[BN ? kPoolBNMaxC : 1];
+  if constexpr (BN) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float a = bn.invstd[c] * (bn.w ? bn.w[c] : 1.f);
+      s_sc[c] = a;
+      s_sh[c] = (bn.b ? bn.b[c] : 0.f) - bn.mean[c] * a;
+    }
+    __syncthreads();
+  }
   const int64_t total = (int64_t)N * OH * OW * CV;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -204,9 +218,8 @@ __global__ void __launch_bounds__(kPoolThreads)
     if constexpr (BN) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int c = cv * 8 + i;
-        sc[i] = bn.invstd[c] * (bn.w ? bn.w[c] : 1.f);
-        sh[i] = (bn.b ? bn.b[c] : 0.f) - bn.mean[c] * sc[i];
+        sc[i] = s_sc[cv * 8 + i];
+        sh[i] = s_sh[cv * 8 + i];
       }
     }
     float best[8];
@@ -451,7 +464,7 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
     const T* xp = static_cast<const T*>(x);
     T* yp = static_cast<T*>(y);
     if constexpr (sizeof(T) == 2) {
-      if (vec && stem_ok(k, s, p, H, W, OH, OW)) {
+      if (vec && stem_ok(k, s, p, H, W, OH, OW) && (!with_bn || C <= kPoolBNMaxC)) {
         if (with_bn)
           hipLaunchKernelGGL((maxpool3s2_fwd_k<T, true>), g, b, 0, st, xp, yp, idx, N, H, W, C,
                              OH, OW, bn);
