@@ -210,6 +210,19 @@ __global__ void __launch_bounds__(kBNThreads)
 }
 
 // ---------------------------------------------------------------- apply
+// channels of one elementwise-pass workgroup: ctile <= 64 lanes x 8 (ngeom)
+constexpr int kBNBlockChans = 64 * 8;
+
+// per-channel constants of the workgroup's channel range [cb, cb + n) computed once,
+// one channel per thread (f(c, slot) writes LDS slot c - cb), then a barrier - every
+// thread of the block must call this before any early exit
+template <typename F>
+__device__ __forceinline__ void stage_params(int C, int cb, int n, F&& f) {
+  const int lim = cb + n < C ? n : C - cb;
+  for (int k = threadIdx.x; k < lim; k += blockDim.x) f(cb + k, k);
+  __syncthreads();
+}
+
 template <typename T, typename TW, bool VEC, int U>
 __global__ void __launch_bounds__(kBNThreads)
     apply_k(const T* __restrict__ x, const float* __restrict__ mean,
@@ -220,11 +233,19 @@ __global__ void __launch_bounds__(kBNThreads)
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
+  // the block's channel parameters, one channel per thread, staged in LDS
+  __shared__ __attribute__((aligned(16))) float s_par[2][kBNBlockChans];
+  const int cb = blockIdx.y * ctile * W;
+  stage_params(C, cb, ctile * W, [&](int c, int k) {
+    chan_affine(mean, invstd, wload(w, c, 1.f), wload(b, c, 0.f), c, s_par[0][k], s_par[1][k]);
+  });
   if (ri >= rows_iter || c0 >= C) return;
   float sc[W], sh[W];
 #pragma unroll
-  for (int i = 0; i < W; ++i)
-    chan_affine(mean, invstd, wload(w, c0 + i, 1.f), wload(b, c0 + i, 0.f), c0 + i, sc[i], sh[i]);
+  for (int i = 0; i < W; ++i) {
+    sc[i] = s_par[0][c0 - cb + i];
+    sh[i] = s_par[1][c0 - cb + i];
+  }
   const int64_t stride = (int64_t)gridDim.x * rows_iter;
   for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
     float v[U][W], zz[U][W];
@@ -274,12 +295,19 @@ __global__ void __launch_bounds__(kBNThreads)
   float mu[W], sc[W], sh[W], s1[W], s2[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) mu[i] = sc[i] = sh[i] = s1[i] = s2[i] = 0.f;
+  __shared__ __attribute__((aligned(16))) float s_par[3][kBNBlockChans];
+  const int cb = blockIdx.y * ctile * W;
+  stage_params(C, cb, ctile * W, [&](int c, int k) {
+    s_par[0][k] = mean[c];
+    chan_affine(mean, invstd, wload(w, c, 1.f), wload(b, c, 0.f), c, s_par[1][k], s_par[2][k]);
+  });
   if (active) {
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-      mu[i] = mean[c0 + i];
-      chan_affine(mean, invstd, wload(w, c0 + i, 1.f), wload(b, c0 + i, 0.f), c0 + i, sc[i],
-                  sh[i]);
+      const int k = c0 - cb + i;
+      mu[i] = s_par[0][k];
+      sc[i] = s_par[1][k];
+      sh[i] = s_par[2][k];
     }
     for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
       float xv[U][W], dv[U][W], zv[U][W];
@@ -332,18 +360,30 @@ __global__ void __launch_bounds__(kBNThreads)
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
+  // the block's channel constants, one channel per thread, staged in LDS (per thread
+  // they were ~7 scalar global loads per channel x 8 channels beside 16 rows of data)
+  __shared__ __attribute__((aligned(16))) float s_par[5][kBNBlockChans];
+  const int cb = blockIdx.y * ctile * W;
+  stage_params(C, cb, ctile * W, [&](int c, int k) {
+    const float wc = wload(w, c, 1.f);
+    chan_affine(mean, invstd, wc, wload(b, c, 0.f), c, s_par[0][k], s_par[1][k]);
+    const float is = invstd[c];
+    const float mdy = sum_dy[c] * inv_n, mdyx = sum_dy_xmu[c] * inv_n;
+    const float q1 = is * wc, q2 = -is * is * is * wc * mdyx;
+    s_par[2][k] = q1;
+    s_par[3][k] = q2;
+    s_par[4][k] = -is * wc * mdy - q2 * mean[c];
+  });
   if (ri >= rows_iter || c0 >= C) return;
   float sc[W], sh[W], k1[W], k2[W], k3[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int c = c0 + i;
-    const float wc = wload(w, c, 1.f);
-    chan_affine(mean, invstd, wc, wload(b, c, 0.f), c, sc[i], sh[i]);
-    const float is = invstd[c];
-    const float mdy = sum_dy[c] * inv_n, mdyx = sum_dy_xmu[c] * inv_n;
-    k1[i] = is * wc;
-    k2[i] = -is * is * is * wc * mdyx;
-    k3[i] = -is * wc * mdy - k2[i] * mean[c];
+    const int k = c0 - cb + i;
+    sc[i] = s_par[0][k];
+    sh[i] = s_par[1][k];
+    k1[i] = s_par[2][k];
+    k2[i] = s_par[3][k];
+    k3[i] = s_par[4][k];
   }
   const int64_t stride = (int64_t)gridDim.x * rows_iter;
   for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
