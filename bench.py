@@ -130,8 +130,23 @@ def parse():
 
 
 def _free_port():
+    """Rendezvous port for self-spawned ranks, drawn below Linux's ephemeral range
+    (32768-60999) so an outgoing connection cannot take it between this check and the
+    store's bind; an ephemeral port is the fallback."""
+    import random
     import socket
 
+    rng = random.Random(os.getpid() ^ int.from_bytes(os.urandom(4), "little"))
+    for _ in range(200):
+        port = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", port))
+            return port
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]

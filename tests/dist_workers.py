@@ -14,6 +14,23 @@ import torch.nn.functional as F
 
 
 def free_port():
+    """A port for a child process's TCP rendezvous, drawn below Linux's ephemeral range
+    (32768-60999): a port the kernel hands out as ephemeral (bind to 0) can be taken by
+    any outgoing connection on a shared box between this check and the child's bind
+    (EADDRINUSE seen on a GPU box)."""
+    import random
+
+    rng = random.Random(os.getpid() ^ int.from_bytes(os.urandom(4), "little"))
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
