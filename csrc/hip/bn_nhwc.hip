@@ -97,8 +97,8 @@ int reduce_splits(int64_t M, const NGeom& g) {
 // per thread (up to 32) that still leaves >= 384 workgroups.  It cut apply + backward
 // 4 % R50-weighted in isolation but measured 0.25 % SLOWER in the training step
 // (same-box A/B, 9662 vs 9687 img/s: the isolated loop re-reads a cache-warm tensor),
-// so the fixed elem_rpt stays the default; APEX_AMD_BN_ELEM_AUTO=1 or
-// bn_set_tuning(elem_rpt=0) selects the rule.
+// so the fixed elem_rpt (8 since the constants moved to LDS, bn_common.h) stays the
+// default; APEX_AMD_BN_ELEM_AUTO=1 or bn_set_tuning(elem_rpt=0) selects the rule.
 int elem_rpt_for(int64_t M, const NGeom& g, int64_t bytes) {
   const BNTuning& t = bn_tuning();
   static const bool env_auto = [] {

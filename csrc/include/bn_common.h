@@ -190,8 +190,12 @@ static inline void launch_reduce_finalize(const float* slab, int splits, int64_t
 // Defaults from the ResNet-50-weighted sweep on MI355X (profiles/bn_tune.txt):
 // reductions -8 %, elementwise passes -18 % vs the first sizing (32/2048, 4/8192).
 struct BNTuning {
-  int red_rpt = 64, red_cap = 1024, red_min = 512;
-  int elem_rpt = 16, elem_cap = 16384, elem_min = 0;
+  // red_rpt 64 -> 32 and elem_rpt 16 -> 8 at the end of round 4, once the elementwise
+  // passes stopped computing channel constants per thread (a cheaper prologue favours
+  // more, shorter workgroups): ResNet-50 same-box pairs +0.3 .. +0.9 % (profiles/r4/y,
+  // profiles/r4/z; docs/PERF.md)
+  int red_rpt = 32, red_cap = 1024, red_min = 512;
+  int elem_rpt = 8, elem_cap = 16384, elem_min = 0;
   bool elem_auto = false;  // per-shape elem_rpt rule (bn_nhwc.hip elem_rpt_for), opt-in
 };
 BNTuning& bn_tuning();
