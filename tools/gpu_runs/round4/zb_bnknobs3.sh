@@ -1,0 +1,16 @@
+# round 4 box ZB: BN reduction grid cap and rows per thread around the new defaults,
+# ResNet-50 two runs each, same box
+set -e
+cd /root/repo
+export TMPDIR=/tmp
+O=gpurun_out/r4zb
+mkdir -p $O
+B="python -u bench.py --steps 20 --warmup 8"
+for r in 1 2; do
+  timeout -k 10 300 $B --json-out $O/def_$r.json > $O/def_$r.log 2>&1
+  APEX_AMD_BN_TUNING="-1,2048,-1,-1,-1,-1" timeout -k 10 300 $B --json-out $O/cap2k_$r.json > $O/cap2k_$r.log 2>&1
+  APEX_AMD_BN_TUNING="-1,4096,-1,-1,-1,-1" timeout -k 10 300 $B --json-out $O/cap4k_$r.json > $O/cap4k_$r.log 2>&1
+  APEX_AMD_BN_TUNING="-1,-1,-1,4,-1,-1" timeout -k 10 300 $B --json-out $O/e4_$r.json > $O/e4_$r.log 2>&1
+  APEX_AMD_BN_TUNING="16,-1,-1,-1,-1,-1" timeout -k 10 300 $B --json-out $O/r16_$r.json > $O/r16_$r.log 2>&1
+done
+echo ok
