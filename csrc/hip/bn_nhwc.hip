@@ -278,11 +278,16 @@ __global__ void __launch_bounds__(kBNThreads)
 }
 
 // ---------------------------------------------------------------- backward reduce
-template <typename T, typename TW, bool VEC, int U>
+// RM (compile time): 0 no ReLU, 1 ReLU from the 1-bit mask, 2 ReLU recomputed with the
+// residual z, 3 ReLU recomputed without z.  With the mode a runtime flag the loop was
+// branches around every load, each followed by a vmcnt(0) wait (1-2 loads in flight:
+// 2.15 TB/s, profiles/r4/zd); rows past the split end load a clamped (valid) row and
+// contribute exactly what the old zero-filled slot did.
+template <typename T, typename TW, bool VEC, int U, int RM>
 __global__ void __launch_bounds__(kBNThreads)
     reduce_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
              const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
-             const T* __restrict__ z, const uint8_t* __restrict__ rmask, int relu, int64_t M,
+             const T* __restrict__ z, const uint8_t* __restrict__ rmask, int64_t M,
              int C, int ctile, int rows_iter, float* __restrict__ slab) {
   constexpr int W = VEC ? 8 : 1;
   const int Cb = C >> 3;
@@ -312,33 +317,34 @@ __global__ void __launch_bounds__(kBNThreads)
     for (int64_t r = r0 + ri; r < r1; r += (int64_t)rows_iter * U) {
       float xv[U][W], dv[U][W], zv[U][W];
       uint32_t mk[U];
+      bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t rr = r + (int64_t)u * rows_iter;
+        ok[u] = rr < r1;
+        const int64_t rc = ok[u] ? rr : r1 - 1;
+        ldw<T, W>(x + rc * C + c0, xv[u]);
+        ldw<T, W>(dy + rc * C + c0, dv[u]);
         mk[u] = 0;
-#pragma unroll
-        for (int i = 0; i < W; ++i) xv[u][i] = dv[u][i] = zv[u][i] = 0.f;  // dy = 0: no-op
-        if (rr < r1) {
-          ldw<T, W>(x + rr * C + c0, xv[u]);
-          ldw<T, W>(dy + rr * C + c0, dv[u]);
-          if (relu && rmask) mk[u] = rmask[rr * Cb + (c0 >> 3)];
-          else if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
-        }
+        if constexpr (RM == 1) mk[u] = rmask[rc * Cb + (c0 >> 3)];
+        if constexpr (RM == 2) ldw<T, W>(z + rc * C + c0, zv[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int i = 0; i < W; ++i) {
           float d = dv[u][i];
-          if (relu && rmask) {
+          if constexpr (RM == 1) {
             d = ((mk[u] >> ((c0 + i) & 7)) & 1u) ? d : 0.f;
-          } else if (relu) {
+          } else if constexpr (RM >= 2) {
             float o = fmaf(xv[u][i], sc[i], sh[i]);
-            if (z) o += zv[u][i];
+            if constexpr (RM == 2) o += zv[u][i];
             d = o > 0.f ? d : 0.f;
           }
+          d = ok[u] ? d : 0.f;
+          const float xe = ok[u] ? xv[u][i] : 0.f;
           s1[i] += d;
-          s2[i] = fmaf(d, xv[u][i] - mu[i], s2[i]);
+          s2[i] = fmaf(d, xe - mu[i], s2[i]);
         }
     }
   }
@@ -348,12 +354,14 @@ __global__ void __launch_bounds__(kBNThreads)
 // ---------------------------------------------------------------- backward elementwise
 // dx = dy'*k1 + x*k2 + k3  with  k1 = invstd*w, k2 = -invstd^3*w*mean(dy'(x-mu)),
 //                                 k3 = -invstd*w*mean(dy') - k2*mu ;  dz = dy'
-template <typename T, typename TW, bool VEC, int U>
+// RM: the ReLU mode of reduce_k, compile time (rows past M load a clamped row; their
+// results are never stored)
+template <typename T, typename TW, bool VEC, int U, int RM>
 __global__ void __launch_bounds__(kBNThreads)
     backward_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
                const float* __restrict__ invstd, const TW* __restrict__ w,
                const TW* __restrict__ b, const float* __restrict__ sum_dy,
-               const float* __restrict__ sum_dy_xmu, float inv_n, int relu,
+               const float* __restrict__ sum_dy_xmu, float inv_n,
                const T* __restrict__ z, const uint8_t* __restrict__ rmask, T* __restrict__ dx,
                T* __restrict__ dz, int64_t M, int C, int ctile, int rows_iter) {
   constexpr int W = VEC ? 8 : 1;
@@ -392,13 +400,12 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t rr = r + (int64_t)u * stride;
+      const int64_t rc = rr < M ? rr : M - 1;
       mk[u] = 0;
-      if (rr < M) {
-        ldw<T, W>(x + rr * C + c0, xv[u]);
-        ldw<T, W>(dy + rr * C + c0, dv[u]);
-        if (relu && rmask) mk[u] = rmask[rr * Cb + (c0 >> 3)];
-        else if (relu && z) ldw<T, W>(z + rr * C + c0, zv[u]);
-      }
+      ldw<T, W>(x + rc * C + c0, xv[u]);
+      ldw<T, W>(dy + rc * C + c0, dv[u]);
+      if constexpr (RM == 1) mk[u] = rmask[rc * Cb + (c0 >> 3)];
+      if constexpr (RM == 2) ldw<T, W>(z + rc * C + c0, zv[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -407,11 +414,11 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
       for (int i = 0; i < W; ++i) {
         float d = dv[u][i];
-        if (relu && rmask) {
+        if constexpr (RM == 1) {
           d = ((mk[u] >> ((c0 + i) & 7)) & 1u) ? d : 0.f;
-        } else if (relu) {
+        } else if constexpr (RM >= 2) {
           float o = fmaf(xv[u][i], sc[i], sh[i]);
-          if (z) o += zv[u][i];
+          if constexpr (RM == 2) o += zv[u][i];
           d = o > 0.f ? d : 0.f;
         }
         dv[u][i] = d;
@@ -646,12 +653,20 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
       using TW = decltype(w0);
       vec_dispatch(vec, [&](auto V) {
         constexpr bool VV = decltype(V)::value;
+        const int rm = !relu ? 0 : rmask ? 1 : z ? 2 : 3;
         auto go = [&](auto u) {
-          hipLaunchKernelGGL((reduce_k<T, TW, VV, decltype(u)::value>), dim3(splits, g.cblocks),
-                             dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
-                             static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
-                             static_cast<const TW*>(b), static_cast<const T*>(z), rmask, relu, M,
-                             (int)C, g.ctile, g.rows_iter, ws);
+          auto launch = [&](auto m) {
+            hipLaunchKernelGGL((reduce_k<T, TW, VV, decltype(u)::value, decltype(m)::value>),
+                               dim3(splits, g.cblocks), dim3(kBNThreads), 0, st,
+                               static_cast<const T*>(dy), static_cast<const T*>(x), mean, invstd,
+                               static_cast<const TW*>(w), static_cast<const TW*>(b),
+                               static_cast<const T*>(z), rmask, M, (int)C, g.ctile, g.rows_iter,
+                               ws);
+          };
+          if (rm == 0) launch(std::integral_constant<int, 0>{});
+          else if (rm == 1) launch(std::integral_constant<int, 1>{});
+          else if (rm == 2) launch(std::integral_constant<int, 2>{});
+          else launch(std::integral_constant<int, 3>{});
         };
         if (bn_unroll().reduce == 4) go(std::integral_constant<int, 4>{});
         else go(std::integral_constant<int, 2>{});
@@ -675,14 +690,21 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
       using T = decltype(t0);
       using TW = decltype(w0);
       vec_dispatch(vec, [&](auto V) {
+        const int rm = !relu ? 0 : rmask ? 1 : z ? 2 : 3;
         auto go = [&](auto u) {
-          hipLaunchKernelGGL((backward_k<T, TW, decltype(V)::value, decltype(u)::value>),
-                             dim3(blocks, g.cblocks), dim3(kBNThreads), 0, st,
-                             static_cast<const T*>(dy), static_cast<const T*>(x), mean, invstd,
-                             static_cast<const TW*>(w), static_cast<const TW*>(b), sum_dy,
-                             sum_dy_xmu, inv_count, relu, static_cast<const T*>(z), rmask,
-                             static_cast<T*>(dx), static_cast<T*>(dz), M, (int)C, g.ctile,
-                             g.rows_iter);
+          auto launch = [&](auto m) {
+            hipLaunchKernelGGL(
+                (backward_k<T, TW, decltype(V)::value, decltype(u)::value, decltype(m)::value>),
+                dim3(blocks, g.cblocks), dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
+                static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
+                static_cast<const TW*>(b), sum_dy, sum_dy_xmu, inv_count,
+                static_cast<const T*>(z), rmask, static_cast<T*>(dx), static_cast<T*>(dz), M,
+                (int)C, g.ctile, g.rows_iter);
+          };
+          if (rm == 0) launch(std::integral_constant<int, 0>{});
+          else if (rm == 1) launch(std::integral_constant<int, 1>{});
+          else if (rm == 2) launch(std::integral_constant<int, 2>{});
+          else launch(std::integral_constant<int, 3>{});
         };
         if (bn_unroll().elem == 4) go(std::integral_constant<int, 4>{});
         else go(std::integral_constant<int, 2>{});
