@@ -411,7 +411,6 @@ def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype):
 # (APEX_AMD_GEMM8P=1) while the kernel trails hipBLASLt on these shapes
 # (profiles/r4/gemm8p_bench.md).
 _G8 = os.environ.get("APEX_AMD_GEMM8P", "0") == "1"
-_T_CACHE = {}  # id(weight) -> (weight, version, data_ptr, transposed copy)
 
 
 def _g8_ok(a, b, *more):
@@ -422,14 +421,11 @@ def _g8_ok(a, b, *more):
 
 
 def _transposed(w):
-    """w^T contiguous, cached while the weight is unchanged (in-place optimizer updates
-    bump its version)."""
-    ent = _T_CACHE.get(id(w))
-    if ent is not None and ent[0] is w and ent[1] == w._version and ent[2] == w.data_ptr():
-        return ent[3]
-    t = w.t().contiguous()
-    _T_CACHE[id(w)] = (w, w._version, w.data_ptr(), t)
-    return t
+    """w^T contiguous, built on every call.  No cache: the fused optimizers and amp's
+    master -> model copy write weights through their data pointers without bumping the
+    version counter, so a cache keyed on (version, data_ptr) would go stale silently;
+    the transpose is one small pass (8 MB for a BERT-large W2) per backward."""
+    return w.t().contiguous()
 
 
 def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):

@@ -14,10 +14,13 @@ An announcement is only sound when that ONE use of the parameter produces its wh
 gradient for the iteration.  So (a) the DDP wrapper excludes parameters listed more than
 once in the module tree (tied weights, ``Reducer.set_no_direct``); (b) the own ops count
 their forward uses of each parameter (``note_use``) and go direct only for a parameter
-used exactly once this iteration (a module called twice takes the autograd path, which
-sums both uses before one AccumulateGrad); (c) the reducer refuses a second announcement
-and, if an autograd gradient of some other use lands on top of an announced one, it
-excludes the parameter from then on and raises if the bucket was already launched.
+used exactly once in the current forward (a module called twice takes the autograd path,
+which sums both uses before one AccumulateGrad); uses are counted per DDP forward call
+(``forward_epoch``), so gradient-accumulation micro-steps and eval forwards in between
+do not disturb the count; (c) the reducer refuses a second announcement, and the ready
+mark itself comes from the AccumulateGrad hook after every use has been summed, so an
+autograd gradient of some other use still lands in the view before the bucket launches
+(the parameter is excluded from the direct path from then on).
 """
 from __future__ import annotations
 
@@ -28,6 +31,18 @@ import torch
 _ON = os.environ.get("APEX_AMD_DDP_DIRECT_GRAD", "1") == "1"
 # lazy zeroing of bucket-view gradients (APEX_AMD_DDP_LAZY_ZERO=0: a zero kernel per step)
 _LAZY = os.environ.get("APEX_AMD_DDP_LAZY_ZERO", "1") == "1"
+
+
+_EPOCH = {}  # id(reducer) -> forward calls of its DDP wrapper
+
+
+def forward_epoch(red):
+    """Start a new use count for ``red``'s parameters (DistributedDataParallel.forward)."""
+    _EPOCH[id(red)] = _EPOCH.get(id(red), 0) + 1
+
+
+def _epoch(red):
+    return _EPOCH.get(id(red), 0)
 
 
 def note_use(*params):
@@ -42,7 +57,7 @@ def note_use(*params):
         red = slot[0]()
         if red is None:
             continue
-        it = red.iteration()
+        it = _epoch(red)
         u = getattr(p, "_amd_ddp_uses", None)
         p._amd_ddp_uses = (it, u[1] + 1) if (u is not None and u[0] == it) else (it, 1)
 
@@ -60,7 +75,7 @@ def slot(p):
     if p.grad is None and red.lazy_view(s[1]) is None:
         return None
     u = getattr(p, "_amd_ddp_uses", None)
-    if u is None or u[1] != 1 or u[0] != red.iteration():
+    if u is None or u[1] != 1 or u[0] != _epoch(red):
         return None
     return red, s[1]
 

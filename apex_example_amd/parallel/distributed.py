@@ -56,8 +56,9 @@ all-reduce for every 16-bit bucket.  How the fp32 sum of a bf16 bucket travels
 (``bf16_wire``, env ``APEX_AMD_DDP_BF16_WIRE``):
 
 * ``"rsag"`` (default): fp32 reduce-scatter + in-place bf16 all-gather - each rank's
-  shard is summed in fp32 and rounded to bf16 once, exactly the fp32 all-reduce's
-  values, at (n-1)/n x 6 bytes per element on the wire instead of 2 (n-1)/n x 4;
+  shard is summed in fp32 and rounded to bf16 once (one rounding of an fp32 sum, as
+  the fp32 all-reduce; bitwise equal to it on gloo, while on RCCL the two may sum in
+  different orders), at (n-1)/n x 6 bytes per element on the wire instead of 2 (n-1)/n x 4;
 * ``"fp32"``: one fp32 all-reduce of an up-cast copy (8 bytes per element);
 * ``"native"``: bf16 all-reduce (4 bytes per element, rounded at every hop).
 
@@ -74,6 +75,7 @@ import torch.distributed as dist
 from torch.nn.modules import Module
 
 from .. import _native
+from ..ops import _ddp_direct
 
 
 XGMI_BUCKET_BYTES = 32 << 20
@@ -507,6 +509,9 @@ class DistributedDataParallel(Module):
                 self._build_reducer()
         if self.prof:
             torch.cuda.nvtx.range_push("forward pass DDP logic")
+        # own ops count their parameters' forward uses per DDP forward (direct-gradient
+        # path eligibility, ops/_ddp_direct.py)
+        _ddp_direct.forward_epoch(self.reducer)
         out = self.module(*inputs, **kwargs)
         if self.prof:
             torch.cuda.nvtx.range_pop()

@@ -242,36 +242,34 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       lazy_[(size_t)i] = 0;
     }
     if (announced) {
+      // The announcement only records that the gradient is in the view (and, for a
+      // side stream, the event the bucket's collective must wait for).  The ready mark
+      // itself is left to the AccumulateGrad post-hook, which fires once every use of
+      // the parameter has been summed: a bucket can then never launch before a late
+      // autograd gradient of another use lands in the same view.
       TORCH_CHECK(!async_marked_[(size_t)i] && !seen_[(size_t)i],
                   "DistributedDataParallel: parameter ", i,
                   " was announced twice in one backward pass (a module used more than once "
                   "per iteration on the direct-gradient path)");
       async_marked_[(size_t)i] = 1;
-    } else if (async_marked_[(size_t)i]) {
-      // the AccumulateGrad post-hook of a gradient that was announced from the side
-      // stream (the Function returned None for it; the hook still runs): consumed
-      async_marked_[(size_t)i] = 0;
-      if (had_grad) {
-        // another use of the parameter accumulated an autograd gradient into the same
-        // bucket view: correct only while its bucket has not been handed to the
-        // collective yet.  Never announce this parameter again.
-        no_direct_[(size_t)i] = 1;
-        const Bucket& b = buckets_[(size_t)bucket_of_[(size_t)i]];
-        TORCH_CHECK(!enabled_ || refresh_ || delay_ || !b.launched,
-                    "DistributedDataParallel: parameter ", i,
-                    " received an autograd gradient after its directly accumulated one was "
-                    "already being all-reduced (a parameter shared between an own-kernel op "
-                    "and another op); it uses the autograd path from the next iteration on, "
-                    "or set APEX_AMD_DDP_DIRECT_GRAD=0");
+      attach_view(i);
+      if (with_event && enabled_ && !refresh_ && !delay_ && comm_active()) {
+        hipEvent_t e = take_event();
+        TORCH_CHECK(hipEventRecord(e, side) == hipSuccess, "hipEventRecord failed");
+        buckets_[(size_t)bucket_of_[(size_t)i]].waits.push_back(e);
       }
       return;
     }
-    attach_view(i);
-    if (announced && with_event && enabled_ && !refresh_ && !delay_ && comm_active()) {
-      hipEvent_t e = take_event();
-      TORCH_CHECK(hipEventRecord(e, side) == hipSuccess, "hipEventRecord failed");
-      buckets_[(size_t)bucket_of_[(size_t)i]].waits.push_back(e);
+    if (async_marked_[(size_t)i]) {
+      // the AccumulateGrad post-hook of an announced gradient (the Function returned
+      // None for it; the hook still runs): the parameter is ready now
+      async_marked_[(size_t)i] = 0;
+      // another use accumulated an autograd gradient on top of the announced one: the
+      // sum in the view is correct (the bucket has not launched), but announcing this
+      // parameter is pointless work from now on
+      if (had_grad) no_direct_[(size_t)i] = 1;
     }
+    attach_view(i);
     if (!enabled_) return;
     if (!callback_queued_) {
       callback_queued_ = true;
