@@ -101,6 +101,9 @@ _SIDE_PRIO = os.environ.get("APEX_AMD_WGRAD_STREAM_PRIO", "auto")
 # contention it removes (profiles/r4/m/).
 _SIDE_CUS = int(os.environ.get("APEX_AMD_WGRAD_STREAM_CUS", "0"))
 _SIDE_EVENTS = {}   # device index -> deque of side-stream events, oldest first
+# test hook (tests/test_ddp_gpu.py race test): GPU cycles the side stream sleeps before
+# each weight gradient, to skew it against the compute stream and the bucket streams
+_TEST_SIDE_SLEEP = 0
 
 
 def _join_side():
@@ -157,6 +160,8 @@ class _SideWgrad:
             return fn()
         self.side.wait_event(self.ev)
         with torch.cuda.stream(self.side):
+            if _TEST_SIDE_SLEEP:
+                torch.cuda._sleep(_TEST_SIDE_SLEEP)
             dw = fn()
             outs = dw if isinstance(dw, tuple) else (dw,)
             if self.mode == "ddp":

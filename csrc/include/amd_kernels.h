@@ -289,6 +289,10 @@ struct G8Args {
 bool gemm8p_supported(int M, int N, int K);
 int gemm8p_mtiles(int M);
 void gemm8p(const G8Args& a, int epi, hipStream_t st);
+// the same GEMM and epilogues with one wave per SIMD, 128 x 128 per wave (gemm4w.hip):
+// N % 256 == 0, K % 64 == 0
+bool gemm4w_supported(int M, int N, int K);
+void gemm4w(const G8Args& a, int epi, hipStream_t st);
 
 // ---- implicit-GEMM convolutions, NHWC bf16, MFMA (conv_igemm.hip) ----------
 // 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64

@@ -100,7 +100,7 @@ std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tenso
   return {dpre, out};
 }
 
-bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
+static bool gemm_layout_ok(const at::Tensor& a, const at::Tensor& b) {
   return a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 &&
          (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf) &&
          b.scalar_type() == a.scalar_type() &&
@@ -108,16 +108,29 @@ bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
          a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
          reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
          reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 && a.size(0) < (1 << 30) &&
+         // the 4-wave kernel's 32-bit DMA offsets: 256 rows of either operand
+         256 * std::max(a.stride(0), b.stride(0)) * a.element_size() < (int64_t(1) << 32);
+}
+
+bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
+  return gemm_layout_ok(a, b) &&
          gemm8p_supported((int)a.size(0), (int)b.size(0), (int)a.size(1));
+}
+
+bool gemm4w_ok(const at::Tensor& a, const at::Tensor& b) {
+  return gemm_layout_ok(a, b) &&
+         gemm4w_supported((int)a.size(0), (int)b.size(0), (int)a.size(1));
 }
 
 std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
                                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
                                   bool want_pre, bool tanh_approx,
-                                  c10::optional<at::ScalarType> bias_grad_dtype) {
+                                  c10::optional<at::ScalarType> bias_grad_dtype, int64_t kernel) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(gemm8p_ok(a, b), "gemm8p: bf16 / fp16 [M, K] x [N, K] with N % 256 == 0, K % 128 == 0, "
-              "unit column stride, 16-byte aligned rows");
+  TORCH_CHECK(kernel == 0 || kernel == 1, "gemm8p: kernel 0 (8-wave gemm8p) | 1 (4-wave gemm4w)");
+  TORCH_CHECK(kernel == 1 ? gemm4w_ok(a, b) : gemm8p_ok(a, b),
+              "gemm8p: bf16 / fp16 [M, K] x [N, K] with N % 256 == 0, K % 128 == 0 (kernel 1: "
+              "K % 64 == 0), unit column stride, 16-byte aligned rows");
   TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8p: epi 0 | 1 | 2");
   const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
   at::Tensor c = at::empty({M, N}, a.options());
@@ -159,7 +172,8 @@ std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
     part = at::empty({(int64_t)gemm8p_mtiles((int)M), N}, a.options().dtype(at::kFloat));
     g.colsum = part.data_ptr<float>();
   }
-  gemm8p(g, (int)epi, cur_stream());
+  if (kernel == 1) gemm4w(g, (int)epi, cur_stream());
+  else gemm8p(g, (int)epi, cur_stream());
   if (part.defined()) {
     at::Tensor db = at::empty({N}, a.options().dtype(*bias_grad_dtype));
     colsum_finalize(part.data_ptr<float>(), (int)part.size(0), (int)N, db.data_ptr(),

@@ -23,10 +23,12 @@ std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tenso
 // and B [N, K] (row-major), with the FFN epilogues.  epi 0: [C]; epi 1: bias + GELU ->
 // [h, pre (when want_pre)]; epi 2: dGELU from aux = pre -> [dpre, bias grad (when
 // bias_grad_dtype is given)].  gemm8p_ok: the shape / dtype / layout qualifies.
+// kernel 1: the one-wave-per-SIMD 128 x 128-per-wave form (csrc/hip/gemm4w.hip).
 bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b);
+bool gemm4w_ok(const at::Tensor& a, const at::Tensor& b);
 std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
                                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
                                   bool want_pre, bool tanh_approx,
-                                  c10::optional<at::ScalarType> bias_grad_dtype);
+                                  c10::optional<at::ScalarType> bias_grad_dtype, int64_t kernel);
 
 }  // namespace amd

@@ -139,8 +139,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   dn.def("wgrad_bgrad_lt", &dense_wgrad_bgrad_op);
   dn.def("gemm8p", &gemm8p_op, py::arg("a"), py::arg("b"), py::arg("epi") = 0,
          py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("want_pre") = false,
-         py::arg("tanh") = false, py::arg("bias_grad_dtype") = py::none());
+         py::arg("tanh") = false, py::arg("bias_grad_dtype") = py::none(),
+         py::arg("kernel") = 0);
   dn.def("gemm8p_ok", &gemm8p_ok);
+  dn.def("gemm4w_ok", &gemm4w_ok);
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);

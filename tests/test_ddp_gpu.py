@@ -86,6 +86,84 @@ def test_ddp_race_condition(pg, streams, dtype):
     assert len(ddp.bucket_layout()) >= 6
 
 
+class _ConvNet(torch.nn.Module):
+    """Own-kernel convs (3x3 MFMA implicit GEMM, 1x1 GEMM) whose weight gradients run on
+    the DDP side stream and write their bucket views directly, plus a SyncBN on the
+    forced collective path: every gradient has a closed form.  With an all-ones input
+    and loss k * sum(conv(x)), dW[co, r, s, ci] = k * (number of pixels whose tap (r, s)
+    lands inside the image) - integers, exact in the fp32 sums, rounded to bf16 once."""
+
+    def __init__(self):
+        super().__init__()
+        from apex_example_amd.ops.conv import Conv2d1x1, Conv2d3x3
+        from apex_example_amd.parallel import SyncBatchNorm
+
+        self.convs = torch.nn.ModuleList(
+            [Conv2d3x3(64, 64) if i % 2 == 0 else Conv2d1x1(64, 128) for i in range(8)])
+        self.convs.to(device="cuda", dtype=torch.bfloat16, memory_format=torch.channels_last)
+        self.bn = SyncBatchNorm(64, force_collectives=True).cuda()
+
+    def forward(self, x, z, ks, kb):
+        out = 0
+        for i, c in enumerate(self.convs):
+            xi = _Skew.apply(x) if i % 3 == 0 else x
+            out = out + ks[i] * c(xi).float().sum()
+        return out + kb * self.bn(z).float().sum()
+
+
+def test_ddp_race_condition_round4_defaults(pg, monkeypatch):
+    """The race test on the DDP defaults: bf16 buckets on the rsag wire (fp32
+    reduce-scatter + bf16 all-gather), own-kernel convs whose weight gradients run on the
+    high-priority side stream and write the (lazily zeroed) bucket views directly, sleep
+    skews on BOTH the compute and the side stream, SyncBN collectives in the same step,
+    zero_grad through the optimizer (lazy zero) and a step that consumes the buckets;
+    60 iterations, every gradient compared exactly with its closed form."""
+    from apex_example_amd.ops import conv as C
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    monkeypatch.setattr(C, "_TEST_SIDE_SLEEP", 1_000_000)
+    torch.manual_seed(0)
+    net = _ConvNet()
+    ddp = DistributedDataParallel(net, message_size=64 * 64 * 9 * 2, force_collectives=True)
+    assert ddp.reducer.collectives_active()
+    opt = FusedSGD(net.parameters(), lr=0.0)  # reads (consumes) every bucket, moves nothing
+    n, h, w = 2, 8, 8
+    x = torch.ones(n, 64, h, w, device="cuda", dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last).requires_grad_(True)
+    # +-1 per channel in equal numbers: mean 0, biased variance 1 exactly
+    z = torch.ones(n, 64, h, w, device="cuda")
+    z[:, :, :, w // 2:] = -1.0
+    z = z.to(memory_format=torch.channels_last)
+    cnt = torch.zeros(3, 3, dtype=torch.float64)
+    for r in range(3):
+        for s in range(3):
+            cnt[r, s] = n * (h - abs(r - 1)) * (w - abs(s - 1))
+    assert ddp._fp32_mode() == 3 and "reduce-scatter" in ddp.wire_format()["torch.bfloat16"]
+    bad = torch.zeros((), device="cuda", dtype=torch.float64)
+    for it in range(60):
+        ks = [float((it + i) % 3 + 1) for i in range(len(net.convs))]
+        kb = float(it % 4 + 1)
+        opt.zero_grad()
+        ddp(x, z, ks, kb).backward()
+        for i, c in enumerate(net.convs):
+            if c.kernel_size == (3, 3):
+                ref = (ks[i] * cnt).view(1, 1, 3, 3).expand(64, 64, 3, 3)
+            else:
+                ref = torch.full((128, 64, 1, 1), ks[i] * n * h * w, dtype=torch.float64)
+            ref = ref.to(torch.bfloat16).to("cuda").double()
+            bad += (c.weight.grad.double() - ref).abs().max()
+        bad += (net.bn.bias.grad.double() - kb * n * h * w).abs().max()
+        bad += (net.bn.weight.grad.double().abs().max() > 1e-3).double()
+        opt.step()
+        x.grad = None
+    torch.cuda.synchronize()
+    assert bad.item() == 0.0
+    # the DDP side stream (high priority) carried the conv weight gradients
+    assert any(key[1] for key in C._SIDE), C._SIDE
+    assert len(ddp.bucket_layout()) >= 4
+
+
 def test_ddp_bucket_timing(pg):
     """Per-bucket launch / join times from the reducer's HIP events: buckets are
     launched in order during backward, and the exposed tail is measured."""

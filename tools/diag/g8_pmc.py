@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Run ONE GEMM shape many times through gemm8p and through torch.mm (hipBLASLt), for
+"""Run ONE GEMM shape many times through gemm8p, gemm4w and torch.mm (hipBLASLt), for
 rocprofv3 --pmc passes (tools/diag/run_pmc.sh tools/diag/g8_pmc.py tools/diag/g8_pmc.txt)."""
 import argparse
 import os
@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--k", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--kernels", default="8p,4w,lt", help="gemm8p, gemm4w, hipBLASLt")
     a = ap.parse_args()
     from apex_example_amd import _native
 
@@ -23,9 +24,14 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.randn(a.m, a.k, device="cuda", generator=g).to(torch.bfloat16)
     w = torch.randn(a.n, a.k, device="cuda", generator=g).to(torch.bfloat16)
+    ks = a.kernels.split(",")
     for _ in range(a.iters):
-        dn.gemm8p(x, w, 0, None, None, False, False, None)
-        torch.mm(x, w.t())
+        if "8p" in ks:
+            dn.gemm8p(x, w, 0, None, None, False, False, None, 0)
+        if "4w" in ks:
+            dn.gemm8p(x, w, 0, None, None, False, False, None, 1)
+        if "lt" in ks:
+            torch.mm(x, w.t())
     torch.cuda.synchronize()
     print("done")
 
