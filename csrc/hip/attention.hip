@@ -118,15 +118,17 @@ __device__ __forceinline__ int tr_addr(int r0, int c0, int lane) {
   return swz_tr(r0 + q, col >> 3) + ((col >> 2) & 1) * 8;
 }
 
-// Counter-based dropout bits: one 32-bit hash per (query, key pair), 16 bits per key.
-// The hash input is a point of a Weyl lattice, base(seed, b*H+h) + q*kDropQ +
-// (key>>1)*kDropK (mod 2^32), so a kernel steps from one (query, key pair) to the next
-// with ONE add whose lattice offset is a compile-time literal; the mixer uses the
-// full-rate 24-bit multiply (v_mul_u32_u24) where the classic 32-bit finalizers need
-// the quarter-rate v_mul_lo_u32 (measured: 2-3 v_mul_lo_u32 per hash were ~60 % of the
-// dropout VALU time).  Statistics checked against the 32-bit finalizer on 2M-score
-// grids (keep rate, neighbour correlations along q / k / diagonal, 2-D spectrum,
-// 16-bit uniformity); tests/test_attention_gpu.py mirrors it bit for bit.
+// Counter-based dropout bits: one 32-bit hash per (query, key QUAD), one byte per key:
+// key k keeps its score iff byte (k & 3) of the hash is >= thr8 = round(256 p) (so p is
+// quantised to 1/256 and the kept scores are scaled by 256 / (256 - thr8), unbiased for
+// the quantised rate).  One hash per four scores instead of per two: the hash was ~half of
+// the forward's VALU (267 of 520 per tile, docs/PERF.md round 4).  The hash input is a
+// point of a Weyl lattice, base(seed, b*H+h) + q*kDropQ + (key>>2)*kDropK (mod 2^32), so
+// a kernel steps from one (query, key quad) to the next with ONE add whose lattice offset
+// is a compile-time literal; the mixer uses the full-rate 24-bit multiply
+// (v_mul_u32_u24) where the classic 32-bit finalizers need the quarter-rate v_mul_lo_u32.
+// tests/test_attention_gpu.py mirrors it bit for bit; tests/test_dropout_hash_cpu.py
+// checks the keep rate, byte uniformity and neighbour correlations of the mirror.
 constexpr uint32_t kDropQ = 0x85EBCA77u, kDropK = 0xC2B2AE3Du;
 
 __device__ __forceinline__ uint32_t drop_base(uint32_t seed, uint32_t bh) {
@@ -150,16 +152,16 @@ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
 
 // the closed form; the kernels' incremental lattice steps compute exactly this
 [[maybe_unused]] __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q,
-                                              uint32_t kp) {
-  return drop_mix(drop_base(seed, bh) + q * kDropQ + kp * kDropK);
+                                              uint32_t kquad) {
+  return drop_mix(drop_base(seed, bh) + q * kDropQ + kquad * kDropK);
 }
 
 // raw v_exp_f32: exp2f() expands to a denormal-safe sequence (compare, select, ldexp:
 // 5-6 VALU per score); softmax arguments are <= 0 and a result below 2^-126 may flush
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
-__device__ __forceinline__ bool drop_keep(uint32_t h, int key, uint32_t thr16) {
-  const uint32_t v = (key & 1) ? (h >> 16) : (h & 0xffffu);
-  return v >= thr16;
+// keep decision of byte e (= key & 3) of a (query, key quad) hash
+__device__ __forceinline__ bool drop_keep8(uint32_t h, int e, uint32_t thr8) {
+  return ((h >> (8 * e)) & 0xffu) >= thr8;
 }
 
 // one v_cvt_pk_{bf16,f16}_f32 per pair (converting the two floats separately and
@@ -206,7 +208,7 @@ struct AttnArgs {
   float* lse;        // [B][H][lse_stride]
   int B, H, S, lse_stride;
   float scale_log2;  // softmax scale * log2(e)
-  uint32_t thr16;    // dropout threshold (p * 65536), 0 = no dropout
+  uint32_t thr8;     // dropout threshold round(p * 256) on a hash byte, 0 = no dropout
   float inv_keep;    // 1 / (1 - p)
   uint32_t seed;
   int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
@@ -278,9 +280,9 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   const int b = bh / a.H, hh = bh - b * a.H;
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;  // this lane's query
-  // dropout lattice point of (q, key pair 2hl) at key tile 0
+  // dropout lattice point of (q, key quad hl) at key tile 0
   const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
-                                    (uint32_t)(2 * hl) * kDropK
+                                    (uint32_t)hl * kDropK
                               : 0u;
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
@@ -419,15 +421,16 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
       }
     }
     if (DROP) {  // dropped P (the 1/(1-p) factor is applied to O once, at the store)
-      const uint32_t tb = dbase + (uint32_t)(k0 >> 1) * kDropK;
+      const uint32_t tb = dbase + (uint32_t)(k0 >> 2) * kDropK;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          // key pair (k0 + 32t + (r&3) + 8(r>>2) + 4hl) >> 1: a literal lattice step
-          const uint32_t hsh = drop_mix(tb + (uint32_t)(16 * t + ((r >> 1) & 1) + 4 * (r >> 2)) * kDropK);
-          x[t][r] = (hsh & 0xffffu) >= a.thr16 ? x[t][r] : 0.f;
-          x[t][r + 1] = (hsh >> 16) >= a.thr16 ? x[t][r + 1] : 0.f;
+        for (int rq = 0; rq < 4; ++rq) {
+          // key quad (k0 + 32t + 8rq + 4hl) >> 2 (keys + r & 3): a literal lattice step
+          const uint32_t hsh = drop_mix(tb + (uint32_t)(8 * t + 2 * rq) * kDropK);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            x[t][4 * rq + e] = drop_keep8(hsh, e, a.thr8) ? x[t][4 * rq + e] : 0.f;
         }
     }
     // O^T[d][q] += V^T[d][key] . P^T[key][q]
@@ -472,7 +475,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;
   const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
-                                    (uint32_t)(2 * hl) * kDropK
+                                    (uint32_t)hl * kDropK
                               : 0u;
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
@@ -610,15 +613,16 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
       }
     }
     if (DROP) {  // dropped P (the 1/(1-p) factor is applied to O once, at the store)
-      const uint32_t tb = dbase + (uint32_t)(k0 >> 1) * kDropK;
+      const uint32_t tb = dbase + (uint32_t)(k0 >> 2) * kDropK;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          // key pair (k0 + 32t + (r&3) + 8(r>>2) + 4hl) >> 1: a literal lattice step
-          const uint32_t hsh = drop_mix(tb + (uint32_t)(16 * t + ((r >> 1) & 1) + 4 * (r >> 2)) * kDropK);
-          x[t][r] = (hsh & 0xffffu) >= a.thr16 ? x[t][r] : 0.f;
-          x[t][r + 1] = (hsh >> 16) >= a.thr16 ? x[t][r + 1] : 0.f;
+        for (int rq = 0; rq < 4; ++rq) {
+          // key quad (k0 + 32t + 8rq + 4hl) >> 2 (keys + r & 3): a literal lattice step
+          const uint32_t hsh = drop_mix(tb + (uint32_t)(8 * t + 2 * rq) * kDropK);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            x[t][4 * rq + e] = drop_keep8(hsh, e, a.thr8) ? x[t][4 * rq + e] : 0.f;
         }
     }
 #pragma unroll
@@ -695,7 +699,7 @@ struct AttnBwdArgs {
   float* D;          // [B][H][lse_stride] rowsum(dO * O)
   int B, H, S, lse_stride;
   float scale, scale_log2;
-  uint32_t thr16;
+  uint32_t thr8;
   float inv_keep;
   uint32_t seed;
   int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
@@ -727,9 +731,9 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
   const int kw0 = kb0 + wid * 32;
   const int key = kw0 + c32;
   const int kk = key < a.S ? key : a.S - 1;
-  // dropout lattice point of (query key & 1, this lane's key pair)
-  const uint32_t kdrop = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)(key >> 1) * kDropK +
-                                    (uint32_t)(key & 1) * kDropQ
+  // dropout lattice point of (query key & 3, this lane's key quad)
+  const uint32_t kdrop = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)(key >> 2) * kDropK +
+                                    (uint32_t)(key & 3) * kDropQ
                               : 0u;
   const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
   const T* dO = static_cast<const T*>(a.dout) + b * a.dsb + hh * a.dsh;
@@ -831,26 +835,24 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
         const float4 dd = *reinterpret_cast<const float4*>(st_D + li);
         const float lsev[4] = {lv.x, lv.y, lv.z, lv.w};
         const float Dv[4] = {dd.x, dd.y, dd.z, dd.w};
-        // keep bits: one hash covers a (query, key pair); the lanes of a key pair
-        // (lane ^ 1) each hash every other query and swap the results over DPP
-        // (quad_perm [1,0,3,2]), so a lane computes 2 hashes per 4 queries, not 4
+        // keep bits: one hash covers a (query, key quad); the 4 lanes of a key quad
+        // each hash one of the group's 4 queries (query li + (key & 3)) and read the
+        // other three over DPP (quad_perm broadcast of lane e), so a lane computes ONE
+        // hash per 4 queries
         uint32_t hq[4];
         if (DROP) {
           const uint32_t qhb = kdrop + (uint32_t)(q0 + 32 * h + 4 * hl) * kDropQ;
-#pragma unroll
-          for (int pr = 0; pr < 2; ++pr) {
-            // query q0 + li + 2pr + (key & 1): a literal lattice step from qhb
-            const uint32_t v = drop_mix(qhb + (uint32_t)(8 * g + 2 * pr) * kDropQ);
-            const uint32_t w = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-            hq[2 * pr] = (key & 1) ? w : v;
-            hq[2 * pr + 1] = (key & 1) ? v : w;
-          }
+          const uint32_t v = drop_mix(qhb + (uint32_t)(8 * g) * kDropQ);
+          hq[0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
+          hq[1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xF, 0xF, false);
+          hq[2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, false);
+          hq[3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, false);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
           bool keep = true;
-          if (DROP) keep = drop_keep(hq[e], key, a.thr16);
+          if (DROP) keep = drop_keep8(hq[e], key & 3, a.thr8);
           float p = fexp2(fmaf(sc[r], a.scale_log2, -lsev[e]));
           // dropped dP scaled by 1/(1-p); the dropped P feeding dV^T is left unscaled
           // (the factor is applied to dV once, at the store)
@@ -935,7 +937,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   const int q = qb0 + wid * 32 + c32;
   const int qq = q < a.S ? q : a.S - 1;
   const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
-                                    (uint32_t)(2 * hl) * kDropK
+                                    (uint32_t)hl * kDropK
                               : 0u;
   const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
   const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
@@ -1045,7 +1047,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
     const unsigned char* Vr = base + 2 * IMG;
     const int k0 = kt * kAKT;
     if (CAUSAL && k0 > qb0 + wid * 32 + 31) continue;
-    const uint32_t tb = dbase + (uint32_t)(k0 >> 1) * kDropK;
+    const uint32_t tb = dbase + (uint32_t)(k0 >> 2) * kDropK;
     // stages of one 32-key half t: S^T / dP^T products, dS^T, mask, dQ^T product
     auto sdp = [&](int t, f32x16_t& sc, f32x16_t& dp) {
 #pragma unroll
@@ -1058,15 +1060,17 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
     };
     auto dsoft = [&](int t, f32x16_t& sc, const f32x16_t& dp) {
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        float dp0 = dp[r], dp1 = dp[r + 1];
-        if (DROP) {
-          const uint32_t hsh = drop_mix(tb + (uint32_t)(16 * t + ((r >> 1) & 1) + 4 * (r >> 2)) * kDropK);
-          dp0 = (hsh & 0xffffu) >= a.thr16 ? dp0 * a.inv_keep : 0.f;
-          dp1 = (hsh >> 16) >= a.thr16 ? dp1 * a.inv_keep : 0.f;
+      for (int rq = 0; rq < 4; ++rq) {
+        uint32_t hsh = 0;
+        // key quad (k0 + 32t + 8rq + 4hl) >> 2: a literal lattice step
+        if (DROP) hsh = drop_mix(tb + (uint32_t)(8 * t + 2 * rq) * kDropK);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * rq + e;
+          float dpr = dp[r];
+          if (DROP) dpr = drop_keep8(hsh, e, a.thr8) ? dpr * a.inv_keep : 0.f;
+          sc[r] = fexp2(fmaf(sc[r], a.scale_log2, -lse_q)) * (dpr - D_q);
         }
-        sc[r] = fexp2(fmaf(sc[r], a.scale_log2, -lse_q)) * (dp0 - D_q);
-        sc[r + 1] = fexp2(fmaf(sc[r + 1], a.scale_log2, -lse_q)) * (dp1 - D_q);
       }
     };
     auto mask = [&](int t, f32x16_t& sc) {
@@ -1110,6 +1114,14 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
                 a.scale);
 }
 
+// host: the byte threshold of a dropout rate (round(256 p); p >= 255.5 / 256 drops all)
+static uint32_t drop_thr8(float p) {
+  if (!(p > 0.f)) return 0u;
+  const float t = p * 256.f + 0.5f;
+  return t >= 256.f ? 256u : (uint32_t)t;
+}
+
+
 }  // namespace
 
 int attn_lse_stride(int S) { return (S + kAKT - 1) / kAKT * kAKT; }
@@ -1123,13 +1135,13 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   a.o = L.o; a.lse = L.lse; a.B = L.B; a.H = L.H; a.S = L.S;
   a.lse_stride = L.lse_stride;
   a.scale_log2 = L.scale * 1.4426950408889634f;
-  a.thr16 = L.dropout > 0.f ? (uint32_t)(L.dropout * 65536.f + 0.5f) : 0u;
-  a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
+  a.thr8 = drop_thr8(L.dropout);
+  a.inv_keep = a.thr8 >= 256u ? 0.f : 256.f / (256.f - (float)a.thr8);
   a.seed = L.seed;
   a.base = attn_base_flag();
   a.addr64 = attn_addr64_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
-  const bool drop = a.thr16 != 0;
+  const bool drop = a.thr8 != 0;
   const bool v2 = !a.base && attn_fwd_variant() == 2;
 #define FWD1(T)                                                                                \
   if (L.causal) {                                                                              \
@@ -1176,13 +1188,13 @@ void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
   a.B = L.B; a.H = L.H; a.S = L.S;
   a.scale = L.scale;
   a.scale_log2 = L.scale * 1.4426950408889634f;
-  a.thr16 = L.dropout > 0.f ? (uint32_t)(L.dropout * 65536.f + 0.5f) : 0u;
-  a.inv_keep = L.dropout > 0.f ? 65536.f / (65536.f - (float)a.thr16) : 1.f;
+  a.thr8 = drop_thr8(L.dropout);
+  a.inv_keep = a.thr8 >= 256u ? 0.f : 256.f / (256.f - (float)a.thr8);
   a.seed = L.seed;
   a.base = attn_base_flag();
   a.addr64 = attn_addr64_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
-  const bool drop = a.thr16 != 0;
+  const bool drop = a.thr8 != 0;
   const bool dq_il = attn_dq_interleave();
 #define DQ_LAUNCH(T, C, D)                                                                     \
   if (dq_il) hipLaunchKernelGGL((attn_bwd_dq_k<T, C, D, true>), grid, block, 0, st, a);          \

@@ -36,21 +36,10 @@ def _umul24(x, c):
 
 def drop_keep_mask(B, H, S, seed, p):
     """[B, H, S(q), S(k)] keep mask of the kernels' hash (int64 torch arithmetic):
-    drop_mix(drop_base(seed, bh) + q * kDropQ + (key >> 1) * kDropK), low 16 bits for
-    even keys, high 16 for odd ones (csrc/hip/attention.hip)."""
-    thr = int(p * 65536 + 0.5)
-    bh = torch.arange(B * H, dtype=torch.int64).view(B, H, 1, 1)
-    q = torch.arange(S, dtype=torch.int64).view(1, 1, S, 1)
-    key = torch.arange(S, dtype=torch.int64).view(1, 1, 1, S)
-    base = _murmur32((seed ^ _mul32(bh, 0x9E3779B1)) & M32)
-    x = (base + _mul32(q, 0x85EBCA77) + _mul32(key >> 1, 0xC2B2AE3D)) & M32
-    x = x ^ (x >> 16)
-    x = _umul24(x, 0xE9846B) ^ (x >> 24)
-    x = x ^ (x >> 13)
-    x = _umul24(x, 0x8B3C2D) ^ (x >> 24)
-    x = x ^ (x >> 16)
-    v = torch.where((key & 1) == 1, x >> 16, x & 0xFFFF)
-    return (v >= thr), 65536.0 / (65536 - thr)
+    drop_mix(drop_base(seed, bh) + q * kDropQ + (key >> 2) * kDropK), byte (key & 3)
+    against round(256 p) (csrc/hip/attention.hip)."""
+    from dropout_hash import keep_mask
+    return keep_mask(B, H, S, seed, p)
 
 
 def ref_attention(q, k, v, causal, p=0.0, seed=0):
