@@ -470,7 +470,80 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   // 4-wave forms on a 2- or 3-deep ring: both k-steps' fragments read ahead, DMA pieces
   // between the MFMA rows (CONV_INTERLEAVE=0 at build time: the burst form, for A/B)
   constexpr bool interleave = CONV_INTERLEAVE != 0;
-  if constexpr (CT == 512 && NB == 3 && BK == 64) {
+  if constexpr (CT == kCT && NB == 4 && BK == 32) {
+    // Pipelined 4-wave form (APEX_AMD_CONV_PIPE): 32-deep K-tiles (one k-step) on a
+    // 4-deep ring, ONE barrier per K-tile, fragments register double-buffered.  Step kt
+    // multiplies F(kt) from registers while it reads F(kt+1) from the ring in the order
+    // the next step's MFMA rows consume them (B fragments, then A row by row: every
+    // counted lgkmcnt covers reads issued >= 2 rows earlier) and issues tile kt+3's DMA
+    // pieces between the MFMA rows.  Tile kt+3 goes to slot (kt+3) % 4 = (kt-1) % 4,
+    // whose tile every wave finished reading in step kt-2 (retired by the lgkmcnt(0) in
+    // front of step kt-1's barrier); the counted vmcnt(G) at the top of step kt leaves
+    // tile kt+2 in flight and retires tile kt+1, which the barrier then publishes to
+    // every wave's reads.  Tiles past the end re-fetch the last tile into the free slot
+    // (every step issues G pieces: the counted waits stay exact).  The burst form above
+    // read each K-tile's fragments right before its MFMAs and waited for them (PMC: 28 %
+    // MFMA busy, 32 % of wave cycles in s_waitcnt / s_barrier, docs/PERF.md round 4).
+    static_assert(KS == 1, "one k-step per K-tile");
+    if (KT > 0) {
+      auto tile_at = [&](int kt_) {  // data of tile min(kt_, KT-1), slot kt_ % NB
+        TileSrc t = tile_src(kt_ < KT ? kt_ : KT - 1);
+        t.A = lds + (kt_ % NB) * BUF;
+        return t;
+      };
+      constexpr int NR = FM + FN;               // fragment reads per step
+      constexpr int RPG = (NR + FM - 1) / FM;   // reads per MFMA row group
+      constexpr int PPG = (G + FM - 1) / FM;    // DMA pieces per MFMA row group
+      // n-th read of a step: B0 .. B(FN-1), then A0 .. A(FM-1)
+      auto rd1 = [&](int kt_, int n, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
+        const unsigned char* A = lds + (kt_ % NB) * BUF;
+        if (n < FN) {
+          bfr[n] = *reinterpret_cast<const bf16x8*>(A + A_BYTES + swzr<RB>(wn * TN + n * 16 + fr, fg));
+        } else {
+          const int i = n - FN;
+          af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, fg));
+        }
+      };
+#pragma unroll
+      for (int p = 0; p < NB - 1; ++p) {
+        const TileSrc t = tile_at(p);
+#pragma unroll
+        for (int q = 0; q < G; ++q) piece(t, q);
+      }
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      rd(0, 0, fa0, fb0);
+      auto step = [&](int kt_, bf16x8 (&ca)[FM], bf16x8 (&cb)[FN], bf16x8 (&na)[FM],
+                      bf16x8 (&nb)[FN]) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const TileSrc tn = tile_at(kt_ + NB - 1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i], cb[j], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < RPG; ++u)
+            if (i * RPG + u < NR) rd1(kt_ + 1, i * RPG + u, na, nb);
+#pragma unroll
+          for (int u = 0; u < PPG; ++u)
+            if (i * PPG + u < G) piece(tn, i * PPG + u);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      for (int kt = 0; kt < KT; kt += 2) {
+        step(kt, fa0, fb0, fa1, fb1);
+        if (kt + 1 < KT) step(kt + 1, fa1, fb1, fa0, fb0);
+      }
+      // the re-fetches past the end write the ring, which the epilogue reuses
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else if constexpr (CT == 512 && NB == 3 && BK == 64) {
     // 8-wave form: ONE barrier per K-tile.  Phase A multiplies k-step 0 of tile kt from
     // registers while it reads k-step 1's fragments and issues the last PA DMA pieces of
     // tile kt+2 between the MFMA rows; phase B waits for tile kt+1 (vmcnt(G) leaves all
@@ -765,6 +838,22 @@ static bool conv_bk32(unsigned wgs) {
   if (e && e[0] == '1') return true;
   return wgs >= 1024;
 }
+// 1x1 data gradients with the BN-backward epilogue over >= 50,176 output pixels
+// (ResNet-50 layers 1-3): 64-row M tiles (APEX_AMD_BNBWD_BM64 = 0 | 1, read per launch).
+// The per-call table of the serialized step (profiles/r5/conv_calls.md) has these at
+// 2.8-3.5 TB/s of epilogue traffic: the K loop is 1-4 K-tiles, the rest is the epilogue's
+// loads and stores, streamed by only 2 workgroups per CU with 128-row tiles.
+static bool bnbwd_bm64(int ksize, int NC, int64_t M) {
+  const char* e = std::getenv("APEX_AMD_BNBWD_BM64");
+  const bool on = e ? e[0] == '1' : false;
+  return on && ksize == 1 && NC % 128 == 0 && M >= 50176;
+}
+// the pipelined 4-deep-ring K loop for the 32-deep forms (conv_tap_k NB = 4;
+// APEX_AMD_CONV_PIPE = 0 | 1, read per launch)
+static bool conv_pipe() {
+  const char* e = std::getenv("APEX_AMD_CONV_PIPE");
+  return e ? e[0] == '1' : false;
+}
 // the 64-wide-tile form (APEX_AMD_CONV_BK32_64 = 0 | 1, default on): layer-1 3x3 64@56
 // 111.1 -> 105.6 us fwd, 102.7 -> 99.4 us dgrad; ResNet-50 same box, two runs each:
 // 10,357 / 10,359 img/s (no BK = 32), 10,490 / 10,563 (128-wide tiles only), 10,564 /
@@ -819,19 +908,30 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  } else if (EPI == 1 && MODE == kFwd1 && bnbwd_bm64(1, g.NC, g.M)) {
+    // memory-bound BN-backward epilogues: 64-row M tiles (36 KB of LDS, up to 4
+    // workgroups per CU: twice the waves streaming the epilogue's residual / BN-input
+    // loads and the gradient stores)
+    const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= conv1x1_nb1_max_kt()) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    if (conv_bk32(grid.x * grid.y * grid.z))
+    if (conv_bk32(grid.x * grid.y * grid.z) && conv_pipe())
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 4, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    else if (conv_bk32(grid.x * grid.y * grid.z))
       hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (conv_bk32_64() && !(EPI == 1 && !bnbwd_nb2())) {
     // 64-wide tiles with 32-deep K-tiles on a 3-deep ring (36 KB of LDS)
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    if (conv_pipe())
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 4, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    else
+      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if ((EPI == 1 && bnbwd_nb2()) || (EPI == 0 && conv64_nb2())) {
     // BN-backward epilogue on 64-wide tiles: a 2-deep ring (48 KB of LDS -> 3 workgroups
     // per CU instead of 2), so more K loops run under each workgroup's epilogue reads
@@ -1749,6 +1849,10 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
   else launch_conv_tap<kFwd1>(xp, wp, yp, g, st, stats_slab, stats_shift);
 }
 
+int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize) {
+  const int64_t M = (int64_t)N * H * W;
+  return bnbwd_bm64(ksize, Cout, M) ? (int)((M + 63) / 64) : conv_fwd_mtiles(N, H, W, Cout, 1);
+}
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H, int W, int Cin,
                          int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,
                          hipStream_t st) {

@@ -304,6 +304,8 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
                    int ksize, int stride, hipStream_t st, float* stats_slab = nullptr,
                    const float* stats_shift = nullptr);
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride);
+// M tiles (slab rows) of conv_nhwc_fwd_bnbwd's stride-1 launch
+int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize);
 // BatchNorm-backward epilogue of a data-gradient conv (conv_nhwc_fwd on dY with the
 // rotated / transposed filter): the conv output o (+ add, the residual gradient) is
 // the gradient of a BN(+ReLU) output; the kernel stores g = relu_mask(x) * o instead

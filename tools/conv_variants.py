@@ -43,9 +43,13 @@ def _select(v):
     4-wave K loop with each tile's DMA as one burst / with read-ahead and DMA pieces
     between the MFMA rows, APEX_AMD_CONV_BURST=1 / 0)"""
     for k in ("APEX_AMD_CONV_BM", "APEX_AMD_CONV_BURST", "APEX_AMD_CONV_BK32",
-              "APEX_AMD_CONV_BK32_64"):
+              "APEX_AMD_CONV_BK32_64", "APEX_AMD_CONV_PIPE"):
         os.environ.pop(k, None)
-    if v in ("bk32on", "bk32off"):  # the auto BK = 32 choice forced on / off
+    if v in ("pipe", "pipebk32"):  # the pipelined 4-deep-ring K loop (+ on every grid)
+        os.environ["APEX_AMD_CONV_PIPE"] = "1"
+        if v == "pipebk32":
+            os.environ["APEX_AMD_CONV_BK32"] = "1"
+    elif v in ("bk32on", "bk32off"):  # the auto BK = 32 choice forced on / off
         os.environ["APEX_AMD_CONV_BK32"] = "1" if v == "bk32on" else "0"
     elif v == "bk32w64":  # the 64-wide-tile BK = 32 form
         os.environ["APEX_AMD_CONV_BK32_64"] = "1"

@@ -89,9 +89,9 @@ def main(argv=None):
                     continue
                 name = row.get("Kernel_Name", "?")
                 if a.dispatch_filter and re.search(a.dispatch_filter, name):
-                    disp.append((s, _short(name, 60), row.get("Grid_Size_X", ""),
-                                 row.get("Grid_Size_Y", ""), row.get("Workgroup_Size_X", ""),
-                                 (e - s) / 1e3))
+                    disp.append((s, _short(name, 140), row.get("Grid_Size_X", ""),
+                                 row.get("Grid_Size_Y", ""), row.get("Grid_Size_Z", ""),
+                                 row.get("Workgroup_Size_X", ""), (e - s) / 1e3))
                 tot[name] += (e - s) / 1e3  # us
                 cnt[name] += 1
                 if a.gaps:
@@ -138,8 +138,8 @@ def main(argv=None):
                 fh.write("%d\t%.1f\t%s\n" % (cnt[k] // div, v / div, re.sub(r"\s+", " ", k)))
     if a.dispatch_out:
         with open(a.dispatch_out, "w") as fh:
-            for s0, n, gx, gy, wg, us in sorted(disp):
-                fh.write("%s\t%s\t%s\t%s\t%.2f\n" % (n, gx, gy, wg, us))
+            for s0, n, gx, gy, gz, wg, us in sorted(disp):
+                fh.write("%d\t%s\t%s\t%s\t%s\t%s\t%.2f\n" % (s0, n, gx, gy, gz, wg, us))
     return 0
 
 
