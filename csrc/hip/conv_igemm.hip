@@ -842,10 +842,11 @@ static bool conv_bk32(unsigned wgs) {
 // (ResNet-50 layers 1-3): 64-row M tiles (APEX_AMD_BNBWD_BM64 = 0 | 1, read per launch).
 // The per-call table of the serialized step (profiles/r5/conv_calls.md) has these at
 // 2.8-3.5 TB/s of epilogue traffic: the K loop is 1-4 K-tiles, the rest is the epilogue's
-// loads and stores, streamed by only 2 workgroups per CU with 128-row tiles.
+// loads and stores, streamed by only 2 workgroups per CU with 128-row tiles.  Same-box
+// ResNet-50: 11,433 / 11,430 img/s with 64-row tiles vs 11,392 / 11,374 (profiles/r5/).
 static bool bnbwd_bm64(int ksize, int NC, int64_t M) {
   const char* e = std::getenv("APEX_AMD_BNBWD_BM64");
-  const bool on = e ? e[0] == '1' : false;
+  const bool on = e ? e[0] == '1' : true;
   return on && ksize == 1 && NC % 128 == 0 && M >= 50176;
 }
 // the pipelined 4-deep-ring K loop for the 32-deep forms (conv_tap_k NB = 4;
