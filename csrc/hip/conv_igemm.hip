@@ -847,7 +847,17 @@ static bool conv_bk32(unsigned wgs) {
 static bool bnbwd_bm64(int ksize, int NC, int64_t M) {
   const char* e = std::getenv("APEX_AMD_BNBWD_BM64");
   const bool on = e ? e[0] == '1' : true;
-  return on && ksize == 1 && NC % 128 == 0 && M >= 50176;
+  // (an explicit APEX_AMD_CONV_BM tiling takes precedence, as in launch_conv_tap)
+  return on && ksize == 1 && NC % 128 == 0 && M >= 50176 && conv_bm_choice() == 0;
+}
+// the same 64-row tiles for plain stride-1 1x1 forwards / data gradients over >= 200,704
+// output pixels (APEX_AMD_FWD1_BM64 = 0 | 1, read per launch).  Measured slower, so off:
+// ResNet-50 11,203 / 11,176 vs 11,315 / 11,330 img/s same box (profiles/r5/ab_r50_fbm64):
+// these K-light convs already stream at 3.5-3.8 TB/s on 128-row tiles.
+static bool fwd1_bm64(int ksize, int NC, int64_t M) {
+  const char* e = std::getenv("APEX_AMD_FWD1_BM64");
+  const bool on = e ? e[0] == '1' : false;
+  return on && ksize == 1 && NC % 128 == 0 && M >= 200704 && conv_bm_choice() == 0;
 }
 // the pipelined 4-deep-ring K loop for the 32-deep forms (conv_tap_k NB = 4;
 // APEX_AMD_CONV_PIPE = 0 | 1, read per launch)
@@ -909,6 +919,11 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  } else if (EPI == 0 && MODE == kFwd1 && fwd1_bm64(1, g.NC, g.M)) {
+    // memory-bound 1x1 forwards / data gradients on the 56x56 and 28x28 layers: the
+    // same 64-row tiles (up to 4 workgroups per CU)
+    const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (EPI == 1 && MODE == kFwd1 && bnbwd_bm64(1, g.NC, g.M)) {
     // memory-bound BN-backward epilogues: 64-row M tiles (36 KB of LDS, up to 4
     // workgroups per CU: twice the waves streaming the epilogue's residual / BN-input
@@ -1830,9 +1845,10 @@ void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipSt
                      static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin, 1);
 }
 
-int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride) {
+int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t M = (int64_t)N * Ho * Wo;
+  if (fwd1_bm64(ksize, Cout, M)) return (int)((M + 63) / 64);
   const int big = Cout % 128 == 0 ? conv_bm_choice() : 0;  // launch_conv_tap's M tile
   const int bm = conv_bm_of(big);
   return (int)((M + bm - 1) / bm);
@@ -1852,7 +1868,10 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
 
 int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize) {
   const int64_t M = (int64_t)N * H * W;
-  return bnbwd_bm64(ksize, Cout, M) ? (int)((M + 63) / 64) : conv_fwd_mtiles(N, H, W, Cout, 1);
+  if (bnbwd_bm64(ksize, Cout, M)) return (int)((M + 63) / 64);
+  const int big = Cout % 128 == 0 ? conv_bm_choice() : 0;  // launch_conv_tap's M tile
+  const int bm = conv_bm_of(big);
+  return (int)((M + bm - 1) / bm);
 }
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H, int W, int Cin,
                          int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,

@@ -303,7 +303,7 @@ bool conv3x3_nhwc_supported(int Cin, int Cout);
 void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
                    int ksize, int stride, hipStream_t st, float* stats_slab = nullptr,
                    const float* stats_shift = nullptr);
-int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride);
+int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize = 3);
 // M tiles (slab rows) of conv_nhwc_fwd_bnbwd's stride-1 launch
 int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize);
 // BatchNorm-backward epilogue of a data-gradient conv (conv_nhwc_fwd on dY with the

@@ -284,6 +284,8 @@ _VARIANTS = [
     {"APEX_AMD_CONV_PIPE": "1"},                    # pipelined 4-deep ring (32-deep forms)
     {"APEX_AMD_CONV_PIPE": "1", "APEX_AMD_CONV_BK32": "1"},  # ... on every 128-wide grid
     {"APEX_AMD_BNBWD_BM64": "1"},                   # 64-row tiles for BN-bwd 1x1 dgrads
+    {"APEX_AMD_BNBWD_BM64": "0"},                   # ... off
+    {"APEX_AMD_FWD1_BM64": "1"},                    # 64-row tiles for plain 1x1 convs
 ]
 
 
@@ -295,6 +297,7 @@ _VARIANTS = [
     (2, 256, 7, 7, 512, 1),
     (3, 128, 9, 11, 256, 3),    # M = 297: partial last tile
     (1, 128, 224, 226, 256, 1),  # M = 50,624: the 64-row BN-bwd tiles (last tile partial)
+    (4, 64, 224, 226, 128, 1),   # M = 202,496: the 64-row plain 1x1 tiles
 ])
 def test_conv_variants_bitwise_equal(shape, variant, monkeypatch):
     N, Ci, H, W, Co, k = shape
@@ -323,7 +326,8 @@ def test_conv_variants_bitwise_equal(shape, variant, monkeypatch):
     for i, (a, b) in enumerate(zip(ref, got)):
         if i in (2, 4, 6) and (a.shape != b.shape or
                                _VARIANTS[variant].get("APEX_AMD_CONV_BM") == "256w8" or
-                               "APEX_AMD_BNBWD_BM64" in _VARIANTS[variant]):
+                               "APEX_AMD_BNBWD_BM64" in _VARIANTS[variant] or
+                               "APEX_AMD_FWD1_BM64" in _VARIANTS[variant]):
             # statistics slabs hold one row pair per M tile, summed over the tile's row
             # groups: the 8-wave 256-row tiling has half the rows and twice the row
             # groups, so only the per-channel totals compare (fp32 summation order)
