@@ -15,6 +15,7 @@ from torch.nn import init
 from torch.nn.parameter import Parameter
 
 from .. import _native
+from ..ops.conv import gate_side_stream
 
 
 def _n2(normalized_shape):
@@ -44,6 +45,7 @@ class FusedLayerNormAffineFunction(torch.autograd.Function):
         grad_input, grad_weight, grad_bias = C.backward(
             grad_output.contiguous(), input_, mean, invvar, _n2(ctx.normalized_shape), weight_,
             ctx.needs_input_grad[1], ctx.needs_input_grad[2], False)
+        gate_side_stream(grad_input)
         return grad_input, grad_weight, grad_bias, None, None
 
 
@@ -126,6 +128,7 @@ class AddDropoutLayerNormFunction(torch.autograd.Function):
         ds, dh, dw, db = C.add_dropout_backward(dy, s, mean, invvar, n2, weight, ds_ext, p, seed,
                                                 ctx.needs_input_grad[2], ctx.needs_input_grad[3],
                                                 h_dtype)
+        gate_side_stream(ds)
         return ds, dh, dw, db, None, None, None, None
 
 
