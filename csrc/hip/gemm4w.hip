@@ -163,6 +163,11 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   const int ntn = p.N >> 8, mtiles = (p.M + 255) >> 8;
   constexpr bool PERSIST = (VAR & 4) != 0;
   constexpr bool TANH = (VAR & 8) != 0;  // GELU flavour of EPI 1 / 2 (p.tanh)
+  // k-half regions (VAR bit 4): each K-tile slot holds its two 32-deep halves as separate
+  // 64-byte-row regions, so a half is refilled as soon as its k-step's fragments are read
+  // (one barrier per k-step): every DMA piece gets two k-steps of lead instead of one
+  constexpr bool KH = (VAR & 16) != 0;
+  static_assert(!(KH && PERSIST), "k-half regions: one tile per workgroup");
   const int G = PERSIST ? (int)gridDim.x : 0, ntiles = mtiles * ntn;
   const int b = w4_xcd_remap(blockIdx.x, gridDim.x);
   // persistent: tiles b, b + G, ...; otherwise one tile per workgroup (a compile-time 1,
@@ -203,13 +208,26 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   auto set_ld = [&](int r) {  // operand panels of tile r (wave-uniform)
     int m0, n0;
     tile_mn(r, m0, n0);
+    if constexpr (KH) {
+      // 64-byte region rows: lane -> (row + lane/4, physical chunk lane%4), logical chunk
+      // = physical ^ w4_key64(row) (row bit 3 = lane bit 5 for a 16-row piece)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rr = wid * 64 + i * 8 + lrow;
-      const int ch = pch ^ w4_key(i * 8 + lrow);
-      const int ar = min(m0 + rr, p.M - 1) - m0;  // rows past M re-read row M-1
-      offA[i] = (uint32_t)ar * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
-      offB[i] = (uint32_t)rr * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+      for (int i = 0; i < 4; ++i) {
+        const int rr = wid * 64 + i * 16 + (lane >> 2);
+        const int ch = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+        const int ar = min(m0 + rr, p.M - 1) - m0;
+        offA[i] = (uint32_t)ar * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+        offB[i] = (uint32_t)rr * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int rr = wid * 64 + i * 8 + lrow;
+        const int ch = pch ^ w4_key(i * 8 + lrow);
+        const int ar = min(m0 + rr, p.M - 1) - m0;  // rows past M re-read row M-1
+        offA[i] = (uint32_t)ar * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+        offB[i] = (uint32_t)rr * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+      }
     }
     rA = w4_rsrc(static_cast<const TT*>(p.A) + (int64_t)m0 * p.lda, 0xffffffffu);
     rB = w4_rsrc(static_cast<const TT*>(p.B) + (int64_t)n0 * p.ldb, 0xffffffffu);
@@ -235,6 +253,15 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
                                              (__attribute__((address_space(3))) void*)dst, 16,
                                              q < 8 ? offA[q] : offB[q - 8], ld_kb, 0, 0);
   };
+  // KH: piece q (0..7: A rows i = q, then B rows i = q - 4, 16 rows each) of k-half h of
+  // K-tile T into region (slot T & 1, half h, operand)
+  auto piece_h = [&](int T, int h, int q) {
+    const int o = q >> 2, i = q & 3;
+    unsigned char* dst = lds + (T & 1) * kW4Slot + h * kW4Op + o * (kW4Op / 2) + wid * 4096 + i * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(o == 0 ? rA : rB,
+                                             (__attribute__((address_space(3))) void*)dst, 16,
+                                             o == 0 ? offA[i] : offB[i], ld_kb + h * 64, 0, 0);
+  };
 
   // fragment reads: A row wm*128 + i*16 + fr; B row w4_brow; logical chunk ks*4 + fg;
   // the key depends on the fragment's parity (row bit 4 for A, the +4 for B)
@@ -255,7 +282,25 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   // groups earlier (in natural order B4-7 came last and stalled every k-step's start).
   auto rd_order = [](int n) { return n < 4 ? 8 + n : n == 4 ? 0 : n < 9 ? 7 + n : n - 8; };
   // read one fragment (r < 8: A[r], else B[r - 8]) of k-step ks of the tile in `slot`
+  // KH region reads: 64-byte rows, key w4_key64 = row bit 3 (x 2); for the A rows
+  // (i*16 + fr) and the permuted B rows (w4_brow) it is ((fr >> 2) & 2) / ((fr >> 2) & 1) * 2
+  const int offKA = fr * 64 + ((fg ^ ((fr >> 2) & 2)) << 4);
+  int offKB[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par)
+    offKB[par] = w4_brow(par, fr) * 64 + ((fg ^ (((fr >> 2) & 1) << 1)) << 4);
   auto rd = [&](int slot, int ks, int r, v8(&fa)[8], v8(&fb)[8]) {
+    if constexpr (KH) {
+      const unsigned char* base = lds + slot * kW4Slot + ks * kW4Op;
+      if (r < 8) {
+        fa[r] = *reinterpret_cast<const v8*>(base + offKA + (wm * 128 + r * 16) * 64);
+      } else {
+        const int j = r - 8;
+        fb[j] = *reinterpret_cast<const v8*>(base + kW4Op / 2 + offKB[j & 1] +
+                                             (wn * 128 + (j >> 1) * 32) * 64);
+      }
+      return;
+    }
     const unsigned char* base = lds + slot * kW4Slot;
     if (r < 8) {
       fa[r] = *reinterpret_cast<const v8*>(base + offRA[ks][r & 1] + (wm * 128 + (r & 6) * 16) * 128);
@@ -385,15 +430,30 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
     }
   };
 
-  // prologue: K-tiles 0 and 1 in flight, wait for K-tile 0, read its k-step-0 fragments
+  // prologue: K-tiles 0 and 1 in flight, wait for K-tile 0 (KH: its k-half 0), read its
+  // k-step-0 fragments
   set_ld(0);
+  if constexpr (KH) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) piece(0, q);
-  ld_next();
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-  for (int q = 0; q < 16; ++q) piece(1, q);
-  ld_next();  // the cursor now names K-tile 2 (issued by k-step 1 of K-tile 0)
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      for (int q = 0; q < 8; ++q) piece_h(0, h, q);
+    ld_next();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) piece_h(1, h, q);
+    ld_next();
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) piece(0, q);
+    ld_next();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) piece(1, q);
+    ld_next();  // the cursor now names K-tile 2 (issued by k-step 1 of K-tile 0)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
   w4_barrier();
 #pragma unroll
   for (int r = 0; r < 16; ++r) rd(0, 0, rd_order(r), fa0, fb0);
@@ -416,6 +476,13 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   auto ktile = [&](int t, auto first_c, bool stores_behind) {
     constexpr bool FIRST = decltype(first_c)::value;
     const int slot = t & 1;
+    if constexpr (KH) {
+      // k-step 0: k-half 1 of this K-tile landed (vmcnt(16) leaves K-tile t+1's two
+      // halves in flight), every wave's k-half-0 reads of this slot retired -> refill it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      w4_barrier();
+    }
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       if constexpr (FIRST) {
@@ -430,13 +497,20 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
         rd(slot, 1, rd_order(2 * g), fa1, fb1);
         rd(slot, 1, rd_order(2 * g + 1), fa1, fb1);
       }
+      if constexpr (KH) {
+        if (g & 1) piece_h(t + 2, 0, g >> 1);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     // k-step 1: K-tile t+1 must have landed (every wave's DMA: vmcnt + barrier; the
     // previous tile's epilogue stores, issued after it, may stay in flight), and every
     // wave's reads of this slot are retired before K-tile t+2's DMA overwrites it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (stores_behind) {
+    if constexpr (KH) {
+      // k-half 0 of K-tile t+1 landed (K-tile t+1's k-half 1 and K-tile t+2's k-half 0 stay
+      // in flight); every wave's k-half-1 reads of this slot retired -> refill it
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else if (stores_behind) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiStores) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -452,7 +526,9 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
         rd(slot ^ 1, 0, rd_order(2 * g), fa0, fb0);
         rd(slot ^ 1, 0, rd_order(2 * g + 1), fa0, fb0);
       }
-      if constexpr ((VAR & 1) == 0) {
+      if constexpr (KH) {
+        if (g & 1) piece_h(t + 2, 1, g >> 1);
+      } else if constexpr ((VAR & 1) == 0) {
         piece(t + 2, g);
       } else if (g < 8) {
         piece(t + 2, 2 * g);
@@ -540,6 +616,8 @@ void gemm4w(const G8Args& a0, int epi, hipStream_t st) {
       case 1: launch(t0, std::integral_constant<int, 1>{}); break;
       case 6: launch(t0, std::integral_constant<int, 6>{}); break;
       case 2: launch(t0, std::integral_constant<int, 2>{}); break;
+      case 16: launch(t0, std::integral_constant<int, 16>{}); break;
+      case 18: launch(t0, std::integral_constant<int, 18>{}); break;
       default: launch(t0, std::integral_constant<int, 0>{}); break;
     }
   };
