@@ -45,9 +45,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # vs_baseline: BASELINE.md publishes no number for the reference; the comparator
-# is the stock PyTorch-ROCm path measured on MI355X with this same harness
-# (BASELINE.md section 2), per GPU, bs 256.
-STOCK_BASELINE_PER_GPU = {"resnet50": 6011.4}
+# is the stock PyTorch-ROCm path (bench.py --impl stock: torch.optim.SGD, PyTorch
+# BatchNorm, MIOpen convs, torch.autocast bf16) measured on MI355X with this same
+# harness, per GPU, bs 256.  Re-measured in round 5 on the headline's box, two runs each
+# (profiles/r5/stock/): stock 5,983.5 / 5,985.6 img/s, this path 11,263.0 / 11,259.0
+# (round 1/2: 6,011.4).
+STOCK_BASELINE_PER_GPU = {"resnet50": 5984.5}
 
 
 def parse():
@@ -76,8 +79,9 @@ def parse():
     ap.add_argument("--no-syncbn", action="store_true",
                     help="per-GPU BatchNorm statistics at N > 1 (not the BASELINE config)")
     ap.add_argument("--message-size", default="auto",
-                    help="DDP bucket elements, or 'auto' = 32 MiB on the wire (the xGMI sizing "
-                         "model of parallel/distributed.py, docs/DDP_TUNING.md)")
+                    help="DDP bucket elements, or 'auto': at N > 1 calibrated from timed "
+                         "all-reduces on the bucket communicator (power of two in [8, 64] MiB, "
+                         "parallel/distributed.py, docs/DDP_TUNING.md); 32 MiB at N = 1")
     ap.add_argument("--force-collectives", action="store_true",
                     help="1 GPU: run the N>1 code path anyway - apex DDP (+ SyncBN for ResNet) "
                          "with every bucket all-reduce and SyncBN all_gather / all_reduce "
