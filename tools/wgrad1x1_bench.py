@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""1x1 weight gradients of ResNet-50 (batch 256): the default split-K hipBLASLt path
+(`ops.conv.wgrad_1x1`, fp32 partials + one native slab reduction) at its own split count
+and at forced larger splits, against the own MFMA tap kernel (`conv.conv_wgrad`,
+ksize 1).  Correctness against an fp32 reference first, then interleaved timing rounds
+in one process (so every row compares on the same box and clocks)."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+# (cin, cout, hw, stride, calls per ResNet-50 step)
+SHAPES = [(64, 64, 56, 1, 1), (64, 256, 56, 1, 4), (256, 64, 56, 1, 2), (256, 128, 56, 1, 1),
+          (128, 512, 28, 1, 4), (512, 128, 28, 1, 3), (512, 256, 28, 1, 1),
+          (256, 1024, 14, 1, 6), (1024, 256, 14, 1, 5), (1024, 512, 14, 1, 1),
+          (512, 2048, 7, 1, 3), (2048, 512, 7, 1, 2)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--splits", default="256,512")
+    args = ap.parse_args()
+    from apex_example_amd import _native
+    from apex_example_amd.ops import conv as C
+
+    cv = _native.require().conv
+    dev = "cuda"
+    splits = [int(s) for s in args.splits.split(",") if s]
+
+    def forced(dyr, xr, s):
+        m, co = dyr.shape
+        ci = xr.shape[1]
+        a = dyr.view(s, m // s, co).transpose(1, 2)
+        b = xr.view(s, m // s, ci)
+        part = torch.bmm(a, b, out_dtype=torch.float32)
+        return cv.splitk_reduce(part, torch.bfloat16, None, True)
+
+    rows = []
+    for (ci, co, hw, st, calls) in SHAPES:
+        n = args.batch
+        g = torch.Generator(device=dev).manual_seed(ci * 7 + co)
+        x = torch.randn(n, ci, hw, hw, device=dev, generator=g).to(
+            torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dy = torch.randn(n, co, hw, hw, device=dev, generator=g).to(
+            torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        xr, dyr = C._as_rows(x), C._as_rows(dy)
+        m = xr.shape[0]
+        ref = (dyr.float().t() @ xr.float())
+        scale = float(ref.abs().max())
+        cands = {"splitk(S=%d)" % C._split_k(m): lambda: C.wgrad_1x1(dyr, xr, torch.bfloat16)}
+        for s in splits:
+            if m % s == 0 and s != C._split_k(m):
+                cands["splitk(S=%d)" % s] = (lambda s=s: forced(dyr, xr, s))
+        cands["own tap"] = lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0, 1, 1)
+        for name, fn in cands.items():
+            out = fn().float().reshape(co, ci)
+            err = float((out - ref).abs().max()) / scale
+            print("check %d->%d @%d %s: rel err %.2e" % (ci, co, hw, name, err), flush=True)
+            assert err < 2e-2, (name, err)
+        times = {k: [] for k in cands}
+        for _ in range(args.rounds):
+            for k, fn in cands.items():
+                times[k].append(timeit(fn))
+        best = {k: min(v) for k, v in times.items()}
+        gf = 2.0 * m * ci * co / 1e9
+        rows.append((ci, co, hw, calls, gf, best))
+        print("| 1x1 %d->%d @%d | %d | %.1f | %s |" % (
+            ci, co, hw, calls, gf, " | ".join("%s %.1f us (%.0f TF)" % (k, t, gf / t * 1e3)
+                                              for k, t in best.items())), flush=True)
+    tot_def = sum(r[3] * list(r[5].values())[0] for r in rows)
+    tot_best = sum(r[3] * min(r[5].values()) for r in rows)
+    print("weighted per step: default %.0f us, best-of %.0f us" % (tot_def, tot_best))
+
+
+if __name__ == "__main__":
+    main()
