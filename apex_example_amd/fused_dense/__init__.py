@@ -153,6 +153,44 @@ def _splitk_chunks(T, o, i, in_dtype, out_dtype):
 _ADDMM_F32 = os.environ.get("APEX_AMD_ADDMM_F32", "1") == "1"
 
 
+# Dense weight gradients on the own transposed-operand MFMA kernel (csrc/hip/wgrad4w.hip):
+# fp32 partials per row split + the slab reduction, for weights with both dimensions
+# multiples of 256.  Opt-in (APEX_AMD_DENSE_W4W=1): measured slower than the hipBLASLt
+# split-K path (BERT FFN 239 vs 146 us, profiles/r5/wgrad_dense.md) - its K loop waits on
+# the operand DMA two thirds of the time (PMC SQ_WAIT_ANY 66 %, TA stalled by TC).
+_DENSE_W4W = os.environ.get("APEX_AMD_DENSE_W4W", "0") == "1"
+
+
+def _w4w_splits(T, o, i):
+    """Row splits for wgrad4w: the largest power of two with splits x tiles <= 256 (one
+    256 x 256 tile per CU), at least 1024 rows (16 K-tiles) per split."""
+    tiles = (o // 256) * (i // 256)
+    S = 1
+    while 2 * S * tiles <= 256 and T % (2 * S * 64) == 0 and T // (2 * S) >= 1024:
+        S *= 2
+    return S
+
+
+def _wgrad_w4w(dy2, x2, dtype, out, accumulate):
+    """wgrad4w when the shapes / dtypes fit, else None."""
+    if not (_DENSE_W4W and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
+            and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
+            and _native.available()):
+        return None
+    T, o = dy2.shape
+    i = x2.shape[1]
+    if o % 256 or i % 256:
+        return None
+    dn = _native.require().dense
+    S = _w4w_splits(T, o, i)
+    if not dn.wgrad4w_ok(dy2, x2, S):
+        return None
+    if out is not None and not out.is_contiguous():
+        return None
+    r = dn.wgrad4w(dy2, x2, S, dtype, out=out, accumulate=accumulate)
+    return out if out is not None else r
+
+
 def _wgrad(dy2, x2, dtype, out=None, accumulate=True):
     """dW = dy2^T x2 written in the parameter's dtype by the GEMM itself (amp O1:
     fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW); split-K over
@@ -160,6 +198,9 @@ def _wgrad(dy2, x2, dtype, out=None, accumulate=True):
     into that [o, i]-contiguous tensor (a DDP bucket view, see _direct_slots) and
     return it - the slab reduction or the GEMM's beta = 1 does the add; with
     ``accumulate=False`` (a lazily zeroed bucket view) overwrite it (beta = 0)."""
+    got = _wgrad_w4w(dy2, x2, dtype, out, accumulate)
+    if got is not None:
+        return got
     if (_DENSE_SPLITK and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
             and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
             and _native.available()):

@@ -1,0 +1,348 @@
+// Weight gradients of the dense layers on the gfx950 matrix cores, one wave per SIMD:
+//
+//   P[s][m][n] = sum over rows k of split s of  A[k][m] * B[k][n]
+//
+// with A = dY [T, M] and B = X [T, N] both stored ROW-major over the token dimension T
+// (dW = dY^T X, the reduction runs down the columns of both operands).  fp32 partials per
+// split s, summed by the slab reduction (splitk_reduce) that also writes the weight dtype.
+//
+// Why: hipBLASLt's split-K batched GEMM tops out near 1.0 PF on these shapes (BERT-large
+// 4096 x 1024 x 16384: 137 us at its best split, TunableOp's online search included,
+// profiles/r5/wgrad_dense.md), while the same tile / K structure in the TN layout runs at
+// 1.43 PF on gemm4w.hip.  This kernel is gemm4w's K loop (256 x 256 workgroup tile, 4
+// waves of 128 x 128 fp32 accumulators, 64-deep K-tiles on a 2-deep LDS ring, buffer-
+// descriptor LDS DMA, fragments of the next k-step read under the current MFMAs, one
+// barrier per k-step) with operands that arrive K-major: the MFMA fragments (8
+// consecutive k of one column per lane) come from ds_read_b64_tr_b16 transposed reads.
+//
+// LDS image of one operand K-tile (64 rows k x 256 columns, 32 KB): 32 blocks of 1 KB,
+// block (row group r >> 4, chunk group c >> 2) holds 16 rows x 4 16-byte chunks, row-major
+// inside the block with the chunk index XORed by 2 on odd 8-row halves:
+//
+//   byte(r, c) = ((r >> 4) * 8 + (c >> 2)) * 1024 + ((r & 15) * 4 + ((c & 3) ^ (((r >> 3) & 1) << 1))) * 16
+//
+// One DMA wave-instruction fills one block (lanes 4 i .. 4 i + 3 read 64 contiguous bytes
+// of row i: coalesced), and every 32-lane half of a transposed fragment read (rows
+// kb .. kb+3 and kb+8 .. kb+11 of two chunks) lands on 16 distinct 16-byte bank slots:
+// conflict-free (MI355X_MICROARCH.md LDS table: ds_read_b64_tr_b16 banks per 32 lanes).
+//
+// The MFMA takes the X fragment as its first operand, so the accumulator lane (fr, fg)
+// holds 4 CONSECUTIVE n of one m: one 16-byte fp32 store each.
+//
+// Three DMA / LDS layouts (template L, APEX_AMD_W4W_LAYOUT): 0 = the 16-row x 64-byte
+// blocks above; 1 = 8-row x 128-byte blocks (chunk key 2 (r >> 1 & 1) + 4 (r >> 3 & 1));
+// 2 = whole 512-byte rows, two per DMA instruction (chunk key 2 ((r & 3) | (r >> 3 & 1) << 2)).
+// All three read conflict-free and are bitwise equal (tests/test_wgrad4w_gpu.py).
+//
+// Status (round 5, profiles/r5/wgrad_dense.md): correct, but 1.6x SLOWER than the hipBLASLt
+// path on the BERT / GPT-2 shapes (FFN 239 us vs 146 us at layout 0, 318 / 347 us at 2 / 1),
+// so fused_dense keeps it opt-in (APEX_AMD_DENSE_W4W=1).  The time per K-tile does not
+// depend on how many workgroups run (32 or 256), and PMC shows 66 % of wave cycles in
+// s_waitcnt and the texture addresser stalled by the L1 (TA_ADDR_STALLED_BY_TC 2.5 M vs 0
+// for hipBLASLt): with one 64-row K-tile of DMA lead the loop is latency-bound on operand
+// rows that change every K-tile (the TN form re-reads the same 256 rows at the next 128
+// bytes); a deeper ring than 128 KB of LDS allows is the open fix.
+//
+// M % 256 == 0, N % 256 == 0, rows per split % 64 == 0.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "amd_dev.h"
+#include "amd_kernels.h"
+
+namespace amd {
+
+namespace {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int uint4_t __attribute__((ext_vector_type(4)));
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+constexpr int kWwT = 256;            // threads: 4 waves, one per SIMD
+constexpr int kWwOp = 32768;         // one operand of one K-tile
+constexpr int kWwSlot = 2 * kWwOp;   // A + B
+
+__device__ __forceinline__ void ww_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int ww_xcd_remap(int bid, int nwg) {
+  const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / 8;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ww_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+// tied-accumulator MFMA (see gemm4w.hip: the builtin lets the allocator shuffle the 256
+// accumulator registers); first operand X (n), second dY (m): acc = P^T per 16 x 16 tile
+template <typename T> struct WwT;
+template <> struct WwT<bf16_t> {
+  typedef bf16x8 v8;
+  static __device__ __forceinline__ void mma(v8 a, v8 b, f32x4_t& c) {
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+  }
+  static __device__ __forceinline__ void mma0(v8 a, v8 b, f32x4_t& c) {
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+  }
+};
+template <> struct WwT<half_t> {
+  typedef f16x8 v8;
+  static __device__ __forceinline__ void mma(v8 a, v8 b, f32x4_t& c) {
+    asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+  }
+  static __device__ __forceinline__ void mma0(v8 a, v8 b, f32x4_t& c) {
+    asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+  }
+};
+
+__device__ __forceinline__ void ww_mfma_drain() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+
+// 8 consecutive k of one column: the two transposed 4-row reads at byte offsets lo, lo+HI
+template <typename V8, int HI>
+__device__ __forceinline__ V8 ww_frag(const unsigned char* p) {
+  const v4s_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)p);
+  const v4s_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p + HI));
+  V8 f;
+  v4s_t* fp = reinterpret_cast<v4s_t*>(&f);
+  fp[0] = a;
+  fp[1] = b;
+  return f;
+}
+
+template <typename TT, int L>
+__global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
+  typedef typename WwT<TT>::v8 v8;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kWwSlot];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int mt = p.M >> 8, nt = p.N >> 8, per_split = mt * nt;
+  const int b = ww_xcd_remap(blockIdx.x, gridDim.x);
+  const int s = b / per_split;
+  int r = b - s * per_split;
+  // grouped order inside a split: group_m m-tiles x all n-tiles
+  int tm, tn;
+  {
+    const int gm = p.group_m, gsz = gm * nt, g = r / gsz;
+    const int first = g * gm, rows = min(gm, mt - first), rr = r - g * gsz;
+    tm = first + rr % rows;
+    tn = rr / rows;
+  }
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int KT = p.rows >> 6;
+  const int64_t k0 = (int64_t)s * p.rows;
+
+  // DMA.  L == 0: wave w fills blocks (row group w, chunk group cg = 0..7) of each operand;
+  // lane (i = lane >> 2, j = lane & 3) reads row 16 w + i, chunk cg*4 + (j ^ 2 (i >> 3 & 1)).
+  // L == 1: blocks of 8 rows x 8 chunks (128 contiguous bytes per row); wave w fills row
+  // groups 2w + h (h = 0, 1) x chunk groups cg = 0..3; lane (i = lane >> 3, j = lane & 7)
+  // reads row 8 (2w + h) + i, chunk cg*8 + (j ^ f), f = 2 (i >> 1 & 1) + 4 h.  The K-tile
+  // and the chunk group go into the (scalar) soffset.
+  // L == 2: blocks of 2 rows x 512 bytes (whole rows); piece q of wave w holds rows
+  // 16 w + 2 q + (lane >> 5), lane & 31 the physical chunk of logical chunk
+  // (lane & 31) ^ key(r), key(r) = 2 ((r & 3) | (r >> 3 & 1) << 2): one offset per piece
+  uint32_t offA[8], offB[8];  // (a fixed bound: an array whose bound depends on L, captured
+  // by the lambdas below, made clang drop the kernel host stub)
+  if constexpr (L == 2) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = wid * 16 + 2 * q + (lane >> 5);
+      const int key = 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+      const uint32_t ch = (uint32_t)((lane & 31) ^ key) * 16u;
+      offA[q] = (uint32_t)r * (uint32_t)p.lda * (uint32_t)sizeof(TT) + ch;
+      offB[q] = (uint32_t)r * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + ch;
+    }
+  } else {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int drow, dch;
+    if constexpr (L == 0) {
+      drow = wid * 16 + (lane >> 2);
+      dch = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    } else {
+      drow = (2 * wid + h) * 8 + (lane >> 3);
+      dch = (lane & 7) ^ ((((lane >> 4) & 1) << 1) | (h << 2));
+    }
+    offA[h] = (uint32_t)drow * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)dch * 16u;
+    offB[h] = (uint32_t)drow * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)dch * 16u;
+  }
+  }
+  const __amdgpu_buffer_rsrc_t rA =
+      ww_rsrc(static_cast<const TT*>(p.A) + k0 * p.lda + m0, 0xffffffffu);
+  const __amdgpu_buffer_rsrc_t rB =
+      ww_rsrc(static_cast<const TT*>(p.B) + k0 * p.ldb + n0, 0xffffffffu);
+  const uint32_t strideA = 64u * (uint32_t)p.lda * (uint32_t)sizeof(TT);  // one K-tile
+  const uint32_t strideB = 64u * (uint32_t)p.ldb * (uint32_t)sizeof(TT);
+  // piece q (0..7 A, 8..15 B) of K-tile T (clamped: past the end the last K-tile is
+  // re-fetched into the free slot, so every K-tile issues the same stream)
+  auto piece = [&](int T, int q) {
+    const int Tc = T < KT ? T : KT - 1;
+    const int qq = q & 7;
+    const int h = L == 2 ? (qq & 7) : L == 0 ? 0 : (qq >> 2);
+    const int blk = L == 1 ? (2 * wid + h) * 4 + (qq & 3) : wid * 8 + qq;
+    const uint32_t cgo = L == 0 ? (uint32_t)qq * 64u : L == 1 ? (uint32_t)(qq & 3) * 128u : 0u;
+    unsigned char* dst = lds + (T & 1) * kWwSlot + (q >> 3) * kWwOp + blk * 1024;
+    if (q < 8) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (__attribute__((address_space(3))) void*)dst, 16,
+                                               offA[h], (uint32_t)Tc * strideA + cgo, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (__attribute__((address_space(3))) void*)dst, 16,
+                                               offB[h], (uint32_t)Tc * strideB + cgo, 0, 0);
+    }
+  };
+
+  // transposed fragment reads: lane (q = (lane & 15) >> 2, p1 = lane >> 1 & 1, p0 = lane & 1,
+  // fg = lane >> 4) of fragment i (columns 16 i .. of the wave's 128) at k-step ks: rows
+  // ks*32 + fg*8 + q (+4 for the second read), chunk 2 i + p1, byte 8 p0.  L == 0: a lane
+  // base per parity of i; L == 1: per i & 3 (the XOR key spans chunk bits 1-2)
+  const int fq = (lane & 15) >> 2, fp1 = (lane >> 1) & 1, fp0 = lane & 1, fg = lane >> 4;
+  constexpr int NLB = L == 0 ? 2 : L == 1 ? 4 : 8;
+  constexpr int HI = L == 0 ? 256 : L == 1 ? 512 : 2048;  // byte distance of rows +4
+  int lb[8];
+#pragma unroll
+  for (int ip = 0; ip < NLB; ++ip) {
+    if constexpr (L == 2) {
+      const int kk = fq | ((fg & 1) << 2);
+      lb[ip] = fg * 4096 + fq * 512 + ((2 * (ip ^ kk) + fp1) << 4) + 8 * fp0;
+    } else if constexpr (L == 0) {
+      lb[ip] = (fg >> 1) * 8 * 1024 + ((fg & 1) * 8 + fq) * 64 +
+               (((2 * ip + fp1) ^ ((fg & 1) << 1)) << 4) + 8 * fp0;
+    } else {
+      const int f = (((fq >> 1) & 1) << 1) | ((fg & 1) << 2);
+      lb[ip] = fg * 4096 + fq * 128 + (((2 * ip + fp1) ^ f) << 4) + 8 * fp0;
+    }
+  }
+  v8 fa0[8], fb0[8], fa1[8], fb1[8];
+  // n-th read of a k-step in the order the next k-step's groups consume them (group g:
+  // A[g / 2] with B[(g & 1) * 4 .. +3]): B0-3, A0, B4-7, A1 .. A7
+  auto rd_order = [](int n) { return n < 4 ? 8 + n : n == 4 ? 0 : n < 9 ? 7 + n : n - 8; };
+  auto frag_off = [&](int i, int w) {
+    if constexpr (L == 2) return lb[i & 7] + w * 256;
+    else if constexpr (L == 0) return lb[i & 1] + w * 4096 + (i >> 1) * 1024;
+    else return lb[i & 3] + w * 2048 + (i >> 2) * 1024;
+  };
+  auto rd = [&](int slot, int ks, int n, v8(&fa)[8], v8(&fb)[8]) {
+    const unsigned char* base = lds + slot * kWwSlot + ks * 16384;
+    if (n < 8) {
+      fa[n] = ww_frag<v8, HI>(base + frag_off(n, wm));
+    } else {
+      const int j = n - 8;
+      fb[j] = ww_frag<v8, HI>(base + kWwOp + frag_off(j, wn));
+    }
+  };
+
+  f32x4_t acc[8][8];
+
+  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed, its k-step-0 fragments read
+#pragma unroll
+  for (int q = 0; q < 16; ++q) piece(0, q);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) piece(1, q);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  ww_barrier();
+#pragma unroll
+  for (int n = 0; n < 16; ++n) rd(0, 0, rd_order(n), fa0, fb0);
+
+#define WW_GROUP(FA, FB, g, OP)                                              \
+  _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                         \
+    const int i_ = (g) >> 1, j_ = ((g) & 1) * 4 + jj;                        \
+    WwT<TT>::OP(FA[i_], FB[j_], acc[i_][j_]);                                \
+  }
+
+  // one K-tile: k-step 0 on F0 while F1 (k 32..63 of this K-tile) is read; then K-tile
+  // t+1 must have landed (its DMA went out during k-step 1 of K-tile t-1) and every wave's
+  // reads of this slot retired, so K-tile t+2 may overwrite it; k-step 1 on F1 while F0 of
+  // K-tile t+1 is read and K-tile t+2's DMA goes out
+  auto ktile = [&](int t, auto first_c) {
+    constexpr bool FIRST = decltype(first_c)::value;
+    const int slot = t & 1;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if constexpr (FIRST) {
+        WW_GROUP(fa0, fb0, g, mma0);
+      } else {
+        WW_GROUP(fa0, fb0, g, mma);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      rd(slot, 1, rd_order(g), fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ww_barrier();
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      WW_GROUP(fa1, fb1, g, mma);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(slot ^ 1, 0, rd_order(g), fa0, fb0);
+      piece(t + 2, g);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  ktile(0, std::true_type{});
+  for (int t = 1; t < KT; ++t) ktile(t, std::false_type{});
+#undef WW_GROUP
+  ww_mfma_drain();
+
+  // epilogue: lane (fr, fg) of acc[i][j] holds P[m0 + wm*128 + 16 i + fr][n0 + wn*128 +
+  // 16 j + 4 fg .. +3]: one 16-byte store per (i, j)
+  const int fr = lane & 15;
+  float* P = p.P + (int64_t)s * p.M * p.N;
+  const __amdgpu_buffer_rsrc_t rP = ww_rsrc(P + (int64_t)m0 * p.N + n0,
+                                            (uint32_t)(255 * p.N + 256) * 4u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t row = (uint32_t)(wm * 128 + i * 16 + fr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t off = (row * (uint32_t)p.N + (uint32_t)(wn * 128 + j * 16 + fg * 4)) * 4u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4_t, acc[i][j]), rP, off, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace
+
+bool wgrad4w_supported(int64_t T, int M, int N, int S) {
+  return M > 0 && N > 0 && M % 256 == 0 && N % 256 == 0 && S >= 1 && T % ((int64_t)S * 64) == 0 &&
+         T / S >= 64 && T / S < (1 << 24) &&
+         (int64_t)T * std::max(M, N) * 2 < ((int64_t)1 << 32) &&
+         (int64_t)M * N * 4 < ((int64_t)1 << 32);
+}
+
+void wgrad4w(const WgradArgs& a0, hipStream_t st) {
+  WgradArgs a = a0;
+  if (a.group_m <= 0) {
+    const char* e = std::getenv("APEX_AMD_W4W_GROUPM");
+    a.group_m = e ? std::max(1, std::atoi(e)) : 4;
+  }
+  const int grid = (a.M / 256) * (a.N / 256) * a.S;
+  // APEX_AMD_W4W_LAYOUT (read per launch, A/B runs): LDS image of 16-row x 64-byte (0) or
+  // 8-row x 128-byte (1, default) DMA blocks
+  const char* e = std::getenv("APEX_AMD_W4W_LAYOUT");
+  const int lay = e ? std::atoi(e) : 1;
+  auto go = [&](auto t0) {
+    using TT = decltype(t0);
+    if (lay == 0)
+      hipLaunchKernelGGL((wgrad4w_k<TT, 0>), dim3(grid), dim3(kWwT), 0, st, a);
+    else if (lay == 2)
+      hipLaunchKernelGGL((wgrad4w_k<TT, 2>), dim3(grid), dim3(kWwT), 0, st, a);
+    else
+      hipLaunchKernelGGL((wgrad4w_k<TT, 1>), dim3(grid), dim3(kWwT), 0, st, a);
+  };
+  if (a.fp16) go(half_t{});
+  else go(bf16_t{});
+}
+
+}  // namespace amd

@@ -293,6 +293,20 @@ void gemm8p(const G8Args& a, int epi, hipStream_t st);
 // N % 256 == 0, K % 64 == 0
 bool gemm4w_supported(int M, int N, int K);
 void gemm4w(const G8Args& a, int epi, hipStream_t st);
+// dense weight gradients P[s] = A_s^T B_s over row splits (wgrad4w.hip): A [T, M], B [T, N]
+// row-major bf16 / fp16, fp32 partials P [S][M][N]; M, N % 256 == 0, (T / S) % 64 == 0
+struct WgradArgs {
+  const void* A;
+  const void* B;
+  float* P;
+  int M, N, lda, ldb;
+  int rows;     // rows of A / B per split (T / S)
+  int S;
+  int fp16;
+  int group_m;  // <= 0: default (APEX_AMD_W4W_GROUPM or 4)
+};
+bool wgrad4w_supported(int64_t T, int M, int N, int S);
+void wgrad4w(const WgradArgs& a, hipStream_t st);
 
 // ---- implicit-GEMM convolutions, NHWC bf16, MFMA (conv_igemm.hip) ----------
 // 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64

@@ -3,6 +3,7 @@
 #include "dense_ops.h"
 
 #include "common.h"
+#include "pool_ops.h"
 
 namespace amd {
 
@@ -120,6 +121,58 @@ bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
 bool gemm4w_ok(const at::Tensor& a, const at::Tensor& b) {
   return gemm_layout_ok(a, b) &&
          gemm4w_supported((int)a.size(0), (int)b.size(0), (int)a.size(1));
+}
+
+bool wgrad4w_ok(const at::Tensor& dy, const at::Tensor& x, int64_t splits) {
+  return dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 &&
+         (dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf) &&
+         x.scalar_type() == dy.scalar_type() && dy.size(0) == x.size(0) &&
+         dy.stride(1) == 1 && x.stride(1) == 1 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0 &&
+         reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 &&
+         reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && splits >= 1 &&
+         dy.size(1) < (1 << 30) && x.size(1) < (1 << 30) &&
+         // 32-bit DMA offsets: a split's rows of either operand
+         (dy.size(0) / splits) * std::max(dy.stride(0), x.stride(0)) * dy.element_size() <
+             (int64_t(1) << 32) &&
+         wgrad4w_supported(dy.size(0), (int)dy.size(1), (int)x.size(1), (int)splits);
+}
+
+// dW [M, N] = dy^T x in out_dtype (fp32 / bf16): fp32 partials per split of the rows, then
+// the slab reduction (which also accumulates into / overwrites `out`, a DDP bucket view)
+at::Tensor wgrad4w_op(at::Tensor dy, at::Tensor x, int64_t splits, at::ScalarType out_dtype,
+                      c10::optional<at::Tensor> out, bool accumulate) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(wgrad4w_ok(dy, x, splits),
+              "wgrad4w: bf16 / fp16 dy [T, M], x [T, N] with unit column stride, M % 256 == 0, "
+              "N % 256 == 0, (T / splits) % 64 == 0");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "wgrad4w: out dtype");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  const bool given = out.has_value() && out->defined();
+  if (given)
+    TORCH_CHECK(out->is_cuda() && out->scalar_type() == out_dtype && out->numel() == M * N &&
+                    out->is_contiguous(),
+                "wgrad4w: out must be a contiguous tensor of M*N elements of out_dtype");
+  WgradArgs g{};
+  g.A = dy.data_ptr();
+  g.B = x.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.lda = (int)dy.stride(0);
+  g.ldb = (int)x.stride(0);
+  g.rows = (int)(T / splits);
+  g.S = (int)splits;
+  g.fp16 = dy.scalar_type() == at::kHalf ? 1 : 0;
+  // one split written straight into an fp32 result (no reduction pass)
+  if (splits == 1 && out_dtype == at::kFloat && !(given && accumulate)) {
+    at::Tensor r = given ? *out : at::empty({M, N}, dy.options().dtype(at::kFloat));
+    g.P = r.data_ptr<float>();
+    wgrad4w(g, cur_stream());
+    return r;
+  }
+  at::Tensor part = at::empty({splits, M, N}, dy.options().dtype(at::kFloat));
+  g.P = part.data_ptr<float>();
+  wgrad4w(g, cur_stream());
+  return splitk_reduce_op(part, out_dtype, out, accumulate);
 }
 
 std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,

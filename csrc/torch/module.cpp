@@ -143,6 +143,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("kernel") = 0);
   dn.def("gemm8p_ok", &gemm8p_ok);
   dn.def("gemm4w_ok", &gemm4w_ok);
+  dn.def("wgrad4w", &wgrad4w_op, py::arg("dy"), py::arg("x"), py::arg("splits"),
+         py::arg("out_dtype"), py::arg("out") = py::none(), py::arg("accumulate") = true);
+  dn.def("wgrad4w_ok", &wgrad4w_ok);
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);

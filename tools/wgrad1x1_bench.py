@@ -38,12 +38,28 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--splits", default="256,512")
+    ap.add_argument("--dense", action="store_true",
+                    help="the transformer dense-layer weight gradients instead (T tokens)")
+    ap.add_argument("--own-only", action="store_true",
+                    help="--dense: only the default split and the own kernel")
+    ap.add_argument("--tuned", default="",
+                    help="read-only TunableOp table tuning/<name>.csv (as bench.py uses)")
+    ap.add_argument("--tune-file", default="",
+                    help="TunableOp ONLINE tuning into this file (every GEMM shape searched)")
     args = ap.parse_args()
     from apex_example_amd import _native
     from apex_example_amd.ops import conv as C
 
     cv = _native.require().conv
     dev = "cuda"
+    if args.tuned:
+        from apex_example_amd.utils.gemm_tuning import use_tuned_gemms
+        print("tuned table:", use_tuned_gemms(args.tuned))
+    if args.tune_file:
+        t = torch.cuda.tunable
+        t.enable(True)
+        t.tuning_enable(True)
+        t.set_filename(args.tune_file, insert_device_ordinal=False)
     splits = [int(s) for s in args.splits.split(",") if s]
 
     def forced(dyr, xr, s):
@@ -54,6 +70,8 @@ def main():
         part = torch.bmm(a, b, out_dtype=torch.float32)
         return cv.splitk_reduce(part, torch.bfloat16, None, True)
 
+    if args.dense:
+        return dense(args, cv, forced)
     rows = []
     for (ci, co, hw, st, calls) in SHAPES:
         n = args.batch
@@ -89,6 +107,55 @@ def main():
     tot_def = sum(r[3] * list(r[5].values())[0] for r in rows)
     tot_best = sum(r[3] * min(r[5].values()) for r in rows)
     print("weighted per step: default %.0f us, best-of %.0f us" % (tot_def, tot_best))
+
+
+DENSE = [("bert ffn-in", 16384, 4096, 1024), ("bert ffn-out", 16384, 1024, 4096),
+         ("bert qkv", 16384, 3072, 1024), ("bert attn-out", 16384, 1024, 1024),
+         ("gpt2 ffn-in", 8192, 4096, 1024), ("gpt2 ffn-out", 8192, 1024, 4096),
+         ("gpt2 qkv", 8192, 3072, 1024), ("gpt2 attn-out", 8192, 1024, 1024)]
+
+
+def _native_dense():
+    from apex_example_amd import _native
+    return _native.require().dense
+
+
+def dense(args, cv, forced):
+    """dW[o, i] = dY^T X over T tokens: the default split (fused_dense._splitk_chunks)
+    against other split counts and the unsplit GEMM (bf16 out)."""
+    from apex_example_amd import fused_dense as FD
+    dev = "cuda"
+    for (name, T, o, i) in DENSE:
+        g = torch.Generator(device=dev).manual_seed(T + o + i)
+        dy = torch.randn(T, o, device=dev, generator=g).to(torch.bfloat16)
+        x = torch.randn(T, i, device=dev, generator=g).to(torch.bfloat16)
+        ref = dy.float().t() @ x.float()
+        scale = float(ref.abs().max())
+        s0 = FD._splitk_chunks(T, o, i, torch.bfloat16, torch.bfloat16)
+        cands = {"default(S=%d)" % s0: lambda: FD._wgrad(dy, x, torch.bfloat16)}
+        for s in (1, 2, 4, 8, 16):
+            if s != s0 and T % s == 0 and not args.own_only:
+                cands["S=%d" % s] = ((lambda s=s: forced(dy, x, s)) if s > 1
+                                     else (lambda: dy.t() @ x))
+        dn = _native_dense()
+        def own(s, lay):
+            os.environ["APEX_AMD_W4W_LAYOUT"] = str(lay)
+            return dn.wgrad4w(dy, x, s, torch.bfloat16)
+        for s in (2, 4, 8):
+            for lay in (0, 1, 2):
+                if dn.wgrad4w_ok(dy, x, s):
+                    cands["wgrad4w L%d S=%d" % (lay, s)] = (lambda s=s, lay=lay: own(s, lay))
+        for k, fn in cands.items():
+            err = float((fn().float().reshape(o, i) - ref).abs().max()) / scale
+            assert err < 2e-2, (name, k, err)
+        times = {k: [] for k in cands}
+        for _ in range(args.rounds):
+            for k, fn in cands.items():
+                times[k].append(timeit(fn))
+        gf = 2.0 * T * o * i / 1e9
+        print("| %s | %d x %d x %d | %s |" % (name, o, i, T, " | ".join(
+            "%s %.1f us (%.0f TF)" % (k, min(v), gf / min(v) * 1e3) for k, v in times.items())),
+            flush=True)
 
 
 if __name__ == "__main__":
