@@ -155,10 +155,13 @@ _ADDMM_F32 = os.environ.get("APEX_AMD_ADDMM_F32", "1") == "1"
 
 # Dense weight gradients on the own transposed-operand MFMA kernel (csrc/hip/wgrad4w.hip):
 # fp32 partials per row split + the slab reduction, for weights with both dimensions
-# multiples of 256.  Opt-in (APEX_AMD_DENSE_W4W=1): measured slower than the hipBLASLt
-# split-K path (BERT FFN 239 vs 146 us, profiles/r5/wgrad_dense.md) - its K loop waits on
-# the operand DMA two thirds of the time (PMC SQ_WAIT_ANY 66 %, TA stalled by TC).
-_DENSE_W4W = os.environ.get("APEX_AMD_DENSE_W4W", "0") == "1"
+# multiples of 256 and >= 48 output tiles of 256 x 256 (the FFN and QKV projections).
+# Same box (profiles/r5/wgrad_dense.md): BERT FFN 114.5 vs 136.8 us, QKV 103.5 vs 107.6 us,
+# GPT-2 FFN 69.7 vs 83.5 us against the hipBLASLt split-K path; the 1024 x 1024 attention
+# output projection (16 tiles) stays on hipBLASLt (57.8 vs 47.8 us).  APEX_AMD_DENSE_W4W=0
+# disables.
+_DENSE_W4W = os.environ.get("APEX_AMD_DENSE_W4W", "1") == "1"
+_W4W_MIN_TILES = 48
 
 
 def _w4w_splits(T, o, i):
@@ -179,7 +182,7 @@ def _wgrad_w4w(dy2, x2, dtype, out, accumulate):
         return None
     T, o = dy2.shape
     i = x2.shape[1]
-    if o % 256 or i % 256:
+    if o % 256 or i % 256 or (o // 256) * (i // 256) < _W4W_MIN_TILES:
         return None
     dn = _native.require().dense
     S = _w4w_splits(T, o, i)

@@ -34,14 +34,13 @@
 // 2 = whole 512-byte rows, two per DMA instruction (chunk key 2 ((r & 3) | (r >> 3 & 1) << 2)).
 // All three read conflict-free and are bitwise equal (tests/test_wgrad4w_gpu.py).
 //
-// Status (round 5, profiles/r5/wgrad_dense.md): correct, but 1.6x SLOWER than the hipBLASLt
-// path on the BERT / GPT-2 shapes (FFN 239 us vs 146 us at layout 0, 318 / 347 us at 2 / 1),
-// so fused_dense keeps it opt-in (APEX_AMD_DENSE_W4W=1).  The time per K-tile does not
-// depend on how many workgroups run (32 or 256), and PMC shows 66 % of wave cycles in
-// s_waitcnt and the texture addresser stalled by the L1 (TA_ADDR_STALLED_BY_TC 2.5 M vs 0
-// for hipBLASLt): with one 64-row K-tile of DMA lead the loop is latency-bound on operand
-// rows that change every K-tile (the TN form re-reads the same 256 rows at the next 128
-// bytes); a deeper ring than 128 KB of LDS allows is the open fix.
+// Status (round 5, profiles/r5/wgrad_dense.md): BERT-large FFN weight gradient 114.5 us
+// (1.20 PF, reduction included) vs 136.8 us for hipBLASLt's best split; one workgroup runs
+// a K-tile in 1.15 us against 0.85 us of MFMA issue.  The first build ran 3.3 us per K-tile
+// whatever the load: with the LDS-DMA as a builtin the compiler put an s_waitcnt vmcnt(0)
+// in front of every transposed read (the DMA writes LDS, the tr-read builtin carries no
+// alias information), i.e. the loop waited out the full memory latency of the next
+// K-tile's DMA at every MFMA group.  The DMA is inline asm now (ww_dma).
 //
 // M % 256 == 0, N % 256 == 0, rows per split % 64 == 0.
 #include <algorithm>
@@ -105,6 +104,20 @@ __device__ __forceinline__ void ww_mfma_drain() {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 }
 
+// One LDS-DMA wave-instruction (16 bytes per lane into M0 + 16 * lane) as inline asm: the
+// compiler does not see it write LDS, so it does not wait for every outstanding DMA piece
+// (vmcnt(0)) in front of each ds_read_b64_tr_b16 - with the builtin form it did, which
+// serialised the K loop on the full memory latency (3.3 us per K-tile for ONE workgroup).
+// The loop orders DMA and fragment reads itself: explicit vmcnt(0) + s_barrier before a
+// slot is read, lgkmcnt(0) + s_barrier before it is overwritten.
+__device__ __forceinline__ void ww_dma(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, uint32_t voff,
+                                       uint32_t soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+               :
+               : "v"(voff), "s"(r), "s"(soff), "{m0}"(lds_addr)
+               : "memory");
+}
+
 // 8 consecutive k of one column: the two transposed 4-row reads at byte offsets lo, lo+HI
 template <typename V8, int HI>
 __device__ __forceinline__ V8 ww_frag(const unsigned char* p) {
@@ -119,6 +132,7 @@ __device__ __forceinline__ V8 ww_frag(const unsigned char* p) {
 
 template <typename TT, int L>
 __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only needs the launch stub)
   typedef typename WwT<TT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kWwSlot];
 
@@ -182,6 +196,7 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
       ww_rsrc(static_cast<const TT*>(p.B) + k0 * p.ldb + n0, 0xffffffffu);
   const uint32_t strideA = 64u * (uint32_t)p.lda * (uint32_t)sizeof(TT);  // one K-tile
   const uint32_t strideB = 64u * (uint32_t)p.ldb * (uint32_t)sizeof(TT);
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
   // piece q (0..7 A, 8..15 B) of K-tile T (clamped: past the end the last K-tile is
   // re-fetched into the free slot, so every K-tile issues the same stream)
   auto piece = [&](int T, int q) {
@@ -190,13 +205,11 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
     const int h = L == 2 ? (qq & 7) : L == 0 ? 0 : (qq >> 2);
     const int blk = L == 1 ? (2 * wid + h) * 4 + (qq & 3) : wid * 8 + qq;
     const uint32_t cgo = L == 0 ? (uint32_t)qq * 64u : L == 1 ? (uint32_t)(qq & 3) * 128u : 0u;
-    unsigned char* dst = lds + (T & 1) * kWwSlot + (q >> 3) * kWwOp + blk * 1024;
+    const uint32_t dst = lds_base + (uint32_t)((T & 1) * kWwSlot + (q >> 3) * kWwOp + blk * 1024);
     if (q < 8) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (__attribute__((address_space(3))) void*)dst, 16,
-                                               offA[h], (uint32_t)Tc * strideA + cgo, 0, 0);
+      ww_dma(rA, dst, offA[h], (uint32_t)Tc * strideA + cgo);
     } else {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (__attribute__((address_space(3))) void*)dst, 16,
-                                               offB[h], (uint32_t)Tc * strideB + cgo, 0, 0);
+      ww_dma(rB, dst, offB[h], (uint32_t)Tc * strideB + cgo);
     }
   };
 
@@ -310,6 +323,9 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+  (void)p;
+#endif
 }
 
 }  // namespace
@@ -328,10 +344,10 @@ void wgrad4w(const WgradArgs& a0, hipStream_t st) {
     a.group_m = e ? std::max(1, std::atoi(e)) : 4;
   }
   const int grid = (a.M / 256) * (a.N / 256) * a.S;
-  // APEX_AMD_W4W_LAYOUT (read per launch, A/B runs): LDS image of 16-row x 64-byte (0) or
-  // 8-row x 128-byte (1, default) DMA blocks
+  // APEX_AMD_W4W_LAYOUT (read per launch, A/B runs): LDS image of 16-row x 64-byte (0,
+  // default), 8-row x 128-byte (1) or whole-row (2) DMA blocks - within 1-5 % of each other
   const char* e = std::getenv("APEX_AMD_W4W_LAYOUT");
-  const int lay = e ? std::atoi(e) : 1;
+  const int lay = e ? std::atoi(e) : 0;
   auto go = [&](auto t0) {
     using TT = decltype(t0);
     if (lay == 0)

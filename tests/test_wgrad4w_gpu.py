@@ -97,7 +97,7 @@ def test_dense_wgrad_routes_through_wgrad4w(monkeypatch, w_dtype):
     bf16 result; fp32 master-style weights: fp32 result, also accumulating into a
     given buffer) and matches the hipBLASLt split-K path within rounding."""
     from apex_example_amd import fused_dense as FD
-    T, o, i = 4096, 1024, 768
+    T, o, i = 4096, 3072, 1024   # 48 output tiles: routed (fewer stay on hipBLASLt)
     dy, x = _ops(T, o, i, torch.bfloat16, 21)
     ref = dy.float().t() @ x.float()
     monkeypatch.setattr(FD, "_DENSE_W4W", False)
@@ -119,3 +119,10 @@ def test_dense_wgrad_routes_through_wgrad4w(monkeypatch, w_dtype):
     acc = torch.ones(o, i, device=DEV, dtype=w_dtype)
     FD._wgrad(dy, x, w_dtype, out=acc, accumulate=True)
     assert _err(acc - 1, ref) < tol
+
+
+def test_dense_wgrad_small_weights_stay_on_library(monkeypatch):
+    from apex_example_amd import fused_dense as FD
+    dy, x = _ops(4096, 1024, 1024, torch.bfloat16, 5)
+    monkeypatch.setattr(FD, "_DENSE_W4W", True)
+    assert FD._wgrad_w4w(dy, x, torch.bfloat16, None, True) is None
