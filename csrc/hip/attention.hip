@@ -57,9 +57,20 @@ __device__ __forceinline__ f32x16_t mfma32(typename Frag<T>::v8 a, typename Frag
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// LDS DMA (16 bytes per lane into M0 + 16 * lane) as inline asm, NOT the builtin: the
+// compiler cannot tell which LDS bytes a pending builtin DMA writes, so it put an
+// s_waitcnt vmcnt(0) in front of LDS reads of the CURRENT tile that follow the next
+// tile's issue (ISA of the round-5 build: one per forward loop, one to two per dQ / dK-dV
+// loop) - every iteration waited out the prefetch it had just started.  Every kernel here
+// orders the ring itself (s_waitcnt vmcnt(0) + barrier before a slot is read, the refill
+// after the barrier), so the compiler need not know about these writes.
+__device__ __forceinline__ uint32_t lds_addr32(const void* l) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)l;
+}
 __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(g), "{m0}"(lds_addr32(l)) : "memory");
+#endif
 }
 
 // Tile DMA addressing: a wave-uniform tile base (SGPRs, one scalar multiply-add per
@@ -70,7 +81,10 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
 // VALU cycles.  Only a tile that reaches past S takes the clamped per-lane path.  The
 // binding keeps row strides below 2^24 elements so the offsets fit 32 bits.
 __device__ __forceinline__ void glds16o(const void* tile_base, uint32_t off, unsigned char* l) {
-  glds16(static_cast<const char*>(tile_base) + off, l);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("global_load_lds_dwordx4 %0, %1" : : "v"(off), "s"(tile_base), "{m0}"(lds_addr32(l))
+               : "memory");
+#endif
 }
 
 template <typename T>

@@ -68,6 +68,20 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// The same DMA as inline asm, for the weight-gradient kernels: there the compiler, unable
+// to tell which LDS bytes a pending builtin DMA writes, put an s_waitcnt vmcnt(0) in front
+// of the first transposed read of the CURRENT K-tile, right after the NEXT K-tile's issue -
+// every K-tile waited out its own prefetch (ISA of the round-5 build, one per kernel).
+// These loops order the ring themselves (explicit vmcnt wait + barrier before a stage is
+// read), so the compiler need not see the writes.  (conv_tap_k keeps the builtin: its
+// ISA has no such wait.)
+__device__ __forceinline__ void glds16a(const void* g, unsigned char* l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)l;
+  asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(g), "{m0}"(la) : "memory");
+#endif
+}
+
 // workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not wait for
 // outstanding global loads / stores (vmcnt), so prefetches and output stores stay in
 // flight; the empty asm statements keep the compiler from moving memory operations
@@ -1215,7 +1229,7 @@ __global__ void __launch_bounds__(512, 1)
     const bool ok = hp >= 1 && hp <= H && wp >= 1 && wp <= W;
     const void* src = ok ? (const void*)(x + (((int64_t)n * H + hp - 1) * W + wp - 1) * 64 + chunk * 8)
                          : (const void*)g_zero16;
-    glds16(src, ring + (P & (kW64Ring - 1)) * RB);
+    glds16a(src, ring + (P & (kW64Ring - 1)) * RB);
   };
   // the 8 dY row groups of K-tile (n, q0)
   auto a_tile = [&](int n, int q0, int buf) {  // 8 row groups: one per wave
@@ -1226,7 +1240,7 @@ __global__ void __launch_bounds__(512, 1)
     const bool ok = qq < HWp && w_ < W;
     const void* src = ok ? (const void*)(dy + (((int64_t)n * H + h_) * W + w_) * 64 + chunk * 8)
                          : (const void*)g_zero16;
-    glds16(src, abuf + buf * A_BYTES + wid * 1024);
+    glds16a(src, abuf + buf * A_BYTES + wid * 1024);
   };
 
   // loop-invariant transposed-read offsets.  A (dY image, 64 co): k rows wk*32 + ...
@@ -1387,7 +1401,7 @@ __global__ void __launch_bounds__(kCT, 2)
       const int p_ = p0_ + (wid * AI + q) * (1024 / RBA) + lane / LPRA;                        \
       const void* src_ = p_ < M ? (const void*)(dy + (int64_t)p_ * Cout + co0 + achunk[q] * 8) \
                                 : (const void*)g_zero16;                                       \
-      glds16(src_, A_ + (wid * AI + q) * 1024);                                                \
+      glds16a(src_, A_ + (wid * AI + q) * 1024);                                               \
     }                                                                                          \
     _Pragma("unroll") for (int q = 0; q < BI; ++q) {                                           \
       const int p_ = p0_ + (wid * BI + q) * (1024 / RBB) + lane / LPRB;                        \
@@ -1401,7 +1415,7 @@ __global__ void __launch_bounds__(kCT, 2)
                                : (int64_t)(n_ * H + hi_) * W + wi_;                            \
       const void* src_ = ok_ ? (const void*)(x + xpix_ * Cin + ci0 + bchunk[q] * 8)            \
                              : (const void*)g_zero16;                                          \
-      glds16(src_, B_ + (wid * BI + q) * 1024);                                                \
+      glds16a(src_, B_ + (wid * BI + q) * 1024);                                               \
     }                                                                                          \
   }
 
