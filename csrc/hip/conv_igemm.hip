@@ -176,6 +176,18 @@ __device__ __forceinline__ int64_t out_pix(const ConvGeom& g, int m, int z) {
   }
 }
 
+// constant sources for the branch-free epilogue loads below (absent tensors)
+__device__ const float g_one8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+__device__ const uint8_t g_ff16[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                       0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+
+// Branch-free: every load is issued unconditionally through a selected pointer (a
+// constant array when the tensor is absent), the per-channel constants first.  With the
+// former conditional loads (`addp ? load : 0`, `ep.w ? ep.w[c] : 1`) the compiler put an
+// s_waitcnt vmcnt(0) at each control-flow join (a register written by a load on one path
+// and by a move on the other) and before the constants' arithmetic - which also drained
+// every row load issued before it: the prefetch ran as ~10 serial memory round trips per
+// workgroup (ISA of the round-5 build).
 template <int MODE, int BM, int BN, int CT>
 __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEpi& ep, int m0,
                                                int n0, int z, BnPre<BM, BN, CT>& P) {
@@ -184,38 +196,44 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
   const int cc = tid % PT::CPR, rg = tid / PT::CPR;
   const int c0 = n0 + cc * 8;
   const int NC = g.NC;
+  const bool rm2 = ep.relu_mode == 2, rm1 = ep.relu_mode == 1;
+  const float* zf = reinterpret_cast<const float*>(g_zero16);
+  {
+    const float* wp = rm2 && ep.w ? ep.w + c0 : g_one8;
+    const float* bp = rm2 && ep.b ? ep.b + c0 : zf;
+    const float* ip = rm2 ? ep.invstd + c0 : zf;
+    const float* mp = ep.mean + c0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      P.mu[i] = mp[i];
+      P.sc[i] = ip[i] * wp[i];
+      P.sh[i] = bp[i] - P.mu[i] * P.sc[i];
+    }
+  }
   const bf16_t* addp = static_cast<const bf16_t*>(ep.add);
   const bf16_t* xp = static_cast<const bf16_t*>(ep.xbn);
+  const bf16_t* zb = reinterpret_cast<const bf16_t*>(g_zero16);
+  const bool x_on = !(ep.diag & 1), s2 = ep.add_s2 && addp;
 #pragma unroll
   for (int q = 0; q < PT::ROWS; ++q) {
     const int m = m0 + q * PT::RGS + rg;
-    const int64_t opix = out_pix<MODE>(g, m < g.M ? m : 0, z);
+    const int mm = m < g.M ? m : 0;
+    const int64_t opix = out_pix<MODE>(g, mm, z);
     const int64_t off = opix * NC + c0;
-    if (ep.add_s2 && addp) {
+    int64_t aoff = off;
+    bool a_on = addp != nullptr;
+    if (s2) {
       // compact stride-2 residual gradient: pixel (n, h, w) receives add[n][h/2][w/2] when
       // h and w are even (dense output pixels: opix = m on a GH x GW grid)
       const int GHW = g.GH * g.GW;
-      const int mm = m < g.M ? m : 0;
       const int n = mm / GHW, rem = mm - n * GHW;
       const int h = rem / g.GW, w = rem - h * g.GW;
-      const int64_t coff = ((int64_t)(n * (g.GH >> 1) + (h >> 1)) * (g.GW >> 1) + (w >> 1)) * NC + c0;
-      P.av[q] = ((h | w) & 1) ? make_uint4(0, 0, 0, 0)
-                              : *reinterpret_cast<const uint4*>(addp + coff);
-    } else {
-      P.av[q] = addp ? *reinterpret_cast<const uint4*>(addp + off) : make_uint4(0, 0, 0, 0);
+      aoff = ((int64_t)(n * (g.GH >> 1) + (h >> 1)) * (g.GW >> 1) + (w >> 1)) * NC + c0;
+      a_on = ((h | w) & 1) == 0;
     }
-    P.xv[q] = (ep.diag & 1) ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(xp + off);
-    P.mk[q] = ep.relu_mode == 1 ? ep.rmask[opix * (NC >> 3) + (c0 >> 3)] : 0xffu;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    P.mu[i] = ep.mean[c0 + i];
-    P.sc[i] = P.sh[i] = 0.f;
-    if (ep.relu_mode == 2) {
-      const float wv = ep.w ? ep.w[c0 + i] : 1.f, bv = ep.b ? ep.b[c0 + i] : 0.f;
-      P.sc[i] = ep.invstd[c0 + i] * wv;
-      P.sh[i] = bv - P.mu[i] * P.sc[i];
-    }
+    P.av[q] = *reinterpret_cast<const uint4*>(a_on ? addp + aoff : zb);
+    P.xv[q] = *reinterpret_cast<const uint4*>(x_on ? xp + off : zb);
+    P.mk[q] = *(rm1 ? ep.rmask + opix * (NC >> 3) + (c0 >> 3) : g_ff16);
   }
 }
 
@@ -231,6 +249,12 @@ __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restric
   const int tid = threadIdx.x;
   const int cc = tid % PT::CPR, rg = tid / PT::CPR;
   const int c0 = n0 + cc * 8;
+  // every prefetched load has landed (they flew under the accumulator -> LDS tile
+  // write): one vmcnt(0) the compiler sees (the builtin, not asm), so the row loop below
+  // issues its stores without a wait per row - the compiler cannot count loads past the
+  // guarded stores and waited vmcnt(0), i.e. for the previous row's store, in front of
+  // every row
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched
 #pragma unroll
   for (int q = 0; q < PT::ROWS; ++q) {
     const int row = q * PT::RGS + rg;
