@@ -223,7 +223,11 @@ __device__ __forceinline__ void stage_params(int C, int cb, int n, F&& f) {
   __syncthreads();
 }
 
-template <typename T, typename TW, bool VEC, int U>
+// ZZ (compile time): a residual z is added.  Loads are issued for all U rows first
+// (clamped rows, no branches) and pinned ahead of the arithmetic: with `if (z)` and
+// `if (rr < M)` around them the compiler waited vmcnt(0) after every row's loads (one row
+// in flight per lane, ISA of the round-5 build).
+template <typename T, typename TW, bool VEC, int U, bool ZZ>
 __global__ void __launch_bounds__(kBNThreads)
     apply_k(const T* __restrict__ x, const float* __restrict__ mean,
             const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
@@ -252,11 +256,11 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t rr = r + (int64_t)u * stride;
-      if (rr < M) {
-        ldw<T, W>(x + rr * C + c0, v[u]);
-        if (z) ldw<T, W>(z + rr * C + c0, zz[u]);
-      }
+      const int64_t rc = rr < M ? rr : M - 1;
+      ldw<T, W>(x + rc * C + c0, v[u]);
+      if constexpr (ZZ) ldw<T, W>(z + rc * C + c0, zz[u]);
     }
+    asm volatile("" ::: "memory");  // every load of the group issues before any store
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t rr = r + (int64_t)u * stride;
@@ -265,7 +269,7 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
       for (int i = 0; i < W; ++i) {
         float o = fmaf(v[u][i], sc[i], sh[i]);
-        if (z) o += zz[u][i];
+        if constexpr (ZZ) o += zz[u][i];
         mb |= (o > 0.f ? 1u : 0u) << i;
         v[u][i] = relu ? fmaxf(o, 0.f) : o;
       }
@@ -407,6 +411,7 @@ __global__ void __launch_bounds__(kBNThreads)
       if constexpr (RM == 1) mk[u] = rmask[rc * Cb + (c0 >> 3)];
       if constexpr (RM == 2) ldw<T, W>(z + rc * C + c0, zv[u]);
     }
+    asm volatile("" ::: "memory");  // every load of the group issues before any store
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t rr = r + (int64_t)u * stride;
@@ -626,12 +631,16 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
       using TW = decltype(w0);
       vec_dispatch(vec, [&](auto V) {
         auto go = [&](auto u) {
-          hipLaunchKernelGGL((apply_k<T, TW, decltype(V)::value, decltype(u)::value>),
-                             dim3(blocks, g.cblocks), dim3(kBNThreads), 0, st,
-                             static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
-                             static_cast<const TW*>(b), static_cast<const T*>(z),
-                             static_cast<T*>(y), vec ? rmask : nullptr, M, (int)C, g.ctile,
-                             g.rows_iter, relu);
+          auto launch = [&](auto zz) {
+            hipLaunchKernelGGL(
+                (apply_k<T, TW, decltype(V)::value, decltype(u)::value, decltype(zz)::value>),
+                dim3(blocks, g.cblocks), dim3(kBNThreads), 0, st, static_cast<const T*>(x), mean,
+                invstd, static_cast<const TW*>(w), static_cast<const TW*>(b),
+                static_cast<const T*>(z), static_cast<T*>(y), vec ? rmask : nullptr, M, (int)C,
+                g.ctile, g.rows_iter, relu);
+          };
+          if (z) launch(std::true_type{});
+          else launch(std::false_type{});
         };
         if (bn_unroll().elem == 4) go(std::integral_constant<int, 4>{});
         else go(std::integral_constant<int, 2>{});

@@ -160,7 +160,7 @@ struct BnPre {
   static constexpr int ROWS = BM / RGS;
   uint4 av[ROWS], xv[ROWS];
   unsigned mk[ROWS];
-  float mu[8], sc[8], sh[8];
+  float mu[8], iv[8], wv[8], bv[8];  // raw per-channel constants (combined after the wait)
 };
 
 template <int MODE>
@@ -206,8 +206,9 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       P.mu[i] = mp[i];
-      P.sc[i] = ip[i] * wp[i];
-      P.sh[i] = bp[i] - P.mu[i] * P.sc[i];
+      P.iv[i] = ip[i];
+      P.wv[i] = wp[i];
+      P.bv[i] = bp[i];
     }
   }
   const bf16_t* addp = static_cast<const bf16_t*>(ep.add);
@@ -255,6 +256,14 @@ __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restric
   // guarded stores and waited vmcnt(0), i.e. for the previous row's store, in front of
   // every row
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched
+  // the BN affine of the ReLU recompute, from the raw constants (arithmetic on them before
+  // this point made the compiler wait for every prefetched row in the prefetch itself)
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = P.iv[i] * P.wv[i];
+    sh[i] = P.bv[i] - P.mu[i] * sc[i];
+  }
 #pragma unroll
   for (int q = 0; q < PT::ROWS; ++q) {
     const int row = q * PT::RGS + rg;
@@ -282,7 +291,7 @@ __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restric
         const int i = 2 * k + h;
         bool keep = true;
         if constexpr (RM == 1) keep = (P.mk[q] >> i) & 1u;
-        else if constexpr (RM == 2) keep = fmaf(xx[h], P.sc[i], P.sh[i]) > 0.f;
+        else if constexpr (RM == 2) keep = fmaf(xx[h], sc[i], sh[i]) > 0.f;
         const bf16_t gb = (bf16_t)(keep ? o[h] : 0.f);
         const float gv = (float)gb;
         s1[i] += gv;
