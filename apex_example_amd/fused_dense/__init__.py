@@ -164,12 +164,19 @@ _DENSE_W4W = os.environ.get("APEX_AMD_DENSE_W4W", "1") == "1"
 _W4W_MIN_TILES = 48
 
 
+# workgroups per weight-gradient launch (one 256 x 256 tile per CU at 256): the kernel
+# holds 128 KB of LDS per workgroup for its whole K loop, so on the side stream a full
+# grid keeps the main stream's kernels off every CU until a tile finishes (A/B knob)
+_W4W_MAX_WG = int(os.environ.get("APEX_AMD_W4W_MAXWG", "256"))
+
+
 def _w4w_splits(T, o, i):
     """Row splits for wgrad4w: the largest power of two with splits x tiles <= 256 (one
     256 x 256 tile per CU), at least 1024 rows (16 K-tiles) per split."""
     tiles = (o // 256) * (i // 256)
     S = 1
-    while 2 * S * tiles <= 256 and T % (2 * S * 64) == 0 and T // (2 * S) >= 1024:
+    while (2 * S * tiles <= _W4W_MAX_WG and T % (2 * S * 64) == 0
+           and T // (2 * S) >= 1024):
         S *= 2
     return S
 
