@@ -164,24 +164,28 @@ _DENSE_W4W = os.environ.get("APEX_AMD_DENSE_W4W", "1") == "1"
 _W4W_MIN_TILES = 48
 
 
-# workgroups per weight-gradient launch (one 256 x 256 tile per CU at 256): the kernel
-# holds 128 KB of LDS per workgroup for its whole K loop, so on the side stream a full
-# grid keeps the main stream's kernels off every CU until a tile finishes (A/B knob)
+# workgroups per weight-gradient launch: 256 (one 256 x 256 tile per CU) on the main
+# stream; on the weight-gradient SIDE stream at most 128 - the kernel holds 128 KB of LDS
+# per workgroup for its whole K loop, so a full grid there keeps the main stream's
+# kernels (LayerNorm backward, attention, the data-gradient GEMMs) off every CU until a
+# tile finishes.  GPT-2-medium O1 (fp32 weight gradients on the side stream), same box:
+# 260.9 / 260.4 k tok/s with 256, 268.3 / 267.6 k with 128 (profiles/r5/ab_wg/).
 _W4W_MAX_WG = int(os.environ.get("APEX_AMD_W4W_MAXWG", "256"))
+_W4W_MAX_WG_SIDE = int(os.environ.get("APEX_AMD_W4W_MAXWG_SIDE", "128"))
 
 
-def _w4w_splits(T, o, i):
-    """Row splits for wgrad4w: the largest power of two with splits x tiles <= 256 (one
-    256 x 256 tile per CU), at least 1024 rows (16 K-tiles) per split."""
+def _w4w_splits(T, o, i, max_wg=None):
+    """Row splits for wgrad4w: the largest power of two with splits x tiles <= max_wg (256:
+    one 256 x 256 tile per CU), at least 1024 rows (16 K-tiles) per split."""
+    cap = _W4W_MAX_WG if max_wg is None else max_wg
     tiles = (o // 256) * (i // 256)
     S = 1
-    while (2 * S * tiles <= _W4W_MAX_WG and T % (2 * S * 64) == 0
-           and T // (2 * S) >= 1024):
+    while 2 * S * tiles <= cap and T % (2 * S * 64) == 0 and T // (2 * S) >= 1024:
         S *= 2
     return S
 
 
-def _wgrad_w4w(dy2, x2, dtype, out, accumulate):
+def _wgrad_w4w(dy2, x2, dtype, out, accumulate, side=False):
     """wgrad4w when the shapes / dtypes fit, else None."""
     if not (_DENSE_W4W and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
             and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
@@ -192,7 +196,7 @@ def _wgrad_w4w(dy2, x2, dtype, out, accumulate):
     if o % 256 or i % 256 or (o // 256) * (i // 256) < _W4W_MIN_TILES:
         return None
     dn = _native.require().dense
-    S = _w4w_splits(T, o, i)
+    S = _w4w_splits(T, o, i, _W4W_MAX_WG_SIDE if side else None)
     if not dn.wgrad4w_ok(dy2, x2, S):
         return None
     if out is not None and not out.is_contiguous():
@@ -201,14 +205,14 @@ def _wgrad_w4w(dy2, x2, dtype, out, accumulate):
     return out if out is not None else r
 
 
-def _wgrad(dy2, x2, dtype, out=None, accumulate=True):
+def _wgrad(dy2, x2, dtype, out=None, accumulate=True, side=False):
     """dW = dy2^T x2 written in the parameter's dtype by the GEMM itself (amp O1:
     fp16 operands, fp32 weight -> no separate fp16->fp32 cast of dW); split-K over
     the tokens when the output has too few tiles to fill the GPU.  ``out``: accumulate
     into that [o, i]-contiguous tensor (a DDP bucket view, see _direct_slots) and
     return it - the slab reduction or the GEMM's beta = 1 does the add; with
     ``accumulate=False`` (a lazily zeroed bucket view) overwrite it (beta = 0)."""
-    got = _wgrad_w4w(dy2, x2, dtype, out, accumulate)
+    got = _wgrad_w4w(dy2, x2, dtype, out, accumulate, side)
     if got is not None:
         return got
     if (_DENSE_SPLITK and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
@@ -270,7 +274,8 @@ def _side_wgrad(side, weight, w_dtype, dy2, x2):
     so, sa = _side_out(side, weight)
     if so is not None and so.dtype != w_dtype:
         so, sa = None, True
-    return lambda: _wgrad(dy2, x2, w_dtype, out=so, accumulate=sa)
+    on = bool(side is not None and side.on)
+    return lambda: _wgrad(dy2, x2, w_dtype, out=so, accumulate=sa, side=on)
 
 
 def _side_wgrad_bgrad(side, weight, w_dtype, b_dtype, dy2, x2):
@@ -278,7 +283,9 @@ def _side_wgrad_bgrad(side, weight, w_dtype, b_dtype, dy2, x2):
     so, sa = _side_out(side, weight)
     if so is None or so.dtype != w_dtype:
         return lambda: _wgrad_bgrad(dy2, x2, w_dtype, b_dtype)
-    return lambda: (_wgrad(dy2, x2, w_dtype, out=so, accumulate=sa), _bias_grad(dy2, b_dtype))
+    on = bool(side is not None and side.on)
+    return lambda: (_wgrad(dy2, x2, w_dtype, out=so, accumulate=sa, side=on),
+                    _bias_grad(dy2, b_dtype))
 
 
 def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):

@@ -19,3 +19,10 @@ def test_w4w_splits_invariants():
             tiles = (o // 256) * (i // 256)
             assert S >= 1 and (S == 1 or (S * tiles <= 256 and T % (S * 64) == 0
                                           and T // S >= 1024))
+
+
+def test_w4w_splits_side_stream_cap():
+    """On the weight-gradient side stream the grid is capped (128 workgroups by default)."""
+    assert FD._w4w_splits(8192, 4096, 1024, 128) == 2
+    assert FD._w4w_splits(16384, 3072, 1024, 128) == 2
+    assert FD._w4w_splits(16384, 4096, 1024, 64) == 1
