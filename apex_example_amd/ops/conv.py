@@ -261,9 +261,14 @@ def _wgrad_1x1_w(dy, x, weight, out=None, accumulate=True):
     return r if out is not None else r.view(weight.shape)
 
 
+# maximum row splits of the 1x1 weight gradients (A/B knob: the split-K GEMMs run on the
+# weight-gradient side stream, where a smaller grid leaves more CUs to the main stream)
+_SPLITK_MAX = int(os.environ.get("APEX_AMD_WGRAD1X1_MAXS", "128"))
+
+
 def _split_k(m):
     s = 1
-    while s < 128 and m % (2 * s) == 0 and m // (2 * s) >= 2048:
+    while s < _SPLITK_MAX and m % (2 * s) == 0 and m // (2 * s) >= 2048:
         s *= 2
     return s
 

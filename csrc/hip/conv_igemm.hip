@@ -1725,7 +1725,13 @@ int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int str
   const int64_t M = (int64_t)N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
   const int total_kt = (int)((M + c.BK - 1) / c.BK);
   const int gx = T * (Cout / c.BM) * (Cin / c.BN);
-  const int slots = c.BK * c.NB * (c.BM + c.BN) * 2 > 80 * 1024 ? 256 : 512;  // WGs per CU
+  int slots = c.BK * c.NB * (c.BM + c.BN) * 2 > 80 * 1024 ? 256 : 512;  // WGs per CU
+  // APEX_AMD_WGRAD3_SLOTS (A/B knob): size the split count for fewer resident workgroups
+  // (the kernel runs on the weight-gradient side stream beside the main stream's work)
+  if (const char* e = std::getenv("APEX_AMD_WGRAD3_SLOTS")) {
+    const int v = std::atoi(e);
+    if (v >= 64 && v < slots) slots = v;
+  }
   const double t_tile = 2.0 * c.BM * c.BN * c.BK / (4096.0 * 2400.0 * 0.5 / (slots / 256));  // us
   const double t_split = (double)T * Cout * Cin * 8.0 / 5.0e6;                     // us
   int best = 1;
