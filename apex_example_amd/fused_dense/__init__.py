@@ -484,11 +484,20 @@ def _g8_ok(a, b, *more):
     return dn.gemm4w_ok(a, b) if _G8_KERNEL == 1 else dn.gemm8p_ok(a, b)
 
 
+_T_KERNEL = os.environ.get("APEX_AMD_DENSE_T_KERNEL", "1") == "1"  # 0: ATen copy (A/B)
+
+
 def _transposed(w):
     """w^T contiguous, built on every call.  No cache: the fused optimizers and amp's
     master -> model copy write weights through their data pointers without bumping the
     version counter, so a cache keyed on (version, data_ptr) would go stale silently;
-    the transpose is one small pass (8 MB for a BERT-large W2) per backward."""
+    the transpose is one small pass (8 MB for a BERT-large W2) per backward - on the
+    64 x 64 LDS-tiled transpose kernel (conv.transpose_weight): ATen's strided copy took
+    25-33 us per layer for it (0.6 ms per BERT-large step, 0.8 ms per GPT-2-medium step)."""
+    if (_T_KERNEL and w.is_cuda and w.dim() == 2 and w.element_size() == 2
+            and w.is_contiguous() and _native.available()):
+        o, i = w.shape
+        return _native.require().conv.transpose_weight(w.view(o, i, 1, 1)).view(i, o)
     return w.t().contiguous()
 
 

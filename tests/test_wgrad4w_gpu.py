@@ -126,3 +126,14 @@ def test_dense_wgrad_small_weights_stay_on_library(monkeypatch):
     dy, x = _ops(4096, 1024, 1024, torch.bfloat16, 5)
     monkeypatch.setattr(FD, "_DENSE_W4W", True)
     assert FD._wgrad_w4w(dy, x, torch.bfloat16, None, True) is None
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(1024, 4096), (4096, 1024), (100, 200)])
+def test_dense_weight_transpose_kernel(shape, dtype):
+    """fused_dense._transposed: the tiled transpose kernel equals w.t() exactly."""
+    from apex_example_amd import fused_dense as FD
+    w = torch.randn(*shape, device=DEV).to(dtype)
+    t = FD._transposed(w)
+    assert t.is_contiguous() and t.shape == (shape[1], shape[0])
+    assert torch.equal(t, w.t())
