@@ -261,6 +261,20 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 
 // ---------------------------------------------------------------- backward (fast, fused)
 // part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
+// constant sources for the branch-free loads of ln_bwd_fast (absent gamma / dres)
+__device__ const float g_ln_ones_f[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+__device__ const unsigned short g_ln_ones_bf16[8] = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                     0x3F80, 0x3F80, 0x3F80, 0x3F80};
+__device__ const unsigned short g_ln_ones_f16[8] = {0x3C00, 0x3C00, 0x3C00, 0x3C00,
+                                                    0x3C00, 0x3C00, 0x3C00, 0x3C00};
+__device__ const float g_ln_zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+template <typename TW>
+__device__ __forceinline__ const TW* ln_ones() {
+  if constexpr (std::is_same<TW, float>::value) return g_ln_ones_f;
+  else if constexpr (std::is_same<TW, bf16_t>::value) return reinterpret_cast<const TW*>(g_ln_ones_bf16);
+  else return reinterpret_cast<const TW*>(g_ln_ones_f16);
+}
+
 template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
@@ -288,26 +302,33 @@ __global__ void __launch_bounds__(kLNThreads)
   for (int64_t row = row0; row < n1; row += wstride) {
     const float mu = rms ? 0.f : mean[row];
     const float iv = invvar[row];
-    float xv[VPT][8], dv[VPT][8];
+    // every load of the row first, unconditionally (clamped column, selected pointer for
+    // an absent gamma / residual gradient): with `if (col < n2)`, `if (gamma ...)` and
+    // `if (fu.dres)` around them the compiler waited vmcnt(0) after each group - about
+    // five serial memory round trips per row (ISA of the round-5 build)
+    float xv[VPT][8], dv[VPT][8], gv[VPT][8], ev[FUSE ? VPT : 1][8];
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      int col = (k * kWave + lane) * 8;
-      if (col < n2) {
-        load8(x + row * n2 + col, xv[k]);
-        load8(reinterpret_cast<const TY*>(dy) + row * n2 + col, dv[k]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) xv[k][i] = dv[k][i] = 0.f;
+      const int col = (k * kWave + lane) * 8;
+      const int cc = col < n2 ? col : 0;
+      load8(x + row * n2 + cc, xv[k]);
+      load8(reinterpret_cast<const TY*>(dy) + row * n2 + cc, dv[k]);
+      load8(gamma ? gamma + cc : ln_ones<TW>(), gv[k]);
+      if constexpr (FUSE) {
+        load8(fu.dres ? static_cast<const T*>(fu.dres) + row * n2 + cc
+                      : reinterpret_cast<const T*>(g_ln_zero), ev[k]);
       }
     }
     float s1 = 0.f, s2 = 0.f;  // sum(dy*g), sum(dy*g*xhat)
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      int col = (k * kWave + lane) * 8;
-      float g[8];
+      const float* g = gv[k];
+      // a column group past n2 read the clamped group 0: it contributes nothing (selected
+      // here, after the loads landed - overwriting the load targets right after the
+      // loads would make the compiler wait for them there)
+      const float ok = (k * kWave + lane) * 8 < n2 ? 1.f : 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = 1.f;
-      if (gamma && col < n2) load8(gamma + col, g);
+      for (int i = 0; i < 8; ++i) dv[k][i] *= ok;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float xh = (xv[k][i] - mu) * iv;
@@ -336,12 +357,8 @@ __global__ void __launch_bounds__(kLNThreads)
         o[i] = t * iv;
       }
       if constexpr (FUSE) {
-        if (fu.dres) {
-          float e[8];
-          load8(static_cast<const T*>(fu.dres) + row * n2 + col, e);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += e[i];
-        }
+        for (int i = 0; i < 8; ++i) o[i] += ev[k][i];  // zeros without a residual gradient
         const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
         float hd[8];
 #pragma unroll
