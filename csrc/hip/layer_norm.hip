@@ -78,6 +78,20 @@ __device__ __forceinline__ uint32_t drop_keep8(uint32_t seed, uint32_t thresh, i
 }
 
 // ---------------------------------------------------------------- forward (fast)
+// constant sources for the branch-free loads of the fast LayerNorm kernels (absent gamma / beta / dres)
+__device__ const float g_ln_ones_f[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+__device__ const unsigned short g_ln_ones_bf16[8] = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                     0x3F80, 0x3F80, 0x3F80, 0x3F80};
+__device__ const unsigned short g_ln_ones_f16[8] = {0x3C00, 0x3C00, 0x3C00, 0x3C00,
+                                                    0x3C00, 0x3C00, 0x3C00, 0x3C00};
+__device__ const float g_ln_zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+template <typename TW>
+__device__ __forceinline__ const TW* ln_ones() {
+  if constexpr (std::is_same<TW, float>::value) return g_ln_ones_f;
+  else if constexpr (std::is_same<TW, bf16_t>::value) return reinterpret_cast<const TW*>(g_ln_ones_bf16);
+  else return reinterpret_cast<const TW*>(g_ln_ones_f16);
+}
+
 template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_fwd_fast(const T* __restrict__ x, const TW* __restrict__ gamma, const TW* __restrict__ beta,
@@ -89,21 +103,28 @@ __global__ void __launch_bounds__(kLNThreads)
   const float inv_n = 1.f / (float)n2;
   for (int64_t row = row0; row < n1; row += wstride) {
     const T* xr = x + row * n2;
-    float v[VPT][8];
+    // the row's loads first, unconditionally (clamped column group): loads inside
+    // `if (col < n2)` with the residual store in between made the compiler wait for the
+    // previous group's store before each group's loads could be used (as in ln_bwd_fast)
+    float v[VPT][8], hv[FUSE ? VPT : 1][8];
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      int col = (k * kWave + lane) * 8;
+      const int col = (k * kWave + lane) * 8;
+      const int cc = col < n2 ? col : 0;
+      load8(xr + cc, v[k]);
+      if constexpr (FUSE) load8(static_cast<const TH*>(fu.h) + row * n2 + cc, hv[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int col = (k * kWave + lane) * 8;
       if (col < n2) {
-        load8(xr + col, v[k]);
         if constexpr (FUSE) {
           // s = residual + keep * h / (1 - p); s is the LayerNorm input (and the
           // new residual stream), written once for the backward / next sublayer
-          float hv[8];
-          load8(static_cast<const TH*>(fu.h) + row * n2 + col, hv);
           const uint32_t keep = drop_keep8(fu.seed, fu.thresh, row * n2 + col);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float t = v[k][i] + (((keep >> i) & 1u) ? hv[i] * fu.scale : 0.f);
+            const float t = v[k][i] + (((keep >> i) & 1u) ? hv[k][i] * fu.scale : 0.f);
             v[k][i] = to_f32(from_f32<T>(t));  // normalise s as stored, like the backward
           }
           store8(static_cast<T*>(fu.s) + row * n2 + col, v[k]);
@@ -145,15 +166,13 @@ __global__ void __launch_bounds__(kLNThreads)
     for (int k = 0; k < VPT; ++k) {
       int col = (k * kWave + lane) * 8;
       if (col >= n2) continue;
+      // gamma / beta through selected pointers (1 / 0 when absent): no branch joins
       float g[8], b[8];
-      if (gamma) load8(gamma + col, g);
-      if (beta) load8(beta + col, b);
+      load8(gamma ? gamma + col : ln_ones<TW>(), g);
+      load8(beta ? beta + col : reinterpret_cast<const TW*>(g_ln_zero), b);
       float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float xh = (v[k][i] - mu) * iv;
-        o[i] = gamma ? fmaf(xh, g[i], beta ? b[i] : 0.f) : xh;
-      }
+      for (int i = 0; i < 8; ++i) o[i] = fmaf((v[k][i] - mu) * iv, g[i], b[i]);
       store8(yr + col, o);
     }
   }
@@ -261,20 +280,6 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 
 // ---------------------------------------------------------------- backward (fast, fused)
 // part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
-// constant sources for the branch-free loads of ln_bwd_fast (absent gamma / dres)
-__device__ const float g_ln_ones_f[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-__device__ const unsigned short g_ln_ones_bf16[8] = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
-                                                     0x3F80, 0x3F80, 0x3F80, 0x3F80};
-__device__ const unsigned short g_ln_ones_f16[8] = {0x3C00, 0x3C00, 0x3C00, 0x3C00,
-                                                    0x3C00, 0x3C00, 0x3C00, 0x3C00};
-__device__ const float g_ln_zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-template <typename TW>
-__device__ __forceinline__ const TW* ln_ones() {
-  if constexpr (std::is_same<TW, float>::value) return g_ln_ones_f;
-  else if constexpr (std::is_same<TW, bf16_t>::value) return reinterpret_cast<const TW*>(g_ln_ones_bf16);
-  else return reinterpret_cast<const TW*>(g_ln_ones_f16);
-}
-
 template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T>
 __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
