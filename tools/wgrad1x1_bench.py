@@ -40,6 +40,11 @@ def main():
     ap.add_argument("--splits", default="256,512")
     ap.add_argument("--dense", action="store_true",
                     help="the transformer dense-layer weight gradients instead (T tokens)")
+    ap.add_argument("--w4w", action="store_true",
+                    help="1x1 shapes: add the wgrad4w kernel where both channel counts are "
+                         "multiples of 256")
+    ap.add_argument("--shapes", default="",
+                    help="comma-separated indices into SHAPES (default: all)")
     ap.add_argument("--own-only", action="store_true",
                     help="--dense: only the default split and the own kernel")
     ap.add_argument("--tuned", default="",
@@ -73,7 +78,8 @@ def main():
     if args.dense:
         return dense(args, cv, forced)
     rows = []
-    for (ci, co, hw, st, calls) in SHAPES:
+    pick = [int(i) for i in args.shapes.split(",") if i] or range(len(SHAPES))
+    for (ci, co, hw, st, calls) in [SHAPES[i] for i in pick]:
         n = args.batch
         g = torch.Generator(device=dev).manual_seed(ci * 7 + co)
         x = torch.randn(n, ci, hw, hw, device=dev, generator=g).to(
@@ -89,6 +95,18 @@ def main():
             if m % s == 0 and s != C._split_k(m):
                 cands["splitk(S=%d)" % s] = (lambda s=s: forced(dyr, xr, s))
         cands["own tap"] = lambda: cv.conv_wgrad(dy, x, torch.bfloat16, 0, 1, 1)
+        if args.w4w:
+            # the dense weight-gradient GEMM (csrc/hip/wgrad4w.hip) at split counts that
+            # put 64-512 workgroups on the 256 x 256 output tiles
+            dn = _native_dense()
+            tiles = (co // 256) * (ci // 256) if co % 256 == 0 and ci % 256 == 0 else 0
+            ok = [s for s in range(1, 1025) if tiles and 64 <= tiles * s <= 640 and
+                  m % (64 * s) == 0 and dn.wgrad4w_ok(dyr, xr, s)]
+            for target in (128, 256, 384, 512):
+                if ok:
+                    s = min(ok, key=lambda s: abs(tiles * s - target))
+                    cands["w4w(S=%d)" % s] = (lambda s=s: dn.wgrad4w(
+                        dyr, xr, s, torch.bfloat16))
         for name, fn in cands.items():
             out = fn().float().reshape(co, ci)
             err = float((out - ref).abs().max()) / scale
