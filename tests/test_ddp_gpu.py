@@ -8,6 +8,7 @@ skew, every grad checked against a closed form right after backward, and the
 bucket buffers consumed immediately by an in-place op.  The bf16 variant
 reduces through a separate fp32 staging tensor, so a missing stream join shows
 up as stale gradients."""
+import math
 import os
 
 import pytest
@@ -351,6 +352,34 @@ def test_bench_self_spawn_two_ranks_one_gpu():
     assert rec["n_gpus"] == 2 and rec["launcher"] == "self-spawn"
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["syncbn"]
     assert rec["ddp"]["buckets"] >= 1 and rec["ddp"]["exposed_tail_ms"] >= 0
+
+
+@pytest.mark.timeout(280)
+@pytest.mark.parametrize("model", ["bert_large", "gpt2_medium"])
+def test_bench_transformers_two_ranks_one_gpu(model):
+    """The transformer bench configs at world 2 (BASELINE: BERT-large O2 FusedLAMB and
+    GPT-2-medium O1 FusedAdam on 8 GPUs): full-size models, short sequences, both ranks
+    on cuda:0 over gloo - apex DDP with the direct dense weight-gradient path, the
+    side-stream wgrad4w calls, the tied-embedding bucket and the fused optimizers at N > 1.
+    The loss must be finite and the JSON must carry the DDP timing block."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, APEX_AMD_SINGLE_DEVICE="1", APEX_AMD_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    shape = ["--batch-size", "2", "--seq-len", "128"] if model == "bert_large" else \
+        ["--batch-size", "1", "--seq-len", "256", "--allow-skipped-steps"]
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--model", model, "--steps", "2", "--warmup", "2",
+                        "--bucket-timing-steps", "1", "--opt-step-iters", "1",
+                        "--message-size", str(8 << 20)] + shape,
+                       env=env, capture_output=True, text=True, timeout=260)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert math.isfinite(rec["final_loss"]) and rec["ddp"]["buckets"] >= 1
 
 
 @pytest.mark.parametrize("residual", [False, True])
