@@ -34,6 +34,16 @@
 // 2 = whole 512-byte rows, two per DMA instruction (chunk key 2 ((r & 3) | (r >> 3 & 1) << 2)).
 // All three read conflict-free and are bitwise equal (tests/test_wgrad4w_gpu.py).
 //
+// Variant 3 (APEX_AMD_W4W_LAYOUT=3) is layout 0 with the slot released per HALF K-tile:
+// wave w DMAs chunk groups 2w, 2w+1 of every row group (instead of row group w), so the
+// rows 0-31 of K-tile t+2 go out during k-step 0 of K-tile t (their half of the slot is
+// free once k-step 0's fragments were read) and rows 32-63 during k-step 1; a barrier
+// after each k-step, both behind the same s_waitcnt vmcnt(16).  A DMA piece then has 1.5
+// K-tiles to land instead of ~1: at full load a K-tile took 1.4-1.9 us against 1.15 us for
+// one workgroup, which looked like the loop waiting on loaded memory latency.  Measured
+// (profiles/r5/wgrad_dense/variant3_sweep.txt): within -3..+2 % of layout 0 on every BERT /
+// GPT-2 shape, so the slack was not the limit; it stays an A/B variant, bitwise equal.
+//
 // Status (round 5, profiles/r5/wgrad_dense.md): BERT-large FFN weight gradient 114.5 us
 // (1.20 PF, reduction included) vs 136.8 us for hipBLASLt's best split; one workgroup runs
 // a K-tile in 1.15 us against 0.85 us of MFMA issue.  The first build ran 3.3 us per K-tile
@@ -130,9 +140,11 @@ __device__ __forceinline__ V8 ww_frag(const unsigned char* p) {
   return f;
 }
 
-template <typename TT, int L>
+template <typename TT, int LV>
 __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only needs the launch stub)
+  constexpr int L = LV == 3 ? 0 : LV;  // LDS layout
+  constexpr bool HB = LV == 3;         // half-K-tile slot release (variant 3)
   typedef typename WwT<TT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kWwSlot];
 
@@ -180,7 +192,8 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
   for (int h = 0; h < 2; ++h) {
     int drow, dch;
     if constexpr (L == 0) {
-      drow = wid * 16 + (lane >> 2);
+      // (variant 3: the row group goes into the soffset, see piece_hb)
+      drow = (HB ? 0 : wid * 16) + (lane >> 2);
       dch = (lane & 3) ^ (((lane >> 5) & 1) << 1);
     } else {
       drow = (2 * wid + h) * 8 + (lane >> 3);
@@ -210,6 +223,22 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
       ww_dma(rA, dst, offA[h], (uint32_t)Tc * strideA + cgo);
     } else {
       ww_dma(rB, dst, offB[h], (uint32_t)Tc * strideB + cgo);
+    }
+  };
+  // variant 3: piece j (0..3 A, 4..7 B) of half hf of K-tile T: block (row group
+  // rg = 2 hf + (j >> 1 & 1), chunk group cg = 2 wid + (j & 1)) - the same LDS image as
+  // layout 0, every wave filling both halves
+  const uint32_t rowgA = 16u * (uint32_t)p.lda * (uint32_t)sizeof(TT);
+  const uint32_t rowgB = 16u * (uint32_t)p.ldb * (uint32_t)sizeof(TT);
+  auto piece_hb = [&](int T, int hf, int j) {
+    const int Tc = T < KT ? T : KT - 1;
+    const int rg = 2 * hf + ((j >> 1) & 1), cg = 2 * wid + (j & 1);
+    const uint32_t dst =
+        lds_base + (uint32_t)((T & 1) * kWwSlot + (j >> 2) * kWwOp + (rg * 8 + cg) * 1024);
+    if (j < 4) {
+      ww_dma(rA, dst, offA[0], (uint32_t)Tc * strideA + (uint32_t)rg * rowgA + (uint32_t)cg * 64u);
+    } else {
+      ww_dma(rB, dst, offB[0], (uint32_t)Tc * strideB + (uint32_t)rg * rowgB + (uint32_t)cg * 64u);
     }
   };
 
@@ -256,14 +285,29 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
   f32x4_t acc[8][8];
 
   // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed, its k-step-0 fragments read
+  if constexpr (HB) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) piece(0, q);
+    for (int T = 0; T < 2; ++T)
 #pragma unroll
-  for (int q = 0; q < 16; ++q) piece(1, q);
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) piece_hb(T, hf, j);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) piece(0, q);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) piece(1, q);
+  }
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   ww_barrier();
 #pragma unroll
   for (int n = 0; n < 16; ++n) rd(0, 0, rd_order(n), fa0, fb0);
+  if constexpr (HB) {
+    // K-tile 2's first half goes into rows 0-31 of slot 0 during k-step 0: every wave's
+    // k-step-0 reads of them must have retired
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ww_barrier();
+  }
 
 #define WW_GROUP(FA, FB, g, OP)                                              \
   _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                         \
@@ -287,18 +331,39 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
       rd(slot, 1, rd_order(g), fa1, fb1);
+      if constexpr (HB) {
+        if ((g & 1) == 0) piece_hb(t + 2, 0, g >> 1);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (HB) {
+      // K-tile t+1's first half landed (issued after it: its second half and K-tile
+      // t+2's first half, 8 pieces each)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     ww_barrier();
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       WW_GROUP(fa1, fb1, g, mma);
       __builtin_amdgcn_sched_barrier(0);
       rd(slot ^ 1, 0, rd_order(g), fa0, fb0);
-      piece(t + 2, g);
+      if constexpr (HB) {
+        if ((g & 1) == 0) piece_hb(t + 2, 1, g >> 1);
+      } else {
+        piece(t + 2, g);
+      }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (HB) {
+      // K-tile t+1's second half landed for the next k-step-0 reads (issued after it: both
+      // halves of K-tile t+2), and this k-step's reads of K-tile t+1's first half retired
+      // in every wave: K-tile t+3's first half overwrites them during the next k-step 0
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      ww_barrier();
     }
   };
   ktile(0, std::true_type{});
@@ -352,6 +417,8 @@ void wgrad4w(const WgradArgs& a0, hipStream_t st) {
     using TT = decltype(t0);
     if (lay == 0)
       hipLaunchKernelGGL((wgrad4w_k<TT, 0>), dim3(grid), dim3(kWwT), 0, st, a);
+    else if (lay == 3)
+      hipLaunchKernelGGL((wgrad4w_k<TT, 3>), dim3(grid), dim3(kWwT), 0, st, a);
     else if (lay == 2)
       hipLaunchKernelGGL((wgrad4w_k<TT, 2>), dim3(grid), dim3(kWwT), 0, st, a);
     else

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """wgrad4w tile order at full load: the XCD-grouped walk (APEX_AMD_W4W_GROUPM m-tiles per
-group, read per launch) swept over the BERT / GPT-2 weight-gradient shapes at the split
+group, read per launch; or another per-launch knob given as the 2nd argument, e.g.
+APEX_AMD_W4W_LAYOUT) swept over the BERT / GPT-2 weight-gradient shapes at the split
 counts the model uses, interleaved rounds in one process (same clocks for every row)."""
 import os
 import sys
@@ -31,13 +32,14 @@ def main():
     from apex_example_amd import _native
     dn = _native.require().dense
     groups = [int(g) for g in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8,16").split(",")]
+    var = sys.argv[2] if len(sys.argv) > 2 else "APEX_AMD_W4W_GROUPM"  # or ..._LAYOUT
     for (name, T, m, n, s) in SHAPES:
         dy = torch.randn(T, m, device="cuda").to(torch.bfloat16)
         x = torch.randn(T, n, device="cuda").to(torch.bfloat16)
         best = {g: 1e9 for g in groups}
         for _ in range(3):
             for g in groups:
-                os.environ["APEX_AMD_W4W_GROUPM"] = str(g)
+                os.environ[var] = str(g)
                 best[g] = min(best[g], timeit(lambda: dn.wgrad4w(dy, x, s, torch.bfloat16)))
         gf = 2.0 * T * m * n / 1e9
         print("| %s | S=%d | %s |" % (name, s, " | ".join(
