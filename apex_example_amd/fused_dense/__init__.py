@@ -31,7 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
-from ..ops import _ddp_direct
+from ..ops import _bias_handoff, _ddp_direct
 from ..ops.conv import _SideWgrad, _side_out
 
 __all__ = ["FusedDense", "FusedDenseGeluDense", "DenseNoBias", "fused_dense_function", "cast_params_once",
@@ -301,6 +301,9 @@ def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):
 
 
 def _bias_grad(g2, dtype):
+    hs = _bias_handoff.take(g2, dtype)  # summed by the residual join's backward already
+    if hs is not None:
+        return hs
     if g2.is_cuda and _native.available():
         return _native.require().dense.bias_grad(g2, dtype)
     return g2.to(torch.promote_types(g2.dtype, torch.float32)).sum(0).to(dtype)

@@ -15,6 +15,7 @@ from torch.nn import init
 from torch.nn.parameter import Parameter
 
 from .. import _native
+from ..ops import _bias_handoff
 from ..ops.conv import gate_side_stream
 
 
@@ -125,9 +126,16 @@ class AddDropoutLayerNormFunction(torch.autograd.Function):
         n2, p, seed, h_dtype = ctx.cfg
         if dy is None:
             dy = torch.zeros_like(s)
-        ds, dh, dw, db = C.add_dropout_backward(dy, s, mean, invvar, n2, weight, ds_ext, p, seed,
-                                                ctx.needs_input_grad[2], ctx.needs_input_grad[3],
-                                                h_dtype)
+        # the column sums of dh (the producing dense layer's bias gradient) ride on the
+        # dgamma / dbeta partials: ops/_bias_handoff.py
+        want_hs = (_bias_handoff.ENABLED and ctx.needs_input_grad[1] and weight is not None
+                   and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]))
+        ds, dh, dw, db, dhs = C.add_dropout_backward(dy, s, mean, invvar, n2, weight, ds_ext, p,
+                                                     seed, ctx.needs_input_grad[2],
+                                                     ctx.needs_input_grad[3], h_dtype,
+                                                     bool(want_hs))
+        if want_hs:
+            _bias_handoff.offer(dh, dhs)
         gate_side_stream(ds)
         return ds, dh, dw, db, None, None, None, None
 

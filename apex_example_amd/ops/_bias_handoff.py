@@ -1,0 +1,46 @@
+"""Bias gradient handed from a fused residual join to the dense layer that produced h.
+
+A post-/pre-LN transformer sublayer ends in ``dense -> dropout -> (+ residual) -> LN``
+(``normalization.fused_add_dropout_layer_norm``).  Its backward kernel forms
+dh = dropout'(ds) row by row and already reduces dgamma / dbeta partials per block;
+with ``APEX_AMD_LN_HSUM`` (default on) it also sums dh's columns in the same pass -
+which is exactly the bias gradient of the dense layer whose output h was.  The dense
+backward (``fused_dense._bias_grad``) then takes that result instead of re-reading
+dh for its own column-sum pass (``csrc/hip/bias_grad.hip``: one full read of dh plus a
+second small kernel per layer).
+
+One slot: the join's backward offers (dh, its version, colsum); the next bias gradient
+over exactly that tensor (same storage address and element count, not modified in
+place since) takes it.  The slot holds a reference to dh, so its address cannot be
+reused by another tensor while the offer stands; any other consumer pattern (dh summed
+with another gradient, cast, sliced) simply misses and computes the sum itself.
+"""
+from __future__ import annotations
+
+import os
+
+ENABLED = os.environ.get("APEX_AMD_LN_HSUM", "1") == "1"
+
+_SLOT = [None]
+
+
+def offer(dh, colsum):
+    _SLOT[0] = (dh, dh._version, colsum) if colsum is not None else None
+
+
+def take(g2, dtype):
+    """colsum(g2) computed by the join's backward, or None."""
+    ent = _SLOT[0]
+    if ent is None:
+        return None
+    dh, ver, cs = ent
+    if (g2.data_ptr() == dh.data_ptr() and g2.numel() == dh.numel() and dh._version == ver
+            and g2.dim() == 2 and g2.size(1) == cs.numel() and cs.dtype == dtype
+            and g2.device == cs.device):
+        _SLOT[0] = None
+        return cs
+    return None
+
+
+def clear():
+    _SLOT[0] = None

@@ -279,14 +279,18 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 }
 
 // ---------------------------------------------------------------- backward (fast, fused)
-// part layout: [nblocks][2][n2]  (dgamma partial, dbeta partial)
-template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T>
+// part layout: [nblocks][R][n2]  (dgamma partial, dbeta partial[, dh partial]); R = 3 with
+// HS (fused join: the column sums of dh = the producing dense layer's bias gradient, so
+// that layer skips its own column-sum pass over dh)
+template <typename T, typename TW, int VPT, bool FUSE = false, typename TH = T, typename TY = T,
+          bool HS = false>
 __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
                 const float* __restrict__ mean, const float* __restrict__ invvar,
                 T* __restrict__ dx, float* __restrict__ part, int64_t n1, int n2, int rms,
                 LnFuse fu = LnFuse{}) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [kLNWaves][2][n2]
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [kLNWaves][R][n2]
+  constexpr int R = HS ? 3 : 2;
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   const int64_t row0 = (int64_t)blockIdx.x * kLNWaves + wid;
@@ -298,11 +302,17 @@ __global__ void __launch_bounds__(kLNThreads)
   // only a few rows): gamma is NOT kept across rows - it is loaded 8 columns at a
   // time where dg = dy*gamma is formed and dg overwrites dy; xhat overwrites x.
   // 142 -> ~100 VGPRs for the fp32 GPT-2 joins (3 -> 5 waves per SIMD).
-  float adg[VPT][8], adb[VPT][8];
+  float adg[VPT][8], adb[VPT][8], adh[HS ? VPT : 1][8];
 #pragma unroll
   for (int k = 0; k < VPT; ++k)
 #pragma unroll
     for (int i = 0; i < 8; ++i) adg[k][i] = adb[k][i] = 0.f;
+  if constexpr (HS) {
+#pragma unroll
+    for (int k = 0; k < VPT; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) adh[k][i] = 0.f;
+  }
 
   for (int64_t row = row0; row < n1; row += wstride) {
     const float mu = rms ? 0.f : mean[row];
@@ -368,6 +378,11 @@ __global__ void __launch_bounds__(kLNThreads)
         float hd[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) hd[i] = ((keep >> i) & 1u) ? o[i] * fu.scale : 0.f;
+        if constexpr (HS) {
+          // the bias gradient sums dh as stored (rounded to TH), like a pass over dh would
+#pragma unroll
+          for (int i = 0; i < 8; ++i) adh[k][i] += to_f32(from_f32<TH>(hd[i]));
+        }
         store8(static_cast<TH*>(fu.dh) + row * n2 + col, hd);
       }
       store8(dxr + col, o);
@@ -376,7 +391,7 @@ __global__ void __launch_bounds__(kLNThreads)
 
   if (!want_part) return;
   // combine the block's waves in LDS, then one partial row pair per block
-  float* my = lds + (size_t)wid * 2 * n2;
+  float* my = lds + (size_t)wid * R * n2;
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     int col = (k * kWave + lane) * 8;
@@ -385,14 +400,15 @@ __global__ void __launch_bounds__(kLNThreads)
     for (int i = 0; i < 8; ++i) {
       my[col + i] = adg[k][i];
       my[n2 + col + i] = adb[k][i];
+      if constexpr (HS) my[2 * n2 + col + i] = adh[k][i];
     }
   }
   __syncthreads();
-  float* out = part + (size_t)blockIdx.x * 2 * n2;
-  for (int c = threadIdx.x; c < 2 * n2; c += blockDim.x) {
+  float* out = part + (size_t)blockIdx.x * R * n2;
+  for (int c = threadIdx.x; c < R * n2; c += blockDim.x) {
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < kLNWaves; ++w) s += lds[(size_t)w * 2 * n2 + c];
+    for (int w = 0; w < kLNWaves; ++w) s += lds[(size_t)w * R * n2 + c];
     out[c] = s;
   }
 }
@@ -452,7 +468,7 @@ __global__ void __launch_bounds__(kLNThreads)
 }
 
 // sum nparts partial rows -> dgamma, dbeta (TW); fixed order -> deterministic.
-// A partial row is [dgamma(n2) | dbeta(n2)] = 2*n2 contiguous floats.  Block =
+// A partial row is [dgamma(n2) | dbeta(n2) (| dh sums(n2))] = R*n2 contiguous floats.  Block =
 // 8 column lanes x 32 row lanes; a lane owns 4 adjacent columns (one 16-byte
 // load per partial row when n2 is even), the 32 row lanes stride over the
 // partials and are combined through LDS.  Grid = ceil(2*n2 / 32) blocks.
@@ -461,11 +477,11 @@ constexpr int kCSColLanes = 8, kCSRowLanes = 32, kCSCols = 4 * kCSColLanes;
 template <typename TW, bool VEC4>
 __global__ void __launch_bounds__(256)
     ln_bwd_colsum(const float* __restrict__ part, int nparts, int n2, TW* __restrict__ dgamma,
-                  TW* __restrict__ dbeta) {
+                  TW* __restrict__ dbeta, TW* __restrict__ dhsum = nullptr, int R = 2) {
   __shared__ float4 red[kCSRowLanes][kCSColLanes];
   const int cl = threadIdx.x % kCSColLanes;
   const int rl = threadIdx.x / kCSColLanes;
-  const int width = 2 * n2;
+  const int width = R * n2;
   const int c0 = blockIdx.x * kCSCols + cl * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c0 < width) {
@@ -514,8 +530,10 @@ __global__ void __launch_bounds__(256)
       if (c >= width) break;
       if (c < n2) {
         if (dgamma) dgamma[c] = from_f32<TW>(v[i]);
-      } else if (dbeta) {
-        dbeta[c - n2] = from_f32<TW>(v[i]);
+      } else if (c < 2 * n2) {
+        if (dbeta) dbeta[c - n2] = from_f32<TW>(v[i]);
+      } else if (dhsum) {
+        dhsum[c - 2 * n2] = from_f32<TW>(v[i]);
       }
     }
   }
@@ -544,7 +562,7 @@ static inline int ln_generic_parts(int64_t n1) {
 }
 
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2) {
-  int64_t a = (int64_t)ln_bwd_blocks(n1) * 2 * n2;
+  int64_t a = (int64_t)ln_bwd_blocks(n1) * 3 * n2;  // (3 rows: with the dh column sums)
   int64_t b = (int64_t)ln_generic_parts(n1) * 2 * n2;
   return a > b ? a : b;
 }
@@ -555,6 +573,8 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
                     const LnFuse* fuse) {
   if (n1 == 0 || n2 == 0) return;
   const bool want_wb = dgamma != nullptr || dbeta != nullptr;
+  // the dh column sums ride on the dgamma / dbeta partials (fused join only)
+  const int R = (fuse && fuse->dhsum && want_wb) ? 3 : 2;
   ln_dispatch(tx, [&](auto t0) {
     ln_dispatch(tw, [&](auto w0) {
       using T = decltype(t0);
@@ -566,19 +586,24 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
       int nparts;
       if (fuse) {  // caller checked alignment / width (layer_norm_fused_ok + dy, dres, dh)
         int blocks = ln_bwd_blocks(n1);
-        size_t lds = want_wb ? (size_t)kLNWaves * 2 * n2 * sizeof(float) : 0;
+        size_t lds = want_wb ? (size_t)kLNWaves * R * n2 * sizeof(float) : 0;
         float* pp = want_wb ? part : nullptr;
         dim3 grid(blocks), block(kLNThreads);
         auto launch = [&](auto h0) {
           using TH = decltype(h0);
           ln_fuse_y_dispatch<T, TH>(fuse->ty, [&](auto y0) {
           using TY = decltype(y0);
-          switch (ln_vpt(n2)) {
-            case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-            case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-            case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-            default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH, TY>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-          }
+          auto go = [&](auto hs0) {
+            constexpr bool HS = decltype(hs0)::value;
+            switch (ln_vpt(n2)) {
+              case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+              case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+              case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+              default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+            }
+          };
+          if (R == 3) go(std::true_type{});
+          else go(std::false_type{});
           });
         };
         ln_fuse_h_dispatch<T>(fuse->th, launch);
@@ -608,13 +633,14 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
         }
       }
       if (want_wb) {
-        dim3 cgrid((unsigned)((2 * n2 + kCSCols - 1) / kCSCols));
+        TW* dhs = R == 3 ? static_cast<TW*>(fuse->dhsum) : nullptr;
+        dim3 cgrid((unsigned)((R * n2 + kCSCols - 1) / kCSCols));
         if (n2 % 2 == 0 && ((uintptr_t)part % 16) == 0)
           hipLaunchKernelGGL((ln_bwd_colsum<TW, true>), cgrid, dim3(256), 0, st, part, nparts,
-                             (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta));
+                             (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta), dhs, R);
         else
           hipLaunchKernelGGL((ln_bwd_colsum<TW, false>), cgrid, dim3(256), 0, st, part, nparts,
-                             (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta));
+                             (int)n2, static_cast<TW*>(dgamma), static_cast<TW*>(dbeta), dhs, R);
       }
     });
   });

@@ -174,6 +174,8 @@ struct LnFuse {
                                   // stream may take an F16 / BF16 sublayer output (amp O1)
   int ty = -1;                    // >= 0 (mixed only): y / dy are in h's 16-bit type, the
                                   // dtype the consuming autocast GEMM reads (no cast kernel)
+  void* dhsum = nullptr;          // bwd (with dgamma / dbeta): column sums of dh in gamma's
+                                  // dtype - the bias gradient of the dense layer producing h
 };
 // fast-path requirements of the fused residual+dropout LayerNorm (16-B aligned, n2 % 8 == 0, <= 2048)
 bool layer_norm_fused_ok(const void* x, const void* h, const void* s, const void* gamma,

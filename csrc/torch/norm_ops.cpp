@@ -128,10 +128,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   return {y, s, mean, invvar};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
-    at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
-    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad,
-    c10::optional<at::ScalarType> h_dtype) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
+add_dropout_layer_norm_backward_op(at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar,
+                                   int64_t n2, OptT gamma, OptT dres, double p, int64_t seed,
+                                   bool need_wgrad, bool need_bgrad,
+                                   c10::optional<at::ScalarType> h_dtype, bool need_hsum) {
   TORCH_CHECK(s.is_cuda(), "add_dropout_layer_norm: GPU tensors only");
   s = s.contiguous();
   dy = dy.contiguous();
@@ -153,9 +154,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
   DType tw = g.defined() ? dtype_of(g) : DType::F32;
   if (need_wgrad && g.defined()) dgam = at::empty_like(g);
   if (need_bgrad && g.defined()) dbet = at::empty_like(g);
+  // column sums of dh (in gamma's dtype) with the dgamma / dbeta partials: the bias
+  // gradient of the dense layer whose output h is (fused_dense picks it up)
+  at::Tensor dhs;
+  if (need_hsum && (dgam.defined() || dbet.defined())) dhs = at::empty_like(g);
   if (dgam.defined() || dbet.defined())
     part = at::empty({layer_norm_bwd_workspace(n1, n2)}, s.options().dtype(at::kFloat));
   LnFuse f = make_fuse(p, seed);
+  f.dhsum = dhs.defined() ? dhs.data_ptr() : nullptr;
   f.dres = e.defined() ? e.data_ptr() : nullptr;
   f.dh = dh.data_ptr();
   if (mixed) f.th = (int)dtype_of(dh);
@@ -167,7 +173,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_nor
                  dgam.defined() ? dgam.data_ptr() : nullptr,
                  dbet.defined() ? dbet.data_ptr() : nullptr,
                  part.defined() ? part.data_ptr<float>() : nullptr, n1, n2, 0, cur_stream(), &f);
-  return {ds, dh, dgam, dbet};
+  return {ds, dh, dgam, dbet, dhs};
 }
 
 // ============================================================================ BatchNorm

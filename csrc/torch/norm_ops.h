@@ -21,11 +21,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layer_norm_backward_op(
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_forward_op(
     at::Tensor x, at::Tensor h, int64_t n2, OptT gamma, OptT beta, double eps, double p,
     int64_t seed, bool y_as_h);
-// -> (ds = LN'(dy) + dres, dh = dropout'(ds), dgamma, dbeta)
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_dropout_layer_norm_backward_op(
-    at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar, int64_t n2, OptT gamma,
-    OptT dres, double p, int64_t seed, bool need_wgrad, bool need_bgrad,
-    c10::optional<at::ScalarType> h_dtype);
+// -> (ds = LN'(dy) + dres, dh = dropout'(ds), dgamma, dbeta, colsum(dh) if need_hsum)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
+add_dropout_layer_norm_backward_op(at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor invvar,
+                                   int64_t n2, OptT gamma, OptT dres, double p, int64_t seed,
+                                   bool need_wgrad, bool need_bgrad,
+                                   c10::optional<at::ScalarType> h_dtype, bool need_hsum);
 
 // BatchNorm building blocks (local / synchronized).
 std::tuple<at::Tensor, at::Tensor> bn_local_stats_op(at::Tensor x);

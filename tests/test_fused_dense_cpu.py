@@ -180,3 +180,24 @@ def test_skip_functions_when_dskip_aliases_dy(gelu):
     (ref + x).pow(2).sum().backward()
     for g, t in zip(got, params):
         torch.testing.assert_close(g, t.grad)
+
+
+def test_bias_handoff_take_rules_cpu():
+    """ops/_bias_handoff: the offered column sums go to exactly the offered tensor, once,
+    and only while it is unmodified and the dtypes match."""
+    from apex_example_amd.ops import _bias_handoff as H
+
+    dh = torch.randn(64, 32)
+    cs = dh.sum(0)
+    H.offer(dh, cs)
+    assert H.take(dh.view(64, 32).contiguous(), torch.float32) is cs
+    assert H.take(dh, torch.float32) is None  # taken once
+    H.offer(dh, cs)
+    assert H.take(dh, torch.bfloat16) is None  # dtype mismatch
+    assert H.take(torch.randn(64, 32), torch.float32) is None  # another tensor
+    assert H.take(dh[:32], torch.float32) is None  # a slice
+    dh.mul_(2)  # modified in place after the offer
+    assert H.take(dh, torch.float32) is None
+    H.offer(dh, None)
+    assert H.take(dh, torch.float32) is None
+    H.clear()
