@@ -185,8 +185,15 @@ def _w4w_splits(T, o, i, max_wg=None):
     return S
 
 
-def _wgrad_w4w(dy2, x2, dtype, out, accumulate, side=False):
-    """wgrad4w when the shapes / dtypes fit, else None."""
+# The bias gradient of a wgrad4w layer from the kernel's own dY fragments (column sums via
+# v_dot2 next to the MFMAs, csrc/hip/wgrad4w.hip variant 4) instead of a separate
+# column-sum pass over dy.  APEX_AMD_W4W_BIAS=0 disables.
+_W4W_BIAS = os.environ.get("APEX_AMD_W4W_BIAS", "1") == "1"
+
+
+def _wgrad_w4w(dy2, x2, dtype, out, accumulate, side=False, b_dtype=None):
+    """wgrad4w when the shapes / dtypes fit, else None; with ``b_dtype`` the pair
+    (dW, db) with db = column sums of dy2 formed inside the same kernel."""
     if not (_DENSE_W4W and dy2.is_cuda and dtype in (torch.bfloat16, torch.float32)
             and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
             and _native.available()):
@@ -201,6 +208,12 @@ def _wgrad_w4w(dy2, x2, dtype, out, accumulate, side=False):
         return None
     if out is not None and not out.is_contiguous():
         return None
+    if b_dtype is not None:
+        if b_dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            return None
+        r, db = dn.wgrad4w_bias(dy2, x2, S, dtype, out=out, accumulate=accumulate,
+                                bias_dtype=b_dtype)
+        return (out if out is not None else r), db
     r = dn.wgrad4w(dy2, x2, S, dtype, out=out, accumulate=accumulate)
     return out if out is not None else r
 
@@ -284,8 +297,7 @@ def _side_wgrad_bgrad(side, weight, w_dtype, b_dtype, dy2, x2):
     if so is None or so.dtype != w_dtype:
         return lambda: _wgrad_bgrad(dy2, x2, w_dtype, b_dtype)
     on = bool(side is not None and side.on)
-    return lambda: (_wgrad(dy2, x2, w_dtype, out=so, accumulate=sa, side=on),
-                    _bias_grad(dy2, b_dtype))
+    return lambda: _wgrad_bgrad(dy2, x2, w_dtype, b_dtype, out=so, accumulate=sa, side=on)
 
 
 def _wgrad_maybe_direct(side, weight, w_dtype, dy2, x2, *used):
@@ -455,14 +467,22 @@ def _lt_call(name, *args):
 _LT_BGRAD = os.environ.get("APEX_AMD_LT_BGRAD", "0") == "1"
 
 
-def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype):
-    """(dW, db): the weight-gradient GEMM + the column-sum kernel, or (opt-in) one
-    hipBLASLt GEMM with the BGRADB epilogue."""
-    if _LT_BGRAD and _lt_ok(dy2, x2):
+def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype, out=None, accumulate=True, side=False):
+    """(dW, db): db handed over by a fused residual join (ops/_bias_handoff.py), else
+    wgrad4w forming db from its own dY fragments, else the weight-gradient GEMM + the
+    column-sum kernel, or (opt-in) one hipBLASLt GEMM with the BGRADB epilogue.  ``out`` /
+    ``accumulate``: as _wgrad (a DDP bucket view)."""
+    hs = _bias_handoff.take(dy2, b_dtype)
+    if hs is None and _W4W_BIAS:
+        got = _wgrad_w4w(dy2, x2, w_dtype, out, accumulate, side, b_dtype=b_dtype)
+        if got is not None:
+            return got
+    if hs is None and out is None and _LT_BGRAD and _lt_ok(dy2, x2):
         res = _lt_call("wgrad_bgrad_lt", dy2, x2, w_dtype, b_dtype)
         if res is not None:
             return res
-    return _wgrad(dy2, x2, w_dtype), _bias_grad(dy2, b_dtype)
+    dw = _wgrad(dy2, x2, w_dtype, out=out, accumulate=accumulate, side=side)
+    return dw, (hs if hs is not None else _bias_grad(dy2, b_dtype))
 
 
 # The FFN on the own MFMA GEMM with its epilogues: forward h = gelu(x W1^T + b1) keeping

@@ -140,11 +140,35 @@ __device__ __forceinline__ V8 ww_frag(const unsigned char* p) {
   return f;
 }
 
+// column sums of A from the dY fragments: lane l holds 8 consecutive k of column l & 15 of
+// fragment i; one v_dot2 with (1, 1) per dword adds a pair exactly in fp32
+template <typename TT, typename V8>
+__device__ __forceinline__ float ww_sum8(V8 f, float acc) {
+  if constexpr (std::is_same<TT, half_t>::value) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 one = {(_Float16)1.0f, (_Float16)1.0f};
+    acc = __builtin_amdgcn_fdot2(__builtin_shufflevector(f, f, 0, 1), one, acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_shufflevector(f, f, 2, 3), one, acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_shufflevector(f, f, 4, 5), one, acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_shufflevector(f, f, 6, 7), one, acc, false);
+  } else {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    const b2 one = {(__bf16)1.0f, (__bf16)1.0f};
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 0, 1), one, acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 2, 3), one, acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 4, 5), one, acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 6, 7), one, acc, false);
+  }
+  return acc;
+}
+
+// LV 4 = layout 0 with the column sums of A (p.colsum)
 template <typename TT, int LV>
 __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only needs the launch stub)
-  constexpr int L = LV == 3 ? 0 : LV;  // LDS layout
+  constexpr int L = (LV == 3 || LV == 4) ? 0 : LV;  // LDS layout
   constexpr bool HB = LV == 3;         // half-K-tile slot release (variant 3)
+  constexpr bool CS = LV == 4;         // column sums of A
   typedef typename WwT<TT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kWwSlot];
 
@@ -283,6 +307,11 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
   };
 
   f32x4_t acc[8][8];
+  float csum[CS ? 8 : 1];
+  if constexpr (CS) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) csum[i] = 0.f;
+  }
 
   // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed, its k-step-0 fragments read
   if constexpr (HB) {
@@ -329,6 +358,9 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
       } else {
         WW_GROUP(fa0, fb0, g, mma);
       }
+      if constexpr (CS) {
+        if ((g & 1) == 0) csum[g >> 1] = ww_sum8<TT>(fa0[g >> 1], csum[g >> 1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
       rd(slot, 1, rd_order(g), fa1, fb1);
       if constexpr (HB) {
@@ -348,6 +380,9 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       WW_GROUP(fa1, fb1, g, mma);
+      if constexpr (CS) {
+        if ((g & 1) == 0) csum[g >> 1] = ww_sum8<TT>(fa1[g >> 1], csum[g >> 1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
       rd(slot ^ 1, 0, rd_order(g), fa0, fb0);
       if constexpr (HB) {
@@ -387,6 +422,22 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (CS) {
+    // the 4 k-groups of a column sit in lanes l, l ^ 16, l ^ 32, l ^ 48; the n-tile 0
+    // workgroup's wn == 0 waves write their 128 columns (every n-tile forms the same sums)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = csum[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      csum[i] = v;
+    }
+    if (tn == 0 && wn == 0 && lane < 16) {
+      float* cp = p.colsum + (int64_t)s * p.M + m0 + wm * 128 + lane;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cp[i * 16] = csum[i];
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
   (void)p;
@@ -415,7 +466,9 @@ void wgrad4w(const WgradArgs& a0, hipStream_t st) {
   const int lay = e ? std::atoi(e) : 0;
   auto go = [&](auto t0) {
     using TT = decltype(t0);
-    if (lay == 0)
+    if (a.colsum)
+      hipLaunchKernelGGL((wgrad4w_k<TT, 4>), dim3(grid), dim3(kWwT), 0, st, a);
+    else if (lay == 0)
       hipLaunchKernelGGL((wgrad4w_k<TT, 0>), dim3(grid), dim3(kWwT), 0, st, a);
     else if (lay == 3)
       hipLaunchKernelGGL((wgrad4w_k<TT, 3>), dim3(grid), dim3(kWwT), 0, st, a);

@@ -306,6 +306,8 @@ struct WgradArgs {
   int S;
   int fp16;
   int group_m;  // <= 0: default (APEX_AMD_W4W_GROUPM or 4)
+  float* colsum = nullptr;  // optional [S][M]: column sums of A per split (the bias gradient
+                            // of dY, formed from the MFMA fragments; layout 0 only)
 };
 bool wgrad4w_supported(int64_t T, int M, int N, int S);
 void wgrad4w(const WgradArgs& a, hipStream_t st);

@@ -175,6 +175,51 @@ at::Tensor wgrad4w_op(at::Tensor dy, at::Tensor x, int64_t splits, at::ScalarTyp
   return splitk_reduce_op(part, out_dtype, out, accumulate);
 }
 
+// wgrad4w_op plus the bias gradient db [M] = column sums of dy in bias_dtype, formed from
+// the kernel's dY fragments (fp32 per split, then the bias-gradient final kernel): the
+// dense layer's separate column-sum pass over dy disappears
+std::tuple<at::Tensor, at::Tensor> wgrad4w_bias_op(at::Tensor dy, at::Tensor x, int64_t splits,
+                                                   at::ScalarType out_dtype,
+                                                   c10::optional<at::Tensor> out, bool accumulate,
+                                                   at::ScalarType bias_dtype) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(wgrad4w_ok(dy, x, splits), "wgrad4w_bias: see wgrad4w");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "wgrad4w: out dtype");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  const bool given = out.has_value() && out->defined();
+  if (given)
+    TORCH_CHECK(out->is_cuda() && out->scalar_type() == out_dtype && out->numel() == M * N &&
+                    out->is_contiguous(),
+                "wgrad4w: out must be a contiguous tensor of M*N elements of out_dtype");
+  at::Tensor cs = at::empty({splits, M}, dy.options().dtype(at::kFloat));
+  WgradArgs g{};
+  g.A = dy.data_ptr();
+  g.B = x.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.lda = (int)dy.stride(0);
+  g.ldb = (int)x.stride(0);
+  g.rows = (int)(T / splits);
+  g.S = (int)splits;
+  g.fp16 = dy.scalar_type() == at::kHalf ? 1 : 0;
+  g.colsum = cs.data_ptr<float>();
+  at::Tensor db = at::empty({M}, dy.options().dtype(bias_dtype));
+  at::Tensor w;
+  if (splits == 1 && out_dtype == at::kFloat && !(given && accumulate)) {
+    w = given ? *out : at::empty({M, N}, dy.options().dtype(at::kFloat));
+    g.P = w.data_ptr<float>();
+    wgrad4w(g, cur_stream());
+  } else {
+    at::Tensor part = at::empty({splits, M, N}, dy.options().dtype(at::kFloat));
+    g.P = part.data_ptr<float>();
+    wgrad4w(g, cur_stream());
+    w = splitk_reduce_op(part, out_dtype, out, accumulate);
+  }
+  colsum_finalize(cs.data_ptr<float>(), (int)splits, (int)M, db.data_ptr(), dtype_of(db),
+                  cur_stream());
+  return {w, db};
+}
+
 std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
                                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
                                   bool want_pre, bool tanh_approx,

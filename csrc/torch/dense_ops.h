@@ -27,6 +27,10 @@ std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tenso
 bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b);
 bool gemm4w_ok(const at::Tensor& a, const at::Tensor& b);
 bool wgrad4w_ok(const at::Tensor& dy, const at::Tensor& x, int64_t splits);
+std::tuple<at::Tensor, at::Tensor> wgrad4w_bias_op(at::Tensor dy, at::Tensor x, int64_t splits,
+                                                   at::ScalarType out_dtype,
+                                                   c10::optional<at::Tensor> out, bool accumulate,
+                                                   at::ScalarType bias_dtype);
 at::Tensor wgrad4w_op(at::Tensor dy, at::Tensor x, int64_t splits, at::ScalarType out_dtype,
                       c10::optional<at::Tensor> out, bool accumulate);
 std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,

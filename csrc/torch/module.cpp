@@ -146,6 +146,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   dn.def("wgrad4w", &wgrad4w_op, py::arg("dy"), py::arg("x"), py::arg("splits"),
          py::arg("out_dtype"), py::arg("out") = py::none(), py::arg("accumulate") = true);
   dn.def("wgrad4w_ok", &wgrad4w_ok);
+  dn.def("wgrad4w_bias", &wgrad4w_bias_op, py::arg("dy"), py::arg("x"), py::arg("splits"),
+         py::arg("out_dtype"), py::arg("out") = py::none(), py::arg("accumulate") = true,
+         py::arg("bias_dtype") = at::kFloat);
   auto xe = m.def_submodule("xentropy", "fused softmax cross entropy + label smoothing");
   xe.def("forward", &xentropy_fwd_op);
   xe.def("backward", &xentropy_bwd_op);

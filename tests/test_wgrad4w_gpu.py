@@ -157,3 +157,57 @@ def test_dense_weight_transpose_kernel(shape, dtype):
     t = FD._transposed(w)
     assert t.is_contiguous() and t.shape == (shape[1], shape[0])
     assert torch.equal(t, w.t())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("tmns", [(64, 256, 256, 1), (1024, 256, 512, 2), (4096, 512, 768, 4),
+                                  (8192, 3072, 1024, 2), (2048, 1024, 1024, 16)])
+@pytest.mark.parametrize("b_dtype", [torch.float32, torch.bfloat16])
+def test_wgrad4w_bias_column_sums(tmns, dtype, b_dtype):
+    """wgrad4w_bias: the same dW as wgrad4w (bitwise) plus db = column sums of dy formed
+    from the kernel's fragments (v_dot2 next to the MFMAs), against fp32."""
+    T, M, N, S = tmns
+    dy, x = _ops(T, M, N, dtype, 5 * T + N)
+    out_dt = torch.bfloat16 if dtype == torch.bfloat16 else torch.float32
+    w, db = _dn().wgrad4w_bias(dy, x, S, out_dt, bias_dtype=b_dtype)
+    assert torch.equal(w, _dn().wgrad4w(dy, x, S, out_dt))
+    ref = dy.double().sum(0)
+    assert db.dtype == b_dtype and db.shape == (M,)
+    assert _err(db, ref.float()) < (1e-2 if b_dtype == torch.bfloat16 else 1e-5)
+    w2, db2 = _dn().wgrad4w_bias(dy, x, S, out_dt, bias_dtype=b_dtype)
+    assert torch.equal(db, db2)  # fixed order
+
+
+def test_wgrad4w_bias_into_bucket_view():
+    T, M, N = 4096, 3072, 1024
+    dy, x = _ops(T, M, N, torch.bfloat16, 19)
+    ref = dy.float().t() @ x.float()
+    acc = torch.ones(M, N, device=DEV)
+    r, db = _dn().wgrad4w_bias(dy, x, 2, torch.float32, out=acc, accumulate=True,
+                               bias_dtype=torch.float32)
+    assert r.data_ptr() == acc.data_ptr()
+    assert _err(acc - 1, ref) < 1e-4
+    assert _err(db, dy.double().sum(0).float()) < 1e-5
+
+
+@pytest.mark.parametrize("w_dtype", [torch.bfloat16, torch.float32])
+def test_dense_wgrad_bgrad_routes_through_wgrad4w_bias(monkeypatch, w_dtype):
+    from apex_example_amd import fused_dense as FD
+    T, o, i = 4096, 3072, 1024
+    dy, x = _ops(T, o, i, torch.bfloat16, 23)
+    dn = _dn()
+    real = dn.wgrad4w_bias
+    called = []
+
+    def spy(*a, **k):
+        called.append(a[2])
+        return real(*a, **k)
+    monkeypatch.setattr(dn, "wgrad4w_bias", spy, raising=False)
+    monkeypatch.setattr(FD, "_W4W_BIAS", True)
+    dw, db = FD._wgrad_bgrad(dy, x, w_dtype, w_dtype)
+    assert called and dw.dtype == w_dtype and db.dtype == w_dtype
+    monkeypatch.setattr(FD, "_W4W_BIAS", False)
+    dw0, db0 = FD._wgrad_bgrad(dy, x, w_dtype, w_dtype)
+    assert torch.equal(dw, dw0)
+    tol = 1e-2 if w_dtype == torch.bfloat16 else 1e-5
+    assert _err(db, db0.float()) < tol
