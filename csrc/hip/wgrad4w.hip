@@ -140,8 +140,11 @@ __device__ __forceinline__ V8 ww_frag(const unsigned char* p) {
   return f;
 }
 
-// column sums of A from the dY fragments: lane l holds 8 consecutive k of column l & 15 of
-// fragment i; one v_dot2 with (1, 1) per dword adds a pair exactly in fp32
+// column sums of A from the dY fragments (variant 4, p.colsum: the dense layer's bias
+// gradient without a separate pass over dY): lane l holds 8 k of column l & 15 of
+// fragment i; one v_dot2 with (1, 1) per bf16 / f16 pair adds it exactly in fp32.  The pairs
+// are taken with __builtin_shufflevector: a bit_cast of the fragment to a dword vector
+// indexed inside the unrolled loop made this compiler read the same register three times
 template <typename TT, typename V8>
 __device__ __forceinline__ float ww_sum8(V8 f, float acc) {
   if constexpr (std::is_same<TT, half_t>::value) {
