@@ -393,10 +393,14 @@ def _dense_bwd(ctx, dy, dskip=None):
         dx = _dgrad(dy2, wc, xc.shape, dskip, dy)
     x2 = xc.reshape(-1, xc.size(-1))
     direct = _direct_slots(side, ctx.params[0], ctx.w_dtype) if ctx.needs_input_grad[1] else None
-    if direct is not None:
+    if direct is not None and need_b:
+        # the weight gradient straight into its bucket view, db from the same kernel
+        # where wgrad4w takes the layer (_wgrad_bgrad)
+        tgt, acc = _ddp_direct.grad_target(ctx.params[0])
+        _, db = _wgrad_bgrad(dy2, x2, ctx.w_dtype, ctx.bias_dtype, out=tgt, accumulate=acc)
+        _ddp_direct.mark_ready(direct)
+    elif direct is not None:
         dw = _wgrad_maybe_direct(side, ctx.params[0], ctx.w_dtype, dy2, x2, xc)
-        if need_b:
-            db = _bias_grad(dy2, ctx.bias_dtype)
     elif ctx.needs_input_grad[1] and need_b:
         dw, db = side.run(_side_wgrad_bgrad(side, ctx.params[0], ctx.w_dtype, ctx.bias_dtype,
                                             dy2, x2), dy2, xc)
