@@ -36,7 +36,7 @@ def take(g2, dtype):
     dh, ver, cs = ent
     if (g2.data_ptr() == dh.data_ptr() and g2.numel() == dh.numel() and dh._version == ver
             and g2.dim() == 2 and g2.size(1) == cs.numel() and cs.dtype == dtype
-            and g2.device == cs.device):
+            and g2.is_contiguous() and dh.is_contiguous() and g2.device == cs.device):
         _SLOT[0] = None
         return cs
     return None

@@ -561,6 +561,12 @@ static inline int ln_generic_parts(int64_t n1) {
   return (int)(p > 0 ? p : 1);
 }
 
+// the dh column sums need a third [kLNWaves][n2] LDS row: within the 64 KB of dynamic LDS
+// a launch gets without a raised attribute (n2 <= 1365)
+bool layer_norm_bwd_hsum_ok(int64_t n2) {
+  return (int64_t)kLNWaves * 3 * n2 * (int64_t)sizeof(float) <= 65536;
+}
+
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2) {
   int64_t a = (int64_t)ln_bwd_blocks(n1) * 3 * n2;  // (3 rows: with the dh column sums)
   int64_t b = (int64_t)ln_generic_parts(n1) * 2 * n2;
@@ -574,7 +580,7 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
   if (n1 == 0 || n2 == 0) return;
   const bool want_wb = dgamma != nullptr || dbeta != nullptr;
   // the dh column sums ride on the dgamma / dbeta partials (fused join only)
-  const int R = (fuse && fuse->dhsum && want_wb) ? 3 : 2;
+  const int R = (fuse && fuse->dhsum && want_wb && layer_norm_bwd_hsum_ok(n2)) ? 3 : 2;
   ln_dispatch(tx, [&](auto t0) {
     ln_dispatch(tw, [&](auto w0) {
       using T = decltype(t0);

@@ -187,6 +187,8 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 // dx [n1,n2]; dgamma/dbeta [n2] (TW) computed if non-null. `part` workspace
 // must hold layer_norm_bwd_workspace(n1, n2) floats.
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2);
+// whether the fused-join backward can also form the dh column sums (LnFuse::dhsum) for n2
+bool layer_norm_bwd_hsum_ok(int64_t n2);
 void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, DType tw,
                     const float* mean, const float* invvar, void* dx, void* dgamma, void* dbeta,
                     float* part, int64_t n1, int64_t n2, int rms, hipStream_t st,

@@ -157,7 +157,8 @@ add_dropout_layer_norm_backward_op(at::Tensor dy, at::Tensor s, at::Tensor mean,
   // column sums of dh (in gamma's dtype) with the dgamma / dbeta partials: the bias
   // gradient of the dense layer whose output h is (fused_dense picks it up)
   at::Tensor dhs;
-  if (need_hsum && (dgam.defined() || dbet.defined())) dhs = at::empty_like(g);
+  if (need_hsum && (dgam.defined() || dbet.defined()) && layer_norm_bwd_hsum_ok(n2))
+    dhs = at::empty_like(g);
   if (dgam.defined() || dbet.defined())
     part = at::empty({layer_norm_bwd_workspace(n1, n2)}, s.options().dtype(at::kFloat));
   LnFuse f = make_fuse(p, seed);

@@ -16,12 +16,14 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_join_dh_colsum_matches_reference(dtype, p):
+@pytest.mark.parametrize("n2", [1024, 2048])
+def test_join_dh_colsum_matches_reference(dtype, p, n2):
+    """n2 = 2048 needs more than 64 KB of LDS for the third partial row: no column sums
+    are offered there (the dense layer sums dh itself)."""
     from apex_example_amd import _native
     from apex_example_amd.normalization import FusedLayerNorm, fused_add_dropout_layer_norm
 
     torch.manual_seed(1)
-    n2 = 1024
     ln = FusedLayerNorm(n2).to(DEV).to(dtype)
     x = torch.randn(2048, n2, device=DEV, dtype=dtype, requires_grad=True)
     h = torch.randn(2048, n2, device=DEV, dtype=dtype, requires_grad=True)
@@ -42,6 +44,9 @@ def test_join_dh_colsum_matches_reference(dtype, p):
         H.clear()
     assert _native.available()
     dh, cs = captured["dh"], captured["cs"]
+    if n2 > 1365:
+        assert cs is None
+        return
     assert cs is not None and cs.dtype == dtype and cs.shape == (n2,)
     assert torch.equal(dh, h.grad)
     ref = dh.double().sum(0)

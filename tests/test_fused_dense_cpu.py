@@ -196,6 +196,10 @@ def test_bias_handoff_take_rules_cpu():
     assert H.take(dh, torch.bfloat16) is None  # dtype mismatch
     assert H.take(torch.randn(64, 32), torch.float32) is None  # another tensor
     assert H.take(dh[:32], torch.float32) is None  # a slice
+    sq = torch.randn(32, 32)
+    H.offer(sq, sq.sum(0))
+    assert H.take(sq.t(), torch.float32) is None  # a transposed view of the same storage
+    H.offer(dh, cs)
     dh.mul_(2)  # modified in place after the offer
     assert H.take(dh, torch.float32) is None
     H.offer(dh, None)
