@@ -15,9 +15,11 @@ gradient for the iteration.  So (a) the DDP wrapper excludes parameters listed m
 once in the module tree (tied weights, ``Reducer.set_no_direct``); (b) the own ops count
 their forward uses of each parameter (``note_use``) and go direct only for a parameter
 used exactly once in the current forward (a module called twice takes the autograd path,
-which sums both uses before one AccumulateGrad); uses are counted per DDP forward call
-(``forward_epoch``), so gradient-accumulation micro-steps and eval forwards in between
-do not disturb the count; (c) the reducer refuses a second announcement, and the ready
+which sums both uses before one AccumulateGrad); a count starts at the first DDP forward
+after a completed backward (``forward_epoch``; the reducer counts backwards under
+``no_sync`` too), so several DDP forwards feeding ONE backward (siamese / contrastive
+losses) share one count and take the autograd path, while gradient-accumulation
+micro-steps and grad-free eval forwards in between do not disturb it; (c) the reducer refuses a second announcement, and the ready
 mark itself comes from the AccumulateGrad hook after every use has been summed, so an
 autograd gradient of some other use still lands in the view before the bucket launches
 (the parameter is excluded from the direct path from then on).
@@ -33,16 +35,22 @@ _ON = os.environ.get("APEX_AMD_DDP_DIRECT_GRAD", "1") == "1"
 _LAZY = os.environ.get("APEX_AMD_DDP_LAZY_ZERO", "1") == "1"
 
 
-_EPOCH = {}  # id(reducer) -> forward calls of its DDP wrapper
+_EPOCH = {}  # id(reducer) -> (use-count epoch, reducer.backwards() when it started)
 
 
 def forward_epoch(red):
-    """Start a new use count for ``red``'s parameters (DistributedDataParallel.forward)."""
-    _EPOCH[id(red)] = _EPOCH.get(id(red), 0) + 1
+    """DistributedDataParallel.forward: start a new use count for ``red``'s parameters
+    if a backward has completed since the current count started, else keep counting
+    (two forwards before one backward: each parameter then shows two uses)."""
+    b = red.backwards()
+    e = _EPOCH.get(id(red))
+    if e is None or e[1] != b:
+        _EPOCH[id(red)] = ((e[0] + 1) if e is not None else 1, b)
 
 
 def _epoch(red):
-    return _EPOCH.get(id(red), 0)
+    e = _EPOCH.get(id(red))
+    return e[0] if e is not None else 0
 
 
 def note_use(*params):

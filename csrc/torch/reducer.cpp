@@ -194,8 +194,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool direct_ok(int64_t i) const {
     return i >= 0 && i < (int64_t)no_direct_.size() && !no_direct_[(size_t)i];
   }
-  // iterations completed (forward-use counting in ops/_ddp_direct.py keys on it)
+  // iterations completed (reduced backwards)
   int64_t iteration() const { return iteration_; }
+  // backward passes that reached this reducer's hooks, counted under no_sync /
+  // disable_allreduce too: ops/_ddp_direct.py starts a new forward-use count only
+  // when a backward has completed since the last DDP forward, so several forwards
+  // feeding one backward (siamese / contrastive) share one count
+  int64_t backwards() const { return backwards_; }
 
   // Lazy zeroing (the optimizers' zero_grad on bucket-view gradients): instead of a
   // memset of the buckets, the parameters' .grad are detached from their views and the
@@ -270,15 +275,15 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       if (had_grad) no_direct_[(size_t)i] = 1;
     }
     attach_view(i);
-    if (!enabled_) return;
     if (!callback_queued_) {
       callback_queued_ = true;
-      if (timing_) timing_record(ev_start_);
+      if (enabled_ && timing_) timing_record(ev_start_);
       std::weak_ptr<Reducer> weak = shared_from_this();
       torch::autograd::Engine::get_default_engine().queue_callback([weak]() {
         if (auto self = weak.lock()) self->finalize();
       });
     }
+    if (!enabled_) return;
     TORCH_CHECK(!seen_[(size_t)i],
                 "DistributedDataParallel: parameter ", i,
                 " received a gradient twice in one backward pass; use delay_allreduce=True "
@@ -298,6 +303,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void finalize() {
     std::lock_guard<std::mutex> g(mu_);
     callback_queued_ = false;
+    ++backwards_;
     if (!enabled_) return;
     RangeGuard rg(prof_, "apex_amd::ddp_epilogue");
     const bool timed = timing_ && !refresh_ && !delay_;
@@ -771,6 +777,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<char> no_direct_;
   std::vector<char> lazy_;
   int64_t iteration_ = 0;
+  int64_t backwards_ = 0;
   bool tapered_ = true;
   int64_t next_ = 0;
   bool refresh_ = true;
@@ -928,6 +935,7 @@ void register_reducer(pybind11::module_& m) {
       .def("lazy_view", &Reducer::lazy_view)
       .def("direct_ok", &Reducer::direct_ok)
       .def("iteration", &Reducer::iteration)
+      .def("backwards", &Reducer::backwards)
       .def("force_collectives", &Reducer::force_collectives)
       .def("collectives_active", &Reducer::collectives_active)
       .def("set_timing", &Reducer::set_timing)

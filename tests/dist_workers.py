@@ -264,12 +264,14 @@ class _DirectNet(nn.Module):
             h = _DirectMul.apply(_DirectMul.apply(h, self.a), self.a)
         elif self.case == "tied":      # tied weight: used through both names
             h = _DirectMul.apply(_DirectMul.apply(h, self.a), self.sub.w)
+        elif self.case == "plain":     # every weight used once per forward
+            h = _DirectMul.apply(h, self.a)
         else:                          # "functional": a direct use + a plain autograd use
             h = _DirectMul.apply(h, self.a) + h * self.a
         return (_DirectMul.apply(h, self.b) ** 2).sum()
 
 
-def ddp_direct_shared(rank, world, case="twice", iters=3):
+def ddp_direct_shared(rank, world, case="twice", iters=3, two_forwards=False):
     """Shared / multiply-used parameters on the direct-gradient path: grads
     must equal the full-batch autograd reference, or (functional use after a launched
     bucket) the reducer raises its explicit error; the parameter is then excluded."""
@@ -289,12 +291,18 @@ def ddp_direct_shared(rank, world, case="twice", iters=3):
             if p.grad is not None:
                 p.grad.zero_()
         try:
-            ddp(xs[rank]).backward()
+            if two_forwards:  # siamese / contrastive: two DDP forwards, one backward
+                (ddp(xs[rank]) + ddp(2.0 * xs[rank])).backward()
+            else:
+                ddp(xs[rank]).backward()
         except RuntimeError as e:
             err = str(e)
             break
         out.append({k: v.grad.clone() for k, v in net.named_parameters()})
-        loss = sum(ref(x) for x in xs) / world
+        if two_forwards:
+            loss = sum(ref(x) + ref(2.0 * x) for x in xs) / world
+        else:
+            loss = sum(ref(x) for x in xs) / world
         ref.zero_grad()
         loss.backward()
         refs.append({k: v.grad.clone() for k, v in ref.named_parameters()})

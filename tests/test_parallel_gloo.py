@@ -281,6 +281,22 @@ def test_ddp_direct_path_functional_second_use(tmp_path):
         assert r["direct_ok"]["a"] is False
 
 
+@pytest.mark.parametrize("case", ["plain", "twice"])
+def test_ddp_direct_path_two_forwards_one_backward(tmp_path, case):
+    """Two DDP forwards before ONE backward (siamese / contrastive pattern):
+    the forward-use count spans both forwards (a new count starts only after a completed
+    backward), so every parameter shows two uses, takes the autograd path, and no
+    parameter is announced twice; gradients equal the full-batch reference."""
+    res = W.run("ddp_direct_shared", 2, str(tmp_path), case=case, two_forwards=True)
+    for r in res:
+        assert r["err"] is None, r["err"]
+        assert r["direct"] == 0
+        assert len(r["grads"]) == 3
+        for got, ref in zip(r["grads"], r["refs"]):
+            for k in ref:
+                torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6)
+
+
 def test_ddp_tapered_tail_buckets(tmp_path):
     """Tapered layout: the buckets cut from the end of the arrival order grow from
     message_size/16 to message_size, so the last-launched bucket (the first layers'
