@@ -89,6 +89,14 @@ struct RangeGuard {  // roctx range when enabled
   }
 };
 
+class Reducer;
+struct SideWaitPreHook : torch::autograd::FunctionPreHook {
+  SideWaitPreHook(std::weak_ptr<Reducer> r, int64_t i) : red(std::move(r)), idx(i) {}
+  torch::autograd::variable_list operator()(const torch::autograd::variable_list& grads) override;
+  std::weak_ptr<Reducer> red;
+  int64_t idx;
+};
+
 class Reducer : public std::enable_shared_from_this<Reducer> {
  public:
   Reducer(std::vector<at::Tensor> params, c10::intrusive_ptr<c10d::ProcessGroup> pg,
@@ -114,6 +122,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     async_marked_.assign(params_.size(), 0);
     no_direct_.assign(params_.size(), 0);
     lazy_.assign(params_.size(), 0);
+    side_ev_.assign(params_.size(), nullptr);
   }
 
   ~Reducer() {
@@ -145,13 +154,40 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
           }));
       accs_.push_back(acc);
       hook_keys_.push_back(key);
+      auto pre = std::make_unique<SideWaitPreHook>(weak, idx);
+      pre_keys_.push_back(pre.get());
+      acc->add_pre_hook(std::move(pre));
     }
   }
 
   void remove_hooks() {
-    for (size_t i = 0; i < accs_.size(); ++i) accs_[i]->del_post_hook(hook_keys_[i]);
+    for (size_t i = 0; i < accs_.size(); ++i) {
+      accs_[i]->del_post_hook(hook_keys_[i]);
+      auto& pres = accs_[i]->pre_hooks();
+      for (auto it = pres.begin(); it != pres.end(); ++it)
+        if (it->get() == pre_keys_[i]) {
+          pres.erase(it);
+          break;
+        }
+    }
     accs_.clear();
     hook_keys_.clear();
+    pre_keys_.clear();
+  }
+
+  // AccumulateGrad pre-hook: a parameter whose gradient a SIDE stream wrote into its
+  // bucket view (mark_ready_on_stream) and that ALSO receives an autograd gradient from
+  // another use (an explicit penalty term, say): AccumulateGrad adds that gradient into
+  // the same view on the compute stream, which must first wait for the side stream's
+  // write.  Without another use the incoming gradient is undefined and
+  // nothing waits.
+  void side_wait(int64_t i, bool incoming) {
+    if (!incoming) return;
+    std::lock_guard<std::mutex> g(mu_);
+    hipEvent_t e = side_ev_[(size_t)i];
+    if (e == nullptr) return;
+    TORCH_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), e, 0) == hipSuccess,
+                "hipStreamWaitEvent failed");
   }
 
   // ---- hook path (autograd engine thread) ---------------------------------
@@ -262,9 +298,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
         hipEvent_t e = take_event();
         TORCH_CHECK(hipEventRecord(e, side) == hipSuccess, "hipEventRecord failed");
         buckets_[(size_t)bucket_of_[(size_t)i]].waits.push_back(e);
+        // (valid until this parameter's bucket launches, which needs its ready mark,
+        // which comes after the AccumulateGrad pre-hook that may wait on it)
+        if (side != nullptr) side_ev_[(size_t)i] = e;
       }
       return;
     }
+    side_ev_[(size_t)i] = nullptr;
     if (async_marked_[(size_t)i]) {
       // the AccumulateGrad post-hook of an announced gradient (the Function returned
       // None for it; the hook still runs): the parameter is ready now
@@ -746,6 +786,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   }
 
   void reset_iteration() {
+    std::fill(side_ev_.begin(), side_ev_.end(), nullptr);
     for (auto& b : buckets_) {
       b.pending = (int)b.params.size();
       b.launched = false;
@@ -788,6 +829,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool timing_ = false, timing_valid_ = false;
   bool prof_ = false;
   std::vector<hipEvent_t> ev_pool_;
+  std::vector<hipEvent_t> side_ev_;  // per parameter: its side-stream announcement event
+  std::vector<torch::autograd::FunctionPreHook*> pre_keys_;
   hipEvent_t ev_main_ = nullptr;
   std::unique_ptr<at::hip::HIPStreamMasqueradingAsCUDA> launch_stream_;
   hipEvent_t ev_start_ = nullptr, ev_bwd_end_ = nullptr;
@@ -797,6 +840,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<std::shared_ptr<torch::autograd::Node>> accs_;
   std::vector<uintptr_t> hook_keys_;
 };
+
+torch::autograd::variable_list SideWaitPreHook::operator()(
+    const torch::autograd::variable_list& grads) {
+  if (auto r = red.lock()) r->side_wait(idx, !grads.empty() && grads[0].defined());
+  return grads;
+}
 
 std::shared_ptr<Reducer> make_reducer(std::vector<at::Tensor> params,
                                       c10::intrusive_ptr<c10d::ProcessGroup> pg,

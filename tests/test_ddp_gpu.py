@@ -692,3 +692,62 @@ def test_ddp_direct_path_shared_parameters_gpu(pg, monkeypatch):
         for a, b in zip(grads[False][it], grads[True][it]):
             scale = float(a.abs().max()) + 1e-30
             assert float((a - b).abs().max()) / scale < 2e-2, it
+
+
+def test_ddp_side_stream_weight_grad_plus_functional_penalty(pg, monkeypatch):
+    """A conv weight whose gradient the DDP side stream writes into its (lazily zeroed)
+    bucket view AND that an explicit penalty term uses through plain autograd
+    (ADVICE r5): AccumulateGrad adds the penalty gradient into the same view on the
+    compute stream, so it must wait for the side stream's write (the reducer's
+    AccumulateGrad pre-hook).  The side stream sleeps before every weight gradient, so
+    a missing wait loses the penalty (the side kernel overwrites the lazily zeroed
+    view after the add).  Gradients have a closed form: k * tap count + lambda."""
+    from apex_example_amd.ops import conv as C
+    from apex_example_amd.optimizers import FusedSGD
+    from apex_example_amd.parallel import DistributedDataParallel
+
+    monkeypatch.setattr(C, "_TEST_SIDE_SLEEP", 2_000_000)
+    torch.manual_seed(0)
+    net = _ConvNet()
+    ddp = DistributedDataParallel(net, message_size=64 * 64 * 9 * 2, force_collectives=True)
+    opt = FusedSGD(net.parameters(), lr=0.0)
+    n, h, w = 2, 8, 8
+    x = torch.ones(n, 64, h, w, device="cuda", dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    z = torch.ones(n, 64, h, w, device="cuda")
+    z[:, :, :, w // 2:] = -1.0
+    z = z.to(memory_format=torch.channels_last)
+    cnt = torch.zeros(3, 3, dtype=torch.float64)
+    for r in range(3):
+        for s in range(3):
+            cnt[r, s] = n * (h - abs(r - 1)) * (w - abs(s - 1))
+    lam = 4.0
+    sides = {"n": 0}
+    orig = C._SideWgrad.run
+
+    def counting(self, fn, *a, _orig=orig):
+        if self.mode == "ddp":
+            sides["n"] += 1
+        return _orig(self, fn, *a)
+    monkeypatch.setattr(C._SideWgrad, "run", counting)
+    bad = torch.zeros((), device="cuda", dtype=torch.float64)
+    for it in range(8):
+        ks = [float((it + i) % 3 + 1) for i in range(len(net.convs))]
+        opt.zero_grad()
+        loss = ddp(x, z, ks, 1.0)
+        # the penalty: a second, plain-autograd use of conv 0's weight
+        loss = loss + lam * net.convs[0].weight.float().sum()
+        loss.backward()
+        for i, c in enumerate(net.convs):
+            if c.kernel_size == (3, 3):
+                ref = (ks[i] * cnt).view(1, 1, 3, 3).expand(64, 64, 3, 3)
+            else:
+                ref = torch.full((128, 64, 1, 1), ks[i] * n * h * w, dtype=torch.float64)
+            if i == 0:
+                ref = ref + lam
+            ref = ref.to(torch.bfloat16).to("cuda").double()
+            bad += (c.weight.grad.double() - ref).abs().max()
+        opt.step()
+    torch.cuda.synchronize()
+    assert sides["n"] > 0
+    assert bad.item() == 0.0
