@@ -226,15 +226,31 @@ class _SideWgrad:
             self.main.wait_event(wait_ev)
         if fresh:
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
+        sid = self.side.cuda_stream
         if self.mode == "ddp":
-            sid = self.side.cuda_stream
             for p, g in zip(self.params, outs):
                 if g is not None:
                     red, i = _ddp_slot(p)
                     red.mark_ready_on_stream(i, sid)
-            none = tuple(None for _ in outs)
-            return none if isinstance(dw, tuple) else None
-        return dw
+        else:
+            # 'free': store the side-stream tensor as .grad here (what AccumulateGrad
+            # would do without a kernel) and hand autograd None.  Another use of the
+            # parameter (a penalty term, a second call of the module) then reaches
+            # AccumulateGrad alone, whose pre-hook makes the compute stream wait for this
+            # side stream before adding into .grad (csrc/torch/reducer.cpp
+            # side_grad_announce); returning the tensor instead would let autograd sum
+            # the two on the compute stream before the side stream has written it.
+            if not all(g is None or (p.grad is None and g.dtype == p.dtype
+                                     and g.shape == p.shape and g.device == p.device)
+                       for p, g in zip(self.params, outs)):
+                raise RuntimeError("side-stream weight gradient does not match its parameter")
+            announce = _native.require().reducer.side_grad_announce
+            for p, g in zip(self.params, outs):
+                if g is not None:
+                    p.grad = g
+                    announce(p, sid)
+        none = tuple(None for _ in outs)
+        return none if isinstance(dw, tuple) else None
 
 
 def _side_out(side, weight, cl=False):

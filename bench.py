@@ -278,6 +278,7 @@ def build_resnet(args, device, world):
             scaler.step(opt)
             scaler.update()
             return loss
+    w.model, w.opt = model, opt
     w.step, w.opt_only, w.batch = step, opt.step, (x, y)
     w.units = bs
     w.metric = "images/sec (whole node) ResNet-50 amp O2" if args.model == "resnet50" else \
@@ -355,6 +356,7 @@ def build_convnet(args, device, world):
             scaler.update()
             return loss
         optname = "torch.optim.SGD(lr=%g)" % lr
+    w.model, w.opt = model, opt
     w.step, w.opt_only, w.batch = step, opt.step, (x, y)
     w.units = bs
     w.metric = "images/sec (whole node) MNIST ConvNet amp %s" % opt_level
@@ -421,6 +423,7 @@ def build_bert(args, device, world):
             opt.step()
             return loss
         optname = "torch.optim.AdamW(fused) (torch has no LAMB)"
+    w.model, w.opt = model, opt
     w.step, w.opt_only, w.batch = step, opt.step, batch
     w.units = bs
     w.metric = "sequences/sec (whole node) BERT-large pretrain amp %s" % opt_level
@@ -486,6 +489,7 @@ def build_gpt2(args, device, world):
             scaler.step(opt)
             scaler.update()
             return loss
+    w.model, w.opt = model, opt
     w.step, w.opt_only, w.batch = step, opt.step, (ids,)
     w.units = bs * seq
     w.metric = "tokens/sec (whole node) GPT-2-medium amp %s" % opt_level
@@ -744,6 +748,8 @@ def main():
             and args.bucket_timing_steps > 0):
         ddp_stats = ddp_timing(ddp, step, batch, args.bucket_timing_steps, device)
 
+    consistency = replica_check(w, args, world) if world > 1 else None
+
     ms_per_step = elapsed / args.steps * 1e3
     value = w.units * world * args.steps / elapsed
     base = STOCK_BASELINE_PER_GPU.get(args.model) if args.impl == "amd" else None
@@ -781,6 +787,8 @@ def main():
     }
     if ddp_stats is not None:
         rec["ddp"] = ddp_stats
+    if consistency is not None:
+        rec["replicas"] = consistency
     if getattr(w, "steps_per_epoch", None):
         # the reference program's metric: "Training complete in" / epochs
         rec["epoch_seconds"] = round(w.steps_per_epoch * ms_per_step / 1e3, 3)
@@ -796,11 +804,50 @@ def main():
         barrier()
     if dist.is_initialized():
         dist.destroy_process_group()
+    if consistency is not None and not consistency["in_sync"]:
+        print("bench.py: the %d replicas are NOT bitwise in sync after the timed steps: %s; "
+              "the throughput above does not measure data-parallel training" % (
+                  world, {k: v["match"] for k, v in consistency["digests"].items()}),
+              file=sys.stderr)
+        sys.exit(5)
     if skipped and not args.allow_skipped_steps:
         print("bench.py: %d of the %d timed steps were skipped by the loss scaler (gradient "
               "overflow); the throughput above does not measure training steps" % (
                   skipped, args.steps), file=sys.stderr)
         sys.exit(4)
+
+
+def replica_check(w, args, world):
+    """N > 1, after the timed region: what the collectives really span (the rank count
+    each RCCL communicator reports) and whether the replicas are still bitwise equal
+    (cross-rank MAX / MIN of per-rank digests of parameters, amp master weights,
+    optimizer state and buffers; apex_example_amd/utils/consistency.py).  BatchNorm
+    running statistics differ legitimately without SyncBN, so buffers only count when
+    SyncBN is on or the model has no BatchNorm."""
+    from apex_example_amd.utils.consistency import (comm_info, cross_rank_match,
+                                                    model_state_groups)
+
+    if os.environ.get("APEX_AMD_TEST_DESYNC_RANK") == str(dist.get_rank()):
+        # test hook (tests/test_ddp_gpu.py): flip the lowest bit of one weight on one rank
+        with torch.no_grad():
+            p = next(iter(w.model.parameters())).detach().view(-1)[:1]
+            p.view({2: torch.int16, 4: torch.int32}[p.element_size()]).add_(1)
+    comms = {"world": comm_info(dist.group.WORLD)}
+    ddp = getattr(w, "ddp", None)
+    if ddp is not None and getattr(ddp, "_comm_pg", None) is not None:
+        comms["ddp"] = comm_info(ddp._comm_pg)
+    if args.impl == "amd" and w.config.get("syncbn"):
+        from apex_example_amd.parallel.sync_batchnorm import syncbn_comm_group
+        comms["syncbn"] = comm_info(syncbn_comm_group())
+    model = w.model.module if hasattr(w.model, "module") else w.model
+    groups = model_state_groups(model, w.opt)
+    digests = cross_rank_match(groups)
+    has_bn = any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in model.modules())
+    required = [k for k in digests if k != "buffers" or w.config.get("syncbn") or not has_bn]
+    in_sync = all(digests[k]["match"] for k in required)
+    sizes_ok = all(c is None or c["size"] == world for c in comms.values())
+    return {"in_sync": bool(in_sync and sizes_ok), "required": required,
+            "digests": digests, "comms": comms, "comm_sizes_ok": sizes_ok}
 
 
 def _amp_scalers(args):

@@ -908,6 +908,21 @@ AllReduceFn rccl_allreduce() {
 
 bool syncbn_raw_available() { return rccl_allgather() && rccl_allreduce(); }
 
+// The rank count and this process's rank as the RCCL communicator itself reports them
+// (bench.py records them at N > 1: what the collectives really span).
+std::tuple<int64_t, int64_t> rccl_comm_info(int64_t comm) {
+  using CountFn = ncclResult_t (*)(const ncclComm_t, int*);
+  static CountFn count = reinterpret_cast<CountFn>(dlsym(RTLD_DEFAULT, "ncclCommCount"));
+  static CountFn urank = reinterpret_cast<CountFn>(dlsym(RTLD_DEFAULT, "ncclCommUserRank"));
+  TORCH_CHECK(count && urank, "rccl_comm_info: RCCL entry points not found");
+  TORCH_CHECK(comm != 0, "rccl_comm_info: no communicator");
+  int n = -1, r = -1;
+  TORCH_CHECK(count(reinterpret_cast<ncclComm_t>(comm), &n) == ncclSuccess, "ncclCommCount failed");
+  TORCH_CHECK(urank(reinterpret_cast<ncclComm_t>(comm), &r) == ncclSuccess,
+              "ncclCommUserRank failed");
+  return {n, r};
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> syncbn_allgather_combine_raw(
     at::Tensor packed, int64_t comm, int64_t world, double eps, double momentum,
     c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
@@ -949,9 +964,55 @@ void syncbn_allreduce_raw(at::Tensor t, int64_t comm) {
   TORCH_CHECK(r == ncclSuccess, "syncbn: ncclAllReduce failed (", (int)r, ")");
 }
 
+// ---- side-stream gradients outside DDP (ops/conv.py _SideWgrad 'free' mode) --------
+// A weight gradient computed on the side stream is stored as the parameter's .grad
+// directly (autograd gets None).  If the parameter has another use whose autograd
+// gradient reaches its AccumulateGrad node (an explicit penalty, a second call of the
+// module), AccumulateGrad adds it into that .grad on the compute stream: this
+// pre-hook makes the compute stream wait for the side stream's write first.  One hook
+// (with its own event) per AccumulateGrad node, installed on first use.
+namespace {
+struct SideGradWait : torch::autograd::FunctionPreHook {
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+  ~SideGradWait() override {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+  torch::autograd::variable_list operator()(const torch::autograd::variable_list& grads) override {
+    if (pending) {
+      pending = false;
+      if (!grads.empty() && grads[0].defined())
+        TORCH_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev, 0) ==
+                        hipSuccess, "hipStreamWaitEvent failed");
+    }
+    return grads;
+  }
+};
+}  // namespace
+
+void side_grad_announce(const at::Tensor& param, int64_t stream) {
+  auto acc = torch::autograd::impl::grad_accumulator(param);
+  TORCH_CHECK(acc, "side_grad_announce: parameter has no grad accumulator");
+  SideGradWait* h = nullptr;
+  for (auto& ph : acc->pre_hooks())
+    if ((h = dynamic_cast<SideGradWait*>(ph.get())) != nullptr) break;
+  if (h == nullptr) {
+    auto u = std::make_unique<SideGradWait>();
+    TORCH_CHECK(hipEventCreateWithFlags(&u->ev, hipEventDisableTiming) == hipSuccess,
+                "hipEventCreateWithFlags failed");
+    h = u.get();
+    acc->add_pre_hook(std::move(u));
+  }
+  TORCH_CHECK(hipEventRecord(h->ev, reinterpret_cast<hipStream_t>(stream)) == hipSuccess,
+              "hipEventRecord failed");
+  h->pending = true;
+}
+
 void register_reducer(pybind11::module_& m) {
+  m.def("side_grad_announce", &side_grad_announce, py::arg("param"), py::arg("stream"));
   namespace py = pybind11;
   m.def("syncbn_raw_available", &syncbn_raw_available);
+  m.def("rccl_comm_info", &rccl_comm_info, py::arg("comm"));
   m.def("syncbn_allgather_combine_raw", &syncbn_allgather_combine_raw, py::arg("packed"),
         py::arg("comm"), py::arg("world"), py::arg("eps"), py::arg("momentum"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("nbt") = py::none(),

@@ -628,3 +628,23 @@ def gpu_dfa(rank, world, steps=5):
     torch.cuda.synchronize()
     return {"params": [p.detach().float().cpu() for p in m.parameters()], "losses": losses,
             "skipped": skipped, "step": opt.state_dict()["param_groups"][0]["step"]}
+
+
+def replica_digests(rank, world, desync=-1):
+    """utils/consistency.py on gloo: identical replicas match; one rank with one bit of
+    one weight flipped is caught in that group only; comm_info reports the world."""
+    from apex_example_amd.utils.consistency import (comm_info, cross_rank_match,
+                                                    model_state_groups)
+
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(8, 16), nn.BatchNorm1d(16), nn.Linear(16, 4))
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    model(torch.randn(4, 8)).sum().backward()
+    opt.step()
+    if rank == desync:
+        with torch.no_grad():
+            model[2].weight.view(-1)[:1].view(torch.int32).add_(1)
+    res = cross_rank_match(model_state_groups(model, opt))
+    return {"match": {k: v["match"] for k, v in res.items()},
+            "digest": {k: v["digest"] for k, v in res.items()},
+            "comm": comm_info(dist.group.WORLD)}

@@ -352,6 +352,33 @@ def test_bench_self_spawn_two_ranks_one_gpu():
     assert rec["n_gpus"] == 2 and rec["launcher"] == "self-spawn"
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["syncbn"]
     assert rec["ddp"]["buckets"] >= 1 and rec["ddp"]["exposed_tail_ms"] >= 0
+    # the N > 1 self-check: both replicas bitwise equal, groups span 2 ranks
+    rep = rec["replicas"]
+    assert rep["in_sync"] and rep["comm_sizes_ok"], rep
+    assert {"params", "optimizer_params", "buffers"} <= set(rep["required"])
+    assert rep["comms"]["syncbn"]["size"] == 2 and rep["comms"]["ddp"]["size"] == 2
+
+
+def test_bench_two_ranks_desynced_replica_fails():
+    """One rank's weight perturbed by one bit after the timed steps (test hook): the JSON
+    records the mismatch and bench.py exits 5 instead of reporting a valid number."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, APEX_AMD_SINGLE_DEVICE="1", APEX_AMD_DIST_BACKEND="gloo",
+               APEX_AMD_TEST_DESYNC_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--model", "resnet18", "--batch-size", "8", "--image-size", "32",
+                        "--steps", "2", "--warmup", "1", "--bucket-timing-steps", "0",
+                        "--opt-step-iters", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 5, p.stdout[-2000:] + p.stderr[-4000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["replicas"]["in_sync"] is False
+    assert rec["replicas"]["digests"]["params"]["match"] is False
 
 
 @pytest.mark.timeout(280)

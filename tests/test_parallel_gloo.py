@@ -314,3 +314,20 @@ def test_ddp_tapered_tail_buckets(tmp_path):
     for a, b in zip(tap, plain):
         for x, y in zip(a["grads"], b["grads"]):
             torch.testing.assert_close(x, y)
+
+
+@pytest.mark.parametrize("desync", [-1, 1])
+def test_replica_digests_catch_a_desynced_rank(tmp_path, desync):
+    """bench.py's N > 1 self-check (utils/consistency.py): per-rank digests of the raw
+    bits of parameters / buffers / optimizer state, all-reduced MAX and MIN.  In-sync
+    replicas match in every group; one flipped bit of one weight on rank 1 fails the
+    'params' group on EVERY rank (so all ranks exit non-zero together) and nothing else."""
+    res = W.run("replica_digests", 3, str(tmp_path), desync=desync)
+    for r in res:
+        assert r["comm"]["size"] == 3 and r["comm"]["backend"] == "gloo"
+        if desync < 0:
+            assert all(r["match"].values()), r["match"]
+        else:
+            assert r["match"]["params"] is False
+            assert r["match"]["buffers"] and r["match"]["optimizer_state"]
+    assert len({r["digest"]["params"] for r in res}) == 1
