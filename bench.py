@@ -830,12 +830,13 @@ def replica_check(w, args, world):
     if os.environ.get("APEX_AMD_TEST_DESYNC_RANK") == str(dist.get_rank()):
         # test hook (tests/test_ddp_gpu.py): flip the lowest bit of one weight on one rank
         with torch.no_grad():
-            p = next(iter(w.model.parameters())).detach().view(-1)[:1]
+            p = next(iter(w.model.parameters())).detach()
+            p = p.as_strided((1,), (1,), p.storage_offset())
             p.view({2: torch.int16, 4: torch.int32}[p.element_size()]).add_(1)
     comms = {"world": comm_info(dist.group.WORLD)}
     ddp = getattr(w, "ddp", None)
-    if ddp is not None and getattr(ddp, "_comm_pg", None) is not None:
-        comms["ddp"] = comm_info(ddp._comm_pg)
+    if ddp is not None:
+        comms["ddp"] = comm_info(getattr(ddp, "_comm_pg", None) or dist.group.WORLD)
     if args.impl == "amd" and w.config.get("syncbn"):
         from apex_example_amd.parallel.sync_batchnorm import syncbn_comm_group
         comms["syncbn"] = comm_info(syncbn_comm_group())
