@@ -493,22 +493,17 @@ def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype, out=None, accumulate=True, side=Fals
 # the pre-activation (no separate GELU pass), backward dpre = (dy W2) * gelu'(pre) with the
 # b1 gradient's column sums (no dh round trip, no column-sum kernels).  bf16 / fp16
 # operands, N % 256 == 0, K % 64 == 0.  Default on the one-wave-per-SIMD gemm4w
-# (csrc/hip/gemm4w.hip, APEX_AMD_FFN_KERNEL=1): BERT-large FFN forward 152 us fused vs
-# 164 us for hipBLASLt addmm + the GELU pass, backward 194 vs 217 us
-# (profiles/r5/gemm4w_bench.md).  APEX_AMD_FFN_KERNEL=0 selects the 8-wave gemm8p
-# (slower than the unfused path), APEX_AMD_GEMM8P=0 the unfused path.
-_G8 = os.environ.get("APEX_AMD_GEMM8P", "1") == "1"
-_G8_KERNEL = int(os.environ.get("APEX_AMD_FFN_KERNEL", "1"))
+# (csrc/hip/gemm4w.hip): BERT-large FFN forward 152 us fused vs 164 us for hipBLASLt
+# addmm + the GELU pass, backward 194 vs 217 us (profiles/r5/gemm4w_bench.md).
 
 
-def _g8_ok(a, b, *more):
-    if not (_G8 and a.is_cuda and a.dtype in (torch.bfloat16, torch.float16)
+def _g4w_ok(a, b, *more):
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16)
             and b.dtype == a.dtype
             and all(t is None or t.dtype in (a.dtype, torch.float32) for t in more)
             and _native.available()):
         return False
-    dn = _native.require().dense
-    return dn.gemm4w_ok(a, b) if _G8_KERNEL == 1 else dn.gemm8p_ok(a, b)
+    return _native.require().dense.gemm4w_ok(a, b)
 
 
 _T_KERNEL = os.environ.get("APEX_AMD_DENSE_T_KERNEL", "1") == "1"  # 0: ATen copy (A/B)
@@ -535,10 +530,9 @@ def _gelu_dense_fwd(ctx, x, w1, b1, w2, b2, approximate):
         w1c, b1c, w2c, b2c = _cast(w1, dt), _cast(b1, dt), _cast(w2, dt), _cast(b2, dt)
         x2 = xc.reshape(-1, xc.size(-1))
         res = None
-        if approximate in ("tanh", "none") and _g8_ok(x2, w1c, b1c):
-            h, pre = _native.require().dense.gemm8p(x2, w1c, 1, bias=b1c, want_pre=True,
-                                                    tanh=approximate == "tanh",
-                                                    kernel=_G8_KERNEL)
+        if approximate in ("tanh", "none") and _g4w_ok(x2, w1c, b1c):
+            h, pre = _native.require().dense.gemm4w(x2, w1c, 1, bias=b1c, want_pre=True,
+                                                    tanh=approximate == "tanh")
             res = (h, pre)
         elif approximate == "tanh" and _lt_ok(x2, w1c, b1c):
             # one GEMM: h = gelu(x W1^T + b1) with pre as the epilogue's aux output
@@ -587,16 +581,16 @@ def _gelu_dense_bwd(ctx, dy, dskip=None):
         db2 = _bias_grad(dy2, ctx.b2_dtype)
     res = None
     w2t = None
-    if (_G8 and dy2.dtype in (torch.bfloat16, torch.float16) and pre.dtype == dy2.dtype
+    if (dy2.dtype in (torch.bfloat16, torch.float16) and pre.dtype == dy2.dtype
             and w2c.dtype == dy2.dtype and pre.is_contiguous() and dy2.is_cuda):
         w2t = _transposed(w2c)
-        if not _g8_ok(dy2, w2t):
+        if not _g4w_ok(dy2, w2t):
             w2t = None
     if w2t is not None:
         # one GEMM on the own kernel: dpre = (dy W2) * gelu'(pre) + the b1 column sums
-        res = tuple(_native.require().dense.gemm8p(
+        res = tuple(_native.require().dense.gemm4w(
             dy2, w2t, 2, aux=pre, tanh=ctx.tanh,
-            bias_grad_dtype=ctx.b1_dtype or dy2.dtype, kernel=_G8_KERNEL))
+            bias_grad_dtype=ctx.b1_dtype or dy2.dtype))
     elif ctx.tanh and _lt_ok(dy2, w2c, pre):
         # one GEMM: dpre = (dy W2) * gelu'(pre) and its column sums, dh never stored
         res = _lt_call("dgelu_bgrad_lt", dy2, w2c, pre, ctx.b1_dtype or dy2.dtype)

@@ -44,13 +44,14 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# vs_baseline: BASELINE.md publishes no number for the reference; the comparator
-# is the stock PyTorch-ROCm path (bench.py --impl stock: torch.optim.SGD, PyTorch
-# BatchNorm, MIOpen convs, torch.autocast bf16) measured on MI355X with this same
-# harness, per GPU, bs 256.  Re-measured in round 5 on the headline's box, two runs each
-# (profiles/r5/stock/): stock 5,983.5 / 5,985.6 img/s, this path 11,263.0 / 11,259.0
-# (round 1/2: 6,011.4).
-STOCK_BASELINE_PER_GPU = {"resnet50": 5984.5}
+# vs_baseline: BASELINE.md publishes no number for the reference; the comparator is the
+# stock PyTorch-ROCm path (bench.py --impl stock: torch.optim.SGD(fused), PyTorch
+# BatchNorm, MIOpen convs, torch.autocast bf16) measured on MI355X with this same harness,
+# per GPU, bs 256, at its BEST setting: round 6 re-measured it with MIOpen find mode
+# (--cudnn-benchmark) - 6,540.2 img/s, and 6,538.9 with TunableOp online tuning on top -
+# against 5,983-5,986 in immediate mode (rounds 1-5); this path on the same box 11,510-11,540
+# (profiles/r6/stock/).
+STOCK_BASELINE_PER_GPU = {"resnet50": 6540.2}
 
 
 def parse():

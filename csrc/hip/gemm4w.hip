@@ -2,9 +2,10 @@
 // 256 x 256 workgroup tile, 4 wave64s (2 x 2), a 128 x 128 fp32 accumulator per wave
 // (64 MFMA tiles of 16 x 16 = 256 accumulator registers), bf16 / fp16 in.
 //
-// Why this shape (docs/PERF.md, round 4 PMC comparison): the 8-wave 128 x 64-per-wave
-// kernel (gemm8p.hip) reads 1.5x the LDS bytes per MFMA of a 128 x 128-per-wave tile and
-// its two waves per SIMD spend ~29 % of their cycles parked in s_waitcnt / s_barrier.
+// Why this shape (docs/PERF.md, round 4 PMC comparison): an 8-wave 128 x 64-per-wave
+// kernel (round 4's gemm8p, removed in round 6) reads 1.5x the LDS bytes per MFMA of a
+// 128 x 128-per-wave tile and its two waves per SIMD spent ~29 % of their cycles parked in
+// s_waitcnt / s_barrier.
 // Here each wave owns its SIMD's matrix pipe: per 32-deep k-step it reads 8 A + 8 B
 // fragments (16 ds_read_b128, 16 KB per wave) for 64 MFMAs, i.e. 1/4 KB of LDS per
 // 16x16x32 MFMA instead of 3/8 KB.
@@ -27,8 +28,8 @@
 //
 // The MFMA takes B as its first operand, so each accumulator holds C^T: a lane owns 4
 // CONSECUTIVE columns of one row, written to the LDS output tile as one 8-byte store
-// (rows padded to 528 B: conflict-free), instead of 4 two-byte stores.  Epilogues as
-// gemm8p.hip: plain store; bias + GELU keeping the pre-activation; dGELU from the saved
+// (rows padded to 528 B: conflict-free), instead of 4 two-byte stores.  Epilogues:
+// plain store; bias + GELU keeping the pre-activation; dGELU from the saved
 // pre-activation + the bias gradient's per-tile column sums.
 //
 // M may be ragged (rows past M re-read row M-1 and are never stored); N % 256 == 0,
@@ -140,19 +141,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t w4_rsrc(const void* base, uint
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
-// One output tile per workgroup by default.  VAR bit 2 (A/B option, measured slower):
-// persistent - gridDim.x workgroups (<= one per CU) walk their output tiles b, b + G, ...
-// (b = the XCD-remapped block index) as ONE flattened stream of K-tiles, the DMA ring
-// running two K-tiles ahead across tile boundaries (no per-tile prologue).  Same-box
-// 8192^3: 747 us one tile per workgroup vs 763-768 us persistent (the tile bookkeeping
-// and the spills around the in-loop epilogue cost more than the prologues it hides).
-//
-// VAR bit 0: the 16 DMA pieces of a K-tile two per MFMA group in the first half of
-// k-step 1 instead of one per group (measured 5-11 % slower); bit 1: the 16 fragment
-// reads of a k-step two per MFMA group in its first half instead of one per group
-// (within +-3 % of the default, run to run).  Bit 3: tanh GELU (EPI 1 / 2).
-template <typename TT, int EPI, int VAR>
-__global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
+// One output tile per workgroup.  Measured and removed (round 5, profiles/r5/gemm4w_bench.md):
+// a persistent grid walking tiles b, b + G, ... as one flattened K-tile stream (1-4 %
+// slower: tile bookkeeping and spills around the in-loop epilogue cost more than the
+// prologues it hid), k-half LDS regions (5-6 % slower), two DMA pieces per MFMA group
+// (5-11 % slower), two fragment reads per group (within +-3 %).
+// TANH: the GELU flavour of EPI 1 / 2 (tanh approximation, else erf).
+template <typename TT, int EPI, bool TANH>
+__global__ void __launch_bounds__(kW4T, 1) gemm4w_k(GemmArgs p) {
   typedef typename W4T<TT>::v8 v8;
   // the ring + 2 KB for the bias-gradient column sums of EPI 2
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kW4Slot + 2048];
@@ -161,26 +157,12 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int ntn = p.N >> 8, mtiles = (p.M + 255) >> 8;
-  constexpr bool PERSIST = (VAR & 4) != 0;
-  constexpr bool TANH = (VAR & 8) != 0;  // GELU flavour of EPI 1 / 2 (p.tanh)
-  // k-half regions (VAR bit 4): each K-tile slot holds its two 32-deep halves as separate
-  // 64-byte-row regions, so a half is refilled as soon as its k-step's fragments are read
-  // (one barrier per k-step): every DMA piece gets two k-steps of lead instead of one
-  constexpr bool KH = (VAR & 16) != 0;
-  static_assert(!(KH && PERSIST), "k-half regions: one tile per workgroup");
-  const int G = PERSIST ? (int)gridDim.x : 0, ntiles = mtiles * ntn;
   const int b = w4_xcd_remap(blockIdx.x, gridDim.x);
-  // persistent: tiles b, b + G, ...; otherwise one tile per workgroup (a compile-time 1,
-  // so the tile loop and the load cursor fold away)
-  const int my = PERSIST ? (ntiles - b + G - 1) / G : 1;
-  if (PERSIST && my <= 0) return;
-  (void)ntiles;
   const int KT = p.K >> 6;
-  const int S = my * KT;  // flattened K-tiles of this workgroup
   const int gm_ = p.group_m;
-  // tile r of this workgroup -> (m0, n0) in the grouped order (group_m m-tiles x ntn)
-  auto tile_mn = [&](int r, int& m0, int& n0) {
-    const int id = r * G + b;
+  // this workgroup's tile -> (m0, n0) in the grouped order (group_m m-tiles x ntn)
+  auto tile_mn = [&](int& m0, int& n0) {
+    const int id = b;
     int tm, tn;
     if (gm_ > 1) {
       const int gsz = gm_ * ntn, g = id / gsz;
@@ -203,64 +185,33 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   // the logical chunk the swizzle stores there.
   const int lrow = lane >> 3, pch = lane & 7;
   uint32_t offA[8], offB[8];
-  __amdgpu_buffer_rsrc_t rA, rB;
-  int ld_r = -1;
-  auto set_ld = [&](int r) {  // operand panels of tile r (wave-uniform)
-    int m0, n0;
-    tile_mn(r, m0, n0);
-    if constexpr (KH) {
-      // 64-byte region rows: lane -> (row + lane/4, physical chunk lane%4), logical chunk
-      // = physical ^ w4_key64(row) (row bit 3 = lane bit 5 for a 16-row piece)
+  int tm0, tn0;
+  tile_mn(tm0, tn0);
+  // operand panels of the tile (wave-uniform descriptors, per-lane 32-bit offsets)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = wid * 64 + i * 16 + (lane >> 2);
-        const int ch = (lane & 3) ^ (((lane >> 5) & 1) << 1);
-        const int ar = min(m0 + rr, p.M - 1) - m0;
-        offA[i] = (uint32_t)ar * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
-        offB[i] = (uint32_t)rr * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int rr = wid * 64 + i * 8 + lrow;
-        const int ch = pch ^ w4_key(i * 8 + lrow);
-        const int ar = min(m0 + rr, p.M - 1) - m0;  // rows past M re-read row M-1
-        offA[i] = (uint32_t)ar * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
-        offB[i] = (uint32_t)rr * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
-      }
-    }
-    rA = w4_rsrc(static_cast<const TT*>(p.A) + (int64_t)m0 * p.lda, 0xffffffffu);
-    rB = w4_rsrc(static_cast<const TT*>(p.B) + (int64_t)n0 * p.ldb, 0xffffffffu);
-    ld_r = r;
-  };
-  // the 16 pieces (8 A + 8 B wave-instructions) of flattened K-tile T go to slot T & 1;
-  // past the end the last K-tile is re-fetched into the free slot (uniform stream).
-  // ld_next() steps the load cursor by one K-tile (no divisions: the scalar work sits
-  // in front of k-step 1's MFMAs every K-tile)
-  int ld_kb = 0, ld_kt = 0, ld_T = 0;
+  for (int i = 0; i < 8; ++i) {
+    const int rr = wid * 64 + i * 8 + lrow;
+    const int ch = pch ^ w4_key(i * 8 + lrow);
+    const int ar = min(tm0 + rr, p.M - 1) - tm0;  // rows past M re-read row M-1
+    offA[i] = (uint32_t)ar * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+    offB[i] = (uint32_t)rr * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)ch * 16u;
+  }
+  const __amdgpu_buffer_rsrc_t rA = w4_rsrc(static_cast<const TT*>(p.A) + (int64_t)tm0 * p.lda, 0xffffffffu);
+  const __amdgpu_buffer_rsrc_t rB = w4_rsrc(static_cast<const TT*>(p.B) + (int64_t)tn0 * p.ldb, 0xffffffffu);
+  // the 16 pieces (8 A + 8 B wave-instructions) of K-tile T go to slot T & 1; past the
+  // end the last K-tile is re-fetched into the free slot (uniform stream).  ld_next()
+  // steps the load cursor by one K-tile
+  int ld_kb = 0, ld_T = 0;
   auto ld_next = [&]() {
-    if (ld_T + 1 >= S) return;  // keep re-fetching the last K-tile
+    if (ld_T + 1 >= KT) return;  // keep re-fetching the last K-tile
     ++ld_T;
-    if (++ld_kt == KT) {
-      ld_kt = 0;
-      set_ld(ld_r + 1);
-    }
-    ld_kb = ld_kt * 128;  // byte offset of the K-tile in a row
+    ld_kb = ld_T * 128;  // byte offset of the K-tile in a row
   };
   auto piece = [&](int T, int q) {
     unsigned char* dst = lds + (T & 1) * kW4Slot + (q >> 3) * kW4Op + wid * 8192 + (q & 7) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 8 ? rA : rB,
                                              (__attribute__((address_space(3))) void*)dst, 16,
                                              q < 8 ? offA[q] : offB[q - 8], ld_kb, 0, 0);
-  };
-  // KH: piece q (0..7: A rows i = q, then B rows i = q - 4, 16 rows each) of k-half h of
-  // K-tile T into region (slot T & 1, half h, operand)
-  auto piece_h = [&](int T, int h, int q) {
-    const int o = q >> 2, i = q & 3;
-    unsigned char* dst = lds + (T & 1) * kW4Slot + h * kW4Op + o * (kW4Op / 2) + wid * 4096 + i * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(o == 0 ? rA : rB,
-                                             (__attribute__((address_space(3))) void*)dst, 16,
-                                             o == 0 ? offA[i] : offB[i], ld_kb + h * 64, 0, 0);
   };
 
   // fragment reads: A row wm*128 + i*16 + fr; B row w4_brow; logical chunk ks*4 + fg;
@@ -282,25 +233,7 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   // groups earlier (in natural order B4-7 came last and stalled every k-step's start).
   auto rd_order = [](int n) { return n < 4 ? 8 + n : n == 4 ? 0 : n < 9 ? 7 + n : n - 8; };
   // read one fragment (r < 8: A[r], else B[r - 8]) of k-step ks of the tile in `slot`
-  // KH region reads: 64-byte rows, key w4_key64 = row bit 3 (x 2); for the A rows
-  // (i*16 + fr) and the permuted B rows (w4_brow) it is ((fr >> 2) & 2) / ((fr >> 2) & 1) * 2
-  const int offKA = fr * 64 + ((fg ^ ((fr >> 2) & 2)) << 4);
-  int offKB[2];
-#pragma unroll
-  for (int par = 0; par < 2; ++par)
-    offKB[par] = w4_brow(par, fr) * 64 + ((fg ^ (((fr >> 2) & 1) << 1)) << 4);
   auto rd = [&](int slot, int ks, int r, v8(&fa)[8], v8(&fb)[8]) {
-    if constexpr (KH) {
-      const unsigned char* base = lds + slot * kW4Slot + ks * kW4Op;
-      if (r < 8) {
-        fa[r] = *reinterpret_cast<const v8*>(base + offKA + (wm * 128 + r * 16) * 64);
-      } else {
-        const int j = r - 8;
-        fb[j] = *reinterpret_cast<const v8*>(base + kW4Op / 2 + offKB[j & 1] +
-                                             (wn * 128 + (j >> 1) * 32) * 64);
-      }
-      return;
-    }
     const unsigned char* base = lds + slot * kW4Slot;
     if (r < 8) {
       fa[r] = *reinterpret_cast<const v8*>(base + offRA[ks][r & 1] + (wm * 128 + (r & 6) * 16) * 128);
@@ -317,11 +250,7 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   // for row block i and column pair q, the 8 consecutive columns wn*128 + q*32 + fg*8 ..
   // +7 of row wm*128 + i*16 + fr (C^T accumulators of B fragments 2q, 2q+1).  Buffer
   // stores against a descriptor that ends at row M: rows past M are dropped by the
-  // hardware, so every store instruction issues and the vmcnt accounting is static.
-  // vmcnt units an epilogue may leave in flight: its 16-byte stores (EPI 1: h and pre, 64;
-  // vmcnt is 6 bits, and 63 still retires every older DMA piece; EPI 2's aux loads are
-  // consumed before its last store)
-  constexpr int kEpiStores = EPI == 1 ? 63 : 32;
+  // hardware, so every store instruction issues.
   float* red = reinterpret_cast<float*>(lds + 2 * kW4Slot);
   auto epilogue = [&](int m0, int n0) {
     const uint32_t rows = (uint32_t)min(256, p.M - m0);
@@ -430,30 +359,14 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
     }
   };
 
-  // prologue: K-tiles 0 and 1 in flight, wait for K-tile 0 (KH: its k-half 0), read its
-  // k-step-0 fragments
-  set_ld(0);
-  if constexpr (KH) {
+  // prologue: K-tiles 0 and 1 in flight, wait for K-tile 0, read its k-step-0 fragments
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+  for (int q = 0; q < 16; ++q) piece(0, q);
+  ld_next();
 #pragma unroll
-      for (int q = 0; q < 8; ++q) piece_h(0, h, q);
-    ld_next();
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) piece_h(1, h, q);
-    ld_next();
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  } else {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) piece(0, q);
-    ld_next();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) piece(1, q);
-    ld_next();  // the cursor now names K-tile 2 (issued by k-step 1 of K-tile 0)
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  }
+  for (int q = 0; q < 16; ++q) piece(1, q);
+  ld_next();  // the cursor now names K-tile 2 (issued by k-step 1 of K-tile 0)
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   w4_barrier();
 #pragma unroll
   for (int r = 0; r < 16; ++r) rd(0, 0, rd_order(r), fa0, fb0);
@@ -473,16 +386,9 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
   // one flattened K-tile t: k-step 0 (FIRST: a tile's first K-tile starts the
   // accumulators from zero) reading F1, then k-step 1 reading the next K-tile's F0 and
   // issuing K-tile t+2's DMA
-  auto ktile = [&](int t, auto first_c, bool stores_behind) {
+  auto ktile = [&](int t, auto first_c) {
     constexpr bool FIRST = decltype(first_c)::value;
     const int slot = t & 1;
-    if constexpr (KH) {
-      // k-step 0: k-half 1 of this K-tile landed (vmcnt(16) leaves K-tile t+1's two
-      // halves in flight), every wave's k-half-0 reads of this slot retired -> refill it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      w4_barrier();
-    }
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       if constexpr (FIRST) {
@@ -491,63 +397,29 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(G8Args p) {
         W4_GROUP(fa0, fb0, g);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((VAR & 2) == 0) {
-        rd(slot, 1, rd_order(g), fa1, fb1);
-      } else if (g < 8) {
-        rd(slot, 1, rd_order(2 * g), fa1, fb1);
-        rd(slot, 1, rd_order(2 * g + 1), fa1, fb1);
-      }
-      if constexpr (KH) {
-        if (g & 1) piece_h(t + 2, 0, g >> 1);
-      }
+      rd(slot, 1, rd_order(g), fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // k-step 1: K-tile t+1 must have landed (every wave's DMA: vmcnt + barrier; the
-    // previous tile's epilogue stores, issued after it, may stay in flight), and every
+    // k-step 1: K-tile t+1 must have landed (every wave's DMA: vmcnt + barrier), and every
     // wave's reads of this slot are retired before K-tile t+2's DMA overwrites it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (KH) {
-      // k-half 0 of K-tile t+1 landed (K-tile t+1's k-half 1 and K-tile t+2's k-half 0 stay
-      // in flight); every wave's k-half-1 reads of this slot retired -> refill it
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    } else if (stores_behind) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiStores) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     w4_barrier();
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       W4_GROUP(fa1, fb1, g);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((VAR & 2) == 0) {
-        rd(slot ^ 1, 0, rd_order(g), fa0, fb0);
-      } else if (g < 8) {
-        rd(slot ^ 1, 0, rd_order(2 * g), fa0, fb0);
-        rd(slot ^ 1, 0, rd_order(2 * g + 1), fa0, fb0);
-      }
-      if constexpr (KH) {
-        if (g & 1) piece_h(t + 2, 1, g >> 1);
-      } else if constexpr ((VAR & 1) == 0) {
-        piece(t + 2, g);
-      } else if (g < 8) {
-        piece(t + 2, 2 * g);
-        piece(t + 2, 2 * g + 1);
-      }
+      rd(slot ^ 1, 0, rd_order(g), fa0, fb0);
+      piece(t + 2, g);
       __builtin_amdgcn_sched_barrier(0);
     }
     ld_next();  // K-tile t+3, for the next K-tile's k-step 1
   };
 
-  int t = 0;
-  for (int r = 0; r < my; ++r) {
-    ktile(t++, std::true_type{}, r > 0);
-    for (int kt = 1; kt < KT; ++kt) ktile(t++, std::false_type{}, false);
-    w4_mfma_drain();
-    int m0, n0;
-    tile_mn(r, m0, n0);
-    epilogue(m0, n0);
-  }
+  ktile(0, std::true_type{});
+  for (int kt = 1; kt < KT; ++kt) ktile(kt, std::false_type{});
+  w4_mfma_drain();
+  epilogue(tm0, tn0);
 #undef W4_GROUP
 #undef W4_GROUP0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -559,67 +431,23 @@ bool gemm4w_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % 256 == 0 && K >= 64 && K % 64 == 0;
 }
 
-// APEX_AMD_G4W_VAR: K-loop variant for A/B runs (see gemm4w_k), read per launch
-static int g4w_var() {
-  const char* e = std::getenv("APEX_AMD_G4W_VAR");
-  return e ? std::atoi(e) : 0;
-}
-
-static int g4w_group_m() {
-  static const int v = [] {
-    const char* e = std::getenv("APEX_AMD_G4W_GROUPM");
-    return e ? std::max(1, std::atoi(e)) : 4;
-  }();
-  return v;
-}
-
-static int g4w_cus() {
-  static const int v = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    return n;
-  }();
-  return v;
-}
-
-void gemm4w(const G8Args& a0, int epi, hipStream_t st) {
-  G8Args a = a0;
-  a.group_m = g4w_group_m();
+void gemm4w(const GemmArgs& a0, int epi, hipStream_t st) {
+  GemmArgs a = a0;
+  a.group_m = 4;  // XCD-grouped tile order: 4 m-tiles per group (measured best, round 5)
   const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
-  // one tile per workgroup (VAR bit 2: persistent, one workgroup per CU)
-  auto launch = [&](auto t0, auto v0) {
+  auto launch = [&](auto t0, auto tanh_c) {
     using TT = decltype(t0);
-    constexpr int V = decltype(v0)::value;
-    const int grid = (V & 4) ? std::min(ntiles, g4w_cus()) : ntiles;
-    hipLaunchKernelGGL((gemm4w_k<TT, 0, V>), dim3(grid), dim3(kW4T), 0, st, a);
-  };
-  // EPI 1 / 2: the default K loop, the GELU flavour as a template bit
-  auto launch_epi = [&](auto t0, auto v0) {
-    using TT = decltype(t0);
-    constexpr int V = decltype(v0)::value;
-    static_assert((V & 4) == 0, "EPI 1 / 2 run one tile per workgroup");
-    const int grid = ntiles;
-    if (epi == 1)
-      hipLaunchKernelGGL((gemm4w_k<TT, 1, V>), dim3(grid), dim3(kW4T), 0, st, a);
+    constexpr bool TH = decltype(tanh_c)::value;
+    if (epi == 0)
+      hipLaunchKernelGGL((gemm4w_k<TT, 0, false>), dim3(ntiles), dim3(kW4T), 0, st, a);
+    else if (epi == 1)
+      hipLaunchKernelGGL((gemm4w_k<TT, 1, TH>), dim3(ntiles), dim3(kW4T), 0, st, a);
     else
-      hipLaunchKernelGGL((gemm4w_k<TT, 2, V>), dim3(grid), dim3(kW4T), 0, st, a);
+      hipLaunchKernelGGL((gemm4w_k<TT, 2, TH>), dim3(ntiles), dim3(kW4T), 0, st, a);
   };
   auto go = [&](auto t0) {
-    if (epi != 0) {
-      if (a.tanh) launch_epi(t0, std::integral_constant<int, 8>{});
-      else launch_epi(t0, std::integral_constant<int, 0>{});
-      return;
-    }
-    switch (g4w_var()) {
-      case 1: launch(t0, std::integral_constant<int, 1>{}); break;
-      case 6: launch(t0, std::integral_constant<int, 6>{}); break;
-      case 2: launch(t0, std::integral_constant<int, 2>{}); break;
-      case 16: launch(t0, std::integral_constant<int, 16>{}); break;
-      case 18: launch(t0, std::integral_constant<int, 18>{}); break;
-      default: launch(t0, std::integral_constant<int, 0>{}); break;
-    }
+    if (a.tanh) launch(t0, std::true_type{});
+    else launch(t0, std::false_type{});
   };
   if (a.fp16) go(half_t{});
   else go(bf16_t{});

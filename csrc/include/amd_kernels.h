@@ -272,12 +272,12 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
 void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int C,
                   hipStream_t st);
 
-// ---- 256 x 256 8-phase MFMA GEMM (gemm8p.hip) ---------------------------------
+// ---- 256 x 256 one-wave-per-SIMD MFMA GEMM (gemm4w.hip) -------------------------
 // C[M, N] = A[M, K] . B[N, K]^T, bf16 / fp16 row-major (K contiguous), fp32 accumulation.
 // epi 0: C = bf16(acc); 1: pre = bf16(acc + bias) -> aux (if non-null), C = gelu(pre);
 // 2: C = bf16(bf16(acc) * gelu'(aux)) and colsum[M-tile][N] = per-tile column sums of C.
-// Requires N % 256 == 0, K % 128 == 0 (gemm8p_supported); M ragged.
-struct G8Args {
+// Requires N % 256 == 0, K % 64 == 0 (gemm4w_supported); M ragged.
+struct GemmArgs {
   const void* A;               // bf16
   const void* B;               // bf16
   void* C;                     // bf16
@@ -288,15 +288,10 @@ struct G8Args {
   float* colsum;               // [ceil(M / 256)][N] (epi 2), may be null
   int tanh;                    // GELU flavour: 1 tanh approximation, 0 erf
   int fp16;                    // operands / outputs fp16 instead of bf16
-  int group_m;                 // tile order: groups of group_m m-tiles (set by gemm8p())
+  int group_m;                 // tile order: groups of group_m m-tiles (set by gemm4w())
 };
-bool gemm8p_supported(int M, int N, int K);
-int gemm8p_mtiles(int M);
-void gemm8p(const G8Args& a, int epi, hipStream_t st);
-// the same GEMM and epilogues with one wave per SIMD, 128 x 128 per wave (gemm4w.hip):
-// N % 256 == 0, K % 64 == 0
 bool gemm4w_supported(int M, int N, int K);
-void gemm4w(const G8Args& a, int epi, hipStream_t st);
+void gemm4w(const GemmArgs& a, int epi, hipStream_t st);
 // dense weight gradients P[s] = A_s^T B_s over row splits (wgrad4w.hip): A [T, M], B [T, N]
 // row-major bf16 / fp16, fp32 partials P [S][M][N]; M, N % 256 == 0, (T / S) % 64 == 0
 struct WgradArgs {

@@ -113,11 +113,6 @@ static bool gemm_layout_ok(const at::Tensor& a, const at::Tensor& b) {
          256 * std::max(a.stride(0), b.stride(0)) * a.element_size() < (int64_t(1) << 32);
 }
 
-bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b) {
-  return gemm_layout_ok(a, b) &&
-         gemm8p_supported((int)a.size(0), (int)b.size(0), (int)a.size(1));
-}
-
 bool gemm4w_ok(const at::Tensor& a, const at::Tensor& b) {
   return gemm_layout_ok(a, b) &&
          gemm4w_supported((int)a.size(0), (int)b.size(0), (int)a.size(1));
@@ -220,19 +215,18 @@ std::tuple<at::Tensor, at::Tensor> wgrad4w_bias_op(at::Tensor dy, at::Tensor x, 
   return {w, db};
 }
 
-std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
+std::vector<at::Tensor> gemm4w_op(at::Tensor a, at::Tensor b, int64_t epi,
                                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
                                   bool want_pre, bool tanh_approx,
-                                  c10::optional<at::ScalarType> bias_grad_dtype, int64_t kernel) {
+                                  c10::optional<at::ScalarType> bias_grad_dtype) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(kernel == 0 || kernel == 1, "gemm8p: kernel 0 (8-wave gemm8p) | 1 (4-wave gemm4w)");
-  TORCH_CHECK(kernel == 1 ? gemm4w_ok(a, b) : gemm8p_ok(a, b),
-              "gemm8p: bf16 / fp16 [M, K] x [N, K] with N % 256 == 0, K % 128 == 0 (kernel 1: "
-              "K % 64 == 0), unit column stride, 16-byte aligned rows");
-  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8p: epi 0 | 1 | 2");
+  TORCH_CHECK(gemm4w_ok(a, b),
+              "gemm4w: bf16 / fp16 [M, K] x [N, K] with N % 256 == 0, K % 64 == 0, unit column "
+              "stride, 16-byte aligned rows");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm4w: epi 0 | 1 | 2");
   const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
   at::Tensor c = at::empty({M, N}, a.options());
-  G8Args g{};
+  GemmArgs g{};
   g.A = a.data_ptr();
   g.B = b.data_ptr();
   g.C = c.data_ptr();
@@ -249,7 +243,7 @@ std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
     if (bias.has_value() && bias->defined()) {
       TORCH_CHECK(bias->is_cuda() && bias->is_contiguous() && bias->numel() == N &&
                       (bias->scalar_type() == a.scalar_type() || bias->scalar_type() == at::kFloat),
-                  "gemm8p: bias must be a contiguous [N] GPU tensor of the operand dtype or fp32");
+                  "gemm4w: bias must be a contiguous [N] GPU tensor of the operand dtype or fp32");
       g.bias = bias->data_ptr();
       g.bias_f32 = bias->scalar_type() == at::kFloat ? 1 : 0;
     }
@@ -262,16 +256,15 @@ std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
     TORCH_CHECK(aux.has_value() && aux->defined() && aux->is_cuda() &&
                     aux->scalar_type() == a.scalar_type() && aux->is_contiguous() &&
                     aux->numel() == M * N,
-                "gemm8p: epi 2 needs the contiguous bf16 [M, N] pre-activation");
+                "gemm4w: epi 2 needs the contiguous bf16 [M, N] pre-activation");
     g.aux = aux->data_ptr();
   }
   at::Tensor part;
   if (epi == 2 && bias_grad_dtype.has_value()) {
-    part = at::empty({(int64_t)gemm8p_mtiles((int)M), N}, a.options().dtype(at::kFloat));
+    part = at::empty({(M + 255) / 256, N}, a.options().dtype(at::kFloat));
     g.colsum = part.data_ptr<float>();
   }
-  if (kernel == 1) gemm4w(g, (int)epi, cur_stream());
-  else gemm8p(g, (int)epi, cur_stream());
+  gemm4w(g, (int)epi, cur_stream());
   if (part.defined()) {
     at::Tensor db = at::empty({N}, a.options().dtype(*bias_grad_dtype));
     colsum_finalize(part.data_ptr<float>(), (int)part.size(0), (int)N, db.data_ptr(),

@@ -19,12 +19,10 @@ at::Tensor gelu_fwd_op(at::Tensor x, bool tanh_approx);
 std::tuple<at::Tensor, at::Tensor> act_bwd_bias_grad_op(at::Tensor dh, at::Tensor y, int64_t act,
                                                         at::ScalarType out_dtype);
 
-// The own 256 x 256 8-phase MFMA GEMM (csrc/hip/gemm8p.hip): C = A . B^T for bf16 A [M, K]
-// and B [N, K] (row-major), with the FFN epilogues.  epi 0: [C]; epi 1: bias + GELU ->
-// [h, pre (when want_pre)]; epi 2: dGELU from aux = pre -> [dpre, bias grad (when
-// bias_grad_dtype is given)].  gemm8p_ok: the shape / dtype / layout qualifies.
-// kernel 1: the one-wave-per-SIMD 128 x 128-per-wave form (csrc/hip/gemm4w.hip).
-bool gemm8p_ok(const at::Tensor& a, const at::Tensor& b);
+// The own 256 x 256 one-wave-per-SIMD MFMA GEMM (csrc/hip/gemm4w.hip): C = A . B^T for
+// bf16 / fp16 A [M, K] and B [N, K] (row-major), with the FFN epilogues.  epi 0: [C];
+// epi 1: bias + GELU -> [h, pre (when want_pre)]; epi 2: dGELU from aux = pre -> [dpre,
+// bias grad (when bias_grad_dtype is given)].  gemm4w_ok: the shape / dtype / layout qualifies.
 bool gemm4w_ok(const at::Tensor& a, const at::Tensor& b);
 bool wgrad4w_ok(const at::Tensor& dy, const at::Tensor& x, int64_t splits);
 std::tuple<at::Tensor, at::Tensor> wgrad4w_bias_op(at::Tensor dy, at::Tensor x, int64_t splits,
@@ -33,9 +31,9 @@ std::tuple<at::Tensor, at::Tensor> wgrad4w_bias_op(at::Tensor dy, at::Tensor x, 
                                                    at::ScalarType bias_dtype);
 at::Tensor wgrad4w_op(at::Tensor dy, at::Tensor x, int64_t splits, at::ScalarType out_dtype,
                       c10::optional<at::Tensor> out, bool accumulate);
-std::vector<at::Tensor> gemm8p_op(at::Tensor a, at::Tensor b, int64_t epi,
+std::vector<at::Tensor> gemm4w_op(at::Tensor a, at::Tensor b, int64_t epi,
                                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux,
                                   bool want_pre, bool tanh_approx,
-                                  c10::optional<at::ScalarType> bias_grad_dtype, int64_t kernel);
+                                  c10::optional<at::ScalarType> bias_grad_dtype);
 
 }  // namespace amd

@@ -137,11 +137,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   dn.def("lt_cache_clear", &lt_algo_cache_clear);
   dn.def("lt_probe", &lt_probe_op);
   dn.def("wgrad_bgrad_lt", &dense_wgrad_bgrad_op);
-  dn.def("gemm8p", &gemm8p_op, py::arg("a"), py::arg("b"), py::arg("epi") = 0,
+  dn.def("gemm4w", &gemm4w_op, py::arg("a"), py::arg("b"), py::arg("epi") = 0,
          py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("want_pre") = false,
-         py::arg("tanh") = false, py::arg("bias_grad_dtype") = py::none(),
-         py::arg("kernel") = 0);
-  dn.def("gemm8p_ok", &gemm8p_ok);
+         py::arg("tanh") = false, py::arg("bias_grad_dtype") = py::none());
   dn.def("gemm4w_ok", &gemm4w_ok);
   dn.def("wgrad4w", &wgrad4w_op, py::arg("dy"), py::arg("x"), py::arg("splits"),
          py::arg("out_dtype"), py::arg("out") = py::none(), py::arg("accumulate") = true);

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Run ONE GEMM shape many times through gemm8p, gemm4w and torch.mm (hipBLASLt), for
+"""Run ONE GEMM shape many times through gemm4w and torch.mm (hipBLASLt), for
 rocprofv3 --pmc passes (tools/diag/run_pmc.sh tools/diag/g8_pmc.py tools/diag/g8_pmc.txt)."""
 import argparse
 import os
@@ -16,7 +16,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--k", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--kernels", default="8p,4w,lt", help="gemm8p, gemm4w, hipBLASLt")
+    ap.add_argument("--kernels", default="4w,lt", help="gemm4w, hipBLASLt")
     a = ap.parse_args()
     from apex_example_amd import _native
 
@@ -26,10 +26,8 @@ def main():
     w = torch.randn(a.n, a.k, device="cuda", generator=g).to(torch.bfloat16)
     ks = a.kernels.split(",")
     for _ in range(a.iters):
-        if "8p" in ks:
-            dn.gemm8p(x, w, 0, None, None, False, False, None, 0)
         if "4w" in ks:
-            dn.gemm8p(x, w, 0, None, None, False, False, None, 1)
+            dn.gemm4w(x, w)
         if "lt" in ks:
             torch.mm(x, w.t())
     torch.cuda.synchronize()

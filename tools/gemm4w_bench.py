@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""The one-wave-per-SIMD GEMM (csrc/hip/gemm4w.hip, 128 x 128 per wave) against the
-8-wave gemm8p and hipBLASLt (torch.mm, TunableOp off) on the transformer FFN shapes and
-square GEMMs: a correctness check against fp32 first, then interleaved timing rounds in
-one process on random data (K-loop variants via APEX_AMD_G4W_VAR, read per launch)."""
+"""The one-wave-per-SIMD GEMM (csrc/hip/gemm4w.hip, 128 x 128 per wave) against
+hipBLASLt (torch.mm, TunableOp off) on the transformer dense shapes and square GEMMs: a
+correctness check against fp32 first, then interleaved timing rounds in one process on
+random data."""
 import argparse
 import os
 import sys
@@ -33,7 +33,6 @@ SHAPES = [("bert ffn-in", 16384, 4096, 1024), ("bert ffn-out", 16384, 1024, 4096
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--vars", default="0,1")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--quick", action="store_true")
     args = ap.parse_args()
@@ -41,7 +40,6 @@ def main():
 
     dn = _native.require().dense
     dev = "cuda"
-    variants = [int(v) for v in args.vars.split(",")]
 
     # correctness vs fp32 (ragged M, odd K-tile counts, fp16), every variant
     for (m, n, k, dt) in [(256, 256, 64, torch.bfloat16), (1000, 512, 192, torch.bfloat16),
@@ -51,15 +49,12 @@ def main():
         a = torch.randn(m, k, device=dev, generator=g).to(dt)
         b = torch.randn(n, k, device=dev, generator=g).to(dt)
         ref = a.float() @ b.float().t()
-        for v in variants:
-            os.environ["APEX_AMD_G4W_VAR"] = str(v)
-            c = dn.gemm8p(a, b, kernel=1)[0]
-            err = float((c.float() - ref).abs().max() / ref.abs().max())
-            print("check %d x %d x %d %s var %d: max rel err %.2e" % (m, n, k, dt, v, err),
-                  flush=True)
-            assert err < 1e-2, err
+        c = dn.gemm4w(a, b)[0]
+        err = float((c.float() - ref).abs().max() / ref.abs().max())
+        print("check %d x %d x %d %s: max rel err %.2e" % (m, n, k, dt, err), flush=True)
+        assert err < 1e-2, err
     shapes = SHAPES[:3] + SHAPES[-1:] if args.quick else SHAPES
-    cols = ["gemm8p"] + ["gemm4w v%d" % v for v in variants] + ["hipBLASLt"]
+    cols = ["gemm4w", "hipBLASLt"]
     print("\n| GEMM | M, N, K | " + " | ".join(cols) + " |")
     print("|---|---|" + "---|" * len(cols))
     for name, m, n, k in shapes:
@@ -67,13 +62,7 @@ def main():
         a = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
         b = torch.randn(n, k, device=dev, generator=g).to(torch.bfloat16)
         gf = 2.0 * m * n * k / 1e9
-        fns = [lambda: dn.gemm8p(a, b)]
-        for v in variants:
-            def f(v=v):
-                os.environ["APEX_AMD_G4W_VAR"] = str(v)
-                return dn.gemm8p(a, b, kernel=1)
-            fns.append(f)
-        fns.append(lambda: torch.mm(a, b.t()))
+        fns = [lambda: dn.gemm4w(a, b), lambda: torch.mm(a, b.t())]
         ts = [[] for _ in fns]
         for _ in range(args.rounds):
             for i, fn in enumerate(fns):
@@ -86,7 +75,6 @@ def main():
 def ffn_rows(dn, dev, rounds):
     """The fused FFN epilogues against the unfused sequence they replace (BERT-large
     shapes: x [16384, 1024], W1 [4096, 1024], W2 [1024, 4096], tanh GELU)."""
-    os.environ["APEX_AMD_G4W_VAR"] = "2"
     m, n, k = 16384, 4096, 1024
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
@@ -107,16 +95,11 @@ def ffn_rows(dn, dev, rounds):
         return dn.gelu_bwd_bias_grad(dh, pre, True, torch.bfloat16)
 
     rows = [("fwd: hipBLASLt addmm + GELU pass", unfused_fwd),
-            ("fwd: gemm8p bias+GELU epilogue",
-             lambda: dn.gemm8p(x, w1, 1, bias=b1, want_pre=True, tanh=True)),
             ("fwd: gemm4w bias+GELU epilogue",
-             lambda: dn.gemm8p(x, w1, 1, bias=b1, want_pre=True, tanh=True, kernel=1)),
+             lambda: dn.gemm4w(x, w1, 1, bias=b1, want_pre=True, tanh=True)),
             ("bwd: hipBLASLt mm + dGELU/bias-grad pass", unfused_bwd),
-            ("bwd: gemm8p dGELU+colsum epilogue",
-             lambda: dn.gemm8p(dy, w2t, 2, aux=pre, tanh=True, bias_grad_dtype=torch.bfloat16)),
             ("bwd: gemm4w dGELU+colsum epilogue",
-             lambda: dn.gemm8p(dy, w2t, 2, aux=pre, tanh=True, bias_grad_dtype=torch.bfloat16,
-                               kernel=1))]
+             lambda: dn.gemm4w(dy, w2t, 2, aux=pre, tanh=True, bias_grad_dtype=torch.bfloat16))]
     ts = [[] for _ in rows]
     for _ in range(rounds):
         for i, (_, fn) in enumerate(rows):
