@@ -34,11 +34,35 @@ def supported(t: torch.Tensor, head_dim: int) -> bool:
             and _native.available())
 
 
+_WARNED = set()
+
+
+def effective_dropout(p: float) -> float:
+    """The dropout rate the kernels apply for a requested ``p``: one hash byte per
+    (query, key) is compared with round(256 p), so the rate is a multiple of 1/256
+    (p = 0.1 runs at 26/256 = 0.1016), and any p > 0 drops at least 1/256."""
+    if p <= 0.0:
+        return 0.0
+    return min(256, max(1, int(p * 256.0 + 0.5))) / 256.0
+
+
+def _check_rate(p: float) -> None:
+    """Warn (once per rate) where the 1/256 quantisation moves the rate by more than 2 %."""
+    q = effective_dropout(p)
+    if p > 0.0 and abs(q - p) > 0.02 * p and p not in _WARNED:
+        import warnings
+
+        _WARNED.add(p)
+        warnings.warn("fused attention: dropout p=%g runs at %g (the kernels quantise the rate "
+                      "to 1/256)" % (p, q))
+
+
 def _seed(dropout_p: float) -> int:
     """Per-call dropout seed from torch's CPU generator (no device sync; follows
     torch.manual_seed)."""
     if dropout_p <= 0.0:
         return 0
+    _check_rate(dropout_p)
     return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
 
 

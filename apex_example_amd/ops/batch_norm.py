@@ -443,8 +443,7 @@ class BatchNormFunction(torch.autograd.Function):
             return (dx, dz if ctx.has_z else None, gw if need_w else None,
                     gb if need_w else None, None, None, None, None, None, None, None, None, None, None, None)
         if ctx.world == 1 and xl.is_cuda:
-            # one persistent launch (reduce + dgamma/dbeta + dx) where the activation fits
-            # the register file, else reduce + elementwise (csrc/hip/bn_persist.hip)
+            # reduce + elementwise, one native call
             dx, dz, gw, gb = C.backward_local(dyl, xl, mean, invstd, weight, bias, zl,
                                               ctx.fuse_relu, need_w, ctx.has_z, mask=mask)
             if ctx.shape_channel_last:

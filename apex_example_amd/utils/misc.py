@@ -25,10 +25,10 @@ def set_deterministic(on=True):
     Every reduction of this framework's own kernels is already fixed-order (slab
     partials + finalize kernels, no float atomics): optimizers / norms, LayerNorm,
     BatchNorm, bias gradients, split-K weight-gradient reductions, attention, the
-    embedding backward (device sort + ordered run sums).  The one kernel family
-    with float atomics, the opt-in persistent BatchNorm (APEX_AMD_BN_PERSIST), is
-    switched off here, MIOpen is constrained to deterministic solvers, and PyTorch
-    ops are asked for their deterministic variants (warn-only).  Returns the mode."""
+    embedding backward (device sort + ordered run sums).  MIOpen is constrained to
+    deterministic solvers, the embedding backward takes its deterministic mode, and
+    PyTorch ops are asked for their deterministic variants (warn-only).  Returns the
+    mode."""
     global _DETERMINISTIC
     _DETERMINISTIC = bool(on)
     if torch.cuda.is_available():
@@ -37,7 +37,6 @@ def set_deterministic(on=True):
     torch.use_deterministic_algorithms(_DETERMINISTIC, warn_only=True)
     from .. import _native
     if _DETERMINISTIC and _native.available():
-        _native.require().bn.persist_enable(0)
         from ..ops import embedding
         embedding._MODE = "det"
     return _DETERMINISTIC

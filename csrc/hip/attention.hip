@@ -225,32 +225,7 @@ struct AttnArgs {
   uint32_t thr8;     // dropout threshold round(p * 256) on a hash byte, 0 = no dropout
   float inv_keep;    // 1 / (1 - p)
   uint32_t seed;
-  int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
-  int addr64;  // APEX_AMD_ATTN_ADDR64=1: per-lane 64-bit tile DMA addresses (A/B only)
 };
-
-int attn_addr64_flag() {
-  const char* e = std::getenv("APEX_AMD_ATTN_ADDR64");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
-int attn_base_flag() {
-  const char* e = std::getenv("APEX_AMD_ATTN_BASE");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
-// APEX_AMD_ATTN_FWD=1|2: forward kernel variant (read per launch, for A/B runs)
-int attn_fwd_variant() {
-  const char* e = std::getenv("APEX_AMD_ATTN_FWD");
-  return (e && e[0] == '2') ? 2 : 1;
-}
-
-// APEX_AMD_ATTN_DQ_IL=0: dQ kernel without the interleaved clean-tile body (A/B;
-// measured 3-4 % slower)
-int attn_dq_interleave() {
-  const char* e = std::getenv("APEX_AMD_ATTN_DQ_IL");
-  return (e && e[0] == '0') ? 0 : 1;
-}
 
 // ---------------------------------------------------------------------------- forward
 // Block -> (tile, b*H+h).  Dispatch order is the flattened block id (x fastest) and
@@ -259,14 +234,8 @@ int attn_dq_interleave() {
 // Q/dO (dK/dV) stream through one L2 instead of up to 8; (2) under a causal mask the
 // tiles with the most work are dispatched first (longest-processing-time order: the
 // last query tiles in fwd / dQ, the first key tiles in dK/dV), so the light diagonal
-// tiles fill the tail instead of a few heavy ones.  `base`: the round-1 mapping (A/B).
-__device__ __forceinline__ void tile_of_block(bool causal, bool heavy_high, int base, int& tile,
-                                              int& bh) {
-  if (base) {
-    tile = blockIdx.x;
-    bh = blockIdx.y;
-    return;
-  }
+// tiles fill the tail instead of a few heavy ones.
+__device__ __forceinline__ void tile_of_block(bool causal, bool heavy_high, int& tile, int& bh) {
   const int nt = gridDim.x, nbh = gridDim.y;
   const int id = blockIdx.x + blockIdx.y * nt;
   const int t = id / nbh;
@@ -290,7 +259,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
-  tile_of_block(CAUSAL, true, a.base, tile, bh);
+  tile_of_block(CAUSAL, true, tile, bh);
   const int b = bh / a.H, hh = bh - b * a.H;
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;  // this lane's query
@@ -328,7 +297,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   auto issue = [&](int kt, int buf) {
     unsigned char* Kl = lds + buf * 2 * kAKT * kARow;
     unsigned char* Vl = Kl + kAKT * kARow;
-    if ((kt + 1) * kAKT <= a.S && !a.addr64) {
+    if ((kt + 1) * kAKT <= a.S) {
       const T* kb = tile_base(K, kt * kAKT, a.kss);
       const T* vb = tile_base(V, kt * kAKT, a.vss);
 #pragma unroll
@@ -414,7 +383,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
     // the O / l rescale by exp2(m - mnew) is skipped while no query of the wave
     // raised its running max (alpha == 1 exactly: same math, 32 fewer multiplies
     // per tile - the common case once the first tiles have set the max)
-    const bool grow = a.base || __any(mnew != m);
+    const bool grow = __any(mnew != m);
     const float alpha = grow ? fexp2(m - mnew) : 1.f;
     m = mnew;
     float psum = 0.f;
@@ -469,234 +438,6 @@ __global__ void __launch_bounds__(kAT, 2) attn_fwd_k(AttnArgs a) {
   }
 }
 
-// Forward, software-pipelined (APEX_AMD_ATTN_FWD=2 selects it; A/B against attn_fwd_k):
-// the QK^T MFMAs of tile kt+1 are issued in the same basic block as the softmax of
-// tile kt, so the matrix pipe and the VALU work on independent streams of one wave;
-// K/V pass through a 3-deep LDS ring (tile kt's V, tile kt+1's K, tile kt+2 in
-// flight).  Tiles that need no mask for any query of the workgroup run this body;
-// boundary / diagonal tiles take the masked, unpipelined body afterwards.
-template <typename T, bool CAUSAL, bool DROP>
-__global__ void __launch_bounds__(kAT, 2) attn_fwd2_k(AttnArgs a) {
-  typedef typename Frag<T>::v8 v8;
-  constexpr int TB = 2 * kAKT * kARow;  // one (K, V) tile: 16 KiB
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * TB];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
-  const int hl = lane >> 5, c32 = lane & 31;
-  int tile, bh;
-  tile_of_block(CAUSAL, true, 0, tile, bh);
-  const int b = bh / a.H, hh = bh - b * a.H;
-  const int qb0 = tile * 128;
-  const int q = qb0 + wid * 32 + c32;
-  const uint32_t dbase = DROP ? drop_base(a.seed, (uint32_t)bh) + (uint32_t)q * kDropQ +
-                                    (uint32_t)hl * kDropK
-                              : 0u;
-  const T* Q = static_cast<const T*>(a.q) + b * a.qsb + hh * a.qsh;
-  const T* K = static_cast<const T*>(a.k) + b * a.ksb + hh * a.ksh;
-  const T* V = static_cast<const T*>(a.v) + b * a.vsb + hh * a.vsh;
-
-  v8 qf[4];
-  {
-    const int qq = q < a.S ? q : a.S - 1;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      qf[s] = *reinterpret_cast<const v8*>(Q + (int64_t)qq * a.qss + 16 * s + 8 * hl);
-  }
-  int nkt = (a.S + kAKT - 1) / kAKT;
-  if (CAUSAL) {
-    const int last = (qb0 + 127 < a.S ? qb0 + 127 : a.S - 1) / kAKT + 1;
-    nkt = last < nkt ? last : nkt;
-  }
-  // tiles [0, nfull): every key < S and (causal) below every query of the workgroup
-  int nfull = a.S / kAKT;
-  if (CAUSAL) nfull = nfull < qb0 / kAKT ? nfull : qb0 / kAKT;
-  nfull = nfull < nkt ? nfull : nkt;
-
-  const int lrow = lane >> 3, pch = lane & 7;
-  uint32_t kof[2], vof[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wid * 2 + i) * 8 + lrow;
-    kof[i] = row_off<T>(row, a.kss, (swz_rows(row, pch) - row * kARow) >> 4);
-    vof[i] = row_off<T>(row, a.vss, (swz_tr(row, pch) - row * kARow) >> 4);
-  }
-  auto issue = [&](int kt) {  // 4 LDS-DMA instructions per lane
-    unsigned char* Kl = lds + (kt % 3) * TB;
-    unsigned char* Vl = Kl + kAKT * kARow;
-    if ((kt + 1) * kAKT <= a.S && !a.addr64) {
-      const T* kb = tile_base(K, kt * kAKT, a.kss);
-      const T* vb = tile_base(V, kt * kAKT, a.vss);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        glds16o(kb, kof[i], Kl + (wid * 2 + i) * 1024);
-        glds16o(vb, vof[i], Vl + (wid * 2 + i) * 1024);
-      }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (wid * 2 + i) * 8 + lrow;
-      const int key = kt * kAKT + row;
-      const int kk = key < a.S ? key : a.S - 1;
-      const int chk = (swz_rows(row, pch) - row * kARow) >> 4;
-      const int chv = (swz_tr(row, pch) - row * kARow) >> 4;
-      glds16(K + (int64_t)kk * a.kss + chk * 8, Kl + (wid * 2 + i) * 1024);
-      glds16(V + (int64_t)kk * a.vss + chv * 8, Vl + (wid * 2 + i) * 1024);
-    }
-  };
-  int koff[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) koff[t][s] = swz_rows(32 * t + c32, 2 * s + hl);
-  int vlo[2][2][2], vhi[2][2][2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r0 = 32 * t + 16 * s + 4 * hl;
-        const int c0 = 32 * dt + ((lane >> 4) & 1) * 16;
-        vlo[dt][t][s] = tr_addr(r0, c0, lane);
-        vhi[dt][t][s] = tr_addr(r0 + 8, c0, lane);
-      }
-  auto qk = [&](f32x16_t (&x)[2], int kt) {
-    const unsigned char* Kl = lds + (kt % 3) * TB;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) x[t][i] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) x[t] = mfma32<T>(lds_row8<T>(Kl, koff[t][s]), qf[s], x[t]);
-    }
-  };
-  // wait until tile kt+1 has landed (the only DMA in flight), then refill the slot
-  // tile kt-1 used (every wave is past its P.V after the barrier)
-  auto top = [&](int kt) {
-    if (kt + 1 < nkt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (kt + 2 < nkt) issue(kt + 2);
-    }
-  };
-
-  f32x16_t o[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) o[0][i] = o[1][i] = 0.f;
-  float m = -INFINITY, l = 0.f;
-
-  // softmax of x (tile at k0; masked or not) folded into (m, l, o), then O += P.V
-  auto finish = [&](f32x16_t (&x)[2], int kt, bool need_mask) {
-    const unsigned char* Vl = lds + (kt % 3) * TB + kAKT * kARow;
-    const int k0 = kt * kAKT;
-    if (need_mask) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= a.S || (CAUSAL && key > q)) x[t][r] = -INFINITY;
-        }
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, x[t][r]);
-    tmax = max_halves(tmax);
-    const float mnew = fmaxf(m, tmax * a.scale_log2);
-    float psum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(fmaf(x[t][r], a.scale_log2, -mnew));
-        psum += p;
-        x[t][r] = p;
-      }
-    const bool grow = __any(mnew != m);
-    const float alpha = grow ? fexp2(m - mnew) : 1.f;
-    m = mnew;
-    l = l * alpha + psum;
-    if (grow) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        o[0][i] *= alpha;
-        o[1][i] *= alpha;
-      }
-    }
-    if (DROP) {  // dropped P (the 1/(1-p) factor is applied to O once, at the store)
-      const uint32_t tb = dbase + (uint32_t)(k0 >> 2) * kDropK;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int rq = 0; rq < 4; ++rq) {
-          // key quad (k0 + 32t + 8rq + 4hl) >> 2 (keys + r & 3): a literal lattice step
-          const uint32_t hsh = drop_mix(tb + (uint32_t)(8 * t + 2 * rq) * kDropK);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            x[t][4 * rq + e] = drop_keep8(hsh, e, a.thr8) ? x[t][4 * rq + e] : 0.f;
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const v8 pf = acc_frag<T>(x[t], s);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          o[dt] = mfma32<T>(lds_tr8<T>(Vl, vlo[dt][t][s], vhi[dt][t][s]), pf, o[dt]);
-      }
-  };
-
-  issue(0);
-  if (1 < nkt) issue(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (2 < nkt) issue(2);
-  f32x16_t sc[2];
-  qk(sc, 0);
-  // invariant at the top of iteration kt: tiles <= kt+1 issued, sc = S of tile kt
-  int kt = 0;
-  for (; kt + 1 < nfull; ++kt) {  // pipelined: S(kt+1) beside softmax(kt)
-    if (kt > 0) top(kt);
-    f32x16_t sn[2];
-    qk(sn, kt + 1);
-    finish(sc, kt, false);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) sc[t] = sn[t];
-  }
-  if (kt < nfull) {  // last full tile: next tile's S only if one follows
-    if (kt > 0) top(kt);
-    if (kt + 1 < nkt) {
-      f32x16_t sn[2];
-      qk(sn, kt + 1);
-      finish(sc, kt, false);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) sc[t] = sn[t];
-    } else {
-      finish(sc, kt, false);
-    }
-    ++kt;
-  }
-  for (; kt < nkt; ++kt) {  // masked tail (boundary / causal diagonal)
-    if (kt > 0) top(kt);
-    const int k0 = kt * kAKT;
-    if (CAUSAL && k0 > qb0 + wid * 32 + 31) continue;  // whole tile masked for this wave
-    if (kt > nfull) qk(sc, kt);
-    const bool need_mask = (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
-    finish(sc, kt, need_mask);
-  }
-
-  const float lt = l + __shfl_xor(l, 32);
-  const float inv = lt > 0.f ? (DROP ? a.inv_keep : 1.f) / lt : 0.f;
-  if (q < a.S) {
-    store_dT<T>(static_cast<T*>(a.o) + (((int64_t)b * a.S + q) * a.H + hh) * kAD, o, hl, inv);
-    if (hl == 0) a.lse[(int64_t)bh * a.lse_stride + q] = m + log2f(lt);
-  }
-}
-
 // ---------------------------------------------------------------------------- backward
 struct AttnBwdArgs {
   const void* q;
@@ -716,8 +457,6 @@ struct AttnBwdArgs {
   uint32_t thr8;
   float inv_keep;
   uint32_t seed;
-  int base;  // APEX_AMD_ATTN_BASE=1: round-1 block order and eager rescale, A/B only
-  int addr64;  // APEX_AMD_ATTN_ADDR64=1: per-lane 64-bit tile DMA addresses (A/B only)
 };
 
 // dK / dV: a workgroup owns 128 keys (32 per wave, one per lane column), loops
@@ -739,7 +478,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
-  tile_of_block(CAUSAL, false, a.base, tile, bh);
+  tile_of_block(CAUSAL, false, tile, bh);
   const int b = bh / a.H, hh = bh - b * a.H;
   const int kb0 = tile * 128;
   const int kw0 = kb0 + wid * 32;
@@ -936,7 +675,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dkdv_k(AttnBwdArgs a) {
 // lse / D are scalars and dQ^T = K^T . dS^T consumes dS^T from the accumulator.
 // K sits in LDS as a row image (A of S^T) and a transposed image (A of dQ^T);
 // V as a row image (A of dP^T = V . dO^T).
-template <typename T, bool CAUSAL, bool DROP, bool IL = true>
+template <typename T, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   typedef typename Frag<T>::v8 v8;
   constexpr int IMG = kAKT * kARow;
@@ -945,7 +684,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform to the compiler
   const int hl = lane >> 5, c32 = lane & 31;
   int tile, bh;
-  tile_of_block(CAUSAL, true, a.base, tile, bh);
+  tile_of_block(CAUSAL, true, tile, bh);
   const int b = bh / a.H, hh = bh - b * a.H;
   const int qb0 = tile * 128;
   const int q = qb0 + wid * 32 + c32;
@@ -1002,7 +741,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
   // images per buffer: 0 = K rows, 1 = K transposed, 2 = V rows
   auto issue = [&](int kt, int buf) {
     unsigned char* base = lds + buf * 3 * IMG;
-    if ((kt + 1) * kAKT <= a.S && !a.addr64) {
+    if ((kt + 1) * kAKT <= a.S) {
       const T* kb = tile_base(K, kt * kAKT, a.kss);
       const T* vb = tile_base(V, kt * kAKT, a.vss);
 #pragma unroll
@@ -1109,7 +848,7 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
     // wave-uniform; unmasked tiles run as one straight-line block (half 0's dQ MFMAs
     // beside half 1's softmax VALU)
     const bool need_mask = (k0 + kAKT > a.S) || (CAUSAL && k0 + kAKT - 1 > qb0 + wid * 32);
-    if (IL && !need_mask) {
+    if (!need_mask) {
       dsoft(0, sc0, dp0);
       accum(0, sc0);
       dsoft(1, sc1, dp1);
@@ -1129,10 +868,13 @@ __global__ void __launch_bounds__(kAT, 2) attn_bwd_dq_k(AttnBwdArgs a) {
 }
 
 // host: the byte threshold of a dropout rate (round(256 p); p >= 255.5 / 256 drops all)
+// keep decisions compare one hash byte with round(256 p): the rate is quantised to 1/256
+// (ops/attention.py effective_dropout warns where that moves it by more than 2 %), and a
+// rate below 1/512 still drops (threshold 1), never silently turns dropout off
 static uint32_t drop_thr8(float p) {
   if (!(p > 0.f)) return 0u;
   const float t = p * 256.f + 0.5f;
-  return t >= 256.f ? 256u : (uint32_t)t;
+  return t >= 256.f ? 256u : (t < 1.f ? 1u : (uint32_t)t);
 }
 
 
@@ -1152,12 +894,9 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
   a.thr8 = drop_thr8(L.dropout);
   a.inv_keep = a.thr8 >= 256u ? 0.f : 256.f / (256.f - (float)a.thr8);
   a.seed = L.seed;
-  a.base = attn_base_flag();
-  a.addr64 = attn_addr64_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr8 != 0;
-  const bool v2 = !a.base && attn_fwd_variant() == 2;
-#define FWD1(T)                                                                                \
+#define ATTN_FWD_LAUNCH(T)                                                                                \
   if (L.causal) {                                                                              \
     if (drop) hipLaunchKernelGGL((attn_fwd_k<T, true, true>), grid, block, 0, st, a);          \
     else hipLaunchKernelGGL((attn_fwd_k<T, true, false>), grid, block, 0, st, a);              \
@@ -1165,25 +904,12 @@ void attn_fwd(const AttnLaunch& L, hipStream_t st) {
     if (drop) hipLaunchKernelGGL((attn_fwd_k<T, false, true>), grid, block, 0, st, a);         \
     else hipLaunchKernelGGL((attn_fwd_k<T, false, false>), grid, block, 0, st, a);             \
   }
-#define ATTN_FWD_LAUNCH(T)                                                                     \
-  if (v2) {                                                                                    \
-    if (L.causal) {                                                                            \
-      if (drop) hipLaunchKernelGGL((attn_fwd2_k<T, true, true>), grid, block, 0, st, a);       \
-      else hipLaunchKernelGGL((attn_fwd2_k<T, true, false>), grid, block, 0, st, a);           \
-    } else {                                                                                   \
-      if (drop) hipLaunchKernelGGL((attn_fwd2_k<T, false, true>), grid, block, 0, st, a);      \
-      else hipLaunchKernelGGL((attn_fwd2_k<T, false, false>), grid, block, 0, st, a);          \
-    }                                                                                          \
-  } else {                                                                                     \
-    FWD1(T)                                                                                    \
-  }
   if (L.dtype == DType::BF16) {
     ATTN_FWD_LAUNCH(bf16_t)
   } else {
     ATTN_FWD_LAUNCH(half_t)
   }
 #undef ATTN_FWD_LAUNCH
-#undef FWD1
 }
 
 void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
@@ -1205,14 +931,9 @@ void attn_bwd(const AttnBwdLaunch& L, hipStream_t st) {
   a.thr8 = drop_thr8(L.dropout);
   a.inv_keep = a.thr8 >= 256u ? 0.f : 256.f / (256.f - (float)a.thr8);
   a.seed = L.seed;
-  a.base = attn_base_flag();
-  a.addr64 = attn_addr64_flag();
   dim3 grid((L.S + 127) / 128, L.B * L.H), block(kAT);
   const bool drop = a.thr8 != 0;
-  const bool dq_il = attn_dq_interleave();
-#define DQ_LAUNCH(T, C, D)                                                                     \
-  if (dq_il) hipLaunchKernelGGL((attn_bwd_dq_k<T, C, D, true>), grid, block, 0, st, a);          \
-  else hipLaunchKernelGGL((attn_bwd_dq_k<T, C, D, false>), grid, block, 0, st, a)
+#define DQ_LAUNCH(T, C, D) hipLaunchKernelGGL((attn_bwd_dq_k<T, C, D>), grid, block, 0, st, a)
 #define ATTN_BWD_LAUNCH(T)                                                                     \
   if (L.causal) {                                                                              \
     if (drop) {                                                                                \

@@ -241,23 +241,6 @@ void bn_backward_elemt(const void* dy, const void* x, DType tx, const float* mea
                        int relu, const void* z, const uint8_t* relu_mask, void* dx, void* dz,
                        int64_t outer, int64_t C, int64_t inner, int channel_last, hipStream_t st);
 
-// One-launch local BatchNorm for channels-last bf16 activations that fit in the
-// register file (bn_persist.hip): forward = statistics + running stats + apply
-// (+ z) (+ ReLU, + mask); backward = reduce + dgamma/dbeta + dx (+ dz).  Return
-// false (nothing launched) when the shape / residency does not qualify.
-bool bn_persist_forward(const void* x, const void* w, const void* b, DType tw, const void* z,
-                        void* y, uint8_t* rmask, float* mean, float* invstd, float* running_mean,
-                        float* running_var, long long* nbt, float eps, float momentum, int64_t M,
-                        int64_t C, int relu, hipStream_t st);
-bool bn_persist_backward(const void* dy, const void* x, const float* mean, const float* invstd,
-                         const void* w, const void* b, DType tw, int relu, const void* z,
-                         const uint8_t* rmask, void* dx, void* dz, void* gw, void* gb, int64_t M,
-                         int64_t C, hipStream_t st);
-int bn_persist_error();
-void bn_persist_reset();
-void bn_persist_enable(int mode);  // 0 off, 1 on, 2 on without barrier fences
-int bn_persist_mode();
-long long bn_persist_launches();
 
 // ---- NHWC max pooling (pool.hip) -------------------------------------------
 // mean != nullptr: pool relu(x * invstd*w + (b - mean*invstd*w)) (BatchNorm + ReLU

@@ -226,11 +226,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bn.def("backward_local", &bn_backward_local_op, py::arg("dy"), py::arg("x"), py::arg("mean"),
          py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("z"), py::arg("relu"),
          py::arg("need_wgrad"), py::arg("want_dz"), py::arg("mask") = py::none());
-  bn.def("persist_error", &bn_persist_error_op);
-  bn.def("persist_reset", &bn_persist_reset_op);
-  bn.def("persist_enable", [](int mode) { bn_persist_enable(mode); });
-  bn.def("persist_mode", []() { return bn_persist_mode(); });
-  bn.def("persist_launches", []() { return bn_persist_launches(); });
 
   auto rd = m.def_submodule("reducer", "DDP bucketed gradient reducer core");
   register_reducer(rd);

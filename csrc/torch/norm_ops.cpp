@@ -403,31 +403,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_forward_local_op(
   x = conform(x, v);
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor mean = at::empty({v.C}, fopt), invstd = at::empty({v.C}, fopt);
-  if (v.cl == 1 && x.scalar_type() == at::kBFloat16 &&
-      (!has(weight) || weight->scalar_type() == at::kFloat) &&
-      (!has(bias) || bias->scalar_type() == at::kFloat) &&
-      (!has(z) || (z->scalar_type() == at::kBFloat16 && z->sizes() == x.sizes()))) {
-    // one persistent launch: statistics + running stats + apply (bn_persist.hip)
-    at::Tensor zc = has(z) ? conform(*z, v) : at::Tensor();
-    at::Tensor y = at::empty_like(x);
-    at::Tensor mask;
-    if (want_mask && relu_mask_ok(v, relu, x, zc, y))
-      mask = at::empty({v.outer, v.C / 8}, x.options().dtype(at::kByte));
-    at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
-    at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
-    if (bn_persist_forward(x.data_ptr(), w.defined() ? w.data_ptr() : nullptr,
-                           b.defined() ? b.data_ptr() : nullptr, DType::F32,
-                           zc.defined() ? zc.data_ptr() : nullptr, y.data_ptr(),
-                           mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
-                           mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                           rs ? running_mean->data_ptr<float>() : nullptr,
-                           rs ? running_var->data_ptr<float>() : nullptr,
-                           has(nbt) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>())
-                                    : nullptr,
-                           (float)eps, (float)momentum, v.outer, v.C, relu ? 1 : 0,
-                           cur_stream()))
-      return {y, mean, invstd, mask};
-  }
   at::Tensor ws = at::empty({bn_stats_workspace(v.outer, v.C, v.inner, v.cl)}, fopt);
   bn_local_train_stats(x.data_ptr(), dtype_of(x), v.outer, v.C, v.inner, v.cl,
                        mean.data_ptr<float>(), invstd.data_ptr<float>(),
@@ -643,37 +618,11 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
   return {dx, dz};
 }
 
-// Local (world 1) backward: one persistent launch (reduce + dgamma/dbeta + dx (+ dz),
-// bn_persist.hip) where the shape qualifies, else reduce_grad + backward_elemt.
+// Local (world 1) backward: reduce_grad + backward_elemt.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
     OptT z, bool relu, bool need_wgrad, bool want_dz, OptT mask) {
   BNView v = bn_view(x);
-  if (x.is_cuda() && v.cl == 1 && x.scalar_type() == at::kBFloat16 &&
-      dy.scalar_type() == at::kBFloat16 && (!has(weight) || weight->scalar_type() == at::kFloat) &&
-      (!has(bias) || bias->scalar_type() == at::kFloat)) {
-    at::Tensor xc = conform(x, v), dyc = conform(dy, v);
-    const uint8_t* mk = mask_ptr(mask, xc, v);
-    at::Tensor zc = (has(z) && !mk) ? conform(*z, v) : at::Tensor();
-    at::Tensor dx = at::empty_like(xc);
-    at::Tensor dz = want_dz ? at::empty_like(xc) : at::Tensor();
-    at::Tensor gw, gb;
-    if (need_wgrad && has(weight)) {
-      gw = at::empty_like(*weight);
-      gb = at::empty_like(*weight);
-    }
-    at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
-    at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
-    if ((!zc.defined() || zc.scalar_type() == at::kBFloat16) &&
-        bn_persist_backward(dyc.data_ptr(), xc.data_ptr(), mean.data_ptr<float>(),
-                            invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
-                            b.defined() ? b.data_ptr() : nullptr, DType::F32, relu ? 1 : 0,
-                            zc.defined() ? zc.data_ptr() : nullptr, mk, dx.data_ptr(),
-                            dz.defined() ? dz.data_ptr() : nullptr,
-                            gw.defined() ? gw.data_ptr() : nullptr,
-                            gb.defined() ? gb.data_ptr() : nullptr, v.outer, v.C, cur_stream()))
-      return {dx, dz, gw, gb};
-  }
   auto r = bn_reduce_grad_op(dy, x, mean, invstd, weight, bias, z, relu, need_wgrad, mask,
                              c10::nullopt);
   const double count = (double)(v.outer * v.inner);
@@ -682,8 +631,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
   return {std::get<0>(e), std::get<1>(e), std::get<2>(r), std::get<3>(r)};
 }
 
-int bn_persist_error_op() { return bn_persist_error(); }
-void bn_persist_reset_op() { bn_persist_reset(); }
 
 std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64_t count,
                                                           OptT shift, OptT running_mean,

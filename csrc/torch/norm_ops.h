@@ -74,8 +74,6 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
     OptT z, bool relu, bool need_wgrad, bool want_dz, OptT mask);
-int bn_persist_error_op();
-void bn_persist_reset_op();
 
 // BatchNorm statistics from a producer's tile-major stats slab [S][2][C]
 // (conv.conv_fwd_stats): local training mode -> (mean, invstd) with the running-stat

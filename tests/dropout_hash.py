@@ -33,7 +33,7 @@ def drop_mix(x):
 
 
 def thr8(p):
-    return 0 if p <= 0 else min(256, int(p * 256 + 0.5))
+    return 0 if p <= 0 else min(256, max(1, int(p * 256 + 0.5)))
 
 
 def hash_bytes(B, H, S, seed, SK=None):

@@ -184,3 +184,23 @@ def test_embedding_wgrad_cpu_reference_op():
     ref[7] = 0
     assert out.dtype == torch.bfloat16 and out.shape == (50, 16)
     torch.testing.assert_close(out.float(), ref.to(torch.bfloat16).float())
+
+
+def test_attention_effective_dropout_rate_cpu():
+    """the attention kernels quantise dropout to 1/256; tiny rates must
+    still drop (never silently 0) and a rate moved by more than 2 % warns once."""
+    import warnings
+
+    from apex_example_amd.ops import attention as A
+
+    assert A.effective_dropout(0.0) == 0.0
+    assert A.effective_dropout(0.1) == 26 / 256
+    assert A.effective_dropout(1e-4) == 1 / 256  # below 1/512: still drops
+    assert A.effective_dropout(1.0) == 1.0
+    A._WARNED.clear()
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        A._check_rate(0.1)          # 1.6 % off: silent
+        A._check_rate(0.01)         # 3/256 = 0.0117: warns
+        A._check_rate(0.01)         # once per rate
+    assert len(w) == 1 and "0.01" in str(w[0].message)
