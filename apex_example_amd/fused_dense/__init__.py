@@ -23,7 +23,6 @@ fall back to GEMM + the kernels above.
 from __future__ import annotations
 
 import collections
-import os
 import threading
 
 import torch
@@ -131,9 +130,8 @@ class cast_params_once:
 # <= 256) gives one batched GEMM with fp32 partials + the slab reduction kernel
 # writing the weight dtype: BERT-large (T = 16384) 101 -> 53 us for 1024 x 1024,
 # 163 -> 130 us for 3072 x 1024, 168 -> 150 us for 4096 x 1024; GPT-2 O1 (T = 8192,
-# fp32 dW) 57 -> 39 us / 91 -> 83 us, but slower at 64 tiles there.  APEX_AMD_DENSE_SPLITK=0
-# disables.
-_DENSE_SPLITK = os.environ.get("APEX_AMD_DENSE_SPLITK", "1") == "1"
+# fp32 dW) 57 -> 39 us / 91 -> 83 us, but slower at 64 tiles there.
+_DENSE_SPLITK = True
 
 
 def _splitk_chunks(T, o, i, in_dtype, out_dtype):
@@ -148,9 +146,9 @@ def _splitk_chunks(T, o, i, in_dtype, out_dtype):
 
 # O1 fp32 bucket-view weight gradients accumulate inside the GEMM (torch.addmm
 # out_dtype=fp32, beta = 1) instead of mm + add: GPT-2-medium with forced world-1
-# collectives 227.2 / 227.3 -> 229.5 / 229.2 k tok/s (same box).  APEX_AMD_ADDMM_F32=0
-# disables; cleared on the first failure.
-_ADDMM_F32 = os.environ.get("APEX_AMD_ADDMM_F32", "1") == "1"
+# collectives 227.2 / 227.3 -> 229.5 / 229.2 k tok/s (same box).  Cleared on the first
+# failure.
+_ADDMM_F32 = True
 
 
 # Dense weight gradients on the own transposed-operand MFMA kernel (csrc/hip/wgrad4w.hip):
@@ -158,9 +156,8 @@ _ADDMM_F32 = os.environ.get("APEX_AMD_ADDMM_F32", "1") == "1"
 # multiples of 256 and >= 48 output tiles of 256 x 256 (the FFN and QKV projections).
 # Same box (profiles/r5/wgrad_dense.md): BERT FFN 114.5 vs 136.8 us, QKV 103.5 vs 107.6 us,
 # GPT-2 FFN 69.7 vs 83.5 us against the hipBLASLt split-K path; the 1024 x 1024 attention
-# output projection (16 tiles) stays on hipBLASLt (57.8 vs 47.8 us).  APEX_AMD_DENSE_W4W=0
-# disables.
-_DENSE_W4W = os.environ.get("APEX_AMD_DENSE_W4W", "1") == "1"
+# output projection (16 tiles) stays on hipBLASLt (57.8 vs 47.8 us).
+_DENSE_W4W = True
 _W4W_MIN_TILES = 48
 
 
@@ -170,8 +167,8 @@ _W4W_MIN_TILES = 48
 # kernels (LayerNorm backward, attention, the data-gradient GEMMs) off every CU until a
 # tile finishes.  GPT-2-medium O1 (fp32 weight gradients on the side stream), same box:
 # 260.9 / 260.4 k tok/s with 256, 268.3 / 267.6 k with 128 (profiles/r5/ab_wg/).
-_W4W_MAX_WG = int(os.environ.get("APEX_AMD_W4W_MAXWG", "256"))
-_W4W_MAX_WG_SIDE = int(os.environ.get("APEX_AMD_W4W_MAXWG_SIDE", "128"))
+_W4W_MAX_WG = 256
+_W4W_MAX_WG_SIDE = 128
 
 
 def _w4w_splits(T, o, i, max_wg=None):
@@ -187,8 +184,8 @@ def _w4w_splits(T, o, i, max_wg=None):
 
 # The bias gradient of a wgrad4w layer from the kernel's own dY fragments (column sums via
 # v_dot2 next to the MFMAs, csrc/hip/wgrad4w.hip variant 4) instead of a separate
-# column-sum pass over dy.  APEX_AMD_W4W_BIAS=0 disables.
-_W4W_BIAS = os.environ.get("APEX_AMD_W4W_BIAS", "1") == "1"
+# column-sum pass over dy.
+_W4W_BIAS = True
 
 
 def _wgrad_w4w(dy2, x2, dtype, out, accumulate, side=False, b_dtype=None):
@@ -357,24 +354,14 @@ def _dense_fwd(ctx, x, weight, bias):
     return y.view(*x.shape[:-1], weight.size(0))
 
 
-# APEX_AMD_DENSE_SIDE: fp32 (default: fp32-weight layers only) | all | attn | ffn | none.
-# BERT-large O2 same box: fp32 (= none there) 664.5 / 666.5, attn 664.4 / 664.1,
-# ffn 645.4 / 644.7 seq/s - its bf16 weight-gradient GEMMs only contend with the
-# data-gradient chain.
-_DENSE_SIDE = os.environ.get("APEX_AMD_DENSE_SIDE", "fp32")
-
-
 def _side_dense(w_dtype, kind="attn"):
     """Dense weight gradients on the side stream (ops/conv.py _SideWgrad) only for fp32
     weights (amp O1: the fp32 weight-gradient GEMMs overlap the fp16 data-gradient
     chain): GPT-2-medium O1 239.5 / 239.9 k -> 246.5 / 249.0 k tok/s, while BERT-large
-    O2 (bf16 weights) measured 666.6 / 666.7 -> 648.7 / 648.7 seq/s (same box)."""
-    if _DENSE_SIDE in ("attn", "ffn"):
-        return kind == _DENSE_SIDE
-    if _DENSE_SIDE == "all":
-        return True
-    if _DENSE_SIDE == "none":
-        return False
+    O2 (bf16 weights) measured 666.6 / 666.7 -> 648.7 / 648.7 seq/s (same box); the
+    attention-only / FFN-only splits for BERT measured 664.4 and 645.4 seq/s against
+    664.5 (round 4) and 722-724 against 728 (round 5, profiles/r5/ab_bert_side_final/)."""
+    del kind
     return w_dtype == torch.float32
 
 
@@ -435,9 +422,9 @@ class FusedDenseSkipFunc(torch.autograd.Function):
         return _dense_bwd(ctx, dy, dskip)
 
 
-# hipBLASLt GELU epilogues (csrc/torch/lt_ops.cpp) for the tanh-GELU FFN; set
-# APEX_AMD_LT_GELU=0 to run GEMM + separate GELU / column-sum kernels instead
-_LT_GELU = os.environ.get("APEX_AMD_LT_GELU", "1") == "1"
+# hipBLASLt GELU epilogues (csrc/torch/lt_ops.cpp) for the tanh-GELU FFN where the own
+# gemm4w epilogues do not apply (tests turn it off to compare with the unfused kernels)
+_LT_GELU = True
 
 
 def _lt_ok(*ts):
@@ -468,7 +455,7 @@ def _lt_call(name, *args):
 # BGRADB kernels for gfx950 are far slower than its plain GEMMs - BERT-large
 # 592 -> 421 seq/s when enabled (same box) - so the plain GEMM + the column-sum
 # kernel stay the default
-_LT_BGRAD = os.environ.get("APEX_AMD_LT_BGRAD", "0") == "1"
+_LT_BGRAD = False
 
 
 def _wgrad_bgrad(dy2, x2, w_dtype, b_dtype, out=None, accumulate=True, side=False):
@@ -506,7 +493,7 @@ def _g4w_ok(a, b, *more):
     return _native.require().dense.gemm4w_ok(a, b)
 
 
-_T_KERNEL = os.environ.get("APEX_AMD_DENSE_T_KERNEL", "1") == "1"  # 0: ATen copy (A/B)
+_T_KERNEL = True
 
 
 def _transposed(w):

@@ -8,7 +8,6 @@ either works).  CPU tensors run the C++ CPU path of the same extension.
 from __future__ import annotations
 
 import numbers
-import os
 
 import torch
 from torch.nn import init
@@ -16,7 +15,6 @@ from torch.nn.parameter import Parameter
 
 from .. import _native
 from ..ops import _bias_handoff
-from ..ops.conv import gate_side_stream
 
 
 def _n2(normalized_shape):
@@ -46,7 +44,6 @@ class FusedLayerNormAffineFunction(torch.autograd.Function):
         grad_input, grad_weight, grad_bias = C.backward(
             grad_output.contiguous(), input_, mean, invvar, _n2(ctx.normalized_shape), weight_,
             ctx.needs_input_grad[1], ctx.needs_input_grad[2], False)
-        gate_side_stream(grad_input)
         return grad_input, grad_weight, grad_bias, None, None
 
 
@@ -136,11 +133,10 @@ class AddDropoutLayerNormFunction(torch.autograd.Function):
                                                      bool(want_hs))
         if want_hs:
             _bias_handoff.offer(dh, dhs)
-        gate_side_stream(ds)
         return ds, dh, dw, db, None, None, None, None
 
 
-_FUSED_ADD_LN = os.environ.get("APEX_AMD_FUSED_ADD_LN", "1") == "1"
+_FUSED_ADD_LN = True  # (tests turn it off to compare with the unfused sublayer join)
 
 
 def _fused_add_ok(x, h, ln):

@@ -219,23 +219,9 @@ def bn_src_of(x):
     return getattr(x, "_amd_bn_src", None)
 
 
-_TUNED = False
-
-
 def _C():
-    global _TUNED
-    C = _native.require().bn
-    if not _TUNED:
-        _TUNED = True
-        # APEX_AMD_BN_TUNING="red_rpt,red_cap,red_min,elem_rpt,elem_cap,elem_min" (-1 = keep):
-        # grid-sizing knobs of the NHWC kernels, for tuning runs (tools/microbench.py bn-tune)
-        import os
-        spec = os.environ.get("APEX_AMD_BN_TUNING")
-        if spec:
-            v = [int(t) for t in spec.split(",")]
-            keys = ("red_rpt", "red_cap", "red_min", "elem_rpt", "elem_cap", "elem_min")
-            C.set_tuning(**dict(zip(keys, v)))
-    return C
+    # (grid sizing of the NHWC kernels: bn.set_tuning, used by tools/microbench.py bn-tune)
+    return _native.require().bn
 
 
 def _to_logical(x, shape_channel_last):

@@ -29,7 +29,8 @@ from .. import _native
 from . import _ddp_direct
 from .batch_norm import bn_src_of
 
-# Weight gradients on a side stream (APEX_AMD_WGRAD_STREAM=0 disables): the data
+# Weight gradients on a side stream (APEX_AMD_WGRAD_STREAM=0 disables; a documented
+# debugging switch, docs/KNOBS.md): the data
 # gradient stays on the critical path of the main stream while the weight gradient
 # (MFMA-bound) runs beside it and beside the following BatchNorm backward passes
 # (HBM-bound); the main stream joins the side stream once, at the end of the
@@ -82,39 +83,15 @@ def _side_mode(params):
 # 10,418 / 10,417 with the high-priority one (tail 0.14 ms) - 98.6 % of the plain step
 # (profiles/r4/).
 _DDP_SIDE = os.environ.get("APEX_AMD_WGRAD_STREAM_DDP", "1") == "1"
-# Bounded side-stream lag: the main stream waits for the weight gradient enqueued
-# APEX_AMD_WGRAD_LAG launches earlier (0 = unbounded; default 4 under DDP, where the last
-# buckets cannot launch before the side stream reaches their gradients), and
-# APEX_AMD_WGRAD_STREAM_PRIO=high creates the side stream with high priority (its weight
-# gradients then run ahead of the data-gradient chain instead of trailing it).
-_LAG = int(os.environ.get("APEX_AMD_WGRAD_LAG", "-1"))
-# priority of the side stream: "auto" = high under DDP, normal for the single-GPU 'free'
-# mode (same box: 10,565 / 10,534 img/s normal vs 10,531 / 10,500 high there)
-_SIDE_PRIO = os.environ.get("APEX_AMD_WGRAD_STREAM_PRIO", "auto")
-# CU partitioning for the side stream (APEX_AMD_WGRAD_STREAM_CUS = 1 | 2 | 3 quarters of the
-# CUs, 0 = all): the weight-gradient GEMMs then run on that share of every XCD instead of
-# competing with the data-gradient chain for every CU (csrc/torch/module.cpp
-# cu_masked_stream; a CU-masked stream has the default priority).  Measured far slower, so
-# off: same box, two runs each, GPT-2-medium 247.3 / 247.8 k tok/s with the plain side
-# stream vs 129 k (1/4 of the CUs), 154 k (1/2), 154 k (3/4); ResNet-50 10,566 / 10,511
-# vs 7,181 / 7,165 img/s (1/2 and 3/4) - the masked queue costs far more than the CU
-# contention it removes (profiles/r4/m/).
-_SIDE_CUS = int(os.environ.get("APEX_AMD_WGRAD_STREAM_CUS", "0"))
+# Bounded side-stream lag under DDP: the main stream waits for the weight gradient
+# enqueued 4 launches earlier (the last buckets cannot launch before the side stream
+# reaches their gradients); unbounded in the single-GPU 'free' mode.  The side stream has
+# high priority under DDP, normal priority in the 'free' mode (same box: 10,565 / 10,534
+# img/s normal vs 10,531 / 10,500 high there).  Measured and removed in round 6: a
+# CU-masked side stream (1/4-3/4 of every XCD: GPT-2 247 -> 129-154 k tok/s, ResNet-50
+# 10,566 -> 7,181 img/s, profiles/r4/m/) and gating the side stream behind the LayerNorm
+# backward passes (neutral on GPT-2, profiles/r5/ab_wg/).
 _SIDE_EVENTS = {}   # device index -> deque of side-stream events, oldest first
-# Gate the side stream behind the compute stream's LayerNorm backward passes
-# (APEX_AMD_WGRAD_GATE_LN=1): a LayerNorm backward records an event on the compute stream
-# (gate_side_stream) and the next side-stream weight gradient waits for it, so a
-# memory-bound LN backward is not shared with a freshly started weight-gradient GEMM
-# (GPT-2-medium's fp32 ln_bwd_fast ran 85 us per call beside them vs ~34 us alone).
-_GATE_LN = os.environ.get("APEX_AMD_WGRAD_GATE_LN", "0") == "1"
-_GATE = {}  # device index -> compute-stream event the next side-stream launch waits for
-
-
-def gate_side_stream(t):
-    """Called by the LayerNorm backward functions after their kernel is enqueued on the
-    current (compute) stream: the next side-stream weight gradient starts behind it."""
-    if _GATE_LN and t.is_cuda and _SIDE and not torch.cuda.is_current_stream_capturing():
-        _GATE[t.device.index] = torch.cuda.current_stream(t.device).record_event()
 
 
 # test hook (tests/test_ddp_gpu.py race test): GPU cycles the side stream sleeps before
@@ -135,8 +112,6 @@ def _join_side():
 
 
 def _lag_for(mode):
-    if _LAG >= 0:
-        return _LAG
     return 4 if mode == "ddp" else 0
 
 
@@ -158,16 +133,12 @@ class _SideWgrad:
         if self.on:
             dev = weight.device
             self.main = torch.cuda.current_stream(dev)
-            high = _SIDE_PRIO == "high" or (_SIDE_PRIO == "auto" and self.mode == "ddp")
+            high = self.mode == "ddp"
             key = (dev.index, high)
             self.side = _SIDE.get(key)
             if self.side is None:
-                if 0 < _SIDE_CUS < 4:
-                    h = _native.require().cu_masked_stream(dev.index, _SIDE_CUS)
-                    self.side = torch.cuda.ExternalStream(h, device=dev)
-                else:
-                    prio = torch.cuda.Stream.priority_range()[1] if high else 0
-                    self.side = torch.cuda.Stream(dev, priority=prio)
+                prio = torch.cuda.Stream.priority_range()[1] if high else 0
+                self.side = torch.cuda.Stream(dev, priority=prio)
                 _SIDE[key] = self.side
             self.ev = self.main.record_event()
 
@@ -175,9 +146,6 @@ class _SideWgrad:
         if not self.on:
             return fn()
         self.side.wait_event(self.ev)
-        gate = _GATE.pop(self.main.device.index, None) if _GATE else None
-        if gate is not None:
-            self.side.wait_event(gate)
         with torch.cuda.stream(self.side):
             if _TEST_SIDE_SLEEP:
                 torch.cuda._sleep(_TEST_SIDE_SLEEP)
@@ -279,7 +247,7 @@ def _wgrad_1x1_w(dy, x, weight, out=None, accumulate=True):
 
 # maximum row splits of the 1x1 weight gradients (A/B knob: the split-K GEMMs run on the
 # weight-gradient side stream, where a smaller grid leaves more CUs to the main stream)
-_SPLITK_MAX = int(os.environ.get("APEX_AMD_WGRAD1X1_MAXS", "128"))
+_SPLITK_MAX = 128
 
 
 def _split_k(m):
@@ -324,9 +292,9 @@ def wgrad_1x1(dy_rows, x_rows, out_dtype, out=None, accumulate=True):
 # reducing ResNet-50 shapes 256->64 @ 56x56 (97 vs 156 us) and 512->128 @ 28x28
 # (50 vs 61 us), and 512->2048 @ 7x7 (46 vs 53 us).  A data gradient is the same
 # 1x1 conv of dY with the transposed weight, so conv3's dgrads (256->64, 512->128)
-# take it too.  (cin, cout) -> minimum rows M = N*H*W; APEX_AMD_OWN1X1=0 disables.
+# take it too.  (cin, cout) -> minimum rows M = N*H*W.
 _OWN1X1 = {(256, 64): 200_000, (512, 128): 100_000, (512, 2048): 0}
-_USE_OWN1X1 = os.environ.get("APEX_AMD_OWN1X1", "1") == "1"
+_USE_OWN1X1 = True
 
 
 def _own_1x1(x_rows_dtype, cin, cout, m):
@@ -447,11 +415,11 @@ def _tag_stats(y):
 # previous block's bn3) it replaces the hipBLASLt addmm + reduce pass + dz store and wins
 # 10-260 us per layer; without one (bn1 / bn2) the extra read of the BN input in the
 # epilogue costs more than the reduce pass it saves except on small layers (7x7: M =
-# 12544), so those fuse only below APEX_AMD_CONV_BN_BWD_MAXM output pixels.  Round 4
+# 12544), so those fuse only below 65,536 output pixels.  Round 4
 # (32-deep K ring): 65536 takes the 14x14 layers (M = 50176) in too - ResNet-50 same box,
 # two runs each: 10,582 / 10,576 img/s at 16384, 10,595 / 10,633 with the 14x14 layers,
 # 10,613 / 10,549 with every layer (profiles/r4/i/).
-_BNBWD_MAX_M = int(os.environ.get("APEX_AMD_CONV_BN_BWD_MAXM", "65536"))
+_BNBWD_MAX_M = 65536
 
 
 def _bnbwd_ok(dy, weight, src, xshape, has_add=False):
@@ -616,8 +584,8 @@ class Conv1x1Stride2Function(torch.autograd.Function):
 # writes all of them) and conv1's data gradient reads it back as the residual term.  One
 # Function for both convs keeps that gradient COMPACT - the plain 1x1 GEMM dY_d W_d on the
 # strided pixels - and conv1's dgrad epilogue adds it onto the even pixels only
-# (ConvBnEpi.add_s2).  APEX_AMD_CONV_PAIR_S2=0 keeps the two Functions.
-_PAIR_S2 = os.environ.get("APEX_AMD_CONV_PAIR_S2", "1") == "1"
+# (ConvBnEpi.add_s2).
+_PAIR_S2 = True
 PAIR_S2_CALLS = [0]  # backward passes that took the compact path (tests)
 
 
@@ -754,11 +722,11 @@ class Conv2d1x1(nn.Conv2d):
 
 # 3x3 weight gradient: "tap" = per-tap MFMA kernel (default), "nine" = the all-taps
 # strip kernel (W <= 56), "miopen" = MIOpen's convolution_backward
-_WGRAD3 = os.environ.get("APEX_AMD_WGRAD3", "tap")
+_WGRAD3 = "tap"
 # 64 -> 64 channel 3x3 stride-1 weight gradients (ResNet layer 1) on the strip-ring kernel
-# (csrc/hip/conv_igemm.hip conv3x3_wgrad_c64_k, algo 4); APEX_AMD_WGRAD64=0 keeps the
-# per-tap kernel
-_WGRAD64 = os.environ.get("APEX_AMD_WGRAD64", "1") == "1"
+# (csrc/hip/conv_igemm.hip conv3x3_wgrad_c64_k, algo 4; 93.8 us / 631 TF vs 175 us for
+# the per-tap kernel, docs/PERF.md round 4)
+_WGRAD64 = True
 
 
 def _wgrad3_algo(x, weight, stride):
@@ -767,9 +735,9 @@ def _wgrad3_algo(x, weight, stride):
             and x.size(3) <= 56):
         return 4
     return 0
-# A/B switches for the reduction / rotation kernels (tools, docs/PERF.md)
-_USE_SPLITK_REDUCE = os.environ.get("APEX_AMD_SPLITK_REDUCE", "1") == "1"
-_USE_ROT_KERNEL = os.environ.get("APEX_AMD_ROT_KERNEL", "1") == "1"
+# the own reduction / rotation kernels (tests turn them off to compare with ATen)
+_USE_SPLITK_REDUCE = True
+_USE_ROT_KERNEL = True
 
 
 def _rot_weight(weight):
@@ -788,8 +756,8 @@ def _rot_weight(weight):
 # (conv.prep_weights) instead of one ~10 us launch per filter (27 per ResNet-50 step).
 # Forward registers the filter; the first backward request prepares every registered
 # filter; the next forward of a filter drops its prepared copy (the optimizer may
-# have rewritten the weights in place since).  APEX_AMD_PREP_WEIGHTS=0 disables.
-_USE_PREP = os.environ.get("APEX_AMD_PREP_WEIGHTS", "1") == "1"
+# have rewritten the weights in place since).
+_USE_PREP = True
 _PREP_PENDING = {}   # id(weight) -> weight
 _PREP_READY = {}     # id(weight) -> (weight, prepared layout)
 

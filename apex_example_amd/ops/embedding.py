@@ -15,12 +15,11 @@ a wave per sorted position; the wave that starts a run of equal ids sums that ru
 output-gradient rows in sorted order (fp32) and writes the weight row in the weight
 dtype.  The grid is sized by the token count (known on the host), so nothing is
 read back, and the fixed summation order makes it bitwise reproducible (the float-
-atomic ``index_add_`` scatter of round 2 was not; ``APEX_AMD_EMB_BWD=atomic`` keeps
-it for A/B runs, ``=stock`` the PyTorch op).  Forward is the regular gather.
+atomic ``index_add_`` scatter of round 2 was not; it stays selectable as ``_MODE =
+"atomic"``, ``"stock"`` is the PyTorch op).  Forward is the regular gather.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -28,9 +27,9 @@ import torch.nn.functional as F
 
 from .. import _native
 
-# APEX_AMD_EMB_BWD = det (default) | atomic | stock   (APEX_AMD_SYNCFREE_EMB=0 = stock)
-_MODE = os.environ.get("APEX_AMD_EMB_BWD", "det")
-_ENABLED = os.environ.get("APEX_AMD_SYNCFREE_EMB", "1") == "1" and _MODE != "stock"
+# backward: "det" (default) | "atomic" | "stock"
+_MODE = "det"
+_ENABLED = _MODE != "stock"
 
 
 # dtypes the deterministic kernel reads / writes (anything else: the scatter below)

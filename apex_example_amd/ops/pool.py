@@ -7,7 +7,6 @@ element written once), replacing ATen's NHWC max_pool2d kernels, which cost
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -16,8 +15,8 @@ import torch.nn.functional as F
 from .. import _native
 
 # A/B switch for the fused stem (tools, docs/PERF.md)
-_FUSE_STEM = os.environ.get("APEX_AMD_FUSE_STEM", "1") == "1"
-_GAP_KERNEL = os.environ.get("APEX_AMD_GAP_OFF", "0") != "1"
+_FUSE_STEM = True
+_GAP_KERNEL = True
 
 
 class MaxPool2dNHWCFunction(torch.autograd.Function):

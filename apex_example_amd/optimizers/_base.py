@@ -19,7 +19,6 @@ from __future__ import annotations
 import functools
 import itertools
 import operator
-import os
 from collections import OrderedDict
 
 import torch
@@ -28,9 +27,9 @@ from .. import _native
 
 
 _GRAD = operator.attrgetter("grad")
-# native StepPlan launches from the second step on (APEX_AMD_STEP_PLAN=0: the per-step
-# Python launch path, for A/B runs)
-_STEP_PLAN = os.environ.get("APEX_AMD_STEP_PLAN", "1") == "1"
+# native StepPlan launches from the second step on (tests turn it off to compare with the
+# per-step Python launch path)
+_STEP_PLAN = True
 
 
 class FusedOptimizerBase(torch.optim.Optimizer):

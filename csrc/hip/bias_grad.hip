@@ -115,31 +115,9 @@ __global__ void __launch_bounds__(kCsThreads)
   }
 }
 
-// stage 2: 64 columns x 4 split lanes per block, each lane summing S/4 partials
-// with 4 independent loads in flight
-template <typename TO>
-__global__ void __launch_bounds__(256)
-    colsum_final_k(const float* __restrict__ part, int S, int N, TO* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float t[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < N) {
-    int s = sl;
-    for (; s + 12 < S; s += 16) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t[i] += part[(int64_t)(s + 4 * i) * N + c];
-    }
-    for (; s < S; s += 4) t[0] += part[(int64_t)s * N + c];
-  }
-  red[sl][cl] = (t[0] + t[1]) + (t[2] + t[3]);
-  __syncthreads();
-  if (sl == 0 && c < N) out[c] = from_f32<TO>((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]));
-}
-
-// stage 2, narrow: 16 columns x 16 split lanes per block, each lane summing S/16
-// partials with 4 loads in flight - 4x the blocks of colsum_final_k and a quarter of
-// its dependent load rounds (the wide form ran 6-11 us per call in the BERT / GPT-2
+// stage 2: 16 columns x 16 split lanes per block, each lane summing S/16 partials with
+// 4 loads in flight - 4x the blocks of a 64-column form and a quarter of its dependent
+// load rounds (that form, removed in round 6, ran 6-11 us per call in the BERT / GPT-2
 // steps for ~0.5 MB of partials: 16 blocks of latency chains).  Same summation
 // order across the partials of one split lane, so deterministic
 template <typename TO>
@@ -167,23 +145,10 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// APEX_AMD_COLSUM_FINAL=64: the wide stage 2 (A/B)
-bool colsum_final_wide() {
-  static const bool wide = [] {
-    const char* e = std::getenv("APEX_AMD_COLSUM_FINAL");
-    return e && e[0] == '6';
-  }();
-  return wide;
-}
-
 template <typename TO>
 void launch_final(const float* part, int S, int N, TO* out, hipStream_t st) {
-  if (colsum_final_wide())
-    hipLaunchKernelGGL(colsum_final_k<TO>, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, part,
-                       S, N, out);
-  else
-    hipLaunchKernelGGL(colsum_final16_k<TO>, dim3((unsigned)((N + 15) / 16)), dim3(256), 0, st,
-                       part, S, N, out);
+  hipLaunchKernelGGL(colsum_final16_k<TO>, dim3((unsigned)((N + 15) / 16)), dim3(256), 0, st,
+                     part, S, N, out);
 }
 
 __device__ __forceinline__ float gelu_f(float x, bool tanh_approx) {

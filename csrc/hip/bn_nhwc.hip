@@ -52,27 +52,9 @@ BNTuning& bn_tuning() {
   return t;
 }
 
-namespace {
-// rows in flight per lane of the read-only reductions; APEX_AMD_BN_U="stats,reduce"
-// (A/B switch for tools/microbench.py bn-u, read per launch)
-struct BNUnroll {
-  int stats = 4, reduce = 2, elem = 2;
-};
-BNUnroll bn_unroll() {
-  BNUnroll u;
-  // rows in flight per lane of the elementwise passes (apply_k, backward_k):
-  // APEX_AMD_BN_EU=2|4 (A/B switch for tools/microbench.py bn-eu)
-  if (const char* e = std::getenv("APEX_AMD_BN_EU")) u.elem = std::atoi(e) == 4 ? 4 : 2;
-  if (const char* e = std::getenv("APEX_AMD_BN_U")) {
-    int a = 0, b = 0;
-    if (std::sscanf(e, "%d,%d", &a, &b) == 2) {
-      u.stats = a;
-      u.reduce = b;
-    }
-  }
-  return u;
-}
-}  // namespace
+// rows in flight per lane: 4 in stats_k, 2 in reduce_k and in the elementwise passes
+// (apply_k, backward_k).  Same-box A/Bs (profiles/r4/ze/, microbench_bn_eu.txt): "4,4" /
+// "8,4" reduction unrolls -2.2 / -2.3 %, 4 elementwise rows in flight -3.4 %.
 
 namespace {
 
@@ -98,14 +80,10 @@ int reduce_splits(int64_t M, const NGeom& g) {
 // 4 % R50-weighted in isolation but measured 0.25 % SLOWER in the training step
 // (same-box A/B, 9662 vs 9687 img/s: the isolated loop re-reads a cache-warm tensor),
 // so the fixed elem_rpt (8 since the constants moved to LDS, bn_common.h) stays the
-// default; APEX_AMD_BN_ELEM_AUTO=1 or bn_set_tuning(elem_rpt=0) selects the rule.
+// default; bn_set_tuning(elem_rpt=0) selects the rule.
 int elem_rpt_for(int64_t M, const NGeom& g, int64_t bytes) {
   const BNTuning& t = bn_tuning();
-  static const bool env_auto = [] {
-    const char* e = std::getenv("APEX_AMD_BN_ELEM_AUTO");
-    return e && e[0] == '1';
-  }();
-  if (!(t.elem_auto || env_auto)) return t.elem_rpt;
+  if (!t.elem_auto) return t.elem_rpt;
   if (bytes > (int64_t)256 << 20) return 8;
   for (int r = 32; r > 8; r >>= 1) {
     const int64_t blocks = (M + (int64_t)g.rows_iter * r - 1) / ((int64_t)g.rows_iter * r) * g.cblocks;
@@ -608,12 +586,8 @@ void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut&
     const T* xp = static_cast<const T*>(x);
     vec_dispatch(vec, [&](auto V) {
       constexpr bool VV = decltype(V)::value;
-      if (bn_unroll().stats == 8)
-        hipLaunchKernelGGL((stats_k<T, VV, 8>), dim3(splits, g.cblocks), dim3(kBNThreads), 0, st,
-                           xp, M, (int)C, g.ctile, g.rows_iter, ws);
-      else
-        hipLaunchKernelGGL((stats_k<T, VV, 4>), dim3(splits, g.cblocks), dim3(kBNThreads), 0, st,
-                           xp, M, (int)C, g.ctile, g.rows_iter, ws);
+      hipLaunchKernelGGL((stats_k<T, VV, 4>), dim3(splits, g.cblocks), dim3(kBNThreads), 0, st,
+                         xp, M, (int)C, g.ctile, g.rows_iter, ws);
     });
     launch_stats_finalize<T>(xp, ws, splits, C, M, (int64_t)1, out, st);
   });
@@ -642,8 +616,7 @@ void nhwc_apply(const void* x, DType tx, const float* mean, const float* invstd,
           if (z) launch(std::true_type{});
           else launch(std::false_type{});
         };
-        if (bn_unroll().elem == 4) go(std::integral_constant<int, 4>{});
-        else go(std::integral_constant<int, 2>{});
+        go(std::integral_constant<int, 2>{});
       });
     });
   });
@@ -677,8 +650,7 @@ void nhwc_reduce(const void* dy, const void* x, DType tx, const float* mean, con
           else if (rm == 2) launch(std::integral_constant<int, 2>{});
           else launch(std::integral_constant<int, 3>{});
         };
-        if (bn_unroll().reduce == 4) go(std::integral_constant<int, 4>{});
-        else go(std::integral_constant<int, 2>{});
+        go(std::integral_constant<int, 2>{});
       });
       launch_reduce_finalize<TW>(ws, splits, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
                          static_cast<TW*>(gb), st, sum_scale);
@@ -715,8 +687,7 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
           else if (rm == 2) launch(std::integral_constant<int, 2>{});
           else launch(std::integral_constant<int, 3>{});
         };
-        if (bn_unroll().elem == 4) go(std::integral_constant<int, 4>{});
-        else go(std::integral_constant<int, 2>{});
+        go(std::integral_constant<int, 2>{});
       });
     });
   });

@@ -34,9 +34,6 @@ namespace {
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kCT = 256;  // threads
-#ifndef CONV_INTERLEAVE
-#define CONV_INTERLEAVE 1
-#endif
 constexpr int kBM = 128;
 constexpr int kBK = 64;
 constexpr int kRowBytes = kBK * 2;  // 128
@@ -141,8 +138,6 @@ __device__ __forceinline__ void conv_tap(int z, int t, int& dh, int& dw, int& wt
 // B rows ([NC][taps][KC]) are kb_stride elements long
 struct ConvGeom {
   int GH, GW, AH, AW, as, YH, YW, ys, KC, NC, M, kb_stride;
-  int burst;  // 1: the 4-wave ring issues each tile's DMA as one burst (A/B reference)
-  int lpt;    // stride-2 dgrad parity classes heaviest first (APEX_AMD_DGRAD_LPT, default 1)
 };
 
 // BN-backward epilogue (conv_tap_k EPI == 1, ConvBnEpi).  Each thread owns one 8-channel
@@ -214,7 +209,7 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
   const bf16_t* addp = static_cast<const bf16_t*>(ep.add);
   const bf16_t* xp = static_cast<const bf16_t*>(ep.xbn);
   const bf16_t* zb = reinterpret_cast<const bf16_t*>(g_zero16);
-  const bool x_on = !(ep.diag & 1), s2 = ep.add_s2 && addp;
+  const bool x_on = true, s2 = ep.add_s2 && addp;
 #pragma unroll
   for (int q = 0; q < PT::ROWS; ++q) {
     const int m = m0 + q * PT::RGS + rg;
@@ -326,15 +321,11 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
 // the LDS goes to more resident workgroups instead (3 per CU: one's loads overlap
 // another's MFMAs and stores; 4 would cap the registers at 128 and spill the epilogue
 // statistics).
-// CT = 512 (8 waves, one workgroup per CU): the 256 x 128 tile on a 3-deep ring (144 KB of
-// LDS), 64 x 64 per wave - two waves per SIMD like the 2-workgroup 128 x 128 form, but two
-// tiles' DMAs stay in flight across every barrier instead of one.
-// BK = 32: 64-byte K-tile rows - half the LDS per ring stage, so a 4-deep ring fits two
-// workgroups per CU with three stages (48 KB) in flight instead of one 32 KB tile.
+// BK = 32: 64-byte K-tile rows - half the LDS per ring stage, so a 3-deep ring keeps two
+// stages (32 KB at 128 x 128) in flight with up to 3 workgroups per CU.
 template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0, int CT = kCT,
           int BK = kBK>
-__global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
-                                       NB * (BM + BN) * BK * 2 > 80 * 1024)
+__global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
                                           ? 1 : (NB == 1 && EPI == 0 ? 3 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
                bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
@@ -366,8 +357,7 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   // dispatched slowest, so the 4-tap class (z = 3) goes out first and the 1-tap class
   // fills the tail (ResNet-50 shapes 118 -> 107, 103 -> 90, 93 -> 82 us,
   // tools/dgrad_s2_bench.py; the 1x1 form's only real class, z = 0, is already first)
-  const int z = MODE == kDgrad3 && g.lpt ? (int)gridDim.z - 1 - (int)blockIdx.z
-                                         : (int)blockIdx.z;
+  const int z = MODE == kDgrad3 ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
   const int ntaps = conv_ntaps<MODE>(z);
   const int KC = g.KC, M = g.M, GHW = g.GH * g.GW;
 
@@ -456,210 +446,7 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   // LDS tile write instead of being waited for at a __syncthreads()
   BnPre<BM, BN, CT> pre;
 
-  // the halo's zero source, pinned in VGPRs: re-materialised inside the loop it is a
-  // GOT load (SMEM), whose lgkmcnt(0) wait would also wait for the fragment reads
-  const void* zsrc = (const void*)g_zero16;
-  asm volatile("" : "+v"(zsrc));
-  // a tile's DMA geometry, computed once per tile (scalar): buffer, A offset, tap, B offset
-  struct TileSrc {
-    unsigned char* A;
-    int64_t aoff;
-    int tap, boff;
-  };
-  auto tile_src = [&](int kt_) {
-    TileSrc t;
-    t.tap = kt_ / kc_per_tap;
-    const int c0_ = (kt_ - t.tap * kc_per_tap) * BK;
-    int dh_, dw_, wt_;
-    conv_tap<MODE>(z, t.tap, dh_, dw_, wt_);
-    t.A = lds + (kt_ % NB) * BUF;
-    t.aoff = (int64_t)(dh_ * g.AW + dw_) * KC + c0_;
-    t.boff = wt_ * KC + c0_;
-    return t;
-  };
-  auto piece = [&](const TileSrc& t, int q) {
-    if (q < AI) {
-      const bool ok = (amask[q] >> t.tap) & 1u;
-      const void* src = (const void*)(abase[q] + t.aoff);
-      glds16(ok ? src : zsrc, t.A + (wid * (BM / NW) + q * RPI) * RB);
-    } else {
-      const int qb = q - AI;
-      glds16(bbase[qb] + t.boff, t.A + A_BYTES + (wid * (BN / NW) + qb * RPI) * RB);
-    }
-  };
-  bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
-  auto rd_a = [&](int kt_, int ks, bf16x8 (&af)[FM]) {
-    const unsigned char* A = lds + (kt_ % NB) * BUF;
-    const int ch = ks * 4 + fg;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, ch));
-  };
-  auto rd_b = [&](int kt_, int ks, bf16x8 (&bfr)[FN]) {
-    const unsigned char* B = lds + (kt_ % NB) * BUF + A_BYTES;
-    const int ch = ks * 4 + fg;
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swzr<RB>(wn * TN + j * 16 + fr, ch));
-  };
-  auto rd = [&](int kt_, int ks, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
-    const unsigned char* A = lds + (kt_ % NB) * BUF;
-    const unsigned char* B = A + A_BYTES;
-    const int ch = ks * 4 + fg;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, ch));
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(B + swzr<RB>(wn * TN + j * 16 + fr, ch));
-  };
-
-  // 4-wave forms on a 2- or 3-deep ring: both k-steps' fragments read ahead, DMA pieces
-  // between the MFMA rows (CONV_INTERLEAVE=0 at build time: the burst form, for A/B)
-  constexpr bool interleave = CONV_INTERLEAVE != 0;
-  if constexpr (CT == kCT && NB == 4 && BK == 32) {
-    // Pipelined 4-wave form (APEX_AMD_CONV_PIPE): 32-deep K-tiles (one k-step) on a
-    // 4-deep ring, ONE barrier per K-tile, fragments register double-buffered.  Step kt
-    // multiplies F(kt) from registers while it reads F(kt+1) from the ring in the order
-    // the next step's MFMA rows consume them (B fragments, then A row by row: every
-    // counted lgkmcnt covers reads issued >= 2 rows earlier) and issues tile kt+3's DMA
-    // pieces between the MFMA rows.  Tile kt+3 goes to slot (kt+3) % 4 = (kt-1) % 4,
-    // whose tile every wave finished reading in step kt-2 (retired by the lgkmcnt(0) in
-    // front of step kt-1's barrier); the counted vmcnt(G) at the top of step kt leaves
-    // tile kt+2 in flight and retires tile kt+1, which the barrier then publishes to
-    // every wave's reads.  Tiles past the end re-fetch the last tile into the free slot
-    // (every step issues G pieces: the counted waits stay exact).  The burst form above
-    // read each K-tile's fragments right before its MFMAs and waited for them (PMC: 28 %
-    // MFMA busy, 32 % of wave cycles in s_waitcnt / s_barrier, docs/PERF.md round 4).
-    static_assert(KS == 1, "one k-step per K-tile");
-    if (KT > 0) {
-      auto tile_at = [&](int kt_) {  // data of tile min(kt_, KT-1), slot kt_ % NB
-        TileSrc t = tile_src(kt_ < KT ? kt_ : KT - 1);
-        t.A = lds + (kt_ % NB) * BUF;
-        return t;
-      };
-      constexpr int NR = FM + FN;               // fragment reads per step
-      constexpr int RPG = (NR + FM - 1) / FM;   // reads per MFMA row group
-      constexpr int PPG = (G + FM - 1) / FM;    // DMA pieces per MFMA row group
-      // n-th read of a step: B0 .. B(FN-1), then A0 .. A(FM-1)
-      auto rd1 = [&](int kt_, int n, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
-        const unsigned char* A = lds + (kt_ % NB) * BUF;
-        if (n < FN) {
-          bfr[n] = *reinterpret_cast<const bf16x8*>(A + A_BYTES + swzr<RB>(wn * TN + n * 16 + fr, fg));
-        } else {
-          const int i = n - FN;
-          af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<RB>(wm * TM + i * 16 + fr, fg));
-        }
-      };
-#pragma unroll
-      for (int p = 0; p < NB - 1; ++p) {
-        const TileSrc t = tile_at(p);
-#pragma unroll
-        for (int q = 0; q < G; ++q) piece(t, q);
-      }
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      rd(0, 0, fa0, fb0);
-      auto step = [&](int kt_, bf16x8 (&ca)[FM], bf16x8 (&cb)[FN], bf16x8 (&na)[FM],
-                      bf16x8 (&nb)[FN]) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const TileSrc tn = tile_at(kt_ + NB - 1);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i], cb[j], acc[i][j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int u = 0; u < RPG; ++u)
-            if (i * RPG + u < NR) rd1(kt_ + 1, i * RPG + u, na, nb);
-#pragma unroll
-          for (int u = 0; u < PPG; ++u)
-            if (i * PPG + u < G) piece(tn, i * PPG + u);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      for (int kt = 0; kt < KT; kt += 2) {
-        step(kt, fa0, fb0, fa1, fb1);
-        if (kt + 1 < KT) step(kt + 1, fa1, fb1, fa0, fb0);
-      }
-      // the re-fetches past the end write the ring, which the epilogue reuses
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  } else if constexpr (CT == 512 && NB == 3 && BK == 64) {
-    // 8-wave form: ONE barrier per K-tile.  Phase A multiplies k-step 0 of tile kt from
-    // registers while it reads k-step 1's fragments and issues the last PA DMA pieces of
-    // tile kt+2 between the MFMA rows; phase B waits for tile kt+1 (vmcnt(G) leaves all
-    // of tile kt+2 in flight), passes the barrier, and multiplies k-step 1 while it reads
-    // tile kt+1's k-step-0 fragments and issues the first PB pieces of tile kt+3.  Tile
-    // T's buffer (T % 3) was last read in phase A(T-3), retired (lgkmcnt(0)) before
-    // barrier B(T-3), after which its first pieces go out; a DMA piece costs ~60 issue
-    // cycles, which the partner wave's MFMAs hide when it sits between MFMA rows instead
-    // of in a burst after a barrier, and a whole tile (48 KB at 256 x 128) stays in
-    // flight across every barrier.
-    constexpr int PA = (G + 1) / 2, PB = G - PA;
-    static_assert(PA <= FM && PB <= FM, "DMA pieces per MFMA row");
-    if (KT > 0) {
-      const TileSrc t0 = tile_src(0);
-#pragma unroll
-      for (int q = 0; q < G; ++q) piece(t0, q);
-    }
-    if (KT > 1) {
-      const TileSrc t1 = tile_src(1);
-#pragma unroll
-      for (int q = 0; q < G; ++q) piece(t1, q);
-    }
-    if (KT > 2) {
-      const TileSrc t2 = tile_src(2);
-#pragma unroll
-      for (int q = 0; q < PB; ++q) piece(t2, q);
-    }
-    if (KT > 2) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + PB) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    rd(0, 0, fa0, fb0);
-    for (int kt = 0; kt < KT; ++kt) {
-      const bool more = kt + 2 < KT, more3 = kt + 3 < KT;
-      const TileSrc tA = tile_src(more ? kt + 2 : kt);
-      const TileSrc tB = tile_src(more3 ? kt + 3 : kt);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (i < PA && more) piece(tA, PB + i);
-        if (i == 0) rd(kt, 1, fa1, fb1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (i < PB && more3) piece(tB, i);
-        if (i == 0 && kt + 1 < KT) rd(kt + 1, 0, fa0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  } else {
+  {
     // prologue: NB-1 tiles in flight
   #pragma unroll
     for (int p = 0; p < NB - 1; ++p)
@@ -680,36 +467,6 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (interleave && BK == 64 && !g.burst) {
-          // both k-steps' fragments first, then the MFMA rows with tile kt+NB-1's DMA
-          // pieces between them (the buffer of tile kt+NB-1 was last read at iteration
-          // kt-1: every wave has passed this barrier, so it is free)
-          const bool issue = kt + NB - 1 < KT;
-          const TileSrc tn = tile_src(issue ? kt + NB - 1 : kt);
-          bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
-          // (at most 15 LDS reads may be outstanding for a counted lgkmcnt: k-step 1's B
-          // fragments go out after the first MFMA row)
-          rd(kt, 0, fa0, fb0);
-          __builtin_amdgcn_sched_barrier(0);
-          rd_a(kt, 1, fa1);
-          __builtin_amdgcn_sched_barrier(0);
-          constexpr int PER = (G + 2 * FM - 1) / (2 * FM);
-#pragma unroll
-          for (int r = 0; r < 2 * FM; ++r) {
-            const int i = r % FM;
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  r < FM ? fa0[i] : fa1[i], r < FM ? fb0[j] : fb1[j], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (r == 0) rd_b(kt, 1, fb1);
-#pragma unroll
-            for (int u = 0; u < PER; ++u)
-              if (issue && r * PER + u < G) piece(tn, r * PER + u);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          continue;
-        }
         if (kt + NB - 1 < KT) CONV_ISSUE(kt + NB - 1);
       }
       const unsigned char* A = lds + (kt % NB) * BUF;
@@ -827,182 +584,42 @@ __global__ void __launch_bounds__(CT, (CT > kCT || BM == 256 ||
   }
 }
 
-// M-tile choice: 128 (2 workgroups / CU, 64x64 per wave) or 256 (1 workgroup / CU,
-// 128x64 per wave: 1/3 less LDS read traffic per MFMA; 2- or 3-deep DMA ring).
-// APEX_AMD_CONV_BM = 128 | 256 | 256x3 for A/B runs (tools/microbench.py conv3x3).
-// 256w8 = 256 x 128 tiles, 8 waves (64 x 64 each), 3-deep ring, one workgroup per CU;
-// 256w8n2 the same on a 2-deep ring; 128w8 = 128 x 128, 8 waves (32 x 64), 3-deep.
-static int conv_bm_choice() {
-  const char* e = std::getenv("APEX_AMD_CONV_BM");
-  if (!e) return 0;
-  if (std::strcmp(e, "256") == 0) return 1;
-  if (std::strcmp(e, "256x3") == 0) return 2;
-  if (std::strcmp(e, "128x3") == 0) return 3;
-  if (std::strcmp(e, "256w8") == 0) return 4;
-  if (std::strcmp(e, "256w8n2") == 0) return 5;
-  if (std::strcmp(e, "128w8") == 0) return 6;
-  if (std::strcmp(e, "bk32") == 0) return 7;
-  if (std::strcmp(e, "bk32n3") == 0) return 8;
-  return 0;
-}
-
-static int conv_bm_of(int big) { return big == 1 || big == 2 || big == 4 || big == 5 ? 256 : 128; }
-
-// 1x1 forward convs with at most this many 64-channel K-tiles run the NB = 1 variant
-// (APEX_AMD_CONV1X1_NB1 = 0 | 1 | 2 | ..., read per launch for A/B runs)
-static int conv1x1_nb1_max_kt() {
-  const char* e = std::getenv("APEX_AMD_CONV1X1_NB1");
-  return e ? std::atoi(e) : 1;
-}
-
-// APEX_AMD_BNBWD_NB2 = 0 | 1 (read per launch, A/B runs): 64-wide BN-backward epilogue
-// tiles on the 2-deep ring
-static bool bnbwd_nb2() {
-  const char* e = std::getenv("APEX_AMD_BNBWD_NB2");
-  return e ? e[0] == '1' : true;
-}
-
-// APEX_AMD_CONV64_NB2 = 0 | 1 (read per launch, A/B runs): 64-wide output tiles without
-// the BN-backward epilogue on the 2-deep ring too (48 KB of LDS: 3 workgroups per CU
-// instead of 2, so more workgroups' DMA prologues and epilogues overlap others' K loops
-// on the short-K layer-1 shapes).  ResNet-50 same-box A/B: 10,465 / 10,455 -> 10,540 /
-// 10,530 img/s.
-static bool conv64_nb2() {
-  const char* e = std::getenv("APEX_AMD_CONV64_NB2");
-  return e ? e[0] == '1' : true;
-}
-
-// 32-deep K-tiles on a 3-deep ring of 16 KB stages (APEX_AMD_CONV_BK32 = auto | 0 | 1, read
-// per launch): 48 KB in flight per workgroup instead of one 32 KB tile and up to 3
-// workgroups per CU - the 128 x 128 convs are latency-bound on their 2-deep ring.  Same-box
-// microbench (tools/conv_variants.py, profiles/r4/f/variants*.md): it wins where the
-// grid is large (128@28 3x3 94.8 -> 86.3 us, 1x1 256->1024@14 58.9 -> 44.2 us) and loses
-// where a grid of <= 784 workgroups leaves each CU one or two long K loops (3x3 256@14
-// 82 -> 96 us: twice the barriers per K), so "auto" takes it from 1024 workgroups up.
-static bool conv_bk32(unsigned wgs) {
-  const char* e = std::getenv("APEX_AMD_CONV_BK32");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
-  return wgs >= 1024;
-}
-// 1x1 data gradients with the BN-backward epilogue over >= 50,176 output pixels
-// (ResNet-50 layers 1-3): 64-row M tiles (APEX_AMD_BNBWD_BM64 = 0 | 1, read per launch).
-// The per-call table of the serialized step (profiles/r5/conv_calls.md) has these at
-// 2.8-3.5 TB/s of epilogue traffic: the K loop is 1-4 K-tiles, the rest is the epilogue's
-// loads and stores, streamed by only 2 workgroups per CU with 128-row tiles.  Same-box
-// ResNet-50: 11,433 / 11,430 img/s with 64-row tiles vs 11,392 / 11,374 (profiles/r5/).
-static bool bnbwd_bm64(int ksize, int NC, int64_t M) {
-  const char* e = std::getenv("APEX_AMD_BNBWD_BM64");
-  const bool on = e ? e[0] == '1' : true;
-  // (an explicit APEX_AMD_CONV_BM tiling takes precedence, as in launch_conv_tap)
-  return on && ksize == 1 && NC % 128 == 0 && M >= 50176 && conv_bm_choice() == 0;
-}
-// the same 64-row tiles for plain stride-1 1x1 forwards / data gradients over >= 200,704
-// output pixels (APEX_AMD_FWD1_BM64 = 0 | 1, read per launch).  Measured slower, so off:
-// ResNet-50 11,203 / 11,176 vs 11,315 / 11,330 img/s same box (profiles/r5/ab_r50_fbm64):
-// these K-light convs already stream at 3.5-3.8 TB/s on 128-row tiles.
-static bool fwd1_bm64(int ksize, int NC, int64_t M) {
-  const char* e = std::getenv("APEX_AMD_FWD1_BM64");
-  const bool on = e ? e[0] == '1' : false;
-  return on && ksize == 1 && NC % 128 == 0 && M >= 200704 && conv_bm_choice() == 0;
-}
-// the pipelined 4-deep-ring K loop for the 32-deep forms (conv_tap_k NB = 4;
-// APEX_AMD_CONV_PIPE = 0 | 1, read per launch)
-static bool conv_pipe() {
-  const char* e = std::getenv("APEX_AMD_CONV_PIPE");
-  return e ? e[0] == '1' : false;
-}
-// the 64-wide-tile form (APEX_AMD_CONV_BK32_64 = 0 | 1, default on): layer-1 3x3 64@56
-// 111.1 -> 105.6 us fwd, 102.7 -> 99.4 us dgrad; ResNet-50 same box, two runs each:
-// 10,357 / 10,359 img/s (no BK = 32), 10,490 / 10,563 (128-wide tiles only), 10,564 /
-// 10,596 (both; profiles/r4/f/)
-static bool conv_bk32_64() {
-  const char* e = std::getenv("APEX_AMD_CONV_BK32_64");
-  return e ? e[0] == '1' : true;
-}
-
-// APEX_AMD_CONV_BURST=1 (read per launch, A/B runs): the 4-wave kernels' pre-round-4 K
-// loop - each tile's DMA pieces as one burst after the barrier, fragments read per k-step
-static int conv_burst() {
-  const char* e = std::getenv("APEX_AMD_CONV_BURST");
-  return e ? (e[0] == '1' ? 1 : 0) : 1;
-}
-
+// Tile choice per launch (measured per shape, docs/PERF.md rounds 3-5; the losing A/B
+// variants - 256-row tiles with 4 or 8 waves, the 4-deep pipelined 32-deep ring, the
+// burst-free interleaved 64-deep loop, 64-row tiles for the large 1x1 forwards - were
+// removed in round 6):
+//  * 1x1 data gradients with the BN-backward epilogue over >= 50,176 output pixels
+//    (ResNet-50 layers 1-3; 2.8-3.5 TB/s of epilogue traffic): 64-row M tiles, up to 4
+//    workgroups per CU (11,373 -> 11,430 img/s, profiles/r5/ab_r50_bm64/);
+//  * 1x1 forwards with one 64-channel K-tile (the layer-1/2 channel-expanding convs): no
+//    DMA ring (NB = 1), 3 workgroups per CU;
+//  * 128-wide output tiles: 32-deep K-tiles on a 3-deep ring where the grid has >= 1024
+//    workgroups (48 KB in flight, up to 3 workgroups per CU; 3x3 128@28 94.8 -> 86.3 us),
+//    64-deep K-tiles on a 2-deep ring on the smaller grids (twice the barriers per K
+//    cost more there: 3x3 256@14 82 -> 96 us);
+//  * 64-wide output tiles: 32-deep K-tiles on a 3-deep ring (layer-1 3x3 64@56 fwd
+//    111 -> 106 us, dgrad 103 -> 99 us).
 template <int MODE, int EPI = 0>
-void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g0,
+void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
                      const ConvBnEpi& ep = ConvBnEpi{}) {
-  if (g0.M == 0) return;
-  ConvGeom g = g0;
-  g.burst = conv_burst();
-  {
-    const char* e = std::getenv("APEX_AMD_DGRAD_LPT");
-    g.lpt = e ? (e[0] == '1') : 1;
-  }
+  if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
-  const int big = g.NC % 128 == 0 ? conv_bm_choice() : 0;
-  if (big == 7 || big == 8) {
-    // 32-deep K-tiles: a 4- (or 3-) deep ring of 16 KB stages, two workgroups per CU
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    if (big == 7)
-      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 4, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-    else
-      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (big >= 4) {
-    const int bm = conv_bm_of(big);
-    const dim3 grid((g.M + bm - 1) / bm, g.NC / 128, nclasses);
-    if (big == 4)
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 4, 2, 3, EPI, 512>), grid, dim3(512), 0, st, a, w, y, g, slab, shift, ep);
-    else if (big == 5)
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 4, 2, 2, EPI, 512>), grid, dim3(512), 0, st, a, w, y, g, slab, shift, ep);
-    else
-      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 4, 2, 3, EPI, 512>), grid, dim3(512), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (big == 3) {
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (big) {
-    const dim3 grid((g.M + 255) / 256, g.NC / 128, nclasses);
-    if (big == 2)
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-    else
-      hipLaunchKernelGGL((conv_tap_k<MODE, 256, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (EPI == 0 && MODE == kFwd1 && fwd1_bm64(1, g.NC, g.M)) {
-    // memory-bound 1x1 forwards / data gradients on the 56x56 and 28x28 layers: the
-    // same 64-row tiles (up to 4 workgroups per CU)
+  if (EPI == 1 && MODE == kFwd1 && g.NC % 128 == 0 && g.M >= 50176) {
     const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (EPI == 1 && MODE == kFwd1 && bnbwd_bm64(1, g.NC, g.M)) {
-    // memory-bound BN-backward epilogues: 64-row M tiles (36 KB of LDS, up to 4
-    // workgroups per CU: twice the waves streaming the epilogue's residual / BN-input
-    // loads and the gradient stores)
-    const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= conv1x1_nb1_max_kt()) {
+  } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= 1) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (g.NC % 128 == 0) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
-    if (conv_bk32(grid.x * grid.y * grid.z) && conv_pipe())
-      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 4, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-    else if (conv_bk32(grid.x * grid.y * grid.z))
+    if (grid.x * grid.y * grid.z >= 1024)
       hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if (conv_bk32_64() && !(EPI == 1 && !bnbwd_nb2())) {
-    // 64-wide tiles with 32-deep K-tiles on a 3-deep ring (36 KB of LDS)
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
-    if (conv_pipe())
-      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 4, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-    else
-      hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
-  } else if ((EPI == 1 && bnbwd_nb2()) || (EPI == 0 && conv64_nb2())) {
-    // BN-backward epilogue on 64-wide tiles: a 2-deep ring (48 KB of LDS -> 3 workgroups
-    // per CU instead of 2), so more K loops run under each workgroup's epilogue reads
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   }
 }
 
@@ -1669,15 +1286,6 @@ __global__ void __launch_bounds__(256) prep_weights_k(PrepArgs a) {
   }
 }
 
-// APEX_AMD_REDUCE_ONE=0: always the two-stage split-K reduction (A/B)
-bool single_pass_reduce() {
-  static const bool on = [] {
-    const char* e = std::getenv("APEX_AMD_REDUCE_ONE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // per-tap kernel tiling: 128 x 128 when both channel counts allow it, else 64 x 64
 // (algo 2/3: tuning variants - deeper DMA ring with a shorter or equal K-tile)
 struct WgTapCfg {
@@ -1725,13 +1333,7 @@ int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int str
   const int64_t M = (int64_t)N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
   const int total_kt = (int)((M + c.BK - 1) / c.BK);
   const int gx = T * (Cout / c.BM) * (Cin / c.BN);
-  int slots = c.BK * c.NB * (c.BM + c.BN) * 2 > 80 * 1024 ? 256 : 512;  // WGs per CU
-  // APEX_AMD_WGRAD3_SLOTS (A/B knob): size the split count for fewer resident workgroups
-  // (the kernel runs on the weight-gradient side stream beside the main stream's work)
-  if (const char* e = std::getenv("APEX_AMD_WGRAD3_SLOTS")) {
-    const int v = std::atoi(e);
-    if (v >= 64 && v < slots) slots = v;
-  }
+  const int slots = c.BK * c.NB * (c.BM + c.BN) * 2 > 80 * 1024 ? 256 : 512;  // WGs per CU
   const double t_tile = 2.0 * c.BM * c.BN * c.BK / (4096.0 * 2400.0 * 0.5 / (slots / 256));  // us
   const double t_split = (double)T * Cout * Cin * 8.0 / 5.0e6;                     // us
   int best = 1;
@@ -1812,7 +1414,7 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
   // stage-1 slabs (conv_wgrad_workspace); one pass when S <= 16 (Cin % 4 == 0)
   const int64_t nout = (int64_t)T * Cout * Cin;
   const int Gn = (S + kRedGroup - 1) / kRedGroup;
-  if (Gn == 1 && Cin % 4 == 0 && single_pass_reduce()) {
+  if (Gn == 1 && Cin % 4 == 0) {
     const int64_t n4 = nout / 4;
     const unsigned blocks = (unsigned)((n4 + 255) / 256);
     if (dw_fp32)
@@ -1846,7 +1448,7 @@ void splitk_reduce(const float* part, int S, int Cout, int Cin, float* stage, vo
                    bool out_fp32, hipStream_t st, bool accum) {
   const int64_t n = (int64_t)Cout * Cin;
   const int Gn = (S + kRedGroup - 1) / kRedGroup;
-  if (Gn == 1 && Cin % 4 == 0 && single_pass_reduce()) {
+  if (Gn == 1 && Cin % 4 == 0) {
     const int64_t n4 = n / 4;
     const unsigned blocks = (unsigned)((n4 + 255) / 256);
     if (out_fp32)
@@ -1901,10 +1503,9 @@ void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipSt
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t M = (int64_t)N * Ho * Wo;
-  if (fwd1_bm64(ksize, Cout, M)) return (int)((M + 63) / 64);
-  const int big = Cout % 128 == 0 ? conv_bm_choice() : 0;  // launch_conv_tap's M tile
-  const int bm = conv_bm_of(big);
-  return (int)((M + bm - 1) / bm);
+  (void)ksize;
+  (void)Cout;
+  return (int)((M + kBM - 1) / kBM);  // launch_conv_tap's M tile (EPI 0)
 }
 
 void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
@@ -1921,10 +1522,9 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
 
 int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize) {
   const int64_t M = (int64_t)N * H * W;
-  if (bnbwd_bm64(ksize, Cout, M)) return (int)((M + 63) / 64);
-  const int big = Cout % 128 == 0 ? conv_bm_choice() : 0;  // launch_conv_tap's M tile
-  const int bm = conv_bm_of(big);
-  return (int)((M + bm - 1) / bm);
+  // launch_conv_tap's M tile with the BN-backward epilogue (64 rows for the large 1x1s)
+  if (ksize == 1 && Cout % 128 == 0 && M >= 50176) return (int)((M + 63) / 64);
+  return (int)((M + kBM - 1) / kBM);
 }
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H, int W, int Cin,
                          int Cout, int ksize, int stride, const ConvBnEpi& ep, float* slab,

@@ -539,16 +539,10 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// fast backward grid: at most 1024 blocks x 4 waves walking rows (APEX_AMD_LN_BWD_BLOCKS
-// overrides, for A/B sweeps; 256 with a row of load lookahead measured 126 vs 77 us per
-// GPT-2 join - occupancy, not lookahead, hides the latency)
-static inline int ln_bwd_block_cap() {
-  static const int cap = [] {
-    const char* e = std::getenv("APEX_AMD_LN_BWD_BLOCKS");
-    return e ? std::atoi(e) : 1024;
-  }();
-  return cap > 0 ? cap : 1024;
-}
+// fast backward grid: at most 1024 blocks x 4 waves walking rows (256 with a row of load
+// lookahead measured 126 vs 77 us per GPT-2 join - occupancy, not lookahead, hides the
+// latency; a 512 / 2048 cap measured equal, profiles/r4/k/)
+static inline int ln_bwd_block_cap() { return 1024; }
 
 static inline int ln_bwd_blocks(int64_t n1) {
   int64_t b = (n1 + kLNWaves - 1) / kLNWaves;

@@ -677,10 +677,6 @@ int device_cu_count() {
   return cus[dev];
 }
 
-int mt_persistent_wgs_per_cu() {
-  const char* e = std::getenv("APEX_AMD_MT_WGS_PER_CU");
-  return e ? std::atoi(e) : 0;  // measured: one WG per chunk is best for SGD / Adam
-}
 
 }  // namespace amd
 

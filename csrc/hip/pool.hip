@@ -330,72 +330,6 @@ __global__ void __launch_bounds__(kPoolThreads)
   }
 }
 
-// input row h is covered by output rows oh = h/2 (h even: tap row 1) or
-// oh = (h-1)/2 (tap row 2) and (h+1)/2 (tap row 0) for odd h
-template <typename T>
-__global__ void __launch_bounds__(kPoolThreads)
-    maxpool3s2_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx,
-                     int N, int H, int W, int C, int OH, int OW) {
-  static_assert(sizeof(T) == 2, "16-bit activations");
-  const int CV = C / 8;
-  const int64_t total = (int64_t)N * H * W * CV;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int cv = (int)(t % CV);
-    int64_t pix = t / CV;
-    const int w = (int)(pix % W);
-    pix /= W;
-    const int h = (int)(pix % H);
-    const int n = (int)(pix / H);
-    int ohs[2], khs[2], ows[2], kws[2];
-    bool oho[2], owo[2];
-    if (h & 1) {
-      ohs[0] = (h - 1) >> 1; khs[0] = 2; ohs[1] = (h + 1) >> 1; khs[1] = 0;
-    } else {
-      ohs[0] = h >> 1; khs[0] = 1; ohs[1] = 0; khs[1] = -1;
-    }
-    if (w & 1) {
-      ows[0] = (w - 1) >> 1; kws[0] = 2; ows[1] = (w + 1) >> 1; kws[1] = 0;
-    } else {
-      ows[0] = w >> 1; kws[0] = 1; ows[1] = 0; kws[1] = -1;
-    }
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      oho[a] = khs[a] >= 0 && ohs[a] < OH;
-      owo[a] = kws[a] >= 0 && ows[a] < OW;
-    }
-    p_u32x4 g[4];
-    uint2 ii[4];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const bool ok = oho[a] && owo[b];
-        const int64_t o = (((int64_t)n * OH + (ok ? ohs[a] : 0)) * OW + (ok ? ows[b] : 0)) * C + cv * 8;
-        g[a * 2 + b] = *reinterpret_cast<const p_u32x4*>(dy + o);
-        ii[a * 2 + b] = *reinterpret_cast<const uint2*>(idx + o);
-      }
-    float acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if (!(oho[a] && owo[b])) continue;
-        const int tap = khs[a] * 3 + kws[b];
-        float gv[8];
-        unpack8_any<T>(g[a * 2 + b], gv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t word = i < 4 ? ii[a * 2 + b].x : ii[a * 2 + b].y;
-          if ((int)((word >> (8 * (i & 3))) & 0xff) == tap) acc[i] += gv[i];
-        }
-      }
-    store8(dx + (((int64_t)n * H + h) * W + w) * C + cv * 8, acc);
-  }
-}
-
 // global average pool backward, NHWC: dx[n, hw, c] = dy[n, c] * inv_hw.  dy is one
 // [C] row per image (L2-resident), dx is written once with 16-byte stores in memory
 // order - the gradient of x.mean((2, 3)) materialised channels-last directly, instead
@@ -431,14 +365,9 @@ void pool_dispatch(DType t, F&& f) {
   }
 }
 
-// the specialised 3x3 / stride-2 / pad-1 kernels (output size floor((H-1)/2)+1);
-// APEX_AMD_POOL_GENERIC=1 forces the generic kernels (A/B)
+// the specialised 3x3 / stride-2 / pad-1 kernels (output size floor((H-1)/2)+1)
 bool stem_ok(int k, int s, int p, int H, int W, int OH, int OW) {
-  static const bool generic = [] {
-    const char* e = std::getenv("APEX_AMD_POOL_GENERIC");
-    return e && e[0] == '1';
-  }();
-  return !generic && k == 3 && s == 2 && p == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1;
+  return k == 3 && s == 2 && p == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1;
 }
 
 int pool_grid(int64_t items) {
@@ -499,17 +428,10 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
     using T = decltype(t0);
     if constexpr (sizeof(T) == 2) {
       if (vec && stem_ok(k, s, p, H, W, OH, OW)) {
-        const char* e = std::getenv("APEX_AMD_POOL_BWD1");  // per launch: A/B tests
-        if (e && e[0] == '1') {
-          hipLaunchKernelGGL((maxpool3s2_bwd_k<T>), dim3(pool_grid(items)), dim3(kPoolThreads),
-                             0, st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W,
-                             C, OH, OW);
-        } else {
-          const int64_t blk = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
-          hipLaunchKernelGGL((maxpool3s2_bwd2_k<T>), dim3(pool_grid(blk)), dim3(kPoolThreads),
-                             0, st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W,
-                             C, OH, OW);
-        }
+        const int64_t blk = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+        hipLaunchKernelGGL((maxpool3s2_bwd2_k<T>), dim3(pool_grid(blk)), dim3(kPoolThreads), 0,
+                           st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C,
+                           OH, OW);
         return;
       }
     }

@@ -29,20 +29,10 @@
 // The MFMA takes the X fragment as its first operand, so the accumulator lane (fr, fg)
 // holds 4 CONSECUTIVE n of one m: one 16-byte fp32 store each.
 //
-// Three DMA / LDS layouts (template L, APEX_AMD_W4W_LAYOUT): 0 = the 16-row x 64-byte
-// blocks above; 1 = 8-row x 128-byte blocks (chunk key 2 (r >> 1 & 1) + 4 (r >> 3 & 1));
-// 2 = whole 512-byte rows, two per DMA instruction (chunk key 2 ((r & 3) | (r >> 3 & 1) << 2)).
-// All three read conflict-free and are bitwise equal (tests/test_wgrad4w_gpu.py).
-//
-// Variant 3 (APEX_AMD_W4W_LAYOUT=3) is layout 0 with the slot released per HALF K-tile:
-// wave w DMAs chunk groups 2w, 2w+1 of every row group (instead of row group w), so the
-// rows 0-31 of K-tile t+2 go out during k-step 0 of K-tile t (their half of the slot is
-// free once k-step 0's fragments were read) and rows 32-63 during k-step 1; a barrier
-// after each k-step, both behind the same s_waitcnt vmcnt(16).  A DMA piece then has 1.5
-// K-tiles to land instead of ~1: at full load a K-tile took 1.4-1.9 us against 1.15 us for
-// one workgroup, which looked like the loop waiting on loaded memory latency.  Measured
-// (profiles/r5/wgrad_dense/variant3_sweep.txt): within -3..+2 % of layout 0 on every BERT /
-// GPT-2 shape, so the slack was not the limit; it stays an A/B variant, bitwise equal.
+// Measured and removed in round 6 (round-5 A/Bs, all bitwise equal to this layout): 8-row x
+// 128-byte and whole-row DMA blocks (within 1-5 %), and the slot released per HALF K-tile
+// so a DMA piece gets 1.5 K-tiles to land (within -3..+2 % on every BERT / GPT-2 shape,
+// profiles/r5/wgrad_dense/variant3_sweep.txt: the load slack was not the limit).
 //
 // Status (round 5, profiles/r5/wgrad_dense.md): BERT-large FFN weight gradient 114.5 us
 // (1.20 PF, reduction included) vs 136.8 us for hipBLASLt's best split; one workgroup runs
@@ -165,13 +155,10 @@ __device__ __forceinline__ float ww_sum8(V8 f, float acc) {
   return acc;
 }
 
-// LV 4 = layout 0 with the column sums of A (p.colsum)
-template <typename TT, int LV>
+// CS: with the column sums of A (p.colsum)
+template <typename TT, bool CS>
 __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only needs the launch stub)
-  constexpr int L = (LV == 3 || LV == 4) ? 0 : LV;  // LDS layout
-  constexpr bool HB = LV == 3;         // half-K-tile slot release (variant 3)
-  constexpr bool CS = LV == 4;         // column sums of A
   typedef typename WwT<TT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kWwSlot];
 
@@ -194,42 +181,13 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
   const int KT = p.rows >> 6;
   const int64_t k0 = (int64_t)s * p.rows;
 
-  // DMA.  L == 0: wave w fills blocks (row group w, chunk group cg = 0..7) of each operand;
-  // lane (i = lane >> 2, j = lane & 3) reads row 16 w + i, chunk cg*4 + (j ^ 2 (i >> 3 & 1)).
-  // L == 1: blocks of 8 rows x 8 chunks (128 contiguous bytes per row); wave w fills row
-  // groups 2w + h (h = 0, 1) x chunk groups cg = 0..3; lane (i = lane >> 3, j = lane & 7)
-  // reads row 8 (2w + h) + i, chunk cg*8 + (j ^ f), f = 2 (i >> 1 & 1) + 4 h.  The K-tile
-  // and the chunk group go into the (scalar) soffset.
-  // L == 2: blocks of 2 rows x 512 bytes (whole rows); piece q of wave w holds rows
-  // 16 w + 2 q + (lane >> 5), lane & 31 the physical chunk of logical chunk
-  // (lane & 31) ^ key(r), key(r) = 2 ((r & 3) | (r >> 3 & 1) << 2): one offset per piece
-  uint32_t offA[8], offB[8];  // (a fixed bound: an array whose bound depends on L, captured
-  // by the lambdas below, made clang drop the kernel host stub)
-  if constexpr (L == 2) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int r = wid * 16 + 2 * q + (lane >> 5);
-      const int key = 2 * ((r & 3) | (((r >> 3) & 1) << 2));
-      const uint32_t ch = (uint32_t)((lane & 31) ^ key) * 16u;
-      offA[q] = (uint32_t)r * (uint32_t)p.lda * (uint32_t)sizeof(TT) + ch;
-      offB[q] = (uint32_t)r * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + ch;
-    }
-  } else {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    int drow, dch;
-    if constexpr (L == 0) {
-      // (variant 3: the row group goes into the soffset, see piece_hb)
-      drow = (HB ? 0 : wid * 16) + (lane >> 2);
-      dch = (lane & 3) ^ (((lane >> 5) & 1) << 1);
-    } else {
-      drow = (2 * wid + h) * 8 + (lane >> 3);
-      dch = (lane & 7) ^ ((((lane >> 4) & 1) << 1) | (h << 2));
-    }
-    offA[h] = (uint32_t)drow * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)dch * 16u;
-    offB[h] = (uint32_t)drow * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)dch * 16u;
-  }
-  }
+  // DMA: wave w fills blocks (row group w, chunk group cg = 0..7) of each operand; lane
+  // (i = lane >> 2, j = lane & 3) reads row 16 w + i, chunk cg*4 + (j ^ 2 (i >> 3 & 1)).
+  // The K-tile and the chunk group go into the (scalar) soffset.
+  const int drow = wid * 16 + (lane >> 2);
+  const int dch = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+  const uint32_t offA = (uint32_t)drow * (uint32_t)p.lda * (uint32_t)sizeof(TT) + (uint32_t)dch * 16u;
+  const uint32_t offB = (uint32_t)drow * (uint32_t)p.ldb * (uint32_t)sizeof(TT) + (uint32_t)dch * 16u;
   const __amdgpu_buffer_rsrc_t rA =
       ww_rsrc(static_cast<const TT*>(p.A) + k0 * p.lda + m0, 0xffffffffu);
   const __amdgpu_buffer_rsrc_t rB =
@@ -242,63 +200,31 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
   auto piece = [&](int T, int q) {
     const int Tc = T < KT ? T : KT - 1;
     const int qq = q & 7;
-    const int h = L == 2 ? (qq & 7) : L == 0 ? 0 : (qq >> 2);
-    const int blk = L == 1 ? (2 * wid + h) * 4 + (qq & 3) : wid * 8 + qq;
-    const uint32_t cgo = L == 0 ? (uint32_t)qq * 64u : L == 1 ? (uint32_t)(qq & 3) * 128u : 0u;
-    const uint32_t dst = lds_base + (uint32_t)((T & 1) * kWwSlot + (q >> 3) * kWwOp + blk * 1024);
+    const uint32_t cgo = (uint32_t)qq * 64u;
+    const uint32_t dst = lds_base + (uint32_t)((T & 1) * kWwSlot + (q >> 3) * kWwOp + (wid * 8 + qq) * 1024);
     if (q < 8) {
-      ww_dma(rA, dst, offA[h], (uint32_t)Tc * strideA + cgo);
+      ww_dma(rA, dst, offA, (uint32_t)Tc * strideA + cgo);
     } else {
-      ww_dma(rB, dst, offB[h], (uint32_t)Tc * strideB + cgo);
-    }
-  };
-  // variant 3: piece j (0..3 A, 4..7 B) of half hf of K-tile T: block (row group
-  // rg = 2 hf + (j >> 1 & 1), chunk group cg = 2 wid + (j & 1)) - the same LDS image as
-  // layout 0, every wave filling both halves
-  const uint32_t rowgA = 16u * (uint32_t)p.lda * (uint32_t)sizeof(TT);
-  const uint32_t rowgB = 16u * (uint32_t)p.ldb * (uint32_t)sizeof(TT);
-  auto piece_hb = [&](int T, int hf, int j) {
-    const int Tc = T < KT ? T : KT - 1;
-    const int rg = 2 * hf + ((j >> 1) & 1), cg = 2 * wid + (j & 1);
-    const uint32_t dst =
-        lds_base + (uint32_t)((T & 1) * kWwSlot + (j >> 2) * kWwOp + (rg * 8 + cg) * 1024);
-    if (j < 4) {
-      ww_dma(rA, dst, offA[0], (uint32_t)Tc * strideA + (uint32_t)rg * rowgA + (uint32_t)cg * 64u);
-    } else {
-      ww_dma(rB, dst, offB[0], (uint32_t)Tc * strideB + (uint32_t)rg * rowgB + (uint32_t)cg * 64u);
+      ww_dma(rB, dst, offB, (uint32_t)Tc * strideB + cgo);
     }
   };
 
   // transposed fragment reads: lane (q = (lane & 15) >> 2, p1 = lane >> 1 & 1, p0 = lane & 1,
   // fg = lane >> 4) of fragment i (columns 16 i .. of the wave's 128) at k-step ks: rows
-  // ks*32 + fg*8 + q (+4 for the second read), chunk 2 i + p1, byte 8 p0.  L == 0: a lane
-  // base per parity of i; L == 1: per i & 3 (the XOR key spans chunk bits 1-2)
+  // ks*32 + fg*8 + q (+4 for the second read), chunk 2 i + p1, byte 8 p0: a lane base
+  // per parity of i
   const int fq = (lane & 15) >> 2, fp1 = (lane >> 1) & 1, fp0 = lane & 1, fg = lane >> 4;
-  constexpr int NLB = L == 0 ? 2 : L == 1 ? 4 : 8;
-  constexpr int HI = L == 0 ? 256 : L == 1 ? 512 : 2048;  // byte distance of rows +4
-  int lb[8];
+  constexpr int HI = 256;  // byte distance of rows +4
+  int lb[2];
 #pragma unroll
-  for (int ip = 0; ip < NLB; ++ip) {
-    if constexpr (L == 2) {
-      const int kk = fq | ((fg & 1) << 2);
-      lb[ip] = fg * 4096 + fq * 512 + ((2 * (ip ^ kk) + fp1) << 4) + 8 * fp0;
-    } else if constexpr (L == 0) {
-      lb[ip] = (fg >> 1) * 8 * 1024 + ((fg & 1) * 8 + fq) * 64 +
-               (((2 * ip + fp1) ^ ((fg & 1) << 1)) << 4) + 8 * fp0;
-    } else {
-      const int f = (((fq >> 1) & 1) << 1) | ((fg & 1) << 2);
-      lb[ip] = fg * 4096 + fq * 128 + (((2 * ip + fp1) ^ f) << 4) + 8 * fp0;
-    }
-  }
+  for (int ip = 0; ip < 2; ++ip)
+    lb[ip] = (fg >> 1) * 8 * 1024 + ((fg & 1) * 8 + fq) * 64 +
+             (((2 * ip + fp1) ^ ((fg & 1) << 1)) << 4) + 8 * fp0;
   v8 fa0[8], fb0[8], fa1[8], fb1[8];
   // n-th read of a k-step in the order the next k-step's groups consume them (group g:
   // A[g / 2] with B[(g & 1) * 4 .. +3]): B0-3, A0, B4-7, A1 .. A7
   auto rd_order = [](int n) { return n < 4 ? 8 + n : n == 4 ? 0 : n < 9 ? 7 + n : n - 8; };
-  auto frag_off = [&](int i, int w) {
-    if constexpr (L == 2) return lb[i & 7] + w * 256;
-    else if constexpr (L == 0) return lb[i & 1] + w * 4096 + (i >> 1) * 1024;
-    else return lb[i & 3] + w * 2048 + (i >> 2) * 1024;
-  };
+  auto frag_off = [&](int i, int w) { return lb[i & 1] + w * 4096 + (i >> 1) * 1024; };
   auto rd = [&](int slot, int ks, int n, v8(&fa)[8], v8(&fb)[8]) {
     const unsigned char* base = lds + slot * kWwSlot + ks * 16384;
     if (n < 8) {
@@ -317,29 +243,14 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
   }
 
   // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed, its k-step-0 fragments read
-  if constexpr (HB) {
 #pragma unroll
-    for (int T = 0; T < 2; ++T)
+  for (int q = 0; q < 16; ++q) piece(0, q);
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) piece_hb(T, hf, j);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) piece(0, q);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) piece(1, q);
-  }
+  for (int q = 0; q < 16; ++q) piece(1, q);
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   ww_barrier();
 #pragma unroll
   for (int n = 0; n < 16; ++n) rd(0, 0, rd_order(n), fa0, fb0);
-  if constexpr (HB) {
-    // K-tile 2's first half goes into rows 0-31 of slot 0 during k-step 0: every wave's
-    // k-step-0 reads of them must have retired
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    ww_barrier();
-  }
 
 #define WW_GROUP(FA, FB, g, OP)                                              \
   _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                         \
@@ -366,19 +277,10 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
       rd(slot, 1, rd_order(g), fa1, fb1);
-      if constexpr (HB) {
-        if ((g & 1) == 0) piece_hb(t + 2, 0, g >> 1);
-      }
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (HB) {
-      // K-tile t+1's first half landed (issued after it: its second half and K-tile
-      // t+2's first half, 8 pieces each)
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ww_barrier();
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
@@ -388,20 +290,8 @@ __global__ void __launch_bounds__(kWwT, 1) wgrad4w_k(WgradArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
       rd(slot ^ 1, 0, rd_order(g), fa0, fb0);
-      if constexpr (HB) {
-        if ((g & 1) == 0) piece_hb(t + 2, 1, g >> 1);
-      } else {
-        piece(t + 2, g);
-      }
+      piece(t + 2, g);
       __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (HB) {
-      // K-tile t+1's second half landed for the next k-step-0 reads (issued after it: both
-      // halves of K-tile t+2), and this k-step's reads of K-tile t+1's first half retired
-      // in every wave: K-tile t+3's first half overwrites them during the next k-step 0
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      ww_barrier();
     }
   };
   ktile(0, std::true_type{});
@@ -458,27 +348,15 @@ bool wgrad4w_supported(int64_t T, int M, int N, int S) {
 
 void wgrad4w(const WgradArgs& a0, hipStream_t st) {
   WgradArgs a = a0;
-  if (a.group_m <= 0) {
-    const char* e = std::getenv("APEX_AMD_W4W_GROUPM");
-    a.group_m = e ? std::max(1, std::atoi(e)) : 4;
-  }
+  // XCD-grouped tile order, 4 m-tiles per group (1 to 16 measured within 3 %, round 5)
+  if (a.group_m <= 0) a.group_m = 4;
   const int grid = (a.M / 256) * (a.N / 256) * a.S;
-  // APEX_AMD_W4W_LAYOUT (read per launch, A/B runs): LDS image of 16-row x 64-byte (0,
-  // default), 8-row x 128-byte (1) or whole-row (2) DMA blocks - within 1-5 % of each other
-  const char* e = std::getenv("APEX_AMD_W4W_LAYOUT");
-  const int lay = e ? std::atoi(e) : 0;
   auto go = [&](auto t0) {
     using TT = decltype(t0);
     if (a.colsum)
-      hipLaunchKernelGGL((wgrad4w_k<TT, 4>), dim3(grid), dim3(kWwT), 0, st, a);
-    else if (lay == 0)
-      hipLaunchKernelGGL((wgrad4w_k<TT, 0>), dim3(grid), dim3(kWwT), 0, st, a);
-    else if (lay == 3)
-      hipLaunchKernelGGL((wgrad4w_k<TT, 3>), dim3(grid), dim3(kWwT), 0, st, a);
-    else if (lay == 2)
-      hipLaunchKernelGGL((wgrad4w_k<TT, 2>), dim3(grid), dim3(kWwT), 0, st, a);
+      hipLaunchKernelGGL((wgrad4w_k<TT, true>), dim3(grid), dim3(kWwT), 0, st, a);
     else
-      hipLaunchKernelGGL((wgrad4w_k<TT, 1>), dim3(grid), dim3(kWwT), 0, st, a);
+      hipLaunchKernelGGL((wgrad4w_k<TT, false>), dim3(grid), dim3(kWwT), 0, st, a);
   };
   if (a.fp16) go(half_t{});
   else go(bf16_t{});

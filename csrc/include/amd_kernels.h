@@ -285,9 +285,9 @@ struct WgradArgs {
   int rows;     // rows of A / B per split (T / S)
   int S;
   int fp16;
-  int group_m;  // <= 0: default (APEX_AMD_W4W_GROUPM or 4)
+  int group_m;  // <= 0: default (4)
   float* colsum = nullptr;  // optional [S][M]: column sums of A per split (the bias gradient
-                            // of dY, formed from the MFMA fragments; layout 0 only)
+                            // of dY, formed from the MFMA fragments)
 };
 bool wgrad4w_supported(int64_t T, int M, int N, int S);
 void wgrad4w(const WgradArgs& a, hipStream_t st);
@@ -319,7 +319,6 @@ struct ConvBnEpi {
   const float* w;        // [C] or null (relu_mode 2)
   const float* b;        // [C] or null (relu_mode 2)
   int relu_mode;
-  int diag;              // timing experiments only: bit 0 = do not read x (sums are wrong)
   int add_s2;            // 1: `add` is COMPACT [N][H/2][W/2][C] and lands on the even
                          // (h, w) pixels only (a stride-2 1x1 downsample's input gradient)
 };

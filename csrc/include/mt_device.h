@@ -57,19 +57,11 @@ static inline void dispatch1(DType a, F&& f) {
 
 static inline dim3 mt_grid(const MTLaunch& L) { return dim3((unsigned)L.nchunks); }
 
-// Persistent grid for the optimizer kernels: min(#chunks, CUs x WGs-per-CU)
-// workgroups walk the chunk list with a grid stride, so a 3,000-chunk step is
-// not a full wave of workgroups plus a half-empty second one (the tail of a
-// non-persistent launch), and each workgroup's descriptor fetch is paid once
-// per several tiles of streaming.  APEX_AMD_MT_WGS_PER_CU overrides (0 = one
-// workgroup per chunk).
-int mt_persistent_wgs_per_cu();
+// Grid of the optimizer kernels (which walk the chunk list with a grid stride): one
+// workgroup per chunk.  A persistent grid of CUs x {1, 2, 3, 4, 8} workgroups measured
+// slower for SGD / Adam (tools/microbench.py optim, profiles/microbench_mb_optim.txt);
+// the sweep knob was removed in round 6.
 int device_cu_count();
-static inline dim3 mt_pgrid(const MTLaunch& L) {
-  const int per = mt_persistent_wgs_per_cu();
-  if (per <= 0) return mt_grid(L);
-  const long cap = (long)device_cu_count() * per;
-  return dim3((unsigned)(L.nchunks < cap ? L.nchunks : cap));
-}
+static inline dim3 mt_pgrid(const MTLaunch& L) { return mt_grid(L); }
 
 }  // namespace amd

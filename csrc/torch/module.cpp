@@ -45,30 +45,6 @@ static std::vector<at::Tensor> unflatten_dense(const at::Tensor& flat,
   return out;
 }
 
-// A HIP stream whose kernels may run on a subset of the CUs (hipExtStreamCreateWithCUMask):
-// `quarters` of every 4 CUs (1..3), chosen so that each XCD gets the same share whether the
-// driver numbers CUs XCD-major (cu / 32) or XCD-interleaved (cu % 8): CU i is in the mask
-// when ((i % 8) + (i / 32)) % 4 < quarters.  The stream lives for the process (returned as
-// a handle for torch.cuda.ExternalStream).  Used to confine the weight-gradient side
-// stream to part of the chip (CU partitioning instead of competing for every CU).
-static int64_t cu_masked_stream(int64_t device, int64_t quarters) {
-  TORCH_CHECK(quarters >= 1 && quarters <= 3, "cu_masked_stream: quarters in 1..3");
-  int prev = 0;
-  TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice");
-  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice");
-  hipDeviceProp_t prop;
-  TORCH_CHECK(hipGetDeviceProperties(&prop, (int)device) == hipSuccess, "hipGetDeviceProperties");
-  const int ncu = prop.multiProcessorCount;
-  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i)
-    if (((i % 8) + (i / 32)) % 4 < quarters) mask[(size_t)i / 32] |= 1u << (i % 32);
-  hipStream_t st = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
-  (void)hipSetDevice(prev);
-  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
-  return (int64_t)(intptr_t)st;
-}
-
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native kernels for apex_example_amd (gfx950)";
   m.attr("arch") = "gfx950";
@@ -112,7 +88,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mt.def("plan_cache_clear", &mt_plan_cache_clear);
   mt.def("plan_cache_size", &mt_plan_cache_size);
 
-  m.def("cu_masked_stream", &cu_masked_stream, py::arg("device"), py::arg("quarters"));
   auto ac = m.def_submodule("apex_C", "flatten / unflatten (apex_C parity)");
   ac.def("flatten", &flatten_dense);
   ac.def("unflatten", &unflatten_dense);

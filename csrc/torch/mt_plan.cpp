@@ -255,11 +255,7 @@ MTPlan mt_plan(const TensorLists& lists) {
       c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None;
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
 
-  static const bool percall = [] {
-    const char* e = std::getenv("APEX_AMD_MT_PERCALL");  // 0: every list enters the cache (A/B)
-    return !(e && e[0] == '0');
-  }();
-  if (percall && !capturing && !seen().check_and_add(key) && ring().ok()) {
+  if (!capturing && !seen().check_and_add(key) && ring().ok()) {
     // First sighting of these addresses: chunk list from the size-keyed cache, the
     // tensor table uploaded for this call only (nothing enters the address cache).
     Key skey;

@@ -185,11 +185,6 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
   ep.b = vecf(bn_b, "bias");
   TORCH_CHECK(ep.mean && ep.invstd, "conv_bnbwd: mean / invstd required");
   ep.relu_mode = (int)relu_mode;
-  static const int diag = [] {
-    const char* e = std::getenv("APEX_AMD_BNBWD_DIAG");  // timing experiments only
-    return e ? std::atoi(e) : 0;
-  }();
-  ep.diag = diag;
   if (relu_mode == 1) {
     TORCH_CHECK(rmask.has_value() && rmask->defined() && rmask->is_cuda() &&
                     rmask->scalar_type() == at::kByte && rmask->is_contiguous() &&

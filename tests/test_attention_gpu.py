@@ -154,24 +154,6 @@ def test_attn_bwd_deterministic():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("S,causal,p", [(512, False, 0.1), (200, True, 0.0), (320, False, 0.0)])
-def test_attn_tile_addressing_variants_bitwise(S, causal, p, monkeypatch):
-    """Scalar tile bases + 32-bit lane offsets (default) vs per-lane 64-bit DMA
-    addresses (APEX_AMD_ATTN_ADDR64=1, read per launch): the same bytes reach LDS, so
-    O / lse / dQ / dK / dV must be bitwise equal (packed qkv strides, ragged S)."""
-    q, k, v = _qkv(2, S, 3, torch.bfloat16)
-    do = torch.randn(2, S, 3, 64, device=DEV, dtype=torch.bfloat16)
-    outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("APEX_AMD_ATTN_ADDR64", flag)
-        o, lse = _C().fwd(q, k, v, causal, p, 99, 0.125)
-        dq, dk, dv = (torch.empty(2, S, 3, 64, device=DEV, dtype=torch.bfloat16) for _ in range(3))
-        _C().bwd(do, q, k, v, o, lse, causal, p, 99, 0.125, dq, dk, dv)
-        outs.append((o, lse, dq, dk, dv))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
 def test_bert_layer_fused_attention_matches_sdpa():
     from apex_example_amd.models.bert import BertConfig, BertLayer
 

@@ -271,35 +271,23 @@ def test_stride2_block_compact_downsample_gradient(monkeypatch):
         assert err < 2e-2, (i, err)
 
 
-# K-loop / tiling variants of conv_tap_k selected per launch by environment (A/B switches
-# and the auto choice): all accumulate the same products in the same k order, so every
-# variant must be bitwise equal to the default - plain forward, forward with the BN
-# statistics epilogue, and the BN-backward epilogue (with and without a residual add)
-_VARIANTS = [
-    {"APEX_AMD_CONV_BK32": "1"},                    # 32-deep ring on every 128-wide grid
-    {"APEX_AMD_CONV_BK32": "0", "APEX_AMD_CONV_BK32_64": "0"},  # the 64-deep rings only
-    {"APEX_AMD_CONV_BURST": "0"},                   # read-ahead + interleaved DMA pieces
-    {"APEX_AMD_CONV_BM": "256w8"},                  # 8-wave one-barrier pipeline
-    {"APEX_AMD_CONV_BM": "bk32"},                   # 32-deep, 4-deep ring
-    {"APEX_AMD_CONV_PIPE": "1"},                    # pipelined 4-deep ring (32-deep forms)
-    {"APEX_AMD_CONV_PIPE": "1", "APEX_AMD_CONV_BK32": "1"},  # ... on every 128-wide grid
-    {"APEX_AMD_BNBWD_BM64": "1"},                   # 64-row tiles for BN-bwd 1x1 dgrads
-    {"APEX_AMD_BNBWD_BM64": "0"},                   # ... off
-    {"APEX_AMD_FWD1_BM64": "1"},                    # 64-row tiles for plain 1x1 convs
-]
-
-
-@pytest.mark.parametrize("variant", range(len(_VARIANTS)))
+# The launch-time tilings of conv_tap_k (launch_conv_tap): 32- vs 64-deep K-tiles by grid
+# size, 64-wide tiles, the ring-free 1x1 form, 64-row tiles for the large BN-backward 1x1
+# dgrads, partial last tiles.  Every output against fp32 (the plain forward), the
+# statistics slab against fp32 channel sums of the bf16 output, and every output bitwise
+# stable across calls.  (The per-launch A/B variants these shapes once compared were
+# removed in round 6.)
 @pytest.mark.parametrize("shape", [
     # (N, C_in, H, W, C_out, k)
-    (2, 128, 14, 14, 128, 3),
-    (3, 64, 28, 28, 64, 3),
+    (2, 128, 14, 14, 128, 3),    # 128-wide, small grid: 64-deep 2-deep ring
+    (8, 128, 28, 28, 128, 3),    # 128-wide, >= 1024 workgroups: 32-deep 3-deep ring
+    (3, 64, 28, 28, 64, 3),      # 64-wide tiles
     (2, 256, 7, 7, 512, 1),
-    (3, 128, 9, 11, 256, 3),    # M = 297: partial last tile
+    (2, 64, 28, 28, 256, 1),     # one K-tile: the ring-free 1x1 form
+    (3, 128, 9, 11, 256, 3),     # M = 297: partial last tile
     (1, 128, 224, 226, 256, 1),  # M = 50,624: the 64-row BN-bwd tiles (last tile partial)
-    (4, 64, 224, 226, 128, 1),   # M = 202,496: the 64-row plain 1x1 tiles
 ])
-def test_conv_variants_bitwise_equal(shape, variant, monkeypatch):
+def test_conv_tilings_vs_fp32_and_stable(shape):
     N, Ci, H, W, Co, k = shape
     C = _C()
     torch.manual_seed(1)
@@ -319,19 +307,14 @@ def test_conv_variants_bitwise_equal(shape, variant, monkeypatch):
         g1, s1 = C.conv.conv_fwd_bnbwd(x, wt, add, xb, None, mean, invstd, bw, bb, 2)
         return [y, ys, slab, g0, s0, g1, s1]
 
-    ref = [t.clone() for t in run()]
-    for kk, v in _VARIANTS[variant].items():
-        monkeypatch.setenv(kk, v)
-    got = run()
-    for i, (a, b) in enumerate(zip(ref, got)):
-        if i in (2, 4, 6) and (a.shape != b.shape or
-                               _VARIANTS[variant].get("APEX_AMD_CONV_BM") == "256w8" or
-                               "APEX_AMD_BNBWD_BM64" in _VARIANTS[variant] or
-                               "APEX_AMD_FWD1_BM64" in _VARIANTS[variant]):
-            # statistics slabs hold one row pair per M tile, summed over the tile's row
-            # groups: the 8-wave 256-row tiling has half the rows and twice the row
-            # groups, so only the per-channel totals compare (fp32 summation order)
-            torch.testing.assert_close(a.double().sum(0), b.double().sum(0), rtol=1e-5,
-                                       atol=1e-3)
-            continue
+    first = run()
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), padding=k // 2)
+    err = float((first[0].float() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2, err
+    assert torch.equal(first[0], first[1])
+    yv = first[1].float() - shift.view(1, -1, 1, 1)
+    sums = first[2].double().view(-1, 2, Co).sum(0)
+    torch.testing.assert_close(sums[0], yv.double().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(sums[1], (yv.double() ** 2).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    for i, (a, b) in enumerate(zip(first, run())):
         assert torch.equal(a, b), i

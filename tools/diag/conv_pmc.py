@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Run ONE implicit-GEMM conv shape many times (for rocprofv3 --pmc passes): 3x3 forward
-of `--c` channels at `--hw`, tiling `--variant` (APEX_AMD_CONV_BM), or the 64-channel
-weight gradient (`--wgrad algo`)."""
+of `--c` channels at `--hw`, or the 3x3 weight gradient (`--wgrad algo`)."""
 import argparse
 import os
 import sys
@@ -15,12 +14,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--c", type=int, default=128)
     ap.add_argument("--hw", type=int, default=28)
-    ap.add_argument("--variant", default="default")
     ap.add_argument("--wgrad", type=int, default=-1)
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
-    if a.variant != "default":
-        os.environ["APEX_AMD_CONV_BM"] = a.variant
     from apex_example_amd import _native
 
     cv = _native.require().conv

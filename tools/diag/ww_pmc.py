@@ -27,9 +27,7 @@ def main():
     x = torch.randn(a.t, a.n, device="cuda", generator=g).to(torch.bfloat16)
     s = a.splits
     for _ in range(a.iters):
-        for lay in (0, 1):
-            os.environ["APEX_AMD_W4W_LAYOUT"] = str(lay)
-            dn.wgrad4w(dy, x, s, torch.bfloat16)
+        dn.wgrad4w(dy, x, s, torch.bfloat16)
         torch.bmm(dy.view(s, a.t // s, a.m).transpose(1, 2), x.view(s, a.t // s, a.n),
                   out_dtype=torch.float32)
     torch.cuda.synchronize()

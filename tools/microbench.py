@@ -94,136 +94,6 @@ R50_BN = {(256, 64, 112, 112): 1, (256, 64, 56, 56): 6, (256, 256, 56, 56): 4,
           (256, 512, 14, 14): 1, (256, 512, 7, 7): 5, (256, 2048, 7, 7): 4}
 
 
-def bench_bn_u(args):
-    """A/B of the rows-in-flight unroll of the read-only BN reductions (stats_k,
-    reduce_k) via APEX_AMD_BN_U: per-shape us and the ResNet-50-weighted total."""
-    import os
-
-    from apex_example_amd import _native
-
-    C_ = _native.require().bn
-    dev = "cuda"
-    variants = ["4,2", "8,2", "4,4", "8,4"]
-    tot = {v: [0.0, 0.0] for v in variants}
-    print("| shape | count | " + " | ".join("stats/reduce U=%s" % v for v in variants) + " |")
-    print("|---|---|" + "---|" * len(variants))
-    for (n, c, h, w), cnt in R50_BN.items():
-        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        dy, z = torch.randn_like(x), torch.randn_like(x)
-        wt, bs = torch.ones(c, device=dev), torch.zeros(c, device=dev)
-        mean, var = C_.local_stats(x)
-        invstd = (var + 1e-5).rsqrt()
-        row = []
-        for v in variants:
-            os.environ["APEX_AMD_BN_U"] = v
-            ts = timeit(lambda: C_.local_stats(x))
-            tr = timeit(lambda: C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True))
-            tot[v][0] += cnt * ts
-            tot[v][1] += cnt * tr
-            row.append("%.0f / %.0f" % (ts, tr))
-        print("| %s | %d | %s |" % ((n, c, h, w), cnt, " | ".join(row)), flush=True)
-    os.environ.pop("APEX_AMD_BN_U", None)
-    print("| R50-weighted total us | | " + " | ".join(
-        "%.0f / %.0f" % tuple(tot[v]) for v in variants) + " |")
-
-
-def bench_bn_persist(args):
-    """A/B of the one-launch persistent BatchNorm (bn_persist.hip) against the split
-    kernels, per ResNet-50 shape: forward_local + backward_local for the BN+ReLU
-    variant (bn1/bn2) and the BN+residual+ReLU+mask variant (bn3), in us."""
-    from apex_example_amd import _native
-
-    C_ = _native.require().bn
-    dev = "cuda"
-    modes = (0, 1, 2)  # split kernels / persistent / persistent without barrier fences
-    shapes = R50_BN if not args.quick else {k: v for k, v in R50_BN.items() if k[2] <= 14}
-    print("modes per cell: split / persistent / persistent without fences (us)")
-    print("| shape | count | fwd relu | bwd relu | fwd z+mask | bwd mask |")
-    print("|---|---|---|---|---|---|")
-    tot = [0.0, 0.0]
-    for (n, c, h, w), cnt in shapes.items():
-        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        dy, z = torch.randn_like(x), torch.randn_like(x)
-        wt, bs = torch.ones(c, device=dev), torch.zeros(c, device=dev)
-        rm, rv = torch.zeros(c, device=dev), torch.ones(c, device=dev)
-        row = []
-        for variant in ("relu", "mask"):
-            zz = z if variant == "mask" else None
-            for phase in ("fwd", "bwd"):
-                ts = []
-                for on in modes:
-                    C_.persist_enable(on)
-                    y, mean, invstd, mask = C_.forward_local(x, wt, bs, rm, rv, None, 1e-5, 0.1,
-                                                             zz, True, variant == "mask")
-                    if phase == "fwd":
-                        fn = lambda: C_.forward_local(x, wt, bs, rm, rv, None, 1e-5, 0.1, zz,
-                                                      True, variant == "mask")
-                    else:
-                        fn = lambda: C_.backward_local(dy, x, mean, invstd, wt, bs, None, True,
-                                                       True, variant == "mask", mask=mask)
-                    ts.append(timeit(fn))
-                row.append(" / ".join("%.0f" % t for t in ts))
-                w8 = cnt if variant == "relu" else 0
-                tot[0] += w8 * ts[0]
-                tot[1] += w8 * min(ts[1:])
-        C_.persist_enable(1)
-        print("| %s | %d | %s |" % ((n, c, h, w), cnt, " | ".join(row)), flush=True)
-    print("R50-weighted BN+ReLU fwd+bwd (count x relu variant): split %.0f us, best persistent %.0f us"
-          % tuple(tot))
-    print("persist barrier error word:", C_.persist_error())
-
-
-def bench_bn_eu(args):
-    """Elementwise BN passes (apply_k with residual + ReLU, backward_k) per shape over
-    rows-in-flight U (APEX_AMD_BN_EU) x rows per thread (elem_rpt): per-shape us, the
-    best config per shape and the ResNet-50-weighted totals of the default vs the
-    per-shape best."""
-    from apex_example_amd import _native
-
-    C_ = _native.require().bn
-    dev = "cuda"
-    default = C_.get_tuning()
-    cfgs = [(u, r) for u in (2, 4) for r in (4, 8, 16, 32)]
-    tot_def = tot_best = tot_auto = 0.0
-    print("| shape | count | " + " | ".join("U%d r%d" % c for c in cfgs) + " | auto | best |")
-    print("|---|---|" + "---|" * (len(cfgs) + 2))
-    for (n, c, h, w), cnt in R50_BN.items():
-        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        dy, z = torch.randn_like(x), torch.randn_like(x)
-        wt, bs = torch.ones(c, device=dev), torch.zeros(c, device=dev)
-        mean, var = C_.local_stats(x)
-        invstd = (var + 1e-5).rsqrt()
-        s1, s2, _, _ = C_.reduce_grad(dy, x, mean, invstd, wt, bs, z, True, True)
-        row, res = [], {}
-        for (u, r) in cfgs:
-            os.environ["APEX_AMD_BN_EU"] = str(u)
-            C_.set_tuning(elem_rpt=r)
-            ta = timeit(lambda: C_.apply(x, mean, invstd, wt, bs, z, True))
-            tb = timeit(lambda: C_.backward_elemt(dy, x, mean, invstd, wt, bs, s1, s2,
-                                                  float(n * h * w), z, True, True))
-            res[(u, r)] = ta + tb
-            row.append("%.0f+%.0f" % (ta, tb))
-        C_.set_tuning(elem_rpt=0)  # the per-shape rule (bn_nhwc.hip elem_rpt_for)
-        os.environ["APEX_AMD_BN_EU"] = "2"
-        t_auto = (timeit(lambda: C_.apply(x, mean, invstd, wt, bs, z, True))
-                  + timeit(lambda: C_.backward_elemt(dy, x, mean, invstd, wt, bs, s1, s2,
-                                                     float(n * h * w), z, True, True)))
-        tot_auto += cnt * t_auto
-        row.append("%.0f" % t_auto)
-        best = min(res, key=res.get)
-        tot_def += cnt * res[(2, default[3])] if (2, default[3]) in res else 0.0
-        tot_best += cnt * res[best]
-        print("| %s | %d | %s | U%d r%d |" % ((n, c, h, w), cnt, " | ".join(row), *best),
-              flush=True)
-    os.environ.pop("APEX_AMD_BN_EU", None)
-    C_.set_tuning(elem_rpt=default[3])
-    print("R50-weighted apply+backward: fixed U2 r%d %.0f us, per-shape rule %.0f us, "
-          "per-shape best %.0f us" % (default[3], tot_def, tot_auto, tot_best))
-
-
 def bench_bn_tune(args):
     """Sweep the NHWC BN grid-sizing knobs; report the ResNet-50-weighted total
     (forward stats+finalize+apply, backward reduce+finalize+elementwise) per config."""
@@ -529,54 +399,6 @@ def bench_wgrad(args):
             n, ci, co, hw, gf, t_cw, gf / (t_cw * 1e-6) / 1e3, " | ".join(cells)), flush=True)
 
 
-def bench_conv_bm(args):
-    """M-tile A/B of the MFMA implicit-GEMM conv (APEX_AMD_CONV_BM = 128 | 256 | 256x3):
-    3x3 forward and stride-1 data gradient at ResNet-50's 128+ channel shapes, plus
-    the 1x1 forward shapes that run on the own kernel."""
-    import os
-
-    from apex_example_amd import _native
-    from apex_example_amd.ops.conv import _rot_weight
-
-    cv = _native.require().conv
-    dev = "cuda"
-    variants = ["128", "128x3", "256", "256x3"]
-    print("| conv | GFLOP | " + " | ".join("BM=%s" % v for v in variants) + " | max diff |")
-    print("|---|---|" + "---|" * len(variants) + "---|")
-    cases = []
-    for (n, c, k, hw) in [(256, 128, 128, 28), (256, 256, 256, 14), (256, 512, 512, 7)]:
-        x = torch.randn(n, c, hw, hw, device=dev, dtype=torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        w = (torch.randn(k, c, 3, 3, device=dev) * 0.05).to(torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        dy = torch.randn(n, k, hw, hw, device=dev, dtype=torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        wr = _rot_weight(w)
-        gf = 2 * n * hw * hw * c * k * 9 / 1e9
-        cases.append(("3x3 fwd %d,%d,%d,%d" % (n, c, k, hw), gf, lambda x=x, w=w: cv.conv_fwd(x, w)))
-        cases.append(("3x3 dgrad %d,%d,%d,%d" % (n, k, c, hw), gf,
-                      lambda dy=dy, wr=wr: cv.conv_fwd(dy, wr)))
-    for (n, ci, co, hw) in [(256, 256, 128, 28), (256, 512, 128, 28), (256, 512, 2048, 7),
-                            (256, 1024, 256, 14)]:
-        x = torch.randn(n, ci, hw, hw, device=dev, dtype=torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        w = (torch.randn(co, ci, 1, 1, device=dev) * 0.05).to(torch.bfloat16).to(
-            memory_format=torch.channels_last)
-        gf = 2 * n * hw * hw * ci * co / 1e9
-        cases.append(("1x1 fwd %d,%d,%d,%d" % (n, ci, co, hw), gf,
-                      lambda x=x, w=w: cv.conv_fwd(x, w, 1)))
-    for name, gf, fn in cases:
-        row, outs = [], []
-        for v in variants:
-            os.environ["APEX_AMD_CONV_BM"] = v
-            t = timeit(fn)
-            outs.append(fn().float())
-            row.append("%.0f us (%.0f TF)" % (t, gf / (t * 1e-6) / 1e3))
-        d = max(float((o - outs[0]).abs().max()) for o in outs[1:])
-        print("| %s | %.1f | %s | %.3g |" % (name, gf, " | ".join(row), d), flush=True)
-    os.environ.pop("APEX_AMD_CONV_BM", None)
-
-
 def bench_conv3x3(args):
     """3x3 stride-1 convs of ResNet-50: MIOpen vs the MFMA implicit-GEMM kernel."""
     from apex_example_amd import _native
@@ -678,17 +500,6 @@ def bench_attn(args):
         q, k, v = (torch.randn(b, s_, h, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
                    for _ in range(3))
         do = torch.randn(b, s_, h, d, device=dev, dtype=torch.bfloat16)
-        # APEX_AMD_ATTN_BASE=1: round-1 kernels (block order, eager rescale, per-lane
-        # dropout hashes); APEX_AMD_ATTN_FWD=2: the software-pipelined forward - both
-        # read per launch, so every variant runs in this process
-        variants = [("gfx950/base", {"APEX_AMD_ATTN_BASE": "1"}), ("gfx950", {}),
-                    ("gfx950/fwd2", {"APEX_AMD_ATTN_FWD": "2"}),
-                    ("gfx950/dq-il0", {"APEX_AMD_ATTN_DQ_IL": "0"}),
-                    ("gfx950/addr64", {"APEX_AMD_ATTN_ADDR64": "1"})]
-        if args.quick:
-            variants = variants[1:]
-        keys = ("APEX_AMD_ATTN_BASE", "APEX_AMD_ATTN_FWD", "APEX_AMD_ATTN_DQ_IL",
-                "APEX_AMD_ATTN_ADDR64")
         # ~2 s of untimed calls first: without it the first variant timed read 10 %
         # slower than the same kernels later in the process (clock / first-use ramp)
         A = _native.require().attn
@@ -700,10 +511,7 @@ def bench_attn(args):
                 A.fwd(q, k, v, causal, 0.1, 1234, 1.0 / d ** 0.5)
                 A.bwd(do, q, k, v, o, lse, causal, 0.1, 1234, 1.0 / d ** 0.5, dq, dk, dv)
             torch.cuda.synchronize()
-        for vname, env in variants:
-            for key in keys:
-                os.environ.pop(key, None)
-            os.environ.update(env)
+        for vname in ("gfx950",):
             for p in (0.0, 0.1):  # training runs use attention dropout 0.1
                 # the native calls themselves (the autograd engine adds a ~80 us host floor
                 # per backward call that hid the kernels; round-4 fix of the committed
@@ -720,10 +528,6 @@ def bench_attn(args):
                 print("%-12s %-12s p=%.1f fwd %.0f us (%.0f TF)  bwd %.0f us (%.0f TF)" % (
                     vname, name, p, tf_,
                     fl / (tf_ * 1e-6) / 1e12, tb, 2.5 * fl / (tb * 1e-6) / 1e12), flush=True)
-        for key in keys:
-            os.environ.pop(key, None)
-    if args.quick:
-        return
     for lib in ("default", "ck"):
         try:
             torch.backends.cuda.preferred_rocm_fa_library(lib)
@@ -750,10 +554,7 @@ def bench_attn(args):
 
 def bench_optim(args):
     """Optimizer-kernel bandwidth on ResNet-50's 161 tensors, straight through
-    amp_C (no Python optimizer bookkeeping in the loop), swept over the
-    persistent-grid size APEX_AMD_MT_WGS_PER_CU (0 = one workgroup per chunk)."""
-    import os
-
+    amp_C (no Python optimizer bookkeeping in the loop)."""
     from apex_example_amd import amp_C
     from apex_example_amd.models import resnet50
     from apex_example_amd.optimizers import FusedAdam, FusedSGD
@@ -779,16 +580,12 @@ def bench_optim(args):
             0, noop, [g32, ps, mom, v], 1e-3, 0.9, 0.999, 1e-6, 1, True, 0.01, True, 1,
             torch.ones(1, device=dev), 1.0)),
     ]
-    print("| kernel | B/param | " + " | ".join("wgs/CU=%s" % w for w in args.wgs) + " |")
-    print("|---|---|" + "---|" * len(args.wgs))
+    print("| kernel | B/param | time |")
+    print("|---|---|---|")
     for name, bpp, fn in cases:
-        row = []
-        for w in args.wgs:
-            os.environ["APEX_AMD_MT_WGS_PER_CU"] = str(w)
-            t = timeit(fn, iters=50, warmup=5)
-            row.append("%.1f us %.2f TB/s" % (t, bpp * n / (t * 1e-6) / 1e12))
-        print("| %s | %d | %s |" % (name, bpp, " | ".join(row)), flush=True)
-    os.environ.pop("APEX_AMD_MT_WGS_PER_CU", None)
+        t = timeit(fn, iters=50, warmup=5)
+        print("| %s | %d | %.1f us %.2f TB/s |" % (name, bpp, t, bpp * n / (t * 1e-6) / 1e12),
+              flush=True)
     # whole optimizer.step() (Python bookkeeping included) vs torch's fused optimizers
     for p_, g_ in zip(ps, g32):
         p_.grad = g_
@@ -870,9 +667,8 @@ def bench_ln_join(args):
                                                 retain_graph=True))
         fb = rows * n2 * (4 + 2 + 4 + 2)
         bb = rows * n2 * (4 + 2 + 4 + 4 + 2)
-        print("| %dx%d | %.1f | %.1f us (%.2f TB/s) | %.1f us (%.2f TB/s) | %s |" % (
-            rows, n2, p, tf, fb / tf / 1e6, tb, bb / tb / 1e6,
-            os.environ.get("APEX_AMD_LN_BWD_BLOCKS", "default")), flush=True)
+        print("| %dx%d | %.1f | %.1f us (%.2f TB/s) | %.1f us (%.2f TB/s) |" % (
+            rows, n2, p, tf, fb / tf / 1e6, tb, bb / tb / 1e6), flush=True)
 
 
 def bench_conv_bnbwd(args):
@@ -969,8 +765,7 @@ def bench_lamb(args):
 def bench_conv1x1_stats(args):
     """Channel-expanding / reducing 1x1 conv forward feeding a BatchNorm: hipBLASLt GEMM
     + the BN statistics pass vs the own MFMA kernel writing the statistics in its
-    epilogue (conv_fwd_stats + the slab finalize), and the own kernel alone.  Run with
-    APEX_AMD_CONV1X1_NB1=0/1/2 for the no-ring variant (read per launch)."""
+    epilogue (conv_fwd_stats + the slab finalize), and the own kernel alone."""
     from apex_example_amd import _native
 
     C = _native.require()
@@ -1016,13 +811,10 @@ def bench_conv1x1_stats(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["bn", "bn-persist", "bn-eu", "bn-tune", "bn-u", "conv-bm", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "ln-join", "conv-bnbwd", "lamb",
+    ap.add_argument("what", choices=["bn", "bn-tune", "conv1x1", "conv1x1-own", "conv1x1-stats", "wgrad", "wgrad-o1", "wgrad-dense", "conv3x3", "conv-s2", "optim", "ln", "ln-join", "conv-bnbwd", "lamb",
                              "attn"])
-    ap.add_argument("--quick", action="store_true", help="bn-persist: 14x14 / 7x7 shapes only")
-    ap.add_argument("--wgs", type=int, nargs="+", default=[0, 1, 2, 3, 4, 8],
-                    help="optim: persistent workgroups per CU to sweep (0 = one per chunk)")
     a = ap.parse_args()
-    {"bn": bench_bn, "bn-persist": bench_bn_persist, "bn-eu": bench_bn_eu, "bn-tune": bench_bn_tune, "bn-u": bench_bn_u, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv1x1-stats": bench_conv1x1_stats, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "conv-bm": bench_conv_bm, "optim": bench_optim,
+    {"bn": bench_bn, "bn-tune": bench_bn_tune, "conv1x1": bench_conv1x1, "conv1x1-own": bench_conv1x1_own, "conv1x1-stats": bench_conv1x1_stats, "wgrad-o1": bench_wgrad_o1, "wgrad-dense": bench_wgrad_dense, "optim": bench_optim,
      "ln": bench_ln, "ln-join": bench_ln_join, "conv-bnbwd": bench_conv_bnbwd, "lamb": bench_lamb, "wgrad": bench_wgrad,
      "conv3x3": bench_conv3x3, "conv-s2": bench_conv_s2, "attn": bench_attn}[a.what](a)
 

@@ -156,13 +156,9 @@ def dense(args, cv, forced):
                 cands["S=%d" % s] = ((lambda s=s: forced(dy, x, s)) if s > 1
                                      else (lambda: dy.t() @ x))
         dn = _native_dense()
-        def own(s, lay):
-            os.environ["APEX_AMD_W4W_LAYOUT"] = str(lay)
-            return dn.wgrad4w(dy, x, s, torch.bfloat16)
         for s in (2, 4, 8):
-            for lay in (0, 1, 2):
-                if dn.wgrad4w_ok(dy, x, s):
-                    cands["wgrad4w L%d S=%d" % (lay, s)] = (lambda s=s, lay=lay: own(s, lay))
+            if dn.wgrad4w_ok(dy, x, s):
+                cands["wgrad4w S=%d" % s] = (lambda s=s: dn.wgrad4w(dy, x, s, torch.bfloat16))
         for k, fn in cands.items():
             err = float((fn().float().reshape(o, i) - ref).abs().max()) / scale
             assert err < 2e-2, (name, k, err)
