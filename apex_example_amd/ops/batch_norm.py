@@ -468,7 +468,7 @@ def take_slab(x, bn):
         return None, None
     del x._amd_bn_stats
     slab, shift, owner = ent
-    if owner is not bn or slab.size(2) != x.size(1):
+    if owner is not bn or slab.size(1) != x.size(1):
         return None, None
     return slab, shift
 

@@ -415,42 +415,84 @@ __global__ void __launch_bounds__(kBNThreads)
 
 
 // ---------------------------------------------------------------- statistics from a
-// producer's epilogue (conv_igemm.hip conv_tap_k with a stats slab): the conv wrote
-// the shifted sums of each M-tile tile-major, slab[S][0|1][C] (one coalesced row per
-// workgroup).  Long slabs are first folded kFoldRows rows at a time (a column per thread,
-// coalesced rows); the final kernel sums the remaining rows per channel in a fixed
-// order and produces what stats_finalize does: mean (+ biased var | invstd),
-// running-stat update, num_batches_tracked += 1.
-// 32 rows per fold workgroup: a 6,272-tile slab (56x56 layers at bs 256) folds in ~200
-// workgroups of 8 four-load chains instead of 49 of 32 chains (~15 -> ~5 us per fold,
-// `profiles/resnet50_o2_serial_r3.md`; the finalize then sums <= 200 rows per channel)
-constexpr int kFoldRows = 32;
+// producer's epilogue (conv_igemm.hip conv_tap_k with a stats slab): the conv wrote the
+// shifted sums of each M-tile channel-major, slab[0|1][C][S].  ONE finalize launch sums
+// each channel's S tile sums - a contiguous row - with TPC = 256 / CH threads per channel
+// (CH channels per workgroup, chosen so each thread adds ~16 values with its loads in
+// flight), fixed-order tree in LDS, and produces what stats_finalize does (mean, biased
+// var | invstd, running stats, num_batches_tracked += 1) or, for a BN-backward slab,
+// what reduce_finalize does.  Round 6: this replaced a fold kernel (32 tile rows at a
+// time) + a finalize kernel over the tile-major [S][2][C] layout: ~10 us and two
+// launches per BatchNorm on ResNet-50's 56 x 56 layers (profiles/r5/serial/).
+constexpr int kSlabPerThread = 16;
 
-__global__ void __launch_bounds__(kBNThreads)
-    slab_fold_k(const float* __restrict__ slab, int S, int C2, float* __restrict__ out) {
-  const int col = blockIdx.x * kBNThreads + threadIdx.x;
-  if (col >= C2) return;
-  const int r0 = blockIdx.y * kFoldRows;
-  const int r1 = r0 + kFoldRows < S ? r0 + kFoldRows : S;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int r = r0;
-  for (; r + 4 <= r1; r += 4) {
-    a0 += slab[(int64_t)r * C2 + col];
-    a1 += slab[(int64_t)(r + 1) * C2 + col];
-    a2 += slab[(int64_t)(r + 2) * C2 + col];
-    a3 += slab[(int64_t)(r + 3) * C2 + col];
+static int slab_ch(int S) {
+  int ch = 1;
+  while (ch < 32 && (int64_t)S * ch * 2 <= (int64_t)kBNThreads * kSlabPerThread) ch *= 2;
+  return ch;
+}
+
+// (sum of row 0 of channel c, sum of row 1) for the CH channels of this workgroup, into
+// out[2 * CH] (LDS); TPC threads per channel, each summing a strided subset in 4 chains
+template <int CH>
+__device__ __forceinline__ void slab_t_sum(const float* __restrict__ slab, int S, int C, int c0,
+                                           float* out) {
+  constexpr int TPC = kBNThreads / CH;
+  __shared__ float red[2][kBNThreads];
+  const int k = threadIdx.x / TPC, t = threadIdx.x - k * TPC;
+  const int c = c0 + k;
+  // 8 chains per row: 16 independent loads in flight per thread (the 64-row-tile slabs
+  // of the 56 x 56 BN-backward convs hold S = 12,544 sums per channel)
+  float a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = b[u] = 0.f;
+  if (c < C) {
+    const float* r0 = slab + (int64_t)c * S;
+    const float* r1 = slab + (int64_t)(C + c) * S;
+    int s = t;
+    for (; s + 7 * TPC < S; s += 8 * TPC) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        va[u] = r0[s + u * TPC];
+        vb[u] = r1[s + u * TPC];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] += va[u];
+        b[u] += vb[u];
+      }
+    }
+    for (; s < S; s += TPC) {
+      a[0] += r0[s];
+      b[0] += r1[s];
+    }
   }
-  for (; r < r1; ++r) a0 += slab[(int64_t)r * C2 + col];
-  out[(int64_t)blockIdx.y * C2 + col] = (a0 + a1) + (a2 + a3);
+  red[0][threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  red[1][threadIdx.x] = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
+  __syncthreads();
+#pragma unroll
+  for (int w = TPC / 2; w > 0; w >>= 1) {
+    if (t < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out[k] = red[0][threadIdx.x];
+    out[CH + k] = red[1][threadIdx.x];
+  }
+  __syncthreads();
 }
 
 template <int CH>
 __global__ void __launch_bounds__(kBNThreads)
-    stats_from_rows_k(const float* __restrict__ slab, int S, int C, int64_t count,
-                      const float* __restrict__ shift, BNStatsOut out) {
+    slab_stats_k(const float* __restrict__ slab, int S, int C, int64_t count,
+                 const float* __restrict__ shift, BNStatsOut out) {
   __shared__ float sums[2 * CH];
   const int c0 = blockIdx.x * CH;
-  slab_sum<CH>(slab, S, C, c0, sums);
+  slab_t_sum<CH>(slab, S, C, c0, sums);
   const int k = threadIdx.x;
   if (k < CH && c0 + k < C) {
     const int c = c0 + k;
@@ -469,6 +511,40 @@ __global__ void __launch_bounds__(kBNThreads)
     }
     if (out.nbt && c == 0) *out.nbt += 1;
     if (out.count_out && c == 0) *out.count_out = out.count_val;
+  }
+}
+
+template <typename TW, int CH>
+__global__ void __launch_bounds__(kBNThreads)
+    slab_reduce_k(const float* __restrict__ slab, int S, int C, const float* __restrict__ invstd,
+                  float* __restrict__ sum_dy, float* __restrict__ sum_dy_xmu, TW* __restrict__ gw,
+                  TW* __restrict__ gb, const float* __restrict__ sum_scale, int accum) {
+  __shared__ float sums[2 * CH];
+  const int c0 = blockIdx.x * CH;
+  slab_t_sum<CH>(slab, S, C, c0, sums);
+  const int k = threadIdx.x;
+  if (k < CH && c0 + k < C) {
+    const int c = c0 + k;
+    const float s1 = sums[k], s2 = sums[CH + k];
+    // SyncBN: the sums leave pre-divided by the global count (device scalar)
+    const float sc = sum_scale ? *sum_scale : 1.f;
+    sum_dy[c] = s1 * sc;
+    sum_dy_xmu[c] = s2 * sc;
+    // accum: add into existing gradients (DDP bucket views) instead of overwriting
+    if (gw) gw[c] = from_f32<TW>(s2 * invstd[c] + (accum ? to_f32(gw[c]) : 0.f));
+    if (gb) gb[c] = from_f32<TW>(s1 + (accum ? to_f32(gb[c]) : 0.f));
+  }
+}
+
+template <typename F>
+static void slab_ch_dispatch(int S, F&& f) {
+  switch (slab_ch(S)) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 16: f(std::integral_constant<int, 16>{}); break;
+    default: f(std::integral_constant<int, 32>{}); break;
   }
 }
 
@@ -504,32 +580,18 @@ void bn_get_tuning(int* o) {
 
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec) { return reduce_splits(M, ngeom(C, vec)); }
 
-int64_t bn_slab_workspace(int S, int64_t C) {
-  return S > 2 * kFoldRows ? (int64_t)((S + kFoldRows - 1) / kFoldRows) * 2 * C : 0;
-}
-
 void bn_stats_from_slab(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                        const BNStatsOut& out, float* ws, hipStream_t st) {
-  const float* rows = slab;
-  int R = S;
-  if (S > 2 * kFoldRows) {  // fold kFoldRows rows at a time first
-    R = (S + kFoldRows - 1) / kFoldRows;
-    const int C2 = (int)(2 * C);
-    hipLaunchKernelGGL(slab_fold_k, dim3((unsigned)((C2 + kBNThreads - 1) / kBNThreads),
-                                         (unsigned)R),
-                       dim3(kBNThreads), 0, st, slab, S, C2, ws);
-    rows = ws;
-  }
-  fin_dispatch(C, [&](auto ch) {
+                        const BNStatsOut& out, hipStream_t st) {
+  slab_ch_dispatch(S, [&](auto ch) {
     constexpr int CH = decltype(ch)::value;
-    hipLaunchKernelGGL((stats_from_rows_k<CH>), dim3((unsigned)((C + CH - 1) / CH)),
-                       dim3(kBNThreads), 0, st, rows, R, (int)C, count, shift, out);
+    hipLaunchKernelGGL((slab_stats_k<CH>), dim3((unsigned)((C + CH - 1) / CH)), dim3(kBNThreads),
+                       0, st, slab, S, (int)C, count, shift, out);
   });
 }
 
 void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
                          float* mean, float* invstd, float* running_mean, float* running_var,
-                         long long* nbt, float eps, float momentum, float* ws, hipStream_t st) {
+                         long long* nbt, float eps, float momentum, hipStream_t st) {
   BNStatsOut o{};
   o.mean = mean;
   o.var = nullptr;
@@ -539,40 +601,34 @@ void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, con
   o.nbt = nbt;
   o.eps = eps;
   o.momentum = momentum;
-  bn_stats_from_slab(slab, S, C, count, shift, o, ws, st);
+  bn_stats_from_slab(slab, S, C, count, shift, o, st);
 }
 
 void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                          float* packed, float* ws, hipStream_t st) {
+                          float* packed, hipStream_t st) {
   BNStatsOut o{};
   o.mean = packed;
   o.var = packed + C;
   o.invstd = nullptr;
   o.count_out = packed + 2 * C;
   o.count_val = (float)count;
-  bn_stats_from_slab(slab, S, C, count, shift, o, ws, st);
+  bn_stats_from_slab(slab, S, C, count, shift, o, st);
 }
 
 // BN backward sums from a data-gradient conv's epilogue (conv_nhwc_fwd_bnbwd): the slab
-// [S][2][C] holds per-M-tile (sum g, sum g*(x-mean)) - the layout reduce_k's partials
-// have - so after the 128-row fold of long slabs the usual reduce finalize applies.
+// [2][C][S] holds per-M-tile (sum g, sum g*(x-mean)) channel-major
 void bn_slab_reduce_grad(const float* slab, int S, int64_t C, const float* invstd,
                          float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, DType tw,
-                         float* ws, hipStream_t st, const float* sum_scale) {
-  const float* rows = slab;
-  int R = S;
-  if (S > 2 * kFoldRows) {
-    R = (S + kFoldRows - 1) / kFoldRows;
-    const int C2 = (int)(2 * C);
-    hipLaunchKernelGGL(slab_fold_k, dim3((unsigned)((C2 + kBNThreads - 1) / kBNThreads),
-                                         (unsigned)R),
-                       dim3(kBNThreads), 0, st, slab, S, C2, ws);
-    rows = ws;
-  }
+                         hipStream_t st, const float* sum_scale) {
   bn_dispatch(tw, [&](auto w0) {
     using TW = decltype(w0);
-    launch_reduce_finalize<TW>(rows, R, C, invstd, sum_dy, sum_dy_xmu, static_cast<TW*>(gw),
-                               static_cast<TW*>(gb), st, sum_scale);
+    slab_ch_dispatch(S, [&](auto ch) {
+      constexpr int CH = decltype(ch)::value;
+      hipLaunchKernelGGL((slab_reduce_k<TW, CH>), dim3((unsigned)((C + CH - 1) / CH)),
+                         dim3(kBNThreads), 0, st, slab, S, (int)C, invstd, sum_dy, sum_dy_xmu,
+                         static_cast<TW*>(gw), static_cast<TW*>(gb), sum_scale,
+                         bn_grad_accumulate() ? 1 : 0);
+    });
   });
 }
 

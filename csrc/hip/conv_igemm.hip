@@ -522,7 +522,8 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
   // column group (kCT % CPR == 0), so the bf16-ROUNDED values it stores (exactly what
   // y holds) also feed its per-channel shifted sums sum(v - s), sum((v - s)^2) with
   // s = that BN's running mean; the row groups are combined through LDS and written
-  // tile-major, slab[m-tile][0|1][c], for the finalize kernels (fixed order).
+  // channel-major, slab[0|1][c][m-tile]: the finalize kernel then reads each channel's
+  // S tile sums as one contiguous row (one coalesced pass, no fold kernel; fixed order).
   float s1[8], s2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
@@ -575,11 +576,12 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
         a += red[q * BN + tid];
         b += red[RGS * BN + q * BN + tid];
       }
-      // tile-major [S][2][C]: one coalesced row segment per workgroup (the parity
-      // classes of a stride-2 dgrad, blockIdx.z, own rows after the M tiles)
-      float* row = slab + ((int64_t)z * gridDim.x + mt) * 2 * g.NC;
-      row[n0 + tid] = a;
-      row[g.NC + n0 + tid] = b;
+      // channel-major [2][C][S] (S = M tiles x parity classes, blockIdx.z after the M
+      // tiles): consecutive M tiles run on one XCD, so its L2 merges the 4-byte stores of
+      // neighbouring workgroups into whole lines
+      const int64_t S = (int64_t)gridDim.x * gridDim.z, s = (int64_t)z * gridDim.x + mt;
+      slab[(int64_t)(n0 + tid) * S + s] = a;
+      slab[(int64_t)(g.NC + n0 + tid) * S + s] = b;
     }
   }
 }

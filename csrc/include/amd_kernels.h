@@ -307,7 +307,7 @@ int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize);
 // BatchNorm-backward epilogue of a data-gradient conv (conv_nhwc_fwd on dY with the
 // rotated / transposed filter): the conv output o (+ add, the residual gradient) is
 // the gradient of a BN(+ReLU) output; the kernel stores g = relu_mask(x) * o instead
-// and writes that BN's per-M-tile sums [S][2][C]: sum(g), sum(g * (x - mean)).
+// and writes that BN's per-M-tile sums [2][C][S]: sum(g), sum(g * (x - mean)).
 // relu_mode 0: no ReLU; 1: bitmask rmask [M][C/8] from the forward; 2: recompute
 // x * invstd * w + (b - mean * invstd * w) > 0 (w, b fp32 or null = 1 / 0).
 struct ConvBnEpi {
@@ -327,15 +327,14 @@ void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* g, int N, int H, i
                          hipStream_t st);
 // BatchNorm statistics from such a slab: local training mode (mean, invstd, running
 // stats, num_batches_tracked) or SyncBN's packed [mean | biased var | count]
-// (slab is tile-major [S][2][C]; ws: bn_slab_workspace(S, C) floats, may be 0)
-int64_t bn_slab_workspace(int S, int64_t C);
+// (slab is channel-major [2][C][S]: one launch, no workspace)
 void bn_slab_train_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
                          float* mean, float* invstd, float* running_mean, float* running_var,
-                         long long* nbt, float eps, float momentum, float* ws, hipStream_t st);
+                         long long* nbt, float eps, float momentum, hipStream_t st);
 void bn_slab_packed_stats(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                          float* packed, float* ws, hipStream_t st);
+                          float* packed, hipStream_t st);
 // BN backward sums (sum_dy, sum_dy_xmu [* sum_scale], dgamma, dbeta) from a
-// conv_nhwc_fwd_bnbwd slab; ws: bn_slab_workspace(S, C) floats
+// conv_nhwc_fwd_bnbwd slab [2][C][S]
 // Host-side switch read when the BN backward finalize is launched (this thread): dgamma /
 // dbeta ACCUMULATE into the caller's gradient buffers - DDP bucket views - instead of
 // being written fresh, saving autograd's two add kernels per BatchNorm (BNAccumScope)
@@ -348,7 +347,7 @@ struct BNAccumScope {
 };
 void bn_slab_reduce_grad(const float* slab, int S, int64_t C, const float* invstd,
                          float* sum_dy, float* sum_dy_xmu, void* gw, void* gb, DType tw,
-                         float* ws, hipStream_t st, const float* sum_scale = nullptr);
+                         hipStream_t st, const float* sum_scale = nullptr);
 // data gradient of a stride-2 conv (H, W even); wt = rotated 3x3 filter / W^T for 1x1
 void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, int W, int Cin,
                         int Cout, int ksize, hipStream_t st);

@@ -200,11 +200,10 @@ struct BNTuning {
 };
 BNTuning& bn_tuning();
 int64_t nhwc_splits(int64_t M, int64_t C, bool vec);
-// statistics from a tile-major slab of per-tile shifted sums [S][2][C] written by a
-// producer kernel's epilogue (conv_igemm.hip); shift may be null (0); ws: workspace of
-// bn_slab_workspace(S, C) floats
+// statistics from a channel-major slab of per-tile shifted sums [2][C][S] written by a
+// producer kernel's epilogue (conv_igemm.hip); shift may be null (0)
 void bn_stats_from_slab(const float* slab, int S, int64_t C, int64_t count, const float* shift,
-                        const BNStatsOut& out, float* ws, hipStream_t st);
+                        const BNStatsOut& out, hipStream_t st);
 void nhwc_stats(const void* x, DType tx, int64_t M, int64_t C, const BNStatsOut& out, float* ws,
                 hipStream_t st);
 // rmask: optional ReLU bitmask [M][C/8] (apply writes it when the VEC path runs,

@@ -637,10 +637,10 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
                                                           OptT running_var, OptT nbt,
                                                           double eps, double momentum) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
+  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(0) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
-              "bn slab stats: fp32 [S][2][C] slab expected");
-  const int64_t S = slab.size(0), C = slab.size(2);
+              "bn slab stats: fp32 [2][C][S] slab expected");
+  const int64_t S = slab.size(2), C = slab.size(1);
   auto f32 = [&](const OptT& t, const char* what) -> float* {
     if (!has(t)) return nullptr;
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C &&
@@ -658,10 +658,9 @@ std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64
   }
   auto fopt = slab.options();
   at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
-  at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, fopt);
   bn_slab_train_stats(slab.data_ptr<float>(), (int)S, C, count, sp, mean.data_ptr<float>(),
                       invstd.data_ptr<float>(), rm, rv, nb, (float)eps, (float)momentum,
-                      ws.data_ptr<float>(), cur_stream());
+                      cur_stream());
   return {mean, invstd};
 }
 
@@ -669,10 +668,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_o
     at::Tensor slab, at::Tensor invstd, OptT weight, bool need_wgrad, OptT sum_scale,
     OptT gw_in, OptT gb_in, bool accumulate) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
+  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(0) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
-              "bn slab reduce: fp32 [S][2][C] slab expected");
-  const int64_t S = slab.size(0), C = slab.size(2);
+              "bn slab reduce: fp32 [2][C][S] slab expected");
+  const int64_t S = slab.size(2), C = slab.size(1);
   TORCH_CHECK(invstd.is_cuda() && invstd.scalar_type() == at::kFloat && invstd.numel() == C,
               "bn slab reduce: invstd must be fp32 [C]");
   auto fopt = slab.options();
@@ -690,20 +689,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_slab_reduce_grad_o
                 "bn slab reduce: sum_scale must be a 1-element fp32 GPU tensor");
     scale = sum_scale->data_ptr<float>();
   }
-  at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, fopt);
   bn_slab_reduce_grad(slab.data_ptr<float>(), (int)S, C, invstd.contiguous().data_ptr<float>(),
                       sum_dy.data_ptr<float>(), sum_dy_xmu.data_ptr<float>(),
                       gw.defined() ? gw.data_ptr() : nullptr, gb.defined() ? gb.data_ptr() : nullptr,
-                      tw, ws.data_ptr<float>(), cur_stream(), scale);
+                      tw, cur_stream(), scale);
   return {sum_dy, sum_dy_xmu, gw, gb};
 }
 
 at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift, OptT out) {
   c10::NoGradGuard no_grad_;
-  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(1) == 2 &&
+  TORCH_CHECK(slab.is_cuda() && slab.dim() == 3 && slab.size(0) == 2 &&
                   slab.scalar_type() == at::kFloat && slab.is_contiguous(),
-              "bn slab stats: fp32 [S][2][C] slab expected");
-  const int64_t S = slab.size(0), C = slab.size(2);
+              "bn slab stats: fp32 [2][C][S] slab expected");
+  const int64_t S = slab.size(2), C = slab.size(1);
   const float* sp = nullptr;
   if (has(shift)) {
     TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
@@ -712,9 +710,8 @@ at::Tensor bn_slab_packed_stats_op(at::Tensor slab, int64_t count, OptT shift, O
     sp = shift->data_ptr<float>();
   }
   at::Tensor packed = packed_out(out, C, slab.options());
-  at::Tensor ws = at::empty({std::max<int64_t>(bn_slab_workspace((int)S, C), 1)}, slab.options());
   bn_slab_packed_stats(slab.data_ptr<float>(), (int)S, C, count, sp, packed.data_ptr<float>(),
-                       ws.data_ptr<float>(), cur_stream());
+                       cur_stream());
   return packed;
 }
 

@@ -75,7 +75,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
     OptT z, bool relu, bool need_wgrad, bool want_dz, OptT mask);
 
-// BatchNorm statistics from a producer's tile-major stats slab [S][2][C]
+// BatchNorm statistics from a producer's channel-major stats slab [2][C][S]
 // (conv.conv_fwd_stats): local training mode -> (mean, invstd) with the running-stat
 // and num_batches_tracked updates; packed mode -> [mean | biased var | count] (SyncBN)
 std::tuple<at::Tensor, at::Tensor> bn_slab_train_stats_op(at::Tensor slab, int64_t count,

@@ -122,7 +122,7 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tens
   at::Tensor y = at::empty({N, Cout, Ho, Wo},
                            x.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int S = conv_fwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)stride, (int)k);
-  at::Tensor slab = at::empty({S, 2, Cout}, x.options().dtype(at::kFloat));
+  at::Tensor slab = at::empty({2, Cout, S}, x.options().dtype(at::kFloat));
   conv_nhwc_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)Cin,
                 (int)Cout, (int)k, (int)stride, cur_stream(), slab.data_ptr<float>(), sp);
   return {y, slab};
@@ -130,7 +130,7 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tens
 
 // Stride-1 data-gradient conv (dy with the rotated 3x3 / transposed 1x1 filter) whose
 // output is the gradient of a BN(+ReLU) output: stores g = relu_mask * (conv + add) and
-// returns it with that BN's per-M-tile backward sums [S][2][C] (ConvBnEpi).
+// returns it with that BN's per-M-tile backward sums [2][C][S] (ConvBnEpi).
 std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
     at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> add, at::Tensor xbn,
     c10::optional<at::Tensor> rmask, at::Tensor mean, at::Tensor invstd,
@@ -196,7 +196,7 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
   w = w.contiguous(cl);
   at::Tensor g = at::empty({N, Cout, H, W}, dy.options().memory_format(cl));
   const int S = conv_bnbwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)k);
-  at::Tensor slab = at::empty({S, 2, Cout}, dy.options().dtype(at::kFloat));
+  at::Tensor slab = at::empty({2, Cout, S}, dy.options().dtype(at::kFloat));
   conv_nhwc_fwd_bnbwd(dy.data_ptr(), w.data_ptr(), g.data_ptr(), (int)N, (int)H, (int)W,
                       (int)Cin, (int)Cout, (int)k, 1, ep, slab.data_ptr<float>(), cur_stream());
   return {g, slab};

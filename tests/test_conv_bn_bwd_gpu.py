@@ -36,6 +36,7 @@ def _bf(t):
     (2, 128, 14, 14, 128, 3),
     (4, 64, 56, 56, 256, 1),     # expanding 1x1 dgrad (bottleneck conv1 <- previous bn3)
     (3, 256, 14, 14, 64, 1),     # M = 588: partial last tile
+    (16, 64, 56, 56, 256, 1),    # M = 50,176: 64-row tiles, S = 784
 ])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("with_add", [False, True])
@@ -71,7 +72,7 @@ def test_bnbwd_epilogue_matches_reference(shape, mode, with_add):
     ref = torch.where(keep, ref, torch.zeros_like(ref))
     ok = ~border
     torch.testing.assert_close(g.float()[ok], ref[ok], rtol=0, atol=0)
-    sums = slab.double().sum(0)                      # [2][C]
+    sums = slab.double().sum(2)                      # [2][C]
     gd = g.double().permute(0, 2, 3, 1).reshape(-1, Co)
     xd = x.double().permute(0, 2, 3, 1).reshape(-1, Co)
     torch.testing.assert_close(sums[0], gd.sum(0), rtol=1e-5, atol=1e-3)
@@ -313,7 +314,7 @@ def test_conv_tilings_vs_fp32_and_stable(shape):
     assert err < 1e-2, err
     assert torch.equal(first[0], first[1])
     yv = first[1].float() - shift.view(1, -1, 1, 1)
-    sums = first[2].double().view(-1, 2, Co).sum(0)
+    sums = first[2].double().view(2, Co, -1).sum(2)
     torch.testing.assert_close(sums[0], yv.double().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(sums[1], (yv.double() ** 2).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     for i, (a, b) in enumerate(zip(first, run())):

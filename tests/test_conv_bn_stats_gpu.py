@@ -25,6 +25,7 @@ def _C():
     (4, 64, 56, 56, 256, 1, 1),    # channel-expanding 1x1
     (2, 256, 28, 28, 512, 1, 2),   # strided 1x1 projection
     (1, 512, 7, 7, 2048, 1, 1),    # M = 49 < one tile
+    (96, 64, 56, 56, 64, 1, 1),    # S = 2,352 tiles: one channel per finalize workgroup
 ])
 @pytest.mark.parametrize("use_shift", [False, True])
 def test_conv_epilogue_stats_match_reference(shape, use_shift):
