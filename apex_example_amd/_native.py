@@ -27,6 +27,11 @@ def _load():
         _C = importlib.import_module("apex_example_amd._C")
     except Exception as e:  # pragma: no cover - exercised only without a build
         _err = e
+    else:
+        # 3x3 stride-1 convs on the halo-resident kernel (csrc/hip/conv_igemm.hip conv3h_k):
+        # APEX_AMD_CONV_HALO = 0 off, 1 automatic (default), 64 / 128 force that tile width
+        # (A/B switch, docs/KNOBS.md)
+        _C.conv.set_halo(int(os.environ.get("APEX_AMD_CONV_HALO", "1")))
     return _C
 
 

@@ -21,6 +21,7 @@
 // writes lane-linearly), so the 16 rows a ds_read_b128 lane group touches land
 // in distinct bank slots.  Workgroups are remapped so consecutive M tiles
 // (which share input rows through the 3x3 halo) run on one XCD's L2.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -623,6 +624,341 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   }
+}
+
+// ============================================================================
+// 3x3 / stride-1 / pad-1 forward with the input HALO resident in LDS (conv3h_k).
+//
+// conv_tap_k loads a fresh 128-pixel A tile for every (tap, channel slice): 9 loads of
+// nearly the same pixels per slice, one 1 KiB LDS-DMA piece per 8 rows - and a DMA piece
+// costs ~60 issue cycles among the MFMAs (MI355X_MICROARCH.md), so at 128 x 128 tiles the
+// piece stream alone is about as long as the MFMA stream (PMC: 23-28 % MFMA busy, 41 % of
+// wave cycles waiting to issue, profiles/r6/conv_pmc).  Here a workgroup's 256 output
+// pixels are consecutive in raster order, and in the zero-PADDED raster (row width
+// Wp = W + 2, two zero rows between images) the input a tap (r, s) needs for output pixel
+// p is at padded position P(p) + (r - 1) Wp + (s - 1): every tap reads one contiguous
+// window of R = P(last) - P(first) + 2 Wp + 3 padded rows.  That window (<= 448 rows x
+// 32 channels) is DMA'd ONCE per 32-channel slice and the nine taps read their A
+// fragments from it at a wave-uniform row shift; only the weights stream per tap.  Pieces
+// per MFMA drop ~3x (128@28: 9 x 32 pieces per slice per 128 x 128 tile -> 28 + 9 x 8 per
+// 256 x 128 tile).
+//
+// LDS images are row-major, 64 bytes (32 channels) per row, with the (row >> 2) & 1 chunk
+// swizzle of conv_tap_k's 64-byte rows - conflict-free for 16 consecutive rows at ANY
+// alignment, which the tap shifts need (the row jumps at image-row ends still cost some
+// 2-way conflicts: 5.7 LDS cycles per fragment read at W = 28 vs 4 ideal, 8 at W <= 14).
+// A DMA wave-instruction fills 16 rows x 4 chunks, so it touches 16 cache lines (a
+// planar layout - lane l -> row l of one chunk plane - touched 64, and ran no faster
+// than conv_tap_k: the address/tag work, not the piece count, bounded it).  Halo rows
+// that are padding or past the window carry an out-of-range buffer offset, which the
+// buffer load returns as zeros.
+//
+// Pipeline (per 32-channel slice c, taps t = 0..8 = K-steps k = 9 c + t): the weights of
+// step k go to ring slot k % 3 two steps ahead; the next slice's halo goes to the other
+// halo buffer in piece pairs during taps 0-3.  One counted vmcnt wait + one barrier per
+// step.  80 KiB of LDS: two workgroups per CU, so one's barrier / DMA issue hides under
+// the other's MFMAs.  Tile 256 x BN (4 waves of 128 x 64 for BN = 128, 64 x 64 for 64).
+constexpr int kHBM = 256;                  // output pixels per workgroup
+// halo rows per buffer: 448 (7 DMA row blocks, 28 KiB) next to the 128-wide weight ring,
+// 512 (32 KiB) next to the 64-wide one - either way 80 KiB in all
+constexpr int halo_rows(int BN) { return BN == 128 ? 448 : 512; }
+constexpr uint32_t kHZero = 0x80000000u;   // out-of-range offset: the DMA writes zeros
+
+__device__ __forceinline__ int halo_ppos(int p, int H, int W, int HW) {
+  const int n = p / HW, r = p - n * HW;
+  const int h = r / W, w = r - h * W;
+  return (n * (H + 2) + h + 1) * (W + 2) + w + 1;
+}
+
+// buffer load of 16 bytes per lane straight into LDS (lane l -> l * 16 from dst).  A
+// __device__ wrapper: with the builtin called in the kernel body on per-lane offsets the
+// HIP host pass dropped the kernel's launch stub without a diagnostic (link error)
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, unsigned char* dst,
+                                          uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16,
+                                           voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+  }
+}
+
+template <int BN, int EPI>
+__global__ void __launch_bounds__(kCT, 2)
+    conv3h_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
+             bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
+             const float* __restrict__ shift, ConvBnEpi ep) {
+  constexpr int BM = kHBM, CT = kCT, WM = BN == 128 ? 2 : 4, WN = 4 / WM;
+  constexpr int kHRows = halo_rows(BN), kHBuf = kHRows * 64;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int BSLOT = BN * 64;           // BN weight rows x 32 channels
+  constexpr int BPW = BN / 64;             // weight pieces (16 rows each) per wave per step
+  constexpr int NHP = kHRows / 64;         // halo pieces per wave per slice (7 | 8)
+  constexpr int RING = 2 * kHBuf + 3 * BSLOT;
+  constexpr int EPI_BYTES = BM * BN * 2;
+  constexpr int LDS_BYTES = RING > EPI_BYTES ? RING : EPI_BYTES;
+  static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
+  unsigned char* const hbuf = lds;
+  unsigned char* const bring = lds + 2 * kHBuf;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int mt = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = mt * BM, n0 = blockIdx.y * BN;
+  const int H = g.GH, W = g.GW, HW = H * W, Wp = W + 2, HpWp = (H + 2) * Wp;
+  const int M = g.M, KC = g.KC;
+  const int p1 = min(m0 + BM, M) - 1;
+  const int base = halo_ppos(m0, H, W, HW) - Wp - 1;   // padded position of halo row 0
+  const int pend = halo_ppos(p1, H, W, HW) + Wp + 1;   // of the last halo row (host-checked)
+  const int lrow = lane >> 2, pch = lane & 3;          // DMA: row in the piece, stored chunk
+
+  // halo DMA: wave w fills row blocks w, w + 4, ... (16 rows each); the descriptor starts
+  // at the window's first image so the 32-bit offsets stay small
+  const int64_t pix0 = (int64_t)(base / HpWp) * HW;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(x + pix0 * KC), 0, 0x7fffffff, 0x00020000);
+  uint32_t hoff[NHP];
+#pragma unroll
+  for (int u = 0; u < NHP; ++u) {
+    const int row = (wid + 4 * u) * 16 + lrow;
+    const int q = base + row;
+    const int n = q / HpWp, rr = q - n * HpWp;
+    const int hp = rr / Wp, wp = rr - hp * Wp;
+    const bool ok = q <= pend && hp >= 1 && hp <= H && wp >= 1 && wp <= W;
+    const int64_t pix = (int64_t)(n * H + hp - 1) * W + wp - 1 - pix0;
+    hoff[u] = ok ? (uint32_t)(pix * KC * 2) + (uint32_t)((pch ^ swz_key<64>(row)) * 16) : kHZero;
+  }
+  // weight DMA: wave w fills weight row blocks w * BPW .. + BPW - 1
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(wt + (int64_t)n0 * g.kb_stride), 0, 0x7fffffff, 0x00020000);
+  uint32_t woff[BPW];
+#pragma unroll
+  for (int u = 0; u < BPW; ++u) {
+    const int row = (wid * BPW + u) * 16 + lrow;
+    woff[u] = (uint32_t)(row * g.kb_stride * 2) + (uint32_t)((pch ^ swz_key<64>(row)) * 16);
+  }
+
+  const int nch = KC / 32, K = 9 * nch;
+  // halo pieces 2t, 2t + 1 of slice c, with constant register indices (a runtime index
+  // put hoff in scratch)
+#define HALO_PIECE(c_, u_) \
+  buf_lds16(rx, hbuf + ((c_) & 1) * kHBuf + (wid + 4 * (u_)) * 1024, hoff[u_], (c_) * 64)
+#define HALO_PIECES(c_, t_)                                                                 \
+  switch (t_) {                                                                             \
+    case 0: HALO_PIECE(c_, 0); HALO_PIECE(c_, 1); break;                                    \
+    case 1: HALO_PIECE(c_, 2); HALO_PIECE(c_, 3); break;                                    \
+    case 2: HALO_PIECE(c_, 4); HALO_PIECE(c_, 5); break;                                    \
+    default: HALO_PIECE(c_, 6); if (NHP > 7) HALO_PIECE(c_, NHP - 1); break;                \
+  }
+#define W_PIECES(k_)                                                                        \
+  {                                                                                         \
+    const int c_ = (k_) / 9, t_ = (k_) - c_ * 9;                                            \
+    _Pragma("unroll") for (int u = 0; u < BPW; ++u)                                         \
+      buf_lds16(rw, bring + ((k_) % 3) * BSLOT + (wid * BPW + u) * 1024, woff[u],           \
+                (t_ * KC + c_ * 32) * 2);                                                   \
+  }
+  // halo pieces of the NEXT slice issued in step k (taps 0-3 of a slice, two per tap)
+  auto hcount = [&](int k) {
+    if (k < 0 || k % 9 >= 4 || k / 9 + 1 >= nch) return 0;
+    const int left = NHP - 2 * (k % 9);
+    return left < 2 ? left : 2;
+  };
+
+  // fragment reads: A row of output pixel m0 + wm*TM + 16 i + fr (past M: the last pixel)
+  // shifted by the tap; B row wn*TN + 16 j + fr; logical chunk fg
+  const int fr = lane & 15, fg = lane >> 4;
+  int arow[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int p = min(m0 + wm * TM + i * 16 + fr, p1);
+    arow[i] = halo_ppos(p, H, W, HW) - base;
+  }
+  const int boff = swzr<64>(wn * TN + fr, fg);
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: slice 0's halo, the weights of steps 0 and 1
+#pragma unroll
+  for (int t = 0; t < 4; ++t) HALO_PIECES(0, t);
+  W_PIECES(0);
+  W_PIECES(1);
+  int c = 0, t = 0;
+  for (int k = 0; k < K; ++k) {
+    // retire step k's weights (and, at t = 0, the slice's halo, issued before them): the
+    // pieces issued after them are step k-2's halo pieces, step k+1's weights and step
+    // k-1's halo pieces
+    vm_wait_n(hcount(k - 2) + (k + 1 < K ? BPW : 0) + hcount(k - 1));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + 2 < K) W_PIECES(k + 2);
+    if (hcount(k)) HALO_PIECES(c + 1, t);
+    const int toff = (t / 3 - 1) * Wp + (t % 3) - 1;
+    const unsigned char* A = hbuf + (c & 1) * kHBuf;
+    const unsigned char* B = bring + (k % 3) * BSLOT + boff;
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(B + j * 1024);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<64>(arow[i] + toff, fg));
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (++t == 9) { t = 0; ++c; }
+  }
+#undef HALO_PIECE
+#undef HALO_PIECES
+#undef W_PIECES
+  // the last step waited vmcnt(0): no DMA in flight
+  __syncthreads();
+  // the statistics shift, loaded only now (held across the loop it cost the registers
+  // the fragment double buffer needs)
+  constexpr int CPR = BN / 8;
+  const bool want_stats = slab != nullptr;
+  const int scc = tid % CPR;
+  float shv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) shv[i] = (EPI == 0 && want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
+
+  // epilogue (as conv_tap_k): accumulators -> bf16 tile in LDS -> coalesced row stores
+  bf16_t* T = reinterpret_cast<bf16_t*>(lds);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * TM + i * 16 + fg * 4 + e;
+        const int col = wn * TN + j * 16 + fr;
+        T[row * BN + col] = (bf16_t)acc[i][j][e];
+      }
+  __syncthreads();
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+  if constexpr (EPI == 1) {
+    // the BN-backward operands are fetched after the accumulators are dead (a 256-row
+    // prefetch held across the tile write would exceed the 2-workgroups-per-CU registers)
+    BnPre<BM, BN, CT> pre;
+    bnbwd_prefetch<kFwd3, BM, BN, CT>(g, ep, m0, n0, 0, pre);
+    bnbwd_store<kFwd3, BM, BN, CT>(T, y, g, ep, m0, n0, 0, pre, s1, s2);
+  } else {
+    for (int q = tid; q < BM * CPR; q += CT) {
+      const int row = q / CPR, cc = q - row * CPR;
+      const int m = m0 + row;
+      if (m >= M) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+      *reinterpret_cast<uint4*>(y + (int64_t)m * g.NC + n0 + cc * 8) = v;
+      if (want_stats) {
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float lo = __uint_as_float(wv[u] << 16) - shv[2 * u];
+          const float hi = __uint_as_float(wv[u] & 0xffff0000u) - shv[2 * u + 1];
+          s1[2 * u] += lo;
+          s2[2 * u] = fmaf(lo, lo, s2[2 * u]);
+          s1[2 * u + 1] += hi;
+          s2[2 * u + 1] = fmaf(hi, hi, s2[2 * u + 1]);
+        }
+      }
+    }
+  }
+  if (want_stats) {
+    constexpr int RGS = CT / CPR;
+    lds_barrier();
+    float* red = reinterpret_cast<float*>(lds);
+    const int rg = tid / CPR;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[rg * BN + scc * 8 + i] = s1[i];
+      red[RGS * BN + rg * BN + scc * 8 + i] = s2[i];
+    }
+    lds_barrier();
+    if (tid < BN) {
+      float a = 0.f, b = 0.f;
+#pragma unroll 4
+      for (int q = 0; q < RGS; ++q) {
+        a += red[q * BN + tid];
+        b += red[RGS * BN + q * BN + tid];
+      }
+      const int64_t S = gridDim.x;
+      slab[(int64_t)(n0 + tid) * S + mt] = a;
+      slab[(int64_t)(g.NC + n0 + tid) * S + mt] = b;
+    }
+  }
+}
+
+// Largest halo window (rows) of any 256-pixel tile of an N x H x W raster, cached per
+// shape (the launch path asks once per conv call).
+int halo_rows_max(int N, int H, int W) {
+  struct Ent { int n, h, w, r; };
+  static Ent cache[16];
+  static int filled = 0;
+  for (int i = 0; i < filled; ++i)
+    if (cache[i].n == N && cache[i].h == H && cache[i].w == W) return cache[i].r;
+  const int64_t M = (int64_t)N * H * W;
+  const int HW = H * W, Wp = W + 2;
+  auto pp = [&](int64_t p) {
+    const int64_t n = p / HW, r = p - n * HW, h = r / W, w = r - h * W;
+    return (n * (H + 2) + h + 1) * Wp + w + 1;
+  };
+  int64_t r = 0;
+  for (int64_t m0 = 0; m0 < M; m0 += kHBM) {
+    const int64_t p1 = std::min<int64_t>(m0 + kHBM, M) - 1;
+    r = std::max<int64_t>(r, pp(p1) - pp(m0) + 2 * Wp + 3);
+  }
+  const int res = (int)std::min<int64_t>(r, 1 << 30);
+  if (filled < 16) cache[filled++] = Ent{N, H, W, res};
+  return res;
+}
+
+// 0: off, 1: automatic tile width, 64 / 128: that width wherever it is possible (A/B)
+int g_conv_halo = 1;
+
+// Output-tile width of the halo kernel for a 3x3 conv, 0 = not eligible: 128 wide where
+// Cout allows and the window fits 448 rows; 64 wide (512-row window) only on grids of
+// >= 1024 pixel tiles - measured (profiles/r6/conv_halo.md, batch 256): 128@28 and
+// 256@14 5-12 % faster than conv_tap_k, 64@56 even to 5 % faster, 512@7 (64 wide: 49
+// pixel tiles) 30 % slower.  (Cin % 64 == 0 is conv3x3_nhwc_supported's.)
+int conv3h_bn(int N, int H, int W, int Cout, int stride) {
+  if (g_conv_halo == 0 || stride != 1 || N <= 0 || Cout % 64 != 0) return 0;
+  const int r = halo_rows_max(N, H, W);
+  const bool w128 = Cout % 128 == 0 && r <= halo_rows(128);
+  const bool w64 = r <= halo_rows(64);
+  const int64_t tiles = ((int64_t)N * H * W + kHBM - 1) / kHBM;
+  if (g_conv_halo == 64 && w64) return 64;
+  if (w128) return 128;
+  return w64 && (g_conv_halo == 64 || tiles >= 1024) ? 64 : 0;
+}
+bool conv3h_ok(int N, int H, int W, int Cout, int stride) {
+  return conv3h_bn(N, H, W, Cout, stride) != 0;
+}
+
+template <int EPI>
+void launch_conv3h(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g, int N,
+                   hipStream_t st, float* slab, const float* shift, const ConvBnEpi& ep) {
+  const int bn = conv3h_bn(N, g.GH, g.GW, g.NC, 1);
+  const dim3 grid((g.M + kHBM - 1) / kHBM, g.NC / bn, 1);
+  if (bn == 128)
+    hipLaunchKernelGGL((conv3h_k<128, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  else
+    hipLaunchKernelGGL((conv3h_k<64, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
 }
 
 // ============================================================================
@@ -1502,11 +1838,13 @@ void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipSt
                      static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out), Cout, Cin, 1);
 }
 
+void conv_halo_enable(int mode) { g_conv_halo = mode; }
+int conv_halo_enabled() { return g_conv_halo; }
+
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t M = (int64_t)N * Ho * Wo;
-  (void)ksize;
-  (void)Cout;
+  if (ksize == 3 && conv3h_ok(N, H, W, Cout, stride)) return (int)((M + kHBM - 1) / kHBM);
   return (int)((M + kBM - 1) / kBM);  // launch_conv_tap's M tile (EPI 0)
 }
 
@@ -1518,7 +1856,9 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
   const auto* xp = static_cast<const bf16_t*>(x);
   const auto* wp = static_cast<const bf16_t*>(w);
   auto* yp = static_cast<bf16_t*>(y);
-  if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st, stats_slab, stats_shift);
+  if (ksize == 3 && conv3h_ok(N, H, W, Cout, stride))
+    launch_conv3h<0>(xp, wp, yp, g, N, st, stats_slab, stats_shift, ConvBnEpi{});
+  else if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st, stats_slab, stats_shift);
   else launch_conv_tap<kFwd1>(xp, wp, yp, g, st, stats_slab, stats_shift);
 }
 
@@ -1526,6 +1866,7 @@ int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize) {
   const int64_t M = (int64_t)N * H * W;
   // launch_conv_tap's M tile with the BN-backward epilogue (64 rows for the large 1x1s)
   if (ksize == 1 && Cout % 128 == 0 && M >= 50176) return (int)((M + 63) / 64);
+  if (ksize == 3 && conv3h_ok(N, H, W, Cout, 1)) return (int)((M + kHBM - 1) / kHBM);
   return (int)((M + kBM - 1) / kBM);
 }
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H, int W, int Cin,
@@ -1536,7 +1877,9 @@ void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H
   const auto* xp = static_cast<const bf16_t*>(dy);
   const auto* wp = static_cast<const bf16_t*>(w);
   auto* yp = static_cast<bf16_t*>(gout);
-  if (ksize == 3) launch_conv_tap<kFwd3, 1>(xp, wp, yp, g, st, slab, nullptr, ep);
+  if (ksize == 3 && stride == 1 && conv3h_ok(N, H, W, Cout, 1))
+    launch_conv3h<1>(xp, wp, yp, g, N, st, slab, nullptr, ep);
+  else if (ksize == 3) launch_conv_tap<kFwd3, 1>(xp, wp, yp, g, st, slab, nullptr, ep);
   else launch_conv_tap<kFwd1, 1>(xp, wp, yp, g, st, slab, nullptr, ep);
 }
 

@@ -295,6 +295,11 @@ void wgrad4w(const WgradArgs& a, hipStream_t st);
 // ---- implicit-GEMM convolutions, NHWC bf16, MFMA (conv_igemm.hip) ----------
 // 3x3 pad 1 or 1x1 pad 0, stride 1 or 2; channel counts multiples of 64
 bool conv3x3_nhwc_supported(int Cin, int Cout);
+// 3x3 stride-1 convs run the halo-resident kernel (conv3h_k) where their window fits,
+// unless disabled here: mode 0 off, 1 automatic, 64 / 128 force that output-tile width
+// where possible (A/B switch; the M tile, hence the stats slab width, follows)
+void conv_halo_enable(int mode);
+int conv_halo_enabled();
 // y is N x Ho x Wo x Cout, Ho = (H-1)/stride + 1; w is [Cout][k*k][Cin]
 // stats_slab (optional, fp32 [conv_fwd_mtiles(...)][2][Cout]): per M-tile shifted sums
 // sum(y - shift[c]), sum((y - shift[c])^2) of the bf16 output for the consuming BN

@@ -155,6 +155,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("rot_weight", &conv3x3_rot_weight_op);
   conv.def("transpose_weight", &conv1x1_transpose_weight_op);
   conv.def("prep_weights", &conv_prep_weights_op);
+  conv.def("set_halo", &conv_halo_enable, py::arg("mode"),
+           "3x3 stride-1 convs on the halo-resident kernel: 0 off, 1 auto, 64 / 128 force "
+           "that output-tile width where possible");
+  conv.def("halo_enabled", &conv_halo_enabled);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);

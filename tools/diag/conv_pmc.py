@@ -16,10 +16,12 @@ def main():
     ap.add_argument("--hw", type=int, default=28)
     ap.add_argument("--wgrad", type=int, default=-1)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--halo", type=int, default=1)
     a = ap.parse_args()
     from apex_example_amd import _native
 
     cv = _native.require().conv
+    cv.set_halo(bool(a.halo))
     g = torch.Generator(device="cuda").manual_seed(0)
     cl = torch.channels_last
     x = torch.randn(256, a.c, a.hw, a.hw, device="cuda", generator=g).to(torch.bfloat16).to(
