@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "amd_dev.h"
 #include "amd_kernels.h"
@@ -679,16 +680,14 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, unsigned cha
                                            voff, soff, 0, 0);
 }
 
-__device__ __forceinline__ void vm_wait_n(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-  }
+// halo pieces of the NEXT slice issued at tap t of a slice (two per tap over taps 0-3)
+constexpr int conv3h_hcount(int t, int nhp) {
+  return t < 0 || t >= 4 ? 0 : (nhp - 2 * t < 2 ? nhp - 2 * t : 2);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_c() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int BN, int EPI>
@@ -748,7 +747,7 @@ __global__ void __launch_bounds__(kCT, 2)
     woff[u] = (uint32_t)(row * g.kb_stride * 2) + (uint32_t)((pch ^ swz_key<64>(row)) * 16);
   }
 
-  const int nch = KC / 32, K = 9 * nch;
+  const int nch = KC / 32;
   // halo pieces 2t, 2t + 1 of slice c, with constant register indices (a runtime index
   // put hoff in scratch)
 #define HALO_PIECE(c_, u_) \
@@ -768,12 +767,6 @@ __global__ void __launch_bounds__(kCT, 2)
                 (t_ * KC + c_ * 32) * 2);                                                   \
   }
   // halo pieces of the NEXT slice issued in step k (taps 0-3 of a slice, two per tap)
-  auto hcount = [&](int k) {
-    if (k < 0 || k % 9 >= 4 || k / 9 + 1 >= nch) return 0;
-    const int left = NHP - 2 * (k % 9);
-    return left < 2 ? left : 2;
-  };
-
   // fragment reads: A row of output pixel m0 + wm*TM + 16 i + fr (past M: the last pixel)
   // shifted by the tap; B row wn*TN + 16 j + fr; logical chunk fg
   const int fr = lane & 15, fg = lane >> 4;
@@ -796,31 +789,59 @@ __global__ void __launch_bounds__(kCT, 2)
   for (int t = 0; t < 4; ++t) HALO_PIECES(0, t);
   W_PIECES(0);
   W_PIECES(1);
-  int c = 0, t = 0;
-  for (int k = 0; k < K; ++k) {
-    // retire step k's weights (and, at t = 0, the slice's halo, issued before them): the
-    // pieces issued after them are step k-2's halo pieces, step k+1's weights and step
-    // k-1's halo pieces
-    vm_wait_n(hcount(k - 2) + (k + 1 < K ? BPW : 0) + hcount(k - 1));
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (k + 2 < K) W_PIECES(k + 2);
-    if (hcount(k)) HALO_PIECES(c + 1, t);
-    const int toff = (t / 3 - 1) * Wp + (t % 3) - 1;
+  // The nine taps of a slice are unrolled (tap index T a compile-time constant): ring slot
+  // (9c + T) % 3 = T % 3, the DMA schedule and every vmcnt count are constants, so a step
+  // carries no scalar bookkeeping or branches beyond `more` (the first build computed
+  // k / 9, k % 3 and the counts per step: 154 SALU + 27 branch instructions per 32 MFMAs).
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;  // a next slice: its halo goes out during taps 0-3
     const unsigned char* A = hbuf + (c & 1) * kHBuf;
-    const unsigned char* B = bring + (k % 3) * BSLOT + boff;
-    bf16x8 af[FM], bfr[FN];
+    auto step = [&](auto tc) {
+      constexpr int T = decltype(tc)::value;
+      // retire this step's weights (and at T = 0 the slice's halo, issued before them):
+      // younger pieces are the halo pieces of steps T-2 and T-1 and the weights of T+1
+      constexpr int HP = conv3h_hcount(T - 2, NHP) + conv3h_hcount(T - 1, NHP);
+      if (more) vm_wait_c<HP + BPW>();
+      else if (T < 8) vm_wait_c<BPW>();
+      else vm_wait_c<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (more || T < 7) {
+        constexpr int T2 = (T + 2) % 9, C2 = (T + 2) / 9;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(B + j * 1024);
+        for (int u = 0; u < BPW; ++u)
+          buf_lds16(rw, bring + ((T + 2) % 3) * BSLOT + (wid * BPW + u) * 1024, woff[u],
+                    (T2 * KC + (c + C2) * 32) * 2);
+      }
+      if constexpr (T < 4) {
+        if (more) HALO_PIECES(c + 1, T);
+      }
+      int toff = (T / 3 - 1) * Wp + (T % 3) - 1;
+      // opaque per step: else the compiler hoists all 9 x FM tap addresses out of the slice
+      // loop (72 live VGPRs, spills)
+      asm volatile("" : "+s"(toff));
+      const unsigned char* B = bring + (T % 3) * BSLOT + boff;
+      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<64>(arow[i] + toff, fg));
+      for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(B + j * 1024);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(A + swzr<64>(arow[i] + toff, fg));
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (++t == 9) { t = 0; ++c; }
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{});
+    step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
   }
 #undef HALO_PIECE
 #undef HALO_PIECES
@@ -932,19 +953,19 @@ int halo_rows_max(int N, int H, int W) {
 int g_conv_halo = 1;
 
 // Output-tile width of the halo kernel for a 3x3 conv, 0 = not eligible: 128 wide where
-// Cout allows and the window fits 448 rows; 64 wide (512-row window) only on grids of
-// >= 1024 pixel tiles - measured (profiles/r6/conv_halo.md, batch 256): 128@28 and
-// 256@14 5-12 % faster than conv_tap_k, 64@56 even to 5 % faster, 512@7 (64 wide: 49
-// pixel tiles) 30 % slower.  (Cin % 64 == 0 is conv3x3_nhwc_supported's.)
+// Cout allows and the window fits 448 rows, else 64 wide (512-row window).  Measured
+// (profiles/r6/conv_halo.md, batch 256, vs conv_tap_k): 128@28 fwd / +stats / +BN-bwd
+// 93 / 97 / 110 -> 85 / 78 / 87 us, 256@14 79 / 82 / 81 -> 63 / 64 / 69, 512@7 (64
+// wide) 75 / 77 / 72 -> 66 / 67 / 69, 64@56 (64 wide) 102 / 110 / 147 -> 79 / 93 / 120.
+// (Cin % 64 == 0 is conv3x3_nhwc_supported's.)
 int conv3h_bn(int N, int H, int W, int Cout, int stride) {
   if (g_conv_halo == 0 || stride != 1 || N <= 0 || Cout % 64 != 0) return 0;
   const int r = halo_rows_max(N, H, W);
   const bool w128 = Cout % 128 == 0 && r <= halo_rows(128);
   const bool w64 = r <= halo_rows(64);
-  const int64_t tiles = ((int64_t)N * H * W + kHBM - 1) / kHBM;
   if (g_conv_halo == 64 && w64) return 64;
   if (w128) return 128;
-  return w64 && (g_conv_halo == 64 || tiles >= 1024) ? 64 : 0;
+  return w64 ? 64 : 0;
 }
 bool conv3h_ok(int N, int H, int W, int Cout, int stride) {
   return conv3h_bn(N, H, W, Cout, stride) != 0;

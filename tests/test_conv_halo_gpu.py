@@ -77,10 +77,8 @@ def test_halo_conv_matches_fp32_and_tap_kernel(shape, mode, halo_switch):
     halo_switch(0)
     t = _run(C, *args)
     assert t[2].shape[2] == (M + 127) // 128
-    # automatic choice: 128-wide tiles where Cout allows, 64-wide only on >= 1024 pixel tiles
-    expect = mode == 64 or Co % 128 == 0
-    tiles = (M + 255) // 256 if expect else (M + 127) // 128
-    assert h[2].shape[2] == tiles, "the halo kernel did not run" if expect else "unexpected halo"
+    tiles = (M + 255) // 256
+    assert h[2].shape[2] == tiles, "the halo kernel did not run"
 
     ref = F.conv2d(x.float(), w.float(), padding=1)
     scale = float(ref.abs().max())
