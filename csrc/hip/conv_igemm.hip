@@ -326,7 +326,7 @@ __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict_
 // BK = 32: 64-byte K-tile rows - half the LDS per ring stage, so a 3-deep ring keeps two
 // stages (32 KB at 128 x 128) in flight with up to 3 workgroups per CU.
 template <int MODE, int BM, int BN, int WM, int WN, int NB, int EPI = 0, int CT = kCT,
-          int BK = kBK>
+          int BK = kBK, bool EARLY = false>
 __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
                                           ? 1 : (NB == 1 && EPI == 0 ? 3 : 2))
     conv_tap_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
@@ -447,6 +447,7 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
   // consumed after barriers that wait for LDS only, so they fly under the accumulator ->
   // LDS tile write instead of being waited for at a __syncthreads()
   BnPre<BM, BN, CT> pre;
+  if constexpr (EPI == 1 && EARLY) bnbwd_prefetch<MODE, BM, BN, CT>(g, ep, m0, n0, z, pre);
 
   {
     // prologue: NB-1 tiles in flight
@@ -495,7 +496,7 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
   // (the K loop ended on a vmcnt(0) wait: no tile DMA is in flight; an LDS-only barrier
   // leaves the epilogue prefetch of EPI == 1 outstanding)
   if constexpr (EPI == 1) {
-    bnbwd_prefetch<MODE, BM, BN, CT>(g, ep, m0, n0, z, pre);
+    if constexpr (!EARLY) bnbwd_prefetch<MODE, BM, BN, CT>(g, ep, m0, n0, z, pre);
     lds_barrier();
   } else {
     __syncthreads();
@@ -603,6 +604,8 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 //    cost more there: 3x3 256@14 82 -> 96 us);
 //  * 64-wide output tiles: 32-deep K-tiles on a 3-deep ring (layer-1 3x3 64@56 fwd
 //    111 -> 106 us, dgrad 103 -> 99 us).
+int g_bnbwd_early = 1;  // BN-backward epilogue prefetch at kernel start for small K (A/B switch)
+
 template <int MODE, int EPI = 0>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
@@ -611,7 +614,13 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
   if (EPI == 1 && MODE == kFwd1 && g.NC % 128 == 0 && g.M >= 50176) {
     const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
-    hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    // K <= 128 (two to four 32-deep K-tiles): the epilogue's loads go out at kernel start
+    // and fly under the K loop's DMA (64 -> 256 @ 56 +skip: 324 -> 307 us, 128 -> 512
+    // @ 28: 176 -> 171; at K = 256 the held registers cost a wave per SIMD: 110 -> 115)
+    if (g_bnbwd_early && g.KC <= 128)
+      hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32, true>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    else
+      hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= 1) {
     const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
@@ -1860,6 +1869,7 @@ void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipSt
 }
 
 void conv_halo_enable(int mode) { g_conv_halo = mode; }
+void conv_bnbwd_early(int mode) { g_bnbwd_early = mode; }
 int conv_halo_enabled() { return g_conv_halo; }
 
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize) {

@@ -300,6 +300,7 @@ bool conv3x3_nhwc_supported(int Cin, int Cout);
 // where possible (A/B switch; the M tile, hence the stats slab width, follows)
 void conv_halo_enable(int mode);
 int conv_halo_enabled();
+void conv_bnbwd_early(int mode);
 // y is N x Ho x Wo x Cout, Ho = (H-1)/stride + 1; w is [Cout][k*k][Cin]
 // stats_slab (optional, fp32 [conv_fwd_mtiles(...)][2][Cout]): per M-tile shifted sums
 // sum(y - shift[c]), sum((y - shift[c])^2) of the bf16 output for the consuming BN

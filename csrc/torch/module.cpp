@@ -159,6 +159,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "3x3 stride-1 convs on the halo-resident kernel: 0 off, 1 auto, 64 / 128 force "
            "that output-tile width where possible");
   conv.def("halo_enabled", &conv_halo_enabled);
+  conv.def("set_bnbwd_early", &conv_bnbwd_early);
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);
