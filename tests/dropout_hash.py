@@ -36,17 +36,17 @@ def thr8(p):
     return 0 if p <= 0 else min(256, max(1, int(p * 256 + 0.5)))
 
 
-def hash_bytes(B, H, S, seed, SK=None):
+def hash_bytes(B, H, S, seed, SK=None, device="cpu"):
     """[B, H, S(q), SK(k)] the byte of each (query, key) score's hash."""
     SK = S if SK is None else SK
-    bh = torch.arange(B * H, dtype=torch.int64).view(B, H, 1, 1)
-    q = torch.arange(S, dtype=torch.int64).view(1, 1, S, 1)
-    key = torch.arange(SK, dtype=torch.int64).view(1, 1, 1, SK)
+    bh = torch.arange(B * H, dtype=torch.int64, device=device).view(B, H, 1, 1)
+    q = torch.arange(S, dtype=torch.int64, device=device).view(1, 1, S, 1)
+    key = torch.arange(SK, dtype=torch.int64, device=device).view(1, 1, 1, SK)
     x = (drop_base(seed, bh) + _mul32(q, K_DROP_Q) + _mul32(key >> 2, K_DROP_K)) & M32
     return (drop_mix(x) >> (8 * (key & 3))) & 0xFF
 
 
-def keep_mask(B, H, S, seed, p):
+def keep_mask(B, H, S, seed, p, device="cpu"):
     """(keep mask [B, H, S, S], scale 1 / (1 - p_quantised))."""
     t = thr8(p)
-    return hash_bytes(B, H, S, seed) >= t, (256.0 / (256 - t) if t < 256 else 0.0)
+    return hash_bytes(B, H, S, seed, device=device) >= t, (256.0 / (256 - t) if t < 256 else 0.0)

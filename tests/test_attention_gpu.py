@@ -34,12 +34,12 @@ def _umul24(x, c):
     return ((x & 0xFFFFFF) * (c & 0xFFFFFF)) & M32
 
 
-def drop_keep_mask(B, H, S, seed, p):
+def drop_keep_mask(B, H, S, seed, p, device="cpu"):
     """[B, H, S(q), S(k)] keep mask of the kernels' hash (int64 torch arithmetic):
     drop_mix(drop_base(seed, bh) + q * kDropQ + (key >> 2) * kDropK), byte (key & 3)
     against round(256 p) (csrc/hip/attention.hip)."""
     from dropout_hash import keep_mask
-    return keep_mask(B, H, S, seed, p)
+    return keep_mask(B, H, S, seed, p, device=device)
 
 
 def ref_attention(q, k, v, causal, p=0.0, seed=0):
@@ -52,8 +52,9 @@ def ref_attention(q, k, v, causal, p=0.0, seed=0):
     lse = torch.logsumexp(s, -1) / math.log(2.0)
     pr = torch.softmax(s, -1)
     if p > 0:
-        keep, scale = drop_keep_mask(B, H, S, seed, p)
-        pr = pr * keep.to(q.device) * scale
+        # the mask mirror runs where the scores are (production shapes: 134 M entries)
+        keep, scale = drop_keep_mask(B, H, S, seed, p, device=q.device)
+        pr = pr * keep * scale
     return (pr @ vf).permute(0, 2, 1, 3), lse
 
 
@@ -193,3 +194,45 @@ def test_contrib_self_mha_fast_matches_default():
     ya.backward(dy)
     yr.backward(dy)
     _close(xa.grad, xr.grad.float(), 3e-2)
+
+
+# ---------------------------------------------------------- production shapes
+# The models' own shapes under the heaviest-first causal tile order and the full dropout
+# path: GPT-2-medium (B 8, S 1024, H 16, causal, fp16 - amp O1) and BERT-large (B 32,
+# S 512, H 16, dropout 0.1, bf16, packed QKV as the model passes it), forward and all three
+# gradients against the fp32 reference (with the kernels' exact keep mask).
+def test_attn_production_gpt2_causal_s1024():
+    from apex_example_amd.ops import fused_attention
+
+    torch.manual_seed(5)
+    B, S, H = 8, 1024, 16
+    q, k, v = (torch.randn(B, S, H, 64, device=DEV, dtype=torch.float16).requires_grad_(True)
+               for _ in range(3))
+    o = fused_attention(q, k, v, causal=True)
+    ro, _ = ref_attention(q.detach(), k.detach(), v.detach(), True)
+    _close(o.detach(), ro, 1e-2)
+    do = torch.randn_like(o)
+    o.backward(do)
+    rq, rk, rv = _ref_grads(q, k, v, do, True)
+    _close(q.grad, rq, 1e-2)
+    _close(k.grad, rk, 1e-2)
+    _close(v.grad, rv, 1e-2)
+
+
+def test_attn_production_bert_dropout_s512():
+    from apex_example_amd.ops.attention import FusedQKVAttentionFunction
+
+    torch.manual_seed(6)
+    B, S, H = 32, 512, 16
+    qkv = torch.randn(B, S, 3, H, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = FusedQKVAttentionFunction.apply(qkv, False, 0.1, 0.125, 777)
+    q, k, v = qkv.detach().unbind(2)
+    ro, _ = ref_attention(q, k, v, False, p=0.1, seed=777)
+    _close(o.detach(), ro, 3e-2)
+    do = torch.randn_like(o)
+    o.backward(do)
+    rq, rk, rv = _ref_grads(q, k, v, do, False, p=0.1, seed=777)
+    g = qkv.grad
+    _close(g[:, :, 0], rq, 3e-2)
+    _close(g[:, :, 1], rk, 3e-2)
+    _close(g[:, :, 2], rv, 3e-2)
