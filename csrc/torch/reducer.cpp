@@ -703,8 +703,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   // fp32 mode 3: a bf16 bucket is reduced as an fp32 reduce-scatter (each rank's shard
   // summed in fp32 over the ring, rounded to bf16 ONCE) followed by an in-place bf16
-  // all-gather: the same values as the fp32 all-reduce of mode 2 at 6 instead of 8 wire
-  // bytes per element ((n-1)/n x (4 + 2) vs 2 (n-1)/n x 4).
+  // all-gather, at 6 instead of 8 wire bytes per element ((n-1)/n x (4 + 2) vs
+  // 2 (n-1)/n x 4).  Same precision class as the fp32 all-reduce of mode 2 (fp32 sums,
+  // one rounding), but not pinned bitwise to it: RCCL may order the fp32 additions of a
+  // reduce-scatter differently from an all-reduce's (tested on gloo only).
   bool split_mode(const Bucket& B) const { return fp32_mode_ == 3 && B.dtype == at::kBFloat16; }
 
   void launch_split(Bucket& B, int64_t bi) {
