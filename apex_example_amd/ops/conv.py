@@ -303,15 +303,22 @@ def _own_1x1(x_rows_dtype, cin, cout, m):
             and x_rows_dtype == torch.bfloat16 and _native.available())
 
 
+def _g4w_1x1(x, ci, co, m):
+    """The native 1x1 forward runs this shape on gemm4w (csrc/hip/conv_igemm.hip
+    conv1x1_g4w: the measured winners, with the statistics epilogue)."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and _native.available() and ci % 64 == 0
+            and _native.require().conv.on_gemm4w_1x1(m, ci, co))
+
+
 def _conv1x1_fwd(x, weight, bn=None):
-    """y = conv1x1(x) for a channels-last bf16 x: own MFMA kernel or hipBLASLt GEMM.
-    With ``bn`` (a BatchNorm consuming y) the own kernel also writes its statistics
-    wherever that beats hipBLASLt + a statistics pass (always for own-kernel shapes;
-    channel-expanding / equal shapes, where the saved pass over the 4x larger output
-    outweighs the library's edge: profiles/microbench_conv1x1_own.txt)."""
+    """y = conv1x1(x) for a channels-last bf16 x: own MFMA kernel, gemm4w or hipBLASLt.
+    With ``bn`` (a BatchNorm consuming y) the native kernel also writes its statistics
+    wherever that beats hipBLASLt + a statistics pass (always for own-kernel and gemm4w
+    shapes; channel-expanding / equal shapes, where the saved pass over the 4x larger
+    output outweighs the library's edge: profiles/microbench_conv1x1_own.txt)."""
     n, ci, h, w = x.shape
     co = weight.shape[0]
-    own = _own_1x1(x.dtype, ci, co, n * h * w)
+    own = _own_1x1(x.dtype, ci, co, n * h * w) or _g4w_1x1(x, ci, co, n * h * w)
     if (bn is not None and weight.dtype == torch.bfloat16 and ci % 64 == 0 and co % 64 == 0
             and (own or co >= ci) and n * h * w < (1 << 31)):
         return _conv_fwd(x, weight, 1, bn)

@@ -1872,10 +1872,32 @@ void conv_halo_enable(int mode) { g_conv_halo = mode; }
 void conv_bnbwd_early(int mode) { g_bnbwd_early = mode; }
 int conv_halo_enabled() { return g_conv_halo; }
 
-int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize) {
+// Stride-1 1x1 forwards on gemm4w (one wave per SIMD, 256 x 256 tiles; BN statistics in
+// its EPI 3 epilogue): 0 off, 1 the measured winners, 2 every eligible shape (A/B).
+// With the statistics epilogue, ResNet-50 bs 256 (tools/diag/conv1x1_g4w_bench.py,
+// profiles/r6/conv1x1_g4w.md, us): 512->2048 @ 7 45 vs 53 (own kernel), 1024->256 @ 14
+// 37 vs 45 (hipBLASLt, plus a statistics pass the own path would add), 64->256 @ 56 177 vs
+// 178; the own kernel keeps 128->512 @ 28 (76 vs 97: two K-tiles per 256 x 256 tile leave
+// gemm4w's epilogue exposed at one workgroup per CU), 256->1024 @ 14 (59 vs 68) and
+// 2048->512 @ 7 (40 vs 48).
+int g_conv1x1_g4w = 1;
+
+bool conv1x1_g4w(int64_t M, int Cin, int Cout, int stride) {
+  if (g_conv1x1_g4w == 0 || stride != 1 || Cout % 256 != 0 || Cin % 64 != 0 ||
+      M >= ((int64_t)1 << 31) || !gemm4w_supported((int)M, Cout, Cin))
+    return false;
+  if (g_conv1x1_g4w == 2) return true;
+  return (Cin == 512 && Cout == 2048) || (Cin == 1024 && Cout == 256) ||
+         (Cin == 64 && Cout == 256);
+}
+void conv_1x1_gemm4w(int mode) { g_conv1x1_g4w = mode; }
+bool conv_1x1_on_gemm4w(int64_t M, int Cin, int Cout) { return conv1x1_g4w(M, Cin, Cout, 1); }
+
+int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize, int Cin) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t M = (int64_t)N * Ho * Wo;
   if (ksize == 3 && conv3h_ok(N, H, W, Cout, stride)) return (int)((M + kHBM - 1) / kHBM);
+  if (ksize == 1 && conv1x1_g4w(M, Cin, Cout, stride)) return (int)((M + 255) / 256);
   return (int)((M + kBM - 1) / kBM);  // launch_conv_tap's M tile (EPI 0)
 }
 
@@ -1887,6 +1909,24 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
   const auto* xp = static_cast<const bf16_t*>(x);
   const auto* wp = static_cast<const bf16_t*>(w);
   auto* yp = static_cast<bf16_t*>(y);
+  if (ksize == 1 && conv1x1_g4w((int64_t)N * Ho * Wo, Cin, Cout, stride)) {
+    // y[M, Cout] = x[M, Cin] . W[Cout, Cin]^T (NHWC rows, KRSC weight rows)
+    GemmArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.A = x;
+    a.B = w;
+    a.C = y;
+    a.M = N * Ho * Wo;
+    a.N = Cout;
+    a.K = Cin;
+    a.lda = Cin;
+    a.ldb = Cin;
+    a.ldc = Cout;
+    a.slab = stats_slab;
+    a.shift = stats_shift;
+    gemm4w(a, stats_slab ? 3 : 0, st);
+    return;
+  }
   if (ksize == 3 && conv3h_ok(N, H, W, Cout, stride))
     launch_conv3h<0>(xp, wp, yp, g, N, st, stats_slab, stats_shift, ConvBnEpi{});
   else if (ksize == 3) launch_conv_tap<kFwd3>(xp, wp, yp, g, st, stats_slab, stats_shift);

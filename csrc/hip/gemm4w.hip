@@ -150,8 +150,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t w4_rsrc(const void* base, uint
 template <typename TT, int EPI, bool TANH>
 __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(GemmArgs p) {
   typedef typename W4T<TT>::v8 v8;
-  // the ring + 2 KB for the bias-gradient column sums of EPI 2
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kW4Slot + 2048];
+  // the ring + 2 KB for the bias-gradient column sums of EPI 2 (4 KB: the two statistics
+  // sums of EPI 3)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * kW4Slot + (EPI == 3 ? 4096 : 2048)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -270,6 +271,65 @@ __global__ void __launch_bounds__(kW4T, 1) gemm4w_k(GemmArgs p) {
                        : p.bias_f32 ? static_cast<const float*>(p.bias)[c]
                                     : (float)static_cast<const TT*>(p.bias)[c];
         }
+    }
+    if constexpr (EPI == 3) {
+      // BatchNorm statistics of the stored (rounded) output for the BN that consumes C
+      // (1x1 conv forward): per column, sum(v - s) and sum((v - s)^2) over the tile's
+      // rows.  Column block q at a time (16 live sums, not 64): rows i in-lane, the 16
+      // lanes fr by DPP row reductions (fixed order), the two wm waves through LDS; one
+      // channel-major slab entry per (column, M-tile), as conv_tap_k's epilogue writes.
+      float* red3 = reinterpret_cast<float*>(lds + 2 * kW4Slot);  // [sum][wm][256]
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float sh[8], s1[8], s2[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sh[e] = p.shift ? p.shift[n0 + ccol + q * 32 + e] : 0.f;
+          s1[e] = s2[e] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int row = wm * 128 + i * 16 + fr;
+          const bool in = m0 + row < p.M;
+          v8 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = (TT)acc[i][2 * q][e];
+            v[4 + e] = (TT)acc[i][2 * q + 1][e];
+          }
+          const uint32_t off = ((uint32_t)row * (uint32_t)p.ldc + (uint32_t)(n0 + ccol + q * 32)) * sizeof(TT);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4_t, v), rC, off, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = in ? (float)v[e] - sh[e] : 0.f;
+            s1[e] += d;
+            s2[e] = fmaf(d, d, s2[e]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float a = s1[e], b = s2[e];
+#define W4_ROWSUM(v_)                                                                                  \
+  v_ += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v_), 0xB1, 0xf, 0xf, true)); \
+  v_ += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v_), 0x4E, 0xf, 0xf, true)); \
+  v_ += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v_), 0x141, 0xf, 0xf, true)); \
+  v_ += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v_), 0x140, 0xf, 0xf, true));
+          W4_ROWSUM(a)
+          W4_ROWSUM(b)
+#undef W4_ROWSUM
+          if (fr == 0) {
+            red3[wm * 256 + ccol + q * 32 + e] = a;
+            red3[512 + wm * 256 + ccol + q * 32 + e] = b;
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      w4_barrier();
+      const int S = (p.M + 255) >> 8, tm = m0 >> 8;
+      p.slab[(int64_t)(n0 + tid) * S + tm] = red3[tid] + red3[256 + tid];
+      p.slab[(int64_t)(p.N + n0 + tid) * S + tm] = red3[512 + tid] + red3[768 + tid];
+      return;
     }
     float colsum[4][8];
 #pragma unroll
@@ -440,6 +500,8 @@ void gemm4w(const GemmArgs& a0, int epi, hipStream_t st) {
     constexpr bool TH = decltype(tanh_c)::value;
     if (epi == 0)
       hipLaunchKernelGGL((gemm4w_k<TT, 0, false>), dim3(ntiles), dim3(kW4T), 0, st, a);
+    else if (epi == 3)
+      hipLaunchKernelGGL((gemm4w_k<TT, 3, false>), dim3(ntiles), dim3(kW4T), 0, st, a);
     else if (epi == 1)
       hipLaunchKernelGGL((gemm4w_k<TT, 1, TH>), dim3(ntiles), dim3(kW4T), 0, st, a);
     else

@@ -272,6 +272,8 @@ struct GemmArgs {
   int tanh;                    // GELU flavour: 1 tanh approximation, 0 erf
   int fp16;                    // operands / outputs fp16 instead of bf16
   int group_m;                 // tile order: groups of group_m m-tiles (set by gemm4w())
+  float* slab;                 // epi 3: BatchNorm statistics [2][N][ceil(M / 256)] (channel-major)
+  const float* shift;          // epi 3: per-column shift s of the sums (v - s), (v - s)^2; may be null
 };
 bool gemm4w_supported(int M, int N, int K);
 void gemm4w(const GemmArgs& a, int epi, hipStream_t st);
@@ -301,13 +303,17 @@ bool conv3x3_nhwc_supported(int Cin, int Cout);
 void conv_halo_enable(int mode);
 int conv_halo_enabled();
 void conv_bnbwd_early(int mode);
+// stride-1 1x1 forwards with Cout % 256 == 0 on gemm4w (statistics epilogue): 0 off, 1 the
+// measured winners, 2 every eligible shape; the query tells whether conv_nhwc_fwd takes it
+void conv_1x1_gemm4w(int mode);
+bool conv_1x1_on_gemm4w(int64_t M, int Cin, int Cout);
 // y is N x Ho x Wo x Cout, Ho = (H-1)/stride + 1; w is [Cout][k*k][Cin]
 // stats_slab (optional, fp32 [conv_fwd_mtiles(...)][2][Cout]): per M-tile shifted sums
 // sum(y - shift[c]), sum((y - shift[c])^2) of the bf16 output for the consuming BN
 void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout,
                    int ksize, int stride, hipStream_t st, float* stats_slab = nullptr,
                    const float* stats_shift = nullptr);
-int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize = 3);
+int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize, int Cin);
 // M tiles (slab rows) of conv_nhwc_fwd_bnbwd's stride-1 launch
 int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize);
 // BatchNorm-backward epilogue of a data-gradient conv (conv_nhwc_fwd on dY with the

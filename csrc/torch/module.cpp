@@ -160,6 +160,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "that output-tile width where possible");
   conv.def("halo_enabled", &conv_halo_enabled);
   conv.def("set_bnbwd_early", &conv_bnbwd_early);
+  conv.def("set_1x1_gemm4w", &conv_1x1_gemm4w);
+  conv.def("on_gemm4w_1x1", &conv_1x1_on_gemm4w, py::arg("M"), py::arg("Cin"), py::arg("Cout"));
 
   auto bn = m.def_submodule("bn", "BatchNorm / SyncBatchNorm kernels (NCHW + NHWC)");
   bn.def("local_stats", &bn_local_stats_op);

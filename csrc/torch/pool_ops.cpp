@@ -121,7 +121,7 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_stats_op(at::Tensor x, at::Tens
   w = w.contiguous(at::MemoryFormat::ChannelsLast);
   at::Tensor y = at::empty({N, Cout, Ho, Wo},
                            x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int S = conv_fwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)stride, (int)k);
+  const int S = conv_fwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)stride, (int)k, (int)Cin);
   at::Tensor slab = at::empty({2, Cout, S}, x.options().dtype(at::kFloat));
   conv_nhwc_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)Cin,
                 (int)Cout, (int)k, (int)stride, cur_stream(), slab.data_ptr<float>(), sp);
