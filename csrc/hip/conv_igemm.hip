@@ -1879,8 +1879,11 @@ int conv_halo_enabled() { return g_conv_halo; }
 // 37 vs 45 (hipBLASLt, plus a statistics pass the own path would add), 64->256 @ 56 177 vs
 // 178; the own kernel keeps 128->512 @ 28 (76 vs 97: two K-tiles per 256 x 256 tile leave
 // gemm4w's epilogue exposed at one workgroup per CU), 256->1024 @ 14 (59 vs 68) and
-// 2048->512 @ 7 (40 vs 48).
-int g_conv1x1_g4w = 1;
+// 2048->512 @ 7 (40 vs 48).  Off by default: in the model the table lost end to end
+// (ResNet-50 same box 11,970 / 11,969 with it vs 12,040 / 12,020 without,
+// profiles/r6/conv1x1_g4w.md) - gemm4w holds a whole CU (132 KB LDS, 512 registers per
+// lane), so the side-stream weight-gradient kernels no longer overlap those convs.
+int g_conv1x1_g4w = 0;
 
 bool conv1x1_g4w(int64_t M, int Cin, int Cout, int stride) {
   if (g_conv1x1_g4w == 0 || stride != 1 || Cout % 256 != 0 || Cin % 64 != 0 ||

@@ -22,7 +22,7 @@ def _C():
 def g4w_switch():
     C = _C()
     yield C.conv.set_1x1_gemm4w
-    C.conv.set_1x1_gemm4w(1)
+    C.conv.set_1x1_gemm4w(0)
 
 
 @pytest.mark.parametrize("shape", [

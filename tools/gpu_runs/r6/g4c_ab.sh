@@ -5,15 +5,8 @@ cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r6g4c
 mkdir -p $out
 timeout -k 10 300 python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread \
-  tests/test_conv_1x1_gemm4w_gpu.py tests/test_conv_bn_stats_gpu.py > $out/tests.log 2>&1
-cat > /tmp/g4c_mode.py <<'PY'
-import os, runpy, sys
-from apex_example_amd import _native
-_native.require().conv.set_1x1_gemm4w(int(os.environ["G4C_MODE"]))
-sys.argv = ["bench.py"] + sys.argv[1:]
-runpy.run_path("bench.py", run_name="__main__")
-PY
+  tests/test_conv_1x1_gemm4w_gpu.py > $out/tests.log 2>&1
 for i in 1 2; do
-  G4C_MODE=1 timeout -k 10 300 python -u /tmp/g4c_mode.py --steps 30 --warmup 10 --json-out $out/r50_g4w_$i.json > $out/r50_g4w_$i.log 2>&1
-  G4C_MODE=0 timeout -k 10 300 python -u /tmp/g4c_mode.py --steps 30 --warmup 10 --json-out $out/r50_own_$i.json > $out/r50_own_$i.log 2>&1
+  APEX_AMD_CONV_1X1_G4W=1 timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 --json-out $out/r50_g4w_$i.json > $out/r50_g4w_$i.log 2>&1
+  APEX_AMD_CONV_1X1_G4W=0 timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 --json-out $out/r50_own_$i.json > $out/r50_own_$i.log 2>&1
 done
