@@ -730,18 +730,29 @@ class Conv2d1x1(nn.Conv2d):
 # 3x3 weight gradient: "tap" = per-tap MFMA kernel (default), "nine" = the all-taps
 # strip kernel (W <= 56), "miopen" = MIOpen's convolution_backward
 _WGRAD3 = "tap"
-# 64 -> 64 channel 3x3 stride-1 weight gradients (ResNet layer 1) on the strip-ring kernel
-# (csrc/hip/conv_igemm.hip conv3x3_wgrad_c64_k, algo 4; 93.8 us / 631 TF vs 175 us for
-# the per-tap kernel, docs/PERF.md round 4)
+# 3x3 stride-1 weight gradients on the strip-ring kernel (csrc/hip/conv_igemm.hip
+# conv3x3_wgrad_c64_k, algo 4: all nine taps per workgroup from one padded-row strip):
+# 64 -> 64 (ResNet layer 1, 93.8 us / 631 TF vs 175 us for the per-tap kernel, docs/PERF.md
+# round 4); round 6 generalised it to 64 x 64 channel tiles: bs 256, incl. the split
+# reduction, 128@28 113 -> 85 us, 256@14 104 -> 93 us; at 7 x 7 every K-tile is a new
+# image (a full strip load each), 110 -> 123 us, so W < 14 keeps the per-tap kernel
+# (profiles/r6/wgrad9_bench.md).  In the model it measured neutral (ResNet-50 same box
+# 11,956 / 11,948 vs 11,982 / 11,906 img/s: the kernel holds a whole CU, 147 KB LDS, so
+# the main-stream kernels it overlapped lose residency), so the wider routing is opt-in
+# (APEX_AMD_WGRAD9=1); the 64 -> 64 shapes always take it
 _WGRAD64 = True
+_WGRAD9_ALL = os.environ.get("APEX_AMD_WGRAD9", "0") == "1"
 
 
 def _wgrad3_algo(x, weight, stride):
     """conv_wgrad algo for a 3x3 weight gradient under _WGRAD3 == "tap"."""
-    if (_WGRAD64 and stride == 1 and x.size(1) == 64 and weight.size(0) == 64
-            and x.size(3) <= 56):
+    cin, cout = x.size(1), weight.size(0)
+    if not (_WGRAD64 and stride == 1 and x.size(3) <= 56 and cin % 64 == 0
+            and cout % 64 == 0):
+        return 0
+    if cin == 64 and cout == 64:
         return 4
-    return 0
+    return 4 if _WGRAD9_ALL and x.size(3) >= 14 else 0
 # the own reduction / rotation kernels (tests turn them off to compare with ATen)
 _USE_SPLITK_REDUCE = True
 _USE_ROT_KERNEL = True

@@ -1217,7 +1217,8 @@ constexpr int kW64BK = 64;                        // pixels per K-tile
 
 __global__ void __launch_bounds__(512, 1)
     conv3x3_wgrad_c64_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                        float* __restrict__ part, int H, int W, int kpi, int kps, int total_kt) {
+                        float* __restrict__ part, int H, int W, int kpi, int kps, int total_kt,
+                        int Cin, int Cout) {
   constexpr int RB = 128;                                   // 64 channels x bf16
   constexpr int A_BYTES = kW64BK * RB;                      // 8 KB per dY K-tile
   constexpr int RING_BYTES = kW64Ring * RB;                 // 32 KB
@@ -1233,6 +1234,10 @@ __global__ void __launch_bounds__(512, 1)
   const int wk = wid >> 2, wn = wid & 3;
   const int Wp = W + 2, HWp = H * Wp;
   const int SR = (kW64BK + 2 * Wp + 2 + 7) & ~7;            // strip rows (8-row aligned)
+  // 64 x 64 channel tile blockIdx.y of a Cout x Cin layer (round 6: the kernel was
+  // 64 -> 64 only)
+  const int ci_tiles = Cin >> 6;
+  const int co0 = ((int)blockIdx.y / ci_tiles) * 64, ci0 = ((int)blockIdx.y % ci_tiles) * 64;
   const float invWp = 1.f / (float)Wp;
   const int kt_begin = blockIdx.x * kps;
   const int kt_end = kt_begin + kps < total_kt ? kt_begin + kps : total_kt;
@@ -1245,7 +1250,7 @@ __global__ void __launch_bounds__(512, 1)
     const int chunk = (tr_swz<RB>(pos, pch) - pos * RB) >> 4;
     const int hp = fdiv(row, Wp, invWp), wp = row - hp * Wp;
     const bool ok = hp >= 1 && hp <= H && wp >= 1 && wp <= W;
-    const void* src = ok ? (const void*)(x + (((int64_t)n * H + hp - 1) * W + wp - 1) * 64 + chunk * 8)
+    const void* src = ok ? (const void*)(x + (((int64_t)n * H + hp - 1) * W + wp - 1) * Cin + ci0 + chunk * 8)
                          : (const void*)g_zero16;
     glds16a(src, ring + (P & (kW64Ring - 1)) * RB);
   };
@@ -1256,7 +1261,7 @@ __global__ void __launch_bounds__(512, 1)
     const int qq = q0 + row;
     const int h_ = fdiv(qq, Wp, invWp), w_ = qq - h_ * Wp;
     const bool ok = qq < HWp && w_ < W;
-    const void* src = ok ? (const void*)(dy + (((int64_t)n * H + h_) * W + w_) * 64 + chunk * 8)
+    const void* src = ok ? (const void*)(dy + (((int64_t)n * H + h_) * W + w_) * Cout + co0 + chunk * 8)
                          : (const void*)g_zero16;
     glds16a(src, abuf + buf * A_BYTES + wid * 1024);
   };
@@ -1333,7 +1338,7 @@ __global__ void __launch_bounds__(512, 1)
   }
   __syncthreads();
   if (wk == 0) {
-    float* out = part + (int64_t)blockIdx.x * 9 * 64 * 64;
+    float* out = part + (int64_t)blockIdx.x * 9 * Cout * Cin;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1343,7 +1348,7 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = i * 16 + fg * 4 + e;
-          out[((int64_t)tap * 64 + co) * 64 + ci] = acc[i][j][e] + o[e];
+          out[((int64_t)tap * Cout + co0 + co) * Cin + ci0 + ci] = acc[i][j][e] + o[e];
         }
       }
   }
@@ -1677,11 +1682,13 @@ bool conv3x3_nhwc_supported(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 
 
 int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int stride, int algo) {
   if (algo == 4) {
-    // one 8-wave workgroup per CU; K-tile ranges of whole images where possible (each
-    // image boundary costs a full strip load)
+    // one 8-wave workgroup per CU over (splits x 64 x 64 channel tiles); K-tile ranges of
+    // whole images where possible (each image boundary costs a full strip load)
     const int kpi = (H * (W + 2) + kW64BK - 1) / kW64BK;
     const int total = N * kpi;
-    int S = N <= 256 ? N : 256;
+    const int tiles = (Cout / 64) * (Cin / 64);
+    int S = 256 / tiles;
+    if (S > N) S = N;
     if (S < 1) S = 1;
     return S > total ? total : S;
   }
@@ -1723,9 +1730,9 @@ int conv_wgrad_splits(int N, int H, int W, int Cin, int Cout, int ksize, int str
 
 bool conv3x3_wgrad_supported(int W, int algo) { return (algo != 1 && algo != 4) || W <= kWgMaxW; }
 
-// the strip-ring kernel's shapes: 3x3 stride 1, 64 -> 64 channels, W <= 56
+// the strip-ring kernel's shapes: 3x3 stride 1, channels % 64 (64 x 64 tiles), W <= 56
 bool conv3x3_wgrad_c64_ok(int W, int Cin, int Cout, int ksize, int stride) {
-  return ksize == 3 && stride == 1 && Cin == 64 && Cout == 64 && W <= kWgMaxW;
+  return ksize == 3 && stride == 1 && Cin % 64 == 0 && Cout % 64 == 0 && W <= kWgMaxW;
 }
 
 int64_t conv_wgrad_workspace(int S, int Cin, int Cout, int ksize) {
@@ -1742,8 +1749,9 @@ void conv_nhwc_wgrad(const void* dy, const void* x, float* part, void* dw, bool 
     const int kpi = (H * (W + 2) + kW64BK - 1) / kW64BK;
     const int total = N * kpi;
     const int kps = (total + S - 1) / S;
-    hipLaunchKernelGGL(conv3x3_wgrad_c64_k, dim3((unsigned)S), dim3(512), 0, st, dyp, xp, part,
-                       H, W, kpi, kps, total);
+    const unsigned tiles = (unsigned)((Cout / 64) * (Cin / 64));
+    hipLaunchKernelGGL(conv3x3_wgrad_c64_k, dim3((unsigned)S, tiles), dim3(512), 0, st, dyp, xp,
+                       part, H, W, kpi, kps, total, Cin, Cout);
   } else if (algo == 1) {
     const int kpi = (H * (W + 2) + kWgBK - 1) / kWgBK;
     const int total = N * kpi;

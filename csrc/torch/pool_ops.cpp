@@ -239,7 +239,7 @@ at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dt
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv_wgrad: out dtype");
   TORCH_CHECK(conv3x3_wgrad_supported((int)W, (int)algo), "conv_wgrad: width > 56 unsupported for algo 1");
   TORCH_CHECK(algo != 4 || conv3x3_wgrad_c64_ok((int)W, (int)Cin, (int)Cout, (int)ksize, (int)stride),
-              "conv_wgrad: algo 4 is the 3x3 stride-1 64 -> 64 channel kernel (W <= 56)");
+              "conv_wgrad: algo 4 is the 3x3 stride-1 strip-ring kernel (channels % 64, W <= 56)");
   TORCH_CHECK(algo != 1 || (Cin % 64 == 0 && Cout % 64 == 0), "conv_wgrad: algo 1 channels");
   // the kernels split pixel indices with a float reciprocal (exact below 2^22)
   TORCH_CHECK(N * H * W < ((int64_t)1 << 22), "conv_wgrad: too many pixels");

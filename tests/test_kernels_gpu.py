@@ -1144,3 +1144,33 @@ def test_conv3x3_wgrad_c64_strip_ring(shape):
     torch.testing.assert_close(got16.float(), wref, rtol=1e-2, atol=1e-2 * wref.abs().max().item())
     # the per-tap kernel agrees too (what the model ran before)
     torch.testing.assert_close(got, cv.conv_wgrad(dy, x, torch.float32, 0), rtol=1e-4, atol=tol)
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 128, 9, 9), (3, 64, 192, 28, 31), (2, 256, 128, 14, 14),
+                                   (2, 512, 512, 7, 7), (1, 128, 64, 56, 56)])
+def test_conv3x3_wgrad_strip_ring_channel_tiles(shape):
+    """The strip-ring weight gradient (algo 4) on 64 x 64 channel tiles of wider layers
+    (round 6): Cin != Cout, tiles on both axes, image-crossing K ranges; fp32 / bf16
+    outputs and accumulation vs the fp32 reference and the per-tap kernel."""
+    from apex_example_amd import _native
+
+    n, ci, co, h, w = shape
+    torch.manual_seed(12)
+    x = torch.randn(n, ci, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    dy = torch.randn(n, co, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    wref = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), torch.zeros(co, ci, 3, 3, device=DEV), None, (1, 1), (1, 1),
+        (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    cv = _native.require().conv
+    tol = 1e-3 * wref.abs().max().item()
+    got = cv.conv_wgrad(dy, x, torch.float32, 4)
+    torch.testing.assert_close(got, wref, rtol=1e-4, atol=tol)
+    base = torch.randn_like(wref).contiguous(memory_format=torch.channels_last)
+    acc = base.clone()
+    cv.conv_wgrad(dy, x, torch.float32, 4, out=acc)
+    torch.testing.assert_close(acc, base + wref, rtol=1e-4, atol=tol)
+    got16 = cv.conv_wgrad(dy, x, torch.bfloat16, 4)
+    torch.testing.assert_close(got16.float(), wref, rtol=1e-2, atol=1e-2 * wref.abs().max().item())
+    torch.testing.assert_close(got, cv.conv_wgrad(dy, x, torch.float32, 0), rtol=1e-4, atol=tol)
