@@ -238,7 +238,7 @@ __device__ __forceinline__ void bnbwd_prefetch(const ConvGeom& g, const ConvBnEp
 // one specialisation per (ReLU-mask mode, residual add): the per-element mode tests are
 // compile-time, so the unrolled store loop is straight-line code (runtime tests there
 // made the compiler branch around every element: +30-60 us per ResNet-50 layer)
-template <int MODE, int BM, int BN, int CT, int RM, bool ADD>
+template <int MODE, int BM, int BN, int CT, int RM, bool ADD, int TS>
 __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restrict__ y,
                                               const ConvGeom& g, int m0, int n0, int z,
                                               const BnPre<BM, BN, CT>& P, float (&s1)[8],
@@ -266,7 +266,7 @@ __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restric
     const int row = q * PT::RGS + rg;
     const int m = m0 + row;
     if (m >= g.M) continue;
-    const uint4 tv = *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+    const uint4 tv = *reinterpret_cast<const uint4*>(T + row * TS + cc * 8);
     const unsigned tw[4] = {tv.x, tv.y, tv.z, tv.w};
     const unsigned aw[4] = {P.av[q].x, P.av[q].y, P.av[q].z, P.av[q].w};
     const unsigned xw[4] = {P.xv[q].x, P.xv[q].y, P.xv[q].z, P.xv[q].w};
@@ -302,19 +302,19 @@ __device__ __forceinline__ void bnbwd_store_t(const bf16_t* T, bf16_t* __restric
   }
 }
 
-template <int MODE, int BM, int BN, int CT>
+template <int MODE, int BM, int BN, int CT, int TS>
 __device__ __forceinline__ void bnbwd_store(const bf16_t* T, bf16_t* __restrict__ y,
                                             const ConvGeom& g, const ConvBnEpi& ep, int m0,
                                             int n0, int z, const BnPre<BM, BN, CT>& P,
                                             float (&s1)[8], float (&s2)[8]) {
   const bool add = ep.add != nullptr;
   switch (ep.relu_mode * 2 + (add ? 1 : 0)) {
-    case 0: bnbwd_store_t<MODE, BM, BN, CT, 0, false>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 1: bnbwd_store_t<MODE, BM, BN, CT, 0, true>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 2: bnbwd_store_t<MODE, BM, BN, CT, 1, false>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 3: bnbwd_store_t<MODE, BM, BN, CT, 1, true>(T, y, g, m0, n0, z, P, s1, s2); break;
-    case 4: bnbwd_store_t<MODE, BM, BN, CT, 2, false>(T, y, g, m0, n0, z, P, s1, s2); break;
-    default: bnbwd_store_t<MODE, BM, BN, CT, 2, true>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 0: bnbwd_store_t<MODE, BM, BN, CT, 0, false, TS>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 1: bnbwd_store_t<MODE, BM, BN, CT, 0, true, TS>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 2: bnbwd_store_t<MODE, BM, BN, CT, 1, false, TS>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 3: bnbwd_store_t<MODE, BM, BN, CT, 1, true, TS>(T, y, g, m0, n0, z, P, s1, s2); break;
+    case 4: bnbwd_store_t<MODE, BM, BN, CT, 2, false, TS>(T, y, g, m0, n0, z, P, s1, s2); break;
+    default: bnbwd_store_t<MODE, BM, BN, CT, 2, true, TS>(T, y, g, m0, n0, z, P, s1, s2); break;
   }
 }
 
@@ -347,7 +347,10 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
   static_assert(AI >= 1 && BI >= 1, "tile rows per wave");
   constexpr int G = AI + BI;        // glds per wave per tile (vmcnt units)
   // the ring, or the epilogue's bf16 tile / statistics exchange if larger
-  constexpr int EPI_BYTES = BM * BN * 2 > 2 * CT * 8 * 4 ? BM * BN * 2 : 2 * CT * 8 * 4;
+  // epilogue tile rows padded by 16 bytes: the 16 lanes of a ds_write_b64 group (16 rows,
+  // one 4-column slice) then hit 16 distinct bank pairs
+  constexpr int TS = BN + 8;
+  constexpr int EPI_BYTES = BM * TS * 2 > 2 * CT * 8 * 4 ? BM * TS * 2 : 2 * CT * 8 * 4;
   constexpr int LDS_BYTES = NB * BUF > EPI_BYTES ? NB * BUF : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
@@ -487,8 +490,8 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
   #pragma unroll
         for (int i = 0; i < FM; ++i)
   #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)  // (B, A): accumulator = C^T, 4 columns per lane
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     }
   }
@@ -502,18 +505,23 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
     __syncthreads();
   }
 
-  // epilogue: accumulators -> bf16 tile in LDS -> coalesced 16-byte row stores
+  // epilogue: accumulators -> bf16 tile in LDS -> coalesced 16-byte row stores.  The
+  // accumulators hold C^T (B was the first MFMA operand): lane (fr, fg) of block (i, j)
+  // has the 4 consecutive columns j*16 + fg*4 .. +3 of row i*16 + fr - one 8-byte LDS
+  // store instead of four 2-byte ones
   bf16_t* T = reinterpret_cast<bf16_t*>(lds);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wm * TM + i * 16 + fg * 4 + e;
-        const int col = wn * TN + j * 16 + fr;
-        T[row * BN + col] = (bf16_t)acc[i][j][e];
-      }
+    for (int j = 0; j < FN; ++j) {
+      const int row = wm * TM + i * 16 + fr;
+      const int col = wn * TN + j * 16 + fg * 4;
+      const unsigned lo = (unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][0]) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][1]) << 16);
+      const unsigned hi = (unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][2]) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][3]) << 16);
+      *reinterpret_cast<uint2*>(T + row * TS + col) = make_uint2(lo, hi);
+    }
   if constexpr (EPI == 1) {
     lds_barrier();
   } else {
@@ -531,7 +539,7 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
   if constexpr (EPI == 1) {
-    bnbwd_store<MODE, BM, BN, CT>(T, y, g, ep, m0, n0, z, pre, s1, s2);
+    bnbwd_store<MODE, BM, BN, CT, TS>(T, y, g, ep, m0, n0, z, pre, s1, s2);
   } else
   for (int c = tid; c < BM * CPR; c += CT) {
     const int row = c / CPR, cc = c - row * CPR;
@@ -544,7 +552,7 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
       const int gh = rem / g.GW, gw = rem - gh * g.GW;
       opix = (int64_t)(n * g.YH + gh * g.ys + (z >> 1)) * g.YW + gw * g.ys + (z & 1);
     }
-    const uint4 v = *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+    const uint4 v = *reinterpret_cast<const uint4*>(T + row * TS + cc * 8);
     *reinterpret_cast<uint4*>(y + opix * g.NC + n0 + cc * 8) = v;
     if (want_stats) {
       const unsigned wv[4] = {v.x, v.y, v.z, v.w};
@@ -711,7 +719,8 @@ __global__ void __launch_bounds__(kCT, 2)
   constexpr int BPW = BN / 64;             // weight pieces (16 rows each) per wave per step
   constexpr int NHP = kHRows / 64;         // halo pieces per wave per slice (7 | 8)
   constexpr int RING = 2 * kHBuf + 3 * BSLOT;
-  constexpr int EPI_BYTES = BM * BN * 2;
+  constexpr int TS = BN + 8;               // padded epilogue tile rows (as conv_tap_k)
+  constexpr int EPI_BYTES = BM * TS * 2;
   constexpr int LDS_BYTES = RING > EPI_BYTES ? RING : EPI_BYTES;
   static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
@@ -839,8 +848,8 @@ __global__ void __launch_bounds__(kCT, 2)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j)  // (B, A): accumulator = C^T (see the epilogue)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     };
     step(std::integral_constant<int, 0>{});
     step(std::integral_constant<int, 1>{});
@@ -866,18 +875,21 @@ __global__ void __launch_bounds__(kCT, 2)
 #pragma unroll
   for (int i = 0; i < 8; ++i) shv[i] = (EPI == 0 && want_stats && shift) ? shift[n0 + scc * 8 + i] : 0.f;
 
-  // epilogue (as conv_tap_k): accumulators -> bf16 tile in LDS -> coalesced row stores
+  // epilogue (as conv_tap_k): C^T accumulators -> bf16 tile in LDS (8-byte stores of 4
+  // consecutive columns, padded rows) -> coalesced row stores
   bf16_t* T = reinterpret_cast<bf16_t*>(lds);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wm * TM + i * 16 + fg * 4 + e;
-        const int col = wn * TN + j * 16 + fr;
-        T[row * BN + col] = (bf16_t)acc[i][j][e];
-      }
+    for (int j = 0; j < FN; ++j) {
+      const int row = wm * TM + i * 16 + fr;
+      const int col = wn * TN + j * 16 + fg * 4;
+      const unsigned lo = (unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][0]) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][1]) << 16);
+      const unsigned hi = (unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][2]) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16_t)acc[i][j][3]) << 16);
+      *reinterpret_cast<uint2*>(T + row * TS + col) = make_uint2(lo, hi);
+    }
   __syncthreads();
   float s1[8], s2[8];
 #pragma unroll
@@ -887,13 +899,13 @@ __global__ void __launch_bounds__(kCT, 2)
     // prefetch held across the tile write would exceed the 2-workgroups-per-CU registers)
     BnPre<BM, BN, CT> pre;
     bnbwd_prefetch<kFwd3, BM, BN, CT>(g, ep, m0, n0, 0, pre);
-    bnbwd_store<kFwd3, BM, BN, CT>(T, y, g, ep, m0, n0, 0, pre, s1, s2);
+    bnbwd_store<kFwd3, BM, BN, CT, TS>(T, y, g, ep, m0, n0, 0, pre, s1, s2);
   } else {
     for (int q = tid; q < BM * CPR; q += CT) {
       const int row = q / CPR, cc = q - row * CPR;
       const int m = m0 + row;
       if (m >= M) continue;
-      const uint4 v = *reinterpret_cast<const uint4*>(T + row * BN + cc * 8);
+      const uint4 v = *reinterpret_cast<const uint4*>(T + row * TS + cc * 8);
       *reinterpret_cast<uint4*>(y + (int64_t)m * g.NC + n0 + cc * 8) = v;
       if (want_stats) {
         const unsigned wv[4] = {v.x, v.y, v.z, v.w};
