@@ -601,9 +601,12 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 // variants - 256-row tiles with 4 or 8 waves, the 4-deep pipelined 32-deep ring, the
 // burst-free interleaved 64-deep loop, 64-row tiles for the large 1x1 forwards - were
 // removed in round 6):
-//  * 1x1 data gradients with the BN-backward epilogue over >= 50,176 output pixels
-//    (ResNet-50 layers 1-3; 2.8-3.5 TB/s of epilogue traffic): 64-row M tiles, up to 4
-//    workgroups per CU (11,373 -> 11,430 img/s, profiles/r5/ab_r50_bm64/);
+//  * 1x1 data gradients with the BN-backward epilogue over >= 50,176 output pixels and
+//    K < 256 (ResNet-50 layers 1-3; 2.8-3.5 TB/s of epilogue traffic): 64-row M tiles, up
+//    to 4 workgroups per CU (11,373 -> 11,430 img/s, profiles/r5/ab_r50_bm64/); from
+//    K = 256 the 128-row tiles win (8 MFMAs per wave per barrier were too few: round 6,
+//    1024->256 @ 14 68 -> 53 us, 512->128 @ 28 91 -> 82, 256->1024 @ 14 113 -> 107,
+//    profiles/r6/bnbwd1x1_k256.md);
 //  * 1x1 forwards with one 64-channel K-tile (the layer-1/2 channel-expanding convs): no
 //    DMA ring (NB = 1), 3 workgroups per CU;
 //  * 128-wide output tiles: 32-deep K-tiles on a 3-deep ring where the grid has >= 1024
@@ -613,6 +616,7 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 //  * 64-wide output tiles: 32-deep K-tiles on a 3-deep ring (layer-1 3x3 64@56 fwd
 //    111 -> 106 us, dgrad 103 -> 99 us).
 int g_bnbwd_early = 1;  // BN-backward epilogue prefetch at kernel start for small K (A/B switch)
+// (the 64-row tile rule below depends on K too: conv_bnbwd_mtiles mirrors it)
 
 template <int MODE, int EPI = 0>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
@@ -620,7 +624,7 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
                      const ConvBnEpi& ep = ConvBnEpi{}) {
   if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
-  if (EPI == 1 && MODE == kFwd1 && g.NC % 128 == 0 && g.M >= 50176) {
+  if (EPI == 1 && MODE == kFwd1 && g.NC % 128 == 0 && g.M >= 50176 && g.KC < 256) {
     const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
     // K <= 128 (two to four 32-deep K-tiles): the epilogue's loads go out at kernel start
     // and fly under the K loop's DMA (64 -> 256 @ 56 +skip: 324 -> 307 us, 128 -> 512
@@ -1956,10 +1960,10 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
   else launch_conv_tap<kFwd1>(xp, wp, yp, g, st, stats_slab, stats_shift);
 }
 
-int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize) {
+int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize, int Cin) {
   const int64_t M = (int64_t)N * H * W;
   // launch_conv_tap's M tile with the BN-backward epilogue (64 rows for the large 1x1s)
-  if (ksize == 1 && Cout % 128 == 0 && M >= 50176) return (int)((M + 63) / 64);
+  if (ksize == 1 && Cout % 128 == 0 && M >= 50176 && Cin < 256) return (int)((M + 63) / 64);
   if (ksize == 3 && conv3h_ok(N, H, W, Cout, 1)) return (int)((M + kHBM - 1) / kHBM);
   return (int)((M + kBM - 1) / kBM);
 }

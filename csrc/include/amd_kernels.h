@@ -315,7 +315,7 @@ void conv_nhwc_fwd(const void* x, const void* w, void* y, int N, int H, int W, i
                    const float* stats_shift = nullptr);
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize, int Cin);
 // M tiles (slab rows) of conv_nhwc_fwd_bnbwd's stride-1 launch
-int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize);
+int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize, int Cin);
 // BatchNorm-backward epilogue of a data-gradient conv (conv_nhwc_fwd on dY with the
 // rotated / transposed filter): the conv output o (+ add, the residual gradient) is
 // the gradient of a BN(+ReLU) output; the kernel stores g = relu_mask(x) * o instead

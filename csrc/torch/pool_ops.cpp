@@ -195,7 +195,7 @@ std::tuple<at::Tensor, at::Tensor> conv_nhwc_fwd_bnbwd_op(
   dy = dy.contiguous(cl);
   w = w.contiguous(cl);
   at::Tensor g = at::empty({N, Cout, H, W}, dy.options().memory_format(cl));
-  const int S = conv_bnbwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)k);
+  const int S = conv_bnbwd_mtiles((int)N, (int)H, (int)W, (int)Cout, (int)k, (int)Cin);
   at::Tensor slab = at::empty({2, Cout, S}, dy.options().dtype(at::kFloat));
   conv_nhwc_fwd_bnbwd(dy.data_ptr(), w.data_ptr(), g.data_ptr(), (int)N, (int)H, (int)W,
                       (int)Cin, (int)Cout, (int)k, 1, ep, slab.data_ptr<float>(), cur_stream());

@@ -37,6 +37,7 @@ def _bf(t):
     (4, 64, 56, 56, 256, 1),     # expanding 1x1 dgrad (bottleneck conv1 <- previous bn3)
     (3, 256, 14, 14, 64, 1),     # M = 588: partial last tile
     (16, 64, 56, 56, 256, 1),    # M = 50,176: 64-row tiles, S = 784
+    (16, 256, 56, 56, 128, 1),   # M = 50,176 but K = 256: 128-row tiles, S = 392
 ])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("with_add", [False, True])

@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+set -eu
+cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/r6k256
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest -x -q -p no:cacheprovider --timeout 150 --timeout-method thread \
+  tests/test_conv_bn_bwd_gpu.py tests/test_conv_bn_stats_gpu.py > $out/tests.log 2>&1
+bash tools/gpu_runs/r6/ab_tree.sh resnet50
