@@ -408,7 +408,8 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 
 #define CONV_ISSUE(kt_)                                                                     \
   {                                                                                         \
-    const int tap_ = (kt_) / kc_per_tap;                                                    \
+    /* 1x1 modes have one tap: no per-K-tile scalar division */                             \
+    const int tap_ = (MODE == kFwd1 || MODE == kDgrad1) ? 0 : (kt_) / kc_per_tap;           \
     const int c0_ = ((kt_) - tap_ * kc_per_tap) * BK;                                       \
     int dh_, dw_, wt_;                                                                      \
     conv_tap<MODE>(z, tap_, dh_, dw_, wt_);                                                 \
