@@ -681,7 +681,7 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
 // halo buffer in piece pairs during taps 0-3.  One counted vmcnt wait + one barrier per
 // step.  80 KiB of LDS: two workgroups per CU, so one's barrier / DMA issue hides under
 // the other's MFMAs.  Tile 256 x BN (4 waves of 128 x 64 for BN = 128, 64 x 64 for 64).
-constexpr int kHBM = 256;                  // output pixels per workgroup
+constexpr int kHBM = 256;                  // output pixels per workgroup (224: a variant)
 // halo rows per buffer: 448 (7 DMA row blocks, 28 KiB) next to the 128-wide weight ring,
 // 512 (32 KiB) next to the 64-wide one - either way 80 KiB in all
 constexpr int halo_rows(int BN) { return BN == 128 ? 448 : 512; }
@@ -712,12 +712,13 @@ __device__ __forceinline__ void vm_wait_c() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BN, int EPI>
+template <int BN, int EPI, int BM_ = kHBM>
 __global__ void __launch_bounds__(kCT, 2)
     conv3h_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt,
              bf16_t* __restrict__ y, ConvGeom g, float* __restrict__ slab,
              const float* __restrict__ shift, ConvBnEpi ep) {
-  constexpr int BM = kHBM, CT = kCT, WM = BN == 128 ? 2 : 4, WN = 4 / WM;
+  constexpr int BM = BM_, CT = kCT, WM = BN == 128 ? 2 : 4, WN = 4 / WM;
+  static_assert(BM % (16 * WM) == 0, "16-row fragments per wave");
   constexpr int kHRows = halo_rows(BN), kHBuf = kHRows * 64;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int BSLOT = BN * 64;           // BN weight rows x 32 channels
@@ -951,14 +952,15 @@ __global__ void __launch_bounds__(kCT, 2)
   }
 }
 
-// Largest halo window (rows) of any 256-pixel tile of an N x H x W raster, cached per
+// Largest halo window (rows) of any BM-pixel tile of an N x H x W raster, cached per
 // shape (the launch path asks once per conv call).
-int halo_rows_max(int N, int H, int W) {
-  struct Ent { int n, h, w, r; };
-  static Ent cache[16];
+int halo_rows_max(int N, int H, int W, int BM) {
+  struct Ent { int n, h, w, bm, r; };
+  static Ent cache[32];
   static int filled = 0;
   for (int i = 0; i < filled; ++i)
-    if (cache[i].n == N && cache[i].h == H && cache[i].w == W) return cache[i].r;
+    if (cache[i].n == N && cache[i].h == H && cache[i].w == W && cache[i].bm == BM)
+      return cache[i].r;
   const int64_t M = (int64_t)N * H * W;
   const int HW = H * W, Wp = W + 2;
   auto pp = [&](int64_t p) {
@@ -966,46 +968,74 @@ int halo_rows_max(int N, int H, int W) {
     return (n * (H + 2) + h + 1) * Wp + w + 1;
   };
   int64_t r = 0;
-  for (int64_t m0 = 0; m0 < M; m0 += kHBM) {
-    const int64_t p1 = std::min<int64_t>(m0 + kHBM, M) - 1;
+  for (int64_t m0 = 0; m0 < M; m0 += BM) {
+    const int64_t p1 = std::min<int64_t>(m0 + BM, M) - 1;
     r = std::max<int64_t>(r, pp(p1) - pp(m0) + 2 * Wp + 3);
   }
   const int res = (int)std::min<int64_t>(r, 1 << 30);
-  if (filled < 16) cache[filled++] = Ent{N, H, W, res};
+  if (filled < 32) cache[filled++] = Ent{N, H, W, BM, res};
   return res;
 }
 
 // 0: off, 1: automatic tile width, 64 / 128: that width wherever it is possible (A/B)
 int g_conv_halo = 1;
+// pixel tile: 0 automatic, 224 / 256 forced (A/B)
+int g_conv_halo_bm = 0;
 
-// Output-tile width of the halo kernel for a 3x3 conv, 0 = not eligible: 128 wide where
-// Cout allows and the window fits 448 rows, else 64 wide (512-row window).  Measured
-// (profiles/r6/conv_halo.md, batch 256, vs conv_tap_k): 128@28 fwd / +stats / +BN-bwd
-// 93 / 97 / 110 -> 85 / 78 / 87 us, 256@14 79 / 82 / 81 -> 63 / 64 / 69, 512@7 (64
-// wide) 75 / 77 / 72 -> 66 / 67 / 69, 64@56 (64 wide) 102 / 110 / 147 -> 79 / 93 / 120.
-// (Cin % 64 == 0 is conv3x3_nhwc_supported's.)
+// Tile of the halo kernel for a 3x3 conv, {0, 0} = not eligible.  Width 128 where Cout
+// allows and the window fits 448 rows, else 64 (512-row window).  Measured (profiles/r6/
+// conv_halo.md, batch 256, vs conv_tap_k): 128@28 fwd / +stats / +BN-bwd 93 / 97 / 110 ->
+// 85 / 78 / 87 us, 256@14 79 / 82 / 81 -> 63 / 64 / 69, 512@7 (64 wide) 75 / 77 / 72 ->
+// 66 / 67 / 69, 64@56 (64 wide) 102 / 110 / 147 -> 79 / 93 / 120.  Pixel tile 256 or 224:
+// the one with the smaller (rounds of 512 workgroup slots - two per CU) x tile work, so a
+// grid that would leave a mostly empty last round, or fill one round only partly, takes
+// the 12.5 % shorter tiles (128 wide only).  (Cin % 64 == 0 is conv3x3_nhwc_supported's.)
+struct Conv3hCfg {
+  int bn, bm;
+};
+Conv3hCfg conv3h_cfg(int N, int H, int W, int Cout, int stride) {
+  if (g_conv_halo == 0 || stride != 1 || N <= 0 || Cout % 64 != 0) return {0, 0};
+  const int64_t M = (int64_t)N * H * W;
+  Conv3hCfg best{0, 0};
+  double best_cost = 1e300;
+  for (int bm : {256, 224}) {
+    if (g_conv_halo_bm != 0 && bm != g_conv_halo_bm) continue;
+    const int r = halo_rows_max(N, H, W, bm);
+    for (int bn : {128, 64}) {
+      if (bn == 128 && (Cout % 128 != 0 || g_conv_halo == 64)) continue;
+      if (bn == 64 && bm != 256) continue;  // 4 x 1 waves: 56-row wave tiles don't exist
+      if (r > halo_rows(bn)) continue;
+      const int64_t tiles = (M + bm - 1) / bm * (Cout / bn);
+      const int64_t rounds = (tiles + 511) / 512;
+      // 64-wide tiles do 64 x 64 per wave (vs 128 x 64): ~5 % less efficient per FLOP
+      const double cost = (double)rounds * bm * bn * (bn == 64 ? 1.05 : 1.0);
+      if (cost < best_cost * 0.999) {
+        best_cost = cost;
+        best = {bn, bm};
+      }
+    }
+  }
+  return best;
+}
 int conv3h_bn(int N, int H, int W, int Cout, int stride) {
-  if (g_conv_halo == 0 || stride != 1 || N <= 0 || Cout % 64 != 0) return 0;
-  const int r = halo_rows_max(N, H, W);
-  const bool w128 = Cout % 128 == 0 && r <= halo_rows(128);
-  const bool w64 = r <= halo_rows(64);
-  if (g_conv_halo == 64 && w64) return 64;
-  if (w128) return 128;
-  return w64 ? 64 : 0;
+  return conv3h_cfg(N, H, W, Cout, stride).bn;
 }
 bool conv3h_ok(int N, int H, int W, int Cout, int stride) {
   return conv3h_bn(N, H, W, Cout, stride) != 0;
 }
+int conv3h_mtile(int N, int H, int W, int Cout) { return conv3h_cfg(N, H, W, Cout, 1).bm; }
 
 template <int EPI>
 void launch_conv3h(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g, int N,
                    hipStream_t st, float* slab, const float* shift, const ConvBnEpi& ep) {
-  const int bn = conv3h_bn(N, g.GH, g.GW, g.NC, 1);
-  const dim3 grid((g.M + kHBM - 1) / kHBM, g.NC / bn, 1);
-  if (bn == 128)
-    hipLaunchKernelGGL((conv3h_k<128, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  const Conv3hCfg c = conv3h_cfg(N, g.GH, g.GW, g.NC, 1);
+  const dim3 grid((g.M + c.bm - 1) / c.bm, g.NC / c.bn, 1);
+  if (c.bn == 128 && c.bm == 256)
+    hipLaunchKernelGGL((conv3h_k<128, EPI, 256>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+  else if (c.bn == 128)
+    hipLaunchKernelGGL((conv3h_k<128, EPI, 224>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   else
-    hipLaunchKernelGGL((conv3h_k<64, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
+    hipLaunchKernelGGL((conv3h_k<64, EPI, 256>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
 }
 
 // ============================================================================
@@ -1894,6 +1924,7 @@ void conv1x1_transpose_weight(const void* w, void* out, int Cout, int Cin, hipSt
 }
 
 void conv_halo_enable(int mode) { g_conv_halo = mode; }
+void conv_halo_mtile(int bm) { g_conv_halo_bm = bm; }
 void conv_bnbwd_early(int mode) { g_bnbwd_early = mode; }
 int conv_halo_enabled() { return g_conv_halo; }
 
@@ -1924,7 +1955,10 @@ bool conv_1x1_on_gemm4w(int64_t M, int Cin, int Cout) { return conv1x1_g4w(M, Ci
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize, int Cin) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int64_t M = (int64_t)N * Ho * Wo;
-  if (ksize == 3 && conv3h_ok(N, H, W, Cout, stride)) return (int)((M + kHBM - 1) / kHBM);
+  if (ksize == 3 && conv3h_ok(N, H, W, Cout, stride)) {
+    const int bm = conv3h_mtile(N, H, W, Cout);
+    return (int)((M + bm - 1) / bm);
+  }
   if (ksize == 1 && conv1x1_g4w(M, Cin, Cout, stride)) return (int)((M + 255) / 256);
   return (int)((M + kBM - 1) / kBM);  // launch_conv_tap's M tile (EPI 0)
 }
@@ -1965,7 +1999,10 @@ int conv_bnbwd_mtiles(int N, int H, int W, int Cout, int ksize, int Cin) {
   const int64_t M = (int64_t)N * H * W;
   // launch_conv_tap's M tile with the BN-backward epilogue (64 rows for the large 1x1s)
   if (ksize == 1 && Cout % 128 == 0 && M >= 50176 && Cin < 256) return (int)((M + 63) / 64);
-  if (ksize == 3 && conv3h_ok(N, H, W, Cout, 1)) return (int)((M + kHBM - 1) / kHBM);
+  if (ksize == 3 && conv3h_ok(N, H, W, Cout, 1)) {
+    const int bm = conv3h_mtile(N, H, W, Cout);
+    return (int)((M + bm - 1) / bm);
+  }
   return (int)((M + kBM - 1) / kBM);
 }
 void conv_nhwc_fwd_bnbwd(const void* dy, const void* w, void* gout, int N, int H, int W, int Cin,

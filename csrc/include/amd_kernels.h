@@ -301,6 +301,8 @@ bool conv3x3_nhwc_supported(int Cin, int Cout);
 // unless disabled here: mode 0 off, 1 automatic, 64 / 128 force that output-tile width
 // where possible (A/B switch; the M tile, hence the stats slab width, follows)
 void conv_halo_enable(int mode);
+// halo kernel pixel tile: 0 automatic (by grid rounds), 224 / 256 forced (A/B)
+void conv_halo_mtile(int bm);
 int conv_halo_enabled();
 void conv_bnbwd_early(int mode);
 // stride-1 1x1 forwards with Cout % 256 == 0 on gemm4w (statistics epilogue): 0 off, 1 the

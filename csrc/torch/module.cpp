@@ -159,6 +159,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "3x3 stride-1 convs on the halo-resident kernel: 0 off, 1 auto, 64 / 128 force "
            "that output-tile width where possible");
   conv.def("halo_enabled", &conv_halo_enabled);
+  conv.def("set_halo_mtile", &conv_halo_mtile, py::arg("bm"));
   conv.def("set_bnbwd_early", &conv_bnbwd_early);
   conv.def("set_1x1_gemm4w", &conv_1x1_gemm4w);
   conv.def("on_gemm4w_1x1", &conv_1x1_on_gemm4w, py::arg("M"), py::arg("Cin"), py::arg("Cout"));

@@ -31,6 +31,7 @@ def halo_switch():
     was = C.conv.halo_enabled()
     yield C.conv.set_halo
     C.conv.set_halo(was)
+    C.conv.set_halo_mtile(0)
 
 
 SHAPES = [
@@ -55,9 +56,9 @@ def _run(C, x, w, shift, xb, add, mean, invstd, bw, bb):
     return y, ys, slab, g0, s0, g1, s1
 
 
-@pytest.mark.parametrize("mode", [1, 64])
+@pytest.mark.parametrize("mode,bm", [(1, 256), (1, 224), (64, 256)])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_halo_conv_matches_fp32_and_tap_kernel(shape, mode, halo_switch):
+def test_halo_conv_matches_fp32_and_tap_kernel(shape, mode, bm, halo_switch):
     N, Ci, H, W, Co = shape
     C = _C()
     torch.manual_seed(3)
@@ -72,13 +73,16 @@ def test_halo_conv_matches_fp32_and_tap_kernel(shape, mode, halo_switch):
     args = (x, w, shift, xb, add, mean, invstd, bw, bb)
     M = N * H * W
 
+    C.conv.set_halo_mtile(bm)           # 224-pixel tiles exist for the 128-wide kernel only
     halo_switch(mode)
     h = _run(C, *args)
     halo_switch(0)
     t = _run(C, *args)
+    halo_switch(mode)
     assert t[2].shape[2] == (M + 127) // 128
-    tiles = (M + 255) // 256
-    assert h[2].shape[2] == tiles, "the halo kernel did not run"
+    halo = not (bm == 224 and Co % 128 != 0)
+    tiles = (M + bm - 1) // bm if halo else (M + 127) // 128
+    assert h[2].shape[2] == tiles, "the halo kernel did not run" if halo else "unexpected"
 
     ref = F.conv2d(x.float(), w.float(), padding=1)
     scale = float(ref.abs().max())
@@ -116,7 +120,6 @@ def test_halo_conv_matches_fp32_and_tap_kernel(shape, mode, halo_switch):
         torch.testing.assert_close(ss[1], (gd * (xd - mean.double())).sum(0), rtol=1e-5, atol=1e-3)
 
     # deterministic: a second run is bitwise identical
-    halo_switch(mode)
     for i, (a, b) in enumerate(zip(h, _run(C, *args))):
         assert torch.equal(a, b), i
 
