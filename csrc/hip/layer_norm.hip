@@ -288,8 +288,9 @@ __global__ void __launch_bounds__(kLNThreads)
     ln_bwd_fast(const T* __restrict__ dy, const T* __restrict__ x, const TW* __restrict__ gamma,
                 const float* __restrict__ mean, const float* __restrict__ invvar,
                 T* __restrict__ dx, float* __restrict__ part, int64_t n1, int n2, int rms,
-                LnFuse fu = LnFuse{}) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [kLNWaves][R][n2]
+                int one = 0, LnFuse fu = LnFuse{}) {
+  // [kLNWaves][R][n2] per-wave partial rows, or [R][n2] with `one` (A/B, off by default)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int R = HS ? 3 : 2;
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
@@ -390,6 +391,34 @@ __global__ void __launch_bounds__(kLNThreads)
   }
 
   if (!want_part) return;
+  float* out = part + (size_t)blockIdx.x * R * n2;
+  if (one) {
+    // ONE [R][n2] LDS row set, the waves adding in turn (wave 0 first: the same order, hence
+    // bits, as the per-wave rows below).  Meant to lift the LDS limit of the fp32 GPT-2
+    // join (48 KB per block: 3 blocks per CU, below the 5 its registers allow); measured
+    // slower end to end (GPT-2-medium 262 vs 264 k tok/s, BERT-large 700.6 vs 705.2 seq/s
+    // same box, profiles/r6/ln_ab/), so off by default (layer_norm_bwd_one_row)
+#pragma unroll
+    for (int w = 0; w < kLNWaves; ++w) {
+      if (wid == w) {
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
+          int col = (k * kWave + lane) * 8;
+          if (col >= n2) continue;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            float* c = lds + col + i;
+            c[0] = (w == 0 ? 0.f : c[0]) + adg[k][i];
+            c[n2] = (w == 0 ? 0.f : c[n2]) + adb[k][i];
+            if constexpr (HS) c[2 * n2] = (w == 0 ? 0.f : c[2 * n2]) + adh[k][i];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    for (int c = threadIdx.x; c < R * n2; c += blockDim.x) out[c] = 0.f + lds[c];
+    return;
+  }
   // combine the block's waves in LDS, then one partial row pair per block
   float* my = lds + (size_t)wid * R * n2;
 #pragma unroll
@@ -404,7 +433,6 @@ __global__ void __launch_bounds__(kLNThreads)
     }
   }
   __syncthreads();
-  float* out = part + (size_t)blockIdx.x * R * n2;
   for (int c = threadIdx.x; c < R * n2; c += blockDim.x) {
     float s = 0.f;
 #pragma unroll
@@ -555,10 +583,15 @@ static inline int ln_generic_parts(int64_t n1) {
   return (int)(p > 0 ? p : 1);
 }
 
+static int g_ln_one = 0;
+void layer_norm_bwd_one_row(int on) { g_ln_one = on; }
+bool layer_norm_bwd_one_row_on() { return g_ln_one != 0; }
+static inline int64_t ln_bwd_lds_rows() { return g_ln_one ? 1 : kLNWaves; }
+
 // the dh column sums need a third [kLNWaves][n2] LDS row: within the 64 KB of dynamic LDS
-// a launch gets without a raised attribute (n2 <= 1365)
+// a launch gets without a raised attribute (n2 <= 1365; any fast-path n2 with one row set)
 bool layer_norm_bwd_hsum_ok(int64_t n2) {
-  return (int64_t)kLNWaves * 3 * n2 * (int64_t)sizeof(float) <= 65536;
+  return ln_bwd_lds_rows() * 3 * n2 * (int64_t)sizeof(float) <= 65536;
 }
 
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2) {
@@ -586,7 +619,7 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
       int nparts;
       if (fuse) {  // caller checked alignment / width (layer_norm_fused_ok + dy, dres, dh)
         int blocks = ln_bwd_blocks(n1);
-        size_t lds = want_wb ? (size_t)kLNWaves * R * n2 * sizeof(float) : 0;
+        size_t lds = want_wb ? (size_t)ln_bwd_lds_rows() * R * n2 * sizeof(float) : 0;
         float* pp = want_wb ? part : nullptr;
         dim3 grid(blocks), block(kLNThreads);
         auto launch = [&](auto h0) {
@@ -596,10 +629,10 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
           auto go = [&](auto hs0) {
             constexpr bool HS = decltype(hs0)::value;
             switch (ln_vpt(n2)) {
-              case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-              case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-              case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
-              default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, *fuse); break;
+              case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one, *fuse); break;
+              case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one, *fuse); break;
+              case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one, *fuse); break;
+              default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4, true, TH, TY, HS>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one, *fuse); break;
             }
           };
           if (R == 3) go(std::true_type{});
@@ -611,14 +644,14 @@ void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, 
       } else if (ln_fast_ok(x, gamma, nullptr, dx, n2) && ((uintptr_t)dy % 16) == 0) {
         int vpt = ln_vpt(n2);
         int blocks = ln_bwd_blocks(n1);
-        size_t lds = want_wb ? (size_t)kLNWaves * 2 * n2 * sizeof(float) : 0;
+        size_t lds = want_wb ? (size_t)ln_bwd_lds_rows() * 2 * n2 * sizeof(float) : 0;
         float* pp = want_wb ? part : nullptr;
         dim3 grid(blocks), block(kLNThreads);
         switch (vpt) {
-          case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
-          case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
-          case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
-          default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms); break;
+          case 1: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 1>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one); break;
+          case 2: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 2>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one); break;
+          case 3: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 3>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one); break;
+          default: hipLaunchKernelGGL((ln_bwd_fast<T, TW, 4>), grid, block, lds, st, dyp, xp, gp, mean, invvar, dxp, pp, n1, (int)n2, rms, g_ln_one); break;
         }
         nparts = blocks;
       } else {

@@ -189,6 +189,10 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2);
 // whether the fused-join backward can also form the dh column sums (LnFuse::dhsum) for n2
 bool layer_norm_bwd_hsum_ok(int64_t n2);
+// backward partial combine through one [R][n2] LDS row set instead of per-wave rows (A/B,
+// default off: measured slower end to end)
+void layer_norm_bwd_one_row(int on);
+bool layer_norm_bwd_one_row_on();
 void layer_norm_bwd(const void* dy, const void* x, DType tx, const void* gamma, DType tw,
                     const float* mean, const float* invvar, void* dx, void* dgamma, void* dbeta,
                     float* part, int64_t n1, int64_t n2, int rms, hipStream_t st,

@@ -97,6 +97,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   ln.def("backward", &layer_norm_backward_op);
   ln.def("add_dropout_forward", &add_dropout_layer_norm_forward_op);
   ln.def("add_dropout_backward", &add_dropout_layer_norm_backward_op);
+  ln.def("set_bwd_one_row", &layer_norm_bwd_one_row);
+  ln.def("bwd_one_row", &layer_norm_bwd_one_row_on);
 
   auto attn = m.def_submodule("attn", "fused attention (head dim 64, MFMA, gfx950)");
   attn.def("fwd", &attn_fwd_op);

@@ -18,8 +18,9 @@ def _rel(a, b):
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("n2", [1024, 2048])
 def test_join_dh_colsum_matches_reference(dtype, p, n2):
-    """n2 = 2048 needs more than 64 KB of LDS for the third partial row: no column sums
-    are offered there (the dense layer sums dh itself)."""
+    """n2 = 2048 needs more than 64 KB of LDS for the third per-wave partial row: no
+    column sums are offered there (the dense layer sums dh itself) unless the one-row-set
+    combine (layer_norm.set_bwd_one_row, off by default) is on."""
     from apex_example_amd import _native
     from apex_example_amd.normalization import FusedLayerNorm, fused_add_dropout_layer_norm
 
@@ -44,7 +45,7 @@ def test_join_dh_colsum_matches_reference(dtype, p, n2):
         H.clear()
     assert _native.available()
     dh, cs = captured["dh"], captured["cs"]
-    if n2 > 1365:
+    if n2 > 1365 and not _native.require().layer_norm.bwd_one_row():
         assert cs is None
         return
     assert cs is not None and cs.dtype == dtype and cs.shape == (n2,)
@@ -99,3 +100,36 @@ def test_bert_layer_takes_handoff_and_matches(monkeypatch, p):
         else:
             assert torch.equal(g_on[n], g_off[n]), n
     assert FD._bias_grad is not None
+
+
+@pytest.mark.parametrize("xdt,hdt", [(torch.float32, torch.float16), (torch.bfloat16, torch.bfloat16)])
+def test_join_one_row_combine_bitwise(xdt, hdt):
+    """The one-row-set LDS combine of the LayerNorm backward partials (A/B switch) adds the
+    waves in the per-wave rows' order: dgamma / dbeta / dx bitwise equal."""
+    from apex_example_amd import _native
+    from apex_example_amd.normalization import FusedLayerNorm
+    from apex_example_amd.normalization.fused_layer_norm import AddDropoutLayerNormFunction
+
+    L = _native.require().layer_norm
+    torch.manual_seed(2)
+    n2 = 1024
+    ln = FusedLayerNorm(n2).to(DEV).to(xdt)
+    x = torch.randn(4096, n2, device=DEV, dtype=xdt)
+    h = torch.randn(4096, n2, device=DEV, dtype=hdt)
+
+    def run(one):
+        L.set_bwd_one_row(one)
+        try:
+            xa, ha = x.clone().requires_grad_(True), h.clone().requires_grad_(True)
+            ln.weight.grad = ln.bias.grad = None
+            torch.manual_seed(5)
+            y, s = AddDropoutLayerNormFunction.apply(xa, ha, ln.weight, ln.bias,
+                                                     ln.normalized_shape, ln.eps, 0.1, True)
+            torch.manual_seed(6)
+            (y.float() * torch.randn_like(y, dtype=torch.float32)).sum().backward()
+            return [xa.grad, ha.grad, ln.weight.grad.clone(), ln.bias.grad.clone()]
+        finally:
+            L.set_bwd_one_row(0)
+
+    for a, b in zip(run(0), run(1)):
+        assert torch.equal(a, b)
