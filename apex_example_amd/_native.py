@@ -34,6 +34,8 @@ def _load():
         _C.conv.set_halo(int(os.environ.get("APEX_AMD_CONV_HALO", "1")))
         # its pixel-tile height: 0 = per-shape cost model (default), 224 / 256 force one
         _C.conv.set_halo_mtile(int(os.environ.get("APEX_AMD_CONV_HALO_BM", "0")))
+        # conv_tap_k tile order (N tiles fastest): 0 off, 1 by shape (default), 2 all
+        _C.conv.set_nfast(int(os.environ.get("APEX_AMD_CONV_NFAST", "1")))
         # stride-1 1x1 forwards with Cout % 256 on gemm4w (statistics epilogue):
         # APEX_AMD_CONV_1X1_G4W = 0 off (default: slower in the model, see conv_igemm.hip),
         # 1 the per-shape winners, 2 every eligible shape

@@ -356,8 +356,13 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int mt = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = mt * BM, n0 = blockIdx.y * BN;
+  // tile order: with gridDim.y == 1 the N tiles are folded into x, N fastest (a launch
+  // with N tiles > 1 on y walks every M tile per N tile): consecutive tiles on one XCD
+  // then share the A rows (one L2 fill per M tile instead of one per N tile)
+  const int NTf = gridDim.y == 1 ? g.NC / BN : 1;
+  const int lt = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lt / NTf, MTn = (int)gridDim.x / NTf;
+  const int m0 = mt * BM, n0 = (gridDim.y == 1 ? lt - mt * NTf : (int)blockIdx.y) * BN;
   // parity classes of a stride-2 3x3 dgrad in longest-first order: blockIdx.z is
   // dispatched slowest, so the 4-tap class (z = 3) goes out first and the 1-tap class
   // fills the tail (ResNet-50 shapes 118 -> 107, 103 -> 90, 93 -> 82 us,
@@ -591,7 +596,7 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
       // channel-major [2][C][S] (S = M tiles x parity classes, blockIdx.z after the M
       // tiles): consecutive M tiles run on one XCD, so its L2 merges the 4-byte stores of
       // neighbouring workgroups into whole lines
-      const int64_t S = (int64_t)gridDim.x * gridDim.z, s = (int64_t)z * gridDim.x + mt;
+      const int64_t S = (int64_t)MTn * gridDim.z, s = (int64_t)z * MTn + mt;
       slab[(int64_t)(n0 + tid) * S + s] = a;
       slab[(int64_t)(g.NC + n0 + tid) * S + s] = b;
     }
@@ -619,14 +624,33 @@ __global__ void __launch_bounds__(CT, (NB * (BM + BN) * BK * 2 > 80 * 1024)
 int g_bnbwd_early = 1;  // BN-backward epilogue prefetch at kernel start for small K (A/B switch)
 // (the 64-row tile rule below depends on K too: conv_bnbwd_mtiles mirrors it)
 
+// N-fastest tile order (N tiles folded into grid x, see conv_tap_k): 0 off, 1 by shape
+// (default), 2 every conv_tap_k launch (A/B switch).  Per call, same box
+// (profiles/r6/nfast/bench*.md, tools/diag/nfast_bench.py): 512 -> 2048 @ 7 51.2 -> 47.6 us,
+// 2048 -> 512 @ 7 43.0 -> 37.4, 256 -> 1024 @ 14 58.0 -> 54.9, the BN-backward 1x1 dgrads
+// 65.2 -> 58.6 / 52.8 -> 45.5 / 82.3 -> 77.2, 64 -> 256 @ 56 172.6 -> 161.7 - but the
+// 4-N-tile launches over >= 1024 M tiles (the @ 28 expansions, 128 -> 512 and the stride-2
+// 256 -> 512 projection) lose (78.0 -> 89.4, 113.4 -> 125.8): those keep M fastest.
+// ResNet-50 (folding every 1x1 launch): 12,367 / 12,228 vs 12,174 / 12,060 img/s.
+int g_conv_nfast = 1;
+
+inline dim3 conv_grid(int mtiles, int ntiles, int nclasses, bool one_by_one) {
+  (void)one_by_one;
+  const bool fold = ntiles > 1 && (g_conv_nfast == 2 ||
+                                   (g_conv_nfast == 1 && !(ntiles == 4 && mtiles >= 1024)));
+  return fold ? dim3((unsigned)(mtiles * ntiles), 1, nclasses)
+              : dim3((unsigned)mtiles, (unsigned)ntiles, nclasses);
+}
+
 template <int MODE, int EPI = 0>
 void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g,
                      hipStream_t st, float* slab = nullptr, const float* shift = nullptr,
                      const ConvBnEpi& ep = ConvBnEpi{}) {
   if (g.M == 0) return;
   const int nclasses = MODE == kDgrad3 || MODE == kDgrad1 ? 4 : 1;
+  constexpr bool k1 = MODE == kFwd1 || MODE == kDgrad1;
   if (EPI == 1 && MODE == kFwd1 && g.NC % 128 == 0 && g.M >= 50176 && g.KC < 256) {
-    const dim3 grid((g.M + 63) / 64, g.NC / 128, nclasses);
+    const dim3 grid = conv_grid((g.M + 63) / 64, g.NC / 128, nclasses, k1);
     // K <= 128 (two to four 32-deep K-tiles): the epilogue's loads go out at kernel start
     // and fly under the K loop's DMA (64 -> 256 @ 56 +skip: 324 -> 307 us, 128 -> 512
     // @ 28: 176 -> 171; at K = 256 the held registers cost a wave per SIMD: 110 -> 115)
@@ -635,16 +659,16 @@ void launch_conv_tap(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 64, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (MODE == kFwd1 && g.NC % 128 == 0 && g.KC / kBK <= 1) {
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
+    const dim3 grid = conv_grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses, k1);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 1, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else if (g.NC % 128 == 0) {
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses);
+    const dim3 grid = conv_grid((g.M + kBM - 1) / kBM, g.NC / 128, nclasses, k1);
     if (grid.x * grid.y * grid.z >= 1024)
       hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
     else
       hipLaunchKernelGGL((conv_tap_k<MODE, 128, 128, 2, 2, 2, EPI>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   } else {
-    const dim3 grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses);
+    const dim3 grid = conv_grid((g.M + kBM - 1) / kBM, g.NC / 64, nclasses, k1);
     hipLaunchKernelGGL((conv_tap_k<MODE, 128, 64, 4, 1, 3, EPI, kCT, 32>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   }
 }
@@ -1950,6 +1974,7 @@ bool conv1x1_g4w(int64_t M, int Cin, int Cout, int stride) {
          (Cin == 64 && Cout == 256);
 }
 void conv_1x1_gemm4w(int mode) { g_conv1x1_g4w = mode; }
+void conv_nfast(int mode) { g_conv_nfast = mode; }
 bool conv_1x1_on_gemm4w(int64_t M, int Cin, int Cout) { return conv1x1_g4w(M, Cin, Cout, 1); }
 
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize, int Cin) {

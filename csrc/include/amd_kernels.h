@@ -305,6 +305,9 @@ bool conv3x3_nhwc_supported(int Cin, int Cout);
 // unless disabled here: mode 0 off, 1 automatic, 64 / 128 force that output-tile width
 // where possible (A/B switch; the M tile, hence the stats slab width, follows)
 void conv_halo_enable(int mode);
+// conv_tap_k tile order: N tiles folded into grid x, N fastest: 0 off, 1 by shape
+// (default), 2 every launch (A/B switch)
+void conv_nfast(int mode);
 // halo kernel pixel tile: 0 automatic (by grid rounds), 224 / 256 forced (A/B)
 void conv_halo_mtile(int bm);
 int conv_halo_enabled();
