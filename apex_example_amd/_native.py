@@ -36,6 +36,7 @@ def _load():
         _C.conv.set_halo_mtile(int(os.environ.get("APEX_AMD_CONV_HALO_BM", "0")))
         # conv_tap_k tile order (N tiles fastest): 0 off, 1 by shape (default), 2 all
         _C.conv.set_nfast(int(os.environ.get("APEX_AMD_CONV_NFAST", "1")))
+        _C.conv.set_halo_nfast(int(os.environ.get("APEX_AMD_CONV_HALO_NFAST", "0")))
         # stride-1 1x1 forwards with Cout % 256 on gemm4w (statistics epilogue):
         # APEX_AMD_CONV_1X1_G4W = 0 off (default: slower in the model, see conv_igemm.hip),
         # 1 the per-shape winners, 2 every eligible shape

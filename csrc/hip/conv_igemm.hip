@@ -760,8 +760,11 @@ __global__ void __launch_bounds__(kCT, 2)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int mt = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = mt * BM, n0 = blockIdx.y * BN;
+  // N tiles folded into grid x when gridDim.y == 1 (N fastest, as conv_tap_k)
+  const int NTf = gridDim.y == 1 ? g.NC / BN : 1;
+  const int lt = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lt / NTf, MTn = (int)gridDim.x / NTf;
+  const int m0 = mt * BM, n0 = (gridDim.y == 1 ? lt - mt * NTf : (int)blockIdx.y) * BN;
   const int H = g.GH, W = g.GW, HW = H * W, Wp = W + 2, HpWp = (H + 2) * Wp;
   const int M = g.M, KC = g.KC;
   const int p1 = min(m0 + BM, M) - 1;
@@ -969,7 +972,7 @@ __global__ void __launch_bounds__(kCT, 2)
         a += red[q * BN + tid];
         b += red[RGS * BN + q * BN + tid];
       }
-      const int64_t S = gridDim.x;
+      const int64_t S = MTn;
       slab[(int64_t)(n0 + tid) * S + mt] = a;
       slab[(int64_t)(g.NC + n0 + tid) * S + mt] = b;
     }
@@ -1049,11 +1052,19 @@ bool conv3h_ok(int N, int H, int W, int Cout, int stride) {
 }
 int conv3h_mtile(int N, int H, int W, int Cout) { return conv3h_cfg(N, H, W, Cout, 1).bm; }
 
+// halo kernel tile order: N tiles folded into grid x, N fastest (1) or on grid y (0).
+// Neutral per call (its M tiles' windows are small next to the weights re-read per tap)
+// and ResNet-50 12,136 / 12,140 vs 12,220 / 12,214 img/s same box (profiles/r6/nfast/halo/):
+// off by default (A/B switch)
+int g_conv3h_nfast = 0;
+
 template <int EPI>
 void launch_conv3h(const bf16_t* a, const bf16_t* w, bf16_t* y, const ConvGeom& g, int N,
                    hipStream_t st, float* slab, const float* shift, const ConvBnEpi& ep) {
   const Conv3hCfg c = conv3h_cfg(N, g.GH, g.GW, g.NC, 1);
-  const dim3 grid((g.M + c.bm - 1) / c.bm, g.NC / c.bn, 1);
+  const int mtiles = (g.M + c.bm - 1) / c.bm, ntiles = g.NC / c.bn;
+  const dim3 grid = g_conv3h_nfast && ntiles > 1 ? dim3((unsigned)(mtiles * ntiles), 1, 1)
+                                                 : dim3((unsigned)mtiles, (unsigned)ntiles, 1);
   if (c.bn == 128 && c.bm == 256)
     hipLaunchKernelGGL((conv3h_k<128, EPI, 256>), grid, dim3(kCT), 0, st, a, w, y, g, slab, shift, ep);
   else if (c.bn == 128)
@@ -1975,6 +1986,7 @@ bool conv1x1_g4w(int64_t M, int Cin, int Cout, int stride) {
 }
 void conv_1x1_gemm4w(int mode) { g_conv1x1_g4w = mode; }
 void conv_nfast(int mode) { g_conv_nfast = mode; }
+void conv_halo_nfast(int on) { g_conv3h_nfast = on; }
 bool conv_1x1_on_gemm4w(int64_t M, int Cin, int Cout) { return conv1x1_g4w(M, Cin, Cout, 1); }
 
 int conv_fwd_mtiles(int N, int H, int W, int Cout, int stride, int ksize, int Cin) {

@@ -308,6 +308,7 @@ void conv_halo_enable(int mode);
 // conv_tap_k tile order: N tiles folded into grid x, N fastest: 0 off, 1 by shape
 // (default), 2 every launch (A/B switch)
 void conv_nfast(int mode);
+void conv_halo_nfast(int on);  // the same for the halo 3x3 kernel (A/B)
 // halo kernel pixel tile: 0 automatic (by grid rounds), 224 / 256 forced (A/B)
 void conv_halo_mtile(int bm);
 int conv_halo_enabled();

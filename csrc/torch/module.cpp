@@ -158,6 +158,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("transpose_weight", &conv1x1_transpose_weight_op);
   conv.def("prep_weights", &conv_prep_weights_op);
   conv.def("set_nfast", &conv_nfast, py::arg("mode"));
+  conv.def("set_halo_nfast", &conv_halo_nfast, py::arg("on"));
   conv.def("set_halo", &conv_halo_enable, py::arg("mode"),
            "3x3 stride-1 convs on the halo-resident kernel: 0 off, 1 auto, 64 / 128 force "
            "that output-tile width where possible");

@@ -34,8 +34,8 @@ def timeit(fn, n=20):
     return ts[len(ts) // 2]
 
 
-print("| shape (N,Cin,H,W,Cout) | op | per-tap us | halo auto us | halo 256-px tiles us | halo 64-wide us | TFLOP/s auto |")
-print("|---|---|---|---|---|---|---|")
+print("| shape (N,Cin,H,W,Cout) | op | per-tap us | halo auto us | halo auto, N tiles fastest us | halo 256-px tiles us | halo 64-wide us | TFLOP/s auto |")
+print("|---|---|---|---|---|---|---|---|")
 for (N, Ci, H, W, Co) in SHAPES:
     x = bf(torch.randn(N, Ci, H, W, device=dev))
     w = bf(torch.randn(Co, Ci, 3, 3, device=dev) / (Ci * 9) ** 0.5)
@@ -54,11 +54,14 @@ for (N, Ci, H, W, Co) in SHAPES:
         t0 = timeit(fn)
         C.conv.set_halo(1)
         t1 = timeit(fn)
+        C.conv.set_halo_nfast(1)
+        t4 = timeit(fn)
+        C.conv.set_halo_nfast(0)
         C.conv.set_halo_mtile(256)
         t3 = timeit(fn)
         C.conv.set_halo_mtile(0)
         C.conv.set_halo(64)
         t2 = timeit(fn)
-        print("| %s | %s | %.1f | %.1f | %.1f | %.1f | %.0f |" % (
-            (N, Ci, H, W, Co), name, t0, t1, t3, t2, flop / t1 / 1e6), flush=True)
+        print("| %s | %s | %.1f | %.1f | %.1f | %.1f | %.1f | %.0f |" % (
+            (N, Ci, H, W, Co), name, t0, t1, t4, t3, t2, flop / t1 / 1e6), flush=True)
 C.conv.set_halo(1)
