@@ -152,6 +152,8 @@ class ResNet(nn.Module):
             self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3,
                                    bias=False)
         self.bn1 = _BNAct(self.inplanes, True, fused_bn)
+        if isinstance(self.conv1, StemConv2d):
+            _link_stats(self.conv1, self.bn1)  # stem BN statistics from the stem epilogue
         pool = MaxPool2dNHWC if fused_bn else nn.MaxPool2d
         self.maxpool = pool(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0], 1, zero_init_residual)

@@ -907,11 +907,18 @@ class StemConvFunction(torch.autograd.Function):
     training from data) falls back to MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, bn=None):
         cv = _native.require().conv
         xp = cv.stem_pad(x)
         ctx.save_for_backward(x, xp, weight)
-        return cv.stem_fwd(xp, _pack_stem_weight(weight))
+        if bn is None:
+            return cv.stem_fwd(xp, _pack_stem_weight(weight))
+        # the stem BN's statistics from the kernel's epilogue (handed to the module, which
+        # tags the output; ops/pool.py bn_relu_maxpool or the BN consume it)
+        shift = _shift_of(bn)
+        y, slab = cv.stem_fwd_stats(xp, _pack_stem_weight(weight), shift)
+        _TLS.slab = (slab, shift, bn)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
@@ -926,7 +933,7 @@ class StemConvFunction(torch.autograd.Function):
             dx = torch.ops.aten.convolution_backward(
                 dy, x, weight, None, (2, 2), (3, 3), (1, 1), False, (0, 0), 1,
                 (True, False, False))[0]
-        return dx, dw
+        return dx, dw, None
 
 
 class StemConv2d(nn.Conv2d):
@@ -941,5 +948,5 @@ class StemConv2d(nn.Conv2d):
                 and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
                 and x.size(2) % 2 == 0 and x.size(3) % 2 == 0 and x.size(3) <= 250
                 and self.in_channels == 3):
-            return StemConvFunction.apply(x, self.weight)
+            return _tag_stats(StemConvFunction.apply(x, self.weight, _stats_bn(self, x)))
         return F.conv2d(x, self.weight, None, self.stride, self.padding)

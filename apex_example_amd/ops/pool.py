@@ -16,6 +16,8 @@ from .. import _native
 
 # A/B switch for the fused stem (tools, docs/PERF.md)
 _FUSE_STEM = True
+# its backward: the BN-backward sums inside the max-pool gather (csrc/hip/pool.hip BNR)
+_FUSE_STEM_BWD = True
 _GAP_KERNEL = True
 
 
@@ -47,10 +49,15 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, nbt, eps, momentum, k, s, p,
-                pg=None):
+                pg=None, slab=None, shift=None):
         C = _native.require()
         inv_total = None
-        if pg is None:
+        count = x.numel() // x.size(1)
+        if pg is None and slab is not None:
+            # statistics from the stem conv's epilogue slab (no pass over x)
+            mean, invstd = C.bn.slab_train_stats(slab, count, shift, running_mean, running_var,
+                                                 nbt, float(eps), float(momentum))
+        elif pg is None:
             mean, invstd = C.bn.train_stats(x, running_mean, running_var, nbt, float(eps),
                                             float(momentum))
         else:
@@ -58,7 +65,8 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
             # (one all_gather of [mean | var | count]), then the fused pool pass
             import torch.distributed as dist
             world = dist.get_world_size(pg)
-            packed = C.bn.local_stats_packed(x)
+            packed = (C.bn.slab_packed_stats(slab, count, shift) if slab is not None
+                      else C.bn.local_stats_packed(x))
             gathered = torch.empty(world * packed.numel(), dtype=packed.dtype, device=x.device)
             if dist.get_backend(pg) == "nccl":
                 dist.all_gather_into_tensor(gathered, packed, group=pg)
@@ -78,14 +86,22 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
         x, weight, bias, mean, invstd, idx = ctx.saved_tensors
         H, W, k, s, p = ctx.geom
         C = _native.require()
-        dbn = C.pool.max_bwd(dy, idx, H, W, k, s, p)
         need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        if ctx.pg is None:
+        if (ctx.pg is None and _FUSE_STEM_BWD and (k, s, p) == (3, 2, 1) and x.size(1) == 64
+                and x.element_size() == 2 and dy.dtype == x.dtype):
+            # the BN-backward sums formed inside the pooling gather (one pass over x instead
+            # of a reduction pass over dbn and x)
+            dbn, slab = C.pool.max_bwd_bn(dy, idx, H, W, x, mean, invstd, weight, bias)
+            sum_dy, sum_dy_xmu, gw, gb = C.bn.slab_reduce_grad(slab, invstd, weight, need_w)
+            count = float(x.numel() // x.size(1))
+        elif ctx.pg is None:
+            dbn = C.pool.max_bwd(dy, idx, H, W, k, s, p)
             sum_dy, sum_dy_xmu, gw, gb = C.bn.reduce_grad(dbn, x, mean, invstd, weight, bias,
                                                           None, True, need_w)
             count = float(x.numel() // x.size(1))
         else:
             import torch.distributed as dist
+            dbn = C.pool.max_bwd(dy, idx, H, W, k, s, p)
             sum_dy, sum_dy_xmu, gw, gb = C.bn.reduce_grad(dbn, x, mean, invstd, weight, bias,
                                                           None, True, need_w,
                                                           sum_scale=ctx.inv_total)
@@ -95,7 +111,7 @@ class BNReLUMaxPoolFunction(torch.autograd.Function):
         dx, _ = C.bn.backward_elemt(dbn, x, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
                                     count, None, True, False)
         return (dx, gw if need_w else None, gb if need_w else None,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)
 
 
 def _stem_pg(bn):
@@ -135,10 +151,13 @@ def bn_relu_maxpool_fusable(x, bn, pool):
 
 
 def bn_relu_maxpool(x, bn, pool):
+    from .batch_norm import take_slab
+
+    slab, shift = take_slab(x, bn)  # the stem conv's epilogue statistics, if it wrote them
     return BNReLUMaxPoolFunction.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                        bn.num_batches_tracked, bn.eps, bn.momentum,
                                        pool.kernel_size, pool.stride, pool.padding,
-                                       _stem_pg(bn))
+                                       _stem_pg(bn), slab, shift)
 
 
 class MaxPool2dNHWC(nn.MaxPool2d):

@@ -16,6 +16,7 @@
 
 #include "amd_dev.h"
 #include "amd_kernels.h"
+#include "bn_common.h"
 
 namespace amd {
 
@@ -263,13 +264,36 @@ __global__ void __launch_bounds__(kPoolThreads)
 // loads of a thread serve 4 input pixels instead of 1 (the per-input form below issues
 // 4x the loads for the same bytes).  Per input the contributions are summed in the
 // per-input kernel's order ((oh, ow) row-major), so the two are bitwise equal.
-template <typename T>
+//
+// BNR (the fused stem's backward, C == 64): dx is the gradient of relu(BN(x)); the kernel
+// also forms the BatchNorm-backward sums of the pre-ReLU gradient d = dx * (BN(x) > 0)
+// (ReLU condition recomputed from x exactly as reduce_k does, d taken as the stored 16-bit
+// dx): sum(d), sum(d * (x - mean)) per channel into a channel-major slab [2][64][gridDim.x]
+// - the separate reduction pass over dx and x (822 MB at ResNet-50 bs 256) disappears; x
+// is read here once instead.  A thread's channel group (t % 8) is fixed: the grid stride is
+// a multiple of 8.
+template <typename T, bool BNR = false>
 __global__ void __launch_bounds__(kPoolThreads)
     maxpool3s2_bwd2_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
-                      T* __restrict__ dx, int N, int H, int W, int C, int OH, int OW) {
+                      T* __restrict__ dx, int N, int H, int W, int C, int OH, int OW,
+                      const T* __restrict__ xin = nullptr, const float* __restrict__ mean = nullptr,
+                      const float* __restrict__ invstd = nullptr,
+                      const float* __restrict__ bw = nullptr, const float* __restrict__ bb = nullptr,
+                      float* __restrict__ slab = nullptr) {
   static_assert(sizeof(T) == 2, "16-bit activations");
   const int CV = C / 8, BH = (H + 1) / 2, BW = (W + 1) / 2;
   const int64_t total = (int64_t)N * BH * BW * CV;
+  float mu[8], sc[8], sh[8], s1[8], s2[8];
+  if constexpr (BNR) {
+    const int cg = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) % CV);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int ch = cg * 8 + c;
+      mu[c] = mean[ch];
+      chan_affine(mean, invstd, bw ? bw[ch] : 1.f, bb ? bb[ch] : 0.f, ch, sc[c], sh[c]);
+      s1[c] = s2[c] = 0.f;
+    }
+  }
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int cv = (int)(t % CV);
@@ -324,8 +348,49 @@ __global__ void __launch_bounds__(kPoolThreads)
               if (tap_of(q, c) == kh * 3 + kw) acc[c] += g[q][c];
           }
         }
-        store8(dx + (((int64_t)n * H + h) * W + w) * C + cv * 8, acc);
+        const int64_t o = (((int64_t)n * H + h) * W + w) * C + cv * 8;
+        store8(dx + o, acc);
+        if constexpr (BNR) {
+          float xv[8];
+          unpack8_any<T>(*reinterpret_cast<const p_u32x4*>(xin + o), xv);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const float g = to_f32(from_f32<T>(acc[c]));  // as stored
+            const float d = fmaf(xv[c], sc[c], sh[c]) > 0.f ? g : 0.f;
+            s1[c] += d;
+            s2[c] = fmaf(d, xv[c] - mu[c], s2[c]);
+          }
+        }
       }
+    }
+  }
+  if constexpr (BNR) {
+    // lanes sharing a channel group: t % 8 == lane % 8 -> xor 8, 16, 32; then the waves
+    __shared__ float red[2][kPoolThreads / 64][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+      for (int m = 8; m < 64; m <<= 1) {
+        s1[c] += __shfl_xor(s1[c], m);
+        s2[c] += __shfl_xor(s2[c], m);
+      }
+    }
+    if (lane < 8) {
+      const int cg = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) % CV);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        red[0][wv][cg * 8 + c] = s1[c];
+        red[1][wv][cg * 8 + c] = s2[c];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const int q = threadIdx.x >> 6, ch = threadIdx.x & 63;
+      float a = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < kPoolThreads / 64; ++w2) a += red[q][w2][ch];
+      slab[((int64_t)q * 64 + ch) * gridDim.x + blockIdx.x] = a;
     }
   }
 }
@@ -418,6 +483,31 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
   });
 }
 
+int maxpool_bwd_bn_grid(int N, int H, int W) {
+  const int64_t blk = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * 8;
+  const int g = pool_grid(blk);
+  return g > 2048 ? 2048 : g;
+}
+
+bool maxpool2d_nhwc_bwd_bn_ok(int H, int W, int C, int OH, int OW, int k, int s, int p) {
+  return C == 64 && stem_ok(k, s, p, H, W, OH, OW);
+}
+
+void maxpool2d_nhwc_bwd_bn(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
+                           int W, int C, int OH, int OW, const void* x, const float* mean,
+                           const float* invstd, const float* bw, const float* bb, float* slab,
+                           hipStream_t st) {
+  const int grid = maxpool_bwd_bn_grid(N, H, W);
+  pool_dispatch(t, [&](auto t0) {
+    using T = decltype(t0);
+    if constexpr (sizeof(T) == 2) {
+      hipLaunchKernelGGL((maxpool3s2_bwd2_k<T, true>), dim3(grid), dim3(kPoolThreads), 0, st,
+                         static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C, OH, OW,
+                         static_cast<const T*>(x), mean, invstd, bw, bb, slab);
+    }
+  });
+}
+
 void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
                         int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
   const bool vec = C % 8 == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0 &&
@@ -429,7 +519,7 @@ void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, i
     if constexpr (sizeof(T) == 2) {
       if (vec && stem_ok(k, s, p, H, W, OH, OW)) {
         const int64_t blk = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
-        hipLaunchKernelGGL((maxpool3s2_bwd2_k<T>), dim3(pool_grid(blk)), dim3(kPoolThreads), 0,
+        hipLaunchKernelGGL((maxpool3s2_bwd2_k<T, false>), dim3(pool_grid(blk)), dim3(kPoolThreads), 0,
                            st, static_cast<const T*>(dy), idx, static_cast<T*>(dx), N, H, W, C,
                            OH, OW);
         return;

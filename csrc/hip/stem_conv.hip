@@ -90,7 +90,7 @@ template <int IB>
 __global__ void __launch_bounds__(kStemWaves * 64, 1)
     stem_fwd_k(const bf16_t* __restrict__ xp, const bf16_t* __restrict__ wk,
                bf16_t* __restrict__ y, int Hp, int Wp, int Ho, int Wo, int total_rows,
-               int rows_per_wave) {
+               int rows_per_wave, float* __restrict__ slab, const float* __restrict__ shift) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[kStemLds];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   unsigned char* ring = lds + wid * kRing * kSlot;
@@ -104,7 +104,40 @@ __global__ void __launch_bounds__(kStemWaves * 64, 1)
   __syncthreads();
   const int t0 = (blockIdx.x * kStemWaves + wid) * rows_per_wave;
   const int t1 = t0 + rows_per_wave < total_rows ? t0 + rows_per_wave : total_rows;
-  if (t0 >= t1) return;  // wave-uniform, after the only workgroup barrier
+  // BatchNorm statistics of y for the stem BN (slab != null): a lane's output stores all
+  // cover the same 8 channels (lane & 7), so it sums the bf16-ROUNDED values it stores
+  // (exactly what y holds), shifted by the BN's running mean, and each wave writes one
+  // column s of the channel-major slab [2][64][S] (S = waves in the grid) - the BN's
+  // separate statistics pass over y (411 MB at bs 256) disappears.
+  const int S = (int)gridDim.x * kStemWaves, sidx = (int)blockIdx.x * kStemWaves + wid;
+  const int scg = lane & 7;
+  float s1[8], s2[8], shv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s1[i] = s2[i] = 0.f;
+    shv[i] = (slab != nullptr && shift != nullptr) ? shift[scg * 8 + i] : 0.f;
+  }
+  auto write_stats = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int m = 8; m < 64; m <<= 1) {
+        s1[i] += __shfl_xor(s1[i], m);
+        s2[i] += __shfl_xor(s2[i], m);
+      }
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        slab[(int64_t)(lane * 8 + i) * S + sidx] = s1[i];
+        slab[(int64_t)(64 + lane * 8 + i) * S + sidx] = s2[i];
+      }
+    }
+  };
+  if (t0 >= t1) {  // wave-uniform, after the only workgroup barrier
+    if (slab != nullptr) write_stats();
+    return;
+  }
   const int cpr = Wp / 2;  // 16-byte chunks per padded row
   const int fr = lane & 15, fg = lane >> 4;
 
@@ -173,7 +206,21 @@ __global__ void __launch_bounds__(kStemWaves * 64, 1)
         const int px = h * 8 + (lane >> 3), c = lane & 7;
         const uint4 v = *reinterpret_cast<const uint4*>(X + px * 128 + ((c ^ (px & 7)) << 4));
         const int p = 16 * i + px;
-        if (p < Wo) *reinterpret_cast<uint4*>(yrow + p * 64 + c * 8) = v;
+        if (p < Wo) {
+          *reinterpret_cast<uint4*>(yrow + p * 64 + c * 8) = v;
+          if (slab != nullptr) {
+            const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float lo = __uint_as_float(wv[q] << 16) - shv[2 * q];
+              const float hi = __uint_as_float(wv[q] & 0xffff0000u) - shv[2 * q + 1];
+              s1[2 * q] += lo;
+              s2[2 * q] = fmaf(lo, lo, s2[2 * q]);
+              s1[2 * q + 1] += hi;
+              s2[2 * q + 1] = fmaf(hi, hi, s2[2 * q + 1]);
+            }
+          }
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -186,6 +233,7 @@ __global__ void __launch_bounds__(kStemWaves * 64, 1)
     }
     key0 = key1;
   }
+  if (slab != nullptr) write_stats();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -337,11 +385,19 @@ void stem_pad(const void* x, void* xp, int N, int H, int W, hipStream_t st) {
                      static_cast<const bf16_t*>(x), static_cast<bf16_t*>(xp), N, H, W);
 }
 
-void stem_fwd(const void* xp, const void* wk, void* y, int N, int H, int W, hipStream_t st) {
+int stem_fwd_grid(int N, int H) {
+  const int total_rows = N * (H / 2);
+  const int grid = (total_rows + kStemWaves - 1) / kStemWaves;
+  return grid > 256 ? 256 : grid;
+}
+
+int stem_fwd_slab_width(int N, int H) { return stem_fwd_grid(N, H) * kStemWaves; }
+
+void stem_fwd(const void* xp, const void* wk, void* y, int N, int H, int W, hipStream_t st,
+              float* slab, const float* shift) {
   const int Hp = H + 6, Wp = W + 6, Ho = H / 2, Wo = W / 2;
   const int total_rows = N * Ho;
-  int grid = (total_rows + kStemWaves - 1) / kStemWaves;
-  if (grid > 256) grid = 256;
+  const int grid = stem_fwd_grid(N, H);
   const int rpw = (total_rows + grid * kStemWaves - 1) / (grid * kStemWaves);
   const auto* xpp = static_cast<const bf16_t*>(xp);
   const auto* wkp = static_cast<const bf16_t*>(wk);
@@ -349,7 +405,7 @@ void stem_fwd(const void* xp, const void* wk, void* y, int N, int H, int W, hipS
   const int ib = (Wo + 15) / 16;
 #define STEM_FWD(IB)                                                                          \
   hipLaunchKernelGGL((stem_fwd_k<IB>), dim3(grid), dim3(kStemWaves * 64), 0, st, xpp, wkp, yp, \
-                     Hp, Wp, Ho, Wo, total_rows, rpw)
+                     Hp, Wp, Ho, Wo, total_rows, rpw, slab, shift)
   if (ib <= 1) STEM_FWD(1);
   else if (ib <= 2) STEM_FWD(2);
   else if (ib <= 4) STEM_FWD(4);

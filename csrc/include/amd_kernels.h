@@ -255,6 +255,15 @@ void maxpool2d_nhwc_fwd(const void* x, DType t, void* y, uint8_t* idx, int N, in
                         const float* bw = nullptr, const float* bb = nullptr);
 void maxpool2d_nhwc_bwd(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
                         int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
+// the 3x3 / stride-2 / pad-1 backward of the fused stem (C == 64, 16-bit) that also writes the
+// BatchNorm + ReLU backward sums of dx: slab [2][64][maxpool_bwd_bn_grid(N, H, W)] of
+// sum(d), sum(d * (x - mean)) with d = dx * (x * invstd*w + b - mean*invstd*w > 0)
+bool maxpool2d_nhwc_bwd_bn_ok(int H, int W, int C, int OH, int OW, int k, int s, int p);
+int maxpool_bwd_bn_grid(int N, int H, int W);
+void maxpool2d_nhwc_bwd_bn(const void* dy, const uint8_t* idx, DType t, void* dx, int N, int H,
+                           int W, int C, int OH, int OW, const void* x, const float* mean,
+                           const float* invstd, const float* bw, const float* bb, float* slab,
+                           hipStream_t st);
 // global average pool backward: dx[N, HW, C] (channels-last) = dy[N, C] / HW
 void gap_nhwc_bwd(const void* dy, DType t, void* dx, int64_t N, int64_t HW, int C,
                   hipStream_t st);
@@ -402,8 +411,12 @@ bool stem_conv_supported(int N, int H, int W);
 // x [N][H][W][3] -> xp [N][H+6][W+6][4] (zero border, zero 4th channel)
 void stem_pad(const void* x, void* xp, int N, int H, int W, hipStream_t st);
 // wk: packed filter [64][7][32] (wk[co][r][4s+c] = W[co][c][r][s], zeros elsewhere);
-// y [N][H/2][W/2][64]
-void stem_fwd(const void* xp, const void* wk, void* y, int N, int H, int W, hipStream_t st);
+// y [N][H/2][W/2][64]; with `slab` also the BatchNorm statistics of y (sums of y - shift and
+// (y - shift)^2 per channel, shift may be null) as a channel-major slab [2][64][S],
+// S = stem_fwd_slab_width(N, H)
+void stem_fwd(const void* xp, const void* wk, void* y, int N, int H, int W, hipStream_t st,
+              float* slab = nullptr, const float* shift = nullptr);
+int stem_fwd_slab_width(int N, int H);
 // fp32 partials [S][64][256] of the packed filter gradient (n = 32 r + 4 s + c)
 int stem_wgrad_splits(int N, int H);
 void stem_wgrad(const void* xp, const void* dy, float* part, int S, int N, int H, int W,

@@ -135,6 +135,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto pool = m.def_submodule("pool", "NHWC max pooling (gather backward, no atomics)");
   pool.def("max_fwd", &maxpool2d_nhwc_fwd_op);
   pool.def("max_bwd", &maxpool2d_nhwc_bwd_op);
+  pool.def("max_bwd_bn", &maxpool2d_nhwc_bwd_bn_op, py::arg("dy"), py::arg("idx"), py::arg("H"),
+           py::arg("W"), py::arg("x"), py::arg("mean"), py::arg("invstd"),
+           py::arg("weight") = py::none(), py::arg("bias") = py::none());
   pool.def("gap_bwd", &gap_nhwc_bwd_op, py::arg("dy"), py::arg("H"), py::arg("W"));
   pool.def("max_fwd_bn", &maxpool2d_nhwc_bn_fwd_op);
   auto conv = m.def_submodule("conv", "MFMA implicit-GEMM convolutions (NHWC bf16)");
@@ -153,6 +156,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("out") = py::none(), py::arg("accumulate") = true);
   conv.def("stem_pad", &stem_pad_op);
   conv.def("stem_fwd", &stem_fwd_op);
+  conv.def("stem_fwd_stats", &stem_fwd_stats_op, py::arg("xp"), py::arg("wk"),
+           py::arg("shift") = py::none());
   conv.def("stem_wgrad", &stem_wgrad_op);
   conv.def("rot_weight", &conv3x3_rot_weight_op);
   conv.def("transpose_weight", &conv1x1_transpose_weight_op);

@@ -59,6 +59,46 @@ at::Tensor maxpool2d_nhwc_bwd_op(at::Tensor dy, at::Tensor idx, int64_t H, int64
   return dx;
 }
 
+// the fused stem's max-pool backward with the BatchNorm + ReLU backward sums (slab [2][64][S]
+// for bn.slab_reduce_grad); null when the shape is not the stem's (the caller falls back)
+std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_bwd_bn_op(at::Tensor dy, at::Tensor idx,
+                                                            int64_t H, int64_t W, at::Tensor x,
+                                                            at::Tensor mean, at::Tensor invstd,
+                                                            c10::optional<at::Tensor> weight,
+                                                            c10::optional<at::Tensor> bias) {
+  c10::NoGradGuard no_grad_;
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  idx = idx.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == at::kByte, "bad pool index");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(0) == N && x.size(1) == C && x.size(2) == H &&
+                  x.size(3) == W && x.scalar_type() == dy.scalar_type() &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "max_bwd_bn: x must be the pooled BN input [N, C, H, W], channels-last, dy's dtype");
+  TORCH_CHECK(dy.element_size() == 2 &&
+                  maxpool2d_nhwc_bwd_bn_ok((int)H, (int)W, (int)C, (int)OH, (int)OW, 3, 2, 1),
+              "max_bwd_bn: 3x3 / stride-2 / pad-1 pooling of 64 16-bit channels only");
+  auto f32c = [&](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() == C && t.is_contiguous(),
+                "max_bwd_bn: ", what, " must be fp32 [C]");
+    return t.data_ptr<float>();
+  };
+  const float* mp = f32c(mean, "mean");
+  const float* ip = f32c(invstd, "invstd");
+  const float* wp = weight.has_value() && weight->defined() ? f32c(*weight, "weight") : nullptr;
+  const float* bp = bias.has_value() && bias->defined() ? f32c(*bias, "bias") : nullptr;
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor slab = at::empty({2, C, (int64_t)maxpool_bwd_bn_grid((int)N, (int)H, (int)W)},
+                              dy.options().dtype(at::kFloat));
+  TORCH_CHECK((uintptr_t)dy.data_ptr() % 16 == 0 && (uintptr_t)dx.data_ptr() % 16 == 0 &&
+                  (uintptr_t)x.data_ptr() % 16 == 0 && (uintptr_t)idx.data_ptr() % 8 == 0,
+              "max_bwd_bn: 16-byte aligned tensors expected");
+  maxpool2d_nhwc_bwd_bn(dy.data_ptr(), idx.data_ptr<uint8_t>(), dtype_of(dy), dx.data_ptr(),
+                        (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW, x.data_ptr(), mp, ip,
+                        wp, bp, slab.data_ptr<float>(), cur_stream());
+  return {dx, slab};
+}
+
 at::Tensor gap_nhwc_bwd_op(at::Tensor dy, int64_t H, int64_t W) {
   c10::NoGradGuard no_grad_;
   TORCH_CHECK(dy.is_cuda() && (dy.dim() == 2 || dy.dim() == 4), "gap_bwd: dy [N, C(, 1, 1)]");
@@ -294,6 +334,32 @@ at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk) {
                            xp.options().memory_format(at::MemoryFormat::ChannelsLast));
   stem_fwd(xp.data_ptr(), wk.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, cur_stream());
   return y;
+}
+
+// stem_fwd_op plus the stem BatchNorm's statistics slab [2][64][S] from the kernel's
+// epilogue (shift: the BN's running mean, or none)
+std::tuple<at::Tensor, at::Tensor> stem_fwd_stats_op(at::Tensor xp, at::Tensor wk,
+                                                     c10::optional<at::Tensor> shift) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(xp.is_cuda() && xp.dim() == 4 && xp.size(3) == 4 && xp.is_contiguous() &&
+                  xp.scalar_type() == at::kBFloat16, "stem_fwd: padded input [N, H+6, W+6, 4]");
+  TORCH_CHECK(wk.is_cuda() && wk.numel() == 64 * 224 && wk.is_contiguous() &&
+                  wk.scalar_type() == at::kBFloat16, "stem_fwd: packed filter [64, 7, 32]");
+  const int64_t N = xp.size(0), H = xp.size(1) - 6, W = xp.size(2) - 6;
+  TORCH_CHECK(stem_conv_supported((int)N, (int)H, (int)W), "stem_fwd: unsupported size");
+  const float* sp = nullptr;
+  if (shift.has_value() && shift->defined()) {
+    TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->numel() == 64 &&
+                    shift->is_contiguous(), "stem_fwd_stats: shift must be fp32 [64]");
+    sp = shift->data_ptr<float>();
+  }
+  at::Tensor y = at::empty({N, 64, H / 2, W / 2},
+                           xp.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor slab = at::empty({2, 64, (int64_t)stem_fwd_slab_width((int)N, (int)H)},
+                              xp.options().dtype(at::kFloat));
+  stem_fwd(xp.data_ptr(), wk.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, cur_stream(),
+           slab.data_ptr<float>(), sp);
+  return {y, slab};
 }
 
 at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy) {

@@ -36,6 +36,13 @@ at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype,
                             c10::optional<at::Tensor> out_acc, bool accumulate = true);
 at::Tensor stem_pad_op(at::Tensor x);
 at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk);
+std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_bwd_bn_op(at::Tensor dy, at::Tensor idx,
+                                                            int64_t H, int64_t W, at::Tensor x,
+                                                            at::Tensor mean, at::Tensor invstd,
+                                                            c10::optional<at::Tensor> weight,
+                                                            c10::optional<at::Tensor> bias);
+std::tuple<at::Tensor, at::Tensor> stem_fwd_stats_op(at::Tensor xp, at::Tensor wk,
+                                                     c10::optional<at::Tensor> shift);
 at::Tensor stem_wgrad_op(at::Tensor xp, at::Tensor dy);
 at::Tensor conv3x3_rot_weight_op(at::Tensor w);
 at::Tensor conv1x1_transpose_weight_op(at::Tensor w);

@@ -891,6 +891,72 @@ def test_stem_conv_mfma(shape):
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=1e-2 * ws)
 
 
+@pytest.mark.parametrize("shape", [(2, 32, 32), (3, 64, 48), (4, 224, 224), (2, 18, 250)])
+@pytest.mark.parametrize("with_shift", [False, True])
+def test_stem_conv_stats_epilogue(shape, with_shift):
+    """stem_fwd_stats: y bitwise equal to stem_fwd, and the [2][64][S] slab sums equal
+    sum(y - shift), sum((y - shift)^2) of the stored bf16 y (fp64 reference)."""
+    from apex_example_amd import _native
+    from apex_example_amd.ops.conv import _pack_stem_weight
+
+    cv = _native.require().conv
+    n, h, w = shape
+    torch.manual_seed(4)
+    x = torch.randn(n, 3, h, w, device=DEV, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    wt = (torch.randn(64, 3, 7, 7, device=DEV) * 0.1).to(torch.bfloat16)
+    xp = cv.stem_pad(x)
+    wk = _pack_stem_weight(wt)
+    y0 = cv.stem_fwd(xp, wk)
+    shift = torch.randn(64, device=DEV) * 0.1 if with_shift else None
+    y1, slab = cv.stem_fwd_stats(xp, wk, shift)
+    assert torch.equal(y0, y1)
+    assert slab.shape[:2] == (2, 64)
+    yd = y1.double().permute(0, 2, 3, 1).reshape(-1, 64)
+    if shift is not None:
+        yd = yd - shift.double()
+    sums = slab.double().sum(2)
+    # fp32 running sums over up to ~2k values per lane: tolerance ~ sqrt(count) ulps
+    tol = 1e-6 * yd.shape[0] ** 0.5
+    torch.testing.assert_close(sums[0], yd.sum(0), rtol=1e-4, atol=tol * yd.abs().max().item())
+    torch.testing.assert_close(sums[1], (yd * yd).sum(0), rtol=1e-4,
+                               atol=tol * (yd * yd).max().item())
+
+
+def test_resnet_stem_bn_stats_from_epilogue():
+    """ResNet-50 stem: the BN statistics taken from the stem kernel's slab give the same
+    running stats and pooled output as the separate statistics pass."""
+    from apex_example_amd.models import resnet50
+    from apex_example_amd.ops import conv as C
+
+    torch.manual_seed(0)
+    m = resnet50(fused_bn=True, gemm_1x1=True).to(DEV).to(memory_format=torch.channels_last)
+    m = m.to(torch.bfloat16)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            mod.float()
+    x = torch.randn(8, 3, 64, 64, device=DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    outs = []
+    for on in (True, False):
+        bn = m.bn1.bn
+        bn.reset_running_stats()
+        old = C._CONV_BN_STATS
+        C._CONV_BN_STATS = on
+        try:
+            y = m.conv1(x)
+            assert (getattr(y, "_amd_bn_stats", None) is not None) == on
+            from apex_example_amd.ops.pool import bn_relu_maxpool
+            p = bn_relu_maxpool(y, bn, m.maxpool)
+        finally:
+            C._CONV_BN_STATS = old
+        outs.append((p.float(), bn.running_mean.clone(), bn.running_var.clone()))
+    (pa, ma, va), (pb, mb, vb) = outs
+    torch.testing.assert_close(ma, mb, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(va, vb, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(pa, pb, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("mn", [(16384, 1024), (333, 4096), (7, 24), (1025, 3072)])
 def test_bias_grad_kernels(dt, mn):
@@ -983,12 +1049,17 @@ def test_mlp_native_backward(activation, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-def test_bn_relu_maxpool_fused_matches_unfused(dt):
+@pytest.mark.parametrize("fuse_bwd", [True, False])
+def test_bn_relu_maxpool_fused_matches_unfused(dt, fuse_bwd, monkeypatch):
     """The ResNet stem's fused BN + ReLU + max-pool (BN applied in the pool's loads)
     vs the unfused fused-BN module + NHWC max-pool: outputs, running stats, counter
-    and every gradient."""
+    and every gradient; with ``fuse_bwd`` the BN-backward sums come from the pooling
+    gather (pool.max_bwd_bn) instead of a reduction pass."""
     from apex_example_amd.ops import BatchNorm2dReLU
+    from apex_example_amd.ops import pool as P
     from apex_example_amd.ops.pool import MaxPool2dNHWC, bn_relu_maxpool, bn_relu_maxpool_fusable
+
+    monkeypatch.setattr(P, "_FUSE_STEM_BWD", fuse_bwd)
 
     torch.manual_seed(0)
     x = (torch.randn(4, 64, 30, 30, device=DEV) * 2 + 0.5).to(dt).to(
@@ -1012,9 +1083,11 @@ def test_bn_relu_maxpool_fused_matches_unfused(dt):
     dy = torch.randn_like(ya)
     ya.backward(dy)
     yb.backward(dy)
-    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(bn_a.weight.grad, bn_b.weight.grad, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(bn_a.bias.grad, bn_b.bias.grad, rtol=1e-5, atol=1e-5)
+    # fused sums: another fp32 summation order (a 16-bit dx may round one step apart)
+    tol = 1e-5 if not (fuse_bwd and dt != torch.float32) else (1e-2 if dt == torch.bfloat16 else 2e-3)
+    torch.testing.assert_close(xa.grad, xb.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(bn_a.weight.grad, bn_b.weight.grad, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(bn_a.bias.grad, bn_b.bias.grad, rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
