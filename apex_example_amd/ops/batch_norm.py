@@ -34,6 +34,22 @@ _BWD_EPI = os.environ.get("APEX_AMD_CONV_BN_BWD", "1") == "1"
 _TLS = threading.local()
 FUSED_BWD_CALLS = [0]  # BN backwards that took the epilogue sums (diagnostics / tests)
 
+# the residual BN's backward sums formed in the consuming BN's elementwise pass
+# (bn.backward_elemt_x2; A/B switch), and a count of the BN backwards that used them
+_X2_BWD = os.environ.get("APEX_AMD_BN_X2", "1") == "1"
+X2_BWD_CALLS = [0]
+
+
+def _x2_target_ok(zc, ctx, weight):
+    """zc (the residual BN's autograd node) can take its sums from ctx's elementwise pass:
+    a local, ReLU-free, residual-free BN over the same rows, weights of one dtype."""
+    return (getattr(zc, "world", 0) == 1 and not getattr(zc, "fuse_relu", True)
+            and not getattr(zc, "has_z", True) and getattr(zc, "count", -1) == ctx.count
+            and not getattr(zc, "shape_channel_last", True) and not ctx.shape_channel_last
+            and (zc.saved_tensors[2] is None) == (weight is None)
+            and (weight is None or zc.saved_tensors[2].dtype == weight.dtype)
+            and zc.saved_tensors[6] is None)
+
 
 class BnBwdSrc:
     """What a stride-1 data-gradient conv that consumes this BN's output needs to do the
@@ -278,6 +294,11 @@ class BatchNormFunction(torch.autograd.Function):
                                           bool(fuse_relu), zl is not None)
             ctx.pg, ctx.world, ctx.fuse_relu, ctx.total, ctx.count = None, 1, bool(fuse_relu), \
                 None, count
+            # a residual input produced by another local BN (ResNet's downsample BN): this
+            # BN's backward may form that BN's sums in its own elementwise pass (_X2_BWD)
+            zg = getattr(z, "grad_fn", None) if z is not None else None
+            ctx.zctx = zg if isinstance(zg, BatchNormFunction._backward_cls) else None
+            ctx.pre = None
             ctx.orig_shape, ctx.has_z, ctx.shape_channel_last = orig_shape, z is not None, \
                 shape_channel_last
             return y.view(orig_shape) if shape_channel_last else y
@@ -400,11 +421,37 @@ class BatchNormFunction(torch.autograd.Function):
             else:
                 sum_dy, sum_dy_xmu, gw, gb = C.slab_reduce_grad(res[1], invstd, weight, need_w)
                 total = float(ctx.count)
+            zc = getattr(ctx, "zctx", None) if ctx.has_z else None
+            if _X2_BWD and zc is not None and ctx.world == 1 and _x2_target_ok(zc, ctx, weight):
+                # dy (= dz) is the residual BN's gradient too: its backward sums ride on
+                # this elementwise pass (reads its input once; no second pass over dy)
+                xd, _, wd, _, md, isd, _ = zc.saved_tensors
+                if C.backward_x2_ok(dyl, xl, xd):
+                    need_wd = wd is not None and (zc.needs_input_grad[2] or zc.needs_input_grad[3])
+                    dx, s1, s2, gw2, gb2 = C.backward_elemt_x2(
+                        dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu, total, xd, md,
+                        isd, wd, need_wd)
+                    zc.pre = (dyl.data_ptr(), dyl._version, s1, s2, gw2, gb2)
+                    return (dx, dyl, gw if need_w else None, gb if need_w else None, None, None,
+                            None, None, None, None, None, None, None, None, None)
             dx, _ = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
                                      total, None, False, False)
             return (dx, dyl if ctx.has_z else None, gw if need_w else None,
                     gb if need_w else None, None, None, None, None, None, None, None, None, None,
                     None, None)
+        pre = getattr(ctx, "pre", None)
+        if pre is not None:
+            ctx.pre = None
+            if pre[0] == dyl.data_ptr() and pre[1] == dyl._version:
+                # sums formed by the consuming BN's elementwise pass (backward_elemt_x2)
+                _, _, sum_dy, sum_dy_xmu, gw, gb = pre
+                X2_BWD_CALLS[0] += 1
+                dx, _ = C.backward_elemt(dyl, xl, mean, invstd, weight, bias, sum_dy, sum_dy_xmu,
+                                         float(ctx.count), None, False, False)
+                if ctx.shape_channel_last:
+                    dx = dx.view(ctx.orig_shape)
+                return (dx, None, gw if need_w else None, gb if need_w else None, None, None,
+                        None, None, None, None, None, None, None, None, None)
         if ctx.world > 1 and xl.is_cuda:
             # SyncBN: the reduce writes (sum_dy | sum_dy_xmu) / global_count into one [2C]
             # buffer (the scale is a device scalar from the forward's combine) -> ONE

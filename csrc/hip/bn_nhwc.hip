@@ -148,6 +148,40 @@ __device__ __forceinline__ void block_slab_write(float (&s1)[W], float (&s2)[W],
   }
 }
 
+// block_slab_write with a CHANNEL-MAJOR slab [2][C][gridDim.x] (the layout the conv epilogues
+// write; bn_slab_reduce_grad reads each channel's partials as one contiguous row - the
+// row-major [blocks][2][C] form read column-wise cost ~40 us per finalize at the
+// elementwise grid's block counts)
+template <int W>
+__device__ __forceinline__ void block_slab_write_cm(float (&s1)[W], float (&s2)[W], int ci,
+                                                    int ri, int ctile, int rows_iter, int c0,
+                                                    int C, float* __restrict__ slab) {
+  __shared__ float lds[2][kBNThreads * W];
+  if (threadIdx.x < rows_iter * ctile) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      lds[0][(ri * ctile + ci) * W + i] = s1[i];
+      lds[1][(ri * ctile + ci) * W + i] = s2[i];
+    }
+  }
+  __syncthreads();
+  if (ri == 0 && c0 < C) {
+    for (int r = 1; r < rows_iter; ++r) {
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        s1[i] += lds[0][(r * ctile + ci) * W + i];
+        s2[i] += lds[1][(r * ctile + ci) * W + i];
+      }
+    }
+    const int64_t S = gridDim.x;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      slab[(int64_t)(c0 + i) * S + blockIdx.x] = s1[i];
+      slab[(int64_t)(C + c0 + i) * S + blockIdx.x] = s2[i];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- statistics
 template <typename T, bool VEC, int U>
 __global__ void __launch_bounds__(kBNThreads)
@@ -338,21 +372,28 @@ __global__ void __launch_bounds__(kBNThreads)
 //                                 k3 = -invstd*w*mean(dy') - k2*mu ;  dz = dy'
 // RM: the ReLU mode of reduce_k, compile time (rows past M load a clamped row; their
 // results are never stored)
-template <typename T, typename TW, bool VEC, int U, int RM>
+//
+// X2: the same pass also forms the backward sums of a SECOND BatchNorm whose output was this
+// one's residual input z (ResNet's downsample BN: its gradient is this BN's d = dy'):
+// sum(d), sum(d * (x2 - mean2)) per block into a channel-major slab2 [2][C][blocks] (for
+// bn_slab_reduce_grad) - that BN's own reduction pass, which re-reads d, disappears.
+template <typename T, typename TW, bool VEC, int U, int RM, bool X2 = false>
 __global__ void __launch_bounds__(kBNThreads)
     backward_k(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean,
                const float* __restrict__ invstd, const TW* __restrict__ w,
                const TW* __restrict__ b, const float* __restrict__ sum_dy,
                const float* __restrict__ sum_dy_xmu, float inv_n,
                const T* __restrict__ z, const uint8_t* __restrict__ rmask, T* __restrict__ dx,
-               T* __restrict__ dz, int64_t M, int C, int ctile, int rows_iter) {
+               T* __restrict__ dz, int64_t M, int C, int ctile, int rows_iter,
+               const T* __restrict__ x2 = nullptr, const float* __restrict__ mean2 = nullptr,
+               float* __restrict__ slab2 = nullptr) {
   constexpr int W = VEC ? 8 : 1;
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
   // the block's channel constants, one channel per thread, staged in LDS (per thread
   // they were ~7 scalar global loads per channel x 8 channels beside 16 rows of data)
-  __shared__ __attribute__((aligned(16))) float s_par[5][kBNBlockChans];
+  __shared__ __attribute__((aligned(16))) float s_par[X2 ? 6 : 5][kBNBlockChans];
   const int cb = blockIdx.y * ctile * W;
   stage_params(C, cb, ctile * W, [&](int c, int k) {
     const float wc = wload(w, c, 1.f);
@@ -363,21 +404,27 @@ __global__ void __launch_bounds__(kBNThreads)
     s_par[2][k] = q1;
     s_par[3][k] = q2;
     s_par[4][k] = -is * wc * mdy - q2 * mean[c];
+    if constexpr (X2) s_par[X2 ? 5 : 0][k] = mean2[c];
   });
-  if (ri >= rows_iter || c0 >= C) return;
+  float t1[W], t2[W], m2[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) t1[i] = t2[i] = m2[i] = 0.f;
+  const bool active = ri < rows_iter && c0 < C;
+  if (!X2 && !active) return;
   float sc[W], sh[W], k1[W], k2[W], k3[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    const int k = c0 - cb + i;
+    const int k = active ? c0 - cb + i : 0;
     sc[i] = s_par[0][k];
     sh[i] = s_par[1][k];
     k1[i] = s_par[2][k];
     k2[i] = s_par[3][k];
     k3[i] = s_par[4][k];
+    if constexpr (X2) m2[i] = s_par[X2 ? 5 : 0][k];
   }
   const int64_t stride = (int64_t)gridDim.x * rows_iter;
-  for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
-    float xv[U][W], dv[U][W], zv[U][W];
+  for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; active && r < M; r += stride * U) {
+    float xv[U][W], dv[U][W], zv[U][W], x2v[X2 ? U : 1][W];
     uint32_t mk[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -388,6 +435,7 @@ __global__ void __launch_bounds__(kBNThreads)
       ldw<T, W>(dy + rc * C + c0, dv[u]);
       if constexpr (RM == 1) mk[u] = rmask[rc * Cb + (c0 >> 3)];
       if constexpr (RM == 2) ldw<T, W>(z + rc * C + c0, zv[u]);
+      if constexpr (X2) ldw<T, W>(x2 + rc * C + c0, x2v[u]);
     }
     asm volatile("" ::: "memory");  // every load of the group issues before any store
 #pragma unroll
@@ -406,11 +454,16 @@ __global__ void __launch_bounds__(kBNThreads)
         }
         dv[u][i] = d;
         xv[u][i] = fmaf(d, k1[i], fmaf(xv[u][i], k2[i], k3[i]));
+        if constexpr (X2) {
+          t1[i] += d;
+          t2[i] = fmaf(d, x2v[u][i] - m2[i], t2[i]);
+        }
       }
       stw<T, W>(dx + rr * C + c0, xv[u]);
       if (dz) stw<T, W>(dz + rr * C + c0, dv[u]);
     }
   }
+  if constexpr (X2) block_slab_write_cm<W>(t1, t2, ci, ri, ctile, rows_iter, c0, C, slab2);
 }
 
 
@@ -747,6 +800,39 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
       });
     });
   });
+}
+
+// nhwc_backward (no ReLU, no z, no mask: the consumer-epilogue path, where dy is already the
+// masked gradient) plus the backward sums and finalize of a second BN over the same rows
+// whose gradient is the same dy: x2 its input, mean2 / invstd2 / w2 its statistics and
+// weight -> sum_dy2, sum_dy_xmu2 (and gw2, gb2 in tw when non-null)
+void nhwc_backward_x2(const void* dy, const void* x, DType tx, const float* mean,
+                      const float* invstd, const void* w, const void* b, DType tw,
+                      const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx,
+                      int64_t M, int64_t C, const void* x2, const float* mean2,
+                      const float* invstd2, float* sum_dy2, float* sum_dy_xmu2, void* gw2,
+                      void* gb2, float* ws, hipStream_t st) {
+  const NGeom g = ngeom(C, true);
+  const int blocks = elem_blocks(M, g, M * C * (tx == DType::F32 ? 4 : 2));
+  bn_dispatch(tx, [&](auto t0) {
+    bn_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      hipLaunchKernelGGL((backward_k<T, TW, true, 2, 0, true>), dim3(blocks, g.cblocks),
+                         dim3(kBNThreads), 0, st, static_cast<const T*>(dy),
+                         static_cast<const T*>(x), mean, invstd, static_cast<const TW*>(w),
+                         static_cast<const TW*>(b), sum_dy, sum_dy_xmu, inv_count,
+                         static_cast<const T*>(nullptr), static_cast<const uint8_t*>(nullptr),
+                         static_cast<T*>(dx), static_cast<T*>(nullptr), M, (int)C, g.ctile,
+                         g.rows_iter, static_cast<const T*>(x2), mean2, ws);
+    });
+  });
+  bn_slab_reduce_grad(ws, blocks, C, invstd2, sum_dy2, sum_dy_xmu2, gw2, gb2, tw, st);
+}
+
+int64_t nhwc_backward_x2_workspace(int64_t M, int64_t C, DType tx) {
+  const NGeom g = ngeom(C, true);
+  return (int64_t)elem_blocks(M, g, M * C * (tx == DType::F32 ? 4 : 2)) * 2 * C;
 }
 
 }  // namespace amd

@@ -188,6 +188,15 @@ void layer_norm_fwd(const void* x, DType tx, const void* gamma, const void* beta
 // must hold layer_norm_bwd_workspace(n1, n2) floats.
 int64_t layer_norm_bwd_workspace(int64_t n1, int64_t n2);
 // whether the fused-join backward can also form the dh column sums (LnFuse::dhsum) for n2
+// nhwc_backward without ReLU / z / mask, plus the reduction (and finalize) of a second BN
+// over the same rows and gradient (X2 mode of backward_k); ws: nhwc_backward_x2_workspace
+void nhwc_backward_x2(const void* dy, const void* x, DType tx, const float* mean,
+                      const float* invstd, const void* w, const void* b, DType tw,
+                      const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx,
+                      int64_t M, int64_t C, const void* x2, const float* mean2,
+                      const float* invstd2, float* sum_dy2, float* sum_dy_xmu2, void* gw2,
+                      void* gb2, float* ws, hipStream_t st);
+int64_t nhwc_backward_x2_workspace(int64_t M, int64_t C, DType tx);
 bool layer_norm_bwd_hsum_ok(int64_t n2);
 // backward partial combine through one [R][n2] LDS row set instead of per-wave rows (A/B,
 // default off: measured slower end to end)

@@ -215,6 +215,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("sum_dy_xmu"), py::arg("count"), py::arg("z"), py::arg("relu"),
          py::arg("want_dz"), py::arg("mask") = py::none());
 
+  bn.def("backward_x2_ok", &bn_backward_x2_ok);
+  bn.def("backward_elemt_x2", &bn_backward_elemt_x2_op, py::arg("dy"), py::arg("x"),
+         py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("bias"),
+         py::arg("sum_dy"), py::arg("sum_dy_xmu"), py::arg("count"), py::arg("x2"),
+         py::arg("mean2"), py::arg("invstd2"), py::arg("weight2"), py::arg("need_wgrad2"));
   bn.def("backward_local", &bn_backward_local_op, py::arg("dy"), py::arg("x"), py::arg("mean"),
          py::arg("invstd"), py::arg("weight"), py::arg("bias"), py::arg("z"), py::arg("relu"),
          py::arg("need_wgrad"), py::arg("want_dz"), py::arg("mask") = py::none());

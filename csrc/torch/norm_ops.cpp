@@ -618,6 +618,64 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
   return {dx, dz};
 }
 
+// backward_elemt (no ReLU / z / mask) plus the backward sums of a SECOND BatchNorm over the
+// same rows whose gradient is this dy (ResNet's downsample BN, whose output was this BN's
+// residual input): (dx, sum_dy2, sum_dy_xmu2, gw2, gb2) - that BN then runs only its
+// elementwise pass.  GPU, channels-last, C % 8 == 0, 16-byte aligned rows only (the caller
+// checks bn.backward_x2_ok).
+bool bn_backward_x2_ok(at::Tensor dy, at::Tensor x, at::Tensor x2) {
+  if (!(dy.is_cuda() && x.is_cuda() && x2.is_cuda())) return false;
+  if (x.sizes() != x2.sizes() || dy.sizes() != x.sizes()) return false;
+  if (x.scalar_type() != x2.scalar_type() || dy.scalar_type() != x.scalar_type()) return false;
+  if (x.scalar_type() == at::kFloat) return false;
+  BNView v = bn_view(x);
+  if (!v.cl || v.C % 8 != 0) return false;
+  for (const at::Tensor* t : {&dy, &x, &x2}) {
+    const at::Tensor c = conform(*t, v);
+    if (!c.is_same(*t) || (uintptr_t)t->data_ptr() % 16 != 0) return false;
+  }
+  return true;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_elemt_x2_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+    at::Tensor sum_dy, at::Tensor sum_dy_xmu, double count, at::Tensor x2, at::Tensor mean2,
+    at::Tensor invstd2, OptT weight2, bool need_wgrad2) {
+  TORCH_CHECK(bn_backward_x2_ok(dy, x, x2), "backward_elemt_x2: see bn_backward_x2_ok");
+  BNView v = bn_view(x);
+  auto f32c = [&](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == v.C,
+                "backward_elemt_x2: ", what, " must be fp32 [C]");
+  };
+  f32c(mean, "mean");
+  f32c(invstd, "invstd");
+  f32c(mean2, "mean2");
+  f32c(invstd2, "invstd2");
+  f32c(sum_dy, "sum_dy");
+  f32c(sum_dy_xmu, "sum_dy_xmu");
+  DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
+  TORCH_CHECK(!has(weight2) || dtype_of(*weight2) == tw,
+              "backward_elemt_x2: both BNs' weights must share a dtype");
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor sum_dy2 = at::empty({v.C}, fopt), sum_dy_xmu2 = at::empty({v.C}, fopt);
+  at::Tensor gw2, gb2;
+  const bool accum = grad_targets(weight2, need_wgrad2, c10::nullopt, c10::nullopt, gw2, gb2);
+  BNAccumScope accum_scope(accum);
+  at::Tensor w = has(weight) ? weight->contiguous() : at::Tensor();
+  at::Tensor b = has(bias) ? bias->contiguous() : at::Tensor();
+  at::Tensor ws = at::empty({nhwc_backward_x2_workspace(v.outer, v.C, dtype_of(x))}, fopt);
+  nhwc_backward_x2(dy.data_ptr(), x.data_ptr(), dtype_of(x), mean.data_ptr<float>(),
+                   invstd.data_ptr<float>(), w.defined() ? w.data_ptr() : nullptr,
+                   b.defined() ? b.data_ptr() : nullptr, tw, sum_dy.data_ptr<float>(),
+                   sum_dy_xmu.data_ptr<float>(), (float)(1.0 / count), dx.data_ptr(), v.outer, v.C,
+                   x2.data_ptr(), mean2.data_ptr<float>(), invstd2.data_ptr<float>(),
+                   sum_dy2.data_ptr<float>(), sum_dy_xmu2.data_ptr<float>(),
+                   gw2.defined() ? gw2.data_ptr() : nullptr, gb2.defined() ? gb2.data_ptr() : nullptr,
+                   ws.data_ptr<float>(), cur_stream());
+  return {dx, sum_dy2, sum_dy_xmu2, gw2, gb2};
+}
+
 // Local (world 1) backward: reduce_grad + backward_elemt.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,

@@ -71,6 +71,12 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
                                                         OptT z, bool relu, bool want_dz,
                                                         OptT mask);
 
+bool bn_backward_x2_ok(at::Tensor dy, at::Tensor x, at::Tensor x2);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_elemt_x2_op(
+    at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
+    at::Tensor sum_dy, at::Tensor sum_dy_xmu, double count, at::Tensor x2, at::Tensor mean2,
+    at::Tensor invstd2, OptT weight2, bool need_wgrad2);
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
     OptT z, bool relu, bool need_wgrad, bool want_dz, OptT mask);
