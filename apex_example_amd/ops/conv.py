@@ -310,6 +310,15 @@ def _g4w_1x1(x, ci, co, m):
             and _native.require().conv.on_gemm4w_1x1(m, ci, co))
 
 
+# Channel-reducing 1x1 forwards consumed by a BatchNorm that run on the own kernel with the
+# statistics epilogue although hipBLASLt alone is faster: the saved statistics pass + its
+# finalize outweigh it (round 6, tools/diag/own1x1_route.py vs the tuned library times of
+# the serialized model profile, profiles/r6/route1x1/): 256 -> 128 @ 56 151 vs 144 + 63 + 7
+# us, 512 -> 256 @ 28 103 vs 83 + 32 + 7, 1024 -> 256 @ 14 43 vs 32 + 11 + 6, 2048 -> 512
+# @ 7 44 vs 38 + 6 + 8; 1024 -> 512 @ 14 stays on the library (77 vs 39 + 6 + 8).
+_OWN1X1_BN = {(256, 128), (512, 256), (1024, 256), (2048, 512)}
+
+
 def _conv1x1_fwd(x, weight, bn=None):
     """y = conv1x1(x) for a channels-last bf16 x: own MFMA kernel, gemm4w or hipBLASLt.
     With ``bn`` (a BatchNorm consuming y) the native kernel also writes its statistics
@@ -320,7 +329,8 @@ def _conv1x1_fwd(x, weight, bn=None):
     co = weight.shape[0]
     own = _own_1x1(x.dtype, ci, co, n * h * w) or _g4w_1x1(x, ci, co, n * h * w)
     if (bn is not None and weight.dtype == torch.bfloat16 and ci % 64 == 0 and co % 64 == 0
-            and (own or co >= ci) and n * h * w < (1 << 31)):
+            and (own or co >= ci or (_USE_OWN1X1 and (ci, co) in _OWN1X1_BN))
+            and n * h * w < (1 << 31)):
         return _conv_fwd(x, weight, 1, bn)
     if own and weight.dtype == torch.bfloat16:
         return _native.require().conv.conv_fwd(x, weight, 1)
