@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batch_norm import BatchNorm2dReLU
+from ..ops.batch_norm import bn_add_bn_relu
 from ..ops.conv import Conv2d1x1, Conv2d3x3, StemConv2d, conv1x1_pair_s2
 from ..ops.pool import (GlobalAvgPool2dNHWC, MaxPool2dNHWC, bn_relu_maxpool,
                         bn_relu_maxpool_fusable)
@@ -106,25 +107,38 @@ class Bottleneck(nn.Module):
         _link_stats(self.conv3, self.bn3)
 
     def forward(self, x):
+        # downsample block with fused BNs: the projection's BN is applied inside bn3's pass
+        # (ops/batch_norm.py bn_add_bn_relu), its output never materialised
+        fuse_ds = self.downsample is not None and self.bn3.fused and self.downsample.bn.fused
+        proj = identity = None
         if (isinstance(self.conv1, Conv2d1x1) and self.downsample is not None
                 and self.downsample.conv.stride == (2, 2)):
             # conv1 and the stride-2 downsample projection read the same input: one
             # Function keeps the projection's input gradient compact (strided pixels
             # only) and conv1's dgrad adds it on the even pixels (ops/conv.py)
             out, proj = conv1x1_pair_s2(self.conv1, self.downsample.conv, x)
-            identity = self.downsample.bn(proj)
         elif isinstance(self.conv1, Conv2d1x1):
             # the block input feeds conv1 and the residual branch (identity or the
             # downsample conv): the two input gradients are summed inside conv1's
             # dgrad GEMM (C += dY @ W into the branch's gradient), not by a separate
             # add kernel over the block input
             out, skip = self.conv1.forward_with_skip(x)
-            identity = skip if self.downsample is None else self.downsample(skip)
+            if self.downsample is None:
+                identity = skip
+            else:
+                proj = self.downsample.conv(skip)
         else:
-            identity = x if self.downsample is None else self.downsample(x)
+            if self.downsample is None:
+                identity = x
+            else:
+                proj = self.downsample.conv(x)
             out = self.conv1(x)
+        if proj is not None and not fuse_ds:
+            identity = self.downsample.bn(proj)
         out = self.bn1(out)
         out = self.bn2(self.conv2(out))
+        if proj is not None and fuse_ds:
+            return bn_add_bn_relu(self.bn3.bn, self.conv3(out), self.downsample.bn.bn, proj)
         return self.bn3(self.conv3(out), identity)
 
 

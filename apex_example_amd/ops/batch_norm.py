@@ -585,3 +585,102 @@ class BatchNorm2dReLU(torch.nn.BatchNorm2d):
                               use_batch, momentum, self.eps, z=z, fuse_relu=self.fuse_relu,
                               process_group=False, num_batches_tracked=nbt,
                               slab=slab if use_batch else None, slab_shift=shift)
+
+
+# ---------------------------------------------------------------- relu(bn3(x) + bn_d(xd))
+# ResNet's downsample block output in ONE apply pass (csrc/hip/bn_nhwc.hip apply_k ZA): the
+# downsample BN's output is formed on load (rounded as its own apply pass would store it, so
+# y and the ReLU mask are bitwise the unfused result) and never written - its apply pass (a
+# read and a write of the tensor) goes; the backward runs bn3's elementwise pass with the
+# downsample BN's sums (backward_elemt_x2) and that BN's elementwise pass.
+_FUSE_DS = os.environ.get("APEX_AMD_BN_DS_FUSE", "1") == "1"
+FUSED_DS_CALLS = [0]
+
+
+class BatchNormAddBNReLUFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, xd, w, b, wd, bd, rm, rv, nbt, rmd, rvd, nbtd, eps, mom, epsd, momd,
+                slab, shift, slabd, shiftd):
+        C = _C()
+        ctx.params = (w, b, wd, bd)
+        if ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            _ddp_direct.note_use(w, b)
+        if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
+            _ddp_direct.note_use(wd, bd)
+        count = x.numel() // x.size(1)
+
+        def stats(t, sl, sh, rm_, rv_, nbt_, eps_, mom_):
+            if sl is not None:
+                return C.slab_train_stats(sl, count, sh, rm_, rv_, nbt_, float(eps_), float(mom_))
+            return C.train_stats(t, rm_, rv_, nbt_, float(eps_), float(mom_))
+
+        mean, invstd = stats(x, slab, shift, rm, rv, nbt, eps, mom)
+        meand, invstdd = stats(xd, slabd, shiftd, rmd, rvd, nbtd, epsd, momd)
+        y, mask = C.apply2_mask(x, mean, invstd, w, b, xd, meand, invstdd, wd, bd)
+        ctx.save_for_backward(x, xd, w, b, wd, bd, mean, invstd, meand, invstdd, mask)
+        ctx.src = _TLS.src = _bwd_src(x, x, mean, invstd, w, b, mask, True, True)
+        ctx.count = count
+        FUSED_DS_CALLS[0] += 1
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x, xd, w, b, wd, bd, mean, invstd, meand, invstdd, mask = ctx.saved_tensors
+        need = w is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        needd = wd is not None and (ctx.needs_input_grad[4] or ctx.needs_input_grad[5])
+        cnt = float(ctx.count)
+        src = ctx.src
+        res = src.result if src is not None else None
+        if res is not None:
+            src.result = None
+        if (res is not None and res[0] == dy.data_ptr() and res[2] == dy._version
+                and dy.is_contiguous(memory_format=torch.channels_last)):
+            # dy is the consuming conv's g (ReLU mask applied) with its sums in a slab
+            FUSED_BWD_CALLS[0] += 1
+            s1, s2, gw, gb = C.slab_reduce_grad(res[1], invstd, w, need)
+            dx, t1, t2, gwd, gbd = C.backward_elemt_x2(dy, x, mean, invstd, w, b, s1, s2, cnt,
+                                                       xd, meand, invstdd, wd, needd)
+            dxd, _ = C.backward_elemt(dy, xd, meand, invstdd, wd, bd, t1, t2, cnt, None, False,
+                                      False)
+        else:
+            dyc = dy.contiguous(memory_format=torch.channels_last)
+            s1, s2, gw, gb = C.reduce_grad(dyc, x, mean, invstd, w, b, None, True, need,
+                                           mask=mask)
+            dx, d = C.backward_elemt(dyc, x, mean, invstd, w, b, s1, s2, cnt, None, True, True,
+                                     mask=mask)
+            dxd, _, gwd, gbd = C.backward_local(d, xd, meand, invstdd, wd, bd, None, False,
+                                                needd, False)
+        return (dx, dxd, gw if need else None, gb if need else None, gwd if needd else None,
+                gbd if needd else None) + (None,) * 14
+
+
+def _ds_fusable(bn, x, bnd, xd):
+    return (_FUSE_DS and type(bn) is BatchNorm2dReLU and type(bnd) is BatchNorm2dReLU
+            and bn.training and bnd.training and bn.fuse_relu and not bnd.fuse_relu
+            and bn.track_running_stats and bnd.track_running_stats
+            and bn.momentum is not None and bnd.momentum is not None
+            and bn.affine == bnd.affine and x.is_cuda and xd.is_cuda and x.dim() == 4
+            and x.shape == xd.shape and x.dtype == xd.dtype
+            and x.dtype in (torch.bfloat16, torch.float16)
+            and (not bn.affine or bn.weight.dtype == bnd.weight.dtype)
+            and _native.available() and _C().backward_x2_ok(x, x, xd))
+
+
+def bn_add_bn_relu(bn, x, bnd, xd):
+    """relu(bn(x) + bnd(xd)) - one fused pass where both are local BatchNorm2dReLU modules in
+    training mode (bn with ReLU, bnd without), else the two module calls."""
+    if not _ds_fusable(bn, x, bnd, xd):
+        return bn(x, bnd(xd))
+    slab, shift = take_slab(x, bn)
+    slabd, shiftd = take_slab(xd, bnd)
+    _TLS.src = None
+    y = BatchNormAddBNReLUFunction.apply(
+        x, xd, bn.weight, bn.bias, bnd.weight, bnd.bias, bn.running_mean, bn.running_var,
+        bn.num_batches_tracked, bnd.running_mean, bnd.running_var, bnd.num_batches_tracked,
+        bn.eps, bn.momentum, bnd.eps, bnd.momentum, slab, shift, slabd, shiftd)
+    src = _TLS.src
+    if src is not None:
+        _TLS.src = None
+        y._amd_bn_src = src
+    return y

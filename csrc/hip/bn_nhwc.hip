@@ -239,28 +239,40 @@ __device__ __forceinline__ void stage_params(int C, int cb, int n, F&& f) {
 // (clamped rows, no branches) and pinned ahead of the arithmetic: with `if (z)` and
 // `if (rr < M)` around them the compiler waited vmcnt(0) after every row's loads (one row
 // in flight per lane, ISA of the round-5 build).
-template <typename T, typename TW, bool VEC, int U, bool ZZ>
+//
+// ZA (with ZZ): z is the RAW input of a second BatchNorm (ResNet's downsample BN) whose
+// affine (meanz, invstdz, wz, bz) is applied here on load, rounded to T exactly as that BN's
+// own apply pass would have stored it - y is bitwise the unfused result and that BN's
+// output is never materialised (its apply pass, a read and a write of the tensor, goes).
+template <typename T, typename TW, bool VEC, int U, bool ZZ, bool ZA = false>
 __global__ void __launch_bounds__(kBNThreads)
     apply_k(const T* __restrict__ x, const float* __restrict__ mean,
             const float* __restrict__ invstd, const TW* __restrict__ w, const TW* __restrict__ b,
             const T* __restrict__ z, T* __restrict__ y, uint8_t* __restrict__ rmask, int64_t M,
-            int C, int ctile, int rows_iter, int relu) {
+            int C, int ctile, int rows_iter, int relu, const float* __restrict__ meanz = nullptr,
+            const float* __restrict__ invstdz = nullptr, const TW* __restrict__ wz = nullptr,
+            const TW* __restrict__ bz = nullptr) {
   constexpr int W = VEC ? 8 : 1;
   const int Cb = C >> 3;
   const int ci = threadIdx.x % ctile, ri = threadIdx.x / ctile;
   const int c0 = (blockIdx.y * ctile + ci) * W;
   // the block's channel parameters, one channel per thread, staged in LDS
-  __shared__ __attribute__((aligned(16))) float s_par[2][kBNBlockChans];
+  __shared__ __attribute__((aligned(16))) float s_par[ZA ? 4 : 2][kBNBlockChans];
   const int cb = blockIdx.y * ctile * W;
   stage_params(C, cb, ctile * W, [&](int c, int k) {
     chan_affine(mean, invstd, wload(w, c, 1.f), wload(b, c, 0.f), c, s_par[0][k], s_par[1][k]);
+    if constexpr (ZA)
+      chan_affine(meanz, invstdz, wload(wz, c, 1.f), wload(bz, c, 0.f), c, s_par[ZA ? 2 : 0][k],
+                  s_par[ZA ? 3 : 1][k]);
   });
   if (ri >= rows_iter || c0 >= C) return;
-  float sc[W], sh[W];
+  float sc[W], sh[W], scz[W], shz[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
     sc[i] = s_par[0][c0 - cb + i];
     sh[i] = s_par[1][c0 - cb + i];
+    scz[i] = ZA ? s_par[ZA ? 2 : 0][c0 - cb + i] : 0.f;
+    shz[i] = ZA ? s_par[ZA ? 3 : 1][c0 - cb + i] : 0.f;
   }
   const int64_t stride = (int64_t)gridDim.x * rows_iter;
   for (int64_t r = (int64_t)blockIdx.x * rows_iter + ri; r < M; r += stride * U) {
@@ -281,7 +293,11 @@ __global__ void __launch_bounds__(kBNThreads)
 #pragma unroll
       for (int i = 0; i < W; ++i) {
         float o = fmaf(v[u][i], sc[i], sh[i]);
-        if constexpr (ZZ) o += zz[u][i];
+        if constexpr (ZA) {
+          o += to_f32(from_f32<T>(fmaf(zz[u][i], scz[i], shz[i])));
+        } else if constexpr (ZZ) {
+          o += zz[u][i];
+        }
         mb |= (o > 0.f ? 1u : 0u) << i;
         v[u][i] = relu ? fmaxf(o, 0.f) : o;
       }
@@ -798,6 +814,27 @@ void nhwc_backward(const void* dy, const void* x, DType tx, const float* mean,
         };
         go(std::integral_constant<int, 2>{});
       });
+    });
+  });
+}
+
+// relu(BN(x) + BNz(xz)) with the ReLU bitmask: apply_k's ZA mode (both BNs' affines on load)
+void nhwc_apply2(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
+                 const void* b, DType tw, const void* xz, const float* meanz,
+                 const float* invstdz, const void* wz, const void* bz, uint8_t* rmask, void* y,
+                 int64_t M, int64_t C, hipStream_t st) {
+  const NGeom g = ngeom(C, true);
+  const int blocks = elem_blocks(M, g, M * C * (tx == DType::F32 ? 4 : 2));
+  bn_dispatch(tx, [&](auto t0) {
+    bn_dispatch(tw, [&](auto w0) {
+      using T = decltype(t0);
+      using TW = decltype(w0);
+      hipLaunchKernelGGL((apply_k<T, TW, true, 2, true, true>), dim3(blocks, g.cblocks),
+                         dim3(kBNThreads), 0, st, static_cast<const T*>(x), mean, invstd,
+                         static_cast<const TW*>(w), static_cast<const TW*>(b),
+                         static_cast<const T*>(xz), static_cast<T*>(y), rmask, M, (int)C,
+                         g.ctile, g.rows_iter, 1, meanz, invstdz, static_cast<const TW*>(wz),
+                         static_cast<const TW*>(bz));
     });
   });
 }

@@ -197,6 +197,12 @@ void nhwc_backward_x2(const void* dy, const void* x, DType tx, const float* mean
                       const float* invstd2, float* sum_dy2, float* sum_dy_xmu2, void* gw2,
                       void* gb2, float* ws, hipStream_t st);
 int64_t nhwc_backward_x2_workspace(int64_t M, int64_t C, DType tx);
+// relu(BN(x) + BNz(xz)) + ReLU bitmask [M][C/8] in one pass (NHWC, C % 8 == 0, 16-byte
+// aligned): the residual BN's output is formed on load, rounded as its apply would store it
+void nhwc_apply2(const void* x, DType tx, const float* mean, const float* invstd, const void* w,
+                 const void* b, DType tw, const void* xz, const float* meanz,
+                 const float* invstdz, const void* wz, const void* bz, uint8_t* rmask, void* y,
+                 int64_t M, int64_t C, hipStream_t st);
 bool layer_norm_bwd_hsum_ok(int64_t n2);
 // backward partial combine through one [R][n2] LDS row set instead of per-wave rows (A/B,
 // default off: measured slower end to end)

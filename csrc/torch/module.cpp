@@ -216,6 +216,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
          py::arg("want_dz"), py::arg("mask") = py::none());
 
   bn.def("backward_x2_ok", &bn_backward_x2_ok);
+  bn.def("apply2_mask", &bn_apply2_mask_op, py::arg("x"), py::arg("mean"), py::arg("invstd"),
+         py::arg("weight"), py::arg("bias"), py::arg("xz"), py::arg("meanz"), py::arg("invstdz"),
+         py::arg("weightz"), py::arg("biasz"));
   bn.def("backward_elemt_x2", &bn_backward_elemt_x2_op, py::arg("dy"), py::arg("x"),
          py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("bias"),
          py::arg("sum_dy"), py::arg("sum_dy_xmu"), py::arg("count"), py::arg("x2"),

@@ -676,6 +676,35 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backwa
   return {dx, sum_dy2, sum_dy_xmu2, gw2, gb2};
 }
 
+// y = relu(BN(x) + BNz(xz)) and its ReLU mask in one pass (the residual BN's output is never
+// stored); GPU, channels-last, C % 8 == 0, 16-byte aligned (bn_backward_x2_ok's conditions)
+std::tuple<at::Tensor, at::Tensor> bn_apply2_mask_op(at::Tensor x, at::Tensor mean,
+                                                     at::Tensor invstd, OptT weight, OptT bias,
+                                                     at::Tensor xz, at::Tensor meanz,
+                                                     at::Tensor invstdz, OptT weightz,
+                                                     OptT biasz) {
+  TORCH_CHECK(bn_backward_x2_ok(x, x, xz), "apply2: GPU channels-last 16-bit x / xz of one shape");
+  BNView v = bn_view(x);
+  DType tw = has(weight) ? dtype_of(*weight) : DType::F32;
+  TORCH_CHECK((has(weightz) ? dtype_of(*weightz) : DType::F32) == tw &&
+                  (has(bias) ? dtype_of(*bias) : tw) == tw &&
+                  (has(biasz) ? dtype_of(*biasz) : tw) == tw,
+              "apply2: one parameter dtype");
+  for (const at::Tensor* t : {&mean, &invstd, &meanz, &invstdz})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == v.C,
+                "apply2: statistics must be fp32 [C]");
+  at::Tensor y = at::empty_like(x);
+  at::Tensor mask = at::empty({v.outer, v.C / 8}, x.options().dtype(at::kByte));
+  auto ptr = [](const OptT& t) -> at::Tensor { return has(t) ? t->contiguous() : at::Tensor(); };
+  at::Tensor w = ptr(weight), b = ptr(bias), wz = ptr(weightz), bz = ptr(biasz);
+  nhwc_apply2(x.data_ptr(), dtype_of(x), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+              w.defined() ? w.data_ptr() : nullptr, b.defined() ? b.data_ptr() : nullptr, tw,
+              xz.data_ptr(), meanz.data_ptr<float>(), invstdz.data_ptr<float>(),
+              wz.defined() ? wz.data_ptr() : nullptr, bz.defined() ? bz.data_ptr() : nullptr,
+              mask.data_ptr<uint8_t>(), y.data_ptr(), v.outer, v.C, cur_stream());
+  return {y, mask};
+}
+
 // Local (world 1) backward: reduce_grad + backward_elemt.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_local_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,

@@ -72,6 +72,11 @@ std::tuple<at::Tensor, at::Tensor> bn_backward_elemt_op(at::Tensor dy, at::Tenso
                                                         OptT mask);
 
 bool bn_backward_x2_ok(at::Tensor dy, at::Tensor x, at::Tensor x2);
+std::tuple<at::Tensor, at::Tensor> bn_apply2_mask_op(at::Tensor x, at::Tensor mean,
+                                                     at::Tensor invstd, OptT weight, OptT bias,
+                                                     at::Tensor xz, at::Tensor meanz,
+                                                     at::Tensor invstdz, OptT weightz,
+                                                     OptT biasz);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward_elemt_x2_op(
     at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd, OptT weight, OptT bias,
     at::Tensor sum_dy, at::Tensor sum_dy_xmu, double count, at::Tensor x2, at::Tensor mean2,

@@ -39,9 +39,12 @@ def test_backward_elemt_x2_sums_match_reference():
     torch.testing.assert_close(gw2.double(), r2 * invstd2.double(), rtol=1e-4, atol=1e-2)
 
 
-def test_resnet50_step_grads_with_x2_fusion():
+def test_resnet50_step_grads_with_x2_fusion(monkeypatch):
     from apex_example_amd.models import resnet50
     from apex_example_amd.ops import batch_norm as B
+
+    # the separate-module downsample path (the fused bn3 + downsample-BN pass replaces it)
+    monkeypatch.setattr(B, "_FUSE_DS", False)
 
     torch.manual_seed(0)
     m = resnet50(fused_bn=True, gemm_1x1=True).to(DEV).to(memory_format=torch.channels_last)
@@ -77,3 +80,67 @@ def test_resnet50_step_grads_with_x2_fusion():
             assert float((a - b).abs().max() / scale) < 1e-3, n
         cos = float(torch.nn.functional.cosine_similarity(a.double(), b.double(), dim=0))
         assert cos > 0.99 or float(b.abs().max()) < 1e-6, (n, cos)
+
+
+def test_apply2_bitwise_equals_two_passes():
+    """apply2_mask: relu(bn(x) + bnd(xd)) with the downsample BN applied on load is bitwise
+    the output and mask of bnd's apply pass followed by bn's apply with z."""
+    from apex_example_amd import _native
+
+    C = _native.require().bn
+    torch.manual_seed(3)
+    n, c, h, w = 4, 512, 14, 14
+    cl = torch.channels_last
+    x = torch.randn(n, c, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
+    xd = (torch.randn(n, c, h, w, device=DEV) * 3).to(torch.bfloat16).contiguous(memory_format=cl)
+    m, i = torch.randn(c, device=DEV) * 0.1, torch.rand(c, device=DEV) + 0.5
+    md, idd = torch.randn(c, device=DEV), torch.rand(c, device=DEV) + 0.2
+    wt, bs = torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV)
+    wd, bd = torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV)
+    y, mask = C.apply2_mask(x, m, i, wt, bs, xd, md, idd, wd, bd)
+    z = C.apply(xd, md, idd, wd, bd, None, False)
+    y2, mask2 = C.apply_mask(x, m, i, wt, bs, z, True)
+    assert torch.equal(y, y2) and torch.equal(mask, mask2)
+
+
+def test_resnet50_step_with_fused_downsample_bn():
+    """ResNet-50 train step with the downsample BN fused into bn3's pass vs the two module
+    calls: identical output and running stats, gradients to bf16 noise."""
+    from apex_example_amd.models import resnet50
+    from apex_example_amd.ops import batch_norm as B
+
+    torch.manual_seed(0)
+    m = resnet50(fused_bn=True, gemm_1x1=True).to(DEV).to(memory_format=torch.channels_last)
+    m = m.to(torch.bfloat16)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            mod.float()
+    x = torch.randn(8, 3, 96, 96, device=DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    runs = []
+    for on in (True, False):
+        m.load_state_dict(state)
+        m.zero_grad(set_to_none=True)
+        old = B._FUSE_DS
+        B._FUSE_DS = on
+        before = B.FUSED_DS_CALLS[0]
+        try:
+            out = m(x)
+            out.float().square().mean().backward()
+        finally:
+            B._FUSE_DS = old
+        assert (B.FUSED_DS_CALLS[0] - before == 4) == on
+        runs.append((out.detach().clone(), {k: v.clone() for k, v in m.state_dict().items()},
+                     {n: p.grad.float().clone() for n, p in m.named_parameters()}))
+    (oa, sa, ga), (ob, sb, gb) = runs
+    assert torch.equal(oa, ob)
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    for n in ga:
+        a, b = ga[n].flatten(), gb[n].flatten()
+        cos = float(torch.nn.functional.cosine_similarity(a.double(), b.double(), dim=0))
+        assert cos > 0.99 or float(b.abs().max()) < 1e-6, (n, cos)
+        if n.startswith("layer4.") or n.startswith("fc."):
+            scale = b.abs().max().clamp_min(1e-6)
+            assert float((a - b).abs().max() / scale) < 2e-2, n
