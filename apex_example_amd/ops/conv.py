@@ -435,8 +435,10 @@ def _tag_stats(y):
 # 12544), so those fuse only below 65,536 output pixels.  Round 4
 # (32-deep K ring): 65536 takes the 14x14 layers (M = 50176) in too - ResNet-50 same box,
 # two runs each: 10,582 / 10,576 img/s at 16384, 10,595 / 10,633 with the 14x14 layers,
-# 10,613 / 10,549 with every layer (profiles/r4/i/).
-_BNBWD_MAX_M = 65536
+# 10,613 / 10,549 with every layer (profiles/r4/i/).  Round 6 (halo / C^T / N-fastest
+# kernels, the epilogue's early prefetch): every layer wins - 12,640 / 12,727 vs 12,581 /
+# 12,656 img/s with the 65,536 cap (profiles/r6/bnbwd_all/), so no cap by default.
+_BNBWD_MAX_M = int(os.environ.get("APEX_AMD_BNBWD_MAX_M", str((1 << 31) - 1)))
 
 
 def _bnbwd_ok(dy, weight, src, xshape, has_add=False):
