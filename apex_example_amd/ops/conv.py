@@ -439,6 +439,10 @@ def _tag_stats(y):
 # kernels, the epilogue's early prefetch): every layer wins - 12,640 / 12,727 vs 12,581 /
 # 12,656 img/s with the 65,536 cap (profiles/r6/bnbwd_all/), so no cap by default.
 _BNBWD_MAX_M = int(os.environ.get("APEX_AMD_BNBWD_MAX_M", str((1 << 31) - 1)))
+# the stride-2 3x3 data gradients (conv_dgrad_s2) with the same epilogue (A/B switch):
+# correct (tests/test_conv_bn_bwd_gpu.py::test_dgrad_s2_bnbwd_epilogue) but neutral end to
+# end - 12,593 / 12,625 vs 12,605 / 12,599 img/s same box (profiles/r6/bnbwd_s2/) - so off
+_BNBWD_S2 = os.environ.get("APEX_AMD_BNBWD_S2", "0") == "1"
 
 
 def _bnbwd_ok(dy, weight, src, xshape, has_add=False):
@@ -851,6 +855,13 @@ class Conv3x3Function(torch.autograd.Function):
                 dx = _dgrad_bn(dy, _rot_weight(weight), None, src)
             elif stride == 1:
                 dx = cv.conv_fwd(dy, _rot_weight(weight), 1)
+            elif _BNBWD_S2 and _bnbwd_ok(dy, weight, src, x.shape):
+                # stride-2 3x3 dgrad with the BN-backward epilogue (no reduction pass for
+                # the BN whose output this conv read)
+                dx, slab = cv.conv_dgrad_s2_bnbwd(
+                    dy, _rot_weight(weight), x.size(2), x.size(3), src.x, src.mask, src.mean,
+                    src.invstd, src.weight, src.bias, src.relu_mode)
+                src.result = (dx.data_ptr(), slab, dx._version)
             else:
                 dx = cv.conv_dgrad_s2(dy, _rot_weight(weight), x.size(2), x.size(3))
         direct = None

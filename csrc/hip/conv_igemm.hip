@@ -2071,4 +2071,21 @@ void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, 
   else launch_conv_tap<kDgrad1>(dyp, wp, dxp, g, st);
 }
 
+// conv_nhwc_dgrad_s2 with the BN-backward epilogue (ConvBnEpi, no residual add): the data
+// gradient of a stride-2 3x3 conv whose input is a BN(+ReLU) output stores g = mask * dX and
+// that BN's backward sums, slab [2][Cin][4 * ceil(N*Ho*Wo / 128)] (every input pixel belongs
+// to exactly one parity class, so each g is final in its epilogue)
+int conv_dgrad_s2_bnbwd_mtiles(int N, int H, int W) {
+  const int64_t M = (int64_t)N * (H / 2) * (W / 2);
+  return 4 * (int)((M + kBM - 1) / kBM);
+}
+void conv_nhwc_dgrad_s2_bnbwd(const void* dy, const void* wt, void* gout, int N, int H, int W,
+                              int Cin, int Cout, const ConvBnEpi& ep, float* slab,
+                              hipStream_t st) {
+  const int Ho = H / 2, Wo = W / 2;
+  const ConvGeom g{Ho, Wo, Ho, Wo, 1, H, W, 2, Cout, Cin, N * Ho * Wo, 9 * Cout};
+  launch_conv_tap<kDgrad3, 1>(static_cast<const bf16_t*>(dy), static_cast<const bf16_t*>(wt),
+                              static_cast<bf16_t*>(gout), g, st, slab, nullptr, ep);
+}
+
 }  // namespace amd

@@ -397,6 +397,12 @@ void bn_slab_reduce_grad(const float* slab, int S, int64_t C, const float* invst
 // data gradient of a stride-2 conv (H, W even); wt = rotated 3x3 filter / W^T for 1x1
 void conv_nhwc_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int H, int W, int Cin,
                         int Cout, int ksize, hipStream_t st);
+// the 3x3 form with the BN-backward epilogue (ep.add must be null); slab [2][Cin][S],
+// S = conv_dgrad_s2_bnbwd_mtiles(N, H, W)
+int conv_dgrad_s2_bnbwd_mtiles(int N, int H, int W);
+void conv_nhwc_dgrad_s2_bnbwd(const void* dy, const void* wt, void* gout, int N, int H, int W,
+                              int Cin, int Cout, const ConvBnEpi& ep, float* slab,
+                              hipStream_t st);
 // weight gradient: split-K over output pixels into fp32 partials [S][k*k][Cout][Cin],
 // then a reduce into dW (KRSC, bf16 or fp32).  algo 0 = per-tap MFMA kernel,
 // 1 = all-9-taps strip kernel (3x3 stride 1, W <= 56), 4 = 64-channel strip-ring kernel

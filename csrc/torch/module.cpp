@@ -149,6 +149,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   conv.def("conv_fwd_stats", &conv_nhwc_fwd_stats_op, py::arg("x"), py::arg("w"),
            py::arg("stride") = 1, py::arg("shift") = py::none());
   conv.def("conv_dgrad_s2", &conv_nhwc_dgrad_s2_op);
+  conv.def("conv_dgrad_s2_bnbwd", &conv_nhwc_dgrad_s2_bnbwd_op, py::arg("dy"), py::arg("wt"),
+           py::arg("H"), py::arg("W"), py::arg("x"), py::arg("rmask"), py::arg("mean"),
+           py::arg("invstd"), py::arg("bn_weight"), py::arg("bn_bias"), py::arg("relu_mode"));
   conv.def("conv_wgrad", &conv_nhwc_wgrad_op, py::arg("dy"), py::arg("x"), py::arg("out_dtype"),
            py::arg("algo") = 0, py::arg("stride") = 1, py::arg("ksize") = 3,
            py::arg("out") = py::none(), py::arg("accumulate") = true);

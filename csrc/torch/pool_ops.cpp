@@ -262,6 +262,60 @@ at::Tensor conv_nhwc_dgrad_s2_op(at::Tensor dy, at::Tensor wt, int64_t H, int64_
   return dx;
 }
 
+// conv_dgrad_s2 (3x3) whose output is the gradient of a BN(+ReLU) output: g = relu_mask *
+// dX and that BN's backward sums [2][C][S] (as conv_fwd_bnbwd, no residual add)
+std::tuple<at::Tensor, at::Tensor> conv_nhwc_dgrad_s2_bnbwd_op(
+    at::Tensor dy, at::Tensor wt, int64_t H, int64_t W, at::Tensor xbn,
+    c10::optional<at::Tensor> rmask, at::Tensor mean, at::Tensor invstd,
+    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode) {
+  c10::NoGradGuard no_grad_;
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && wt.dim() == 4, "dgrad_s2_bnbwd: 4-D GPU tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && wt.scalar_type() == at::kBFloat16 &&
+                  xbn.scalar_type() == at::kBFloat16, "dgrad_s2_bnbwd: bf16 only");
+  const int64_t N = dy.size(0), Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  const int64_t Cin = wt.size(0);
+  TORCH_CHECK(wt.size(1) == Cout && wt.size(2) == 3 && wt.size(3) == 3,
+              "dgrad_s2_bnbwd: rotated 3x3 weight [Cin, Cout, 3, 3] expected");
+  TORCH_CHECK(H == 2 * Ho && W == 2 * Wo, "dgrad_s2_bnbwd: even input sizes only");
+  TORCH_CHECK(conv3x3_nhwc_supported((int)Cout, (int)Cin), "dgrad_s2_bnbwd: channels x64");
+  TORCH_CHECK(N * H * W < (int64_t)1 << 31, "dgrad_s2_bnbwd: too many pixels");
+  TORCH_CHECK(relu_mode >= 0 && relu_mode <= 2, "dgrad_s2_bnbwd: relu_mode 0 | 1 | 2");
+  const auto cl = at::MemoryFormat::ChannelsLast;
+  TORCH_CHECK(xbn.is_cuda() && xbn.dim() == 4 && xbn.size(0) == N && xbn.size(1) == Cin &&
+                  xbn.size(2) == H && xbn.size(3) == W && xbn.is_contiguous(cl),
+              "dgrad_s2_bnbwd: x must be the BN input, channels-last bf16 [N, Cin, H, W]");
+  ConvBnEpi ep{};
+  ep.xbn = xbn.data_ptr();
+  auto vecf = [&](const c10::optional<at::Tensor>& t, const char* what) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() == Cin,
+                "dgrad_s2_bnbwd: ", what, " must be a contiguous fp32 [C] GPU tensor");
+    return t->data_ptr<float>();
+  };
+  ep.mean = vecf(mean, "mean");
+  ep.invstd = vecf(invstd, "invstd");
+  ep.w = vecf(bn_w, "weight");
+  ep.b = vecf(bn_b, "bias");
+  TORCH_CHECK(ep.mean && ep.invstd, "dgrad_s2_bnbwd: mean / invstd required");
+  ep.relu_mode = (int)relu_mode;
+  if (relu_mode == 1) {
+    TORCH_CHECK(rmask.has_value() && rmask->defined() && rmask->is_cuda() &&
+                    rmask->scalar_type() == at::kByte && rmask->is_contiguous() &&
+                    rmask->numel() == N * H * W * (Cin / 8),
+                "dgrad_s2_bnbwd: relu_mode 1 needs the forward's [M][C/8] uint8 bitmask");
+    ep.rmask = rmask->data_ptr<uint8_t>();
+  }
+  dy = dy.contiguous(cl);
+  wt = wt.contiguous(cl);
+  at::Tensor g = at::empty({N, Cin, H, W}, dy.options().memory_format(cl));
+  at::Tensor slab = at::empty({2, Cin, (int64_t)conv_dgrad_s2_bnbwd_mtiles((int)N, (int)H, (int)W)},
+                              dy.options().dtype(at::kFloat));
+  conv_nhwc_dgrad_s2_bnbwd(dy.data_ptr(), wt.data_ptr(), g.data_ptr(), (int)N, (int)H, (int)W,
+                           (int)Cin, (int)Cout, ep, slab.data_ptr<float>(), cur_stream());
+  return {g, slab};
+}
+
 at::Tensor conv_nhwc_wgrad_op(at::Tensor dy, at::Tensor x, at::ScalarType out_dtype, int64_t algo,
                               int64_t stride, int64_t ksize, c10::optional<at::Tensor> out,
                               bool accumulate) {

@@ -36,6 +36,10 @@ at::Tensor splitk_reduce_op(at::Tensor part, at::ScalarType out_dtype,
                             c10::optional<at::Tensor> out_acc, bool accumulate = true);
 at::Tensor stem_pad_op(at::Tensor x);
 at::Tensor stem_fwd_op(at::Tensor xp, at::Tensor wk);
+std::tuple<at::Tensor, at::Tensor> conv_nhwc_dgrad_s2_bnbwd_op(
+    at::Tensor dy, at::Tensor wt, int64_t H, int64_t W, at::Tensor xbn,
+    c10::optional<at::Tensor> rmask, at::Tensor mean, at::Tensor invstd,
+    c10::optional<at::Tensor> bn_w, c10::optional<at::Tensor> bn_b, int64_t relu_mode);
 std::tuple<at::Tensor, at::Tensor> maxpool2d_nhwc_bwd_bn_op(at::Tensor dy, at::Tensor idx,
                                                             int64_t H, int64_t W, at::Tensor x,
                                                             at::Tensor mean, at::Tensor invstd,

@@ -320,3 +320,35 @@ def test_conv_tilings_vs_fp32_and_stable(shape):
     torch.testing.assert_close(sums[1], (yv.double() ** 2).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     for i, (a, b) in enumerate(zip(first, run())):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 28, 28, 128), (2, 256, 14, 14, 256), (3, 64, 20, 12, 128)])
+@pytest.mark.parametrize("relu_mode", [0, 2])
+def test_dgrad_s2_bnbwd_epilogue(shape, relu_mode):
+    """Stride-2 3x3 data gradient with the BN-backward epilogue (conv_dgrad_s2_bnbwd): g is
+    the ReLU-masked plain stride-2 dgrad (bitwise), the slab sums equal sum(g),
+    sum(g * (x - mean)) in fp64."""
+    from apex_example_amd import _native
+
+    C = _native.require()
+    torch.manual_seed(7)
+    n, cin, h, w, cout = shape
+    cl = torch.channels_last
+    dy = torch.randn(n, cout, h // 2, w // 2, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    wt = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
+    wrot = C.conv.rot_weight(wt)
+    xb = torch.randn(n, cin, h, w, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    mean, invstd = torch.randn(cin, device="cuda") * 0.1, torch.rand(cin, device="cuda") + 0.5
+    bw, bb = torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.1
+    g, slab = C.conv.conv_dgrad_s2_bnbwd(dy, wrot, h, w, xb, None, mean, invstd, bw, bb, relu_mode)
+    ref = C.conv.conv_dgrad_s2(dy, wrot, h, w)
+    if relu_mode == 2:
+        keep = (xb.float() * (invstd * bw).view(1, -1, 1, 1)
+                + (bb - mean * invstd * bw).view(1, -1, 1, 1)) > 0
+        ref = torch.where(keep, ref, torch.zeros_like(ref))
+    torch.testing.assert_close(g.float(), ref.float(), rtol=0, atol=0)
+    sums = slab.double().sum(2)
+    gd = g.double().permute(0, 2, 3, 1).reshape(-1, cin)
+    xd = xb.double().permute(0, 2, 3, 1).reshape(-1, cin)
+    torch.testing.assert_close(sums[0], gd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(sums[1], (gd * (xd - mean.double())).sum(0), rtol=1e-5, atol=1e-3)
