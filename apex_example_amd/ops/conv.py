@@ -247,7 +247,7 @@ def _wgrad_1x1_w(dy, x, weight, out=None, accumulate=True):
 
 # maximum row splits of the 1x1 weight gradients (A/B knob: the split-K GEMMs run on the
 # weight-gradient side stream, where a smaller grid leaves more CUs to the main stream)
-_SPLITK_MAX = 128
+_SPLITK_MAX = int(os.environ.get("APEX_AMD_WGRAD1X1_SPLITS", "128"))
 
 
 def _split_k(m):
