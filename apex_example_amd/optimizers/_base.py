@@ -35,6 +35,9 @@ _STEP_PLAN = True
 class FusedOptimizerBase(torch.optim.Optimizer):
     _amp_fused = True
     _amp_writes_model_copy = True
+    # amp O1 16-bit weight copies written by the step (fused_dense.cast_params_once); the
+    # optimizers whose kernels take a copy list opt in
+    _o1_copies = False
 
     def __init__(self, params, defaults, set_grad_none=True, materialize_master_grads=True):
         super().__init__(params, defaults)
@@ -217,7 +220,16 @@ class FusedOptimizerBase(torch.optim.Optimizer):
                     continue
                 if p.grad.is_sparse:
                     raise RuntimeError("fused optimizers do not support sparse gradients")
-                add((p.grad.dtype, p.dtype, None, o1_scaled), p.grad, p, None, o1_scaled, p)
+                cp = None
+                if self._o1_copies and p.dtype == torch.float32 and p.is_cuda:
+                    # amp O1: the step also writes the 16-bit copy the next forward's
+                    # cast_params_once would otherwise re-cast (fused_dense.o1_copy_of)
+                    from ..fused_dense import o1_copy_of
+                    cp = o1_copy_of(p)
+                add((p.grad.dtype, p.dtype, cp.dtype if cp is not None else None, o1_scaled),
+                    p.grad, p, cp, o1_scaled, p)
+                if cp is not None:
+                    sets[(p.grad.dtype, p.dtype, cp.dtype, o1_scaled)]["o1"] = True
         return sets
 
     def _scale_args(self, scaled):

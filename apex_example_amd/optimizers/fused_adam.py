@@ -12,10 +12,12 @@ from __future__ import annotations
 import torch
 
 from .. import amp_C
+from ..fused_dense import o1_mark_fresh
 from ._base import FusedOptimizerBase
 
 
 class FusedAdam(FusedOptimizerBase):
+    _o1_copies = True
     def __init__(self, params, lr=1e-3, bias_correction=True, betas=(0.9, 0.999), eps=1e-8,
                  adam_w_mode=True, weight_decay=0., amsgrad=False, set_grad_none=True,
                  materialize_master_grads=True):
@@ -48,6 +50,9 @@ class FusedAdam(FusedOptimizerBase):
             noop = self._noop(dev)
             planned, last = True, len(sets) - 1
             for i, (key, s) in enumerate(sets.items()):
+                if s.get("o1"):
+                    # the depth-5 launch below refreshes the amp O1 16-bit weight copies
+                    o1_mark_fresh(s["params"], s["copies"])
                 # exponential moving averages of the gradient and its square
                 m, v = self._state_lists(s, ("exp_avg", "exp_avg_sq"))
                 plan = s.get("_plan")

@@ -196,3 +196,52 @@ def test_gpt2_o1_fused_adam_tracks_stock_autocast_adamw():
     ours, theirs = [float(v) for v in ours], [float(v) for v in theirs]
     assert ours[-1] < ours[0] - 2.0 and theirs[-1] < theirs[0] - 2.0
     _assert_curves_close(ours, theirs, 0.05, 0.05, "gpt2 O1 FusedAdam vs autocast AdamW")
+
+
+def test_gpt2_o1_fused_weight_copies_bitwise():
+    """amp O1 + FusedAdam: the step writes the 16-bit weight copies the next forward uses
+    (fused_dense.cast_params_once skips its cast pass) - losses and parameters bitwise the
+    same as re-casting every forward; the skip really happens; a parameter edited between
+    steps is re-cast."""
+    from apex_example_amd import amp, fused_dense
+    from apex_example_amd.amp import amp as _amp
+    from apex_example_amd.models.gpt2 import GPT2Config, GPT2LMHeadModel, lm_loss
+    from apex_example_amd.optimizers import FusedAdam
+
+    kw = dict(n_layer=2, resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 50257, (2, 128), generator=g).cuda()
+    torch.manual_seed(0)
+    init = GPT2LMHeadModel(GPT2Config(**kw)).state_dict()
+    runs = []
+    for on in (True, False):
+        old = fused_dense._O1_FUSED_COPIES
+        fused_dense._O1_FUSED_COPIES = on
+        try:
+            m = GPT2LMHeadModel(GPT2Config(**kw)).cuda()
+            m.load_state_dict(init)
+            opt = FusedAdam(m.parameters(), lr=3e-4, weight_decay=0.01)
+            m, opt = amp.initialize(m, opt, opt_level="O1", verbosity=0)
+            before = fused_dense.O1_CAST_SKIPPED[0]
+            losses = []
+            for i in range(6):
+                if i == 4:
+                    with torch.no_grad():  # an edit outside the optimizer: must be re-cast
+                        next(m.parameters()).mul_(0.5)
+                loss = lm_loss(m(ids), ids)
+                opt.zero_grad()
+                with amp.scale_loss(loss, opt) as s:
+                    s.backward()
+                opt.step()
+                losses.append(loss.detach().float().clone())
+            skipped = fused_dense.O1_CAST_SKIPPED[0] - before
+            runs.append((torch.stack(losses), [p.detach().clone() for p in m.parameters()],
+                         skipped))
+        finally:
+            _amp.deinit()
+            fused_dense._O1_FUSED_COPIES = old
+    (la, pa, sa), (lb, pb, sb) = runs
+    assert sa >= 3 and sb == 0, (sa, sb)
+    assert torch.equal(la, lb)
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
